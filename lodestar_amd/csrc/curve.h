@@ -1,0 +1,318 @@
+// G1 (y^2 = x^3 + 4 over Fp) and G2 (y^2 = x^3 + 4(1+i) over Fp2): Jacobian arithmetic
+// (a = 0: dbl-2009-l, madd-2007-bl, add-2007-bl), ZCash decoding with blst's accept/reject rules,
+// Scott's endomorphism subgroup tests, and 64-bit scalar multiplication.
+#pragma once
+#include "fp2.h"
+
+namespace gbv {
+
+// ---- overloads so the point code is written once for both fields --------------------------
+GBV_HD Fp f_add(const Fp& a, const Fp& b) { return fp_add(a, b); }
+GBV_HD Fp f_sub(const Fp& a, const Fp& b) { return fp_sub(a, b); }
+GBV_HD Fp f_neg(const Fp& a) { return fp_neg(a); }
+GBV_HD Fp f_dbl(const Fp& a) { return fp_dbl(a); }
+GBV_HD Fp f_mul(const Fp& a, const Fp& b) { return fp_mul(a, b); }
+GBV_HD Fp f_sqr(const Fp& a) { return fp_sqr(a); }
+GBV_HD bool f_is_zero(const Fp& a) { return fp_is_zero(a); }
+GBV_HD bool f_eq(const Fp& a, const Fp& b) { return fp_eq(a, b); }
+GBV_HD Fp f_sel(bool c, const Fp& a, const Fp& b) { return fp_sel(c, a, b); }
+GBV_HD Fp f_inv(const Fp& a) { return fp_inv(a); }
+GBV_HD void f_one(Fp& r) { r = FP_ONE; }
+GBV_HD void f_zero(Fp& r) { r = fp_zero(); }
+
+GBV_HD Fp2 f_add(const Fp2& a, const Fp2& b) { return fp2_add(a, b); }
+GBV_HD Fp2 f_sub(const Fp2& a, const Fp2& b) { return fp2_sub(a, b); }
+GBV_HD Fp2 f_neg(const Fp2& a) { return fp2_neg(a); }
+GBV_HD Fp2 f_dbl(const Fp2& a) { return fp2_dbl(a); }
+GBV_HD Fp2 f_mul(const Fp2& a, const Fp2& b) { return fp2_mul(a, b); }
+GBV_HD Fp2 f_sqr(const Fp2& a) { return fp2_sqr(a); }
+GBV_HD bool f_is_zero(const Fp2& a) { return fp2_is_zero(a); }
+GBV_HD bool f_eq(const Fp2& a, const Fp2& b) { return fp2_eq(a, b); }
+GBV_HD Fp2 f_sel(bool c, const Fp2& a, const Fp2& b) { return fp2_sel(c, a, b); }
+GBV_HD Fp2 f_inv(const Fp2& a) { return fp2_inv(a); }
+GBV_HD void f_one(Fp2& r) { r = fp2_one(); }
+GBV_HD void f_zero(Fp2& r) { r = fp2_zero(); }
+
+template <class F> struct Jac { F x, y, z; };   // infinity <=> z == 0
+template <class F> struct Aff { F x, y; };      // infinity tracked by the caller
+
+using G1J = Jac<Fp>;
+using G1A = Aff<Fp>;
+using G2J = Jac<Fp2>;
+using G2A = Aff<Fp2>;
+
+template <class F> GBV_HD Jac<F> jac_infinity() {
+  Jac<F> r;
+  f_one(r.x);
+  f_one(r.y);
+  f_zero(r.z);
+  return r;
+}
+
+template <class F> GBV_HD Jac<F> jac_from_aff(const Aff<F>& a) {
+  Jac<F> r;
+  r.x = a.x;
+  r.y = a.y;
+  f_one(r.z);
+  return r;
+}
+
+template <class F> GBV_HD bool jac_is_inf(const Jac<F>& p) { return f_is_zero(p.z); }
+
+template <class F> GBV_HD Jac<F> jac_sel(bool c, const Jac<F>& a, const Jac<F>& b) {
+  return Jac<F>{f_sel(c, a.x, b.x), f_sel(c, a.y, b.y), f_sel(c, a.z, b.z)};
+}
+
+template <class F> GBV_HD Jac<F> jac_neg(const Jac<F>& p) { return Jac<F>{p.x, f_neg(p.y), p.z}; }
+
+// dbl-2009-l, 2M + 5S.  Complete for a = 0 (2-torsion and infinity give z3 = 0).
+template <class F> GBV_HD Jac<F> jac_dbl(const Jac<F>& p) {
+  F A = f_sqr(p.x);
+  F B = f_sqr(p.y);
+  F C = f_sqr(B);
+  F D = f_dbl(f_sub(f_sub(f_sqr(f_add(p.x, B)), A), C));
+  F E = f_add(f_dbl(A), A);
+  F Fv = f_sqr(E);
+  Jac<F> r;
+  r.x = f_sub(Fv, f_dbl(D));
+  F C8 = f_dbl(f_dbl(f_dbl(C)));
+  r.y = f_sub(f_mul(E, f_sub(D, r.x)), C8);
+  r.z = f_dbl(f_mul(p.y, p.z));
+  return r;
+}
+
+// madd-2007-bl (q affine, not infinity), 7M + 4S, with the exceptional cases handled.
+template <class F> GBV_HD Jac<F> jac_add_aff(const Jac<F>& p, const Aff<F>& q) {
+  F Z1Z1 = f_sqr(p.z);
+  F U2 = f_mul(q.x, Z1Z1);
+  F S2 = f_mul(q.y, f_mul(p.z, Z1Z1));
+  F H = f_sub(U2, p.x);
+  F rr = f_dbl(f_sub(S2, p.y));
+  bool p_inf = f_is_zero(p.z);
+  if (f_is_zero(H) && !p_inf) {  // same x: doubling or inverse points (rare, divergent)
+    if (f_is_zero(rr)) return jac_dbl(p);
+    return jac_infinity<F>();
+  }
+  F HH = f_sqr(H);
+  F I = f_dbl(f_dbl(HH));
+  F J = f_mul(H, I);
+  F V = f_mul(p.x, I);
+  Jac<F> r;
+  r.x = f_sub(f_sub(f_sqr(rr), J), f_dbl(V));
+  r.y = f_sub(f_mul(rr, f_sub(V, r.x)), f_dbl(f_mul(p.y, J)));
+  r.z = f_sub(f_sub(f_sqr(f_add(p.z, H)), Z1Z1), HH);
+  return jac_sel(p_inf, jac_from_aff(q), r);
+}
+
+// add-2007-bl, 11M + 5S, complete via the same exceptional-case handling.
+template <class F> GBV_HD Jac<F> jac_add(const Jac<F>& p, const Jac<F>& q) {
+  bool p_inf = f_is_zero(p.z);
+  bool q_inf = f_is_zero(q.z);
+  F Z1Z1 = f_sqr(p.z);
+  F Z2Z2 = f_sqr(q.z);
+  F U1 = f_mul(p.x, Z2Z2);
+  F U2 = f_mul(q.x, Z1Z1);
+  F S1 = f_mul(p.y, f_mul(q.z, Z2Z2));
+  F S2 = f_mul(q.y, f_mul(p.z, Z1Z1));
+  F H = f_sub(U2, U1);
+  F rr = f_dbl(f_sub(S2, S1));
+  if (f_is_zero(H) && !p_inf && !q_inf) {
+    if (f_is_zero(rr)) return jac_dbl(p);
+    return jac_infinity<F>();
+  }
+  F I = f_sqr(f_dbl(H));
+  F J = f_mul(H, I);
+  F V = f_mul(U1, I);
+  Jac<F> r;
+  r.x = f_sub(f_sub(f_sqr(rr), J), f_dbl(V));
+  r.y = f_sub(f_mul(rr, f_sub(V, r.x)), f_dbl(f_mul(S1, J)));
+  r.z = f_mul(f_sub(f_sub(f_sqr(f_add(p.z, q.z)), Z1Z1), Z2Z2), H);
+  r = jac_sel(q_inf, p, r);
+  return jac_sel(p_inf, q, r);
+}
+
+// returns false for infinity
+template <class F> GBV_HD bool jac_to_aff(Aff<F>& out, const Jac<F>& p) {
+  F zi = f_inv(p.z);
+  F zi2 = f_sqr(zi);
+  out.x = f_mul(p.x, zi2);
+  out.y = f_mul(p.y, f_mul(zi2, zi));
+  return !f_is_zero(p.z);
+}
+
+// p == q (q affine, not infinity)?
+template <class F> GBV_HD bool jac_eq_aff(const Jac<F>& p, const Aff<F>& q) {
+  F z2 = f_sqr(p.z);
+  bool ex = f_eq(p.x, f_mul(q.x, z2));
+  bool ey = f_eq(p.y, f_mul(q.y, f_mul(z2, p.z)));
+  return ex && ey && !f_is_zero(p.z);
+}
+
+// [k] q for a 64-bit k (left-to-right double-and-add, q affine, not infinity)
+template <class F> GBV_HD Jac<F> jac_mul_u64(const Aff<F>& q, uint64_t k) {
+  Jac<F> r = jac_infinity<F>();
+  if (k == 0) return r;
+  int top = 63;
+  while (((k >> top) & 1ull) == 0) --top;
+  r = jac_from_aff(q);
+  for (int i = top - 1; i >= 0; --i) {
+    r = jac_dbl(r);
+    if ((k >> i) & 1ull) r = jac_add_aff(r, q);
+  }
+  return r;
+}
+
+// [|x|] q, |x| = 0xd201000000010000 (fixed public scalar: uniform control flow)
+template <class F> GBV_HD Jac<F> jac_mul_xabs(const Aff<F>& q) {
+  Jac<F> r = jac_from_aff(q);
+  for (int i = 62; i >= 0; --i) {
+    r = jac_dbl(r);
+    if ((X_ABS >> i) & 1ull) r = jac_add_aff(r, q);
+  }
+  return r;
+}
+
+template <class F> GBV_HD Jac<F> jac_mul_xabs_jac(const Jac<F>& q) {
+  Jac<F> r = q;
+  for (int i = 62; i >= 0; --i) {
+    r = jac_dbl(r);
+    if ((X_ABS >> i) & 1ull) r = jac_add(r, q);
+  }
+  return r;
+}
+
+// ---- curve constants & decoding -------------------------------------------------------------
+enum : uint8_t {
+  GBV_PT_OK = 0,
+  GBV_PT_BAD_ENCODING = 1,
+  GBV_PT_NOT_ON_CURVE = 2,
+  GBV_PT_NOT_IN_GROUP = 3,
+  GBV_PT_INFINITY = 4,
+};
+
+GBV_HD bool bytes_zero(const uint8_t* b, int n) {
+  uint32_t acc = 0;
+  for (int i = 0; i < n; ++i) acc |= b[i];
+  return acc == 0;
+}
+
+// blst POINTonE1_Uncompress_Z (PublicKey.fromBytes): 48 bytes -> affine (Montgomery).
+// Returns GBV_PT_INFINITY for the canonical infinity encoding.
+GBV_HD uint8_t g1_decompress(G1A& out, const uint8_t* in) {
+  uint8_t in0 = in[0];
+  if ((in0 & 0x80) == 0) return GBV_PT_BAD_ENCODING;
+  if (in0 & 0x40) {
+    if ((in0 & 0x3f) == 0 && bytes_zero(in + 1, 47)) return GBV_PT_INFINITY;
+    return GBV_PT_BAD_ENCODING;
+  }
+  Fp xr = fp_load_be48(in, true);
+  if (!fp_raw_is_canonical(xr)) return GBV_PT_BAD_ENCODING;
+  Fp x = fp_to_mont(xr);
+  Fp y2 = fp_add(fp_mul(fp_sqr(x), x), FP_B1);
+  Fp y = fp_sqrt_candidate(y2);
+  if (!fp_eq(fp_sqr(y), y2)) return GBV_PT_NOT_ON_CURVE;
+  bool want_large = (in0 & 0x20) != 0;
+  if (fp_is_lexi_large(y) != want_large) y = fp_neg(y);
+  out.x = x;
+  out.y = y;
+  if (fp_is_zero(x)) return GBV_PT_NOT_IN_GROUP;
+  return GBV_PT_OK;
+}
+
+GBV_HD void g1_compress(uint8_t* out, const G1A& a, bool inf) {
+  if (inf) {
+    out[0] = 0xc0;
+    for (int i = 1; i < 48; ++i) out[i] = 0;
+    return;
+  }
+  fp_store_be48(out, fp_from_mont(a.x));
+  out[0] |= 0x80;
+  if (fp_is_lexi_large(a.y)) out[0] |= 0x20;
+}
+
+GBV_HD bool g2_on_curve(const G2A& a) {
+  Fp2 y2 = fp2_sqr(a.y);
+  Fp2 rhs = fp2_add(fp2_mul(fp2_sqr(a.x), a.x), FP2_B2);
+  return fp2_eq(y2, rhs);
+}
+
+// blst POINTonE2_Uncompress_Z (96 bytes) / POINTonE2_Deserialize_Z (192 bytes).
+GBV_HD uint8_t g2_decode(G2A& out, const uint8_t* in, uint32_t len) {
+  uint8_t in0 = in[0];
+  if (len == 96) {
+    if ((in0 & 0x80) == 0) return GBV_PT_BAD_ENCODING;
+    if (in0 & 0x40) {
+      if ((in0 & 0x3f) == 0 && bytes_zero(in + 1, 95)) return GBV_PT_INFINITY;
+      return GBV_PT_BAD_ENCODING;
+    }
+    Fp x1r = fp_load_be48(in, true);
+    Fp x0r = fp_load_be48(in + 48, false);
+    if (!fp_raw_is_canonical(x1r) || !fp_raw_is_canonical(x0r)) return GBV_PT_BAD_ENCODING;
+    Fp2 x{fp_to_mont(x0r), fp_to_mont(x1r)};
+    Fp2 y2 = fp2_add(fp2_mul(fp2_sqr(x), x), FP2_B2);
+    Fp2 y;
+    if (!fp2_sqrt(y, y2)) return GBV_PT_NOT_ON_CURVE;
+    bool want_large = (in0 & 0x20) != 0;
+    if (fp2_is_lexi_large(y) != want_large) y = fp2_neg(y);
+    out.x = x;
+    out.y = y;
+    if (fp2_is_zero(x)) return GBV_PT_NOT_IN_GROUP;
+    return GBV_PT_OK;
+  }
+  if (len == 192) {
+    if (in0 & 0x80) return GBV_PT_BAD_ENCODING;
+    if (in0 & 0xe0) {
+      if ((in0 & 0x40) && (in0 & 0x3f) == 0 && bytes_zero(in + 1, 191)) return GBV_PT_INFINITY;
+      return GBV_PT_BAD_ENCODING;
+    }
+    Fp r[4];
+    for (int i = 0; i < 4; ++i) {
+      r[i] = fp_load_be48(in + 48 * i, false);
+      if (!fp_raw_is_canonical(r[i])) return GBV_PT_BAD_ENCODING;
+    }
+    out.x = Fp2{fp_to_mont(r[1]), fp_to_mont(r[0])};
+    out.y = Fp2{fp_to_mont(r[3]), fp_to_mont(r[2])};
+    if (!g2_on_curve(out)) return GBV_PT_NOT_ON_CURVE;
+    if (fp2_is_zero(out.x)) return GBV_PT_NOT_IN_GROUP;
+    return GBV_PT_OK;
+  }
+  return GBV_PT_BAD_ENCODING;
+}
+
+GBV_HD void g2_compress(uint8_t* out, const G2A& a, bool inf) {
+  if (inf) {
+    out[0] = 0xc0;
+    for (int i = 1; i < 96; ++i) out[i] = 0;
+    return;
+  }
+  fp_store_be48(out, fp_from_mont(a.x.c1));
+  fp_store_be48(out + 48, fp_from_mont(a.x.c0));
+  out[0] |= 0x80;
+  if (fp2_is_lexi_large(a.y)) out[0] |= 0x20;
+}
+
+// psi(x, y) = (conj(x) PSI_X, conj(y) PSI_Y)
+GBV_HD G2A g2_psi(const G2A& a) {
+  return G2A{fp2_mul(fp2_conj(a.x), PSI_X), fp2_mul(fp2_conj(a.y), PSI_Y)};
+}
+
+GBV_HD G2J g2_psi_jac(const G2J& a) {
+  return G2J{fp2_mul(fp2_conj(a.x), PSI_X), fp2_mul(fp2_conj(a.y), PSI_Y), fp2_conj(a.z)};
+}
+
+// G2 membership (Scott 2021): psi(Q) == [x] Q = -[|x|] Q.  Q affine, not infinity.
+GBV_HD bool g2_in_subgroup(const G2A& q) {
+  G2J xq = jac_neg(jac_mul_xabs(q));
+  return jac_eq_aff(xq, g2_psi(q));
+}
+
+// G1 membership (Scott 2021): (beta x, y) == [-x^2] P.  P affine, not infinity.
+GBV_HD bool g1_in_subgroup(const G1A& p) {
+  G1J t = jac_mul_xabs(p);           // [|x|] P
+  t = jac_mul_xabs_jac(t);           // [x^2] P
+  t = jac_neg(t);                    // [-x^2] P
+  G1A phi{fp_mul(p.x, FP_BETA), p.y};
+  return jac_eq_aff(t, phi);
+}
+
+}  // namespace gbv

@@ -1,0 +1,198 @@
+// Fp arithmetic for BLS12-381 on the gfx950 integer VALU.
+//
+// One thread owns one element: 12 x 32-bit limbs in VGPRs, Montgomery form.  Multiplication is
+// CIOS Montgomery with the "no final carry" shortcut (top limb of p < 2^31), so every
+// limb product is one v_mad_u64_u32 (u32 x u32 + u64 -> u64) -- measured full-rate on MI355X
+// (tools/ubench_int.hip).  There is no floating point anywhere in this library.
+//
+// The blst operations this replaces: mul_fp / sqr_fp / add_fp / sub_fp /
+// sqrt_fp / reciprocal_fp inside @chainsafe/blst 2.1.0 (yarn.lock:446-457).
+#pragma once
+#include "fp_types.h"
+#include "bls_constants.h"
+
+namespace gbv {
+
+GBV_HD Fp fp_zero() {
+  Fp r;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) r.v[i] = 0;
+  return r;
+}
+
+GBV_HD bool fp_is_zero(const Fp& a) {
+  uint32_t acc = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) acc |= a.v[i];
+  return acc == 0;
+}
+
+GBV_HD bool fp_eq(const Fp& a, const Fp& b) {
+  uint32_t acc = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) acc |= a.v[i] ^ b.v[i];
+  return acc == 0;
+}
+
+// r = c ? a : b  (branch-free select; the compiler emits v_cndmask)
+GBV_HD Fp fp_sel(bool c, const Fp& a, const Fp& b) {
+  Fp r;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) r.v[i] = c ? a.v[i] : b.v[i];
+  return r;
+}
+
+// Raw 384-bit helpers ------------------------------------------------------------------------
+// s = a - b, returns borrow (1 if a < b)
+GBV_HD uint32_t raw_sub(Fp& s, const Fp& a, const Fp& b) {
+  uint32_t br = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    uint64_t d = (uint64_t)a.v[i] - b.v[i] - br;
+    s.v[i] = (uint32_t)d;
+    br = (uint32_t)(d >> 63);
+  }
+  return br;
+}
+
+GBV_HD uint32_t raw_add(Fp& s, const Fp& a, const Fp& b) {
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    c += (uint64_t)a.v[i] + b.v[i];
+    s.v[i] = (uint32_t)c;
+    c >>= 32;
+  }
+  return (uint32_t)c;
+}
+
+// reduce x in [0, 2p) to [0, p)
+GBV_HD Fp fp_reduce_once(const Fp& x) {
+  Fp t;
+  uint32_t br = raw_sub(t, x, P_RAW);
+  return fp_sel(br != 0, x, t);
+}
+
+GBV_HD Fp fp_add(const Fp& a, const Fp& b) {
+  Fp s;
+  raw_add(s, a, b);  // < 2p < 2^382: no carry out
+  return fp_reduce_once(s);
+}
+
+GBV_HD Fp fp_sub(const Fp& a, const Fp& b) {
+  Fp d, t;
+  uint32_t br = raw_sub(d, a, b);
+  raw_add(t, d, P_RAW);
+  return fp_sel(br != 0, t, d);
+}
+
+GBV_HD Fp fp_neg(const Fp& a) {
+  Fp d;
+  raw_sub(d, P_RAW, a);
+  return fp_sel(fp_is_zero(a), a, d);
+}
+
+GBV_HD Fp fp_dbl(const Fp& a) { return fp_add(a, a); }
+
+// Montgomery product a*b*2^-384 mod p.  Inputs < p, output < p.
+GBV_HD Fp fp_mul_inl(const Fp& a, const Fp& b) {
+  uint32_t t[12];
+#pragma unroll
+  for (int i = 0; i < 12; ++i) t[i] = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    const uint32_t bi = b.v[i];
+    uint64_t A = (uint64_t)a.v[0] * bi + t[0];
+    const uint32_t m = (uint32_t)A * NP0;
+    uint64_t C = (uint64_t)m * P_RAW.v[0] + (uint32_t)A;
+    A >>= 32;
+    C >>= 32;
+#pragma unroll
+    for (int j = 1; j < 12; ++j) {
+      A = (uint64_t)a.v[j] * bi + t[j] + A;
+      C = (uint64_t)m * P_RAW.v[j] + (uint32_t)A + C;
+      t[j - 1] = (uint32_t)C;
+      A >>= 32;
+      C >>= 32;
+    }
+    t[11] = (uint32_t)(A + C);
+  }
+  Fp r;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) r.v[i] = t[i];
+  return fp_reduce_once(r);
+}
+
+GBV_HD Fp fp_sqr_inl(const Fp& a) { return fp_mul_inl(a, a); }
+
+// Out-of-line versions: keep the hot loops of the big kernels inside the instruction cache.
+GBV_NI Fp fp_mul(Fp a, Fp b) { return fp_mul_inl(a, b); }
+GBV_NI Fp fp_sqr(Fp a) { return fp_sqr_inl(a); }
+
+GBV_HD Fp fp_to_mont(const Fp& raw) { return fp_mul(raw, R2_RAW); }
+
+GBV_HD Fp fp_from_mont(const Fp& a) {
+  Fp one = fp_zero();
+  one.v[0] = 1;
+  return fp_mul(a, one);
+}
+
+// a^e for a fixed public exponent (12 little-endian words, top bit index nbits-1).
+// Square-and-multiply; the branch is on the public exponent so all lanes agree.
+GBV_NI Fp fp_pow(Fp a, const uint32_t* e, int nbits) {
+  Fp r = a;
+  for (int i = nbits - 2; i >= 0; --i) {
+    r = fp_sqr(r);
+    if ((e[i >> 5] >> (i & 31)) & 1) r = fp_mul(r, a);
+  }
+  return r;
+}
+
+GBV_HD Fp fp_inv(const Fp& a) { return fp_pow(a, EXP_INV, EXP_INV_BITS); }  // 0 -> 0
+
+// Canonical (non-Montgomery) value comparisons used by sign rules ----------------------------
+// true iff canonical(a) > (p-1)/2
+GBV_HD bool fp_is_lexi_large(const Fp& a_mont) {
+  Fp c = fp_from_mont(a_mont);
+  Fp t;
+  uint32_t br = raw_sub(t, P_HALF_RAW, c);  // borrow iff half < c
+  return br != 0;
+}
+
+GBV_HD uint32_t fp_parity(const Fp& a_mont) { return fp_from_mont(a_mont).v[0] & 1u; }
+
+// Big-endian 48-byte decoding/encoding -------------------------------------------------------
+// Loads 48 big-endian bytes (optionally masking the top 3 flag bits) into raw limbs.
+GBV_HD Fp fp_load_be48(const uint8_t* b, bool mask_flags) {
+  Fp r;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    const uint8_t* q = b + 44 - 4 * i;
+    r.v[i] = ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | (uint32_t)q[3];
+  }
+  if (mask_flags) r.v[11] &= 0x1fffffffu;
+  return r;
+}
+
+GBV_HD void fp_store_be48(uint8_t* b, const Fp& raw) {
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    uint8_t* q = b + 44 - 4 * i;
+    uint32_t w = raw.v[i];
+    q[0] = (uint8_t)(w >> 24);
+    q[1] = (uint8_t)(w >> 16);
+    q[2] = (uint8_t)(w >> 8);
+    q[3] = (uint8_t)w;
+  }
+}
+
+// raw < p ?
+GBV_HD bool fp_raw_is_canonical(const Fp& raw) {
+  Fp t;
+  return raw_sub(t, raw, P_RAW) != 0;
+}
+
+// Square root candidate a^((p+1)/4); caller checks r^2 == a.
+GBV_HD Fp fp_sqrt_candidate(const Fp& a) { return fp_pow(a, EXP_SQRT, EXP_SQRT_BITS); }
+
+}  // namespace gbv

@@ -1,0 +1,114 @@
+// Fp6 = Fp2[v]/(v^3 - xi), Fp12 = Fp6[w]/(w^2 - v), xi = 1 + i.
+// Sparse line multiplication for the Miller loop and the final exponentiation
+// (easy part by Frobenius, hard part by the x-chain 3(p^4-p^2+1)/r = (x-1)^2 (x+p)(x^2+p^2-1) + 3).
+#pragma once
+#include "fp2.h"
+
+namespace gbv {
+
+GBV_HD Fp6 fp6_zero() { return Fp6{fp2_zero(), fp2_zero(), fp2_zero()}; }
+GBV_HD Fp6 fp6_one() { return Fp6{fp2_one(), fp2_zero(), fp2_zero()}; }
+GBV_HD Fp6 fp6_add(const Fp6& a, const Fp6& b) { return Fp6{fp2_add(a.c0, b.c0), fp2_add(a.c1, b.c1), fp2_add(a.c2, b.c2)}; }
+GBV_HD Fp6 fp6_sub(const Fp6& a, const Fp6& b) { return Fp6{fp2_sub(a.c0, b.c0), fp2_sub(a.c1, b.c1), fp2_sub(a.c2, b.c2)}; }
+GBV_HD Fp6 fp6_neg(const Fp6& a) { return Fp6{fp2_neg(a.c0), fp2_neg(a.c1), fp2_neg(a.c2)}; }
+GBV_HD bool fp6_eq(const Fp6& a, const Fp6& b) { return fp2_eq(a.c0, b.c0) && fp2_eq(a.c1, b.c1) && fp2_eq(a.c2, b.c2); }
+// multiply by v: (c0, c1, c2) -> (xi c2, c0, c1)
+GBV_HD Fp6 fp6_mul_v(const Fp6& a) { return Fp6{fp2_mul_xi(a.c2), a.c0, a.c1}; }
+
+GBV_HD Fp6 fp6_mul(const Fp6& a, const Fp6& b) {
+  Fp2 t0 = fp2_mul(a.c0, b.c0);
+  Fp2 t1 = fp2_mul(a.c1, b.c1);
+  Fp2 t2 = fp2_mul(a.c2, b.c2);
+  Fp2 c0 = fp2_add(t0, fp2_mul_xi(fp2_sub(fp2_sub(fp2_mul(fp2_add(a.c1, a.c2), fp2_add(b.c1, b.c2)), t1), t2)));
+  Fp2 c1 = fp2_add(fp2_sub(fp2_sub(fp2_mul(fp2_add(a.c0, a.c1), fp2_add(b.c0, b.c1)), t0), t1), fp2_mul_xi(t2));
+  Fp2 c2 = fp2_add(fp2_sub(fp2_sub(fp2_mul(fp2_add(a.c0, a.c2), fp2_add(b.c0, b.c2)), t0), t2), t1);
+  return Fp6{c0, c1, c2};
+}
+
+// (f0, f1, f2) * (a, b, 0)
+GBV_HD Fp6 fp6_mul_by_01(const Fp6& f, const Fp2& a, const Fp2& b) {
+  Fp2 t0 = fp2_mul(f.c0, a);
+  Fp2 t1 = fp2_mul(f.c1, b);
+  Fp2 c1 = fp2_sub(fp2_sub(fp2_mul(fp2_add(f.c0, f.c1), fp2_add(a, b)), t0), t1);
+  Fp2 c0 = fp2_add(t0, fp2_mul_xi(fp2_mul(f.c2, b)));
+  Fp2 c2 = fp2_add(t1, fp2_mul(f.c2, a));
+  return Fp6{c0, c1, c2};
+}
+
+// (f0, f1, f2) * (0, c, 0) = (xi f2 c, f0 c, f1 c)
+GBV_HD Fp6 fp6_mul_by_1(const Fp6& f, const Fp2& c) {
+  return Fp6{fp2_mul_xi(fp2_mul(f.c2, c)), fp2_mul(f.c0, c), fp2_mul(f.c1, c)};
+}
+
+GBV_HD Fp6 fp6_inv(const Fp6& a) {
+  Fp2 t0 = fp2_sub(fp2_sqr(a.c0), fp2_mul_xi(fp2_mul(a.c1, a.c2)));
+  Fp2 t1 = fp2_sub(fp2_mul_xi(fp2_sqr(a.c2)), fp2_mul(a.c0, a.c1));
+  Fp2 t2 = fp2_sub(fp2_sqr(a.c1), fp2_mul(a.c0, a.c2));
+  Fp2 d = fp2_add(fp2_mul(a.c0, t0), fp2_mul_xi(fp2_add(fp2_mul(a.c2, t1), fp2_mul(a.c1, t2))));
+  Fp2 di = fp2_inv(d);
+  return Fp6{fp2_mul(t0, di), fp2_mul(t1, di), fp2_mul(t2, di)};
+}
+
+// ---- Fp12 ----------------------------------------------------------------------------------
+GBV_HD Fp12 fp12_one() { return Fp12{fp6_one(), fp6_zero()}; }
+GBV_HD bool fp12_eq(const Fp12& a, const Fp12& b) { return fp6_eq(a.c0, b.c0) && fp6_eq(a.c1, b.c1); }
+GBV_HD bool fp12_is_one(const Fp12& a) { return fp12_eq(a, fp12_one()); }
+GBV_HD Fp12 fp12_conj(const Fp12& a) { return Fp12{a.c0, fp6_neg(a.c1)}; }
+
+GBV_NI Fp12 fp12_mul(Fp12 a, Fp12 b) {
+  Fp6 t0 = fp6_mul(a.c0, b.c0);
+  Fp6 t1 = fp6_mul(a.c1, b.c1);
+  Fp6 c1 = fp6_sub(fp6_sub(fp6_mul(fp6_add(a.c0, a.c1), fp6_add(b.c0, b.c1)), t0), t1);
+  return Fp12{fp6_add(t0, fp6_mul_v(t1)), c1};
+}
+
+GBV_NI Fp12 fp12_sqr(Fp12 a) {
+  Fp6 t = fp6_mul(a.c0, a.c1);
+  Fp6 c0 = fp6_sub(fp6_sub(fp6_mul(fp6_add(a.c0, a.c1), fp6_add(a.c0, fp6_mul_v(a.c1))), t), fp6_mul_v(t));
+  return Fp12{c0, fp6_add(t, t)};
+}
+
+// f * line, line = (c0 + c2 v) + (c3 v) w  (coefficients at w^0, w^2, w^3)
+GBV_NI Fp12 fp12_mul_line(Fp12 f, Fp2 c0, Fp2 c2, Fp2 c3) {
+  Fp6 a = fp6_mul_by_01(f.c0, c0, c2);
+  Fp6 b = fp6_mul_by_1(f.c1, c3);
+  Fp6 e = fp6_mul_by_01(fp6_add(f.c0, f.c1), c0, fp2_add(c2, c3));
+  return Fp12{fp6_add(a, fp6_mul_v(b)), fp6_sub(fp6_sub(e, a), b)};
+}
+
+GBV_NI Fp12 fp12_inv(Fp12 a) {
+  Fp6 d = fp6_sub(fp6_mul(a.c0, a.c0), fp6_mul_v(fp6_mul(a.c1, a.c1)));
+  Fp6 di = fp6_inv(d);
+  return Fp12{fp6_mul(a.c0, di), fp6_neg(fp6_mul(a.c1, di))};
+}
+
+GBV_NI Fp12 fp12_frob(Fp12 a) {
+  Fp6 c0{fp2_conj(a.c0.c0), fp2_mul(fp2_conj(a.c0.c1), FROB_V1), fp2_mul(fp2_conj(a.c0.c2), FROB_V2)};
+  Fp6 c1{fp2_mul(fp2_conj(a.c1.c0), FROB_W), fp2_mul(fp2_conj(a.c1.c1), FROB_V1W), fp2_mul(fp2_conj(a.c1.c2), FROB_V2W)};
+  return Fp12{c0, c1};
+}
+
+// a^|x| for a in the cyclotomic subgroup, then conjugate: a^x (x < 0)
+GBV_NI Fp12 fp12_exp_x(Fp12 a) {
+  Fp12 r = a;
+  for (int i = 62; i >= 0; --i) {
+    r = fp12_sqr(r);
+    if ((X_ABS >> i) & 1ull) r = fp12_mul(r, a);
+  }
+  return fp12_conj(r);
+}
+
+// f^(3 (p^12 - 1)/r).  Equal to 1 iff f^((p^12-1)/r) == 1 (gcd(3, r) = 1).
+GBV_NI Fp12 final_exponentiation(Fp12 f) {
+  Fp12 t = fp12_mul(fp12_conj(f), fp12_inv(f));  // f^(p^6 - 1)
+  t = fp12_mul(fp12_frob(fp12_frob(t)), t);       // ^(p^2 + 1)
+  Fp12 a = fp12_mul(fp12_exp_x(t), fp12_conj(t)); // t^(x-1)
+  a = fp12_mul(fp12_exp_x(a), fp12_conj(a));      // t^((x-1)^2)
+  Fp12 b = fp12_mul(fp12_exp_x(a), fp12_frob(a)); // a^(x+p)
+  Fp12 c = fp12_mul(fp12_exp_x(fp12_exp_x(b)), fp12_frob(fp12_frob(b)));
+  c = fp12_mul(c, fp12_conj(b));                  // b^(x^2+p^2-1)
+  Fp12 t3 = fp12_mul(fp12_sqr(t), t);
+  return fp12_mul(c, t3);
+}
+
+}  // namespace gbv

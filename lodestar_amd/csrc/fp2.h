@@ -1,0 +1,86 @@
+// Fp2 = Fp[i]/(i^2 + 1).  Karatsuba multiplication; the three base products are inlined into one
+// out-of-line function so the scheduler can interleave their independent v_mad_u64_u32 chains.
+#pragma once
+#include "fp.h"
+
+namespace gbv {
+
+GBV_HD Fp2 fp2_zero() { return Fp2{fp_zero(), fp_zero()}; }
+GBV_HD Fp2 fp2_one() { return Fp2{FP_ONE, fp_zero()}; }
+GBV_HD Fp2 fp2_make(const Fp& a, const Fp& b) { return Fp2{a, b}; }
+GBV_HD bool fp2_is_zero(const Fp2& a) { return fp_is_zero(a.c0) && fp_is_zero(a.c1); }
+GBV_HD bool fp2_eq(const Fp2& a, const Fp2& b) { return fp_eq(a.c0, b.c0) && fp_eq(a.c1, b.c1); }
+GBV_HD Fp2 fp2_sel(bool c, const Fp2& a, const Fp2& b) { return Fp2{fp_sel(c, a.c0, b.c0), fp_sel(c, a.c1, b.c1)}; }
+GBV_HD Fp2 fp2_add(const Fp2& a, const Fp2& b) { return Fp2{fp_add(a.c0, b.c0), fp_add(a.c1, b.c1)}; }
+GBV_HD Fp2 fp2_sub(const Fp2& a, const Fp2& b) { return Fp2{fp_sub(a.c0, b.c0), fp_sub(a.c1, b.c1)}; }
+GBV_HD Fp2 fp2_neg(const Fp2& a) { return Fp2{fp_neg(a.c0), fp_neg(a.c1)}; }
+GBV_HD Fp2 fp2_dbl(const Fp2& a) { return Fp2{fp_dbl(a.c0), fp_dbl(a.c1)}; }
+GBV_HD Fp2 fp2_conj(const Fp2& a) { return Fp2{a.c0, fp_neg(a.c1)}; }
+// (a0 + a1 i)(1 + i) = (a0 - a1) + (a0 + a1) i
+GBV_HD Fp2 fp2_mul_xi(const Fp2& a) { return Fp2{fp_sub(a.c0, a.c1), fp_add(a.c0, a.c1)}; }
+
+GBV_HD Fp2 fp2_mul_inl(const Fp2& a, const Fp2& b) {
+  Fp t0 = fp_mul_inl(a.c0, b.c0);
+  Fp t1 = fp_mul_inl(a.c1, b.c1);
+  Fp t2 = fp_mul_inl(fp_add(a.c0, a.c1), fp_add(b.c0, b.c1));
+  return Fp2{fp_sub(t0, t1), fp_sub(fp_sub(t2, t0), t1)};
+}
+
+GBV_HD Fp2 fp2_sqr_inl(const Fp2& a) {
+  Fp t0 = fp_mul_inl(fp_add(a.c0, a.c1), fp_sub(a.c0, a.c1));
+  Fp t1 = fp_mul_inl(a.c0, a.c1);
+  return Fp2{t0, fp_dbl(t1)};
+}
+
+GBV_NI Fp2 fp2_mul(Fp2 a, Fp2 b) { return fp2_mul_inl(a, b); }
+GBV_NI Fp2 fp2_sqr(Fp2 a) { return fp2_sqr_inl(a); }
+
+GBV_HD Fp2 fp2_mul_fp(const Fp2& a, const Fp& s) { return Fp2{fp_mul(a.c0, s), fp_mul(a.c1, s)}; }
+
+GBV_HD Fp2 fp2_inv(const Fp2& a) {
+  Fp n = fp_add(fp_sqr(a.c0), fp_sqr(a.c1));
+  Fp ni = fp_inv(n);
+  return Fp2{fp_mul(a.c0, ni), fp_neg(fp_mul(a.c1, ni))};
+}
+
+// RFC 9380 sgn0 for Fp2 (canonical values)
+GBV_HD uint32_t fp2_sgn0(const Fp2& a) {
+  Fp c0 = fp_from_mont(a.c0);
+  Fp c1 = fp_from_mont(a.c1);
+  uint32_t sign0 = c0.v[0] & 1u;
+  uint32_t zero0 = fp_is_zero(c0) ? 1u : 0u;
+  uint32_t sign1 = c1.v[0] & 1u;
+  return sign0 | (zero0 & sign1);
+}
+
+// ZCash "lexicographically largest" (c1 first, then c0) -- blst sgn0_pty_mod_384x sign bit.
+GBV_HD bool fp2_is_lexi_large(const Fp2& a) {
+  bool c1_zero = fp_is_zero(a.c1);
+  bool l1 = fp_is_lexi_large(a.c1);
+  bool l0 = fp_is_lexi_large(a.c0);
+  return c1_zero ? l0 : l1;
+}
+
+// Square root in Fp2 with uniform cost (two Fp exponentiations, no data-dependent branch):
+//   alpha = sqrt(a0^2 + a1^2);  delta = (a0 + alpha)/2 (or (a0 - alpha)/2 if that is 0);
+//   t = delta^((p-3)/4);  x0 = t*delta;  if x0*t == 1: root = (x0, a1 t / 2) else (-a1 t / 2, x0).
+// Returns true iff a is a square (root^2 == a).  Prototype: tests/test_algorithm_prototypes.py.
+GBV_HD bool fp2_sqrt(Fp2& root, const Fp2& a) {
+  Fp n = fp_add(fp_sqr(a.c0), fp_sqr(a.c1));
+  Fp alpha = fp_pow(n, EXP_SQRT, EXP_SQRT_BITS);
+  Fp delta = fp_mul(fp_add(a.c0, alpha), FP_INV2);
+  Fp delta2 = fp_mul(fp_sub(a.c0, alpha), FP_INV2);
+  delta = fp_sel(fp_is_zero(delta), delta2, delta);
+  Fp t = fp_pow(delta, EXP_SQRT_M3, EXP_SQRT_M3_BITS);
+  Fp x0 = fp_mul(t, delta);
+  bool qr = fp_eq(fp_mul(x0, t), FP_ONE);
+  Fp h = fp_mul(fp_mul(a.c1, t), FP_INV2);
+  root.c0 = fp_sel(qr, x0, fp_neg(h));
+  root.c1 = fp_sel(qr, h, x0);
+  return fp2_eq(fp2_sqr(root), a);
+}
+
+// Frobenius / psi helpers -------------------------------------------------------------------
+GBV_HD Fp2 fp2_frob(const Fp2& a) { return fp2_conj(a); }
+
+}  // namespace gbv

@@ -1,0 +1,93 @@
+// Host build of the device arithmetic library (lodestar_amd/csrc/*.h) for CPU unit tests.
+// This is NOT a product code path: it exists so the field/curve/pairing code can be checked
+// against the Python oracle without a GPU.  Built by tests/native/build_hosttest.sh.
+#include "../../lodestar_amd/csrc/pairing.h"
+#include "../../lodestar_amd/csrc/hash_to_curve.h"
+
+using namespace gbv;
+
+static Fp load_mont(const uint8_t* be48) { return fp_to_mont(fp_load_be48(be48, false)); }
+static void store_canon(uint8_t* be48, const Fp& a) { fp_store_be48(be48, fp_from_mont(a)); }
+static void store_fp2(uint8_t* out, const Fp2& a) { store_canon(out, a.c0); store_canon(out + 48, a.c1); }
+static Fp2 load_fp2(const uint8_t* in) { return Fp2{load_mont(in), load_mont(in + 48)}; }
+
+extern "C" {
+void ht_fp_mul(uint8_t* out, const uint8_t* a, const uint8_t* b) { store_canon(out, fp_mul(load_mont(a), load_mont(b))); }
+void ht_fp_inv(uint8_t* out, const uint8_t* a) { store_canon(out, fp_inv(load_mont(a))); }
+int ht_fp2_sqrt(uint8_t* out, const uint8_t* a) {
+  Fp2 r;
+  bool ok = fp2_sqrt(r, load_fp2(a));
+  store_fp2(out, r);
+  return ok;
+}
+void ht_fp2_mul(uint8_t* out, const uint8_t* a, const uint8_t* b) { store_fp2(out, fp2_mul(load_fp2(a), load_fp2(b))); }
+// out: x.c0 x.c1 y.c0 y.c1 (canonical BE)
+void ht_hash_to_g2(uint8_t* out, const uint8_t* msg32) {
+  uint32_t w[8];
+  for (int i = 0; i < 8; ++i) w[i] = ((uint32_t)msg32[4*i] << 24) | ((uint32_t)msg32[4*i+1] << 16) | ((uint32_t)msg32[4*i+2] << 8) | msg32[4*i+3];
+  G2A q = hash_to_g2(w);
+  store_fp2(out, q.x);
+  store_fp2(out + 96, q.y);
+}
+void ht_expand(uint8_t* out256, const uint8_t* msg32) {
+  uint32_t w[8], o[64];
+  for (int i = 0; i < 8; ++i) w[i] = ((uint32_t)msg32[4*i] << 24) | ((uint32_t)msg32[4*i+1] << 16) | ((uint32_t)msg32[4*i+2] << 8) | msg32[4*i+3];
+  expand_message_xmd_32(o, w);
+  for (int i = 0; i < 64; ++i) { out256[4*i] = o[i] >> 24; out256[4*i+1] = o[i] >> 16; out256[4*i+2] = o[i] >> 8; out256[4*i+3] = o[i]; }
+}
+int ht_g2_decode(uint8_t* out, const uint8_t* in, uint32_t len) {
+  G2A a;
+  uint8_t st = g2_decode(a, in, len);
+  if (st == GBV_PT_OK) { store_fp2(out, a.x); store_fp2(out + 96, a.y); }
+  return st;
+}
+int ht_g2_in_subgroup(const uint8_t* xy) {
+  G2A a{load_fp2(xy), load_fp2(xy + 96)};
+  return g2_in_subgroup(a);
+}
+int ht_g1_decompress(uint8_t* out, const uint8_t* in) {
+  G1A a;
+  uint8_t st = g1_decompress(a, in);
+  if (st == GBV_PT_OK) { store_canon(out, a.x); store_canon(out + 48, a.y); }
+  return st;
+}
+int ht_g1_in_subgroup(const uint8_t* xy) {
+  G1A a{load_mont(xy), load_mont(xy + 48)};
+  return g1_in_subgroup(a);
+}
+// scalar mult by u64 for G2 (affine in/out)
+int ht_g2_mul_u64(uint8_t* out, const uint8_t* xy, uint64_t k) {
+  G2A a{load_fp2(xy), load_fp2(xy + 96)};
+  G2A r;
+  bool ok = jac_to_aff(r, jac_mul_u64(a, k));
+  store_fp2(out, r.x); store_fp2(out + 96, r.y);
+  return ok;
+}
+int ht_g1_mul_u64(uint8_t* out, const uint8_t* xy, uint64_t k) {
+  G1A a{load_mont(xy), load_mont(xy + 48)};
+  G1A r;
+  bool ok = jac_to_aff(r, jac_mul_u64(a, k));
+  store_canon(out, r.x); store_canon(out + 48, r.y);
+  return ok;
+}
+// Miller loop (1 pair) + final exponentiation, Fp12 out as 12 canonical Fp in tower order
+void ht_pairing(uint8_t* out, const uint8_t* p96, const uint8_t* q192) {
+  G1A P{load_mont(p96), load_mont(p96 + 48)};
+  G2A Q{load_fp2(q192), load_fp2(q192 + 96)};
+  Fp12 f = final_exponentiation(miller_loop_1(P, Q));
+  const Fp2* c[6] = {&f.c0.c0, &f.c0.c1, &f.c0.c2, &f.c1.c0, &f.c1.c1, &f.c1.c2};
+  for (int i = 0; i < 6; ++i) store_fp2(out + 96 * i, *c[i]);
+}
+// verify(pk48, msg32, sig) following the blst accept/reject rules
+int ht_verify(const uint8_t* pk48, const uint8_t* msg32, const uint8_t* sig, uint32_t sig_len) {
+  G1A pk;
+  if (g1_decompress(pk, pk48) != GBV_PT_OK) return 0;
+  G2A s;
+  if (g2_decode(s, sig, sig_len) != GBV_PT_OK) return 0;
+  if (!g2_in_subgroup(s)) return 0;
+  uint32_t w[8];
+  for (int i = 0; i < 8; ++i) w[i] = ((uint32_t)msg32[4*i] << 24) | ((uint32_t)msg32[4*i+1] << 16) | ((uint32_t)msg32[4*i+2] << 8) | msg32[4*i+3];
+  G2A h = hash_to_g2(w);
+  return pairing_check_2(pk, false, h, g1_neg_generator(), false, s);
+}
+}

@@ -1,0 +1,155 @@
+"""Device arithmetic library (lodestar_amd/csrc) built for the HOST, checked against the oracle.
+
+Catches logic errors in the field/curve/pairing code without a GPU.  This host build is a test
+fixture only; the product (lodestar_amd) loads nothing but the gfx950 code object.
+"""
+import ctypes
+import os
+import random
+import subprocess
+
+import pytest
+
+from oracle import bls_oracle as o
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "native", "libhosttest.so")
+
+
+@pytest.fixture(scope="module")
+def lib():
+    srcs = [os.path.join(HERE, "native", "hosttest.cpp")] + [
+        os.path.join(HERE, "..", "lodestar_amd", "csrc", f) for f in os.listdir(os.path.join(HERE, "..", "lodestar_amd", "csrc")) if f.endswith(".h")]
+    if not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(s) for s in srcs):
+        subprocess.check_call([os.path.join(HERE, "native", "build_hosttest.sh")])
+    return ctypes.CDLL(LIB)
+
+
+def be(x):
+    return (x % o.P).to_bytes(48, "big")
+
+
+def fp2b(a):
+    return be(a[0]) + be(a[1])
+
+
+def b2fp2(b):
+    return (int.from_bytes(b[:48], "big"), int.from_bytes(b[48:96], "big"))
+
+
+def buf(n):
+    return ctypes.create_string_buffer(n)
+
+
+def test_fp_mul_inv(lib):
+    rng = random.Random(1)
+    for _ in range(50):
+        a, b = rng.randrange(o.P), rng.randrange(o.P)
+        out = buf(48)
+        lib.ht_fp_mul(out, be(a), be(b))
+        assert int.from_bytes(out.raw, "big") == a * b % o.P
+    for a in (1, 2, o.P - 1, rng.randrange(o.P)):
+        out = buf(48)
+        lib.ht_fp_inv(out, be(a))
+        assert int.from_bytes(out.raw, "big") * a % o.P == 1
+
+
+def test_fp2_mul_sqrt(lib):
+    rng = random.Random(2)
+    for k in range(40):
+        a = (rng.randrange(o.P), rng.randrange(o.P))
+        b = (rng.randrange(o.P), rng.randrange(o.P))
+        out = buf(96)
+        lib.ht_fp2_mul(out, fp2b(a), fp2b(b))
+        assert b2fp2(out.raw) == o.f2_mul(a, b)
+        if k < 4:
+            a = [(0, 0), (4, 0), (o.P - 4, 0), (0, 5)][k]
+        ok = lib.ht_fp2_sqrt(out, fp2b(a))
+        ref = o.f2_sqrt(a)
+        assert bool(ok) == (ref is not None)
+        if ok:
+            assert o.f2_sqr(b2fp2(out.raw)) == (a[0] % o.P, a[1] % o.P)
+
+
+def test_expand_message(lib):
+    for msg in (bytes(32), bytes(range(32)), b"\xff" * 32):
+        out = buf(256)
+        lib.ht_expand(out, msg)
+        assert out.raw == o.expand_message_xmd(msg, o.DST_POP, 256)
+
+
+def test_hash_to_g2(lib):
+    rng = random.Random(3)
+    for _ in range(4):
+        msg = bytes(rng.randrange(256) for _ in range(32))
+        out = buf(192)
+        lib.ht_hash_to_g2(out, msg)
+        ref = o.hash_to_g2(msg)
+        assert (b2fp2(out.raw[:96]), b2fp2(out.raw[96:])) == ref
+
+
+def test_g2_decode_and_subgroup(lib):
+    sk = 7
+    sig = o.sign(sk, bytes(32))
+    for enc in (o.g2_compress(sig), o.g2_serialize(sig)):
+        out = buf(192)
+        st = lib.ht_g2_decode(out, enc, len(enc))
+        assert st == 0
+        assert (b2fp2(out.raw[:96]), b2fp2(out.raw[96:])) == sig
+        assert lib.ht_g2_in_subgroup(out.raw) == 1
+    # malformed / infinity / non-subgroup
+    out = buf(192)
+    assert lib.ht_g2_decode(out, bytes([10]) * 96, 96) != 0
+    assert lib.ht_g2_decode(out, bytes([0xC0]) + bytes(95), 96) == 4
+    q = o.iso_map_g2(o.map_to_curve_sswu_g2((5, 7)))
+    assert lib.ht_g2_decode(out, o.g2_compress(q), 96) == 0
+    assert lib.ht_g2_in_subgroup(out.raw) == 0
+
+
+def test_g1(lib):
+    pk = o.sk_to_pk(12345)
+    out = buf(96)
+    assert lib.ht_g1_decompress(out, o.g1_compress(pk)) == 0
+    assert (int.from_bytes(out.raw[:48], "big"), int.from_bytes(out.raw[48:], "big")) == pk
+    assert lib.ht_g1_in_subgroup(out.raw) == 1
+    x = 1
+    while o.fp_sqrt(x ** 3 + 4) is None:
+        x += 1
+    bad = (x, o.fp_sqrt(x ** 3 + 4))
+    assert lib.ht_g1_in_subgroup(be(bad[0]) + be(bad[1])) == 0
+    r = buf(96)
+    lib.ht_g1_mul_u64.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint64]
+    k = 0xFEDCBA9876543210
+    assert lib.ht_g1_mul_u64(r, be(pk[0]) + be(pk[1]), k) == 1
+    ref = o.g1_mul(pk, k)
+    assert (int.from_bytes(r.raw[:48], "big"), int.from_bytes(r.raw[48:], "big")) == ref
+
+
+def test_g2_mul_u64(lib):
+    q = o.g2_mul(o.G2_GEN, 99)
+    lib.ht_g2_mul_u64.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint64]
+    r = buf(192)
+    k = 0x8000000000000001
+    assert lib.ht_g2_mul_u64(r, fp2b(q[0]) + fp2b(q[1]), k) == 1
+    assert (b2fp2(r.raw[:96]), b2fp2(r.raw[96:])) == o.g2_mul(q, k)
+
+
+def test_pairing_value(lib):
+    Pg = o.g1_mul(o.G1_GEN, 3)
+    Qg = o.g2_mul(o.G2_GEN, 5)
+    out = buf(576)
+    lib.ht_pairing(out, be(Pg[0]) + be(Pg[1]), fp2b(Qg[0]) + fp2b(Qg[1]))
+    e = o.f12_pow(o.pairing(Pg, Qg), 3)  # device FE computes f^(3 (p^12-1)/r)
+    flat = [e[0][0], e[0][1], e[0][2], e[1][0], e[1][1], e[1][2]]
+    got = [b2fp2(out.raw[96 * i:96 * i + 96]) for i in range(6)]
+    assert got == flat
+
+
+def test_verify(lib):
+    sk = o.interop_secret_key(3)
+    pk = o.g1_compress(o.sk_to_pk(sk))
+    msg = bytes(range(32))
+    sig = o.g2_compress(o.sign(sk, msg))
+    assert lib.ht_verify(pk, msg, sig, 96) == 1
+    assert lib.ht_verify(pk, bytes(32), sig, 96) == 0
+    assert lib.ht_verify(pk, msg, bytes([10]) * 96, 96) == 0
