@@ -1,0 +1,129 @@
+/*
+ * gbv.h -- C ABI of the MI355X BLS12-381 signature-set verifier ("GPU BLS verifier").
+ *
+ * This is the drop-in boundary for Lodestar's IBlsVerifier hot path
+ * (/root/reference/packages/beacon-node/src/chain/bls/interface.ts:25-68).  A Node-API addon
+ *  or the Python host mirror (lodestar_amd/verifier.py) binds these symbols; no
+ * torch or HIP types appear in the signatures.  All entry points are called from one host thread
+ * per context; each context owns one GPU, one HIP stream and the HBM-resident pubkey table.
+ *
+ * Error convention: return 0 on success; per-set "false" results are carried
+ * in the output byte arrays, never as errors.  Negative codes map to promise rejections:
+ *   GBV_E_EMPTY_AGGREGATE  -- an aggregate set has no pubkeys (blst EMPTY_AGGREGATE_ARRAY,
+ *                             bls/utils.ts:12 throws -> job.reject, multithread/index.ts:398-412)
+ *   GBV_E_DEVICE           -- HIP error (rejects in-flight work like a worker comms failure,
+ *                             multithread/index.ts:498-507)
+ *   GBV_E_CLOSED           -- context destroyed / closed (QueueError QUEUE_ABORTED, index.ts:303-305)
+ *   GBV_E_ARG              -- invalid argument (null pointer, index out of table range)
+ */
+#ifndef GBV_H
+#define GBV_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GBV_OK 0
+#define GBV_E_ARG (-1)
+#define GBV_E_DEVICE (-2)
+#define GBV_E_EMPTY_AGGREGATE (-3)
+#define GBV_E_CLOSED (-4)
+#define GBV_E_OOM (-5)
+
+/* Point status codes written by gbv_pubkeys_append (blst BLST_ERROR equivalents). */
+#define GBV_PT_OK 0
+#define GBV_PT_BAD_ENCODING 1
+#define GBV_PT_NOT_ON_CURVE 2
+#define GBV_PT_NOT_IN_GROUP 3
+#define GBV_PT_INFINITY 4
+
+typedef struct gbv_ctx gbv_ctx;
+
+/* One signature set of IBlsVerifier.verifySignatureSets (ISignatureSet,
+ * state-transition/src/util/signatureSets.ts:4-23), in index form: the pubkeys are validator
+ * indices into the HBM-resident index2pubkey table (epochCache.ts:126-133) -- idx_len == 1 for a
+ * SingleSignatureSet, k for an AggregatedSignatureSet -- unless raw_pk48 is non-null (sets whose
+ * pubkey comes from the message itself, e.g. blsToExecutionChange.ts:19-44; validated like
+ * PublicKey.fromBytes(pk, true)). */
+typedef struct gbv_set {
+  uint32_t idx_off;          /* offset into index_arena */
+  uint32_t idx_len;          /* number of pubkeys (0 => GBV_E_EMPTY_AGGREGATE) */
+  const uint8_t* raw_pk48;   /* optional compressed pubkey, overrides the indices */
+  const uint8_t* msg32;      /* signing root */
+  const uint8_t* sig;        /* signature bytes as received (untrusted) */
+  uint32_t sig_len;          /* 96 (compressed) or 192 (uncompressed); other lengths are invalid */
+} gbv_set;
+
+/* Create a context on HIP device `device` (one process per GPU; device is usually 0 or LOCAL_RANK). */
+int gbv_init(int device, gbv_ctx** out);
+/* Release the device table, stream and buffers.  Replaces close() of the worker pool
+ * (multithread/index.ts:238-259). */
+void gbv_destroy(gbv_ctx* ctx);
+/* Human-readable description of the last error on this context. */
+const char* gbv_last_error(gbv_ctx* ctx);
+
+/* index2pubkey ingest (pubkeyCache.ts:50-69 syncPubkeys, epochCache.ts:1064-1083 addFinalizedPubkey):
+ * decompress n 48-byte pubkeys on the device into table slots [first_index, first_index + n).
+ * validate != 0 additionally runs the G1 subgroup + infinity check (PublicKey.fromBytes(pk, true)).
+ * status (optional, n bytes) receives GBV_PT_* per key; invalid keys make their slot unusable. */
+int gbv_pubkeys_append(gbv_ctx* ctx, uint32_t first_index, const uint8_t* pk48, size_t n, int validate,
+                       uint8_t* status);
+/* Number of table slots currently allocated (max index + 1). */
+size_t gbv_pubkeys_count(gbv_ctx* ctx);
+
+/* IBlsVerifier.verifySignatureSets (interface.ts:47; multithread/index.ts:157-207).
+ * The sets are split with chunkifyMaximizeChunkSize(sets, 128) (multithread/utils.ts:4-18) and
+ * each chunk is verified as one randomised batch (maybeBatch.ts:15-45).  *all_valid = AND over
+ * chunks (0 for an empty list).  chunk_valid (optional) receives one byte per chunk.
+ * Returns GBV_E_EMPTY_AGGREGATE if any set has idx_len == 0 and raw_pk48 == NULL. */
+int gbv_verify_sets(gbv_ctx* ctx, const gbv_set* sets, size_t n, const uint32_t* index_arena,
+                    uint8_t* all_valid, uint8_t* chunk_valid);
+
+/* IBlsVerifier.verifySignatureSetsSameMessage (interface.ts:55-59; multithread/index.ts:212-236):
+ * n sets {validator index, 96-byte signature} over one 32-byte message.  valid[i] receives the
+ * per-set boolean in input order (all-true on a passing randomised aggregate check, otherwise
+ * per-set verification, jobItem.ts:93-125). */
+int gbv_verify_same_message(gbv_ctx* ctx, const uint32_t* idx, const uint8_t* sigs96, size_t n,
+                            const uint8_t* msg32, uint8_t* valid);
+
+/* Many independent verifySignatureSetsSameMessage calls in one device pass (the GPU analogue of
+ * the pool's job grouping, multithread/index.ts:519-534): call g covers sets
+ * [call_off[g], call_off[g+1]) with message msgs32[32*g].  Each call is chunked exactly like
+ * gbv_verify_same_message.  valid has call_off[n_calls] bytes. */
+int gbv_verify_same_message_multi(gbv_ctx* ctx, size_t n_calls, const uint32_t* call_off, const uint32_t* idx,
+                                  const uint8_t* sigs96, const uint8_t* msgs32, uint8_t* valid);
+
+/* aggregatePublicKeys(index2pubkey[idx[0..k)]).toBytes() (bls/utils.ts:5-20), byte-identical.
+ * k == 0 returns GBV_E_EMPTY_AGGREGATE. */
+int gbv_aggregate_pubkeys(gbv_ctx* ctx, const uint32_t* idx, size_t k, uint8_t out48[48]);
+
+/* ---- device-resident batches (inputs staged in HBM once, verified many times) ------------- */
+typedef struct gbv_sm_batch gbv_sm_batch;
+/* Stage a same-message workload (as gbv_verify_same_message_multi) in HBM. */
+int gbv_sm_batch_create(gbv_ctx* ctx, size_t n_calls, const uint32_t* call_off, const uint32_t* idx,
+                        const uint8_t* sigs96, const uint8_t* msgs32, gbv_sm_batch** out);
+/* Verify a staged batch; valid (host, optional) receives the per-set booleans. */
+int gbv_sm_batch_verify(gbv_ctx* ctx, gbv_sm_batch* b, uint8_t* valid);
+void gbv_sm_batch_destroy(gbv_ctx* ctx, gbv_sm_batch* b);
+/* Device time (ms) of each kernel of the last gbv_sm_batch_verify, measured with HIP events on
+ * the context stream: [hash, prepare, group_sum, pairing, fallback]; returns the count written. */
+int gbv_last_kernel_ms(gbv_ctx* ctx, float* out, int max);
+
+/* ---- utilities for tests and synthetic workloads (not on the verification path) ----------- */
+/* sk32 (big-endian scalars) -> compressed pubkeys, on the device. */
+int gbv_util_sk_to_pk(gbv_ctx* ctx, const uint8_t* sk32, size_t n, uint8_t* pk48);
+/* sig[i] = sk[i] * H(msgs32[grp[i]]) compressed, on the device. */
+int gbv_util_sign(gbv_ctx* ctx, const uint8_t* sk32, size_t n, const uint32_t* grp, const uint8_t* msgs32,
+                  size_t n_msgs, uint8_t* sig96);
+/* hash_to_G2 of n 32-byte messages, uncompressed 192-byte affine output. */
+int gbv_util_hash_to_g2(gbv_ctx* ctx, const uint8_t* msgs32, size_t n, uint8_t* out192);
+/* Duplicate table slots: slot[dst_first + i] = slot[src_first + (i % src_n)], i < n (synthetic tables). */
+int gbv_pubkeys_replicate(gbv_ctx* ctx, uint32_t src_first, uint32_t src_n, uint32_t dst_first, size_t n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GBV_H */

@@ -1,0 +1,103 @@
+"""ctypes binding of the C ABI in include/gbv.h (lodestar_amd/libgbv.so, built for gfx950).
+
+There is deliberately no fallback: if the HIP library is missing or no GPU is visible, loading
+raises.  The CPU oracle under oracle/ is test infrastructure and is never imported here.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libgbv.so")
+
+GBV_OK = 0
+GBV_E_ARG = -1
+GBV_E_DEVICE = -2
+GBV_E_EMPTY_AGGREGATE = -3
+GBV_E_CLOSED = -4
+GBV_E_OOM = -5
+
+EXPORTED_SYMBOLS = (
+    "gbv_init", "gbv_destroy", "gbv_last_error", "gbv_pubkeys_append", "gbv_pubkeys_count",
+    "gbv_verify_sets", "gbv_verify_same_message", "gbv_verify_same_message_multi",
+    "gbv_aggregate_pubkeys", "gbv_sm_batch_create", "gbv_sm_batch_verify", "gbv_sm_batch_destroy",
+    "gbv_last_kernel_ms", "gbv_util_sk_to_pk", "gbv_util_sign", "gbv_util_hash_to_g2",
+    "gbv_pubkeys_replicate",
+)
+
+
+class GbvSet(ctypes.Structure):
+    """struct gbv_set (include/gbv.h)."""
+    _fields_ = [
+        ("idx_off", ctypes.c_uint32),
+        ("idx_len", ctypes.c_uint32),
+        ("raw_pk48", ctypes.c_void_p),
+        ("msg32", ctypes.c_void_p),
+        ("sig", ctypes.c_void_p),
+        ("sig_len", ctypes.c_uint32),
+    ]
+
+
+class GbvError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("gbv error %d: %s" % (code, msg))
+        self.code = code
+
+
+class EmptyAggregateError(GbvError):
+    """blst EMPTY_AGGREGATE_ARRAY: aggregatePublicKeys([]) throws (bls/utils.ts:12)."""
+
+
+class QueueAbortedError(GbvError):
+    """QueueError(QUEUE_ABORTED) (multithread/index.ts:303-305)."""
+
+
+_lib = None
+
+
+def load_library(path=LIB_PATH):
+    """Load libgbv.so and declare prototypes.  Raises OSError when it is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise OSError("lodestar_amd: HIP library %s not built (run __graft_entry__.build())" % path)
+    lib = ctypes.CDLL(path)
+    vp, u32, sz, cp, i32 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_int
+    P = ctypes.POINTER
+    sig = {
+        "gbv_init": (i32, [i32, P(vp)]),
+        "gbv_destroy": (None, [vp]),
+        "gbv_last_error": (cp, [vp]),
+        "gbv_pubkeys_append": (i32, [vp, u32, vp, sz, i32, vp]),
+        "gbv_pubkeys_count": (sz, [vp]),
+        "gbv_verify_sets": (i32, [vp, P(GbvSet), sz, vp, vp, vp]),
+        "gbv_verify_same_message": (i32, [vp, vp, vp, sz, vp, vp]),
+        "gbv_verify_same_message_multi": (i32, [vp, sz, vp, vp, vp, vp, vp]),
+        "gbv_aggregate_pubkeys": (i32, [vp, vp, sz, vp]),
+        "gbv_sm_batch_create": (i32, [vp, sz, vp, vp, vp, vp, P(vp)]),
+        "gbv_sm_batch_verify": (i32, [vp, vp, vp]),
+        "gbv_sm_batch_destroy": (None, [vp, vp]),
+        "gbv_last_kernel_ms": (i32, [vp, P(ctypes.c_float), i32]),
+        "gbv_util_sk_to_pk": (i32, [vp, vp, sz, vp]),
+        "gbv_util_sign": (i32, [vp, vp, sz, vp, vp, sz, vp]),
+        "gbv_util_hash_to_g2": (i32, [vp, vp, sz, vp]),
+        "gbv_pubkeys_replicate": (i32, [vp, u32, u32, u32, sz]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(lib, ctx, rc):
+    if rc == GBV_OK:
+        return
+    msg = lib.gbv_last_error(ctx)
+    msg = msg.decode() if msg else ""
+    if rc == GBV_E_EMPTY_AGGREGATE:
+        raise EmptyAggregateError(rc, msg)
+    if rc == GBV_E_CLOSED:
+        raise QueueAbortedError(rc, msg)
+    raise GbvError(rc, msg)

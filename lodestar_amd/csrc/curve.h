@@ -162,6 +162,16 @@ template <class F> GBV_HD Jac<F> jac_mul_u64(const Aff<F>& q, uint64_t k) {
   return r;
 }
 
+// [k] q for a 256-bit scalar given as 8 little-endian words (utility signing / key derivation)
+template <class F> GBV_HD Jac<F> jac_mul_u256(const Aff<F>& q, const uint32_t k[8]) {
+  Jac<F> r = jac_infinity<F>();
+  for (int i = 255; i >= 0; --i) {
+    r = jac_dbl(r);
+    if ((k[i >> 5] >> (i & 31)) & 1u) r = jac_add_aff(r, q);
+  }
+  return r;
+}
+
 // [|x|] q, |x| = 0xd201000000010000 (fixed public scalar: uniform control flow)
 template <class F> GBV_HD Jac<F> jac_mul_xabs(const Aff<F>& q) {
   Jac<F> r = jac_from_aff(q);
@@ -183,11 +193,11 @@ template <class F> GBV_HD Jac<F> jac_mul_xabs_jac(const Jac<F>& q) {
 
 // ---- curve constants & decoding -------------------------------------------------------------
 enum : uint8_t {
-  GBV_PT_OK = 0,
-  GBV_PT_BAD_ENCODING = 1,
-  GBV_PT_NOT_ON_CURVE = 2,
-  GBV_PT_NOT_IN_GROUP = 3,
-  GBV_PT_INFINITY = 4,
+  PT_OK = 0,
+  PT_BAD_ENCODING = 1,
+  PT_NOT_ON_CURVE = 2,
+  PT_NOT_IN_GROUP = 3,
+  PT_INFINITY = 4,
 };
 
 GBV_HD bool bytes_zero(const uint8_t* b, int n) {
@@ -197,26 +207,26 @@ GBV_HD bool bytes_zero(const uint8_t* b, int n) {
 }
 
 // blst POINTonE1_Uncompress_Z (PublicKey.fromBytes): 48 bytes -> affine (Montgomery).
-// Returns GBV_PT_INFINITY for the canonical infinity encoding.
+// Returns PT_INFINITY for the canonical infinity encoding.
 GBV_HD uint8_t g1_decompress(G1A& out, const uint8_t* in) {
   uint8_t in0 = in[0];
-  if ((in0 & 0x80) == 0) return GBV_PT_BAD_ENCODING;
+  if ((in0 & 0x80) == 0) return PT_BAD_ENCODING;
   if (in0 & 0x40) {
-    if ((in0 & 0x3f) == 0 && bytes_zero(in + 1, 47)) return GBV_PT_INFINITY;
-    return GBV_PT_BAD_ENCODING;
+    if ((in0 & 0x3f) == 0 && bytes_zero(in + 1, 47)) return PT_INFINITY;
+    return PT_BAD_ENCODING;
   }
   Fp xr = fp_load_be48(in, true);
-  if (!fp_raw_is_canonical(xr)) return GBV_PT_BAD_ENCODING;
+  if (!fp_raw_is_canonical(xr)) return PT_BAD_ENCODING;
   Fp x = fp_to_mont(xr);
   Fp y2 = fp_add(fp_mul(fp_sqr(x), x), FP_B1);
   Fp y = fp_sqrt_candidate(y2);
-  if (!fp_eq(fp_sqr(y), y2)) return GBV_PT_NOT_ON_CURVE;
+  if (!fp_eq(fp_sqr(y), y2)) return PT_NOT_ON_CURVE;
   bool want_large = (in0 & 0x20) != 0;
   if (fp_is_lexi_large(y) != want_large) y = fp_neg(y);
   out.x = x;
   out.y = y;
-  if (fp_is_zero(x)) return GBV_PT_NOT_IN_GROUP;
-  return GBV_PT_OK;
+  if (fp_is_zero(x)) return PT_NOT_IN_GROUP;
+  return PT_OK;
 }
 
 GBV_HD void g1_compress(uint8_t* out, const G1A& a, bool inf) {
@@ -240,43 +250,43 @@ GBV_HD bool g2_on_curve(const G2A& a) {
 GBV_HD uint8_t g2_decode(G2A& out, const uint8_t* in, uint32_t len) {
   uint8_t in0 = in[0];
   if (len == 96) {
-    if ((in0 & 0x80) == 0) return GBV_PT_BAD_ENCODING;
+    if ((in0 & 0x80) == 0) return PT_BAD_ENCODING;
     if (in0 & 0x40) {
-      if ((in0 & 0x3f) == 0 && bytes_zero(in + 1, 95)) return GBV_PT_INFINITY;
-      return GBV_PT_BAD_ENCODING;
+      if ((in0 & 0x3f) == 0 && bytes_zero(in + 1, 95)) return PT_INFINITY;
+      return PT_BAD_ENCODING;
     }
     Fp x1r = fp_load_be48(in, true);
     Fp x0r = fp_load_be48(in + 48, false);
-    if (!fp_raw_is_canonical(x1r) || !fp_raw_is_canonical(x0r)) return GBV_PT_BAD_ENCODING;
+    if (!fp_raw_is_canonical(x1r) || !fp_raw_is_canonical(x0r)) return PT_BAD_ENCODING;
     Fp2 x{fp_to_mont(x0r), fp_to_mont(x1r)};
     Fp2 y2 = fp2_add(fp2_mul(fp2_sqr(x), x), FP2_B2);
     Fp2 y;
-    if (!fp2_sqrt(y, y2)) return GBV_PT_NOT_ON_CURVE;
+    if (!fp2_sqrt(y, y2)) return PT_NOT_ON_CURVE;
     bool want_large = (in0 & 0x20) != 0;
     if (fp2_is_lexi_large(y) != want_large) y = fp2_neg(y);
     out.x = x;
     out.y = y;
-    if (fp2_is_zero(x)) return GBV_PT_NOT_IN_GROUP;
-    return GBV_PT_OK;
+    if (fp2_is_zero(x)) return PT_NOT_IN_GROUP;
+    return PT_OK;
   }
   if (len == 192) {
-    if (in0 & 0x80) return GBV_PT_BAD_ENCODING;
+    if (in0 & 0x80) return PT_BAD_ENCODING;
     if (in0 & 0xe0) {
-      if ((in0 & 0x40) && (in0 & 0x3f) == 0 && bytes_zero(in + 1, 191)) return GBV_PT_INFINITY;
-      return GBV_PT_BAD_ENCODING;
+      if ((in0 & 0x40) && (in0 & 0x3f) == 0 && bytes_zero(in + 1, 191)) return PT_INFINITY;
+      return PT_BAD_ENCODING;
     }
     Fp r[4];
     for (int i = 0; i < 4; ++i) {
       r[i] = fp_load_be48(in + 48 * i, false);
-      if (!fp_raw_is_canonical(r[i])) return GBV_PT_BAD_ENCODING;
+      if (!fp_raw_is_canonical(r[i])) return PT_BAD_ENCODING;
     }
     out.x = Fp2{fp_to_mont(r[1]), fp_to_mont(r[0])};
     out.y = Fp2{fp_to_mont(r[3]), fp_to_mont(r[2])};
-    if (!g2_on_curve(out)) return GBV_PT_NOT_ON_CURVE;
-    if (fp2_is_zero(out.x)) return GBV_PT_NOT_IN_GROUP;
-    return GBV_PT_OK;
+    if (!g2_on_curve(out)) return PT_NOT_ON_CURVE;
+    if (fp2_is_zero(out.x)) return PT_NOT_IN_GROUP;
+    return PT_OK;
   }
-  return GBV_PT_BAD_ENCODING;
+  return PT_BAD_ENCODING;
 }
 
 GBV_HD void g2_compress(uint8_t* out, const G2A& a, bool inf) {

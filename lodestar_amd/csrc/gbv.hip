@@ -1,0 +1,476 @@
+// Host side of the C ABI (include/gbv.h): device memory, the HBM pubkey table, chunking exactly
+// as the reference pool does it, kernel sequencing on one HIP stream per context.
+#include "../../include/gbv.h"
+#include "kernels.h"
+
+#include <sys/random.h>
+
+#include <algorithm>
+#include <cstring>
+#include <string>
+#include <vector>
+
+using namespace gbv;
+
+namespace {
+
+constexpr uint32_t MAX_SIGNATURE_SETS_PER_JOB = 128;  // multithread/index.ts:56
+constexpr int TPB = 64;
+
+// chunkifyMaximizeChunkSize (multithread/utils.ts:4-18): returns chunk start offsets + end.
+std::vector<uint32_t> chunk_offsets(uint32_t len, uint32_t min_per_chunk) {
+  std::vector<uint32_t> off;
+  uint32_t chunk_count = len / min_per_chunk;
+  if (chunk_count <= 1) {
+    off.push_back(0);
+    off.push_back(len);
+    return off;
+  }
+  uint32_t per_chunk = (len + chunk_count - 1) / chunk_count;
+  for (uint32_t i = 0; i < len; i += per_chunk) off.push_back(i);
+  off.push_back(len);
+  return off;
+}
+
+unsigned blocks_for(size_t n, int tpb = TPB) { return (unsigned)((n + tpb - 1) / tpb); }
+
+}  // namespace
+
+struct gbv_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  G1A* table = nullptr;
+  uint8_t* table_ok = nullptr;
+  size_t table_cap = 0;
+  size_t table_n = 0;
+  std::string err;
+  uint32_t nonce = 0;
+  hipEvent_t ev[6] = {};
+  float last_ms[5] = {};
+  bool closed = false;
+};
+
+struct gbv_sm_batch {
+  size_t n = 0, G = 0, n_calls = 0;
+  uint32_t *idx = nullptr, *grp_off = nullptr, *grp_msg = nullptr, *set_grp = nullptr, *n_fallback = nullptr;
+  uint8_t *sig = nullptr, *msgs = nullptr, *status = nullptr, *grp_state = nullptr, *valid = nullptr;
+  G2A *H = nullptr, *S = nullptr, *Sg = nullptr;
+  G2J* rS = nullptr;
+  G1J* rP = nullptr;
+  G1A* Pg = nullptr;
+};
+
+static int fail(gbv_ctx* c, int code, const std::string& msg) {
+  if (c) c->err = msg;
+  return code;
+}
+
+#define HIP_CHECK(ctx, call)                                                             \
+  do {                                                                                   \
+    hipError_t e_ = (call);                                                              \
+    if (e_ != hipSuccess)                                                                \
+      return fail(ctx, GBV_E_DEVICE, std::string(#call) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+template <class T> static hipError_t dalloc(T** p, size_t count) {
+  return hipMalloc((void**)p, std::max<size_t>(count, 1) * sizeof(T));
+}
+
+static Seed fresh_seed() {
+  Seed s;
+  size_t got = 0;
+  while (got < sizeof(s.w)) {
+    ssize_t r = getrandom((uint8_t*)s.w + got, sizeof(s.w) - got, 0);
+    if (r > 0) got += (size_t)r;
+  }
+  return s;
+}
+
+extern "C" {
+
+int gbv_init(int device, gbv_ctx** out) {
+  if (!out) return GBV_E_ARG;
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return GBV_E_DEVICE;
+  if (device < 0 || device >= ndev) return GBV_E_ARG;
+  gbv_ctx* c = new gbv_ctx();
+  c->device = device;
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return GBV_E_DEVICE;
+  }
+  for (auto& e : c->ev) hipEventCreate(&e);
+  *out = c;
+  return GBV_OK;
+}
+
+void gbv_destroy(gbv_ctx* c) {
+  if (!c) return;
+  hipSetDevice(c->device);
+  if (c->stream) hipStreamSynchronize(c->stream);
+  hipFree(c->table);
+  hipFree(c->table_ok);
+  for (auto& e : c->ev) hipEventDestroy(e);
+  if (c->stream) hipStreamDestroy(c->stream);
+  delete c;
+}
+
+const char* gbv_last_error(gbv_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+size_t gbv_pubkeys_count(gbv_ctx* c) { return c ? c->table_n : 0; }
+
+static int table_reserve(gbv_ctx* c, size_t need) {
+  if (need <= c->table_cap) return GBV_OK;
+  size_t cap = std::max(need, c->table_cap * 2);
+  G1A* t = nullptr;
+  uint8_t* ok = nullptr;
+  HIP_CHECK(c, dalloc(&t, cap));
+  HIP_CHECK(c, dalloc(&ok, cap));
+  HIP_CHECK(c, hipMemsetAsync(ok, 0, cap, c->stream));
+  if (c->table_n) {
+    HIP_CHECK(c, hipMemcpyAsync(t, c->table, c->table_n * sizeof(G1A), hipMemcpyDeviceToDevice, c->stream));
+    HIP_CHECK(c, hipMemcpyAsync(ok, c->table_ok, c->table_n, hipMemcpyDeviceToDevice, c->stream));
+  }
+  HIP_CHECK(c, hipStreamSynchronize(c->stream));
+  hipFree(c->table);
+  hipFree(c->table_ok);
+  c->table = t;
+  c->table_ok = ok;
+  c->table_cap = cap;
+  return GBV_OK;
+}
+
+int gbv_pubkeys_append(gbv_ctx* c, uint32_t first, const uint8_t* pk48, size_t n, int validate, uint8_t* status) {
+  if (!c) return GBV_E_ARG;
+  if (c->closed) return GBV_E_CLOSED;
+  if (n == 0) return GBV_OK;
+  if (!pk48) return fail(c, GBV_E_ARG, "null pk48");
+  HIP_CHECK(c, hipSetDevice(c->device));
+  int rc = table_reserve(c, (size_t)first + n);
+  if (rc) return rc;
+  uint8_t *d_pk = nullptr, *d_st = nullptr;
+  HIP_CHECK(c, dalloc(&d_pk, 48 * n));
+  HIP_CHECK(c, dalloc(&d_st, n));
+  HIP_CHECK(c, hipMemcpyAsync(d_pk, pk48, 48 * n, hipMemcpyHostToDevice, c->stream));
+  hipLaunchKernelGGL(k_pk_decompress, dim3(blocks_for(n)), dim3(TPB), 0, c->stream, (uint32_t)n, d_pk, validate,
+                     c->table + first, c->table_ok + first, d_st);
+  HIP_CHECK(c, hipGetLastError());
+  if (status) HIP_CHECK(c, hipMemcpyAsync(status, d_st, n, hipMemcpyDeviceToHost, c->stream));
+  HIP_CHECK(c, hipStreamSynchronize(c->stream));
+  hipFree(d_pk);
+  hipFree(d_st);
+  c->table_n = std::max(c->table_n, (size_t)first + n);
+  return GBV_OK;
+}
+
+int gbv_pubkeys_replicate(gbv_ctx* c, uint32_t src_first, uint32_t src_n, uint32_t dst_first, size_t n) {
+  if (!c || src_n == 0 || (size_t)src_first + src_n > c->table_n) return fail(c, GBV_E_ARG, "bad replicate range");
+  HIP_CHECK(c, hipSetDevice(c->device));
+  int rc = table_reserve(c, (size_t)dst_first + n);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_pk_replicate, dim3(blocks_for(n, 256)), dim3(256), 0, c->stream, c->table, c->table_ok, src_first, src_n,
+                     dst_first, (uint32_t)n);
+  HIP_CHECK(c, hipGetLastError());
+  HIP_CHECK(c, hipStreamSynchronize(c->stream));
+  c->table_n = std::max(c->table_n, (size_t)dst_first + n);
+  return GBV_OK;
+}
+
+int gbv_aggregate_pubkeys(gbv_ctx* c, const uint32_t* idx, size_t k, uint8_t out48[48]) {
+  if (!c) return GBV_E_ARG;
+  if (c->closed) return GBV_E_CLOSED;
+  if (k == 0) return fail(c, GBV_E_EMPTY_AGGREGATE, "EMPTY_AGGREGATE_ARRAY");
+  if (!idx || !out48) return fail(c, GBV_E_ARG, "null argument");
+  for (size_t i = 0; i < k; ++i)
+    if (idx[i] >= c->table_n) return fail(c, GBV_E_ARG, "validator index out of range");
+  HIP_CHECK(c, hipSetDevice(c->device));
+  uint32_t *d_idx = nullptr, *d_bad = nullptr;
+  uint8_t* d_out = nullptr;
+  HIP_CHECK(c, dalloc(&d_idx, k));
+  HIP_CHECK(c, dalloc(&d_bad, 1));
+  HIP_CHECK(c, dalloc(&d_out, 48));
+  HIP_CHECK(c, hipMemcpyAsync(d_idx, idx, 4 * k, hipMemcpyHostToDevice, c->stream));
+  HIP_CHECK(c, hipMemsetAsync(d_bad, 0, 4, c->stream));
+  hipLaunchKernelGGL(k_aggregate, dim3(1), dim3(256), 0, c->stream, d_idx, (uint32_t)k, c->table, c->table_ok, d_out, d_bad);
+  HIP_CHECK(c, hipGetLastError());
+  uint32_t bad = 0;
+  HIP_CHECK(c, hipMemcpyAsync(out48, d_out, 48, hipMemcpyDeviceToHost, c->stream));
+  HIP_CHECK(c, hipMemcpyAsync(&bad, d_bad, 4, hipMemcpyDeviceToHost, c->stream));
+  HIP_CHECK(c, hipStreamSynchronize(c->stream));
+  hipFree(d_idx);
+  hipFree(d_bad);
+  hipFree(d_out);
+  if (bad) return fail(c, GBV_E_ARG, "aggregate over an invalid table entry");
+  return GBV_OK;
+}
+
+// ---- same-message batches ------------------------------------------------------------------
+void gbv_sm_batch_destroy(gbv_ctx* c, gbv_sm_batch* b) {
+  (void)c;
+  if (!b) return;
+  hipFree(b->idx); hipFree(b->grp_off); hipFree(b->grp_msg); hipFree(b->set_grp); hipFree(b->n_fallback);
+  hipFree(b->sig); hipFree(b->msgs); hipFree(b->status); hipFree(b->grp_state); hipFree(b->valid);
+  hipFree(b->H); hipFree(b->S); hipFree(b->Sg); hipFree(b->rS); hipFree(b->rP); hipFree(b->Pg);
+  delete b;
+}
+
+int gbv_sm_batch_create(gbv_ctx* c, size_t n_calls, const uint32_t* call_off, const uint32_t* idx, const uint8_t* sigs96,
+                        const uint8_t* msgs32, gbv_sm_batch** out) {
+  if (!c || !out) return GBV_E_ARG;
+  if (c->closed) return GBV_E_CLOSED;
+  *out = nullptr;
+  if (n_calls && (!call_off || !msgs32)) return fail(c, GBV_E_ARG, "null argument");
+  size_t n = n_calls ? call_off[n_calls] : 0;
+  if (n && (!idx || !sigs96)) return fail(c, GBV_E_ARG, "null argument");
+  for (size_t g = 0; g < n_calls; ++g)
+    if (call_off[g + 1] < call_off[g]) return fail(c, GBV_E_ARG, "call offsets not monotone");
+  for (size_t i = 0; i < n; ++i)
+    if (idx[i] >= c->table_n) return fail(c, GBV_E_ARG, "validator index out of range");
+  // chunk every call exactly like verifySignatureSetsSameMessage (index.ts:218-219)
+  std::vector<uint32_t> grp_off, grp_msg, set_grp(n);
+  for (size_t g = 0; g < n_calls; ++g) {
+    uint32_t len = call_off[g + 1] - call_off[g];
+    if (len == 0) continue;
+    std::vector<uint32_t> co = chunk_offsets(len, MAX_SIGNATURE_SETS_PER_JOB);
+    for (size_t j = 0; j + 1 < co.size(); ++j) {
+      uint32_t gid = (uint32_t)grp_msg.size();
+      grp_off.push_back(call_off[g] + co[j]);
+      grp_msg.push_back((uint32_t)g);
+      for (uint32_t i = call_off[g] + co[j]; i < call_off[g] + co[j + 1]; ++i) set_grp[i] = gid;
+    }
+  }
+  grp_off.push_back((uint32_t)n);
+  size_t G = grp_msg.size();
+  HIP_CHECK(c, hipSetDevice(c->device));
+  gbv_sm_batch* b = new gbv_sm_batch();
+  b->n = n;
+  b->G = G;
+  b->n_calls = n_calls;
+  hipError_t e = hipSuccess;
+  auto chk = [&](hipError_t x) { if (x != hipSuccess && e == hipSuccess) e = x; };
+  chk(dalloc(&b->idx, n)); chk(dalloc(&b->sig, 96 * n)); chk(dalloc(&b->grp_off, G + 1)); chk(dalloc(&b->grp_msg, G));
+  chk(dalloc(&b->set_grp, n)); chk(dalloc(&b->msgs, 32 * n_calls)); chk(dalloc(&b->n_fallback, 1));
+  chk(dalloc(&b->status, n)); chk(dalloc(&b->grp_state, G)); chk(dalloc(&b->valid, n));
+  chk(dalloc(&b->H, n_calls)); chk(dalloc(&b->S, n)); chk(dalloc(&b->rS, n)); chk(dalloc(&b->rP, n));
+  chk(dalloc(&b->Pg, G)); chk(dalloc(&b->Sg, G));
+  if (e != hipSuccess) {
+    gbv_sm_batch_destroy(c, b);
+    return fail(c, GBV_E_OOM, std::string("hipMalloc: ") + hipGetErrorString(e));
+  }
+  if (n) {
+    chk(hipMemcpyAsync(b->idx, idx, 4 * n, hipMemcpyHostToDevice, c->stream));
+    chk(hipMemcpyAsync(b->sig, sigs96, 96 * n, hipMemcpyHostToDevice, c->stream));
+    chk(hipMemcpyAsync(b->set_grp, set_grp.data(), 4 * n, hipMemcpyHostToDevice, c->stream));
+  }
+  chk(hipMemcpyAsync(b->grp_off, grp_off.data(), 4 * (G + 1), hipMemcpyHostToDevice, c->stream));
+  if (G) chk(hipMemcpyAsync(b->grp_msg, grp_msg.data(), 4 * G, hipMemcpyHostToDevice, c->stream));
+  if (n_calls) chk(hipMemcpyAsync(b->msgs, msgs32, 32 * n_calls, hipMemcpyHostToDevice, c->stream));
+  chk(hipStreamSynchronize(c->stream));
+  if (e != hipSuccess) {
+    gbv_sm_batch_destroy(c, b);
+    return fail(c, GBV_E_DEVICE, std::string("upload: ") + hipGetErrorString(e));
+  }
+  *out = b;
+  return GBV_OK;
+}
+
+int gbv_sm_batch_verify(gbv_ctx* c, gbv_sm_batch* b, uint8_t* valid) {
+  if (!c || !b) return GBV_E_ARG;
+  if (c->closed) return GBV_E_CLOSED;
+  if (b->n == 0) return GBV_OK;
+  HIP_CHECK(c, hipSetDevice(c->device));
+  Seed seed = fresh_seed();
+  uint32_t nonce = c->nonce++;
+  hipStream_t s = c->stream;
+  HIP_CHECK(c, hipMemsetAsync(b->n_fallback, 0, 4, s));
+  hipEventRecord(c->ev[0], s);
+  hipLaunchKernelGGL(k_hash_msgs, dim3(blocks_for(b->n_calls)), dim3(TPB), 0, s, b->msgs, (uint32_t)b->n_calls, b->H);
+  hipEventRecord(c->ev[1], s);
+  hipLaunchKernelGGL(k_sm_prepare, dim3(blocks_for(b->n)), dim3(TPB), 0, s, (uint32_t)b->n, b->idx, b->sig, c->table, c->table_ok,
+                     (uint32_t)c->table_n, seed, nonce, b->S, b->rS, b->rP, b->status);
+  hipEventRecord(c->ev[2], s);
+  hipLaunchKernelGGL(k_sm_group_sum, dim3(blocks_for(b->G)), dim3(TPB), 0, s, (uint32_t)b->G, b->grp_off, b->status, b->rS, b->rP,
+                     b->Pg, b->Sg, b->grp_state);
+  hipEventRecord(c->ev[3], s);
+  hipLaunchKernelGGL(k_sm_group_pairing, dim3(blocks_for(b->G)), dim3(TPB), 0, s, (uint32_t)b->G, b->grp_msg, b->Pg, b->Sg, b->H,
+                     b->grp_state, b->n_fallback);
+  hipEventRecord(c->ev[4], s);
+  HIP_CHECK(c, hipGetLastError());
+  uint32_t nfb = 0;
+  HIP_CHECK(c, hipMemcpyAsync(&nfb, b->n_fallback, 4, hipMemcpyDeviceToHost, s));
+  HIP_CHECK(c, hipStreamSynchronize(s));
+  hipLaunchKernelGGL(k_sm_fallback, dim3(blocks_for(b->n)), dim3(TPB), 0, s, (uint32_t)b->n, b->set_grp, b->grp_msg, b->grp_state,
+                     b->status, b->idx, c->table, b->S, b->H, b->valid, nfb ? 1 : 0);
+  hipEventRecord(c->ev[5], s);
+  HIP_CHECK(c, hipGetLastError());
+  if (valid) HIP_CHECK(c, hipMemcpyAsync(valid, b->valid, b->n, hipMemcpyDeviceToHost, s));
+  HIP_CHECK(c, hipStreamSynchronize(s));
+  for (int k = 0; k < 5; ++k) hipEventElapsedTime(&c->last_ms[k], c->ev[k], c->ev[k + 1]);
+  return GBV_OK;
+}
+
+int gbv_last_kernel_ms(gbv_ctx* c, float* out, int max) {
+  if (!c || !out) return 0;
+  int k = std::min(max, 5);
+  for (int i = 0; i < k; ++i) out[i] = c->last_ms[i];
+  return k;
+}
+
+int gbv_verify_same_message_multi(gbv_ctx* c, size_t n_calls, const uint32_t* call_off, const uint32_t* idx, const uint8_t* sigs96,
+                                  const uint8_t* msgs32, uint8_t* valid) {
+  gbv_sm_batch* b = nullptr;
+  int rc = gbv_sm_batch_create(c, n_calls, call_off, idx, sigs96, msgs32, &b);
+  if (rc) return rc;
+  rc = gbv_sm_batch_verify(c, b, valid);
+  gbv_sm_batch_destroy(c, b);
+  return rc;
+}
+
+int gbv_verify_same_message(gbv_ctx* c, const uint32_t* idx, const uint8_t* sigs96, size_t n, const uint8_t* msg32, uint8_t* valid) {
+  uint32_t off[2] = {0, (uint32_t)n};
+  return gbv_verify_same_message_multi(c, 1, off, idx, sigs96, msg32, valid);
+}
+
+// ---- distinct-message sets -----------------------------------------------------------------
+int gbv_verify_sets(gbv_ctx* c, const gbv_set* sets, size_t n, const uint32_t* arena, uint8_t* all_valid, uint8_t* chunk_valid) {
+  if (!c || !all_valid) return GBV_E_ARG;
+  if (c->closed) return GBV_E_CLOSED;
+  *all_valid = 0;
+  if (n && !sets) return fail(c, GBV_E_ARG, "null sets");
+  // aggregation throws before any verification: the whole call rejects (index.ts:398-412)
+  for (size_t i = 0; i < n; ++i)
+    if (!sets[i].raw_pk48 && sets[i].idx_len == 0) return fail(c, GBV_E_EMPTY_AGGREGATE, "EMPTY_AGGREGATE_ARRAY");
+  for (size_t i = 0; i < n; ++i) {
+    if (!sets[i].msg32 || (!sets[i].sig && sets[i].sig_len)) return fail(c, GBV_E_ARG, "null msg/sig");
+    if (!sets[i].raw_pk48) {
+      if (!arena) return fail(c, GBV_E_ARG, "null index arena");
+      for (uint32_t j = 0; j < sets[i].idx_len; ++j)
+        if (arena[sets[i].idx_off + j] >= c->table_n) return fail(c, GBV_E_ARG, "validator index out of range");
+    }
+  }
+  if (n == 0) {  // verifySignatureSetsMaybeBatch([]) throws -> false (maybeBatch.ts:29-31,39-44)
+    if (chunk_valid) chunk_valid[0] = 0;
+    return GBV_OK;
+  }
+  std::vector<uint32_t> co = chunk_offsets((uint32_t)n, MAX_SIGNATURE_SETS_PER_JOB);
+  size_t C = co.size() - 1;
+  uint32_t stride = 96;
+  for (size_t i = 0; i < n; ++i)
+    if (sets[i].sig_len == 192) stride = 192;
+  std::vector<uint32_t> set_idx_off(n + 1), idx_flat, sig_len(n);
+  std::vector<uint8_t> raw_flag(n), raw_pk(48 * n), msgs(32 * n), sig((size_t)stride * n, 0);
+  for (size_t i = 0; i < n; ++i) {
+    set_idx_off[i] = (uint32_t)idx_flat.size();
+    if (sets[i].raw_pk48) {
+      raw_flag[i] = 1;
+      memcpy(&raw_pk[48 * i], sets[i].raw_pk48, 48);
+    } else {
+      for (uint32_t j = 0; j < sets[i].idx_len; ++j) idx_flat.push_back(arena[sets[i].idx_off + j]);
+    }
+    memcpy(&msgs[32 * i], sets[i].msg32, 32);
+    uint32_t L = sets[i].sig_len;
+    sig_len[i] = (L == 96 || L == 192) ? L : 0;  // other lengths: BAD_ENCODING -> false
+    if (sig_len[i]) memcpy(&sig[(size_t)stride * i], sets[i].sig, L);
+  }
+  set_idx_off[n] = (uint32_t)idx_flat.size();
+  HIP_CHECK(c, hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  uint32_t *d_off, *d_idx, *d_siglen, *d_chunk_off;
+  uint8_t *d_raw_flag, *d_raw_pk, *d_msgs, *d_sig, *d_status, *d_cv;
+  Fp12* d_f;
+  G2J* d_rS;
+  HIP_CHECK(c, dalloc(&d_off, n + 1)); HIP_CHECK(c, dalloc(&d_idx, idx_flat.size())); HIP_CHECK(c, dalloc(&d_siglen, n));
+  HIP_CHECK(c, dalloc(&d_chunk_off, C + 1)); HIP_CHECK(c, dalloc(&d_raw_flag, n)); HIP_CHECK(c, dalloc(&d_raw_pk, 48 * n));
+  HIP_CHECK(c, dalloc(&d_msgs, 32 * n)); HIP_CHECK(c, dalloc(&d_sig, (size_t)stride * n)); HIP_CHECK(c, dalloc(&d_status, n));
+  HIP_CHECK(c, dalloc(&d_cv, C)); HIP_CHECK(c, dalloc(&d_f, n)); HIP_CHECK(c, dalloc(&d_rS, n));
+  HIP_CHECK(c, hipMemcpyAsync(d_off, set_idx_off.data(), 4 * (n + 1), hipMemcpyHostToDevice, s));
+  if (!idx_flat.empty()) HIP_CHECK(c, hipMemcpyAsync(d_idx, idx_flat.data(), 4 * idx_flat.size(), hipMemcpyHostToDevice, s));
+  HIP_CHECK(c, hipMemcpyAsync(d_siglen, sig_len.data(), 4 * n, hipMemcpyHostToDevice, s));
+  HIP_CHECK(c, hipMemcpyAsync(d_chunk_off, co.data(), 4 * (C + 1), hipMemcpyHostToDevice, s));
+  HIP_CHECK(c, hipMemcpyAsync(d_raw_flag, raw_flag.data(), n, hipMemcpyHostToDevice, s));
+  HIP_CHECK(c, hipMemcpyAsync(d_raw_pk, raw_pk.data(), 48 * n, hipMemcpyHostToDevice, s));
+  HIP_CHECK(c, hipMemcpyAsync(d_msgs, msgs.data(), 32 * n, hipMemcpyHostToDevice, s));
+  HIP_CHECK(c, hipMemcpyAsync(d_sig, sig.data(), (size_t)stride * n, hipMemcpyHostToDevice, s));
+  Seed seed = fresh_seed();
+  uint32_t nonce = c->nonce++;
+  hipLaunchKernelGGL(k_vs_prepare, dim3(blocks_for(n)), dim3(TPB), 0, s, (uint32_t)n, d_off, d_idx, d_raw_flag, d_raw_pk, d_msgs, d_sig,
+                     stride, d_siglen, c->table, c->table_ok, seed, nonce, d_f, d_rS, d_status);
+  hipLaunchKernelGGL(k_vs_chunk, dim3(blocks_for(C)), dim3(TPB), 0, s, (uint32_t)C, d_chunk_off, d_status, d_f, d_rS, d_cv);
+  HIP_CHECK(c, hipGetLastError());
+  std::vector<uint8_t> cv(C);
+  HIP_CHECK(c, hipMemcpyAsync(cv.data(), d_cv, C, hipMemcpyDeviceToHost, s));
+  HIP_CHECK(c, hipStreamSynchronize(s));
+  hipFree(d_off); hipFree(d_idx); hipFree(d_siglen); hipFree(d_chunk_off); hipFree(d_raw_flag); hipFree(d_raw_pk);
+  hipFree(d_msgs); hipFree(d_sig); hipFree(d_status); hipFree(d_cv); hipFree(d_f); hipFree(d_rS);
+  uint8_t all = 1;
+  for (size_t k = 0; k < C; ++k) all &= cv[k];
+  *all_valid = all;
+  if (chunk_valid) memcpy(chunk_valid, cv.data(), C);
+  return GBV_OK;
+}
+
+// ---- utilities -----------------------------------------------------------------------------
+int gbv_util_sk_to_pk(gbv_ctx* c, const uint8_t* sk32, size_t n, uint8_t* pk48) {
+  if (!c || (n && (!sk32 || !pk48))) return GBV_E_ARG;
+  if (n == 0) return GBV_OK;
+  HIP_CHECK(c, hipSetDevice(c->device));
+  uint8_t *d_sk, *d_pk;
+  HIP_CHECK(c, dalloc(&d_sk, 32 * n));
+  HIP_CHECK(c, dalloc(&d_pk, 48 * n));
+  HIP_CHECK(c, hipMemcpyAsync(d_sk, sk32, 32 * n, hipMemcpyHostToDevice, c->stream));
+  hipLaunchKernelGGL(k_util_sk_to_pk, dim3(blocks_for(n)), dim3(TPB), 0, c->stream, (uint32_t)n, d_sk, d_pk);
+  HIP_CHECK(c, hipGetLastError());
+  HIP_CHECK(c, hipMemcpyAsync(pk48, d_pk, 48 * n, hipMemcpyDeviceToHost, c->stream));
+  HIP_CHECK(c, hipStreamSynchronize(c->stream));
+  hipFree(d_sk);
+  hipFree(d_pk);
+  return GBV_OK;
+}
+
+int gbv_util_hash_to_g2(gbv_ctx* c, const uint8_t* msgs32, size_t n, uint8_t* out192) {
+  if (!c || (n && (!msgs32 || !out192))) return GBV_E_ARG;
+  if (n == 0) return GBV_OK;
+  HIP_CHECK(c, hipSetDevice(c->device));
+  uint8_t *d_m, *d_o;
+  G2A* d_H;
+  HIP_CHECK(c, dalloc(&d_m, 32 * n));
+  HIP_CHECK(c, dalloc(&d_o, 192 * n));
+  HIP_CHECK(c, dalloc(&d_H, n));
+  HIP_CHECK(c, hipMemcpyAsync(d_m, msgs32, 32 * n, hipMemcpyHostToDevice, c->stream));
+  hipLaunchKernelGGL(k_hash_msgs, dim3(blocks_for(n)), dim3(TPB), 0, c->stream, d_m, (uint32_t)n, d_H);
+  hipLaunchKernelGGL(k_util_g2_out, dim3(blocks_for(n)), dim3(TPB), 0, c->stream, (uint32_t)n, d_H, d_o);
+  HIP_CHECK(c, hipGetLastError());
+  HIP_CHECK(c, hipMemcpyAsync(out192, d_o, 192 * n, hipMemcpyDeviceToHost, c->stream));
+  HIP_CHECK(c, hipStreamSynchronize(c->stream));
+  hipFree(d_m); hipFree(d_o); hipFree(d_H);
+  return GBV_OK;
+}
+
+int gbv_util_sign(gbv_ctx* c, const uint8_t* sk32, size_t n, const uint32_t* grp, const uint8_t* msgs32, size_t n_msgs, uint8_t* sig96) {
+  if (!c || (n && (!sk32 || !grp || !msgs32 || !sig96))) return GBV_E_ARG;
+  if (n == 0) return GBV_OK;
+  for (size_t i = 0; i < n; ++i)
+    if (grp[i] >= n_msgs) return fail(c, GBV_E_ARG, "message index out of range");
+  HIP_CHECK(c, hipSetDevice(c->device));
+  uint8_t *d_sk, *d_m, *d_sig;
+  uint32_t* d_grp;
+  G2A* d_H;
+  HIP_CHECK(c, dalloc(&d_sk, 32 * n));
+  HIP_CHECK(c, dalloc(&d_m, 32 * n_msgs));
+  HIP_CHECK(c, dalloc(&d_sig, 96 * n));
+  HIP_CHECK(c, dalloc(&d_grp, n));
+  HIP_CHECK(c, dalloc(&d_H, n_msgs));
+  HIP_CHECK(c, hipMemcpyAsync(d_sk, sk32, 32 * n, hipMemcpyHostToDevice, c->stream));
+  HIP_CHECK(c, hipMemcpyAsync(d_m, msgs32, 32 * n_msgs, hipMemcpyHostToDevice, c->stream));
+  HIP_CHECK(c, hipMemcpyAsync(d_grp, grp, 4 * n, hipMemcpyHostToDevice, c->stream));
+  hipLaunchKernelGGL(k_hash_msgs, dim3(blocks_for(n_msgs)), dim3(TPB), 0, c->stream, d_m, (uint32_t)n_msgs, d_H);
+  hipLaunchKernelGGL(k_util_sign, dim3(blocks_for(n)), dim3(TPB), 0, c->stream, (uint32_t)n, d_sk, d_grp, d_H, d_sig);
+  HIP_CHECK(c, hipGetLastError());
+  HIP_CHECK(c, hipMemcpyAsync(sig96, d_sig, 96 * n, hipMemcpyDeviceToHost, c->stream));
+  HIP_CHECK(c, hipStreamSynchronize(c->stream));
+  hipFree(d_sk); hipFree(d_m); hipFree(d_sig); hipFree(d_grp); hipFree(d_H);
+  return GBV_OK;
+}
+
+}  // extern "C"

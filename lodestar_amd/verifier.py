@@ -1,0 +1,349 @@
+"""GpuBlsVerifier -- host-side mirror of Lodestar's IBlsVerifier over the gfx950 C ABI.
+
+Reference interface: packages/beacon-node/src/chain/bls/interface.ts:25-68
+  verifySignatureSets(sets, opts?)                -> Promise<boolean>
+  verifySignatureSetsSameMessage(sets, msg, opts?) -> Promise<boolean[]>
+  close()                                         -> Promise<void>
+  canAcceptWork()                                 -> boolean
+Default implementation replaced: BlsMultiThreadWorkerPool (multithread/index.ts:113).
+
+The pool's scheduling semantics are kept (VerifySignatureOpts, interface.ts:4-23): batchable
+jobs wait at most MAX_BUFFER_WAIT_MS or until more than MAX_BUFFERED_SIGS signatures are buffered
+(index.ts:320-339), priority jobs go to the front (index.ts:343-349), verifyOnMainThread runs
+synchronously.  Work is dispatched to the device in groups: every queued same-message job of one
+dispatch becomes ONE device pass (gbv_verify_same_message_multi), which is what lets small gossip
+batches (32-128 sets) fill 256 CUs.  Device calls run on a worker thread (the analogue of the
+Node-API async work the addon would use), so the event loop never blocks on the GPU.
+
+Signature sets are in index form: pubkeys are validator indices into the HBM-resident
+index2pubkey table (state-transition/src/cache/epochCache.ts:126-133) fed by add_pubkeys()
+(syncPubkeys, pubkeyCache.ts:50-69; addFinalizedPubkey, epochCache.ts:1064-1083).
+"""
+from __future__ import annotations
+
+import asyncio
+import ctypes
+import time
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence, Tuple, Union
+
+from . import _native
+from ._native import EmptyAggregateError, GbvError, GbvSet, QueueAbortedError  # noqa: F401
+
+MAX_SIGNATURE_SETS_PER_JOB = 128   # multithread/index.ts:56
+MAX_BUFFERED_SIGS = 32             # multithread/index.ts:65
+MAX_BUFFER_WAIT_MS = 100           # multithread/index.ts:74
+MAX_JOBS_CAN_ACCEPT_WORK = 512     # multithread/index.ts:79
+
+
+@dataclass
+class SingleSignatureSet:
+    """SingleSignatureSet (state-transition/src/util/signatureSets.ts:9-14), index form.
+    ``pubkey`` (48-byte compressed) overrides ``index`` for sets whose key comes from the message."""
+    index: int
+    signing_root: bytes
+    signature: bytes
+    pubkey: Optional[bytes] = None
+
+
+@dataclass
+class AggregatedSignatureSet:
+    """AggregatedSignatureSet (signatureSets.ts:16-21), index form."""
+    indices: Sequence[int]
+    signing_root: bytes
+    signature: bytes
+
+
+ISignatureSet = Union[SingleSignatureSet, AggregatedSignatureSet]
+
+
+@dataclass
+class VerifySignatureOpts:
+    """VerifySignatureOpts (interface.ts:4-23)."""
+    batchable: bool = False
+    verify_on_main_thread: bool = False
+    priority: bool = False
+
+
+def chunkify_maximize_chunk_size(arr, min_per_chunk):
+    """chunkifyMaximizeChunkSize (multithread/utils.ts:4-18)."""
+    chunk_count = len(arr) // min_per_chunk
+    if chunk_count <= 1:
+        return [list(arr)]
+    per_chunk = -(-len(arr) // chunk_count)
+    return [list(arr[i:i + per_chunk]) for i in range(0, len(arr), per_chunk)]
+
+
+@dataclass
+class _Job:
+    kind: str  # "default" | "same_message"
+    opts: VerifySignatureOpts
+    future: asyncio.Future
+    sets: list
+    message: bytes = b""
+    added: float = field(default_factory=time.monotonic)
+
+    def sig_sets(self):
+        # jobItemSigSets (jobItem.ts:38-45): a same-message job counts as one
+        return len(self.sets) if self.kind == "default" else 1
+
+
+class GpuBlsVerifier:
+    """IBlsVerifier on one MI355X (one process per GPU)."""
+
+    def __init__(self, device: int = 0):
+        self._lib = _native.load_library()
+        ctx = ctypes.c_void_p()
+        rc = self._lib.gbv_init(int(device), ctypes.byref(ctx))
+        if rc != _native.GBV_OK:
+            raise GbvError(rc, "gbv_init(%d) failed: no usable HIP device" % device)
+        self._ctx = ctx
+        self._closed = False
+        self._jobs: List[_Job] = []
+        self._buffered: Optional[dict] = None
+        self._busy = 0
+        self._run_scheduled = False
+        self.metrics = {"total_sig_sets": 0, "batchable_sig_sets": 0, "same_message_sets": 0,
+                        "device_passes": 0, "same_message_retry_sets": 0}
+
+    # ---- index2pubkey table ------------------------------------------------------------------
+    def add_pubkeys(self, first_index: int, pubkeys: Union[bytes, Sequence[bytes]], validate: bool = False) -> bytes:
+        """Decompress 48-byte pubkeys into HBM slots [first_index, first_index+n).  Returns the
+        per-key status bytes (0 = ok, see GBV_PT_* in include/gbv.h)."""
+        self._check_open()
+        blob = pubkeys if isinstance(pubkeys, (bytes, bytearray)) else b"".join(pubkeys)
+        if len(blob) % 48:
+            raise ValueError("pubkeys must be 48-byte compressed points")
+        n = len(blob) // 48
+        st = ctypes.create_string_buffer(max(n, 1))
+        rc = self._lib.gbv_pubkeys_append(self._ctx, first_index, blob, n, 1 if validate else 0, st)
+        _native.check(self._lib, self._ctx, rc)
+        return st.raw[:n]
+
+    def replicate_pubkeys(self, src_first: int, src_n: int, dst_first: int, n: int):
+        _native.check(self._lib, self._ctx, self._lib.gbv_pubkeys_replicate(self._ctx, src_first, src_n, dst_first, n))
+
+    @property
+    def pubkey_count(self) -> int:
+        return int(self._lib.gbv_pubkeys_count(self._ctx))
+
+    def aggregate_pubkeys(self, indices: Sequence[int]) -> bytes:
+        """aggregatePublicKeys(index2pubkey[indices]).toBytes() (bls/utils.ts:5-20)."""
+        self._check_open()
+        arr = (ctypes.c_uint32 * max(len(indices), 1))(*indices)
+        out = ctypes.create_string_buffer(48)
+        _native.check(self._lib, self._ctx, self._lib.gbv_aggregate_pubkeys(self._ctx, arr, len(indices), out))
+        return out.raw
+
+    # ---- synchronous device calls (also the verifyOnMainThread path) ---------------------------
+    def verify_signature_sets_sync(self, sets: Sequence[ISignatureSet]) -> bool:
+        self._check_open()
+        n = len(sets)
+        arena: List[int] = []
+        keep = []
+        arr = (GbvSet * max(n, 1))()
+        for i, s in enumerate(sets):
+            root = bytes(s.signing_root)
+            sig = bytes(s.signature)
+            if len(root) != 32:
+                raise ValueError("signing root must be 32 bytes")
+            keep.extend([root, sig])
+            e = arr[i]
+            e.msg32 = ctypes.cast(ctypes.c_char_p(root), ctypes.c_void_p)
+            e.sig = ctypes.cast(ctypes.c_char_p(sig), ctypes.c_void_p) if sig else None
+            e.sig_len = len(sig)
+            if isinstance(s, AggregatedSignatureSet):
+                e.idx_off, e.idx_len = len(arena), len(s.indices)
+                arena.extend(int(x) for x in s.indices)
+            elif s.pubkey is not None:
+                pk = bytes(s.pubkey)
+                if len(pk) != 48:
+                    raise ValueError("raw pubkey must be 48 bytes")
+                keep.append(pk)
+                e.raw_pk48 = ctypes.cast(ctypes.c_char_p(pk), ctypes.c_void_p)
+                e.idx_off, e.idx_len = len(arena), 0
+            else:
+                e.idx_off, e.idx_len = len(arena), 1
+                arena.append(int(s.index))
+        ar = (ctypes.c_uint32 * max(len(arena), 1))(*arena)
+        allv = ctypes.c_uint8(0)
+        rc = self._lib.gbv_verify_sets(self._ctx, arr, n, ar, ctypes.byref(allv), None)
+        _native.check(self._lib, self._ctx, rc)
+        self.metrics["device_passes"] += 1
+        return bool(allv.value)
+
+    def verify_same_message_multi_sync(self, calls: Sequence[Tuple[Sequence[Tuple[int, bytes]], bytes]]) -> List[List[bool]]:
+        """Many verifySignatureSetsSameMessage calls in one device pass."""
+        self._check_open()
+        off = [0]
+        idx: List[int] = []
+        sigs = []
+        msgs = []
+        for sets, message in calls:
+            if len(message) != 32:
+                raise ValueError("message must be 32 bytes")
+            msgs.append(bytes(message))
+            for index, sig in sets:
+                sig = bytes(sig)
+                # SSZ Bytes96 on the wire; any other length throws in fromBytes -> that set is false.
+                # Mapped to the 96-byte all-0x00 encoding, which blst rejects (no compression bit).
+                sigs.append(sig if len(sig) == 96 else bytes(96))
+                idx.append(int(index))
+            off.append(len(idx))
+        n = len(idx)
+        offa = (ctypes.c_uint32 * len(off))(*off)
+        idxa = (ctypes.c_uint32 * max(n, 1))(*idx)
+        valid = ctypes.create_string_buffer(max(n, 1))
+        rc = self._lib.gbv_verify_same_message_multi(self._ctx, len(calls), offa, idxa, b"".join(sigs),
+                                                     b"".join(msgs) or bytes(32), valid)
+        _native.check(self._lib, self._ctx, rc)
+        self.metrics["device_passes"] += 1
+        out, raw = [], valid.raw
+        for g in range(len(calls)):
+            out.append([raw[i] == 1 for i in range(off[g], off[g + 1])])
+        return out
+
+    def verify_signature_sets_same_message_sync(self, sets: Sequence[Tuple[int, bytes]], message: bytes) -> List[bool]:
+        return self.verify_same_message_multi_sync([(sets, message)])[0]
+
+    # ---- IBlsVerifier (async) -------------------------------------------------------------------
+    async def verify_signature_sets(self, sets: Sequence[ISignatureSet], opts: Optional[VerifySignatureOpts] = None) -> bool:
+        opts = opts or VerifySignatureOpts()
+        self.metrics["total_sig_sets"] += len(sets)
+        if opts.batchable:
+            self.metrics["batchable_sig_sets"] += len(sets)
+        if opts.verify_on_main_thread:
+            return self.verify_signature_sets_sync(sets)
+        loop = asyncio.get_running_loop()
+        futs = []
+        for chunk in chunkify_maximize_chunk_size(list(sets), MAX_SIGNATURE_SETS_PER_JOB):
+            fut = loop.create_future()
+            self._queue(_Job("default", opts, fut, chunk))
+            futs.append(fut)
+        results = await asyncio.gather(*futs)
+        return all(r is True for r in results)
+
+    async def verify_signature_sets_same_message(self, sets: Sequence[Tuple[int, bytes]], message: bytes,
+                                                 opts: Optional[VerifySignatureOpts] = None) -> List[bool]:
+        opts = opts or VerifySignatureOpts()
+        self.metrics["same_message_sets"] += len(sets)
+        loop = asyncio.get_running_loop()
+        futs = []
+        # chunkify here too so a job carries at most one reference chunk (index.ts:218-219); the
+        # device re-applies the same chunk rule to the job it receives, which is then a no-op.
+        for chunk in chunkify_maximize_chunk_size(list(sets), MAX_SIGNATURE_SETS_PER_JOB):
+            fut = loop.create_future()
+            self._queue(_Job("same_message", opts, fut, chunk, bytes(message)))
+            futs.append(fut)
+        results = await asyncio.gather(*futs)
+        return [b for r in results for b in r]
+
+    async def close(self):
+        if self._closed:
+            return
+        self._closed = True
+        if self._buffered and self._buffered["timer"]:
+            self._buffered["timer"].cancel()
+        for job in self._jobs + (self._buffered["jobs"] if self._buffered else []):
+            if not job.future.done():
+                job.future.set_exception(QueueAbortedError(_native.GBV_E_CLOSED, "QUEUE_ABORTED"))
+        self._jobs = []
+        self._buffered = None
+        self._lib.gbv_destroy(self._ctx)
+        self._ctx = None
+
+    def can_accept_work(self) -> bool:
+        """index.ts:149-155: a device pass in flight counts as the busy pool."""
+        return self._busy == 0 and len(self._jobs) < MAX_JOBS_CAN_ACCEPT_WORK
+
+    # ---- queueing (index.ts:302-352, 539-550) ------------------------------------------------
+    def _check_open(self):
+        if self._closed:
+            raise QueueAbortedError(_native.GBV_E_CLOSED, "QUEUE_ABORTED")
+
+    def _queue(self, job: _Job):
+        self._check_open()
+        loop = asyncio.get_running_loop()
+        if job.opts.batchable:
+            if self._buffered is None:
+                self._buffered = {"jobs": [], "prio": [], "sigs": 0,
+                                  "timer": loop.call_later(MAX_BUFFER_WAIT_MS / 1000.0, self._run_buffered)}
+            (self._buffered["prio"] if job.opts.priority else self._buffered["jobs"]).append(job)
+            self._buffered["sigs"] += job.sig_sets()
+            if self._buffered["sigs"] > MAX_BUFFERED_SIGS:
+                self._buffered["timer"].cancel()
+                self._run_buffered()
+        else:
+            if job.opts.priority:
+                self._jobs.insert(0, job)
+            else:
+                self._jobs.append(job)
+            self._schedule()
+
+    def _run_buffered(self):
+        b = self._buffered
+        if b is None:
+            return
+        self._buffered = None
+        self._jobs.extend(b["jobs"])
+        for job in b["prio"]:
+            self._jobs.insert(0, job)
+        self._schedule()
+
+    def _schedule(self):
+        if not self._run_scheduled:
+            self._run_scheduled = True
+            asyncio.get_running_loop().call_soon(lambda: asyncio.ensure_future(self._run_jobs()))
+
+    async def _run_jobs(self):
+        self._run_scheduled = False
+        if self._closed or self._busy or not self._jobs:
+            return
+        jobs, self._jobs = self._jobs, []
+        self._busy += 1
+        try:
+            sm = [j for j in jobs if j.kind == "same_message"]
+            df = [j for j in jobs if j.kind == "default"]
+            if sm:
+                try:
+                    res = await asyncio.to_thread(self.verify_same_message_multi_sync, [(j.sets, j.message) for j in sm])
+                    for j, r in zip(sm, res):
+                        if not j.future.done():
+                            j.future.set_result(r)
+                except Exception as e:  # device failure rejects the whole group (index.ts:498-507)
+                    for j in sm:
+                        if not j.future.done():
+                            j.future.set_exception(e)
+            for j in df:
+                try:
+                    r = await asyncio.to_thread(self.verify_signature_sets_sync, j.sets)
+                    if not j.future.done():
+                        j.future.set_result(r)
+                except Exception as e:
+                    if not j.future.done():
+                        j.future.set_exception(e)
+        finally:
+            self._busy -= 1
+        if self._jobs:
+            self._schedule()
+
+    # ---- utilities (synthetic workloads / tests; not on the verification path) ----------------
+    def util_sk_to_pk(self, sks32: Sequence[bytes]) -> List[bytes]:
+        n = len(sks32)
+        out = ctypes.create_string_buffer(max(48 * n, 1))
+        _native.check(self._lib, self._ctx, self._lib.gbv_util_sk_to_pk(self._ctx, b"".join(sks32), n, out))
+        return [out.raw[48 * i:48 * i + 48] for i in range(n)]
+
+    def util_sign(self, sks32: Sequence[bytes], grp: Sequence[int], msgs32: Sequence[bytes]) -> List[bytes]:
+        n = len(sks32)
+        out = ctypes.create_string_buffer(max(96 * n, 1))
+        g = (ctypes.c_uint32 * max(n, 1))(*grp)
+        rc = self._lib.gbv_util_sign(self._ctx, b"".join(sks32), n, g, b"".join(msgs32), len(msgs32), out)
+        _native.check(self._lib, self._ctx, rc)
+        return [out.raw[96 * i:96 * i + 96] for i in range(n)]
+
+    def util_hash_to_g2(self, msgs32: Sequence[bytes]) -> List[bytes]:
+        n = len(msgs32)
+        out = ctypes.create_string_buffer(max(192 * n, 1))
+        _native.check(self._lib, self._ctx, self._lib.gbv_util_hash_to_g2(self._ctx, b"".join(msgs32), n, out))
+        return [out.raw[192 * i:192 * i + 192] for i in range(n)]

@@ -38,7 +38,7 @@ void ht_expand(uint8_t* out256, const uint8_t* msg32) {
 int ht_g2_decode(uint8_t* out, const uint8_t* in, uint32_t len) {
   G2A a;
   uint8_t st = g2_decode(a, in, len);
-  if (st == GBV_PT_OK) { store_fp2(out, a.x); store_fp2(out + 96, a.y); }
+  if (st == PT_OK) { store_fp2(out, a.x); store_fp2(out + 96, a.y); }
   return st;
 }
 int ht_g2_in_subgroup(const uint8_t* xy) {
@@ -48,7 +48,7 @@ int ht_g2_in_subgroup(const uint8_t* xy) {
 int ht_g1_decompress(uint8_t* out, const uint8_t* in) {
   G1A a;
   uint8_t st = g1_decompress(a, in);
-  if (st == GBV_PT_OK) { store_canon(out, a.x); store_canon(out + 48, a.y); }
+  if (st == PT_OK) { store_canon(out, a.x); store_canon(out + 48, a.y); }
   return st;
 }
 int ht_g1_in_subgroup(const uint8_t* xy) {
@@ -81,9 +81,9 @@ void ht_pairing(uint8_t* out, const uint8_t* p96, const uint8_t* q192) {
 // verify(pk48, msg32, sig) following the blst accept/reject rules
 int ht_verify(const uint8_t* pk48, const uint8_t* msg32, const uint8_t* sig, uint32_t sig_len) {
   G1A pk;
-  if (g1_decompress(pk, pk48) != GBV_PT_OK) return 0;
+  if (g1_decompress(pk, pk48) != PT_OK) return 0;
   G2A s;
-  if (g2_decode(s, sig, sig_len) != GBV_PT_OK) return 0;
+  if (g2_decode(s, sig, sig_len) != PT_OK) return 0;
   if (!g2_in_subgroup(s)) return 0;
   uint32_t w[8];
   for (int i = 0; i < 8; ++i) w[i] = ((uint32_t)msg32[4*i] << 24) | ((uint32_t)msg32[4*i+1] << 16) | ((uint32_t)msg32[4*i+2] << 8) | msg32[4*i+3];
