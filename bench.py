@@ -1,0 +1,203 @@
+#!/usr/bin/env python3
+"""Headline benchmark: signature sets verified per second on MI355X (BASELINE.json `metric`).
+
+Workload (BASELINE.json configs[1]): the gossip attestation stream -- 1,048,576
+single-pubkey signature sets in verifySignatureSetsSameMessage calls of 32-128 sets (uniform
+sizes, numpy PCG64(seed=2)), validators drawn without replacement from a 1,048,576-entry
+HBM-resident index2pubkey table whose keys are interop keys sk_i = interopSecretKey(i mod 1024)
+(state-transition/src/util/interop.ts:18-22), messages m_g = sha256("gbv-bench" || u64le(g)),
+signatures sk*H(m) produced on the GPU before timing.  A "step" = one verification pass over the
+whole staged workload (inputs resident in HBM, per-set booleans copied back to the host).
+
+Multi-GPU: one process per GPU (torch.distributed.run), each rank verifies its own 1M-set stream
+(weak scaling, no data-path collective); barrier + max-over-ranks time around the timed steps.
+
+Prints ONE JSON line on rank 0 (contract in the task statement) with `roofline` for the dominant
+kernel (k_sm_prepare, integer-VALU bound) and `cpu_baseline` (the C port in oracle/, timed on the
+host cores of this box on a bounded sample).
+"""
+import argparse
+import hashlib
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+R_ORDER = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
+N_VALIDATORS = 1 << 20
+N_KEYS = 1024
+# Algorithmic work per unit, in Fp-multiplication equivalents (FME; 1 FME = 300 u32 MACs,
+# 12-limb CIOS Montgomery).  SURVEY.md 8(d) component counts: G2 decompress 1.8k + G2 subgroup
+# 1.25k + r*pk (64-bit, G1) 0.8k + r*sig (64-bit, G2) 1.95k per set; per same-message chunk
+# hash_to_G2 7.2k + 2-pair Miller loop 8.8k + shared squarings 2.3k + final exponentiation 8.4k.
+W_PREPARE_FME = 5800
+W_CHUNK_FME = 26700
+MAC_PER_FME = 300
+# Integer VALU peak: v_mad_u64_u32 measured at 37.0 T lane-ops/s on MI355X
+# (tools/ubench_int.hip, profiles/r01_ubench_int.txt); theoretical 256 CU x 4 SIMD x 16 lanes x 2.4 GHz = 39.3 T.
+PEAK_MAC_PER_S = 37.0e12
+
+
+def interop_sk_bytes(i):
+    d = hashlib.sha256(i.to_bytes(32, "little")).digest()
+    return (int.from_bytes(d, "little") % R_ORDER).to_bytes(32, "big")
+
+
+def build_workload(v, n_sets, rank, log):
+    t0 = time.time()
+    sks = [interop_sk_bytes(i) for i in range(N_KEYS)]
+    pks = v.util_sk_to_pk(sks)
+    st = v.add_pubkeys(0, pks)
+    assert st == bytes(N_KEYS), "pubkey ingest failed"
+    v.replicate_pubkeys(0, N_KEYS, N_KEYS, N_VALIDATORS - N_KEYS)
+    rng = np.random.Generator(np.random.PCG64(2))
+    sizes = []
+    total = 0
+    while total < n_sets:
+        s = int(rng.integers(32, 129))
+        s = min(s, n_sets - total)
+        sizes.append(s)
+        total += s
+    call_off = np.zeros(len(sizes) + 1, dtype=np.uint32)
+    call_off[1:] = np.cumsum(sizes)
+    perm = np.random.Generator(np.random.PCG64(0x1D5 + rank)).permutation(N_VALIDATORS)
+    idx = perm[np.arange(n_sets) % N_VALIDATORS].astype(np.uint32)
+    grp = np.repeat(np.arange(len(sizes), dtype=np.uint32), sizes)
+    msgs = [hashlib.sha256(b"gbv-bench" + (g + rank * 10_000_000).to_bytes(8, "little")).digest()
+            for g in range(len(sizes))]
+    sk_arr = np.frombuffer(b"".join(sks), dtype=np.uint8).reshape(N_KEYS, 32)
+    set_sks = sk_arr[idx % N_KEYS]
+    log("workload: %d sets in %d calls, keys/table ready in %.1fs" % (n_sets, len(sizes), time.time() - t0))
+    t1 = time.time()
+    sigs = []
+    CH = 1 << 18
+    for a in range(0, n_sets, CH):
+        b = min(n_sets, a + CH)
+        sigs.extend(v.util_sign([bytes(r) for r in set_sks[a:b]], grp[a:b].tolist(), msgs))
+    log("signed %d sets on the GPU in %.1fs" % (n_sets, time.time() - t1))
+    return call_off, idx, b"".join(sigs), b"".join(msgs)
+
+
+def p50_batch_latency(v, call_off, idx, sigs, msgs, reps=20):
+    """Latency of one gossip batch (one verifySignatureSetsSameMessage call of 64 sets) alone."""
+    n = 64
+    lat = []
+    for r in range(reps):
+        t = time.perf_counter()
+        v.verify_same_message_multi_sync([([(int(idx[i]), sigs[96 * i:96 * i + 96]) for i in range(n)], msgs[:32])])
+        lat.append((time.perf_counter() - t) * 1e3)
+    return float(np.median(lat))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--sets", type=int, default=1 << 20)
+    ap.add_argument("--cpu-sample", type=int, default=None, help="sets in the CPU baseline sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+
+    def log(msg):
+        if rank == 0:
+            print("[bench] " + msg, file=sys.stderr, flush=True)
+
+    from lodestar_amd import GpuBlsVerifier
+    from lodestar_amd.build import build
+    build()
+    v = GpuBlsVerifier(local_rank)
+    call_off, idx, sigs, msgs = build_workload(v, args.sets, rank, log)
+    staged = v.stage_same_message(call_off, idx, sigs, msgs)
+
+    for _ in range(args.warmup):
+        res = staged.verify(True)
+    if args.warmup:
+        ok = sum(res)
+        assert ok == args.sets, "warmup: %d of %d sets verified" % (ok, args.sets)
+        log("warmup ok: all %d sets valid" % ok)
+
+    kms = np.zeros(5)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res = staged.verify(True)
+        kms += np.array(v.last_kernel_ms())
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    assert sum(res) == args.sets
+    kms /= max(args.steps, 1)
+    total_sets = args.sets * world * args.steps
+    value = total_sets / elapsed
+    ms_per_step = elapsed / args.steps * 1e3
+
+    lat = p50_batch_latency(v, call_off, idx, sigs, msgs)
+
+    n_chunks = len(call_off) - 1  # calls of 32-128 sets are single chunks
+    t_prep = kms[1] * 1e-3
+    achieved = args.sets * W_PREPARE_FME * MAC_PER_FME / t_prep / 1e12 if t_prep > 0 else 0.0
+    peak = PEAK_MAC_PER_S / 1e12
+    roofline = {"bound": "valu-int", "kernel": "k_sm_prepare", "achieved": round(achieved, 4), "peak": peak,
+                "unit": "T u32-MAC/s", "frac": round(achieved / peak, 5), "traffic": None,
+                "work_per_unit_fme": W_PREPARE_FME, "units_per_launch": args.sets,
+                "kernel_ms": {k: round(float(x), 3) for k, x in zip(
+                    ["hash", "prepare", "group_sum", "pairing", "fallback"], kms)}}
+
+    cpu = None
+    if rank == 0 and not args.no_cpu_baseline:
+        from oracle import cpu_baseline
+        cpu = cpu_baseline.measure_same_message(sample=args.cpu_sample)
+
+    line = {
+        "metric": "signature sets verified/sec (batch verify, same-message gossip stream)",
+        "value": round(value, 1),
+        "unit": "sets/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 3),
+        "p50_batch_latency_ms": round(lat, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32 (381-bit Montgomery, integer VALU)",
+        "data": "synthetic (interop keys, sha256 messages, GPU-signed)",
+        "config": {"workload": "C2 gossip attestation stream: 1M single-pubkey sets, same-message calls of 32-128",
+                   "sets_per_gpu": args.sets, "calls_per_gpu": n_chunks, "table": N_VALIDATORS,
+                   "parallelism": "replicas/dp%d" % world},
+        "roofline": roofline,
+        "cpu_baseline": cpu,
+    }
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    staged.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,6 +1,7 @@
 """Build the gfx950 HIP library in-tree (lodestar_amd/libgbv.so) with hipcc."""
 import os
 import subprocess
+import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
@@ -21,11 +22,35 @@ def needs_build():
     return any(os.path.getmtime(s) > t for s in sources())
 
 
-def build(force=False, verbose=False):
+def _compile(src, obj, verbose):
+    cmd = ["hipcc", "--offload-arch=%s" % ARCH, "-O3", "-fPIC", "-std=c++17", "-c", src, "-o", obj + ".tmp"]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.check_call(cmd)
+    os.replace(obj + ".tmp", obj)
+    return obj
+
+
+def build(force=False, verbose=False, jobs=None):
+    """Compile each kernel family (lodestar_amd/csrc/*.hip) in parallel and link libgbv.so."""
     if not force and not needs_build():
         return LIB
-    cmd = ["hipcc", "--offload-arch=%s" % ARCH, "-O3", "-fPIC", "-shared", "-std=c++17",
-           "-o", LIB + ".tmp", os.path.join(CSRC, "gbv.hip")]
+    from concurrent.futures import ThreadPoolExecutor
+    objdir = os.path.join(HERE, "build")
+    os.makedirs(objdir, exist_ok=True)
+    tus = [os.path.join(CSRC, f) for f in sorted(os.listdir(CSRC)) if f.endswith(".hip")]
+    headers_t = max(os.path.getmtime(s) for s in sources() if not s.endswith(".hip"))
+    jobs = jobs or min(len(tus), max(1, (os.cpu_count() or 4)))
+    todo = []
+    objs = []
+    for src in tus:
+        obj = os.path.join(objdir, os.path.basename(src)[:-4] + ".o")
+        objs.append(obj)
+        if force or not os.path.exists(obj) or os.path.getmtime(obj) < max(headers_t, os.path.getmtime(src)):
+            todo.append((src, obj))
+    with ThreadPoolExecutor(jobs) as ex:
+        list(ex.map(lambda t: _compile(t[0], t[1], verbose), todo))
+    cmd = ["hipcc", "--offload-arch=%s" % ARCH, "-shared", "-fPIC", "-o", LIB + ".tmp"] + objs
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.check_call(cmd)
@@ -34,5 +59,7 @@ def build(force=False, verbose=False):
 
 
 if __name__ == "__main__":
-    build(force=True, verbose=True)
-    print("built", LIB)
+    import time
+    t = time.time()
+    build(force="--force" in sys.argv, verbose=True)
+    print("built", LIB, "in %.1fs" % (time.time() - t))

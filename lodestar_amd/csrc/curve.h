@@ -191,6 +191,14 @@ template <class F> GBV_HD Jac<F> jac_mul_xabs_jac(const Jac<F>& q) {
   return r;
 }
 
+// Out-of-line scalar multiplications (coarse: the point crosses the call once).
+GBV_NI G1J g1_mul_u64(G1A q, uint64_t k) { return jac_mul_u64(q, k); }
+GBV_NI G2J g2_mul_u64(G2A q, uint64_t k) { return jac_mul_u64(q, k); }
+GBV_NI G2J g2_mul_xabs(G2A q) { return jac_mul_xabs(q); }
+GBV_NI G2J g2_mul_xabs_jac(G2J q) { return jac_mul_xabs_jac(q); }
+GBV_NI G1J g1_mul_u256(G1A q, const uint32_t* k) { return jac_mul_u256(q, k); }
+GBV_NI G2J g2_mul_u256(G2A q, const uint32_t* k) { return jac_mul_u256(q, k); }
+
 // ---- curve constants & decoding -------------------------------------------------------------
 enum : uint8_t {
   PT_OK = 0,
@@ -311,13 +319,13 @@ GBV_HD G2J g2_psi_jac(const G2J& a) {
 }
 
 // G2 membership (Scott 2021): psi(Q) == [x] Q = -[|x|] Q.  Q affine, not infinity.
-GBV_HD bool g2_in_subgroup(const G2A& q) {
-  G2J xq = jac_neg(jac_mul_xabs(q));
+GBV_NI bool g2_in_subgroup(G2A q) {
+  G2J xq = jac_neg(g2_mul_xabs(q));
   return jac_eq_aff(xq, g2_psi(q));
 }
 
 // G1 membership (Scott 2021): (beta x, y) == [-x^2] P.  P affine, not infinity.
-GBV_HD bool g1_in_subgroup(const G1A& p) {
+GBV_NI bool g1_in_subgroup(G1A p) {
   G1J t = jac_mul_xabs(p);           // [|x|] P
   t = jac_mul_xabs_jac(t);           // [x^2] P
   t = jac_neg(t);                    // [-x^2] P

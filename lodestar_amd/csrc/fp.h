@@ -94,33 +94,57 @@ GBV_HD Fp fp_neg(const Fp& a) {
 
 GBV_HD Fp fp_dbl(const Fp& a) { return fp_add(a, a); }
 
-// Montgomery product a*b*2^-384 mod p.  Inputs < p, output < p.
+// One multiply-accumulate into a 96-bit column accumulator {acc (64), top (32)}:
+//   acc += a * b  (v_mad_u64_u32 with carry-out in VCC),  top += carry  (v_addc_co_u32).
+GBV_HD void mac96(uint64_t& acc, uint32_t& top, uint32_t a, uint32_t b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\tv_addc_co_u32 %1, vcc, 0, %1, vcc"
+      : "+v"(acc), "+v"(top)
+      : "v"(a), "v"(b)
+      : "vcc");
+#else  // host build used only by tests/native/hosttest.cpp
+  uint64_t p = (uint64_t)a * b;
+  uint64_t s = acc + p;
+  top += (s < acc) ? 1u : 0u;
+  acc = s;
+#endif
+}
+
+// Montgomery product a*b*2^-384 mod p by finely integrated product scanning (FIPS): column k of
+// a*b and of m*p accumulate into one 96-bit accumulator, m_k is derived from the column's low
+// word.  2 VALU instructions per limb product (288 products), no carry propagation passes.
+// Inputs < p, output < p.
 GBV_HD Fp fp_mul_inl(const Fp& a, const Fp& b) {
-  uint32_t t[12];
+  uint32_t m[12], r[12];
+  uint64_t acc = 0;
+  uint32_t top = 0;
 #pragma unroll
-  for (int i = 0; i < 12; ++i) t[i] = 0;
+  for (int k = 0; k < 12; ++k) {
 #pragma unroll
-  for (int i = 0; i < 12; ++i) {
-    const uint32_t bi = b.v[i];
-    uint64_t A = (uint64_t)a.v[0] * bi + t[0];
-    const uint32_t m = (uint32_t)A * NP0;
-    uint64_t C = (uint64_t)m * P_RAW.v[0] + (uint32_t)A;
-    A >>= 32;
-    C >>= 32;
+    for (int i = 0; i <= k; ++i) mac96(acc, top, a.v[i], b.v[k - i]);
 #pragma unroll
-    for (int j = 1; j < 12; ++j) {
-      A = (uint64_t)a.v[j] * bi + t[j] + A;
-      C = (uint64_t)m * P_RAW.v[j] + (uint32_t)A + C;
-      t[j - 1] = (uint32_t)C;
-      A >>= 32;
-      C >>= 32;
-    }
-    t[11] = (uint32_t)(A + C);
+    for (int i = 0; i < k; ++i) mac96(acc, top, m[i], P_RAW.v[k - i]);
+    m[k] = (uint32_t)acc * NP0;
+    mac96(acc, top, m[k], P_RAW.v[0]);
+    acc = (acc >> 32) | ((uint64_t)top << 32);
+    top = 0;
   }
-  Fp r;
 #pragma unroll
-  for (int i = 0; i < 12; ++i) r.v[i] = t[i];
-  return fp_reduce_once(r);
+  for (int k = 12; k < 23; ++k) {
+#pragma unroll
+    for (int i = k - 11; i < 12; ++i) {
+      mac96(acc, top, a.v[i], b.v[k - i]);
+      mac96(acc, top, m[i], P_RAW.v[k - i]);
+    }
+    r[k - 12] = (uint32_t)acc;
+    acc = (acc >> 32) | ((uint64_t)top << 32);
+    top = 0;
+  }
+  r[11] = (uint32_t)acc;
+  Fp o;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) o.v[i] = r[i];
+  return fp_reduce_once(o);
 }
 
 GBV_HD Fp fp_sqr_inl(const Fp& a) { return fp_mul_inl(a, a); }

@@ -1,11 +1,14 @@
 // Host side of the C ABI (include/gbv.h): device memory, the HBM pubkey table, chunking exactly
 // as the reference pool does it, kernel sequencing on one HIP stream per context.
 #include "../../include/gbv.h"
-#include "kernels.h"
+#include "launch.h"
+#include "kernel_common.h"
 
 #include <sys/random.h>
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -86,6 +89,16 @@ static Seed fresh_seed() {
   return s;
 }
 
+namespace gbv {
+void debug_sync(hipStream_t s, const char* kernel) {
+  static int on = getenv("GBV_SYNC_DEBUG") ? atoi(getenv("GBV_SYNC_DEBUG")) : 0;
+  if (!on) return;
+  hipError_t e = hipStreamSynchronize(s);
+  if (e == hipSuccess) e = hipGetLastError();
+  fprintf(stderr, "[gbv] %s: %s\n", kernel, hipGetErrorString(e));
+}
+}  // namespace gbv
+
 extern "C" {
 
 int gbv_init(int device, gbv_ctx** out) {
@@ -153,7 +166,7 @@ int gbv_pubkeys_append(gbv_ctx* c, uint32_t first, const uint8_t* pk48, size_t n
   HIP_CHECK(c, dalloc(&d_pk, 48 * n));
   HIP_CHECK(c, dalloc(&d_st, n));
   HIP_CHECK(c, hipMemcpyAsync(d_pk, pk48, 48 * n, hipMemcpyHostToDevice, c->stream));
-  hipLaunchKernelGGL(k_pk_decompress, dim3(blocks_for(n)), dim3(TPB), 0, c->stream, (uint32_t)n, d_pk, validate,
+  launch_pk_decompress(LaunchCfg{blocks_for(n), TPB, c->stream}, (uint32_t)n, d_pk, validate,
                      c->table + first, c->table_ok + first, d_st);
   HIP_CHECK(c, hipGetLastError());
   if (status) HIP_CHECK(c, hipMemcpyAsync(status, d_st, n, hipMemcpyDeviceToHost, c->stream));
@@ -169,7 +182,7 @@ int gbv_pubkeys_replicate(gbv_ctx* c, uint32_t src_first, uint32_t src_n, uint32
   HIP_CHECK(c, hipSetDevice(c->device));
   int rc = table_reserve(c, (size_t)dst_first + n);
   if (rc) return rc;
-  hipLaunchKernelGGL(k_pk_replicate, dim3(blocks_for(n, 256)), dim3(256), 0, c->stream, c->table, c->table_ok, src_first, src_n,
+  launch_pk_replicate(LaunchCfg{blocks_for(n, 256), 256, c->stream}, c->table, c->table_ok, src_first, src_n,
                      dst_first, (uint32_t)n);
   HIP_CHECK(c, hipGetLastError());
   HIP_CHECK(c, hipStreamSynchronize(c->stream));
@@ -192,7 +205,7 @@ int gbv_aggregate_pubkeys(gbv_ctx* c, const uint32_t* idx, size_t k, uint8_t out
   HIP_CHECK(c, dalloc(&d_out, 48));
   HIP_CHECK(c, hipMemcpyAsync(d_idx, idx, 4 * k, hipMemcpyHostToDevice, c->stream));
   HIP_CHECK(c, hipMemsetAsync(d_bad, 0, 4, c->stream));
-  hipLaunchKernelGGL(k_aggregate, dim3(1), dim3(256), 0, c->stream, d_idx, (uint32_t)k, c->table, c->table_ok, d_out, d_bad);
+  launch_aggregate(LaunchCfg{1, 256, c->stream}, d_idx, (uint32_t)k, c->table, c->table_ok, d_out, d_bad);
   HIP_CHECK(c, hipGetLastError());
   uint32_t bad = 0;
   HIP_CHECK(c, hipMemcpyAsync(out48, d_out, 48, hipMemcpyDeviceToHost, c->stream));
@@ -285,22 +298,22 @@ int gbv_sm_batch_verify(gbv_ctx* c, gbv_sm_batch* b, uint8_t* valid) {
   hipStream_t s = c->stream;
   HIP_CHECK(c, hipMemsetAsync(b->n_fallback, 0, 4, s));
   hipEventRecord(c->ev[0], s);
-  hipLaunchKernelGGL(k_hash_msgs, dim3(blocks_for(b->n_calls)), dim3(TPB), 0, s, b->msgs, (uint32_t)b->n_calls, b->H);
+  launch_hash_msgs(LaunchCfg{blocks_for(b->n_calls), TPB, s}, b->msgs, (uint32_t)b->n_calls, b->H);
   hipEventRecord(c->ev[1], s);
-  hipLaunchKernelGGL(k_sm_prepare, dim3(blocks_for(b->n)), dim3(TPB), 0, s, (uint32_t)b->n, b->idx, b->sig, c->table, c->table_ok,
+  launch_sm_prepare(LaunchCfg{blocks_for(b->n), TPB, s}, (uint32_t)b->n, b->idx, b->sig, c->table, c->table_ok,
                      (uint32_t)c->table_n, seed, nonce, b->S, b->rS, b->rP, b->status);
   hipEventRecord(c->ev[2], s);
-  hipLaunchKernelGGL(k_sm_group_sum, dim3(blocks_for(b->G)), dim3(TPB), 0, s, (uint32_t)b->G, b->grp_off, b->status, b->rS, b->rP,
+  launch_sm_group_sum(LaunchCfg{blocks_for(b->G), TPB, s}, (uint32_t)b->G, b->grp_off, b->status, b->rS, b->rP,
                      b->Pg, b->Sg, b->grp_state);
   hipEventRecord(c->ev[3], s);
-  hipLaunchKernelGGL(k_sm_group_pairing, dim3(blocks_for(b->G)), dim3(TPB), 0, s, (uint32_t)b->G, b->grp_msg, b->Pg, b->Sg, b->H,
+  launch_sm_group_pairing(LaunchCfg{blocks_for(b->G), TPB, s}, (uint32_t)b->G, b->grp_msg, b->Pg, b->Sg, b->H,
                      b->grp_state, b->n_fallback);
   hipEventRecord(c->ev[4], s);
   HIP_CHECK(c, hipGetLastError());
   uint32_t nfb = 0;
   HIP_CHECK(c, hipMemcpyAsync(&nfb, b->n_fallback, 4, hipMemcpyDeviceToHost, s));
   HIP_CHECK(c, hipStreamSynchronize(s));
-  hipLaunchKernelGGL(k_sm_fallback, dim3(blocks_for(b->n)), dim3(TPB), 0, s, (uint32_t)b->n, b->set_grp, b->grp_msg, b->grp_state,
+  launch_sm_fallback(LaunchCfg{blocks_for(b->n), TPB, s}, (uint32_t)b->n, b->set_grp, b->grp_msg, b->grp_state,
                      b->status, b->idx, c->table, b->S, b->H, b->valid, nfb ? 1 : 0);
   hipEventRecord(c->ev[5], s);
   HIP_CHECK(c, hipGetLastError());
@@ -394,9 +407,9 @@ int gbv_verify_sets(gbv_ctx* c, const gbv_set* sets, size_t n, const uint32_t* a
   HIP_CHECK(c, hipMemcpyAsync(d_sig, sig.data(), (size_t)stride * n, hipMemcpyHostToDevice, s));
   Seed seed = fresh_seed();
   uint32_t nonce = c->nonce++;
-  hipLaunchKernelGGL(k_vs_prepare, dim3(blocks_for(n)), dim3(TPB), 0, s, (uint32_t)n, d_off, d_idx, d_raw_flag, d_raw_pk, d_msgs, d_sig,
+  launch_vs_prepare(LaunchCfg{blocks_for(n), TPB, s}, (uint32_t)n, d_off, d_idx, d_raw_flag, d_raw_pk, d_msgs, d_sig,
                      stride, d_siglen, c->table, c->table_ok, seed, nonce, d_f, d_rS, d_status);
-  hipLaunchKernelGGL(k_vs_chunk, dim3(blocks_for(C)), dim3(TPB), 0, s, (uint32_t)C, d_chunk_off, d_status, d_f, d_rS, d_cv);
+  launch_vs_chunk(LaunchCfg{blocks_for(C), TPB, s}, (uint32_t)C, d_chunk_off, d_status, d_f, d_rS, d_cv);
   HIP_CHECK(c, hipGetLastError());
   std::vector<uint8_t> cv(C);
   HIP_CHECK(c, hipMemcpyAsync(cv.data(), d_cv, C, hipMemcpyDeviceToHost, s));
@@ -419,7 +432,7 @@ int gbv_util_sk_to_pk(gbv_ctx* c, const uint8_t* sk32, size_t n, uint8_t* pk48) 
   HIP_CHECK(c, dalloc(&d_sk, 32 * n));
   HIP_CHECK(c, dalloc(&d_pk, 48 * n));
   HIP_CHECK(c, hipMemcpyAsync(d_sk, sk32, 32 * n, hipMemcpyHostToDevice, c->stream));
-  hipLaunchKernelGGL(k_util_sk_to_pk, dim3(blocks_for(n)), dim3(TPB), 0, c->stream, (uint32_t)n, d_sk, d_pk);
+  launch_util_sk_to_pk(LaunchCfg{blocks_for(n), TPB, c->stream}, (uint32_t)n, d_sk, d_pk);
   HIP_CHECK(c, hipGetLastError());
   HIP_CHECK(c, hipMemcpyAsync(pk48, d_pk, 48 * n, hipMemcpyDeviceToHost, c->stream));
   HIP_CHECK(c, hipStreamSynchronize(c->stream));
@@ -438,8 +451,8 @@ int gbv_util_hash_to_g2(gbv_ctx* c, const uint8_t* msgs32, size_t n, uint8_t* ou
   HIP_CHECK(c, dalloc(&d_o, 192 * n));
   HIP_CHECK(c, dalloc(&d_H, n));
   HIP_CHECK(c, hipMemcpyAsync(d_m, msgs32, 32 * n, hipMemcpyHostToDevice, c->stream));
-  hipLaunchKernelGGL(k_hash_msgs, dim3(blocks_for(n)), dim3(TPB), 0, c->stream, d_m, (uint32_t)n, d_H);
-  hipLaunchKernelGGL(k_util_g2_out, dim3(blocks_for(n)), dim3(TPB), 0, c->stream, (uint32_t)n, d_H, d_o);
+  launch_hash_msgs(LaunchCfg{blocks_for(n), TPB, c->stream}, d_m, (uint32_t)n, d_H);
+  launch_util_g2_out(LaunchCfg{blocks_for(n), TPB, c->stream}, (uint32_t)n, d_H, d_o);
   HIP_CHECK(c, hipGetLastError());
   HIP_CHECK(c, hipMemcpyAsync(out192, d_o, 192 * n, hipMemcpyDeviceToHost, c->stream));
   HIP_CHECK(c, hipStreamSynchronize(c->stream));
@@ -464,8 +477,8 @@ int gbv_util_sign(gbv_ctx* c, const uint8_t* sk32, size_t n, const uint32_t* grp
   HIP_CHECK(c, hipMemcpyAsync(d_sk, sk32, 32 * n, hipMemcpyHostToDevice, c->stream));
   HIP_CHECK(c, hipMemcpyAsync(d_m, msgs32, 32 * n_msgs, hipMemcpyHostToDevice, c->stream));
   HIP_CHECK(c, hipMemcpyAsync(d_grp, grp, 4 * n, hipMemcpyHostToDevice, c->stream));
-  hipLaunchKernelGGL(k_hash_msgs, dim3(blocks_for(n_msgs)), dim3(TPB), 0, c->stream, d_m, (uint32_t)n_msgs, d_H);
-  hipLaunchKernelGGL(k_util_sign, dim3(blocks_for(n)), dim3(TPB), 0, c->stream, (uint32_t)n, d_sk, d_grp, d_H, d_sig);
+  launch_hash_msgs(LaunchCfg{blocks_for(n_msgs), TPB, c->stream}, d_m, (uint32_t)n_msgs, d_H);
+  launch_util_sign(LaunchCfg{blocks_for(n), TPB, c->stream}, (uint32_t)n, d_sk, d_grp, d_H, d_sig);
   HIP_CHECK(c, hipGetLastError());
   HIP_CHECK(c, hipMemcpyAsync(sig96, d_sig, 96 * n, hipMemcpyDeviceToHost, c->stream));
   HIP_CHECK(c, hipStreamSynchronize(c->stream));

@@ -118,7 +118,7 @@ GBV_HD Fp fp_from_be64_words(const uint32_t w[16]) {
 }
 
 // ---- simplified SWU onto E2': y^2 = x^3 + A'x + B', A' = 240i, B' = 1012(1+i), Z = -(2+i) ----
-GBV_HD G2A map_to_curve_sswu(const Fp2& u) {
+GBV_NI G2A map_to_curve_sswu(Fp2 u) {
   Fp2 u2 = fp2_sqr(u);
   Fp2 zu2 = fp2_mul(SSWU_Z, u2);
   Fp2 tv1 = fp2_add(fp2_sqr(zu2), zu2);
@@ -139,7 +139,7 @@ GBV_HD G2A map_to_curve_sswu(const Fp2& u) {
 
 // 3-isogeny E2' -> E2 (RFC 9380 E.3), output in Jacobian coordinates (no inversion):
 //   Z = xd*yd, X = xn*xd*yd^2, Y = y*yn*xd^3*yd^2
-GBV_HD G2J iso_map(const G2A& p) {
+GBV_NI G2J iso_map(G2A p) {
   const Fp2& x = p.x;
   Fp2 xn = fp2_add(fp2_mul(fp2_add(fp2_mul(fp2_add(fp2_mul(ISO_XNUM_3, x), ISO_XNUM_2), x), ISO_XNUM_1), x), ISO_XNUM_0);
   Fp2 xd = fp2_add(fp2_mul(fp2_add(x, ISO_XDEN_1), x), ISO_XDEN_0);
@@ -155,20 +155,20 @@ GBV_HD G2J iso_map(const G2A& p) {
 }
 
 // RFC 9380 G.3 clear_cofactor: h_eff P = [x^2-x-1]P + [x-1]psi(P) + psi^2(2P)
-GBV_HD G2J clear_cofactor_g2(const G2J& p) {
-  G2J t1 = jac_neg(jac_mul_xabs_jac(p));         // [x] P
+GBV_NI G2J clear_cofactor_g2(G2J p) {
+  G2J t1 = jac_neg(g2_mul_xabs_jac(p));         // [x] P
   G2J t2 = g2_psi_jac(p);                         // psi(P)
   G2J t3 = g2_psi_jac(g2_psi_jac(jac_dbl(p)));    // psi^2(2P)
   t3 = jac_add(t3, jac_neg(t2));
   t2 = jac_add(t1, t2);
-  t2 = jac_neg(jac_mul_xabs_jac(t2));             // [x] t2
+  t2 = jac_neg(g2_mul_xabs_jac(t2));             // [x] t2
   t3 = jac_add(t3, t2);
   t3 = jac_add(t3, jac_neg(t1));
   return jac_add(t3, jac_neg(p));
 }
 
 // hash_to_G2(msg32) as an affine point (Montgomery).  msg given as 8 big-endian words.
-GBV_HD G2A hash_to_g2(const uint32_t msg[8]) {
+GBV_NI G2A hash_to_g2(const uint32_t* msg) {
   uint32_t u[64];
   expand_message_xmd_32(u, msg);
   Fp2 u0{fp_from_be64_words(u), fp_from_be64_words(u + 16)};

@@ -1,0 +1,35 @@
+// hash_to_G2 kernels.
+#include "launch.h"
+#include "kernel_common.h"
+
+namespace gbv {
+
+// ---- hashing ----------------------------------------------------------------------------------
+__global__ void __launch_bounds__(64) k_hash_msgs(const uint8_t* __restrict__ msgs32, uint32_t n, G2A* __restrict__ H) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t w[8];
+  load_msg_words(w, msgs32 + 32ull * i);
+  H[i] = hash_to_g2(w);
+}
+
+__global__ void __launch_bounds__(64) k_util_g2_out(uint32_t n, const G2A* __restrict__ H, uint8_t* __restrict__ out192) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint8_t* o = out192 + 192ull * i;
+  fp_store_be48(o, fp_from_mont(H[i].x.c1));
+  fp_store_be48(o + 48, fp_from_mont(H[i].x.c0));
+  fp_store_be48(o + 96, fp_from_mont(H[i].y.c1));
+  fp_store_be48(o + 144, fp_from_mont(H[i].y.c0));
+}
+
+
+void launch_hash_msgs(LaunchCfg c, const uint8_t* msgs32, uint32_t n, G2A* H) {
+  hipLaunchKernelGGL(k_hash_msgs, dim3(c.blocks), dim3(c.threads), 0, c.stream, msgs32, n, H);
+  debug_sync(c.stream, "k_hash_msgs");
+}
+void launch_util_g2_out(LaunchCfg c, uint32_t n, const G2A* H, uint8_t* out192) {
+  hipLaunchKernelGGL(k_util_g2_out, dim3(c.blocks), dim3(c.threads), 0, c.stream, n, H, out192);
+  debug_sync(c.stream, "k_util_g2_out");
+}
+}  // namespace gbv

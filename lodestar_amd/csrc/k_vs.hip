@@ -1,0 +1,89 @@
+// Distinct-message path kernels (verifySignatureSets).
+#include "launch.h"
+#include "kernel_common.h"
+
+namespace gbv {
+
+// ---- distinct-message path (verifySignatureSets) ------------------------------------------------
+__global__ void __launch_bounds__(64) k_vs_prepare(uint32_t n, const uint32_t* __restrict__ set_idx_off, const uint32_t* __restrict__ idx,
+                                                   const uint8_t* __restrict__ raw_flag, const uint8_t* __restrict__ raw_pk48,
+                                                   const uint8_t* __restrict__ msgs32, const uint8_t* __restrict__ sig, uint32_t sig_stride,
+                                                   const uint32_t* __restrict__ sig_len, const G1A* __restrict__ table,
+                                                   const uint8_t* __restrict__ table_ok, Seed seed, uint32_t nonce,
+                                                   Fp12* __restrict__ f_out, G2J* __restrict__ rS_out, uint8_t* __restrict__ status) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint8_t st = SET_OK;
+  // public key: raw (validated like PublicKey.fromBytes(pk, true)) or aggregate of table entries
+  G1A pk;
+  bool pk_inf = false;
+  if (raw_flag[i]) {
+    uint8_t ds = g1_decompress(pk, raw_pk48 + 48ull * i);
+    if (ds != PT_OK || !g1_in_subgroup(pk)) st = SET_BAD_PK;
+  } else {
+    uint32_t b = set_idx_off[i], e = set_idx_off[i + 1];
+    G1J acc = jac_infinity<Fp>();
+    for (uint32_t j = b; j < e; ++j) {
+      uint32_t k = idx[j];
+      if (!table_ok[k]) st = SET_BAD_PK;
+      acc = jac_add_aff(acc, table[k]);
+    }
+    pk_inf = !jac_to_aff(pk, acc);
+  }
+  if (pk_inf) st = SET_BAD_PK;  // verify with an infinity pubkey fails in blst
+  G2A s;
+  uint8_t ds = g2_decode(s, sig + (size_t)sig_stride * i, sig_len[i]);
+  if (ds != PT_OK || !g2_in_subgroup(s)) st = SET_BAD_SIG;
+  status[i] = st;
+  if (st != SET_OK) return;
+  uint64_t r = prf_scalar(seed, i, nonce);
+  G1A rp;
+  jac_to_aff(rp, g1_mul_u64(pk, r));
+  rS_out[i] = g2_mul_u64(s, r);
+  uint32_t w[8];
+  load_msg_words(w, msgs32 + 32ull * i);
+  G2A h = hash_to_g2(w);
+  f_out[i] = miller_loop_1(rp, h);
+}
+
+__global__ void __launch_bounds__(64) k_vs_chunk(uint32_t C, const uint32_t* __restrict__ chunk_off, const uint8_t* __restrict__ status,
+                                                 const Fp12* __restrict__ f, const G2J* __restrict__ rS, uint8_t* __restrict__ chunk_valid) {
+  uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  uint32_t b = chunk_off[c], e = chunk_off[c + 1];
+  bool ok = b < e;
+  for (uint32_t i = b; i < e; ++i) ok &= status[i] == SET_OK;
+  if (!ok) {
+    chunk_valid[c] = 0;
+    return;
+  }
+  Fp12 acc = f[b];
+  G2J s = rS[b];
+  for (uint32_t i = b + 1; i < e; ++i) {
+    acc = fp12_mul(acc, f[i]);
+    s = jac_add(s, rS[i]);
+  }
+  G2A sa;
+  if (!jac_to_aff(sa, s)) {
+    chunk_valid[c] = 0;
+    return;
+  }
+  acc = fp12_mul(acc, miller_loop_1(g1_neg_generator(), sa));
+  chunk_valid[c] = fp12_is_one(final_exponentiation(acc)) ? 1 : 0;
+}
+
+
+void launch_vs_prepare(LaunchCfg c, uint32_t n, const uint32_t* set_idx_off, const uint32_t* idx, const uint8_t* raw_flag,
+                       const uint8_t* raw_pk48, const uint8_t* msgs32, const uint8_t* sig, uint32_t sig_stride, const uint32_t* sig_len,
+                       const G1A* table, const uint8_t* table_ok, const Seed& seed, uint32_t nonce, Fp12* f_out, G2J* rS_out,
+                       uint8_t* status) {
+  hipLaunchKernelGGL(k_vs_prepare, dim3(c.blocks), dim3(c.threads), 0, c.stream, n, set_idx_off, idx, raw_flag, raw_pk48, msgs32, sig,
+                     sig_stride, sig_len, table, table_ok, seed, nonce, f_out, rS_out, status);
+  debug_sync(c.stream, "k_vs_prepare");
+}
+void launch_vs_chunk(LaunchCfg c, uint32_t C, const uint32_t* chunk_off, const uint8_t* status, const Fp12* f, const G2J* rS,
+                     uint8_t* chunk_valid) {
+  hipLaunchKernelGGL(k_vs_chunk, dim3(c.blocks), dim3(c.threads), 0, c.stream, C, chunk_off, status, f, rS, chunk_valid);
+  debug_sync(c.stream, "k_vs_chunk");
+}
+}  // namespace gbv

@@ -1,0 +1,48 @@
+// Shared pieces of the gfx950 kernels of the signature-set verifier.  One thread owns one signature set (or one
+// chunk / one message) and keeps its field elements in VGPRs; the kernels of one call run back to
+// back on the context's HIP stream.
+//
+// Reference mapping:
+//   k_hash_msgs         hash_to_G2 inside blst verify / verifyMultipleAggregateSignatures
+//   k_sm_prepare        aggregateWithRandomness per set: Signature.fromBytes(sig, true) + r_i*pk, r_i*sig
+//                       (multithread/jobItem.ts:73)
+//   k_sm_group_sum      sum_i r_i pk_i, sum_i r_i sig_i per same-message chunk
+//   k_sm_group_pairing  verify(msg, aggPk, aggSig) of the chunk (worker.ts:29-107 -> maybeBatch n = 1)
+//   k_sm_fallback       retry each set individually (jobItem.ts:93-125)
+//   k_vs_prepare        per-set part of verifyMultipleAggregateSignatures (+ aggregatePublicKeys
+//                       of index lists, bls/utils.ts:5-20)
+//   k_vs_chunk          per-chunk multi-pairing product + one final exponentiation (maybeBatch.ts:17-26)
+#pragma once
+#include "hash_to_curve.h"
+#include "pairing.h"
+
+namespace gbv {
+
+struct Seed { uint32_t w[8]; };
+
+enum : uint8_t { SET_OK = 0, SET_BAD_SIG = 1, SET_BAD_PK = 2 };
+enum : uint8_t { GRP_PENDING = 0, GRP_FALLBACK = 1, GRP_OK = 2 };
+
+// Per-set random 64-bit scalar r_i = SHA-256(seed || i || nonce)[0..8), forced non-zero.
+// blst draws 64-bit random scalars for the same purpose; only the booleans are compared.
+__device__ inline uint64_t prf_scalar(const Seed& s, uint32_t i, uint32_t nonce) {
+  uint32_t st[8];
+  sha256_init(st);
+  uint32_t blk[16];
+  for (int k = 0; k < 8; ++k) blk[k] = s.w[k];
+  blk[8] = i;
+  blk[9] = nonce;
+  blk[10] = 0x80000000u;
+  for (int k = 11; k < 15; ++k) blk[k] = 0;
+  blk[15] = 40u * 8u;
+  sha256_compress(st, blk);
+  uint64_t r = ((uint64_t)st[0] << 32) | st[1];
+  return r ? r : 1ull;
+}
+
+__device__ inline void load_msg_words(uint32_t w[8], const uint8_t* m) {
+  for (int i = 0; i < 8; ++i)
+    w[i] = ((uint32_t)m[4 * i] << 24) | ((uint32_t)m[4 * i + 1] << 16) | ((uint32_t)m[4 * i + 2] << 8) | m[4 * i + 3];
+}
+
+}  // namespace gbv

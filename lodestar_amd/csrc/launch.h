@@ -1,0 +1,43 @@
+// Host-side launchers of the gfx950 kernels (one translation unit per kernel family so the build
+// parallelises; gbv.hip sequences them on the context stream).
+#pragma once
+#include <hip/hip_runtime.h>
+#include "curve.h"
+#include "fp12.h"
+
+namespace gbv {
+struct Seed;
+struct LaunchCfg { unsigned blocks; unsigned threads; hipStream_t stream; };
+
+void launch_hash_msgs(LaunchCfg c, const uint8_t* msgs32, uint32_t n, G2A* H);
+void launch_util_g2_out(LaunchCfg c, uint32_t n, const G2A* H, uint8_t* out192);
+
+void launch_sm_prepare(LaunchCfg c, uint32_t n, const uint32_t* idx, const uint8_t* sig96, const G1A* table, const uint8_t* table_ok,
+                       uint32_t table_n, const Seed& seed, uint32_t nonce, G2A* S_out, G2J* rS_out, G1J* rP_out, uint8_t* status);
+void launch_sm_group_sum(LaunchCfg c, uint32_t G, const uint32_t* grp_off, const uint8_t* status, const G2J* rS, const G1J* rP, G1A* Pg,
+                         G2A* Sg, uint8_t* grp_state);
+void launch_sm_group_pairing(LaunchCfg c, uint32_t G, const uint32_t* grp_msg, const G1A* Pg, const G2A* Sg, const G2A* H,
+                             uint8_t* grp_state, uint32_t* n_fallback);
+void launch_sm_fallback(LaunchCfg c, uint32_t n, const uint32_t* set_grp, const uint32_t* grp_msg, const uint8_t* grp_state,
+                        const uint8_t* status, const uint32_t* idx, const G1A* table, const G2A* S, const G2A* H, uint8_t* valid,
+                        int do_fallback);
+
+void launch_pk_decompress(LaunchCfg c, uint32_t n, const uint8_t* pk48, int validate, G1A* table, uint8_t* table_ok, uint8_t* status);
+void launch_pk_replicate(LaunchCfg c, G1A* table, uint8_t* table_ok, uint32_t src_first, uint32_t src_n, uint32_t dst_first, uint32_t n);
+void launch_aggregate(LaunchCfg c, const uint32_t* idx, uint32_t k, const G1A* table, const uint8_t* table_ok, uint8_t* out48,
+                      uint32_t* bad);
+void launch_util_sk_to_pk(LaunchCfg c, uint32_t n, const uint8_t* sk32, uint8_t* pk48);
+void launch_util_sign(LaunchCfg c, uint32_t n, const uint8_t* sk32, const uint32_t* grp, const G2A* H, uint8_t* sig96);
+
+void launch_vs_prepare(LaunchCfg c, uint32_t n, const uint32_t* set_idx_off, const uint32_t* idx, const uint8_t* raw_flag,
+                       const uint8_t* raw_pk48, const uint8_t* msgs32, const uint8_t* sig, uint32_t sig_stride, const uint32_t* sig_len,
+                       const G1A* table, const uint8_t* table_ok, const Seed& seed, uint32_t nonce, Fp12* f_out, G2J* rS_out,
+                       uint8_t* status);
+void launch_vs_chunk(LaunchCfg c, uint32_t C, const uint32_t* chunk_off, const uint8_t* status, const Fp12* f, const G2J* rS,
+                     uint8_t* chunk_valid);
+}  // namespace gbv
+
+namespace gbv {
+// GBV_SYNC_DEBUG=1: synchronise after every launch and report the failing kernel by name.
+void debug_sync(hipStream_t s, const char* kernel);
+}  // namespace gbv

@@ -206,6 +206,26 @@ class GpuBlsVerifier:
     def verify_signature_sets_same_message_sync(self, sets: Sequence[Tuple[int, bytes]], message: bytes) -> List[bool]:
         return self.verify_same_message_multi_sync([(sets, message)])[0]
 
+    # ---- device-resident batches (bench / replay: inputs staged in HBM once) -------------------
+    def stage_same_message(self, call_off, idx, sigs96: bytes, msgs32: bytes) -> "StagedSameMessage":
+        """Stage many verifySignatureSetsSameMessage calls (CSR call_off / idx arrays, concatenated
+        96-byte signatures and 32-byte messages) in HBM; see gbv_sm_batch_create."""
+        self._check_open()
+        import numpy as np
+        off = np.ascontiguousarray(call_off, dtype=np.uint32)
+        ix = np.ascontiguousarray(idx, dtype=np.uint32)
+        h = ctypes.c_void_p()
+        rc = self._lib.gbv_sm_batch_create(self._ctx, len(off) - 1, off.ctypes.data, ix.ctypes.data, sigs96, msgs32,
+                                           ctypes.byref(h))
+        _native.check(self._lib, self._ctx, rc)
+        return StagedSameMessage(self, h, int(off[-1]))
+
+    def last_kernel_ms(self) -> List[float]:
+        """Device time of each kernel of the last staged verify: [hash, prepare, group_sum, pairing, fallback]."""
+        buf = (ctypes.c_float * 5)()
+        k = self._lib.gbv_last_kernel_ms(self._ctx, buf, 5)
+        return [buf[i] for i in range(k)]
+
     # ---- IBlsVerifier (async) -------------------------------------------------------------------
     async def verify_signature_sets(self, sets: Sequence[ISignatureSet], opts: Optional[VerifySignatureOpts] = None) -> bool:
         opts = opts or VerifySignatureOpts()
@@ -347,3 +367,31 @@ class GpuBlsVerifier:
         out = ctypes.create_string_buffer(max(192 * n, 1))
         _native.check(self._lib, self._ctx, self._lib.gbv_util_hash_to_g2(self._ctx, b"".join(msgs32), n, out))
         return [out.raw[192 * i:192 * i + 192] for i in range(n)]
+
+
+class StagedSameMessage:
+    """Handle of a gbv_sm_batch (device-resident same-message workload)."""
+
+    def __init__(self, verifier: GpuBlsVerifier, handle: ctypes.c_void_p, n: int):
+        self._v = verifier
+        self._h = handle
+        self.n = n
+
+    def verify(self, want_results: bool = True):
+        v = self._v
+        out = ctypes.create_string_buffer(max(self.n, 1)) if want_results else None
+        rc = v._lib.gbv_sm_batch_verify(v._ctx, self._h, out)
+        _native.check(v._lib, v._ctx, rc)
+        v.metrics["device_passes"] += 1
+        return out.raw[:self.n] if want_results else None
+
+    def close(self):
+        if self._h:
+            self._v._lib.gbv_sm_batch_destroy(self._v._ctx, self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

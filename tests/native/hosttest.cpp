@@ -1,6 +1,7 @@
 // Host build of the device arithmetic library (lodestar_amd/csrc/*.h) for CPU unit tests.
 // This is NOT a product code path: it exists so the field/curve/pairing code can be checked
 // against the Python oracle without a GPU.  Built by tests/native/build_hosttest.sh.
+#define GBV_HOST_TEST 1
 #include "../../lodestar_amd/csrc/pairing.h"
 #include "../../lodestar_amd/csrc/hash_to_curve.h"
 
