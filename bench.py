@@ -79,8 +79,9 @@ def build_workload(v, n_sets, rank, log):
     for a in range(0, n_sets, CH):
         b = min(n_sets, a + CH)
         sigs.extend(v.util_sign([bytes(r) for r in set_sks[a:b]], grp[a:b].tolist(), msgs))
+        log("  signed %d/%d (%.1fs)" % (b, n_sets, time.time() - t1))
     log("signed %d sets on the GPU in %.1fs" % (n_sets, time.time() - t1))
-    return call_off, idx, b"".join(sigs), b"".join(msgs)
+    return call_off, idx, b"".join(sigs), b"".join(msgs), pks
 
 
 def p50_batch_latency(v, call_off, idx, sigs, msgs, reps=20):
@@ -121,7 +122,7 @@ def main():
     from lodestar_amd.build import build
     build()
     v = GpuBlsVerifier(local_rank)
-    call_off, idx, sigs, msgs = build_workload(v, args.sets, rank, log)
+    call_off, idx, sigs, msgs, key_pks = build_workload(v, args.sets, rank, log)
     staged = v.stage_same_message(call_off, idx, sigs, msgs)
 
     for _ in range(args.warmup):
@@ -132,6 +133,7 @@ def main():
         log("warmup ok: all %d sets valid" % ok)
 
     kms = np.zeros(5)
+    kcnt = np.zeros(5)
 
     def barrier():
         if dist is not None:
@@ -141,7 +143,9 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         res = staged.verify(True)
-        kms += np.array(v.last_kernel_ms())
+        ms, cnt = v.last_kernel_ms()
+        kms += np.array(ms)
+        kcnt += np.array(cnt)
     barrier()
     elapsed = time.perf_counter() - t0
     if dist is not None:
@@ -150,7 +154,9 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     assert sum(res) == args.sets
+    avg_launch_ms = kms / np.maximum(kcnt, 1)
     kms /= max(args.steps, 1)
+    prep_launches_per_step = kcnt[1] / max(args.steps, 1)
     total_sets = args.sets * world * args.steps
     value = total_sets / elapsed
     ms_per_step = elapsed / args.steps * 1e3
@@ -158,19 +164,24 @@ def main():
     lat = p50_batch_latency(v, call_off, idx, sigs, msgs)
 
     n_chunks = len(call_off) - 1  # calls of 32-128 sets are single chunks
-    t_prep = kms[1] * 1e-3
-    achieved = args.sets * W_PREPARE_FME * MAC_PER_FME / t_prep / 1e12 if t_prep > 0 else 0.0
+    # per launch: algorithmic MACs of the sets one k_sm_prepare launch processes / its average duration
+    units_per_launch = args.sets / max(prep_launches_per_step, 1)
+    t_launch = avg_launch_ms[1] * 1e-3
+    achieved = units_per_launch * W_PREPARE_FME * MAC_PER_FME / t_launch / 1e12 if t_launch > 0 else 0.0
     peak = PEAK_MAC_PER_S / 1e12
     roofline = {"bound": "valu-int", "kernel": "k_sm_prepare", "achieved": round(achieved, 4), "peak": peak,
                 "unit": "T u32-MAC/s", "frac": round(achieved / peak, 5), "traffic": None,
-                "work_per_unit_fme": W_PREPARE_FME, "units_per_launch": args.sets,
+                "work_per_unit_fme": W_PREPARE_FME, "units_per_launch": round(units_per_launch, 1),
+                "avg_launch_ms": round(float(avg_launch_ms[1]), 3),
                 "kernel_ms": {k: round(float(x), 3) for k, x in zip(
                     ["hash", "prepare", "group_sum", "pairing", "fallback"], kms)}}
 
     cpu = None
     if rank == 0 and not args.no_cpu_baseline:
         from oracle import cpu_baseline
-        cpu = cpu_baseline.measure_same_message(sample=args.cpu_sample)
+        cpu = cpu_baseline.measure_same_message(call_off, idx, sigs, msgs, key_pks, N_KEYS,
+                                                target_sets=args.cpu_sample or 32768)
+        log("cpu baseline: %s" % cpu)
 
     line = {
         "metric": "signature sets verified/sec (batch verify, same-message gossip stream)",

@@ -108,9 +108,10 @@ int gbv_sm_batch_create(gbv_ctx* ctx, size_t n_calls, const uint32_t* call_off, 
 /* Verify a staged batch; valid (host, optional) receives the per-set booleans. */
 int gbv_sm_batch_verify(gbv_ctx* ctx, gbv_sm_batch* b, uint8_t* valid);
 void gbv_sm_batch_destroy(gbv_ctx* ctx, gbv_sm_batch* b);
-/* Device time (ms) of each kernel of the last gbv_sm_batch_verify, measured with HIP events on
- * the context stream: [hash, prepare, group_sum, pairing, fallback]; returns the count written. */
-int gbv_last_kernel_ms(gbv_ctx* ctx, float* out, int max);
+/* Device time (ms, summed over launches) and launch count of each kernel of the last
+ * gbv_sm_batch_verify, measured with HIP events on the stream each kernel runs on:
+ * [hash, prepare, group_sum, pairing, fallback]; returns the number of entries written. */
+int gbv_last_kernel_ms(gbv_ctx* ctx, float* ms_out, int* launches_out, int max);
 
 /* ---- utilities for tests and synthetic workloads (not on the verification path) ----------- */
 /* sk32 (big-endian scalars) -> compressed pubkeys, on the device. */

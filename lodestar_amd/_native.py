@@ -77,7 +77,7 @@ def load_library(path=LIB_PATH):
         "gbv_sm_batch_create": (i32, [vp, sz, vp, vp, vp, vp, P(vp)]),
         "gbv_sm_batch_verify": (i32, [vp, vp, vp]),
         "gbv_sm_batch_destroy": (None, [vp, vp]),
-        "gbv_last_kernel_ms": (i32, [vp, P(ctypes.c_float), i32]),
+        "gbv_last_kernel_ms": (i32, [vp, P(ctypes.c_float), P(ctypes.c_int), i32]),
         "gbv_util_sk_to_pk": (i32, [vp, vp, sz, vp]),
         "gbv_util_sign": (i32, [vp, vp, sz, vp, vp, sz, vp]),
         "gbv_util_hash_to_g2": (i32, [vp, vp, sz, vp]),

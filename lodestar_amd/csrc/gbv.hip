@@ -48,13 +48,16 @@ struct gbv_ctx {
   size_t table_n = 0;
   std::string err;
   uint32_t nonce = 0;
-  hipEvent_t ev[6] = {};
+  hipStream_t stream2 = nullptr;
+  std::vector<hipEvent_t> events;
   float last_ms[5] = {};
+  int last_launches[5] = {};
   bool closed = false;
 };
 
 struct gbv_sm_batch {
   size_t n = 0, G = 0, n_calls = 0;
+  std::vector<uint32_t> grp_off_host;
   uint32_t *idx = nullptr, *grp_off = nullptr, *grp_msg = nullptr, *set_grp = nullptr, *n_fallback = nullptr;
   uint8_t *sig = nullptr, *msgs = nullptr, *status = nullptr, *grp_state = nullptr, *valid = nullptr;
   G2A *H = nullptr, *S = nullptr, *Sg = nullptr;
@@ -113,7 +116,11 @@ int gbv_init(int device, gbv_ctx** out) {
     delete c;
     return GBV_E_DEVICE;
   }
-  for (auto& e : c->ev) hipEventCreate(&e);
+  if (hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess) {
+    hipStreamDestroy(c->stream);
+    delete c;
+    return GBV_E_DEVICE;
+  }
   *out = c;
   return GBV_OK;
 }
@@ -124,8 +131,10 @@ void gbv_destroy(gbv_ctx* c) {
   if (c->stream) hipStreamSynchronize(c->stream);
   hipFree(c->table);
   hipFree(c->table_ok);
-  for (auto& e : c->ev) hipEventDestroy(e);
+  if (c->stream2) hipStreamSynchronize(c->stream2);
+  for (auto& e : c->events) hipEventDestroy(e);
   if (c->stream) hipStreamDestroy(c->stream);
+  if (c->stream2) hipStreamDestroy(c->stream2);
   delete c;
 }
 
@@ -260,6 +269,7 @@ int gbv_sm_batch_create(gbv_ctx* c, size_t n_calls, const uint32_t* call_off, co
   b->n = n;
   b->G = G;
   b->n_calls = n_calls;
+  b->grp_off_host = grp_off;
   hipError_t e = hipSuccess;
   auto chk = [&](hipError_t x) { if (x != hipSuccess && e == hipSuccess) e = x; };
   chk(dalloc(&b->idx, n)); chk(dalloc(&b->sig, 96 * n)); chk(dalloc(&b->grp_off, G + 1)); chk(dalloc(&b->grp_msg, G));
@@ -288,6 +298,9 @@ int gbv_sm_batch_create(gbv_ctx* c, size_t n_calls, const uint32_t* call_off, co
   return GBV_OK;
 }
 
+// Stream B hashes the messages while stream A runs the throughput-bound per-set kernel
+// (k_sm_prepare); the per-chunk kernels then run once over all chunks (they are latency-bound:
+// one launch over every chunk costs the same wall time as a launch over a few).
 int gbv_sm_batch_verify(gbv_ctx* c, gbv_sm_batch* b, uint8_t* valid) {
   if (!c || !b) return GBV_E_ARG;
   if (c->closed) return GBV_E_CLOSED;
@@ -295,38 +308,87 @@ int gbv_sm_batch_verify(gbv_ctx* c, gbv_sm_batch* b, uint8_t* valid) {
   HIP_CHECK(c, hipSetDevice(c->device));
   Seed seed = fresh_seed();
   uint32_t nonce = c->nonce++;
-  hipStream_t s = c->stream;
-  HIP_CHECK(c, hipMemsetAsync(b->n_fallback, 0, 4, s));
-  hipEventRecord(c->ev[0], s);
-  launch_hash_msgs(LaunchCfg{blocks_for(b->n_calls), TPB, s}, b->msgs, (uint32_t)b->n_calls, b->H);
-  hipEventRecord(c->ev[1], s);
-  launch_sm_prepare(LaunchCfg{blocks_for(b->n), TPB, s}, (uint32_t)b->n, b->idx, b->sig, c->table, c->table_ok,
-                     (uint32_t)c->table_n, seed, nonce, b->S, b->rS, b->rP, b->status);
-  hipEventRecord(c->ev[2], s);
-  launch_sm_group_sum(LaunchCfg{blocks_for(b->G), TPB, s}, (uint32_t)b->G, b->grp_off, b->status, b->rS, b->rP,
-                     b->Pg, b->Sg, b->grp_state);
-  hipEventRecord(c->ev[3], s);
-  launch_sm_group_pairing(LaunchCfg{blocks_for(b->G), TPB, s}, (uint32_t)b->G, b->grp_msg, b->Pg, b->Sg, b->H,
-                     b->grp_state, b->n_fallback);
-  hipEventRecord(c->ev[4], s);
+  hipStream_t sa = c->stream, sb = c->stream2;
+  // sub-batches of ~SUB_SETS sets, cut at chunk boundaries
+  const size_t SUB_SETS = (size_t)1 << 31;  // one launch per kernel (see above)
+  std::vector<uint32_t> gcut{0};
+  if (b->n > SUB_SETS) {
+    size_t next = SUB_SETS;
+    for (size_t g = 1; g < b->G; ++g)
+      if (b->grp_off_host[g] >= next) {
+        gcut.push_back((uint32_t)g);
+        next = b->grp_off_host[g] + SUB_SETS;
+      }
+  }
+  gcut.push_back((uint32_t)b->G);
+  size_t S = gcut.size() - 1;
+  if (c->events.size() < 8 * S + 8) {
+    size_t old = c->events.size();
+    c->events.resize(8 * S + 8);
+    for (size_t k = old; k < c->events.size(); ++k) hipEventCreate(&c->events[k]);
+  }
+  hipEvent_t* ev = c->events.data();
+  // ev layout: [0,1] hash; per s: [2+6s .. 7+6s] = prep start/end, sum start/end, pair start/end; then fallback
+  HIP_CHECK(c, hipMemsetAsync(b->n_fallback, 0, 4, sb));
+  hipEventRecord(ev[0], sb);
+  launch_hash_msgs(LaunchCfg{blocks_for(b->n_calls), TPB, sb}, b->msgs, (uint32_t)b->n_calls, b->H);
+  hipEventRecord(ev[1], sb);
+  for (size_t s = 0; s < S; ++s) {
+    hipEvent_t* e = ev + 2 + 6 * s;
+    uint32_t s0 = b->grp_off_host[gcut[s]], s1 = b->grp_off_host[gcut[s + 1]];
+    hipEventRecord(e[0], sa);
+    launch_sm_prepare(LaunchCfg{blocks_for(s1 - s0), TPB, sa}, s0, s1 - s0, b->idx, b->sig, c->table, c->table_ok,
+                      (uint32_t)c->table_n, seed, nonce, b->S, b->rS, b->rP, b->status);
+    hipEventRecord(e[1], sa);
+    HIP_CHECK(c, hipStreamWaitEvent(sb, e[1], 0));
+    uint32_t g0 = gcut[s], G = gcut[s + 1] - gcut[s];
+    hipEventRecord(e[2], sb);
+    launch_sm_group_sum(LaunchCfg{blocks_for(G), TPB, sb}, g0, G, b->grp_off, b->status, b->rS, b->rP, b->Pg, b->Sg, b->grp_state);
+    hipEventRecord(e[3], sb);
+    hipEventRecord(e[4], sb);
+    launch_sm_group_pairing(LaunchCfg{blocks_for(G), TPB, sb}, g0, G, b->grp_msg, b->Pg, b->Sg, b->H, b->grp_state, b->n_fallback);
+    hipEventRecord(e[5], sb);
+  }
   HIP_CHECK(c, hipGetLastError());
   uint32_t nfb = 0;
-  HIP_CHECK(c, hipMemcpyAsync(&nfb, b->n_fallback, 4, hipMemcpyDeviceToHost, s));
-  HIP_CHECK(c, hipStreamSynchronize(s));
-  launch_sm_fallback(LaunchCfg{blocks_for(b->n), TPB, s}, (uint32_t)b->n, b->set_grp, b->grp_msg, b->grp_state,
-                     b->status, b->idx, c->table, b->S, b->H, b->valid, nfb ? 1 : 0);
-  hipEventRecord(c->ev[5], s);
+  HIP_CHECK(c, hipMemcpyAsync(&nfb, b->n_fallback, 4, hipMemcpyDeviceToHost, sb));
+  HIP_CHECK(c, hipStreamSynchronize(sb));
+  HIP_CHECK(c, hipStreamSynchronize(sa));
+  hipEvent_t* ef = ev + 2 + 6 * S;
+  hipEventRecord(ef[0], sa);
+  launch_sm_fallback(LaunchCfg{blocks_for(b->n), TPB, sa}, (uint32_t)b->n, b->set_grp, b->grp_msg, b->grp_state, b->status, b->idx,
+                     c->table, b->S, b->H, b->valid, nfb ? 1 : 0);
+  hipEventRecord(ef[1], sa);
   HIP_CHECK(c, hipGetLastError());
-  if (valid) HIP_CHECK(c, hipMemcpyAsync(valid, b->valid, b->n, hipMemcpyDeviceToHost, s));
-  HIP_CHECK(c, hipStreamSynchronize(s));
-  for (int k = 0; k < 5; ++k) hipEventElapsedTime(&c->last_ms[k], c->ev[k], c->ev[k + 1]);
+  if (valid) HIP_CHECK(c, hipMemcpyAsync(valid, b->valid, b->n, hipMemcpyDeviceToHost, sa));
+  HIP_CHECK(c, hipStreamSynchronize(sa));
+  float t;
+  for (auto& x : c->last_ms) x = 0.f;
+  for (auto& x : c->last_launches) x = 0;
+  hipEventElapsedTime(&t, ev[0], ev[1]);
+  c->last_ms[0] = t;
+  c->last_launches[0] = 1;
+  for (size_t s = 0; s < S; ++s) {
+    hipEvent_t* e = ev + 2 + 6 * s;
+    for (int k = 0; k < 3; ++k) {
+      hipEventElapsedTime(&t, e[2 * k], e[2 * k + 1]);
+      c->last_ms[1 + k] += t;
+      c->last_launches[1 + k] += 1;
+    }
+  }
+  hipEventElapsedTime(&t, ef[0], ef[1]);
+  c->last_ms[4] = t;
+  c->last_launches[4] = 1;
   return GBV_OK;
 }
 
-int gbv_last_kernel_ms(gbv_ctx* c, float* out, int max) {
+int gbv_last_kernel_ms(gbv_ctx* c, float* out, int* launches, int max) {
   if (!c || !out) return 0;
   int k = std::min(max, 5);
-  for (int i = 0; i < k; ++i) out[i] = c->last_ms[i];
+  for (int i = 0; i < k; ++i) {
+    out[i] = c->last_ms[i];
+    if (launches) launches[i] = c->last_launches[i];
+  }
   return k;
 }
 

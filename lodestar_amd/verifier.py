@@ -220,11 +220,13 @@ class GpuBlsVerifier:
         _native.check(self._lib, self._ctx, rc)
         return StagedSameMessage(self, h, int(off[-1]))
 
-    def last_kernel_ms(self) -> List[float]:
-        """Device time of each kernel of the last staged verify: [hash, prepare, group_sum, pairing, fallback]."""
+    def last_kernel_ms(self):
+        """(total device ms, launches) of each kernel of the last staged verify:
+        [hash, prepare, group_sum, pairing, fallback]."""
         buf = (ctypes.c_float * 5)()
-        k = self._lib.gbv_last_kernel_ms(self._ctx, buf, 5)
-        return [buf[i] for i in range(k)]
+        cnt = (ctypes.c_int * 5)()
+        k = self._lib.gbv_last_kernel_ms(self._ctx, buf, cnt, 5)
+        return [buf[i] for i in range(k)], [cnt[i] for i in range(k)]
 
     # ---- IBlsVerifier (async) -------------------------------------------------------------------
     async def verify_signature_sets(self, sets: Sequence[ISignatureSet], opts: Optional[VerifySignatureOpts] = None) -> bool:
@@ -352,7 +354,8 @@ class GpuBlsVerifier:
         n = len(sks32)
         out = ctypes.create_string_buffer(max(48 * n, 1))
         _native.check(self._lib, self._ctx, self._lib.gbv_util_sk_to_pk(self._ctx, b"".join(sks32), n, out))
-        return [out.raw[48 * i:48 * i + 48] for i in range(n)]
+        raw = out.raw
+        return [raw[48 * i:48 * i + 48] for i in range(n)]
 
     def util_sign(self, sks32: Sequence[bytes], grp: Sequence[int], msgs32: Sequence[bytes]) -> List[bytes]:
         n = len(sks32)
@@ -360,13 +363,15 @@ class GpuBlsVerifier:
         g = (ctypes.c_uint32 * max(n, 1))(*grp)
         rc = self._lib.gbv_util_sign(self._ctx, b"".join(sks32), n, g, b"".join(msgs32), len(msgs32), out)
         _native.check(self._lib, self._ctx, rc)
-        return [out.raw[96 * i:96 * i + 96] for i in range(n)]
+        raw = out.raw
+        return [raw[96 * i:96 * i + 96] for i in range(n)]
 
     def util_hash_to_g2(self, msgs32: Sequence[bytes]) -> List[bytes]:
         n = len(msgs32)
         out = ctypes.create_string_buffer(max(192 * n, 1))
         _native.check(self._lib, self._ctx, self._lib.gbv_util_hash_to_g2(self._ctx, b"".join(msgs32), n, out))
-        return [out.raw[192 * i:192 * i + 192] for i in range(n)]
+        raw = out.raw
+        return [raw[192 * i:192 * i + 192] for i in range(n)]
 
 
 class StagedSameMessage:

@@ -1,5 +1,67 @@
-"""CPU baseline leg of bench.py -- TEST/BENCH INFRASTRUCTURE ONLY (see oracle/bls_oracle.py header)."""
+"""CPU baseline leg of bench.py -- TEST/BENCH INFRASTRUCTURE ONLY (see oracle/bls_oracle.py header).
+
+Times oracle/c/blsport.c (a C port of the same-message verification path; "CPU stand-in, not
+blst") through the reference pool's shape: availableParallelism()-1 worker
+threads (multithread/index.ts:46, poolSize.ts:7) pulling <=128-set chunks, on a bounded sample of
+the bench workload.  Never imported by the product package.
+"""
+import ctypes
+import os
+import subprocess
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "c", "libblsport.so")
 
 
-def measure_same_message(sample=None):
-    return None
+def load():
+    src = os.path.join(HERE, "c", "blsport.c")
+    if not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(src):
+        subprocess.check_call([os.path.join(HERE, "c", "build.sh")])
+    lib = ctypes.CDLL(LIB)
+    lib.port_verify_same_message_batch.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_char_p,
+                                                   ctypes.c_char_p, ctypes.c_char_p, ctypes.c_void_p, ctypes.c_uint64]
+    lib.port_g1_decompress.argtypes = [ctypes.c_char_p, ctypes.c_void_p]
+    return lib
+
+
+def pool_threads():
+    """availableParallelism() - 1, bounded by the CPU share the job may use."""
+    n = len(os.sched_getaffinity(0))
+    cap = os.environ.get("OMP_NUM_THREADS")
+    if cap and cap.isdigit():
+        n = min(n, int(cap))
+    return max(1, n - 1)
+
+
+def measure_same_message(call_off, idx, sigs96, msgs32, table_pk48, n_keys, target_sets=32768, threads=None):
+    """Verify the first calls of the workload (about `target_sets` sets) on the CPU pool shape.
+    table_pk48: compressed pubkeys of the key set (validator i uses key i mod n_keys).
+    Returns the `cpu_baseline` dict of the bench line."""
+    lib = load()
+    threads = threads or pool_threads()
+    call_off = np.asarray(call_off, dtype=np.uint32)
+    k = int(np.searchsorted(call_off, min(target_sets, int(call_off[-1])), side="left"))
+    k = max(1, min(k, len(call_off) - 1))
+    n = int(call_off[k])
+    # index2pubkey is already deserialized in the reference (PublicKey objects): not timed
+    aff = []
+    for pk in table_pk48:
+        out = ctypes.create_string_buffer(96)
+        assert lib.port_g1_decompress(pk, out) == 0
+        aff.append(out.raw)
+    aff = np.frombuffer(b"".join(aff), dtype=np.uint8).reshape(len(table_pk48), 96)
+    pk_aff = np.ascontiguousarray(aff[np.asarray(idx[:n]) % n_keys]).tobytes()
+    valid = (ctypes.c_uint8 * n)()
+    off = np.ascontiguousarray(call_off[:k + 1])
+    t = time.perf_counter()
+    lib.port_verify_same_message_batch(threads, k, off.ctypes.data, pk_aff, bytes(sigs96[:96 * n]), bytes(msgs32[:32 * k]),
+                                       valid, int.from_bytes(os.urandom(8), "little"))
+    dt = time.perf_counter() - t
+    ok = sum(valid)
+    return {"value": round(n / dt, 1), "unit": "sets/s", "cores": threads, "kind": "port",
+            "sample": "%d sets in %d same-message calls (first calls of the bench workload), %.2fs wall, "
+                      "%d/%d valid; oracle/c/blsport.c, C port not blst, %d worker threads" % (n, k, dt, ok, n, threads),
+            "all_valid": ok == n}
