@@ -20,6 +20,11 @@ GBV_HD Fp2 fp2_conj(const Fp2& a) { return Fp2{a.c0, fp_neg(a.c1)}; }
 // (a0 + a1 i)(1 + i) = (a0 - a1) + (a0 + a1) i
 GBV_HD Fp2 fp2_mul_xi(const Fp2& a) { return Fp2{fp_sub(a.c0, a.c1), fp_add(a.c0, a.c1)}; }
 
+#ifndef GBV_FP2_IMPL
+#define GBV_FP2_IMPL 0
+#endif
+
+#if GBV_FP2_IMPL == 0
 GBV_NI Fp2 fp2_mul(Fp2 a, Fp2 b) {
   Fp t0 = fp_mul_inl(a.c0, b.c0);
   Fp t1 = fp_mul_inl(a.c1, b.c1);
@@ -32,6 +37,36 @@ GBV_NI Fp2 fp2_sqr(Fp2 a) {
   Fp t1 = fp_mul_inl(a.c0, a.c1);
   return Fp2{t0, fp_dbl(t1)};
 }
+#elif GBV_FP2_IMPL == 2
+// Fully inlined Karatsuba (sequential Fp products): no calls anywhere in the point layer.
+GBV_HD Fp2 fp2_mul(const Fp2& a, const Fp2& b) {
+  Fp t0 = fp_mul_inl(a.c0, b.c0);
+  Fp t1 = fp_mul_inl(a.c1, b.c1);
+  Fp t2 = fp_mul_inl(fp_add(a.c0, a.c1), fp_add(b.c0, b.c1));
+  return Fp2{fp_sub(t0, t1), fp_sub(fp_sub(t2, t0), t1)};
+}
+
+GBV_HD Fp2 fp2_sqr(const Fp2& a) {
+  Fp t0 = fp_mul_inl(fp_add(a.c0, a.c1), fp_sub(a.c0, a.c1));
+  Fp t1 = fp_mul_inl(a.c0, a.c1);
+  return Fp2{t0, fp_dbl(t1)};
+}
+#else
+// Karatsuba over out-of-line Fp products: the Fp2 layer is inlined into its caller and only the
+// 70-VGPR Fp product is a call, so occupancy (not in-thread ILP) hides the mad latency.
+GBV_HD Fp2 fp2_mul(const Fp2& a, const Fp2& b) {
+  Fp t0 = fp_mul(a.c0, b.c0);
+  Fp t1 = fp_mul(a.c1, b.c1);
+  Fp t2 = fp_mul(fp_add(a.c0, a.c1), fp_add(b.c0, b.c1));
+  return Fp2{fp_sub(t0, t1), fp_sub(fp_sub(t2, t0), t1)};
+}
+
+GBV_HD Fp2 fp2_sqr(const Fp2& a) {
+  Fp t0 = fp_mul(fp_add(a.c0, a.c1), fp_sub(a.c0, a.c1));
+  Fp t1 = fp_mul(a.c0, a.c1);
+  return Fp2{t0, fp_dbl(t1)};
+}
+#endif
 
 
 GBV_HD Fp2 fp2_mul_fp(const Fp2& a, const Fp& s) { return Fp2{fp_mul(a.c0, s), fp_mul(a.c1, s)}; }

@@ -4,7 +4,7 @@
 //   build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -o tools/ubench_fp tools/ubench_fp.hip
 #include <hip/hip_runtime.h>
 #include <cstdio>
-#include "../lodestar_amd/csrc/fp2.h"
+#include "../lodestar_amd/csrc/curve.h"
 
 using namespace gbv;
 #define ITERS 256
@@ -49,6 +49,16 @@ __global__ void __launch_bounds__(256) k_fp2_mul_call(Fp* out) {
   out[blockIdx.x * blockDim.x + threadIdx.x] = fp_add(a.c0, a.c1);
 }
 
+// realistic G2 work: 64-bit scalar multiplication (63 dbl + ~32 madd, ~1.94k FME)
+__global__ void __launch_bounds__(256) k_g2_mul64(Fp* out) {
+  G2A q{Fp2{FP_ONE, FP_ONE}, Fp2{FP_B1, FP_ONE}};
+  q.x.c0.v[0] += threadIdx.x;
+  q.y.c1.v[1] += blockIdx.x;
+  uint64_t k = 0x9E3779B97F4A7C15ull * (blockIdx.x * blockDim.x + threadIdx.x + 1) | (1ull << 63);
+  G2J r = g2_mul_u64(q, k);
+  out[blockIdx.x * blockDim.x + threadIdx.x] = fp_add(r.x.c0, r.z.c1);
+}
+
 typedef void (*kfn)(Fp*);
 static void run(const char* name, kfn f, Fp* out, int blocks, int threads, double muls_per_thread) {
   hipEvent_t a, b;
@@ -66,6 +76,7 @@ static void run(const char* name, kfn f, Fp* out, int blocks, int threads, doubl
   double muls = (double)reps * blocks * threads * muls_per_thread;
   printf("%-14s blocks=%6d threads=%d  %8.3f ms  %7.1f G Fp-mul/s  %6.2f T u32-MAC/s (288 MAC/mul)\n", name, blocks, threads,
          ms, muls / (ms * 1e-3) / 1e9, muls * 288 / (ms * 1e-3) / 1e12);
+  fflush(stdout);
 }
 
 int main() {
@@ -79,6 +90,7 @@ int main() {
     run("fp_mul_inl x2", k_fp_mul_2, out, bl, 256, ITERS);
     run("fp_mul call", k_fp_mul_call, out, bl, 256, ITERS);
     run("fp2_mul call", k_fp2_mul_call, out, bl, 256, 3.0 * (ITERS / 3));
+    run("g2_mul_u64", k_g2_mul64, out, bl / 8, 256, 1940.0);
   }
   return 0;
 }
