@@ -10,6 +10,7 @@
 #pragma once
 #include "fp_types.h"
 #include "bls_constants.h"
+#include "fp_asm.h"
 
 namespace gbv {
 
@@ -43,29 +44,48 @@ GBV_HD Fp fp_sel(bool c, const Fp& a, const Fp& b) {
 }
 
 // Raw 384-bit helpers ------------------------------------------------------------------------
-// s = a - b, returns borrow (1 if a < b)
+// s = a - b, returns borrow (1 if a < b).  __builtin_subc/__builtin_addc lower to one
+// v_sub_co/v_subb_co (v_add_co/v_addc_co) carry chain: 12 VALU ops per 384-bit add or subtract.
 GBV_HD uint32_t raw_sub(Fp& s, const Fp& a, const Fp& b) {
-  uint32_t br = 0;
+  unsigned br = 0;
 #pragma unroll
-  for (int i = 0; i < 12; ++i) {
-    uint64_t d = (uint64_t)a.v[i] - b.v[i] - br;
-    s.v[i] = (uint32_t)d;
-    br = (uint32_t)(d >> 63);
-  }
+  for (int i = 0; i < 12; ++i) s.v[i] = __builtin_subc(a.v[i], b.v[i], br, &br);
   return br;
 }
 
 GBV_HD uint32_t raw_add(Fp& s, const Fp& a, const Fp& b) {
-  uint64_t c = 0;
+  unsigned c = 0;
 #pragma unroll
-  for (int i = 0; i < 12; ++i) {
-    c += (uint64_t)a.v[i] + b.v[i];
-    s.v[i] = (uint32_t)c;
-    c >>= 32;
-  }
-  return (uint32_t)c;
+  for (int i = 0; i < 12; ++i) s.v[i] = __builtin_addc(a.v[i], b.v[i], c, &c);
+  return c;
 }
 
+#if defined(__HIP_DEVICE_COMPILE__)
+// Device: each modular add/sub is one inline-asm carry chain (fp_asm.h).  Written this way the
+// chain links issue back to back; compiled from C the gfx950 backend pads every VCC hand-off.
+GBV_HD Fp fp_reduce_once(const Fp& x) {
+  Fp r;
+  const Fp p = P_RAW;
+  GBV_ASM_REDUCE_ONCE(r, x, p);
+  return r;
+}
+
+GBV_HD Fp fp_add(const Fp& a, const Fp& b) {
+  Fp s, r;
+  const Fp p = P_RAW;
+  GBV_ASM_ADD_MOD(s, r, a, b, p);
+  return r;
+}
+
+GBV_HD Fp fp_sub(const Fp& a, const Fp& b) {
+  Fp d, m;
+  const Fp p = P_RAW;
+  GBV_ASM_SUB_MOD(d, m, a, b, p);
+  return d;
+}
+
+GBV_HD Fp fp_neg(const Fp& a) { return fp_sub(fp_zero(), a); }
+#else
 // reduce x in [0, 2p) to [0, p)
 GBV_HD Fp fp_reduce_once(const Fp& x) {
   Fp t;
@@ -91,6 +111,7 @@ GBV_HD Fp fp_neg(const Fp& a) {
   raw_sub(d, P_RAW, a);
   return fp_sel(fp_is_zero(a), a, d);
 }
+#endif
 
 GBV_HD Fp fp_dbl(const Fp& a) { return fp_add(a, a); }
 

@@ -21,7 +21,7 @@ GBV_HD Fp2 fp2_conj(const Fp2& a) { return Fp2{a.c0, fp_neg(a.c1)}; }
 GBV_HD Fp2 fp2_mul_xi(const Fp2& a) { return Fp2{fp_sub(a.c0, a.c1), fp_add(a.c0, a.c1)}; }
 
 #ifndef GBV_FP2_IMPL
-#define GBV_FP2_IMPL 0
+#define GBV_FP2_IMPL 1
 #endif
 
 #if GBV_FP2_IMPL == 0

@@ -9,6 +9,9 @@
 #if defined(GBV_HOST_TEST)
 #define GBV_HD __host__ __device__ __forceinline__
 #define GBV_NI __host__ __device__ __noinline__ inline
+#elif defined(GBV_ALL_INLINE)
+#define GBV_HD __device__ __forceinline__
+#define GBV_NI __device__ __forceinline__
 #else
 #define GBV_HD __device__ __forceinline__
 #define GBV_NI __device__ __noinline__ inline

@@ -5,7 +5,7 @@
 namespace gbv {
 
 // ---- hashing ----------------------------------------------------------------------------------
-__global__ void __launch_bounds__(64) k_hash_msgs(const uint8_t* __restrict__ msgs32, uint32_t n, G2A* __restrict__ H) {
+__global__ void GBV_KERNEL_ATTR k_hash_msgs(const uint8_t* __restrict__ msgs32, uint32_t n, G2A* __restrict__ H) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint32_t w[8];
@@ -13,7 +13,7 @@ __global__ void __launch_bounds__(64) k_hash_msgs(const uint8_t* __restrict__ ms
   H[i] = hash_to_g2(w);
 }
 
-__global__ void __launch_bounds__(64) k_util_g2_out(uint32_t n, const G2A* __restrict__ H, uint8_t* __restrict__ out192) {
+__global__ void GBV_KERNEL_ATTR k_util_g2_out(uint32_t n, const G2A* __restrict__ H, uint8_t* __restrict__ out192) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint8_t* o = out192 + 192ull * i;

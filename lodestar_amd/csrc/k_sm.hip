@@ -5,7 +5,7 @@
 namespace gbv {
 
 // ---- same-message path ------------------------------------------------------------------------
-__global__ void __launch_bounds__(64) k_sm_prepare(uint32_t base, uint32_t n, const uint32_t* __restrict__ idx, const uint8_t* __restrict__ sig96,
+__global__ void GBV_KERNEL_ATTR k_sm_prepare(uint32_t base, uint32_t n, const uint32_t* __restrict__ idx, const uint8_t* __restrict__ sig96,
                                                    const G1A* __restrict__ table, const uint8_t* __restrict__ table_ok, uint32_t table_n,
                                                    Seed seed, uint32_t nonce, G2A* __restrict__ S_out, G2J* __restrict__ rS_out,
                                                    G1J* __restrict__ rP_out, uint8_t* __restrict__ status) {
@@ -26,7 +26,7 @@ __global__ void __launch_bounds__(64) k_sm_prepare(uint32_t base, uint32_t n, co
   rP_out[i] = g1_mul_u64(table[k], r);
 }
 
-__global__ void __launch_bounds__(64) k_sm_group_sum(uint32_t g0, uint32_t G, const uint32_t* __restrict__ grp_off, const uint8_t* __restrict__ status,
+__global__ void GBV_KERNEL_ATTR k_sm_group_sum(uint32_t g0, uint32_t G, const uint32_t* __restrict__ grp_off, const uint8_t* __restrict__ status,
                                                      const G2J* __restrict__ rS, const G1J* __restrict__ rP, G1A* __restrict__ Pg,
                                                      G2A* __restrict__ Sg, uint8_t* __restrict__ grp_state) {
   uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
@@ -54,7 +54,7 @@ __global__ void __launch_bounds__(64) k_sm_group_sum(uint32_t g0, uint32_t G, co
   grp_state[g] = ok ? GRP_PENDING : GRP_FALLBACK;
 }
 
-__global__ void __launch_bounds__(64) k_sm_group_pairing(uint32_t g0, uint32_t G, const uint32_t* __restrict__ grp_msg, const G1A* __restrict__ Pg,
+__global__ void GBV_KERNEL_ATTR k_sm_group_pairing(uint32_t g0, uint32_t G, const uint32_t* __restrict__ grp_msg, const G1A* __restrict__ Pg,
                                                          const G2A* __restrict__ Sg, const G2A* __restrict__ H,
                                                          uint8_t* __restrict__ grp_state, uint32_t* __restrict__ n_fallback) {
   uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
@@ -70,7 +70,7 @@ __global__ void __launch_bounds__(64) k_sm_group_pairing(uint32_t g0, uint32_t G
 }
 
 // valid[i] for every set; sets of failed chunks are verified one by one (2-pair check each).
-__global__ void __launch_bounds__(64) k_sm_fallback(uint32_t n, const uint32_t* __restrict__ set_grp, const uint32_t* __restrict__ grp_msg,
+__global__ void GBV_KERNEL_ATTR k_sm_fallback(uint32_t n, const uint32_t* __restrict__ set_grp, const uint32_t* __restrict__ grp_msg,
                                                     const uint8_t* __restrict__ grp_state, const uint8_t* __restrict__ status,
                                                     const uint32_t* __restrict__ idx, const G1A* __restrict__ table,
                                                     const G2A* __restrict__ S, const G2A* __restrict__ H, uint8_t* __restrict__ valid,

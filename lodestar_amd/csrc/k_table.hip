@@ -5,7 +5,7 @@
 namespace gbv {
 
 // ---- pubkey table -------------------------------------------------------------------------------
-__global__ void __launch_bounds__(64) k_pk_decompress(uint32_t n, const uint8_t* __restrict__ pk48, int validate,
+__global__ void GBV_KERNEL_ATTR k_pk_decompress(uint32_t n, const uint8_t* __restrict__ pk48, int validate,
                                                       G1A* __restrict__ table, uint8_t* __restrict__ table_ok,
                                                       uint8_t* __restrict__ status) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -64,7 +64,7 @@ __device__ inline void load_scalar_be32(uint32_t k[8], const uint8_t* b) {
   }
 }
 
-__global__ void __launch_bounds__(64) k_util_sk_to_pk(uint32_t n, const uint8_t* __restrict__ sk32, uint8_t* __restrict__ pk48) {
+__global__ void GBV_KERNEL_ATTR k_util_sk_to_pk(uint32_t n, const uint8_t* __restrict__ sk32, uint8_t* __restrict__ pk48) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint32_t k[8];
@@ -75,7 +75,7 @@ __global__ void __launch_bounds__(64) k_util_sk_to_pk(uint32_t n, const uint8_t*
   g1_compress(pk48 + 48ull * i, a, !fin);
 }
 
-__global__ void __launch_bounds__(64) k_util_sign(uint32_t n, const uint8_t* __restrict__ sk32, const uint32_t* __restrict__ grp,
+__global__ void GBV_KERNEL_ATTR k_util_sign(uint32_t n, const uint8_t* __restrict__ sk32, const uint32_t* __restrict__ grp,
                                                   const G2A* __restrict__ H, uint8_t* __restrict__ sig96) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;

@@ -5,7 +5,7 @@
 namespace gbv {
 
 // ---- distinct-message path (verifySignatureSets) ------------------------------------------------
-__global__ void __launch_bounds__(64) k_vs_prepare(uint32_t n, const uint32_t* __restrict__ set_idx_off, const uint32_t* __restrict__ idx,
+__global__ void GBV_KERNEL_ATTR k_vs_prepare(uint32_t n, const uint32_t* __restrict__ set_idx_off, const uint32_t* __restrict__ idx,
                                                    const uint8_t* __restrict__ raw_flag, const uint8_t* __restrict__ raw_pk48,
                                                    const uint8_t* __restrict__ msgs32, const uint8_t* __restrict__ sig, uint32_t sig_stride,
                                                    const uint32_t* __restrict__ sig_len, const G1A* __restrict__ table,
@@ -46,7 +46,7 @@ __global__ void __launch_bounds__(64) k_vs_prepare(uint32_t n, const uint32_t* _
   f_out[i] = miller_loop_1(rp, h);
 }
 
-__global__ void __launch_bounds__(64) k_vs_chunk(uint32_t C, const uint32_t* __restrict__ chunk_off, const uint8_t* __restrict__ status,
+__global__ void GBV_KERNEL_ATTR k_vs_chunk(uint32_t C, const uint32_t* __restrict__ chunk_off, const uint8_t* __restrict__ status,
                                                  const Fp12* __restrict__ f, const G2J* __restrict__ rS, uint8_t* __restrict__ chunk_valid) {
   uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;

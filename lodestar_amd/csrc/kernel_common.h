@@ -16,6 +16,11 @@
 #include "hash_to_curve.h"
 #include "pairing.h"
 
+// One wave per workgroup; the register budget is capped so that two waves share each SIMD
+// (measured on MI355X, tools/ubench_fp.hip: 2 waves/SIMD beat 1 and 3 for the point kernels,
+// whose live state -- a Jacobian G2 point plus its operand -- does not fit the 128 VGPRs of 4).
+#define GBV_KERNEL_ATTR __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
+
 namespace gbv {
 
 struct Seed { uint32_t w[8]; };
