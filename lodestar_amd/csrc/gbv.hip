@@ -50,8 +50,9 @@ struct gbv_ctx {
   uint32_t nonce = 0;
   hipStream_t stream2 = nullptr;
   std::vector<hipEvent_t> events;
-  float last_ms[5] = {};
-  int last_launches[5] = {};
+  static constexpr int NK = 7;  // hash, prepare, chunk_reduce, miller, seg_check, group_pairing, fallback
+  float last_ms[NK] = {};
+  int last_launches[NK] = {};
   bool closed = false;
 };
 
@@ -59,9 +60,12 @@ struct gbv_sm_batch {
   size_t n = 0, G = 0, n_calls = 0;
   std::vector<uint32_t> grp_off_host;
   uint32_t *idx = nullptr, *grp_off = nullptr, *grp_msg = nullptr, *set_grp = nullptr, *n_fallback = nullptr;
-  uint8_t *sig = nullptr, *msgs = nullptr, *status = nullptr, *grp_state = nullptr, *valid = nullptr;
-  G2A *H = nullptr, *S = nullptr, *Sg = nullptr;
-  G2J* rS = nullptr;
+  uint8_t *sig = nullptr, *msgs = nullptr, *status = nullptr, *grp_state = nullptr, *valid = nullptr, *seg_ok = nullptr;
+  uint8_t* seg_ok_host = nullptr;  // pinned
+  size_t seg_cap = 0;
+  G2A *H = nullptr, *S = nullptr;
+  G2J *rS = nullptr, *SgJ = nullptr;
+  Fp12* F = nullptr;
   G1J* rP = nullptr;
   G1A* Pg = nullptr;
 };
@@ -233,7 +237,8 @@ void gbv_sm_batch_destroy(gbv_ctx* c, gbv_sm_batch* b) {
   if (!b) return;
   hipFree(b->idx); hipFree(b->grp_off); hipFree(b->grp_msg); hipFree(b->set_grp); hipFree(b->n_fallback);
   hipFree(b->sig); hipFree(b->msgs); hipFree(b->status); hipFree(b->grp_state); hipFree(b->valid);
-  hipFree(b->H); hipFree(b->S); hipFree(b->Sg); hipFree(b->rS); hipFree(b->rP); hipFree(b->Pg);
+  hipFree(b->H); hipFree(b->S); hipFree(b->SgJ); hipFree(b->rS); hipFree(b->rP); hipFree(b->Pg);
+  hipFree(b->F); hipFree(b->seg_ok); hipHostFree(b->seg_ok_host);
   delete b;
 }
 
@@ -276,7 +281,10 @@ int gbv_sm_batch_create(gbv_ctx* c, size_t n_calls, const uint32_t* call_off, co
   chk(dalloc(&b->set_grp, n)); chk(dalloc(&b->msgs, 32 * n_calls)); chk(dalloc(&b->n_fallback, 1));
   chk(dalloc(&b->status, n)); chk(dalloc(&b->grp_state, G)); chk(dalloc(&b->valid, n));
   chk(dalloc(&b->H, n_calls)); chk(dalloc(&b->S, n)); chk(dalloc(&b->rS, n)); chk(dalloc(&b->rP, n));
-  chk(dalloc(&b->Pg, G)); chk(dalloc(&b->Sg, G));
+  chk(dalloc(&b->Pg, G)); chk(dalloc(&b->SgJ, G)); chk(dalloc(&b->F, G));
+  b->seg_cap = 64;
+  chk(dalloc(&b->seg_ok, b->seg_cap));
+  chk(hipHostMalloc((void**)&b->seg_ok_host, b->seg_cap, hipHostMallocDefault));
   if (e != hipSuccess) {
     gbv_sm_batch_destroy(c, b);
     return fail(c, GBV_E_OOM, std::string("hipMalloc: ") + hipGetErrorString(e));
@@ -298,9 +306,12 @@ int gbv_sm_batch_create(gbv_ctx* c, size_t n_calls, const uint32_t* call_off, co
   return GBV_OK;
 }
 
-// Stream B hashes the messages while stream A runs the throughput-bound per-set kernel
-// (k_sm_prepare); the per-chunk kernels then run once over all chunks (they are latency-bound:
-// one launch over every chunk costs the same wall time as a launch over a few).
+// Pipelined over segments of ~n/8 sets (cut at chunk boundaries):
+//   stream A: k_sm_prepare(segment s)                                  -- throughput-bound
+//   stream B: k_hash_msgs; per s: wait(prepare s) k_sm_chunk_reduce, k_sm_miller, k_sm_seg_check
+// so the latency-bound chunk kernels of segment s run beside the prepare of segment s+1.  Each
+// segment ends in ONE randomised multi-pairing check over all its chunks; only a failing segment
+// pays per-chunk checks (k_sm_group_pairing) and only a failing chunk pays per-set retries.
 int gbv_sm_batch_verify(gbv_ctx* c, gbv_sm_batch* b, uint8_t* valid) {
   if (!c || !b) return GBV_E_ARG;
   if (c->closed) return GBV_E_CLOSED;
@@ -309,82 +320,99 @@ int gbv_sm_batch_verify(gbv_ctx* c, gbv_sm_batch* b, uint8_t* valid) {
   Seed seed = fresh_seed();
   uint32_t nonce = c->nonce++;
   hipStream_t sa = c->stream, sb = c->stream2;
-  // sub-batches of ~SUB_SETS sets, cut at chunk boundaries
-  const size_t SUB_SETS = (size_t)1 << 31;  // one launch per kernel (see above)
+  const size_t max_seg = b->seg_cap;
+  const size_t n_seg = getenv("GBV_SEGMENTS") ? (size_t)std::max(1, atoi(getenv("GBV_SEGMENTS"))) : 1;
+  size_t sub_sets = std::max<size_t>((b->n + n_seg - 1) / n_seg, 32768);
   std::vector<uint32_t> gcut{0};
-  if (b->n > SUB_SETS) {
-    size_t next = SUB_SETS;
+  {
+    size_t next = sub_sets;
     for (size_t g = 1; g < b->G; ++g)
-      if (b->grp_off_host[g] >= next) {
+      if (b->grp_off_host[g] >= next && gcut.size() < max_seg) {
         gcut.push_back((uint32_t)g);
-        next = b->grp_off_host[g] + SUB_SETS;
+        next = b->grp_off_host[g] + sub_sets;
       }
   }
   gcut.push_back((uint32_t)b->G);
   size_t S = gcut.size() - 1;
-  if (c->events.size() < 8 * S + 8) {
+  // events: [0,1] hash; per segment 8 (prep, reduce, miller, check); then 2 group_pairing + 2 fallback
+  size_t need = 2 + 8 * S + 4;
+  if (c->events.size() < need) {
     size_t old = c->events.size();
-    c->events.resize(8 * S + 8);
-    for (size_t k = old; k < c->events.size(); ++k) hipEventCreate(&c->events[k]);
+    c->events.resize(need);
+    for (size_t k = old; k < need; ++k) hipEventCreate(&c->events[k]);
   }
   hipEvent_t* ev = c->events.data();
-  // ev layout: [0,1] hash; per s: [2+6s .. 7+6s] = prep start/end, sum start/end, pair start/end; then fallback
   HIP_CHECK(c, hipMemsetAsync(b->n_fallback, 0, 4, sb));
   hipEventRecord(ev[0], sb);
   launch_hash_msgs(LaunchCfg{blocks_for(b->n_calls), TPB, sb}, b->msgs, (uint32_t)b->n_calls, b->H);
   hipEventRecord(ev[1], sb);
   for (size_t s = 0; s < S; ++s) {
-    hipEvent_t* e = ev + 2 + 6 * s;
-    uint32_t s0 = b->grp_off_host[gcut[s]], s1 = b->grp_off_host[gcut[s + 1]];
+    hipEvent_t* e = ev + 2 + 8 * s;
+    uint32_t g0 = gcut[s], G = gcut[s + 1] - gcut[s];
+    uint32_t s0 = b->grp_off_host[g0], s1 = b->grp_off_host[gcut[s + 1]];
     hipEventRecord(e[0], sa);
     launch_sm_prepare(LaunchCfg{blocks_for(s1 - s0), TPB, sa}, s0, s1 - s0, b->idx, b->sig, c->table, c->table_ok,
                       (uint32_t)c->table_n, seed, nonce, b->S, b->rS, b->rP, b->status);
     hipEventRecord(e[1], sa);
     HIP_CHECK(c, hipStreamWaitEvent(sb, e[1], 0));
-    uint32_t g0 = gcut[s], G = gcut[s + 1] - gcut[s];
     hipEventRecord(e[2], sb);
-    launch_sm_group_sum(LaunchCfg{blocks_for(G), TPB, sb}, g0, G, b->grp_off, b->status, b->rS, b->rP, b->Pg, b->Sg, b->grp_state);
+    launch_sm_chunk_reduce(LaunchCfg{G, 64, sb}, g0, b->grp_off, b->status, b->rS, b->rP, b->Pg, b->SgJ, b->grp_state, b->n_fallback);
     hipEventRecord(e[3], sb);
     hipEventRecord(e[4], sb);
-    launch_sm_group_pairing(LaunchCfg{blocks_for(G), TPB, sb}, g0, G, b->grp_msg, b->Pg, b->Sg, b->H, b->grp_state, b->n_fallback);
+    launch_sm_miller(LaunchCfg{blocks_for(G), TPB, sb}, g0, G, b->grp_msg, b->grp_state, b->Pg, b->H, b->F);
     hipEventRecord(e[5], sb);
+    hipEventRecord(e[6], sb);
+    launch_sm_seg_check(LaunchCfg{1, 64, sb}, g0, G, b->grp_state, b->F, b->SgJ, b->seg_ok + s);
+    hipEventRecord(e[7], sb);
   }
   HIP_CHECK(c, hipGetLastError());
-  uint32_t nfb = 0;
-  HIP_CHECK(c, hipMemcpyAsync(&nfb, b->n_fallback, 4, hipMemcpyDeviceToHost, sb));
+  HIP_CHECK(c, hipMemcpyAsync(b->seg_ok_host, b->seg_ok, S, hipMemcpyDeviceToHost, sb));
   HIP_CHECK(c, hipStreamSynchronize(sb));
   HIP_CHECK(c, hipStreamSynchronize(sa));
-  hipEvent_t* ef = ev + 2 + 6 * S;
-  hipEventRecord(ef[0], sa);
+  hipEvent_t* ep = ev + 2 + 8 * S;
+  bool any_fail = false;
+  hipEventRecord(ep[0], sa);
+  for (size_t s = 0; s < S; ++s) {
+    if (b->seg_ok_host[s]) continue;
+    any_fail = true;
+    uint32_t g0 = gcut[s], G = gcut[s + 1] - gcut[s];
+    launch_sm_group_pairing(LaunchCfg{blocks_for(G), TPB, sa}, g0, G, b->grp_msg, b->Pg, b->SgJ, b->H, b->grp_state, b->n_fallback);
+  }
+  hipEventRecord(ep[1], sa);
+  uint32_t nfb = 0;
+  HIP_CHECK(c, hipMemcpyAsync(&nfb, b->n_fallback, 4, hipMemcpyDeviceToHost, sa));
+  HIP_CHECK(c, hipStreamSynchronize(sa));
+  hipEventRecord(ep[2], sa);
   launch_sm_fallback(LaunchCfg{blocks_for(b->n), TPB, sa}, (uint32_t)b->n, b->set_grp, b->grp_msg, b->grp_state, b->status, b->idx,
                      c->table, b->S, b->H, b->valid, nfb ? 1 : 0);
-  hipEventRecord(ef[1], sa);
+  hipEventRecord(ep[3], sa);
   HIP_CHECK(c, hipGetLastError());
   if (valid) HIP_CHECK(c, hipMemcpyAsync(valid, b->valid, b->n, hipMemcpyDeviceToHost, sa));
   HIP_CHECK(c, hipStreamSynchronize(sa));
   float t;
   for (auto& x : c->last_ms) x = 0.f;
   for (auto& x : c->last_launches) x = 0;
-  hipEventElapsedTime(&t, ev[0], ev[1]);
-  c->last_ms[0] = t;
-  c->last_launches[0] = 1;
-  for (size_t s = 0; s < S; ++s) {
-    hipEvent_t* e = ev + 2 + 6 * s;
-    for (int k = 0; k < 3; ++k) {
-      hipEventElapsedTime(&t, e[2 * k], e[2 * k + 1]);
-      c->last_ms[1 + k] += t;
-      c->last_launches[1 + k] += 1;
+  auto acc = [&](int k, hipEvent_t a0, hipEvent_t a1) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, a0, a1) == hipSuccess) {
+      c->last_ms[k] += ms;
+      c->last_launches[k] += 1;
     }
+  };
+  acc(0, ev[0], ev[1]);
+  for (size_t s = 0; s < S; ++s) {
+    hipEvent_t* e = ev + 2 + 8 * s;
+    for (int k = 0; k < 4; ++k) acc(1 + k, e[2 * k], e[2 * k + 1]);
   }
-  hipEventElapsedTime(&t, ef[0], ef[1]);
-  c->last_ms[4] = t;
-  c->last_launches[4] = 1;
+  if (any_fail) acc(5, ep[0], ep[1]);
+  acc(6, ep[2], ep[3]);
+  (void)t;
   return GBV_OK;
 }
 
 int gbv_last_kernel_ms(gbv_ctx* c, float* out, int* launches, int max) {
   if (!c || !out) return 0;
-  int k = std::min(max, 5);
+  int k = std::min(max, (int)gbv_ctx::NK);
   for (int i = 0; i < k; ++i) {
     out[i] = c->last_ms[i];
     if (launches) launches[i] = c->last_launches[i];

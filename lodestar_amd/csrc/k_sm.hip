@@ -26,47 +26,135 @@ __global__ void GBV_KERNEL_ATTR k_sm_prepare(uint32_t base, uint32_t n, const ui
   rP_out[i] = g1_mul_u64(table[k], r);
 }
 
-__global__ void GBV_KERNEL_ATTR k_sm_group_sum(uint32_t g0, uint32_t G, const uint32_t* __restrict__ grp_off, const uint8_t* __restrict__ status,
-                                                     const G2J* __restrict__ rS, const G1J* __restrict__ rP, G1A* __restrict__ Pg,
-                                                     G2A* __restrict__ Sg, uint8_t* __restrict__ grp_state) {
-  uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= G) return;
-  g += g0;
+// ---- wave-level helpers ---------------------------------------------------------------------
+__device__ inline Fp shfl_down_fp(const Fp& a, unsigned d) {
+  Fp r;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) r.v[i] = __shfl_down((unsigned)a.v[i], d, 64);
+  return r;
+}
+__device__ inline Fp2 shfl_down_fp(const Fp2& a, unsigned d) { return Fp2{shfl_down_fp(a.c0, d), shfl_down_fp(a.c1, d)}; }
+template <class F> __device__ inline Jac<F> shfl_down_jac(const Jac<F>& a, unsigned d) {
+  return Jac<F>{shfl_down_fp(a.x, d), shfl_down_fp(a.y, d), shfl_down_fp(a.z, d)};
+}
+__device__ inline Fp6 shfl_down_fp6(const Fp6& a, unsigned d) {
+  return Fp6{shfl_down_fp(a.c0, d), shfl_down_fp(a.c1, d), shfl_down_fp(a.c2, d)};
+}
+__device__ inline Fp12 shfl_down_fp12(const Fp12& a, unsigned d) { return Fp12{shfl_down_fp6(a.c0, d), shfl_down_fp6(a.c1, d)}; }
+
+GBV_NI G1J g1_add(G1J a, G1J b) { return jac_add(a, b); }
+GBV_NI G2J g2_add(G2J a, G2J b) { return jac_add(a, b); }
+
+// One wave per same-message chunk: P_g = sum r_i pk_i (G1, to affine) and S_g = sum r_i sig_i (G2,
+// Jacobian) by a cross-lane tree.  A chunk holding a malformed / non-subgroup signature goes
+// straight to the per-set retry, as aggregateWithRandomness throwing does (index.ts:406-409).
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
+k_sm_chunk_reduce(uint32_t g0, const uint32_t* __restrict__ grp_off, const uint8_t* __restrict__ status, const G2J* __restrict__ rS,
+                  const G1J* __restrict__ rP, G1A* __restrict__ Pg, G2J* __restrict__ SgJ, uint8_t* __restrict__ grp_state,
+                  uint32_t* __restrict__ n_fallback) {
+  uint32_t g = g0 + blockIdx.x;
+  unsigned lane = threadIdx.x;
   uint32_t b = grp_off[g], e = grp_off[g + 1];
-  bool bad = (b == e);
-  for (uint32_t i = b; i < e; ++i) bad |= status[i] != SET_OK;
-  if (bad) {
-    grp_state[g] = GRP_FALLBACK;
+  int bad = (b == e);
+  for (uint32_t i = b + lane; i < e; i += 64) bad |= status[i] != SET_OK;
+  if (__any(bad)) {
+    if (lane == 0) {
+      grp_state[g] = GRP_FALLBACK;
+      atomicAdd(n_fallback, 1u);
+    }
     return;
   }
-  G2J s = rS[b];
-  G1J p = rP[b];
-  for (uint32_t i = b + 1; i < e; ++i) {
-    s = jac_add(s, rS[i]);
-    p = jac_add(p, rP[i]);
+  G1J p = jac_infinity<Fp>();
+  G2J s = jac_infinity<Fp2>();
+  for (uint32_t i = b + lane; i < e; i += 64) {
+    p = g1_add(p, rP[i]);
+    s = g2_add(s, rS[i]);
   }
-  G1A pa;
-  G2A sa;
-  bool ok = jac_to_aff(pa, p);
-  ok &= jac_to_aff(sa, s);
-  Pg[g] = pa;
-  Sg[g] = sa;
-  grp_state[g] = ok ? GRP_PENDING : GRP_FALLBACK;
+  for (unsigned d = 32; d >= 1; d >>= 1) {
+    G1J po = shfl_down_jac(p, d);
+    G2J so = shfl_down_jac(s, d);
+    if (lane < d) {
+      p = g1_add(p, po);
+      s = g2_add(s, so);
+    }
+  }
+  if (lane == 0) {
+    G1A pa;
+    bool ok = jac_to_aff(pa, p);
+    Pg[g] = pa;
+    SgJ[g] = s;
+    grp_state[g] = ok ? GRP_PENDING : GRP_FALLBACK;
+    if (!ok) atomicAdd(n_fallback, 1u);
+  }
 }
 
-__global__ void GBV_KERNEL_ATTR k_sm_group_pairing(uint32_t g0, uint32_t G, const uint32_t* __restrict__ grp_msg, const G1A* __restrict__ Pg,
-                                                         const G2A* __restrict__ Sg, const G2A* __restrict__ H,
-                                                         uint8_t* __restrict__ grp_state, uint32_t* __restrict__ n_fallback) {
+// Miller value f_g = f_{|x|, H(m_g)}(P_g) of every pending chunk (one thread per chunk).
+__global__ void GBV_KERNEL_ATTR k_sm_miller(uint32_t g0, uint32_t G, const uint32_t* __restrict__ grp_msg, const uint8_t* __restrict__ grp_state,
+                                            const G1A* __restrict__ Pg, const G2A* __restrict__ H, Fp12* __restrict__ F) {
   uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= G) return;
   g += g0;
-  uint8_t st = grp_state[g];
-  if (st == GRP_PENDING) {
-    bool ok = pairing_check_2(Pg[g], false, H[grp_msg[g]], g1_neg_generator(), false, Sg[g]);
-    st = ok ? GRP_OK : GRP_FALLBACK;
-    grp_state[g] = st;
+  if (grp_state[g] != GRP_PENDING) return;
+  F[g] = miller_loop_1(Pg[g], H[grp_msg[g]]);
+}
+
+// One wave per segment of chunks: the randomised chunk equations of the whole segment are folded
+// into one check  prod_g e(P_g, H(m_g)) * e(-g1, sum_g S_g) == 1  (one shared final
+// exponentiation).  Every set carries its own random 64-bit scalar, so this is blst's
+// verifyMultipleAggregateSignatures over the segment's sets: it passes iff every chunk would
+// pass its own aggregate check, except with probability ~2^-64 (the same bound each chunk check
+// has).  Pass -> every pending chunk is valid; fail -> seg_ok = 0 and the host runs the
+// per-chunk checks (k_sm_group_pairing), then the per-set retry.
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
+k_sm_seg_check(uint32_t g0, uint32_t G, uint8_t* __restrict__ grp_state, const Fp12* __restrict__ F, const G2J* __restrict__ SgJ,
+               uint8_t* __restrict__ seg_ok) {
+  unsigned lane = threadIdx.x;
+  Fp12 f = fp12_one();
+  G2J s = jac_infinity<Fp2>();
+  int any = 0;
+  for (uint32_t g = g0 + lane; g < g0 + G; g += 64) {
+    if (grp_state[g] != GRP_PENDING) continue;
+    f = any ? fp12_mul(f, F[g]) : F[g];
+    s = g2_add(s, SgJ[g]);
+    any = 1;
   }
-  if (st == GRP_FALLBACK) atomicAdd(n_fallback, 1u);
+  for (unsigned d = 32; d >= 1; d >>= 1) {
+    Fp12 fo = shfl_down_fp12(f, d);
+    G2J so = shfl_down_jac(s, d);
+    int ao = __shfl_down(any, d, 64);
+    if (lane < d && ao) {
+      f = any ? fp12_mul(f, fo) : fo;
+      s = g2_add(s, so);
+      any = 1;
+    }
+  }
+  int ok = 1;
+  if (lane == 0 && any) {
+    G2A sa;
+    if (jac_to_aff(sa, s)) f = fp12_mul(f, miller_loop_1(g1_neg_generator(), sa));
+    ok = fp12_is_one(final_exponentiation(f)) ? 1 : 0;
+  }
+  ok = __shfl(ok, 0, 64);
+  if (lane == 0) seg_ok[0] = (uint8_t)ok;
+  if (!ok) return;
+  for (uint32_t g = g0 + lane; g < g0 + G; g += 64)
+    if (grp_state[g] == GRP_PENDING) grp_state[g] = GRP_OK;
+}
+
+// Failure path of a segment: each pending chunk on its own, e(P_g, H(m_g)) e(-g1, S_g) == 1
+// (verify(msg, aggPk, aggSig) of the chunk, maybeBatch.ts:34-38).
+__global__ void GBV_KERNEL_ATTR k_sm_group_pairing(uint32_t g0, uint32_t G, const uint32_t* __restrict__ grp_msg, const G1A* __restrict__ Pg,
+                                                   const G2J* __restrict__ SgJ, const G2A* __restrict__ H,
+                                                   uint8_t* __restrict__ grp_state, uint32_t* __restrict__ n_fallback) {
+  uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= G) return;
+  g += g0;
+  if (grp_state[g] != GRP_PENDING) return;
+  G2A sa;
+  bool ok = jac_to_aff(sa, SgJ[g]);
+  ok = ok && pairing_check_2(Pg[g], false, H[grp_msg[g]], g1_neg_generator(), false, sa);
+  grp_state[g] = ok ? GRP_OK : GRP_FALLBACK;
+  if (!ok) atomicAdd(n_fallback, 1u);
 }
 
 // valid[i] for every set; sets of failed chunks are verified one by one (2-pair check each).
@@ -98,14 +186,23 @@ void launch_sm_prepare(LaunchCfg c, uint32_t base, uint32_t n, const uint32_t* i
                      S_out, rS_out, rP_out, status);
   debug_sync(c.stream, "k_sm_prepare");
 }
-void launch_sm_group_sum(LaunchCfg c, uint32_t g0, uint32_t G, const uint32_t* grp_off, const uint8_t* status, const G2J* rS, const G1J* rP, G1A* Pg,
-                         G2A* Sg, uint8_t* grp_state) {
-  hipLaunchKernelGGL(k_sm_group_sum, dim3(c.blocks), dim3(c.threads), 0, c.stream, g0, G, grp_off, status, rS, rP, Pg, Sg, grp_state);
-  debug_sync(c.stream, "k_sm_group_sum");
+void launch_sm_chunk_reduce(LaunchCfg c, uint32_t g0, const uint32_t* grp_off, const uint8_t* status, const G2J* rS, const G1J* rP,
+                            G1A* Pg, G2J* SgJ, uint8_t* grp_state, uint32_t* n_fallback) {
+  hipLaunchKernelGGL(k_sm_chunk_reduce, dim3(c.blocks), dim3(64), 0, c.stream, g0, grp_off, status, rS, rP, Pg, SgJ, grp_state, n_fallback);
+  debug_sync(c.stream, "k_sm_chunk_reduce");
 }
-void launch_sm_group_pairing(LaunchCfg c, uint32_t g0, uint32_t G, const uint32_t* grp_msg, const G1A* Pg, const G2A* Sg, const G2A* H,
+void launch_sm_miller(LaunchCfg c, uint32_t g0, uint32_t G, const uint32_t* grp_msg, const uint8_t* grp_state, const G1A* Pg, const G2A* H,
+                      Fp12* F) {
+  hipLaunchKernelGGL(k_sm_miller, dim3(c.blocks), dim3(c.threads), 0, c.stream, g0, G, grp_msg, grp_state, Pg, H, F);
+  debug_sync(c.stream, "k_sm_miller");
+}
+void launch_sm_seg_check(LaunchCfg c, uint32_t g0, uint32_t G, uint8_t* grp_state, const Fp12* F, const G2J* SgJ, uint8_t* seg_ok) {
+  hipLaunchKernelGGL(k_sm_seg_check, dim3(1), dim3(64), 0, c.stream, g0, G, grp_state, F, SgJ, seg_ok);
+  debug_sync(c.stream, "k_sm_seg_check");
+}
+void launch_sm_group_pairing(LaunchCfg c, uint32_t g0, uint32_t G, const uint32_t* grp_msg, const G1A* Pg, const G2J* SgJ, const G2A* H,
                              uint8_t* grp_state, uint32_t* n_fallback) {
-  hipLaunchKernelGGL(k_sm_group_pairing, dim3(c.blocks), dim3(c.threads), 0, c.stream, g0, G, grp_msg, Pg, Sg, H, grp_state, n_fallback);
+  hipLaunchKernelGGL(k_sm_group_pairing, dim3(c.blocks), dim3(c.threads), 0, c.stream, g0, G, grp_msg, Pg, SgJ, H, grp_state, n_fallback);
   debug_sync(c.stream, "k_sm_group_pairing");
 }
 void launch_sm_fallback(LaunchCfg c, uint32_t n, const uint32_t* set_grp, const uint32_t* grp_msg, const uint8_t* grp_state,

@@ -6,8 +6,11 @@
 //   k_hash_msgs         hash_to_G2 inside blst verify / verifyMultipleAggregateSignatures
 //   k_sm_prepare        aggregateWithRandomness per set: Signature.fromBytes(sig, true) + r_i*pk, r_i*sig
 //                       (multithread/jobItem.ts:73)
-//   k_sm_group_sum      sum_i r_i pk_i, sum_i r_i sig_i per same-message chunk
-//   k_sm_group_pairing  verify(msg, aggPk, aggSig) of the chunk (worker.ts:29-107 -> maybeBatch n = 1)
+//   k_sm_chunk_reduce   sum_i r_i pk_i, sum_i r_i sig_i per same-message chunk (one wave per chunk)
+//   k_sm_miller         Miller value of (sum r_i pk_i, H(m)) per chunk
+//   k_sm_seg_check      one randomised multi-pairing check over a segment of chunks
+//   k_sm_group_pairing  verify(msg, aggPk, aggSig) of the chunk (worker.ts:29-107 -> maybeBatch n = 1),
+//                       only for chunks of a failing segment
 //   k_sm_fallback       retry each set individually (jobItem.ts:93-125)
 //   k_vs_prepare        per-set part of verifyMultipleAggregateSignatures (+ aggregatePublicKeys
 //                       of index lists, bls/utils.ts:5-20)

@@ -222,10 +222,10 @@ class GpuBlsVerifier:
 
     def last_kernel_ms(self):
         """(total device ms, launches) of each kernel of the last staged verify:
-        [hash, prepare, group_sum, pairing, fallback]."""
-        buf = (ctypes.c_float * 5)()
-        cnt = (ctypes.c_int * 5)()
-        k = self._lib.gbv_last_kernel_ms(self._ctx, buf, cnt, 5)
+        [hash, prepare, chunk_reduce, miller, seg_check, group_pairing, fallback]."""
+        buf = (ctypes.c_float * 7)()
+        cnt = (ctypes.c_int * 7)()
+        k = self._lib.gbv_last_kernel_ms(self._ctx, buf, cnt, 7)
         return [buf[i] for i in range(k)], [cnt[i] for i in range(k)]
 
     # ---- IBlsVerifier (async) -------------------------------------------------------------------

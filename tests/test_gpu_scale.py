@@ -1,0 +1,122 @@
+"""GPU parity at bench scale: many same-message calls across several pipeline segments, with invalid
+sets injected the way the reference tests build them (bls.test.ts:73 valid-point signature over
+another message, bls.test.ts:79 malformed bytes([10]*96)), plus the infinity signature.
+
+Expected booleans hold by construction: every set is signed on the GPU with its own interop key
+(util_sign, pinned bit-exactly by the K1 deposit signature in test_gpu_parity.py) except the
+injected ones.  A spot sample is re-checked against the CPU oracle.
+
+Run on an MI355X: python -m pytest tests -m gpu
+"""
+import hashlib
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+R_ORDER = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
+N_KEYS = 256
+N_TABLE = 4096
+
+
+def _sk(i):
+    d = hashlib.sha256(i.to_bytes(32, "little")).digest()
+    return (int.from_bytes(d, "little") % R_ORDER).to_bytes(32, "big")
+
+
+@pytest.fixture(scope="module")
+def world():
+    from lodestar_amd import GpuBlsVerifier
+    v = GpuBlsVerifier(0)
+    sks = [_sk(i) for i in range(N_KEYS)]
+    pks = v.util_sk_to_pk(sks)
+    assert v.add_pubkeys(0, pks, validate=True) == bytes(N_KEYS)
+    v.replicate_pubkeys(0, N_KEYS, N_KEYS, N_TABLE - N_KEYS)
+    yield v, sks, pks
+
+
+def _workload(v, sks, n_sets, seed):
+    rng = np.random.Generator(np.random.PCG64(seed))
+    sizes = []
+    while sum(sizes) < n_sets:
+        sizes.append(int(min(rng.integers(32, 129), n_sets - sum(sizes))))
+    off = np.zeros(len(sizes) + 1, dtype=np.uint32)
+    off[1:] = np.cumsum(sizes)
+    idx = rng.integers(0, N_TABLE, size=n_sets).astype(np.uint32)
+    grp = np.repeat(np.arange(len(sizes)), sizes)
+    msgs = [hashlib.sha256(b"gbv-scale" + seed.to_bytes(4, "little") + g.to_bytes(8, "little")).digest()
+            for g in range(len(sizes))]
+    sigs = v.util_sign([sks[int(i) % N_KEYS] for i in idx], grp.tolist(), msgs)
+    return off, idx, grp, sigs, msgs
+
+
+def _run_staged(v, off, idx, sigs, msgs):
+    st = v.stage_same_message(off, idx, b"".join(sigs), b"".join(msgs))
+    try:
+        return [b == 1 for b in st.verify(True)]
+    finally:
+        st.close()
+
+
+@pytest.fixture
+def segments(monkeypatch):
+    monkeypatch.setenv("GBV_SEGMENTS", "4")  # read by gbv_sm_batch_verify on every call
+
+
+def test_same_message_all_valid_multi_segment(world, segments):
+    v, sks, _ = world
+    off, idx, grp, sigs, msgs = _workload(v, sks, 80000, 11)
+    res = _run_staged(v, off, idx, sigs, msgs)
+    assert all(res)
+    ms, cnt = v.last_kernel_ms()
+    assert cnt[4] >= 2, "expected several pipeline segments"
+    assert cnt[5] == 0, "no segment should have failed"
+
+
+def test_same_message_injected_invalid(world, segments):
+    v, sks, _ = world
+    off, idx, grp, sigs, msgs = _workload(v, sks, 80000, 12)
+    n = len(sigs)
+    bad = {}
+    # wrong message: a valid G2 point that signs another call's message
+    for i in (5, 40001, 79990):
+        j = int(np.searchsorted(off, i, side="right"))  # a set in the next call
+        j = int(off[j]) if j < len(off) - 1 else 0
+        bad[i] = sigs[j] if grp[j] != grp[i] else sigs[(i + 200) % n]
+    bad[33333] = bytes([10]) * 96                  # malformed (no compression flag)
+    bad[50000] = bytes([0xC0]) + bytes(95)         # infinity signature
+    bad[60000] = sigs[60000][:95] + bytes([sigs[60000][95] ^ 1])  # flipped bit: off-curve or wrong point
+    sigs = list(sigs)
+    for i, s in bad.items():
+        sigs[i] = s
+    res = _run_staged(v, off, idx, sigs, msgs)
+    expected = [True] * n
+    for i in bad:
+        expected[i] = False
+    assert res == expected
+    ms, cnt = v.last_kernel_ms()
+    assert cnt[5] >= 1, "failing segments must have run the per-chunk checks"
+
+
+def test_same_message_spot_check_oracle(world):
+    """A few GPU-signed sets re-verified by the CPU oracle (pins util_sign beyond K1)."""
+    from oracle import bls_oracle as O
+    v, sks, pks = world
+    off, idx, grp, sigs, msgs = _workload(v, sks, 64, 13)
+    for i in (0, 17, 63):
+        k = int(idx[i]) % N_KEYS
+        assert O.set_is_valid(O.pubkey_from_bytes(pks[k]), msgs[int(grp[i])], sigs[i])
+
+
+def test_verify_sets_large_chunks(world):
+    """verifySignatureSets over 300 distinct-message sets (chunks of <=128) with one bad set."""
+    from lodestar_amd import SingleSignatureSet
+    v, sks, _ = world
+    msgs = [hashlib.sha256(b"vs" + i.to_bytes(4, "little")).digest() for i in range(300)]
+    idx = [(7 * i) % N_TABLE for i in range(300)]
+    sigs = v.util_sign([sks[i % N_KEYS] for i in idx], list(range(300)), msgs)
+    sets = [SingleSignatureSet(idx[i], msgs[i], sigs[i]) for i in range(300)]
+    assert v.verify_signature_sets_sync(sets) is True
+    sets[150] = SingleSignatureSet(idx[150], msgs[151], sigs[150])
+    assert v.verify_signature_sets_sync(sets) is False
