@@ -66,6 +66,9 @@ struct gbv_sm_batch {
   G2A *H = nullptr, *S = nullptr;
   G2J *rS = nullptr, *SgJ = nullptr;
   Fp12* F = nullptr;
+  Fp12* Fpart = nullptr;  // per 64-chunk block partials of a segment (reused segment after segment)
+  G2J* Spart = nullptr;
+  uint8_t* has = nullptr;
   G1J* rP = nullptr;
   G1A* Pg = nullptr;
 };
@@ -239,6 +242,7 @@ void gbv_sm_batch_destroy(gbv_ctx* c, gbv_sm_batch* b) {
   hipFree(b->sig); hipFree(b->msgs); hipFree(b->status); hipFree(b->grp_state); hipFree(b->valid);
   hipFree(b->H); hipFree(b->S); hipFree(b->SgJ); hipFree(b->rS); hipFree(b->rP); hipFree(b->Pg);
   hipFree(b->F); hipFree(b->seg_ok); hipHostFree(b->seg_ok_host);
+  hipFree(b->Fpart); hipFree(b->Spart); hipFree(b->has);
   delete b;
 }
 
@@ -282,6 +286,7 @@ int gbv_sm_batch_create(gbv_ctx* c, size_t n_calls, const uint32_t* call_off, co
   chk(dalloc(&b->status, n)); chk(dalloc(&b->grp_state, G)); chk(dalloc(&b->valid, n));
   chk(dalloc(&b->H, n_calls)); chk(dalloc(&b->S, n)); chk(dalloc(&b->rS, n)); chk(dalloc(&b->rP, n));
   chk(dalloc(&b->Pg, G)); chk(dalloc(&b->SgJ, G)); chk(dalloc(&b->F, G));
+  chk(dalloc(&b->Fpart, G / 64 + 1)); chk(dalloc(&b->Spart, G / 64 + 1)); chk(dalloc(&b->has, G / 64 + 1));
   b->seg_cap = 64;
   chk(dalloc(&b->seg_ok, b->seg_cap));
   chk(hipHostMalloc((void**)&b->seg_ok_host, b->seg_cap, hipHostMallocDefault));
@@ -359,10 +364,10 @@ int gbv_sm_batch_verify(gbv_ctx* c, gbv_sm_batch* b, uint8_t* valid) {
     launch_sm_chunk_reduce(LaunchCfg{G, 64, sb}, g0, b->grp_off, b->status, b->rS, b->rP, b->Pg, b->SgJ, b->grp_state, b->n_fallback);
     hipEventRecord(e[3], sb);
     hipEventRecord(e[4], sb);
-    launch_sm_miller(LaunchCfg{blocks_for(G), TPB, sb}, g0, G, b->grp_msg, b->grp_state, b->Pg, b->H, b->F);
+    launch_sm_miller(LaunchCfg{G, 64, sb}, g0, G, b->grp_msg, b->grp_state, b->Pg, b->H, b->F);
     hipEventRecord(e[5], sb);
     hipEventRecord(e[6], sb);
-    launch_sm_seg_check(LaunchCfg{1, 64, sb}, g0, G, b->grp_state, b->F, b->SgJ, b->seg_ok + s);
+    launch_sm_seg_check(LaunchCfg{1, 64, sb}, g0, G, b->grp_state, b->F, b->SgJ, b->Fpart, b->Spart, b->has, b->seg_ok + s);
     hipEventRecord(e[7], sb);
   }
   HIP_CHECK(c, hipGetLastError());
@@ -376,7 +381,7 @@ int gbv_sm_batch_verify(gbv_ctx* c, gbv_sm_batch* b, uint8_t* valid) {
     if (b->seg_ok_host[s]) continue;
     any_fail = true;
     uint32_t g0 = gcut[s], G = gcut[s + 1] - gcut[s];
-    launch_sm_group_pairing(LaunchCfg{blocks_for(G), TPB, sa}, g0, G, b->grp_msg, b->Pg, b->SgJ, b->H, b->grp_state, b->n_fallback);
+    launch_sm_group_pairing(LaunchCfg{G, 64, sa}, g0, G, b->grp_msg, b->Pg, b->SgJ, b->H, b->grp_state, b->n_fallback);
   }
   hipEventRecord(ep[1], sa);
   uint32_t nfb = 0;

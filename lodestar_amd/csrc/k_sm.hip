@@ -88,36 +88,16 @@ k_sm_chunk_reduce(uint32_t g0, const uint32_t* __restrict__ grp_off, const uint8
   }
 }
 
-// Miller value f_g = f_{|x|, H(m_g)}(P_g) of every pending chunk (one thread per chunk).
-__global__ void GBV_KERNEL_ATTR k_sm_miller(uint32_t g0, uint32_t G, const uint32_t* __restrict__ grp_msg, const uint8_t* __restrict__ grp_state,
-                                            const G1A* __restrict__ Pg, const G2A* __restrict__ H, Fp12* __restrict__ F) {
-  uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= G) return;
-  g += g0;
-  if (grp_state[g] != GRP_PENDING) return;
-  F[g] = miller_loop_1(Pg[g], H[grp_msg[g]]);
-}
-
-// One wave per segment of chunks: the randomised chunk equations of the whole segment are folded
-// into one check  prod_g e(P_g, H(m_g)) * e(-g1, sum_g S_g) == 1  (one shared final
-// exponentiation).  Every set carries its own random 64-bit scalar, so this is blst's
-// verifyMultipleAggregateSignatures over the segment's sets: it passes iff every chunk would
-// pass its own aggregate check, except with probability ~2^-64 (the same bound each chunk check
-// has).  Pass -> every pending chunk is valid; fail -> seg_ok = 0 and the host runs the
-// per-chunk checks (k_sm_group_pairing), then the per-set retry.
+// Per block of 64 chunks of a segment: product of the pending chunks' Miller values and sum of
+// their S_g, by a cross-lane tree.  has[blk] = 0 when the block holds no pending chunk.
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
-k_sm_seg_check(uint32_t g0, uint32_t G, uint8_t* __restrict__ grp_state, const Fp12* __restrict__ F, const G2J* __restrict__ SgJ,
-               uint8_t* __restrict__ seg_ok) {
+k_sm_seg_reduce(uint32_t g0, uint32_t G, const uint8_t* __restrict__ grp_state, const Fp12* __restrict__ F, const G2J* __restrict__ SgJ,
+                Fp12* __restrict__ Fpart, G2J* __restrict__ Spart, uint8_t* __restrict__ has) {
   unsigned lane = threadIdx.x;
-  Fp12 f = fp12_one();
-  G2J s = jac_infinity<Fp2>();
-  int any = 0;
-  for (uint32_t g = g0 + lane; g < g0 + G; g += 64) {
-    if (grp_state[g] != GRP_PENDING) continue;
-    f = any ? fp12_mul(f, F[g]) : F[g];
-    s = g2_add(s, SgJ[g]);
-    any = 1;
-  }
+  uint32_t g = g0 + blockIdx.x * 64 + lane;
+  int any = g < g0 + G && grp_state[g] == GRP_PENDING;
+  Fp12 f = any ? F[g] : fp12_one();
+  G2J s = any ? SgJ[g] : jac_infinity<Fp2>();
   for (unsigned d = 32; d >= 1; d >>= 1) {
     Fp12 fo = shfl_down_fp12(f, d);
     G2J so = shfl_down_jac(s, d);
@@ -128,33 +108,13 @@ k_sm_seg_check(uint32_t g0, uint32_t G, uint8_t* __restrict__ grp_state, const F
       any = 1;
     }
   }
-  int ok = 1;
-  if (lane == 0 && any) {
-    G2A sa;
-    if (jac_to_aff(sa, s)) f = fp12_mul(f, miller_loop_1(g1_neg_generator(), sa));
-    ok = fp12_is_one(final_exponentiation(f)) ? 1 : 0;
+  if (lane == 0) {
+    has[blockIdx.x] = (uint8_t)any;
+    if (any) {
+      Fpart[blockIdx.x] = f;
+      Spart[blockIdx.x] = s;
+    }
   }
-  ok = __shfl(ok, 0, 64);
-  if (lane == 0) seg_ok[0] = (uint8_t)ok;
-  if (!ok) return;
-  for (uint32_t g = g0 + lane; g < g0 + G; g += 64)
-    if (grp_state[g] == GRP_PENDING) grp_state[g] = GRP_OK;
-}
-
-// Failure path of a segment: each pending chunk on its own, e(P_g, H(m_g)) e(-g1, S_g) == 1
-// (verify(msg, aggPk, aggSig) of the chunk, maybeBatch.ts:34-38).
-__global__ void GBV_KERNEL_ATTR k_sm_group_pairing(uint32_t g0, uint32_t G, const uint32_t* __restrict__ grp_msg, const G1A* __restrict__ Pg,
-                                                   const G2J* __restrict__ SgJ, const G2A* __restrict__ H,
-                                                   uint8_t* __restrict__ grp_state, uint32_t* __restrict__ n_fallback) {
-  uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= G) return;
-  g += g0;
-  if (grp_state[g] != GRP_PENDING) return;
-  G2A sa;
-  bool ok = jac_to_aff(sa, SgJ[g]);
-  ok = ok && pairing_check_2(Pg[g], false, H[grp_msg[g]], g1_neg_generator(), false, sa);
-  grp_state[g] = ok ? GRP_OK : GRP_FALLBACK;
-  if (!ok) atomicAdd(n_fallback, 1u);
 }
 
 // valid[i] for every set; sets of failed chunks are verified one by one (2-pair check each).
@@ -191,19 +151,10 @@ void launch_sm_chunk_reduce(LaunchCfg c, uint32_t g0, const uint32_t* grp_off, c
   hipLaunchKernelGGL(k_sm_chunk_reduce, dim3(c.blocks), dim3(64), 0, c.stream, g0, grp_off, status, rS, rP, Pg, SgJ, grp_state, n_fallback);
   debug_sync(c.stream, "k_sm_chunk_reduce");
 }
-void launch_sm_miller(LaunchCfg c, uint32_t g0, uint32_t G, const uint32_t* grp_msg, const uint8_t* grp_state, const G1A* Pg, const G2A* H,
-                      Fp12* F) {
-  hipLaunchKernelGGL(k_sm_miller, dim3(c.blocks), dim3(c.threads), 0, c.stream, g0, G, grp_msg, grp_state, Pg, H, F);
-  debug_sync(c.stream, "k_sm_miller");
-}
-void launch_sm_seg_check(LaunchCfg c, uint32_t g0, uint32_t G, uint8_t* grp_state, const Fp12* F, const G2J* SgJ, uint8_t* seg_ok) {
-  hipLaunchKernelGGL(k_sm_seg_check, dim3(1), dim3(64), 0, c.stream, g0, G, grp_state, F, SgJ, seg_ok);
-  debug_sync(c.stream, "k_sm_seg_check");
-}
-void launch_sm_group_pairing(LaunchCfg c, uint32_t g0, uint32_t G, const uint32_t* grp_msg, const G1A* Pg, const G2J* SgJ, const G2A* H,
-                             uint8_t* grp_state, uint32_t* n_fallback) {
-  hipLaunchKernelGGL(k_sm_group_pairing, dim3(c.blocks), dim3(c.threads), 0, c.stream, g0, G, grp_msg, Pg, SgJ, H, grp_state, n_fallback);
-  debug_sync(c.stream, "k_sm_group_pairing");
+void launch_sm_seg_reduce(LaunchCfg c, uint32_t g0, uint32_t G, const uint8_t* grp_state, const Fp12* F, const G2J* SgJ, Fp12* Fpart,
+                          G2J* Spart, uint8_t* has) {
+  hipLaunchKernelGGL(k_sm_seg_reduce, dim3((G + 63) / 64), dim3(64), 0, c.stream, g0, G, grp_state, F, SgJ, Fpart, Spart, has);
+  debug_sync(c.stream, "k_sm_seg_reduce");
 }
 void launch_sm_fallback(LaunchCfg c, uint32_t n, const uint32_t* set_grp, const uint32_t* grp_msg, const uint8_t* grp_state,
                         const uint8_t* status, const uint32_t* idx, const G1A* table, const G2A* S, const G2A* H, uint8_t* valid,

@@ -18,7 +18,10 @@ void launch_sm_chunk_reduce(LaunchCfg c, uint32_t g0, const uint32_t* grp_off, c
                             G1A* Pg, G2J* SgJ, uint8_t* grp_state, uint32_t* n_fallback);
 void launch_sm_miller(LaunchCfg c, uint32_t g0, uint32_t G, const uint32_t* grp_msg, const uint8_t* grp_state, const G1A* Pg, const G2A* H,
                       Fp12* F);
-void launch_sm_seg_check(LaunchCfg c, uint32_t g0, uint32_t G, uint8_t* grp_state, const Fp12* F, const G2J* SgJ, uint8_t* seg_ok);
+void launch_sm_seg_reduce(LaunchCfg c, uint32_t g0, uint32_t G, const uint8_t* grp_state, const Fp12* F, const G2J* SgJ, Fp12* Fpart,
+                          G2J* Spart, uint8_t* has);
+void launch_sm_seg_check(LaunchCfg c, uint32_t g0, uint32_t G, uint8_t* grp_state, const Fp12* F, const G2J* SgJ, Fp12* Fpart, G2J* Spart,
+                         uint8_t* has, uint8_t* seg_ok);
 void launch_sm_group_pairing(LaunchCfg c, uint32_t g0, uint32_t G, const uint32_t* grp_msg, const G1A* Pg, const G2J* SgJ, const G2A* H,
                              uint8_t* grp_state, uint32_t* n_fallback);
 void launch_sm_fallback(LaunchCfg c, uint32_t n, const uint32_t* set_grp, const uint32_t* grp_msg, const uint8_t* grp_state,

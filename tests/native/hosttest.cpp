@@ -4,6 +4,8 @@
 #define GBV_HOST_TEST 1
 #include "../../lodestar_amd/csrc/pairing.h"
 #include "../../lodestar_amd/csrc/hash_to_curve.h"
+#include "../../lodestar_amd/csrc/coop.h"
+#include <vector>
 
 using namespace gbv;
 
@@ -90,5 +92,21 @@ int ht_verify(const uint8_t* pk48, const uint8_t* msg32, const uint8_t* sig, uin
   for (int i = 0; i < 8; ++i) w[i] = ((uint32_t)msg32[4*i] << 24) | ((uint32_t)msg32[4*i+1] << 16) | ((uint32_t)msg32[4*i+2] << 8) | msg32[4*i+3];
   G2A h = hash_to_g2(w);
   return pairing_check_2(pk, false, h, g1_neg_generator(), false, s);
+}
+// Wave-cooperative drivers (coop.h) run lane by lane: Miller loop over 1 or 2 pairs, then the
+// final exponentiation; out = the FE value (12 canonical Fp, tower order); returns is_one.
+int ht_coop_pairing(uint8_t* out, const uint8_t* p96, const uint8_t* q192, int npairs) {
+  std::vector<Fp> mem(coop::MILLER_WS + coop::FINAL_EXP_WS);
+  for (int j = 0; j < npairs; ++j) {
+    G1A P{load_mont(p96 + 96 * j), load_mont(p96 + 96 * j + 48)};
+    G2A Q{load_fp2(q192 + 192 * j), load_fp2(q192 + 192 * j + 96)};
+    coop::miller_load_pair(mem.data(), j, P, Q);
+  }
+  coop::miller_loop(mem.data(), npairs);
+  Fp* fe = mem.data() + coop::MILLER_WS;
+  coop::copy(fe + coop::E_F, mem.data() + coop::M_F, 12);
+  int ok = coop::final_exp_is_one(fe) ? 1 : 0;
+  for (int i = 0; i < 12; ++i) store_canon(out + 48 * i, fe[coop::E_C + i]);
+  return ok;
 }
 }

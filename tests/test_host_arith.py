@@ -153,3 +153,28 @@ def test_verify(lib):
     assert lib.ht_verify(pk, msg, sig, 96) == 1
     assert lib.ht_verify(pk, bytes(32), sig, 96) == 0
     assert lib.ht_verify(pk, msg, bytes([10]) * 96, 96) == 0
+
+
+def test_coop_pairing_value(lib):
+    """coop.h Miller loop + final exponentiation (host build, lanes run in sequence) = oracle."""
+    Pg = o.g1_mul(o.G1_GEN, 3)
+    Qg = o.g2_mul(o.G2_GEN, 5)
+    out = buf(576)
+    assert lib.ht_coop_pairing(out, be(Pg[0]) + be(Pg[1]), fp2b(Qg[0]) + fp2b(Qg[1]), 1) == 0
+    e = o.f12_pow(o.pairing(Pg, Qg), 3)
+    flat = [e[0][0], e[0][1], e[0][2], e[1][0], e[1][1], e[1][2]]
+    got = [b2fp2(out.raw[96 * i:96 * i + 96]) for i in range(6)]
+    assert got == flat
+
+
+def test_coop_two_pair_check(lib):
+    sk = o.interop_secret_key(5)
+    msg = bytes(range(1, 33))
+    pk, sig, H = o.sk_to_pk(sk), o.sign(sk, msg), o.hash_to_g2(msg)
+    ng = o.g1_neg(o.G1_GEN)
+    ps = be(pk[0]) + be(pk[1]) + be(ng[0]) + be(ng[1])
+    out = buf(576)
+    assert lib.ht_coop_pairing(out, ps, fp2b(H[0]) + fp2b(H[1]) + fp2b(sig[0]) + fp2b(sig[1]), 2) == 1
+    H2 = o.hash_to_g2(bytes(32))
+    assert lib.ht_coop_pairing(out, ps, fp2b(H2[0]) + fp2b(H2[1]) + fp2b(sig[0]) + fp2b(sig[1]), 2) == 0
+
