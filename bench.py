@@ -42,7 +42,7 @@ MAC_PER_FME = 300
 # (tools/ubench_int.hip, profiles/r01_ubench_int.txt); theoretical 256 CU x 4 SIMD x 16 lanes x 2.4 GHz = 39.3 T.
 PEAK_MAC_PER_S = 37.0e12
 # device kernels of one same-message verify, in gbv_last_kernel_ms order
-KERNELS = ["hash", "prepare", "chunk_reduce", "miller", "seg_check", "group_pairing", "fallback"]
+KERNELS = ["hash", "prepare", "chunk_finish", "miller", "seg_check", "group_pairing", "fallback"]
 
 
 def interop_sk_bytes(i):

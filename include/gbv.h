@@ -110,7 +110,7 @@ int gbv_sm_batch_verify(gbv_ctx* ctx, gbv_sm_batch* b, uint8_t* valid);
 void gbv_sm_batch_destroy(gbv_ctx* ctx, gbv_sm_batch* b);
 /* Device time (ms, summed over launches) and launch count of each kernel of the last
  * gbv_sm_batch_verify, measured with HIP events on the stream each kernel runs on:
- * [hash, prepare, chunk_reduce, miller, seg_check, group_pairing, fallback]; returns the number of
+ * [hash, prepare, chunk_finish, miller, seg_check, group_pairing, fallback]; returns the number of
  * entries written (at most 7). */
 int gbv_last_kernel_ms(gbv_ctx* ctx, float* ms_out, int* launches_out, int max);
 

@@ -22,17 +22,19 @@ namespace gbv {
 namespace coop {
 
 struct Term { uint8_t src, idx; int16_t coef; };
-struct Prod { uint16_t a0, an, b0, bn; };
-struct Part { uint16_t t0, tn, z; };
-struct Out { uint16_t t0, tn; uint8_t dst, idx; };
+// Fixed-size per-lane records (tools/gen_coop.py): product k = prods[20k .. 20k+19]
+// (A terms 0..9, B terms 10..19), partial j = parts[8j ..] -> Z[n_prod + j], output o = outs[8o ..]
+// -> operand out_dst[o], coordinate out_idx[o].  Padding terms have coef 0.
 struct Prog {
   uint8_t n_rounds, n_part, n_out;
   uint16_t round_end[6];
-  const Prod* prods;
-  const Part* parts;
-  const Out* outs;
-  const Term* terms;
+  const Term* prods;
+  const Term* parts;
+  const Term* outs;
+  const uint8_t* out_dst;
+  const uint8_t* out_idx;
 };
+constexpr int OPW = 10;
 enum { SRC_Z = 6, SRC_C = 7 };
 
 }  // namespace coop
@@ -46,62 +48,105 @@ namespace coop {
 constexpr int LANES = 64;
 constexpr int ZSLOTS = 128;
 
+// LDS-typed pointers so workspace accesses compile to ds_read/ds_write (a generic pointer would
+// give flat instructions, which wait on both the vector-memory and LDS counters).
+#if defined(GBV_HOST_TEST)
+typedef Fp LFp;
+#define GBV_LDS(p) (p)
+#else
+typedef __attribute__((address_space(3))) Fp LFp;
+#define GBV_LDS(p) ((LFp*)(p))
+#endif
+
+GBV_HD Fp ld(const LFp* p) {
+  Fp r;
+  r.v = p->v;
+  return r;
+}
+GBV_HD void st(LFp* p, const Fp& a) { p->v = a.v; }
+
 // Per-wave workspace: mem[] is LDS on the device; operand k of a program lives at mem + op[k].
 struct Ws {
-  Fp* mem;
+  LFp* mem;
   uint16_t op[6];
   uint16_t z;
 };
 
-GBV_HD Fp ws_get(const Ws& w, uint8_t src, uint8_t idx) {
-  if (src == SRC_C) return CONSTS[idx];
-  uint32_t base = src == SRC_Z ? w.z : w.op[src];
-  return w.mem[base + idx];
+GBV_HD Term term_of(uint32_t u) { return Term{(uint8_t)u, (uint8_t)(u >> 8), (int16_t)(u >> 16)}; }
+
+// Copy n (multiple of 4) terms into registers with 16-byte loads: one memory latency per record.
+template <int N> GBV_HD void load_terms(uint32_t (&r)[N], const Term* t) {
+  static_assert(N % 4 == 0, "records are whole 16-byte units");
+  const uint4* q = (const uint4*)t;
+#pragma unroll
+  for (int i = 0; i < N / 4; ++i) {
+    uint4 x = q[i];
+    r[4 * i] = x.x;
+    r[4 * i + 1] = x.y;
+    r[4 * i + 2] = x.z;
+    r[4 * i + 3] = x.w;
+  }
 }
 
-// sum of coef * value over a term list (coefficients are small integers: double-and-add)
-GBV_HD Fp lin_eval(const Ws& w, const Term* t, int n) {
-  Fp acc = fp_zero();
-  for (int i = 0; i < n; ++i) {
-    Term tt = t[i];
-    Fp v = ws_get(w, tt.src, tt.idx);
-    int c = tt.coef;
-    bool neg = c < 0;
-    if (neg) c = -c;
-    Fp s;
-    if (c == 1) {
-      s = v;
-    } else {
-      bool have = false;
-      while (c) {
-        if (c & 1) {
-          s = have ? fp_add(s, v) : v;
-          have = true;
-        }
-        c >>= 1;
-        if (c) v = fp_dbl(v);
-      }
+GBV_HD Fp ws_get(const Ws& w, Term t) {
+  if (t.src == SRC_C) return CONSTS[t.idx];
+  uint32_t base = t.src == SRC_Z ? w.z : t.src == 0 ? w.op[0] : t.src == 1 ? w.op[1] : t.src == 2 ? w.op[2]
+                 : t.src == 3 ? w.op[3] : t.src == 4 ? w.op[4] : w.op[5];
+  return ld(w.mem + base + t.idx);
+}
+
+// c * v for a small integer c >= 2 (rare: scaled terms of the doubling/cyclotomic formulas)
+GBV_NI Fp scale_small(Fp v, int c) {
+  Fp s = v;
+  bool have = false;
+  while (c) {
+    if (c & 1) {
+      s = have ? fp_add(s, v) : v;
+      have = true;
     }
-    acc = i == 0 ? (neg ? fp_neg(s) : s) : (neg ? fp_sub(acc, s) : fp_add(acc, s));
+    c >>= 1;
+    if (c) v = fp_dbl(v);
+  }
+  return s;
+}
+
+// p - s for s < p, without reduction (s = 0 gives p, which every consumer below accepts: it only
+// ever enters fp_add next to a value < p).
+GBV_HD Fp fp_neg_raw(const Fp& s) {
+  Fp d;
+  raw_sub(d, P_RAW, s);
+  return d;
+}
+
+// sum of coef * value over N packed terms: all N operand loads are issued first, then each term is
+// conditionally negated / zeroed with selects and added -- no divergent branch per term (a lane's
+// term count and signs differ from its neighbours').
+template <int N> GBV_HD Fp lin_eval(const Ws& w, const uint32_t* r) {
+  Fp v[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] = ws_get(w, term_of(r[i]));
+  Fp acc = fp_zero();
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    int c = (int16_t)(r[i] >> 16);
+    int m = c < 0 ? -c : c;
+    Fp s = v[i];
+    if (m > 1) s = scale_small(s, m);  // rare (doubling / cyclotomic constants)
+    Fp t = fp_sel(c < 0, fp_neg_raw(s), s);
+    t = fp_sel(c == 0, fp_zero(), t);
+    acc = fp_add(acc, t);
   }
   return acc;
 }
 
-GBV_HD void prod_lane(const Prog& P, int k, const Ws& w) {
-  Prod pr = P.prods[k];
-  Fp x = lin_eval(w, P.terms + pr.a0, pr.an);
-  Fp y = lin_eval(w, P.terms + pr.b0, pr.bn);
-  w.mem[w.z + k] = fp_mul(x, y);
+GBV_HD void prod_lane(const uint32_t (&r)[2 * OPW], int k, const Ws& w) {
+  Fp x = lin_eval<OPW>(w, r);
+  Fp y = lin_eval<OPW>(w, r + OPW);
+  st(w.mem + w.z + k, fp_mul(x, y));
 }
 
-GBV_HD void part_lane(const Prog& P, int j, const Ws& w) {
-  Part pt = P.parts[j];
-  w.mem[w.z + pt.z] = lin_eval(w, P.terms + pt.t0, pt.tn);
-}
-
-GBV_HD Fp out_lane(const Prog& P, int o, const Ws& w) {
-  Out ou = P.outs[o];
-  return lin_eval(w, P.terms + ou.t0, ou.tn);
+GBV_HD void part_lane(const Prog& P, const uint32_t (&r)[8], int j, const Ws& w) {
+  st(w.mem + w.z + P.round_end[P.n_rounds - 1] + j, lin_eval<8>(w, r));
 }
 
 #if defined(GBV_HOST_TEST)
@@ -111,14 +156,24 @@ inline void barrier() {}
 // Host: the lanes of each phase run one after another.
 inline void run(const Prog& P, const Ws& w) {
   int p0 = 0;
+  uint32_t rec[2 * OPW], r8[8];
   for (int r = 0; r < P.n_rounds; ++r) {
-    for (int k = p0; k < P.round_end[r]; ++k) prod_lane(P, k, w);
+    for (int k = p0; k < P.round_end[r]; ++k) {
+      load_terms(rec, P.prods + 2 * OPW * k);
+      prod_lane(rec, k, w);
+    }
     p0 = P.round_end[r];
   }
-  for (int j = 0; j < P.n_part; ++j) part_lane(P, j, w);
+  for (int j = 0; j < P.n_part; ++j) {
+    load_terms(r8, P.parts + 8 * j);
+    part_lane(P, r8, j, w);
+  }
   Fp o[LANES];
-  for (int k = 0; k < P.n_out; ++k) o[k] = out_lane(P, k, w);
-  for (int k = 0; k < P.n_out; ++k) w.mem[w.op[P.outs[k].dst] + P.outs[k].idx] = o[k];
+  for (int k = 0; k < P.n_out; ++k) {
+    load_terms(r8, P.outs + 8 * k);
+    o[k] = lin_eval<8>(w, r8);
+  }
+  for (int k = 0; k < P.n_out; ++k) st(w.mem + w.op[P.out_dst[k]] + P.out_idx[k], o[k]);
 }
 #define COOP_LANES(l) for (unsigned l = 0; l < (unsigned)LANES; ++l)
 #define COOP_LANE0 if (true)
@@ -126,41 +181,57 @@ inline void run(const Prog& P, const Ws& w) {
 __device__ inline unsigned lane_id() { return threadIdx.x; }
 __device__ inline void barrier() { __syncthreads(); }
 
-__device__ inline void run(const Prog& P, const Ws& w) {
+// All of a lane's records for this program are fetched up front (one memory latency), the next
+// round's while the current round computes.
+__device__ __noinline__ void run_ni(const Prog* PP, LFp* mem, uint32_t op01, uint32_t op23, uint32_t op45, uint32_t z) {
+  const Prog& P = *PP;
+  const Ws w{mem, {(uint16_t)op01, (uint16_t)(op01 >> 16), (uint16_t)op23, (uint16_t)(op23 >> 16), (uint16_t)op45, (uint16_t)(op45 >> 16)},
+             (uint16_t)z};
   const int lane = (int)threadIdx.x;
+  uint32_t rec[2 * OPW], rpart[8], rout[8];
+  bool have_part = lane < P.n_part, have_out = lane < P.n_out;
   int p0 = 0;
+  if (lane < P.round_end[0]) load_terms(rec, P.prods + 2 * OPW * lane);
+  if (have_part) load_terms(rpart, P.parts + 8 * lane);
+  if (have_out) load_terms(rout, P.outs + 8 * lane);
   for (int r = 0; r < P.n_rounds; ++r) {
     int p1 = P.round_end[r];
-    if (p0 + lane < p1) prod_lane(P, p0 + lane, w);  // every round has <= 64 products
+    if (p0 + lane < p1) prod_lane(rec, p0 + lane, w);  // every round has <= 64 products
+    if (r + 1 < P.n_rounds && p1 + lane < P.round_end[r + 1]) load_terms(rec, P.prods + 2 * OPW * (p1 + lane));
     p0 = p1;
     __syncthreads();
   }
-  if (lane < P.n_part) {
-    part_lane(P, lane, w);
-  }
+  if (have_part) part_lane(P, rpart, lane, w);
   if (P.n_part) __syncthreads();
   Fp o;
-  bool have = lane < P.n_out;
-  if (have) o = out_lane(P, lane, w);
+  if (have_out) o = lin_eval<8>(w, rout);
   __syncthreads();
-  if (have) w.mem[w.op[P.outs[lane].dst] + P.outs[lane].idx] = o;
+  if (have_out) st(w.mem + w.op[P.out_dst[lane]] + P.out_idx[lane], o);
   __syncthreads();
+}
+// One out-of-line copy of the interpreter serves every call site (the drivers make hundreds).
+__device__ inline void run(const Prog& P, const Ws& w) {
+  run_ni(&P, w.mem, w.op[0] | ((uint32_t)w.op[1] << 16), w.op[2] | ((uint32_t)w.op[3] << 16), w.op[4] | ((uint32_t)w.op[5] << 16), w.z);
 }
 #define COOP_LANES(l) for (unsigned l = threadIdx.x; l == threadIdx.x; l = ~0u)
 #define COOP_LANE0 if (threadIdx.x == 0)
 #endif
 
 // ---- operand helpers (lane-parallel, end with a barrier) ------------------------------------
-GBV_HD void set_one12(Fp* f) {
-  COOP_LANES(l) if (l < 12) f[l] = l == 0 ? FP_ONE : fp_zero();
+GBV_HD void set_one12(Fp* fg) {
+  LFp* f = GBV_LDS(fg);
+  COOP_LANES(l) if (l < 12) st(f + l, l == 0 ? FP_ONE : fp_zero());
   barrier();
 }
-GBV_HD void copy(Fp* dst, const Fp* src, unsigned n) {
-  COOP_LANES(l) if (l < n) dst[l] = src[l];
+GBV_HD void copy(Fp* dstg, const Fp* srcg, unsigned n) {
+  LFp* dst = GBV_LDS(dstg);
+  const LFp* src = GBV_LDS(srcg);
+  COOP_LANES(l) if (l < n) st(dst + l, ld(src + l));
   barrier();
 }
-GBV_HD void conj12(Fp* f) {  // negate the w-odd half (coordinates 6..11)
-  COOP_LANES(l) if (l >= 6 && l < 12) f[l] = fp_neg(f[l]);
+GBV_HD void conj12(Fp* fg) {  // negate the w-odd half (coordinates 6..11)
+  LFp* f = GBV_LDS(fg);
+  COOP_LANES(l) if (l >= 6 && l < 12) st(f + l, fp_neg(ld(f + l)));
   barrier();
 }
 GBV_HD bool is_one12(const Fp* f) {
@@ -169,8 +240,8 @@ GBV_HD bool is_one12(const Fp* f) {
   return ok;
 }
 
-GBV_HD Ws ws2(Fp* mem, uint16_t z, uint16_t a, uint16_t b) { return Ws{mem, {a, b, 0, 0, 0, 0}, z}; }
-GBV_HD Ws ws3(Fp* mem, uint16_t z, uint16_t a, uint16_t b, uint16_t c) { return Ws{mem, {a, b, c, 0, 0, 0}, z}; }
+GBV_HD Ws ws2(Fp* mem, uint16_t z, uint16_t a, uint16_t b) { return Ws{GBV_LDS(mem), {a, b, 0, 0, 0, 0}, z}; }
+GBV_HD Ws ws3(Fp* mem, uint16_t z, uint16_t a, uint16_t b, uint16_t c) { return Ws{GBV_LDS(mem), {a, b, c, 0, 0, 0}, z}; }
 
 GBV_HD void mul12(Fp* mem, uint16_t z, uint16_t a, uint16_t b, uint16_t c) { run(FP12_MUL, ws3(mem, z, a, b, c)); }
 GBV_HD void cyc_sqr12(Fp* mem, uint16_t z, uint16_t a, uint16_t c) { run(FP12_CYC_SQR, ws2(mem, z, a, c)); }
@@ -184,7 +255,7 @@ constexpr int MILLER_WS = M_Z + ZSLOTS;
 
 // Load pair j: P affine G1, Q affine G2 (neither infinity).  Lane-parallel, ends with a barrier.
 GBV_HD void miller_load_pair(Fp* mem, int j, const G1A& P, const G2A& Q) {
-  Fp* b = mem + M_PAIR + 12 * j;
+  LFp* b = GBV_LDS(mem + M_PAIR + 12 * j);
   COOP_LANES(l) {
     if (l < 12) {
       Fp v;
@@ -202,7 +273,7 @@ GBV_HD void miller_load_pair(Fp* mem, int j, const G1A& P, const G2A& Q) {
         case 10: v = fp_neg(P.x); break;
         default: v = P.y; break;
       }
-      b[l] = v;
+      st(b + l, v);
     }
   }
   barrier();
@@ -215,13 +286,13 @@ GBV_HD void miller_loop(Fp* mem, int npairs) {
     if (i != 62) run(FP12_SQR, ws2(mem, M_Z, M_F, M_F));
     for (int j = 0; j < npairs; ++j) {
       uint16_t t = M_PAIR + 12 * j;
-      run(G2_DBL_STEP, Ws{mem, {t, (uint16_t)(t + 10), t, M_L, 0, 0}, M_Z});
+      run(G2_DBL_STEP, Ws{GBV_LDS(mem), {t, (uint16_t)(t + 10), t, M_L, 0, 0}, M_Z});
       run(FP12_MUL_LINE, ws3(mem, M_Z, M_F, M_L, M_F));
     }
     if ((X_ABS >> i) & 1ull) {
       for (int j = 0; j < npairs; ++j) {
         uint16_t t = M_PAIR + 12 * j;
-        run(G2_ADD_STEP, Ws{mem, {t, (uint16_t)(t + 6), (uint16_t)(t + 10), t, M_L, 0}, M_Z});
+        run(G2_ADD_STEP, Ws{GBV_LDS(mem), {t, (uint16_t)(t + 6), (uint16_t)(t + 10), t, M_L, 0}, M_Z});
         run(FP12_MUL_LINE, ws3(mem, M_Z, M_F, M_L, M_F));
       }
     }

@@ -48,7 +48,7 @@ struct gbv_ctx {
   size_t table_n = 0;
   std::string err;
   uint32_t nonce = 0;
-  hipStream_t stream2 = nullptr;
+  hipStream_t stream2 = nullptr, stream3 = nullptr;
   std::vector<hipEvent_t> events;
   static constexpr int NK = 7;  // hash, prepare, chunk_reduce, miller, seg_check, group_pairing, fallback
   float last_ms[NK] = {};
@@ -70,7 +70,7 @@ struct gbv_sm_batch {
   G2J* Spart = nullptr;
   uint8_t* has = nullptr;
   G1J* rP = nullptr;
-  G1A* Pg = nullptr;
+  G1J* PgJ = nullptr;
 };
 
 static int fail(gbv_ctx* c, int code, const std::string& msg) {
@@ -123,8 +123,11 @@ int gbv_init(int device, gbv_ctx** out) {
     delete c;
     return GBV_E_DEVICE;
   }
-  if (hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess) {
+  if (hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->stream3, hipStreamNonBlocking) != hipSuccess) {
     hipStreamDestroy(c->stream);
+    if (c->stream2) hipStreamDestroy(c->stream2);
+  if (c->stream3) hipStreamDestroy(c->stream3);
     delete c;
     return GBV_E_DEVICE;
   }
@@ -139,9 +142,11 @@ void gbv_destroy(gbv_ctx* c) {
   hipFree(c->table);
   hipFree(c->table_ok);
   if (c->stream2) hipStreamSynchronize(c->stream2);
+  if (c->stream3) hipStreamSynchronize(c->stream3);
   for (auto& e : c->events) hipEventDestroy(e);
   if (c->stream) hipStreamDestroy(c->stream);
   if (c->stream2) hipStreamDestroy(c->stream2);
+  if (c->stream3) hipStreamDestroy(c->stream3);
   delete c;
 }
 
@@ -240,7 +245,7 @@ void gbv_sm_batch_destroy(gbv_ctx* c, gbv_sm_batch* b) {
   if (!b) return;
   hipFree(b->idx); hipFree(b->grp_off); hipFree(b->grp_msg); hipFree(b->set_grp); hipFree(b->n_fallback);
   hipFree(b->sig); hipFree(b->msgs); hipFree(b->status); hipFree(b->grp_state); hipFree(b->valid);
-  hipFree(b->H); hipFree(b->S); hipFree(b->SgJ); hipFree(b->rS); hipFree(b->rP); hipFree(b->Pg);
+  hipFree(b->H); hipFree(b->S); hipFree(b->SgJ); hipFree(b->rS); hipFree(b->rP); hipFree(b->PgJ);
   hipFree(b->F); hipFree(b->seg_ok); hipHostFree(b->seg_ok_host);
   hipFree(b->Fpart); hipFree(b->Spart); hipFree(b->has);
   delete b;
@@ -285,8 +290,10 @@ int gbv_sm_batch_create(gbv_ctx* c, size_t n_calls, const uint32_t* call_off, co
   chk(dalloc(&b->set_grp, n)); chk(dalloc(&b->msgs, 32 * n_calls)); chk(dalloc(&b->n_fallback, 1));
   chk(dalloc(&b->status, n)); chk(dalloc(&b->grp_state, G)); chk(dalloc(&b->valid, n));
   chk(dalloc(&b->H, n_calls)); chk(dalloc(&b->S, n)); chk(dalloc(&b->rS, n)); chk(dalloc(&b->rP, n));
-  chk(dalloc(&b->Pg, G)); chk(dalloc(&b->SgJ, G)); chk(dalloc(&b->F, G));
-  chk(dalloc(&b->Fpart, G / 64 + 1)); chk(dalloc(&b->Spart, G / 64 + 1)); chk(dalloc(&b->has, G / 64 + 1));
+  chk(dalloc(&b->PgJ, G)); chk(dalloc(&b->SgJ, G)); chk(dalloc(&b->F, G));
+  // block partials: one region per segment stream (two segments' reductions can be in flight)
+  chk(dalloc(&b->Fpart, 2 * (G / 64 + G / 4096 + 4))); chk(dalloc(&b->Spart, 2 * (G / 64 + G / 4096 + 4)));
+  chk(dalloc(&b->has, 2 * (G / 64 + G / 4096 + 4)));
   b->seg_cap = 64;
   chk(dalloc(&b->seg_ok, b->seg_cap));
   chk(hipHostMalloc((void**)&b->seg_ok_host, b->seg_cap, hipHostMallocDefault));
@@ -311,12 +318,14 @@ int gbv_sm_batch_create(gbv_ctx* c, size_t n_calls, const uint32_t* call_off, co
   return GBV_OK;
 }
 
-// Pipelined over segments of ~n/8 sets (cut at chunk boundaries):
-//   stream A: k_sm_prepare(segment s)                                  -- throughput-bound
-//   stream B: k_hash_msgs; per s: wait(prepare s) k_sm_chunk_reduce, k_sm_miller, k_sm_seg_check
-// so the latency-bound chunk kernels of segment s run beside the prepare of segment s+1.  Each
-// segment ends in ONE randomised multi-pairing check over all its chunks; only a failing segment
-// pays per-chunk checks (k_sm_group_pairing) and only a failing chunk pays per-set retries.
+// Pipelined over segments of ~n/S sets (cut at chunk boundaries):
+//   stream A      : k_sm_prepare(segment s)  -- throughput-bound, also forms per-wave chunk sums
+//   streams B0/B1 : (segment s alternates) wait(prepare s), k_sm_chunk_finish, k_sm_miller,
+//                   k_sm_seg_reduce + k_sm_seg_check
+// The chunk kernels of segment s are latency-bound and small (one thread per chunk, one wave for
+// the check), so they run beside the prepare of later segments.  Each segment ends in ONE
+// randomised multi-pairing check over all its chunks; only a failing segment pays per-chunk checks
+// (k_sm_group_pairing) and only a failing chunk pays per-set retries (k_sm_fallback).
 int gbv_sm_batch_verify(gbv_ctx* c, gbv_sm_batch* b, uint8_t* valid) {
   if (!c || !b) return GBV_E_ARG;
   if (c->closed) return GBV_E_CLOSED;
@@ -324,10 +333,10 @@ int gbv_sm_batch_verify(gbv_ctx* c, gbv_sm_batch* b, uint8_t* valid) {
   HIP_CHECK(c, hipSetDevice(c->device));
   Seed seed = fresh_seed();
   uint32_t nonce = c->nonce++;
-  hipStream_t sa = c->stream, sb = c->stream2;
+  hipStream_t sa = c->stream, sbs[2] = {c->stream2, c->stream3};
   const size_t max_seg = b->seg_cap;
   const size_t n_seg = getenv("GBV_SEGMENTS") ? (size_t)std::max(1, atoi(getenv("GBV_SEGMENTS"))) : 1;
-  size_t sub_sets = std::max<size_t>((b->n + n_seg - 1) / n_seg, 32768);
+  size_t sub_sets = std::max<size_t>((b->n + n_seg - 1) / n_seg, 16384);
   std::vector<uint32_t> gcut{0};
   {
     size_t next = sub_sets;
@@ -339,49 +348,56 @@ int gbv_sm_batch_verify(gbv_ctx* c, gbv_sm_batch* b, uint8_t* valid) {
   }
   gcut.push_back((uint32_t)b->G);
   size_t S = gcut.size() - 1;
-  // events: [0,1] hash; per segment 8 (prep, reduce, miller, check); then 2 group_pairing + 2 fallback
-  size_t need = 2 + 8 * S + 4;
+  // events: [0,1] hash, [2] hash done; per segment 8 (prep, finish, miller, check); then 4
+  size_t need = 3 + 8 * S + 4;
   if (c->events.size() < need) {
     size_t old = c->events.size();
     c->events.resize(need);
-    for (size_t k = old; k < need; ++k) hipEventCreate(&c->events[k]);
+    for (size_t k = old; k < need; ++k) hipEventCreateWithFlags(&c->events[k], hipEventDefault);
   }
   hipEvent_t* ev = c->events.data();
-  HIP_CHECK(c, hipMemsetAsync(b->n_fallback, 0, 4, sb));
-  hipEventRecord(ev[0], sb);
-  launch_hash_msgs(LaunchCfg{blocks_for(b->n_calls), TPB, sb}, b->msgs, (uint32_t)b->n_calls, b->H);
-  hipEventRecord(ev[1], sb);
+  const size_t part_stride = b->G / 64 + b->G / 4096 + 4;
+  HIP_CHECK(c, hipMemsetAsync(b->n_fallback, 0, 4, sbs[0]));
+  hipEventRecord(ev[0], sbs[0]);
+  launch_hash_msgs(LaunchCfg{blocks_for(b->n_calls), TPB, sbs[0]}, b->msgs, (uint32_t)b->n_calls, b->H);
+  hipEventRecord(ev[1], sbs[0]);
+  HIP_CHECK(c, hipStreamWaitEvent(sbs[1], ev[1], 0));
   for (size_t s = 0; s < S; ++s) {
-    hipEvent_t* e = ev + 2 + 8 * s;
+    hipEvent_t* e = ev + 3 + 8 * s;
+    hipStream_t sb = sbs[s & 1];
     uint32_t g0 = gcut[s], G = gcut[s + 1] - gcut[s];
     uint32_t s0 = b->grp_off_host[g0], s1 = b->grp_off_host[gcut[s + 1]];
     hipEventRecord(e[0], sa);
-    launch_sm_prepare(LaunchCfg{blocks_for(s1 - s0), TPB, sa}, s0, s1 - s0, b->idx, b->sig, c->table, c->table_ok,
-                      (uint32_t)c->table_n, seed, nonce, b->S, b->rS, b->rP, b->status);
+    launch_sm_prepare(LaunchCfg{0, 64, sa}, s0, s1 - s0, b->idx, b->sig, b->set_grp, c->table, c->table_ok, (uint32_t)c->table_n, seed,
+                      nonce, b->S, b->rS, b->rP, b->status);
     hipEventRecord(e[1], sa);
     HIP_CHECK(c, hipStreamWaitEvent(sb, e[1], 0));
     hipEventRecord(e[2], sb);
-    launch_sm_chunk_reduce(LaunchCfg{G, 64, sb}, g0, b->grp_off, b->status, b->rS, b->rP, b->Pg, b->SgJ, b->grp_state, b->n_fallback);
+    launch_sm_chunk_finish(LaunchCfg{0, 64, sb}, g0, G, s0, b->grp_off, b->status, b->rS, b->rP, b->PgJ, b->SgJ, b->grp_state,
+                           b->n_fallback);
     hipEventRecord(e[3], sb);
     hipEventRecord(e[4], sb);
-    launch_sm_miller(LaunchCfg{G, 64, sb}, g0, G, b->grp_msg, b->grp_state, b->Pg, b->H, b->F);
+    launch_sm_miller(LaunchCfg{0, 64, sb}, g0, G, b->grp_msg, b->grp_state, b->PgJ, b->H, b->F);
     hipEventRecord(e[5], sb);
     hipEventRecord(e[6], sb);
-    launch_sm_seg_check(LaunchCfg{1, 64, sb}, g0, G, b->grp_state, b->F, b->SgJ, b->Fpart, b->Spart, b->has, b->seg_ok + s);
+    size_t po = (s & 1) * part_stride;
+    launch_sm_seg_check(LaunchCfg{1, 64, sb}, g0, G, b->grp_state, b->F, b->SgJ, b->Fpart + po, b->Spart + po, b->has + po,
+                        b->seg_ok + s);
     hipEventRecord(e[7], sb);
   }
   HIP_CHECK(c, hipGetLastError());
-  HIP_CHECK(c, hipMemcpyAsync(b->seg_ok_host, b->seg_ok, S, hipMemcpyDeviceToHost, sb));
-  HIP_CHECK(c, hipStreamSynchronize(sb));
+  HIP_CHECK(c, hipStreamSynchronize(sbs[1]));
+  HIP_CHECK(c, hipMemcpyAsync(b->seg_ok_host, b->seg_ok, S, hipMemcpyDeviceToHost, sbs[0]));
+  HIP_CHECK(c, hipStreamSynchronize(sbs[0]));
   HIP_CHECK(c, hipStreamSynchronize(sa));
-  hipEvent_t* ep = ev + 2 + 8 * S;
+  hipEvent_t* ep = ev + 3 + 8 * S;
   bool any_fail = false;
   hipEventRecord(ep[0], sa);
   for (size_t s = 0; s < S; ++s) {
     if (b->seg_ok_host[s]) continue;
     any_fail = true;
     uint32_t g0 = gcut[s], G = gcut[s + 1] - gcut[s];
-    launch_sm_group_pairing(LaunchCfg{G, 64, sa}, g0, G, b->grp_msg, b->Pg, b->SgJ, b->H, b->grp_state, b->n_fallback);
+    launch_sm_group_pairing(LaunchCfg{G, 64, sa}, g0, G, b->grp_msg, b->PgJ, b->SgJ, b->H, b->grp_state, b->n_fallback);
   }
   hipEventRecord(ep[1], sa);
   uint32_t nfb = 0;
@@ -394,7 +410,6 @@ int gbv_sm_batch_verify(gbv_ctx* c, gbv_sm_batch* b, uint8_t* valid) {
   HIP_CHECK(c, hipGetLastError());
   if (valid) HIP_CHECK(c, hipMemcpyAsync(valid, b->valid, b->n, hipMemcpyDeviceToHost, sa));
   HIP_CHECK(c, hipStreamSynchronize(sa));
-  float t;
   for (auto& x : c->last_ms) x = 0.f;
   for (auto& x : c->last_launches) x = 0;
   auto acc = [&](int k, hipEvent_t a0, hipEvent_t a1) {
@@ -406,12 +421,11 @@ int gbv_sm_batch_verify(gbv_ctx* c, gbv_sm_batch* b, uint8_t* valid) {
   };
   acc(0, ev[0], ev[1]);
   for (size_t s = 0; s < S; ++s) {
-    hipEvent_t* e = ev + 2 + 8 * s;
+    hipEvent_t* e = ev + 3 + 8 * s;
     for (int k = 0; k < 4; ++k) acc(1 + k, e[2 * k], e[2 * k + 1]);
   }
   if (any_fail) acc(5, ep[0], ep[1]);
   acc(6, ep[2], ep[3]);
-  (void)t;
   return GBV_OK;
 }
 

@@ -10,18 +10,6 @@ namespace gbv {
 GBV_NI G2J g2_add_j(G2J a, G2J b) { return jac_add(a, b); }
 #define g2_add g2_add_j
 
-// Miller value f_g = f_{|x|, H(m_g)}(P_g) of every pending chunk: one wave per chunk running the
-// cooperative Miller loop (coop.h), so a chunk costs ~300 dependent Fp products of latency.
-__global__ void __launch_bounds__(64) k_sm_miller(uint32_t g0, const uint32_t* __restrict__ grp_msg, const uint8_t* __restrict__ grp_state,
-                                                  const G1A* __restrict__ Pg, const G2A* __restrict__ H, Fp12* __restrict__ F) {
-  __shared__ Fp ws[coop::MILLER_WS];
-  uint32_t g = g0 + blockIdx.x;
-  if (grp_state[g] != GRP_PENDING) return;
-  coop::miller_load_pair(ws, 0, Pg[g], H[grp_msg[g]]);
-  coop::miller_loop(ws, 1);
-  if (threadIdx.x < 12) ((Fp*)&F[g])[threadIdx.x] = ws[coop::M_F + threadIdx.x];
-}
-
 // One wave per segment: the randomised chunk equations of the whole segment are folded into one
 // check  prod_g e(P_g, H(m_g)) * e(-g1, sum_g S_g) == 1  with ONE final exponentiation.  Every
 // set carries its own random 64-bit scalar, so this is blst's verifyMultipleAggregateSignatures
@@ -29,7 +17,7 @@ __global__ void __launch_bounds__(64) k_sm_miller(uint32_t g0, const uint32_t* _
 // with probability ~2^-64 (the bound each chunk check has).  Pass -> every pending chunk is
 // valid; fail -> seg_ok = 0 and the host runs the per-chunk checks, then the per-set retries.
 constexpr int SEG_WS = coop::MILLER_WS + coop::FINAL_EXP_WS;
-__global__ void __launch_bounds__(64) k_sm_seg_check(uint32_t g0, uint32_t G, uint32_t nb, const Fp12* __restrict__ Fpart,
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_sm_seg_check(uint32_t g0, uint32_t G, uint32_t nb, const Fp12* __restrict__ Fpart,
                                                      const G2J* __restrict__ Spart, const uint8_t* __restrict__ has,
                                                      uint8_t* __restrict__ grp_state, uint8_t* __restrict__ seg_ok) {
   __shared__ Fp ws[SEG_WS];
@@ -37,7 +25,7 @@ __global__ void __launch_bounds__(64) k_sm_seg_check(uint32_t g0, uint32_t G, ui
   Fp* ml = ws;
   Fp* fe = ws + coop::MILLER_WS;
   unsigned lane = threadIdx.x;
-  // fe[E_F] = product of the block partials (cooperative, one after another), S = their sum
+  // fe[E_F] = product of the (<= 4) final partials (cooperative, one after another), S = their sum
   if (lane == 0) flags[0] = 0;
   coop::set_one12(fe + coop::E_F);
   G2J s = jac_infinity<Fp2>();
@@ -85,27 +73,30 @@ __global__ void __launch_bounds__(64) k_sm_seg_check(uint32_t g0, uint32_t G, ui
 
 // Failure path of a segment: each pending chunk on its own, e(P_g, H(m_g)) e(-g1, S_g) == 1
 // (verify(msg, aggPk, aggSig) of the chunk, maybeBatch.ts:34-38); one wave per chunk.
-__global__ void __launch_bounds__(64) k_sm_group_pairing(uint32_t g0, const uint32_t* __restrict__ grp_msg, const G1A* __restrict__ Pg,
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_sm_group_pairing(uint32_t g0, const uint32_t* __restrict__ grp_msg, const G1J* __restrict__ PgJ,
                                                          const G2J* __restrict__ SgJ, const G2A* __restrict__ H,
                                                          uint8_t* __restrict__ grp_state, uint32_t* __restrict__ n_fallback) {
   __shared__ Fp ws[SEG_WS];
-  __shared__ Fp sa_lds[4];
+  __shared__ Fp sa_lds[6];
   __shared__ int sa_ok;
   uint32_t g = g0 + blockIdx.x;
   if (grp_state[g] != GRP_PENDING) return;
   unsigned lane = threadIdx.x;
   if (lane == 0) {
     G2A sa;
-    sa_ok = jac_to_aff(sa, SgJ[g]) ? 1 : 0;
+    G1A pa;
+    sa_ok = jac_to_aff(sa, SgJ[g]) && jac_to_aff(pa, PgJ[g]) ? 1 : 0;
     sa_lds[0] = sa.x.c0;
     sa_lds[1] = sa.x.c1;
     sa_lds[2] = sa.y.c0;
     sa_lds[3] = sa.y.c1;
+    sa_lds[4] = pa.x;
+    sa_lds[5] = pa.y;
   }
   coop::barrier();
   bool ok = false;
   if (sa_ok) {
-    coop::miller_load_pair(ws, 0, Pg[g], H[grp_msg[g]]);
+    coop::miller_load_pair(ws, 0, G1A{sa_lds[4], sa_lds[5]}, H[grp_msg[g]]);
     coop::miller_load_pair(ws, 1, g1_neg_generator(), G2A{Fp2{sa_lds[0], sa_lds[1]}, Fp2{sa_lds[2], sa_lds[3]}});
     coop::miller_loop(ws, 2);
     Fp* fe = ws + coop::MILLER_WS;
@@ -119,21 +110,16 @@ __global__ void __launch_bounds__(64) k_sm_group_pairing(uint32_t g0, const uint
 }
 
 
-void launch_sm_miller(LaunchCfg c, uint32_t g0, uint32_t G, const uint32_t* grp_msg, const uint8_t* grp_state, const G1A* Pg, const G2A* H,
-                      Fp12* F) {
-  hipLaunchKernelGGL(k_sm_miller, dim3(G), dim3(64), 0, c.stream, g0, grp_msg, grp_state, Pg, H, F);
-  debug_sync(c.stream, "k_sm_miller");
-}
 void launch_sm_seg_check(LaunchCfg c, uint32_t g0, uint32_t G, uint8_t* grp_state, const Fp12* F, const G2J* SgJ, Fp12* Fpart, G2J* Spart,
                          uint8_t* has, uint8_t* seg_ok) {
-  launch_sm_seg_reduce(c, g0, G, grp_state, F, SgJ, Fpart, Spart, has);
-  uint32_t nb = (G + 63) / 64;
-  hipLaunchKernelGGL(k_sm_seg_check, dim3(1), dim3(64), 0, c.stream, g0, G, nb, Fpart, Spart, has, grp_state, seg_ok);
+  uint32_t nb = 0;
+  uint32_t off = launch_sm_seg_reduce(c, g0, G, grp_state, F, SgJ, Fpart, Spart, has, &nb);
+  hipLaunchKernelGGL(k_sm_seg_check, dim3(1), dim3(64), 0, c.stream, g0, G, nb, Fpart + off, Spart + off, has + off, grp_state, seg_ok);
   debug_sync(c.stream, "k_sm_seg_check");
 }
-void launch_sm_group_pairing(LaunchCfg c, uint32_t g0, uint32_t G, const uint32_t* grp_msg, const G1A* Pg, const G2J* SgJ, const G2A* H,
+void launch_sm_group_pairing(LaunchCfg c, uint32_t g0, uint32_t G, const uint32_t* grp_msg, const G1J* PgJ, const G2J* SgJ, const G2A* H,
                              uint8_t* grp_state, uint32_t* n_fallback) {
-  hipLaunchKernelGGL(k_sm_group_pairing, dim3(G), dim3(64), 0, c.stream, g0, grp_msg, Pg, SgJ, H, grp_state, n_fallback);
+  hipLaunchKernelGGL(k_sm_group_pairing, dim3(G), dim3(64), 0, c.stream, g0, grp_msg, PgJ, SgJ, H, grp_state, n_fallback);
   debug_sync(c.stream, "k_sm_group_pairing");
 }
 }  // namespace gbv

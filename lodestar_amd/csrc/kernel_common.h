@@ -6,8 +6,9 @@
 //   k_hash_msgs         hash_to_G2 inside blst verify / verifyMultipleAggregateSignatures
 //   k_sm_prepare        aggregateWithRandomness per set: Signature.fromBytes(sig, true) + r_i*pk, r_i*sig
 //                       (multithread/jobItem.ts:73)
-//   k_sm_chunk_reduce   sum_i r_i pk_i, sum_i r_i sig_i per same-message chunk (one wave per chunk)
-//   k_sm_miller         Miller value of (sum r_i pk_i, H(m)) per chunk
+//   k_sm_prepare        also sums r_i pk_i, r_i sig_i per chunk within each wave (segmented scan)
+//   k_sm_chunk_finish   sum_i r_i pk_i, sum_i r_i sig_i per same-message chunk from the wave sums
+//   k_sm_miller         Miller value of (sum r_i pk_i, H(m)) per chunk (thread per chunk)
 //   k_sm_seg_check      one randomised multi-pairing check over a segment of chunks
 //   k_sm_group_pairing  verify(msg, aggPk, aggSig) of the chunk (worker.ts:29-107 -> maybeBatch n = 1),
 //                       only for chunks of a failing segment

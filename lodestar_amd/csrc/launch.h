@@ -12,17 +12,18 @@ struct LaunchCfg { unsigned blocks; unsigned threads; hipStream_t stream; };
 void launch_hash_msgs(LaunchCfg c, const uint8_t* msgs32, uint32_t n, G2A* H);
 void launch_util_g2_out(LaunchCfg c, uint32_t n, const G2A* H, uint8_t* out192);
 
-void launch_sm_prepare(LaunchCfg c, uint32_t base, uint32_t n, const uint32_t* idx, const uint8_t* sig96, const G1A* table, const uint8_t* table_ok,
-                       uint32_t table_n, const Seed& seed, uint32_t nonce, G2A* S_out, G2J* rS_out, G1J* rP_out, uint8_t* status);
-void launch_sm_chunk_reduce(LaunchCfg c, uint32_t g0, const uint32_t* grp_off, const uint8_t* status, const G2J* rS, const G1J* rP,
-                            G1A* Pg, G2J* SgJ, uint8_t* grp_state, uint32_t* n_fallback);
-void launch_sm_miller(LaunchCfg c, uint32_t g0, uint32_t G, const uint32_t* grp_msg, const uint8_t* grp_state, const G1A* Pg, const G2A* H,
+void launch_sm_prepare(LaunchCfg c, uint32_t base, uint32_t n, const uint32_t* idx, const uint8_t* sig96, const uint32_t* set_grp,
+                       const G1A* table, const uint8_t* table_ok, uint32_t table_n, const Seed& seed, uint32_t nonce, G2A* S_out, G2J* Sh,
+                       G1J* Ph, uint8_t* status);
+void launch_sm_chunk_finish(LaunchCfg c, uint32_t g0, uint32_t G, uint32_t s0, const uint32_t* grp_off, const uint8_t* status, const G2J* Sh,
+                            const G1J* Ph, G1J* PgJ, G2J* SgJ, uint8_t* grp_state, uint32_t* n_fallback);
+void launch_sm_miller(LaunchCfg c, uint32_t g0, uint32_t G, const uint32_t* grp_msg, const uint8_t* grp_state, const G1J* PgJ, const G2A* H,
                       Fp12* F);
-void launch_sm_seg_reduce(LaunchCfg c, uint32_t g0, uint32_t G, const uint8_t* grp_state, const Fp12* F, const G2J* SgJ, Fp12* Fpart,
-                          G2J* Spart, uint8_t* has);
+uint32_t launch_sm_seg_reduce(LaunchCfg c, uint32_t g0, uint32_t G, const uint8_t* grp_state, const Fp12* F, const G2J* SgJ, Fp12* Fpart,
+                              G2J* Spart, uint8_t* has, uint32_t* n_out);
 void launch_sm_seg_check(LaunchCfg c, uint32_t g0, uint32_t G, uint8_t* grp_state, const Fp12* F, const G2J* SgJ, Fp12* Fpart, G2J* Spart,
                          uint8_t* has, uint8_t* seg_ok);
-void launch_sm_group_pairing(LaunchCfg c, uint32_t g0, uint32_t G, const uint32_t* grp_msg, const G1A* Pg, const G2J* SgJ, const G2A* H,
+void launch_sm_group_pairing(LaunchCfg c, uint32_t g0, uint32_t G, const uint32_t* grp_msg, const G1J* PgJ, const G2J* SgJ, const G2A* H,
                              uint8_t* grp_state, uint32_t* n_fallback);
 void launch_sm_fallback(LaunchCfg c, uint32_t n, const uint32_t* set_grp, const uint32_t* grp_msg, const uint8_t* grp_state,
                         const uint8_t* status, const uint32_t* idx, const G1A* table, const G2A* S, const G2A* H, uint8_t* valid,

@@ -98,6 +98,27 @@ GBV_NI Fp12 miller_loop_1(G1A P0, G2A Q0) {
   return fp12_conj(f);
 }
 
+// single pair with P in Jacobian coordinates (X : Y : Z), Z != 0: every line is the affine line
+// times Z^3 (c0 * Z^3, c2 from -X Z, c3 from Y), an Fp factor the final exponentiation removes,
+// so no inversion is needed to get P affine.
+GBV_NI Fp12 miller_loop_1j(G1J P, G2A Q0) {
+  Fp z2 = fp_sqr(P.z);
+  Fp z3 = fp_mul(z2, P.z);
+  Fp nxz = fp_neg(fp_mul(P.x, P.z));
+  G2Proj T0{Q0.x, Q0.y, fp2_one()};
+  Fp12 f = fp12_one();
+  for (int i = 62; i >= 0; --i) {
+    if (i != 62) f = fp12_sqr(f);
+    Line l0 = dbl_step(T0, nxz, P.y);
+    f = fp12_mul_line(f, fp2_mul_fp(l0.c0, z3), l0.c2, l0.c3);
+    if ((X_ABS >> i) & 1ull) {
+      l0 = add_step(T0, Q0, nxz, P.y);
+      f = fp12_mul_line(f, fp2_mul_fp(l0.c0, z3), l0.c2, l0.c3);
+    }
+  }
+  return fp12_conj(f);
+}
+
 // e(P0, Q0) * e(P1, Q1) == 1 ?
 GBV_HD bool pairing_check_2(const G1A& P0, bool inf0, const G2A& Q0, const G1A& P1, bool inf1, const G2A& Q1) {
   Fp12 f = miller_loop_2(P0, inf0, Q0, P1, inf1, Q1);

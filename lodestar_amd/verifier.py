@@ -222,7 +222,7 @@ class GpuBlsVerifier:
 
     def last_kernel_ms(self):
         """(total device ms, launches) of each kernel of the last staged verify:
-        [hash, prepare, chunk_reduce, miller, seg_check, group_pairing, fallback]."""
+        [hash, prepare, chunk_finish, miller, seg_check, group_pairing, fallback]."""
         buf = (ctypes.c_float * 7)()
         cnt = (ctypes.c_int * 7)()
         k = self._lib.gbv_last_kernel_ms(self._ctx, buf, cnt, 7)
