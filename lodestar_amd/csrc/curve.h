@@ -333,4 +333,69 @@ GBV_NI bool g1_in_subgroup(G1A p) {
   return jac_eq_aff(t, phi);
 }
 
+// ---- randomised batch scalars (aggregateWithRandomness / verifyMultipleAggregateSignatures) ----
+// The batch scalar of a set is r = a - b x^2 (mod r) with
+//   a = sum_{i<32} (2 s_i - 1) 2^i,  b = sum_{i<32} (2 t_i - 1) 2^i   (s = bits 0..31, t = 32..63 of
+// a random 64-bit word).  (a, b) -> r is injective (|a|, |b| < 2^32, x^2 ~ 2^127), so r takes 2^64
+// distinct values: the same 2^-64 soundness bound as blst's 64-bit random scalars; only booleans
+// are compared with the reference, never the scalars.  Both groups have a cheap endomorphism with
+// eigenvalue -x^2:  G1: phi(x, y) = (beta x, y);  G2: -psi^2(x, y) = (c x, y)  (psi^2 = [x^2]).
+// So r P = a P + b phi(P): a 32-step joint signed-digit ladder whose every digit pair adds one of
+// +-(P + phi P), +-(P - phi P) -- no zero digits, so no lane of a wave idles on a skipped add.
+
+// R = sum_i 2^i (d_i S) for the digit pairs of (sa, sb); S1 = P + E(P), S2 = P - E(P), affine.
+template <class F> GBV_HD Jac<F> jac_mul_2d_signed(const Aff<F>& S1, const Aff<F>& S2, uint32_t sa, uint32_t sb) {
+  auto pick = [&](int i) {
+    bool s = (sa >> i) & 1u, t = (sb >> i) & 1u;
+    Aff<F> T{f_sel(s == t, S1.x, S2.x), f_sel(s == t, S1.y, S2.y)};
+    T.y = f_sel(s, T.y, f_neg(T.y));
+    return T;
+  };
+  Jac<F> R = jac_from_aff(pick(31));
+  for (int i = 30; i >= 0; --i) {
+    R = jac_dbl(R);
+    R = jac_add_aff(R, pick(i));
+  }
+  return R;
+}
+
+GBV_HD G1A g1_phi(const G1A& p) { return G1A{fp_mul(p.x, FP_BETA), p.y}; }
+GBV_HD G2A g2_neg_psi2(const G2A& q) { return G2A{fp2_mul_fp(q.x, PSI2_C1), q.y}; }
+
+template <class F> GBV_HD Aff<F> aff_from_jac_inv(const Jac<F>& p, const F& zinv) {
+  F z2 = f_sqr(zinv);
+  return Aff<F>{f_mul(p.x, z2), f_mul(p.y, f_mul(z2, zinv))};
+}
+
+// [r] P and [r] Q for the same batch scalar r (digits r64).  The four ladder tables
+// P +- phi(P), Q +- (-psi^2 Q) are made affine with ONE shared Fp inversion (Montgomery's trick
+// over z1 z2 N(Z1 Z2)).  Returns false only for points of small order (P = +-phi(P) etc.), which
+// subgroup-checked inputs never are; the caller then re-verifies that set unrandomised.
+GBV_NI bool randomize_pair(G1A P, G2A Q, uint64_t r64, G1J* rP, G2J* rQ) {
+  G1A ph = g1_phi(P);
+  G2A qh = g2_neg_psi2(Q);
+  G1J a1 = jac_add_aff(jac_from_aff(P), ph);
+  G1J a2 = jac_add_aff(jac_from_aff(P), G1A{ph.x, fp_neg(ph.y)});
+  G2J b1 = jac_add_aff(jac_from_aff(Q), qh);
+  G2J b2 = jac_add_aff(jac_from_aff(Q), G2A{qh.x, fp2_neg(qh.y)});
+  Fp2 W = fp2_mul(b1.z, b2.z);
+  Fp nW = fp_add(fp_sqr(W.c0), fp_sqr(W.c1));
+  Fp u = fp_mul(a1.z, a2.z);
+  Fp tot = fp_mul(u, nW);
+  if (fp_is_zero(tot)) return false;
+  Fp inv = fp_inv(tot);
+  Fp inv_u = fp_mul(inv, nW);
+  Fp inv_nW = fp_mul(inv, u);
+  Fp2 Winv = fp2_mul_fp(fp2_conj(W), inv_nW);
+  G1A P1 = aff_from_jac_inv(a1, fp_mul(a2.z, inv_u));
+  G1A P2 = aff_from_jac_inv(a2, fp_mul(a1.z, inv_u));
+  G2A Q1 = aff_from_jac_inv(b1, fp2_mul(b2.z, Winv));
+  G2A Q2 = aff_from_jac_inv(b2, fp2_mul(b1.z, Winv));
+  uint32_t sa = (uint32_t)r64, sb = (uint32_t)(r64 >> 32);
+  *rP = jac_mul_2d_signed(P1, P2, sa, sb);
+  *rQ = jac_mul_2d_signed(Q1, Q2, sa, sb);
+  return true;
+}
+
 }  // namespace gbv
+

@@ -51,8 +51,11 @@ __global__ void GBV_KERNEL_ATTR k_sm_prepare(uint32_t base, uint32_t n, const ui
     if (st == SET_OK) {
       S_out[i] = s;
       uint64_t r = prf_scalar(seed, i, nonce);
-      rs = g2_mul_u64(s, r);
-      rp = g1_mul_u64(table[k], r);
+      G1A pk = table[k];
+      if (!randomize_pair(pk, s, r, &rp, &rs)) {  // unreachable for subgroup points; plain 64-bit r then
+        rs = g2_mul_u64(s, r);
+        rp = g1_mul_u64(pk, r);
+      }
     }
   }
   for (unsigned d = 1; d < 64; d <<= 1) {

@@ -37,13 +37,17 @@ __global__ void GBV_KERNEL_ATTR k_vs_prepare(uint32_t n, const uint32_t* __restr
   status[i] = st;
   if (st != SET_OK) return;
   uint64_t r = prf_scalar(seed, i, nonce);
-  G1A rp;
-  jac_to_aff(rp, g1_mul_u64(pk, r));
-  rS_out[i] = g2_mul_u64(s, r);
+  G1J rp;
+  G2J rs;
+  if (!randomize_pair(pk, s, r, &rp, &rs)) {  // unreachable for subgroup points; plain 64-bit r then
+    rs = g2_mul_u64(s, r);
+    rp = g1_mul_u64(pk, r);
+  }
+  rS_out[i] = rs;
   uint32_t w[8];
   load_msg_words(w, msgs32 + 32ull * i);
   G2A h = hash_to_g2(w);
-  f_out[i] = miller_loop_1(rp, h);
+  f_out[i] = miller_loop_1j(rp, h);
 }
 
 __global__ void GBV_KERNEL_ATTR k_vs_chunk(uint32_t C, const uint32_t* __restrict__ chunk_off, const uint8_t* __restrict__ status,

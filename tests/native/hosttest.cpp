@@ -109,4 +109,19 @@ int ht_coop_pairing(uint8_t* out, const uint8_t* p96, const uint8_t* q192, int n
   for (int i = 0; i < 12; ++i) store_canon(out + 48 * i, fe[coop::E_C + i]);
   return ok;
 }
+// [r] P, [r] Q for the batch scalar r = a - b x^2 of the 64-bit digit word r64 (curve.h)
+int ht_randomize(uint8_t* outp, uint8_t* outq, const uint8_t* p96, const uint8_t* q192, uint64_t r64) {
+  G1A P{load_mont(p96), load_mont(p96 + 48)};
+  G2A Q{load_fp2(q192), load_fp2(q192 + 96)};
+  G1J rp;
+  G2J rq;
+  if (!randomize_pair(P, Q, r64, &rp, &rq)) return 0;
+  G1A pa;
+  G2A qa;
+  jac_to_aff(pa, rp);
+  jac_to_aff(qa, rq);
+  store_canon(outp, pa.x); store_canon(outp + 48, pa.y);
+  store_fp2(outq, qa.x); store_fp2(outq + 96, qa.y);
+  return 1;
+}
 }

@@ -178,3 +178,22 @@ def test_coop_two_pair_check(lib):
     H2 = o.hash_to_g2(bytes(32))
     assert lib.ht_coop_pairing(out, ps, fp2b(H2[0]) + fp2b(H2[1]) + fp2b(sig[0]) + fp2b(sig[1]), 2) == 0
 
+
+def _digits_scalar(r64):
+    a = sum((1 if (r64 >> i) & 1 else -1) << i for i in range(32))
+    b = sum((1 if (r64 >> (32 + i)) & 1 else -1) << i for i in range(32))
+    return (a - b * o.X * o.X) % o.R
+
+
+@pytest.mark.parametrize("r64", [0, 0xFFFFFFFFFFFFFFFF, 0x0123456789ABCDEF, 0xDEADBEEF00C0FFEE])
+def test_randomize_pair(lib, r64):
+    """Endomorphism-split batch scalar: [a - b x^2] on G1 and G2 (curve.h randomize_pair)."""
+    P = o.g1_mul(o.G1_GEN, 0x1234)
+    Q = o.g2_mul(o.G2_GEN, 0x5678)
+    lib.ht_randomize.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint64]
+    op, oq = buf(96), buf(192)
+    assert lib.ht_randomize(op, oq, be(P[0]) + be(P[1]), fp2b(Q[0]) + fp2b(Q[1]), r64) == 1
+    r = _digits_scalar(r64)
+    assert (int.from_bytes(op.raw[:48], "big"), int.from_bytes(op.raw[48:], "big")) == o.g1_mul(P, r)
+    assert (b2fp2(oq.raw[:96]), b2fp2(oq.raw[96:])) == o.g2_mul(Q, r)
+
