@@ -32,11 +32,12 @@ R_ORDER = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
 N_VALIDATORS = 1 << 20
 N_KEYS = 1024
 # Algorithmic work per unit, in Fp-multiplication equivalents (FME; 1 FME = 300 u32 MACs,
-# 12-limb CIOS Montgomery).  SURVEY.md 8(d) component counts: G2 decompress 1.8k + G2 subgroup
-# 1.25k + r*pk (64-bit, G1) 0.8k + r*sig (64-bit, G2) 1.95k per set; per same-message chunk
-# hash_to_G2 7.2k + 2-pair Miller loop 8.8k + shared squarings 2.3k + final exponentiation 8.4k.
-W_PREPARE_FME = 5800
-W_CHUNK_FME = 26700
+# 12-limb Montgomery), counted from the k_sm_prepare code path:
+#   G2 decompress 1230 (two 379-bit exponentiations, 606 + 605)  + G2 subgroup check 1170
+#   (63 dbl x 16 + 5 madd x 29 + psi)  + randomisation 2695 (4 table madds, one shared 381-bit
+#   inversion 608, affine tables ~40, G1 ladder 31 x 18, G2 ladder 31 x 45)  + per-wave chunk scan
+#   354 (6 levels x (43 + 16))  = 5450 per set.
+W_PREPARE_FME = 5450
 MAC_PER_FME = 300
 # Integer VALU peak: v_mad_u64_u32 measured at 37.0 T lane-ops/s on MI355X
 # (tools/ubench_int.hip, profiles/r01_ubench_int.txt); theoretical 256 CU x 4 SIMD x 16 lanes x 2.4 GHz = 39.3 T.
@@ -105,6 +106,8 @@ def main():
     ap.add_argument("--sets", type=int, default=1 << 20)
     ap.add_argument("--cpu-sample", type=int, default=None, help="sets in the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-stream", dest="stream", action="store_false",
+                    help="one batch at a time (no overlap of consecutive verifications)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -126,11 +129,14 @@ def main():
     v = GpuBlsVerifier(local_rank)
     call_off, idx, sigs, msgs, key_pks = build_workload(v, args.sets, rank, log)
     staged = v.stage_same_message(call_off, idx, sigs, msgs)
+    # streaming submission: two staged copies of the workload so that one batch's chunk-level tail
+    # overlaps the next batch's per-set kernel (each verification still runs start to finish)
+    stages = [staged, v.stage_same_message(call_off, idx, sigs, msgs)] if args.stream else [staged]
 
     for _ in range(args.warmup):
         res = staged.verify(True)
     if args.warmup:
-        ok = sum(res)
+        ok = res.count(1)
         assert ok == args.sets, "warmup: %d of %d sets verified" % (ok, args.sets)
         log("warmup ok: all %d sets valid" % ok)
 
@@ -141,13 +147,28 @@ def main():
         if dist is not None:
             dist.barrier()
 
+    def collect(b):
+        r = b.wait(True)
+        ms, cnt = v.last_kernel_ms()
+        kms[:] += np.array(ms)
+        kcnt[:] += np.array(cnt)
+        return r.count(1)
+
+    n_valid = []
     barrier()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        res = staged.verify(True)
-        ms, cnt = v.last_kernel_ms()
-        kms += np.array(ms)
-        kcnt += np.array(cnt)
+    pending = None
+    for k in range(args.steps):
+        b = stages[k % len(stages)]
+        if pending is b:  # one stage only: finish it before resubmitting
+            n_valid.append(collect(b))
+            pending = None
+        b.submit()
+        if pending is not None:
+            n_valid.append(collect(pending))
+        pending = b
+    if pending is not None:
+        n_valid.append(collect(pending))
     barrier()
     elapsed = time.perf_counter() - t0
     if dist is not None:
@@ -155,7 +176,7 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    assert sum(res) == args.sets
+    assert n_valid == [args.sets] * args.steps, n_valid
     avg_launch_ms = kms / np.maximum(kcnt, 1)
     kms /= max(args.steps, 1)
     prep_launches_per_step = kcnt[1] / max(args.steps, 1)
@@ -200,7 +221,8 @@ def main():
         "data": "synthetic (interop keys, sha256 messages, GPU-signed)",
         "config": {"workload": "C2 gossip attestation stream: 1M single-pubkey sets, same-message calls of 32-128",
                    "sets_per_gpu": args.sets, "calls_per_gpu": n_chunks, "table": N_VALIDATORS,
-                   "parallelism": "replicas/dp%d" % world},
+                   "parallelism": "replicas/dp%d" % world,
+                   "submission": "streamed: 2 batches in flight" if args.stream else "one batch at a time"},
         "roofline": roofline,
         "cpu_baseline": cpu,
     }

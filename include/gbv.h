@@ -107,6 +107,12 @@ int gbv_sm_batch_create(gbv_ctx* ctx, size_t n_calls, const uint32_t* call_off, 
                         const uint8_t* sigs96, const uint8_t* msgs32, gbv_sm_batch** out);
 /* Verify a staged batch; valid (host, optional) receives the per-set booleans. */
 int gbv_sm_batch_verify(gbv_ctx* ctx, gbv_sm_batch* b, uint8_t* valid);
+/* Streaming form of gbv_sm_batch_verify: submit enqueues the whole verification and returns;
+ * wait blocks until it is done and copies the per-set booleans.  Submitting batch k+1 before
+ * waiting on batch k overlaps k's chunk-level tail with k+1's per-set kernel (gossip stream).
+ * A batch can have one verification in flight at a time. */
+int gbv_sm_batch_submit(gbv_ctx* ctx, gbv_sm_batch* b);
+int gbv_sm_batch_wait(gbv_ctx* ctx, gbv_sm_batch* b, uint8_t* valid);
 void gbv_sm_batch_destroy(gbv_ctx* ctx, gbv_sm_batch* b);
 /* Device time (ms, summed over launches) and launch count of each kernel of the last
  * gbv_sm_batch_verify, measured with HIP events on the stream each kernel runs on:

@@ -48,7 +48,7 @@ struct gbv_ctx {
   size_t table_n = 0;
   std::string err;
   uint32_t nonce = 0;
-  hipStream_t stream2 = nullptr, stream3 = nullptr;
+  hipStream_t stream2 = nullptr, stream3 = nullptr, stream4 = nullptr;
   std::vector<hipEvent_t> events;
   static constexpr int NK = 7;  // hash, prepare, chunk_reduce, miller, seg_check, group_pairing, fallback
   float last_ms[NK] = {};
@@ -62,7 +62,13 @@ struct gbv_sm_batch {
   uint32_t *idx = nullptr, *grp_off = nullptr, *grp_msg = nullptr, *set_grp = nullptr, *n_fallback = nullptr;
   uint8_t *sig = nullptr, *msgs = nullptr, *status = nullptr, *grp_state = nullptr, *valid = nullptr, *seg_ok = nullptr;
   uint8_t* seg_ok_host = nullptr;  // pinned
+  uint8_t* valid_host = nullptr;   // pinned, n bytes: results of the last submitted verify
   size_t seg_cap = 0;
+  // in-flight state of the last gbv_sm_batch_submit
+  bool in_flight = false;
+  size_t n_seg = 0;
+  std::vector<hipEvent_t> ev;
+  hipEvent_t done = nullptr;
   G2A *H = nullptr, *S = nullptr;
   G2J *rS = nullptr, *SgJ = nullptr;
   Fp12* F = nullptr;
@@ -124,10 +130,12 @@ int gbv_init(int device, gbv_ctx** out) {
     return GBV_E_DEVICE;
   }
   if (hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&c->stream3, hipStreamNonBlocking) != hipSuccess) {
+      hipStreamCreateWithFlags(&c->stream3, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->stream4, hipStreamNonBlocking) != hipSuccess) {
     hipStreamDestroy(c->stream);
     if (c->stream2) hipStreamDestroy(c->stream2);
   if (c->stream3) hipStreamDestroy(c->stream3);
+  if (c->stream4) hipStreamDestroy(c->stream4);
     delete c;
     return GBV_E_DEVICE;
   }
@@ -143,10 +151,12 @@ void gbv_destroy(gbv_ctx* c) {
   hipFree(c->table_ok);
   if (c->stream2) hipStreamSynchronize(c->stream2);
   if (c->stream3) hipStreamSynchronize(c->stream3);
+  if (c->stream4) hipStreamSynchronize(c->stream4);
   for (auto& e : c->events) hipEventDestroy(e);
   if (c->stream) hipStreamDestroy(c->stream);
   if (c->stream2) hipStreamDestroy(c->stream2);
   if (c->stream3) hipStreamDestroy(c->stream3);
+  if (c->stream4) hipStreamDestroy(c->stream4);
   delete c;
 }
 
@@ -246,6 +256,10 @@ void gbv_sm_batch_destroy(gbv_ctx* c, gbv_sm_batch* b) {
   hipFree(b->idx); hipFree(b->grp_off); hipFree(b->grp_msg); hipFree(b->set_grp); hipFree(b->n_fallback);
   hipFree(b->sig); hipFree(b->msgs); hipFree(b->status); hipFree(b->grp_state); hipFree(b->valid);
   hipFree(b->H); hipFree(b->S); hipFree(b->SgJ); hipFree(b->rS); hipFree(b->rP); hipFree(b->PgJ);
+  if (b->in_flight && b->done) hipEventSynchronize(b->done);
+  for (auto& e : b->ev) hipEventDestroy(e);
+  if (b->done) hipEventDestroy(b->done);
+  hipHostFree(b->valid_host);
   hipFree(b->F); hipFree(b->seg_ok); hipHostFree(b->seg_ok_host);
   hipFree(b->Fpart); hipFree(b->Spart); hipFree(b->has);
   delete b;
@@ -297,6 +311,8 @@ int gbv_sm_batch_create(gbv_ctx* c, size_t n_calls, const uint32_t* call_off, co
   b->seg_cap = 64;
   chk(dalloc(&b->seg_ok, b->seg_cap));
   chk(hipHostMalloc((void**)&b->seg_ok_host, b->seg_cap, hipHostMallocDefault));
+  chk(hipHostMalloc((void**)&b->valid_host, std::max<size_t>(n, 1), hipHostMallocDefault));
+  chk(hipEventCreateWithFlags(&b->done, hipEventDisableTiming));
   if (e != hipSuccess) {
     gbv_sm_batch_destroy(c, b);
     return fail(c, GBV_E_OOM, std::string("hipMalloc: ") + hipGetErrorString(e));
@@ -318,22 +334,26 @@ int gbv_sm_batch_create(gbv_ctx* c, size_t n_calls, const uint32_t* call_off, co
   return GBV_OK;
 }
 
-// Pipelined over segments of ~n/S sets (cut at chunk boundaries):
+// Pipelined over segments of ~n/S sets (cut at chunk boundaries), all enqueued without a host
+// round trip so consecutive submits overlap (the chunk-level tail of batch k runs beside the
+// throughput-bound k_sm_prepare of batch k+1):
+//   stream H      : k_hash_msgs
 //   stream A      : k_sm_prepare(segment s)  -- throughput-bound, also forms per-wave chunk sums
-//   streams B0/B1 : (segment s alternates) wait(prepare s), k_sm_chunk_finish, k_sm_miller,
-//                   k_sm_seg_reduce + k_sm_seg_check
-// The chunk kernels of segment s are latency-bound and small (one thread per chunk, one wave for
-// the check), so they run beside the prepare of later segments.  Each segment ends in ONE
-// randomised multi-pairing check over all its chunks; only a failing segment pays per-chunk checks
-// (k_sm_group_pairing) and only a failing chunk pays per-set retries (k_sm_fallback).
-int gbv_sm_batch_verify(gbv_ctx* c, gbv_sm_batch* b, uint8_t* valid) {
+//   streams B0/B1 : (segment s alternates) wait(prepare s, hash) k_sm_chunk_finish, k_sm_miller,
+//                   k_sm_seg_reduce + k_sm_seg_check, k_sm_group_pairing (exits at once unless
+//                   the segment check failed)
+//   stream B0     : wait(all) k_sm_fallback (per-set retry of failed chunks only), copy-out
+// Each segment ends in ONE randomised multi-pairing check over all its chunks; only a failing
+// segment pays per-chunk checks and only a failing chunk pays per-set retries.
+int gbv_sm_batch_submit(gbv_ctx* c, gbv_sm_batch* b) {
   if (!c || !b) return GBV_E_ARG;
   if (c->closed) return GBV_E_CLOSED;
-  if (b->n == 0) return GBV_OK;
+  if (b->in_flight) return fail(c, GBV_E_ARG, "batch already in flight");
   HIP_CHECK(c, hipSetDevice(c->device));
+  if (b->n == 0) return GBV_OK;
   Seed seed = fresh_seed();
   uint32_t nonce = c->nonce++;
-  hipStream_t sa = c->stream, sbs[2] = {c->stream2, c->stream3};
+  hipStream_t sa = c->stream, sh = c->stream4, sbs[2] = {c->stream2, c->stream3};
   const size_t max_seg = b->seg_cap;
   const size_t n_seg = getenv("GBV_SEGMENTS") ? (size_t)std::max(1, atoi(getenv("GBV_SEGMENTS"))) : 1;
   size_t sub_sets = std::max<size_t>((b->n + n_seg - 1) / n_seg, 16384);
@@ -348,22 +368,22 @@ int gbv_sm_batch_verify(gbv_ctx* c, gbv_sm_batch* b, uint8_t* valid) {
   }
   gcut.push_back((uint32_t)b->G);
   size_t S = gcut.size() - 1;
-  // events: [0,1] hash, [2] hash done; per segment 8 (prep, finish, miller, check); then 4
-  size_t need = 3 + 8 * S + 4;
-  if (c->events.size() < need) {
-    size_t old = c->events.size();
-    c->events.resize(need);
-    for (size_t k = old; k < need; ++k) hipEventCreateWithFlags(&c->events[k], hipEventDefault);
+  b->n_seg = S;
+  // events: [0,1] hash; per segment 10 (prep, finish, miller, check, group); then [tail] 2 fallback
+  size_t need = 2 + 10 * S + 2;
+  if (b->ev.size() < need) {
+    size_t old = b->ev.size();
+    b->ev.resize(need);
+    for (size_t k = old; k < need; ++k) HIP_CHECK(c, hipEventCreateWithFlags(&b->ev[k], hipEventDefault));
   }
-  hipEvent_t* ev = c->events.data();
+  hipEvent_t* ev = b->ev.data();
   const size_t part_stride = b->G / 64 + b->G / 4096 + 4;
-  HIP_CHECK(c, hipMemsetAsync(b->n_fallback, 0, 4, sbs[0]));
-  hipEventRecord(ev[0], sbs[0]);
-  launch_hash_msgs(LaunchCfg{blocks_for(b->n_calls), TPB, sbs[0]}, b->msgs, (uint32_t)b->n_calls, b->H);
-  hipEventRecord(ev[1], sbs[0]);
-  HIP_CHECK(c, hipStreamWaitEvent(sbs[1], ev[1], 0));
+  HIP_CHECK(c, hipMemsetAsync(b->n_fallback, 0, 4, sh));
+  hipEventRecord(ev[0], sh);
+  launch_hash_msgs(LaunchCfg{blocks_for(b->n_calls), TPB, sh}, b->msgs, (uint32_t)b->n_calls, b->H);
+  hipEventRecord(ev[1], sh);
   for (size_t s = 0; s < S; ++s) {
-    hipEvent_t* e = ev + 3 + 8 * s;
+    hipEvent_t* e = ev + 2 + 10 * s;
     hipStream_t sb = sbs[s & 1];
     uint32_t g0 = gcut[s], G = gcut[s + 1] - gcut[s];
     uint32_t s0 = b->grp_off_host[g0], s1 = b->grp_off_host[gcut[s + 1]];
@@ -372,6 +392,7 @@ int gbv_sm_batch_verify(gbv_ctx* c, gbv_sm_batch* b, uint8_t* valid) {
                       nonce, b->S, b->rS, b->rP, b->status);
     hipEventRecord(e[1], sa);
     HIP_CHECK(c, hipStreamWaitEvent(sb, e[1], 0));
+    HIP_CHECK(c, hipStreamWaitEvent(sb, ev[1], 0));
     hipEventRecord(e[2], sb);
     launch_sm_chunk_finish(LaunchCfg{0, 64, sb}, g0, G, s0, b->grp_off, b->status, b->rS, b->rP, b->PgJ, b->SgJ, b->grp_state,
                            b->n_fallback);
@@ -384,49 +405,59 @@ int gbv_sm_batch_verify(gbv_ctx* c, gbv_sm_batch* b, uint8_t* valid) {
     launch_sm_seg_check(LaunchCfg{1, 64, sb}, g0, G, b->grp_state, b->F, b->SgJ, b->Fpart + po, b->Spart + po, b->has + po,
                         b->seg_ok + s);
     hipEventRecord(e[7], sb);
+    hipEventRecord(e[8], sb);
+    launch_sm_group_pairing(LaunchCfg{G, 64, sb}, g0, G, b->grp_msg, b->PgJ, b->SgJ, b->H, b->seg_ok + s, b->grp_state, b->n_fallback);
+    hipEventRecord(e[9], sb);
   }
-  HIP_CHECK(c, hipGetLastError());
-  HIP_CHECK(c, hipStreamSynchronize(sbs[1]));
-  HIP_CHECK(c, hipMemcpyAsync(b->seg_ok_host, b->seg_ok, S, hipMemcpyDeviceToHost, sbs[0]));
-  HIP_CHECK(c, hipStreamSynchronize(sbs[0]));
-  HIP_CHECK(c, hipStreamSynchronize(sa));
-  hipEvent_t* ep = ev + 3 + 8 * S;
-  bool any_fail = false;
-  hipEventRecord(ep[0], sa);
-  for (size_t s = 0; s < S; ++s) {
-    if (b->seg_ok_host[s]) continue;
-    any_fail = true;
-    uint32_t g0 = gcut[s], G = gcut[s + 1] - gcut[s];
-    launch_sm_group_pairing(LaunchCfg{G, 64, sa}, g0, G, b->grp_msg, b->PgJ, b->SgJ, b->H, b->grp_state, b->n_fallback);
+  hipEvent_t* ep = ev + 2 + 10 * S;
+  // the tail runs on B0 after everything of this batch (B1's last segment included)
+  if (S > 1) {
+    size_t last_b1 = (S - 1) & 1 ? S - 1 : S - 2;  // last segment that ran on B1
+    HIP_CHECK(c, hipStreamWaitEvent(sbs[0], ev[2 + 10 * last_b1 + 9], 0));
   }
-  hipEventRecord(ep[1], sa);
-  uint32_t nfb = 0;
-  HIP_CHECK(c, hipMemcpyAsync(&nfb, b->n_fallback, 4, hipMemcpyDeviceToHost, sa));
-  HIP_CHECK(c, hipStreamSynchronize(sa));
-  hipEventRecord(ep[2], sa);
-  launch_sm_fallback(LaunchCfg{blocks_for(b->n), TPB, sa}, (uint32_t)b->n, b->set_grp, b->grp_msg, b->grp_state, b->status, b->idx,
-                     c->table, b->S, b->H, b->valid, nfb ? 1 : 0);
-  hipEventRecord(ep[3], sa);
+  hipEventRecord(ep[0], sbs[0]);
+  launch_sm_fallback(LaunchCfg{blocks_for(b->n), TPB, sbs[0]}, (uint32_t)b->n, b->set_grp, b->grp_msg, b->grp_state, b->status, b->idx,
+                     c->table, b->S, b->H, b->valid, 1);
+  hipEventRecord(ep[1], sbs[0]);
+  HIP_CHECK(c, hipMemcpyAsync(b->valid_host, b->valid, b->n, hipMemcpyDeviceToHost, sbs[0]));
+  HIP_CHECK(c, hipEventRecord(b->done, sbs[0]));
   HIP_CHECK(c, hipGetLastError());
-  if (valid) HIP_CHECK(c, hipMemcpyAsync(valid, b->valid, b->n, hipMemcpyDeviceToHost, sa));
-  HIP_CHECK(c, hipStreamSynchronize(sa));
+  b->in_flight = true;
+  return GBV_OK;
+}
+
+int gbv_sm_batch_wait(gbv_ctx* c, gbv_sm_batch* b, uint8_t* valid) {
+  if (!c || !b) return GBV_E_ARG;
+  if (b->n == 0) return GBV_OK;
+  if (!b->in_flight) return fail(c, GBV_E_ARG, "batch not submitted");
+  HIP_CHECK(c, hipSetDevice(c->device));
+  b->in_flight = false;
+  HIP_CHECK(c, hipEventSynchronize(b->done));
+  if (valid) memcpy(valid, b->valid_host, b->n);
   for (auto& x : c->last_ms) x = 0.f;
   for (auto& x : c->last_launches) x = 0;
-  auto acc = [&](int k, hipEvent_t a0, hipEvent_t a1) {
+  hipEvent_t* ev = b->ev.data();
+  auto acc = [&](int k, hipEvent_t a0, hipEvent_t a1, bool count = true) {
     float ms = 0.f;
     if (hipEventElapsedTime(&ms, a0, a1) == hipSuccess) {
       c->last_ms[k] += ms;
-      c->last_launches[k] += 1;
+      c->last_launches[k] += count ? 1 : 0;
     }
   };
   acc(0, ev[0], ev[1]);
-  for (size_t s = 0; s < S; ++s) {
-    hipEvent_t* e = ev + 3 + 8 * s;
-    for (int k = 0; k < 4; ++k) acc(1 + k, e[2 * k], e[2 * k + 1]);
+  for (size_t s = 0; s < b->n_seg; ++s) {
+    hipEvent_t* e = ev + 2 + 10 * s;
+    for (int k = 0; k < 5; ++k) acc(1 + k, e[2 * k], e[2 * k + 1]);
   }
-  if (any_fail) acc(5, ep[0], ep[1]);
-  acc(6, ep[2], ep[3]);
+  hipEvent_t* ep = ev + 2 + 10 * b->n_seg;
+  acc(6, ep[0], ep[1]);
   return GBV_OK;
+}
+
+int gbv_sm_batch_verify(gbv_ctx* c, gbv_sm_batch* b, uint8_t* valid) {
+  int rc = gbv_sm_batch_submit(c, b);
+  if (rc) return rc;
+  return gbv_sm_batch_wait(c, b, valid);
 }
 
 int gbv_last_kernel_ms(gbv_ctx* c, float* out, int* launches, int max) {

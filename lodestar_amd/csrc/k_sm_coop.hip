@@ -74,13 +74,13 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
 // Failure path of a segment: each pending chunk on its own, e(P_g, H(m_g)) e(-g1, S_g) == 1
 // (verify(msg, aggPk, aggSig) of the chunk, maybeBatch.ts:34-38); one wave per chunk.
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_sm_group_pairing(uint32_t g0, const uint32_t* __restrict__ grp_msg, const G1J* __restrict__ PgJ,
-                                                         const G2J* __restrict__ SgJ, const G2A* __restrict__ H,
+                                                         const G2J* __restrict__ SgJ, const G2A* __restrict__ H, const uint8_t* __restrict__ seg_ok,
                                                          uint8_t* __restrict__ grp_state, uint32_t* __restrict__ n_fallback) {
   __shared__ Fp ws[SEG_WS];
   __shared__ Fp sa_lds[6];
   __shared__ int sa_ok;
   uint32_t g = g0 + blockIdx.x;
-  if (grp_state[g] != GRP_PENDING) return;
+  if (*seg_ok || grp_state[g] != GRP_PENDING) return;  // launched unconditionally: no host round trip
   unsigned lane = threadIdx.x;
   if (lane == 0) {
     G2A sa;
@@ -118,8 +118,8 @@ void launch_sm_seg_check(LaunchCfg c, uint32_t g0, uint32_t G, uint8_t* grp_stat
   debug_sync(c.stream, "k_sm_seg_check");
 }
 void launch_sm_group_pairing(LaunchCfg c, uint32_t g0, uint32_t G, const uint32_t* grp_msg, const G1J* PgJ, const G2J* SgJ, const G2A* H,
-                             uint8_t* grp_state, uint32_t* n_fallback) {
-  hipLaunchKernelGGL(k_sm_group_pairing, dim3(G), dim3(64), 0, c.stream, g0, grp_msg, PgJ, SgJ, H, grp_state, n_fallback);
+                             const uint8_t* seg_ok, uint8_t* grp_state, uint32_t* n_fallback) {
+  hipLaunchKernelGGL(k_sm_group_pairing, dim3(G), dim3(64), 0, c.stream, g0, grp_msg, PgJ, SgJ, H, seg_ok, grp_state, n_fallback);
   debug_sync(c.stream, "k_sm_group_pairing");
 }
 }  // namespace gbv

@@ -390,6 +390,19 @@ class StagedSameMessage:
         v.metrics["device_passes"] += 1
         return out.raw[:self.n] if want_results else None
 
+    def submit(self):
+        """Enqueue one verification and return at once (gbv_sm_batch_submit)."""
+        v = self._v
+        _native.check(v._lib, v._ctx, v._lib.gbv_sm_batch_submit(v._ctx, self._h))
+
+    def wait(self, want_results: bool = True):
+        """Block until the submitted verification is done (gbv_sm_batch_wait)."""
+        v = self._v
+        out = ctypes.create_string_buffer(max(self.n, 1)) if want_results else None
+        _native.check(v._lib, v._ctx, v._lib.gbv_sm_batch_wait(v._ctx, self._h, out))
+        v.metrics["device_passes"] += 1
+        return out.raw[:self.n] if want_results else None
+
     def close(self):
         if self._h:
             self._v._lib.gbv_sm_batch_destroy(self._v._ctx, self._h)
