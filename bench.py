@@ -33,11 +33,12 @@ N_VALIDATORS = 1 << 20
 N_KEYS = 1024
 # Algorithmic work per unit, in Fp-multiplication equivalents (FME; 1 FME = 300 u32 MACs,
 # 12-limb Montgomery), counted from the k_sm_prepare code path:
-#   G2 decompress 1230 (two 379-bit exponentiations, 606 + 605)  + G2 subgroup check 1170
-#   (63 dbl x 16 + 5 madd x 29 + psi)  + randomisation 2695 (4 table madds, one shared 381-bit
-#   inversion 608, affine tables ~40, G1 ladder 31 x 18, G2 ladder 31 x 45)  + per-wave chunk scan
-#   354 (6 levels x (43 + 16))  = 5450 per set.
-W_PREPARE_FME = 5450
+#   G2 decompress 952 (two 379-bit sliding-window exponentiations, 378 sqr + 86 mul each)
+#   + G2 subgroup check 1170 (63 dbl x 16 + 5 madd x 29 + psi)
+#   + randomisation 2088 (4 table madds, affine tables ~40, G1 ladder 31 x 18, G2 ladder 31 x 45;
+#     the shared inversion is a binary GCD: no multiplications, so it counts 1)
+#   + per-wave chunk scan 354 (6 levels x (43 + 16))  = 4564 per set.
+W_PREPARE_FME = 4564
 MAC_PER_FME = 300
 # Integer VALU peak: v_mad_u64_u32 measured at 37.0 T lane-ops/s on MI355X
 # (tools/ubench_int.hip, profiles/r01_ubench_int.txt); theoretical 256 CU x 4 SIMD x 16 lanes x 2.4 GHz = 39.3 T.

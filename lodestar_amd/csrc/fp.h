@@ -14,6 +14,14 @@
 
 namespace gbv {
 
+GBV_HD Fp fp_one_raw() {
+  Fp r;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) r.v[i] = i == 0 ? 1u : 0u;
+  return r;
+}
+#define FP_ONE_RAW_ fp_one_raw()
+
 GBV_HD Fp fp_zero() {
   Fp r;
 #pragma unroll
@@ -193,7 +201,77 @@ GBV_NI Fp fp_pow(Fp a, const uint32_t* e, int nbits) {
   return r;
 }
 
-GBV_HD Fp fp_inv(const Fp& a) { return fp_pow(a, EXP_INV, EXP_INV_BITS); }  // 0 -> 0
+// a^e for a fixed public exponent given as a sliding-window schedule (tools/gen_constants.py
+// c_sched): table of odd powers a^1..a^15, ~76 multiplications for a 379-bit exponent instead of
+// ~228 by square-and-multiply.  The table index is wave-uniform; picked with selects.
+GBV_NI Fp fp_pow_sched(Fp a, const uint8_t* nsq, const uint8_t* idx, int steps) {
+  Fp t[8];
+  t[0] = a;
+  Fp a2 = fp_sqr(a);
+#pragma unroll
+  for (int j = 1; j < 8; ++j) t[j] = fp_mul(t[j - 1], a2);
+  auto pick = [&](uint32_t k) {
+    Fp s = t[0];
+#pragma unroll
+    for (int j = 1; j < 8; ++j) s = fp_sel(k == (uint32_t)j, t[j], s);
+    return s;
+  };
+  Fp r = pick(idx[0]);
+  for (int s = 1; s < steps; ++s) {
+    for (int q = 0; q < nsq[s]; ++q) r = fp_sqr(r);
+    if (idx[s] != 255) r = fp_mul(r, pick(idx[s]));
+  }
+  return r;
+}
+
+GBV_HD Fp fp_inv_pow(const Fp& a) { return fp_pow(a, EXP_INV, EXP_INV_BITS); }  // 0 -> 0
+
+// x / 2 mod p (x < p): (x + (x odd ? p : 0)) >> 1, the sum < 2p < 2^382 never carries out
+GBV_HD Fp fp_half(const Fp& x) {
+  Fp t;
+  raw_add(t, x, P_RAW);
+  t = fp_sel(x.v[0] & 1u, t, x);
+  Fp r;
+#pragma unroll
+  for (int i = 0; i < 11; ++i) r.v[i] = (t.v[i] >> 1) | (t.v[i + 1] << 31);
+  r.v[11] = t.v[11] >> 1;
+  return r;
+}
+
+// Inverse by a branch-free binary extended GCD on the canonical value A = a R (Montgomery form
+// in, Montgomery form out, 0 -> 0).  Invariants u = A x1, v = A x2 (mod p), v odd:
+//   if u odd: (u < v ? swap(u,v), swap(x1,x2)); u -= v; x1 -= x2;   then u /= 2, x1 /= 2 (mod p)
+// until u == 0, when v = 1 and x2 = A^-1; the result is A^-1 R^3 R^-1 = a^-1 R.  Every lane runs
+// the same straight-line step (~190 VALU ops), checked for completion every 32 steps: about
+// 2.5x cheaper than the 381-bit exponentiation (608 Fp products) it replaces.
+GBV_NI Fp fp_inv(Fp a) {
+  Fp u = a, v = P_RAW, x1 = FP_ONE_RAW_, x2 = fp_zero();
+  for (int outer = 0; outer < 48; ++outer) {  // <= 2 * 381 steps are needed; 48 * 32 = 1536
+    for (int k = 0; k < 32; ++k) {
+      Fp d;
+      uint32_t lt = raw_sub(d, u, v);     // borrow: u < v
+      bool odd = u.v[0] & 1u;
+      bool sw = odd && lt;
+      Fp nu = fp_sel(sw, v, u), nv = fp_sel(sw, u, v);
+      Fp nx1 = fp_sel(sw, x2, x1), nx2 = fp_sel(sw, x1, x2);
+      raw_sub(d, nu, nv);
+      u = fp_sel(odd, d, nu);
+      v = nv;
+      x1 = fp_sel(odd, fp_sub(nx1, nx2), nx1);
+      x2 = nx2;
+#pragma unroll
+      for (int i = 0; i < 11; ++i) u.v[i] = (u.v[i] >> 1) | (u.v[i + 1] << 31);
+      u.v[11] >>= 1;
+      x1 = fp_half(x1);
+    }
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (!__any(!fp_is_zero(u))) break;
+#else
+    if (fp_is_zero(u)) break;
+#endif
+  }
+  return fp_mul(x2, R3_RAW);
+}
 
 // Canonical (non-Montgomery) value comparisons used by sign rules ----------------------------
 // true iff canonical(a) > (p-1)/2
@@ -238,6 +316,6 @@ GBV_HD bool fp_raw_is_canonical(const Fp& raw) {
 }
 
 // Square root candidate a^((p+1)/4); caller checks r^2 == a.
-GBV_HD Fp fp_sqrt_candidate(const Fp& a) { return fp_pow(a, EXP_SQRT, EXP_SQRT_BITS); }
+GBV_HD Fp fp_sqrt_candidate(const Fp& a) { return fp_pow_sched(a, SCHED_SQRT_NSQ, SCHED_SQRT_IDX, SCHED_SQRT_STEPS); }
 
 }  // namespace gbv

@@ -101,11 +101,11 @@ GBV_HD bool fp2_is_lexi_large(const Fp2& a) {
 // Returns true iff a is a square (root^2 == a).  Prototype: tests/test_algorithm_prototypes.py.
 GBV_HD bool fp2_sqrt(Fp2& root, const Fp2& a) {
   Fp n = fp_add(fp_sqr(a.c0), fp_sqr(a.c1));
-  Fp alpha = fp_pow(n, EXP_SQRT, EXP_SQRT_BITS);
+  Fp alpha = fp_pow_sched(n, SCHED_SQRT_NSQ, SCHED_SQRT_IDX, SCHED_SQRT_STEPS);
   Fp delta = fp_mul(fp_add(a.c0, alpha), FP_INV2);
   Fp delta2 = fp_mul(fp_sub(a.c0, alpha), FP_INV2);
   delta = fp_sel(fp_is_zero(delta), delta2, delta);
-  Fp t = fp_pow(delta, EXP_SQRT_M3, EXP_SQRT_M3_BITS);
+  Fp t = fp_pow_sched(delta, SCHED_SQRT_M3_NSQ, SCHED_SQRT_M3_IDX, SCHED_SQRT_M3_STEPS);
   Fp x0 = fp_mul(t, delta);
   bool qr = fp_eq(fp_mul(x0, t), FP_ONE);
   Fp h = fp_mul(fp_mul(a.c1, t), FP_INV2);

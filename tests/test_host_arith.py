@@ -54,6 +54,16 @@ def test_fp_mul_inv(lib):
         assert int.from_bytes(out.raw, "big") * a % o.P == 1
 
 
+def test_fp_inv_edges(lib):
+    """Binary-GCD inversion (fp.h fp_inv) at edge values; 0 maps to 0 like the exponentiation."""
+    out = buf(48)
+    for a in (1, 2, 3, o.P - 1, o.P - 2, (o.P - 1) // 2, 1 << 380, (1 << 381) % o.P, 0x1234567):
+        lib.ht_fp_inv(out, be(a))
+        assert int.from_bytes(out.raw, "big") * a % o.P == 1, hex(a)
+    lib.ht_fp_inv(out, be(0))
+    assert out.raw == bytes(48)
+
+
 def test_fp2_mul_sqrt(lib):
     rng = random.Random(2)
     for k in range(40):
