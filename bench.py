@@ -37,8 +37,8 @@ N_KEYS = 1024
 #   + G2 subgroup check 1170 (63 dbl x 16 + 5 madd x 29 + psi)
 #   + randomisation 2088 (4 table madds, affine tables ~40, G1 ladder 31 x 18, G2 ladder 31 x 45;
 #     the shared inversion is a binary GCD: no multiplications, so it counts 1)
-#   + per-wave chunk scan 354 (6 levels x (43 + 16))  = 4564 per set.
-W_PREPARE_FME = 4564
+#   + per-group chunk scan 177 (3 levels x (43 + 16))  = 4387 per set.
+W_PREPARE_FME = 4387
 MAC_PER_FME = 300
 # Integer VALU peak: v_mad_u64_u32 measured at 37.0 T lane-ops/s on MI355X
 # (tools/ubench_int.hip, profiles/r01_ubench_int.txt); theoretical 256 CU x 4 SIMD x 16 lanes x 2.4 GHz = 39.3 T.

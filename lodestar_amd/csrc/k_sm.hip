@@ -23,11 +23,12 @@ __device__ inline Fp12 shfl_down_fp12(const Fp12& a, unsigned d) { return Fp12{s
 GBV_NI G1J g1_add(G1J a, G1J b) { return jac_add(a, b); }
 GBV_NI G2J g2_add(G2J a, G2J b) { return jac_add(a, b); }
 // ---- same-message path ------------------------------------------------------------------------
+constexpr unsigned SCAN_W = 8;  // lanes per scan group (power of two, <= 64)
 // Per set: Signature.fromBytes(sig, true) (decode + subgroup), then the randomised terms
-// r_i sig_i, r_i pk_i of aggregateWithRandomness (jobItem.ts:73).  The wave then sums its terms
-// per chunk with a segmented suffix scan (6 levels of point additions for 64 sets -- <1% of the
-// per-set work) and the first lane of every chunk segment in the wave writes the segment's sum
-// at its own set index; k_sm_chunk_finish adds the <= ceil(len/64)+1 segment sums of a chunk.
+// r_i sig_i, r_i pk_i of aggregateWithRandomness (jobItem.ts:73).  Each group of SCAN_W lanes
+// then sums its terms per chunk with a segmented suffix scan (log2(SCAN_W) levels of point
+// additions) and the first lane of every chunk segment in the group writes the segment's sum at
+// its own set index; k_sm_chunk_finish adds the <= ceil(len/SCAN_W)+1 segment sums of a chunk.
 __global__ void GBV_KERNEL_ATTR k_sm_prepare(uint32_t base, uint32_t n, const uint32_t* __restrict__ idx, const uint8_t* __restrict__ sig96,
                                              const uint32_t* __restrict__ set_grp, const G1A* __restrict__ table,
                                              const uint8_t* __restrict__ table_ok, uint32_t table_n, Seed seed, uint32_t nonce,
@@ -58,24 +59,26 @@ __global__ void GBV_KERNEL_ATTR k_sm_prepare(uint32_t base, uint32_t n, const ui
       }
     }
   }
-  for (unsigned d = 1; d < 64; d <<= 1) {
+  // segmented suffix scan inside each group of SCAN_W lanes (3 levels: the whole wave pays every
+  // level, so fewer levels = less work here; k_sm_chunk_finish adds the group sums of a chunk)
+  for (unsigned d = 1; d < SCAN_W; d <<= 1) {
     G2J so = shfl_down_jac(rs, d);
     G1J po = shfl_down_jac(rp, d);
     uint32_t ko = __shfl_down(key, d, 64);
-    if (lane + d < 64 && ko == key) {
+    if ((lane & (SCAN_W - 1)) + d < SCAN_W && ko == key) {
       rs = g2_add(rs, so);
       rp = g1_add(rp, po);
     }
   }
   uint32_t kprev = __shfl_up(key, 1, 64);
-  if (act && (lane == 0 || kprev != key)) {
+  if (act && ((lane & (SCAN_W - 1)) == 0 || kprev != key)) {
     Sh_out[i] = rs;
     Ph_out[i] = rp;
   }
 }
 
 // Per chunk (one thread): P_g = sum r_i pk_i, S_g = sum r_i sig_i from the segment sums at the
-// chunk start and at every 64-set wave boundary inside it.  P_g stays Jacobian: the Miller loop
+// chunk start and at every SCAN_W-set group boundary inside it.  P_g stays Jacobian: the Miller loop
 // takes Jacobian P (lines scaled by Z^3, which the final exponentiation removes).  A chunk holding
 // a malformed / non-subgroup signature goes straight to the per-set retry, as
 // aggregateWithRandomness throwing does (index.ts:406-409).
@@ -92,7 +95,7 @@ __global__ void GBV_KERNEL_ATTR k_sm_chunk_finish(uint32_t g0, uint32_t G, uint3
   if (!bad) {
     G1J p = Ph[b];
     G2J s = Sh[b];
-    for (uint32_t q = s0 + ((b - s0) / 64 + 1) * 64; q < e; q += 64) {
+    for (uint32_t q = s0 + ((b - s0) / SCAN_W + 1) * SCAN_W; q < e; q += SCAN_W) {
       p = g1_add(p, Ph[q]);
       s = g2_add(s, Sh[q]);
     }
