@@ -367,11 +367,36 @@ template <class F> GBV_HD Aff<F> aff_from_jac_inv(const Jac<F>& p, const F& zinv
   return Aff<F>{f_mul(p.x, z2), f_mul(p.y, f_mul(z2, zinv))};
 }
 
+// Ladder tables S1 = P + E(P), S2 = P - E(P) live in a per-lane table object: registers on the
+// host / in the generic path, LDS in k_sm_prepare (the two affine G2 points are 96 VGPRs that
+// would otherwise be spilled to scratch around every out-of-line Fp product of the ladder).
+template <class A> struct RegTab2 {
+  A t[2];
+  GBV_HD A load(int k) const { return k ? t[1] : t[0]; }
+  GBV_HD void store(int k, const A& a) { t[k] = a; }
+};
+
+template <class F, class Tab> GBV_HD Jac<F> jac_mul_2d_signed_tab(const Tab& tab, uint32_t sa, uint32_t sb) {
+  auto pick = [&](int i) {
+    bool s = (sa >> i) & 1u, t = (sb >> i) & 1u;
+    Aff<F> T = tab.load(s == t ? 0 : 1);
+    T.y = f_sel(s, T.y, f_neg(T.y));
+    return T;
+  };
+  Jac<F> R = jac_from_aff(pick(31));
+  for (int i = 30; i >= 0; --i) {
+    R = jac_dbl(R);
+    R = jac_add_aff(R, pick(i));
+  }
+  return R;
+}
+
 // [r] P and [r] Q for the same batch scalar r (digits r64).  The four ladder tables
 // P +- phi(P), Q +- (-psi^2 Q) are made affine with ONE shared Fp inversion (Montgomery's trick
 // over z1 z2 N(Z1 Z2)).  Returns false only for points of small order (P = +-phi(P) etc.), which
 // subgroup-checked inputs never are; the caller then re-verifies that set unrandomised.
-GBV_NI bool randomize_pair(G1A P, G2A Q, uint64_t r64, G1J* rP, G2J* rQ) {
+template <class Tab1, class Tab2> GBV_HD bool randomize_pair_tab(const G1A& P, const G2A& Q, uint64_t r64, G1J* rP, G2J* rQ, Tab1& t1,
+                                                                 Tab2& t2) {
   G1A ph = g1_phi(P);
   G2A qh = g2_neg_psi2(Q);
   G1J a1 = jac_add_aff(jac_from_aff(P), ph);
@@ -387,14 +412,20 @@ GBV_NI bool randomize_pair(G1A P, G2A Q, uint64_t r64, G1J* rP, G2J* rQ) {
   Fp inv_u = fp_mul(inv, nW);
   Fp inv_nW = fp_mul(inv, u);
   Fp2 Winv = fp2_mul_fp(fp2_conj(W), inv_nW);
-  G1A P1 = aff_from_jac_inv(a1, fp_mul(a2.z, inv_u));
-  G1A P2 = aff_from_jac_inv(a2, fp_mul(a1.z, inv_u));
-  G2A Q1 = aff_from_jac_inv(b1, fp2_mul(b2.z, Winv));
-  G2A Q2 = aff_from_jac_inv(b2, fp2_mul(b1.z, Winv));
+  t1.store(0, aff_from_jac_inv(a1, fp_mul(a2.z, inv_u)));
+  t1.store(1, aff_from_jac_inv(a2, fp_mul(a1.z, inv_u)));
+  t2.store(0, aff_from_jac_inv(b1, fp2_mul(b2.z, Winv)));
+  t2.store(1, aff_from_jac_inv(b2, fp2_mul(b1.z, Winv)));
   uint32_t sa = (uint32_t)r64, sb = (uint32_t)(r64 >> 32);
-  *rP = jac_mul_2d_signed(P1, P2, sa, sb);
-  *rQ = jac_mul_2d_signed(Q1, Q2, sa, sb);
+  *rP = jac_mul_2d_signed_tab<Fp>(t1, sa, sb);
+  *rQ = jac_mul_2d_signed_tab<Fp2>(t2, sa, sb);
   return true;
+}
+
+GBV_NI bool randomize_pair(G1A P, G2A Q, uint64_t r64, G1J* rP, G2J* rQ) {
+  RegTab2<G1A> t1;
+  RegTab2<G2A> t2;
+  return randomize_pair_tab(P, Q, r64, rP, rQ, t1, t2);
 }
 
 }  // namespace gbv

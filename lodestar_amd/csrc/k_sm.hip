@@ -24,6 +24,7 @@ GBV_NI G1J g1_add(G1J a, G1J b) { return jac_add(a, b); }
 GBV_NI G2J g2_add(G2J a, G2J b) { return jac_add(a, b); }
 // ---- same-message path ------------------------------------------------------------------------
 constexpr unsigned SCAN_W = 8;  // lanes per scan group (power of two, <= 64)
+
 // Per set: Signature.fromBytes(sig, true) (decode + subgroup), then the randomised terms
 // r_i sig_i, r_i pk_i of aggregateWithRandomness (jobItem.ts:73).  Each group of SCAN_W lanes
 // then sums its terms per chunk with a segmented suffix scan (log2(SCAN_W) levels of point
