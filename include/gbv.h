@@ -114,6 +114,21 @@ int gbv_sm_batch_verify(gbv_ctx* ctx, gbv_sm_batch* b, uint8_t* valid);
 int gbv_sm_batch_submit(gbv_ctx* ctx, gbv_sm_batch* b);
 int gbv_sm_batch_wait(gbv_ctx* ctx, gbv_sm_batch* b, uint8_t* valid);
 void gbv_sm_batch_destroy(gbv_ctx* ctx, gbv_sm_batch* b);
+/* ---- multi-GPU verifySignatureSets (one process per GPU) ----------------------------------
+ * Sets shard across GPUs; each GPU reduces its shard to ONE Fp12 Miller product (its sets' pairs
+ * and its own (-g1, sum r_i sig_i) pair, no final exponentiation) -- an opaque 576-byte blob in
+ * the device's internal layout.  The blobs are all-gathered (RCCL over xGMI, 576 B per GPU) and
+ * every rank runs gbv_fp12_check on all of them: prod == 1 after ONE final exponentiation iff every
+ * set of every shard is valid (randomised batch verification, blst
+ * verifyMultipleAggregateSignatures semantics, replaces BlsMultiThreadWorkerPool.verifySignatureSets
+ * at multithread/index.ts:157-207 for calls too large for one device).  shard_ok = 0 when a set of
+ * the shard is malformed / not in the subgroup / has an infinity aggregate pubkey (the call is then
+ * false).  Empty aggregates reject like gbv_verify_sets. */
+#define GBV_FP12_PARTIAL_BYTES 576
+int gbv_vs_partial(gbv_ctx* ctx, const gbv_set* sets, size_t n, const uint32_t* index_arena,
+                   uint8_t out576[GBV_FP12_PARTIAL_BYTES], uint8_t* shard_ok);
+int gbv_fp12_check(gbv_ctx* ctx, const uint8_t* partials576, size_t k, uint8_t* is_one);
+
 /* Device time (ms, summed over launches) and launch count of each kernel of the last
  * gbv_sm_batch_verify, measured with HIP events on the stream each kernel runs on:
  * [hash, prepare, chunk_finish, miller, seg_check, group_pairing, fallback]; returns the number of

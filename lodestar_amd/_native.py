@@ -20,7 +20,7 @@ EXPORTED_SYMBOLS = (
     "gbv_init", "gbv_destroy", "gbv_last_error", "gbv_pubkeys_append", "gbv_pubkeys_count",
     "gbv_verify_sets", "gbv_verify_same_message", "gbv_verify_same_message_multi",
     "gbv_aggregate_pubkeys", "gbv_sm_batch_create", "gbv_sm_batch_verify", "gbv_sm_batch_destroy",
-    "gbv_sm_batch_submit", "gbv_sm_batch_wait",
+    "gbv_sm_batch_submit", "gbv_sm_batch_wait", "gbv_vs_partial", "gbv_fp12_check",
     "gbv_last_kernel_ms", "gbv_util_sk_to_pk", "gbv_util_sign", "gbv_util_hash_to_g2",
     "gbv_pubkeys_replicate",
 )
@@ -78,6 +78,8 @@ def load_library(path=LIB_PATH):
         "gbv_sm_batch_create": (i32, [vp, sz, vp, vp, vp, vp, P(vp)]),
         "gbv_sm_batch_verify": (i32, [vp, vp, vp]),
         "gbv_sm_batch_submit": (i32, [vp, vp]),
+        "gbv_vs_partial": (i32, [vp, P(GbvSet), sz, vp, vp, vp]),
+        "gbv_fp12_check": (i32, [vp, vp, sz, vp]),
         "gbv_sm_batch_wait": (i32, [vp, vp, vp]),
         "gbv_sm_batch_destroy": (None, [vp, vp]),
         "gbv_last_kernel_ms": (i32, [vp, P(ctypes.c_float), P(ctypes.c_int), i32]),

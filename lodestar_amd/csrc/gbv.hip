@@ -95,6 +95,27 @@ template <class T> static hipError_t dalloc(T** p, size_t count) {
   return hipMalloc((void**)p, std::max<size_t>(count, 1) * sizeof(T));
 }
 
+// Fp is a 12 x u32 ext_vector (64-byte slots in memory); the C ABI's Fp12 blobs are packed to
+// 12 x 48 bytes of little-endian limbs.
+static void fp12_pack(uint8_t* out576, const Fp12& a) {
+  const Fp* f = (const Fp*)&a;
+  for (int i = 0; i < 12; ++i) memcpy(out576 + 48 * i, &f[i], 48);
+}
+static Fp12 fp12_unpack(const uint8_t* in576) {
+  Fp12 r;
+  memset(&r, 0, sizeof(r));
+  Fp* f = (Fp*)&r;
+  for (int i = 0; i < 12; ++i) memcpy(&f[i], in576 + 48 * i, 48);
+  return r;
+}
+
+static Fp12 fp12_one_host() {
+  Fp12 r;
+  memset(&r, 0, sizeof(r));
+  r.c0.c0.c0 = FP_ONE;
+  return r;
+}
+
 static Seed fresh_seed() {
   Seed s;
   size_t got = 0;
@@ -486,12 +507,22 @@ int gbv_verify_same_message(gbv_ctx* c, const uint32_t* idx, const uint8_t* sigs
 }
 
 // ---- distinct-message sets -----------------------------------------------------------------
-int gbv_verify_sets(gbv_ctx* c, const gbv_set* sets, size_t n, const uint32_t* arena, uint8_t* all_valid, uint8_t* chunk_valid) {
-  if (!c || !all_valid) return GBV_E_ARG;
-  if (c->closed) return GBV_E_CLOSED;
-  *all_valid = 0;
+// Device buffers of one staged verifySignatureSets call after k_vs_prepare.
+struct VsDev {
+  uint32_t *off = nullptr, *idx = nullptr, *siglen = nullptr;
+  uint8_t *raw_flag = nullptr, *raw_pk = nullptr, *msgs = nullptr, *sig = nullptr, *status = nullptr;
+  Fp12* f = nullptr;
+  G2J* rS = nullptr;
+  void release() {
+    hipFree(off); hipFree(idx); hipFree(siglen); hipFree(raw_flag); hipFree(raw_pk); hipFree(msgs); hipFree(sig);
+    hipFree(status); hipFree(f); hipFree(rS);
+  }
+};
+
+// Argument checks shared by the verifySignatureSets entry points: empty aggregates reject the
+// whole call before any verification (aggregatePublicKeys throws, index.ts:398-412).
+static int vs_check_args(gbv_ctx* c, const gbv_set* sets, size_t n, const uint32_t* arena) {
   if (n && !sets) return fail(c, GBV_E_ARG, "null sets");
-  // aggregation throws before any verification: the whole call rejects (index.ts:398-412)
   for (size_t i = 0; i < n; ++i)
     if (!sets[i].raw_pk48 && sets[i].idx_len == 0) return fail(c, GBV_E_EMPTY_AGGREGATE, "EMPTY_AGGREGATE_ARRAY");
   for (size_t i = 0; i < n; ++i) {
@@ -502,12 +533,12 @@ int gbv_verify_sets(gbv_ctx* c, const gbv_set* sets, size_t n, const uint32_t* a
         if (arena[sets[i].idx_off + j] >= c->table_n) return fail(c, GBV_E_ARG, "validator index out of range");
     }
   }
-  if (n == 0) {  // verifySignatureSetsMaybeBatch([]) throws -> false (maybeBatch.ts:29-31,39-44)
-    if (chunk_valid) chunk_valid[0] = 0;
-    return GBV_OK;
-  }
-  std::vector<uint32_t> co = chunk_offsets((uint32_t)n, MAX_SIGNATURE_SETS_PER_JOB);
-  size_t C = co.size() - 1;
+  return GBV_OK;
+}
+
+// Stage n > 0 sets in HBM and run k_vs_prepare (per set: pubkey aggregate / decode, signature
+// decode + subgroup, randomisation, hash_to_G2, Miller value) on stream s.
+static int vs_stage_prepare(gbv_ctx* c, const gbv_set* sets, size_t n, const uint32_t* arena, hipStream_t s, VsDev& d) {
   uint32_t stride = 96;
   for (size_t i = 0; i < n; ++i)
     if (sets[i].sig_len == 192) stride = 192;
@@ -527,39 +558,124 @@ int gbv_verify_sets(gbv_ctx* c, const gbv_set* sets, size_t n, const uint32_t* a
     if (sig_len[i]) memcpy(&sig[(size_t)stride * i], sets[i].sig, L);
   }
   set_idx_off[n] = (uint32_t)idx_flat.size();
-  HIP_CHECK(c, hipSetDevice(c->device));
-  hipStream_t s = c->stream;
-  uint32_t *d_off, *d_idx, *d_siglen, *d_chunk_off;
-  uint8_t *d_raw_flag, *d_raw_pk, *d_msgs, *d_sig, *d_status, *d_cv;
-  Fp12* d_f;
-  G2J* d_rS;
-  HIP_CHECK(c, dalloc(&d_off, n + 1)); HIP_CHECK(c, dalloc(&d_idx, idx_flat.size())); HIP_CHECK(c, dalloc(&d_siglen, n));
-  HIP_CHECK(c, dalloc(&d_chunk_off, C + 1)); HIP_CHECK(c, dalloc(&d_raw_flag, n)); HIP_CHECK(c, dalloc(&d_raw_pk, 48 * n));
-  HIP_CHECK(c, dalloc(&d_msgs, 32 * n)); HIP_CHECK(c, dalloc(&d_sig, (size_t)stride * n)); HIP_CHECK(c, dalloc(&d_status, n));
-  HIP_CHECK(c, dalloc(&d_cv, C)); HIP_CHECK(c, dalloc(&d_f, n)); HIP_CHECK(c, dalloc(&d_rS, n));
-  HIP_CHECK(c, hipMemcpyAsync(d_off, set_idx_off.data(), 4 * (n + 1), hipMemcpyHostToDevice, s));
-  if (!idx_flat.empty()) HIP_CHECK(c, hipMemcpyAsync(d_idx, idx_flat.data(), 4 * idx_flat.size(), hipMemcpyHostToDevice, s));
-  HIP_CHECK(c, hipMemcpyAsync(d_siglen, sig_len.data(), 4 * n, hipMemcpyHostToDevice, s));
-  HIP_CHECK(c, hipMemcpyAsync(d_chunk_off, co.data(), 4 * (C + 1), hipMemcpyHostToDevice, s));
-  HIP_CHECK(c, hipMemcpyAsync(d_raw_flag, raw_flag.data(), n, hipMemcpyHostToDevice, s));
-  HIP_CHECK(c, hipMemcpyAsync(d_raw_pk, raw_pk.data(), 48 * n, hipMemcpyHostToDevice, s));
-  HIP_CHECK(c, hipMemcpyAsync(d_msgs, msgs.data(), 32 * n, hipMemcpyHostToDevice, s));
-  HIP_CHECK(c, hipMemcpyAsync(d_sig, sig.data(), (size_t)stride * n, hipMemcpyHostToDevice, s));
+  HIP_CHECK(c, dalloc(&d.off, n + 1)); HIP_CHECK(c, dalloc(&d.idx, idx_flat.size())); HIP_CHECK(c, dalloc(&d.siglen, n));
+  HIP_CHECK(c, dalloc(&d.raw_flag, n)); HIP_CHECK(c, dalloc(&d.raw_pk, 48 * n)); HIP_CHECK(c, dalloc(&d.msgs, 32 * n));
+  HIP_CHECK(c, dalloc(&d.sig, (size_t)stride * n)); HIP_CHECK(c, dalloc(&d.status, n)); HIP_CHECK(c, dalloc(&d.f, n));
+  HIP_CHECK(c, dalloc(&d.rS, n));
+  HIP_CHECK(c, hipMemcpyAsync(d.off, set_idx_off.data(), 4 * (n + 1), hipMemcpyHostToDevice, s));
+  if (!idx_flat.empty()) HIP_CHECK(c, hipMemcpyAsync(d.idx, idx_flat.data(), 4 * idx_flat.size(), hipMemcpyHostToDevice, s));
+  HIP_CHECK(c, hipMemcpyAsync(d.siglen, sig_len.data(), 4 * n, hipMemcpyHostToDevice, s));
+  HIP_CHECK(c, hipMemcpyAsync(d.raw_flag, raw_flag.data(), n, hipMemcpyHostToDevice, s));
+  HIP_CHECK(c, hipMemcpyAsync(d.raw_pk, raw_pk.data(), 48 * n, hipMemcpyHostToDevice, s));
+  HIP_CHECK(c, hipMemcpyAsync(d.msgs, msgs.data(), 32 * n, hipMemcpyHostToDevice, s));
+  HIP_CHECK(c, hipMemcpyAsync(d.sig, sig.data(), (size_t)stride * n, hipMemcpyHostToDevice, s));
   Seed seed = fresh_seed();
   uint32_t nonce = c->nonce++;
-  launch_vs_prepare(LaunchCfg{blocks_for(n), TPB, s}, (uint32_t)n, d_off, d_idx, d_raw_flag, d_raw_pk, d_msgs, d_sig,
-                     stride, d_siglen, c->table, c->table_ok, seed, nonce, d_f, d_rS, d_status);
-  launch_vs_chunk(LaunchCfg{blocks_for(C), TPB, s}, (uint32_t)C, d_chunk_off, d_status, d_f, d_rS, d_cv);
+  launch_vs_prepare(LaunchCfg{blocks_for(n), TPB, s}, (uint32_t)n, d.off, d.idx, d.raw_flag, d.raw_pk, d.msgs, d.sig, stride, d.siglen,
+                    c->table, c->table_ok, seed, nonce, d.f, d.rS, d.status);
   HIP_CHECK(c, hipGetLastError());
-  std::vector<uint8_t> cv(C);
-  HIP_CHECK(c, hipMemcpyAsync(cv.data(), d_cv, C, hipMemcpyDeviceToHost, s));
+  // the host vectors above are freed on return: the copies must have landed
   HIP_CHECK(c, hipStreamSynchronize(s));
-  hipFree(d_off); hipFree(d_idx); hipFree(d_siglen); hipFree(d_chunk_off); hipFree(d_raw_flag); hipFree(d_raw_pk);
-  hipFree(d_msgs); hipFree(d_sig); hipFree(d_status); hipFree(d_cv); hipFree(d_f); hipFree(d_rS);
-  uint8_t all = 1;
-  for (size_t k = 0; k < C; ++k) all &= cv[k];
-  *all_valid = all;
-  if (chunk_valid) memcpy(chunk_valid, cv.data(), C);
+  return GBV_OK;
+}
+
+int gbv_verify_sets(gbv_ctx* c, const gbv_set* sets, size_t n, const uint32_t* arena, uint8_t* all_valid, uint8_t* chunk_valid) {
+  if (!c || !all_valid) return GBV_E_ARG;
+  if (c->closed) return GBV_E_CLOSED;
+  *all_valid = 0;
+  int rc = vs_check_args(c, sets, n, arena);
+  if (rc) return rc;
+  if (n == 0) {  // verifySignatureSetsMaybeBatch([]) throws -> false (maybeBatch.ts:29-31,39-44)
+    if (chunk_valid) chunk_valid[0] = 0;
+    return GBV_OK;
+  }
+  HIP_CHECK(c, hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  std::vector<uint32_t> co = chunk_offsets((uint32_t)n, MAX_SIGNATURE_SETS_PER_JOB);
+  size_t C = co.size() - 1;
+  VsDev d;
+  uint32_t* d_chunk_off = nullptr;
+  uint8_t* d_cv = nullptr;
+  rc = vs_stage_prepare(c, sets, n, arena, s, d);
+  if (rc == GBV_OK) {
+    HIP_CHECK(c, dalloc(&d_chunk_off, C + 1));
+    HIP_CHECK(c, dalloc(&d_cv, C));
+    HIP_CHECK(c, hipMemcpyAsync(d_chunk_off, co.data(), 4 * (C + 1), hipMemcpyHostToDevice, s));
+    launch_vs_chunk_coop(LaunchCfg{(unsigned)C, 64, s}, (uint32_t)C, d_chunk_off, d.status, d.f, d.rS, d_cv);
+    HIP_CHECK(c, hipGetLastError());
+    std::vector<uint8_t> cv(C);
+    HIP_CHECK(c, hipMemcpyAsync(cv.data(), d_cv, C, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(c, hipStreamSynchronize(s));
+    uint8_t all = 1;
+    for (size_t k = 0; k < C; ++k) all &= cv[k];
+    *all_valid = all;
+    if (chunk_valid) memcpy(chunk_valid, cv.data(), C);
+  }
+  d.release();
+  hipFree(d_chunk_off);
+  hipFree(d_cv);
+  return rc;
+}
+
+// One shard of a verifySignatureSets call spread over several GPUs.
+int gbv_vs_partial(gbv_ctx* c, const gbv_set* sets, size_t n, const uint32_t* arena, uint8_t out576[GBV_FP12_PARTIAL_BYTES],
+                   uint8_t* shard_ok) {
+  if (!c || !out576 || !shard_ok) return GBV_E_ARG;
+  if (c->closed) return GBV_E_CLOSED;
+  int rc = vs_check_args(c, sets, n, arena);
+  if (rc) return rc;
+  *shard_ok = 1;
+  Fp12 one = fp12_one_host();
+  if (n == 0) {
+    fp12_pack(out576, one);
+    return GBV_OK;
+  }
+  HIP_CHECK(c, hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  VsDev d;
+  rc = vs_stage_prepare(c, sets, n, arena, s, d);
+  Fp12 *part = nullptr, *d_out = nullptr;
+  G2J* spart = nullptr;
+  uint8_t *has = nullptr, *d_flag = nullptr;
+  if (rc == GBV_OK) {
+    size_t np = n / 64 + n / 4096 + 4;
+    HIP_CHECK(c, dalloc(&part, np)); HIP_CHECK(c, dalloc(&spart, np)); HIP_CHECK(c, dalloc(&has, np));
+    HIP_CHECK(c, dalloc(&d_out, 1)); HIP_CHECK(c, dalloc(&d_flag, 1));
+    // status doubles as the per-"chunk" state: SET_OK == GRP_PENDING (every valid set takes part)
+    launch_sm_seg_check(LaunchCfg{1, 64, s}, 0, (uint32_t)n, d.status, d.f, d.rS, part, spart, has, d_flag, d_out);
+    HIP_CHECK(c, hipGetLastError());
+    std::vector<uint8_t> st(n);
+    HIP_CHECK(c, hipMemcpyAsync(st.data(), d.status, n, hipMemcpyDeviceToHost, s));
+    Fp12 h;
+    HIP_CHECK(c, hipMemcpyAsync(&h, d_out, sizeof(Fp12), hipMemcpyDeviceToHost, s));
+    HIP_CHECK(c, hipStreamSynchronize(s));
+    fp12_pack(out576, h);
+    for (size_t i = 0; i < n; ++i)
+      if (st[i] != SET_OK) *shard_ok = 0;
+  }
+  d.release();
+  hipFree(part); hipFree(spart); hipFree(has); hipFree(d_out); hipFree(d_flag);
+  return rc;
+}
+
+int gbv_fp12_check(gbv_ctx* c, const uint8_t* partials, size_t k, uint8_t* is_one) {
+  if (!c || !is_one || (k && !partials)) return GBV_E_ARG;
+  if (c->closed) return GBV_E_CLOSED;
+  HIP_CHECK(c, hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  Fp12* d_p = nullptr;
+  uint8_t* d_o = nullptr;
+  HIP_CHECK(c, dalloc(&d_p, k));
+  HIP_CHECK(c, dalloc(&d_o, 1));
+  std::vector<Fp12> hp(k);
+  for (size_t j = 0; j < k; ++j) hp[j] = fp12_unpack(partials + GBV_FP12_PARTIAL_BYTES * j);
+  if (k) HIP_CHECK(c, hipMemcpyAsync(d_p, hp.data(), sizeof(Fp12) * k, hipMemcpyHostToDevice, s));
+  launch_fp12_check(LaunchCfg{1, 64, s}, (uint32_t)k, d_p, d_o);
+  HIP_CHECK(c, hipGetLastError());
+  HIP_CHECK(c, hipMemcpyAsync(is_one, d_o, 1, hipMemcpyDeviceToHost, s));
+  HIP_CHECK(c, hipStreamSynchronize(s));
+  hipFree(d_p);
+  hipFree(d_o);
   return GBV_OK;
 }
 

@@ -10,6 +10,39 @@ namespace gbv {
 GBV_NI G2J g2_add_j(G2J a, G2J b) { return jac_add(a, b); }
 #define g2_add g2_add_j
 
+__device__ inline Fp shfl_down_fp_c(const Fp& a, unsigned d) {
+  Fp r;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) r.v[i] = __shfl_down((unsigned)a.v[i], d, 64);
+  return r;
+}
+
+// cross-lane tree: lane 0 ends with the product of the lanes' f and the sum of their s
+__device__ inline void wave_reduce_fs_coop(Fp12& f, G2J& s, int& any) {
+  unsigned lane = threadIdx.x;
+  for (unsigned d = 32; d >= 1; d >>= 1) {
+    Fp12 fo;
+    G2J so;
+    Fp* fd = (Fp*)&fo;
+    const Fp* fsrc = (const Fp*)&f;
+    for (int i = 0; i < 12; ++i) fd[i] = shfl_down_fp_c(fsrc[i], d);
+    Fp* sd = (Fp*)&so;
+    const Fp* ssrc = (const Fp*)&s;
+    for (int i = 0; i < 6; ++i) sd[i] = shfl_down_fp_c(ssrc[i], d);
+    int ao = __shfl_down(any, d, 64);
+    if (lane < d && ao) {
+      f = any ? fp12_mul(f, fo) : fo;
+      s = any ? g2_add(s, so) : so;
+      any = 1;
+    }
+  }
+}
+
+__device__ inline void store12(Fp* dst, const Fp12& a) {
+  const Fp* s = (const Fp*)&a;
+  for (int i = 0; i < 12; ++i) dst[i] = s[i];
+}
+
 // One wave per segment: the randomised chunk equations of the whole segment are folded into one
 // check  prod_g e(P_g, H(m_g)) * e(-g1, sum_g S_g) == 1  with ONE final exponentiation.  Every
 // set carries its own random 64-bit scalar, so this is blst's verifyMultipleAggregateSignatures
@@ -19,7 +52,8 @@ GBV_NI G2J g2_add_j(G2J a, G2J b) { return jac_add(a, b); }
 constexpr int SEG_WS = coop::MILLER_WS + coop::FINAL_EXP_WS;
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_sm_seg_check(uint32_t g0, uint32_t G, uint32_t nb, const Fp12* __restrict__ Fpart,
                                                      const G2J* __restrict__ Spart, const uint8_t* __restrict__ has,
-                                                     uint8_t* __restrict__ grp_state, uint8_t* __restrict__ seg_ok) {
+                                                     uint8_t* __restrict__ grp_state, uint8_t* __restrict__ seg_ok,
+                                                     Fp12* __restrict__ miller_out) {
   __shared__ Fp ws[SEG_WS];
   __shared__ int flags[2];
   Fp* ml = ws;
@@ -63,7 +97,12 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
       coop::miller_loop(ml, 1);
       coop::mul12(ws, coop::MILLER_WS + coop::E_Z, coop::MILLER_WS + coop::E_F, coop::M_F, coop::MILLER_WS + coop::E_F);
     }
-    ok = coop::final_exp_is_one(fe) ? 1 : 0;
+    if (!miller_out) ok = coop::final_exp_is_one(fe) ? 1 : 0;
+  }
+  if (miller_out) {  // shard mode: hand out the Miller product, the caller combines shards
+    if (lane < 12) ((Fp*)miller_out)[lane] = fe[coop::E_F + lane];
+    if (lane == 0) seg_ok[0] = (uint8_t)flags[0];
+    return;
   }
   if (lane == 0) seg_ok[0] = (uint8_t)ok;
   if (!ok) return;
@@ -111,15 +150,94 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
 
 
 void launch_sm_seg_check(LaunchCfg c, uint32_t g0, uint32_t G, uint8_t* grp_state, const Fp12* F, const G2J* SgJ, Fp12* Fpart, G2J* Spart,
-                         uint8_t* has, uint8_t* seg_ok) {
+                         uint8_t* has, uint8_t* seg_ok, Fp12* miller_out) {
   uint32_t nb = 0;
   uint32_t off = launch_sm_seg_reduce(c, g0, G, grp_state, F, SgJ, Fpart, Spart, has, &nb);
-  hipLaunchKernelGGL(k_sm_seg_check, dim3(1), dim3(64), 0, c.stream, g0, G, nb, Fpart + off, Spart + off, has + off, grp_state, seg_ok);
+  hipLaunchKernelGGL(k_sm_seg_check, dim3(1), dim3(64), 0, c.stream, g0, G, nb, Fpart + off, Spart + off, has + off, grp_state, seg_ok,
+                     miller_out);
   debug_sync(c.stream, "k_sm_seg_check");
 }
 void launch_sm_group_pairing(LaunchCfg c, uint32_t g0, uint32_t G, const uint32_t* grp_msg, const G1J* PgJ, const G2J* SgJ, const G2A* H,
                              const uint8_t* seg_ok, uint8_t* grp_state, uint32_t* n_fallback) {
   hipLaunchKernelGGL(k_sm_group_pairing, dim3(G), dim3(64), 0, c.stream, g0, grp_msg, PgJ, SgJ, H, seg_ok, grp_state, n_fallback);
   debug_sync(c.stream, "k_sm_group_pairing");
+}
+// Product of k Fp12 Miller partials (one per shard / GPU) and ONE final exponentiation == 1?
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
+k_fp12_check(uint32_t k, const Fp12* __restrict__ parts, uint8_t* __restrict__ out) {
+  __shared__ Fp ws[coop::FINAL_EXP_WS];
+  unsigned lane = threadIdx.x;
+  coop::set_one12(ws + coop::E_F);
+  for (uint32_t j = 0; j < k; ++j) {
+    if (lane < 12) ws[coop::E_TMP + lane] = ((const Fp*)&parts[j])[lane];
+    coop::barrier();
+    coop::mul12(ws, coop::E_Z, coop::E_F, coop::E_TMP, coop::E_F);
+  }
+  bool ok = coop::final_exp_is_one(ws);
+  if (lane == 0) out[0] = ok ? 1 : 0;
+}
+
+// verifySignatureSets chunks (<= 255 sets each, chunkifyMaximizeChunkSize): one wave per chunk
+// multiplies its sets' Miller values and sums r_i sig_i (cross-lane tree), then runs the
+// (-g1, sum) pair and the final exponentiation cooperatively (maybeBatch.ts:17-26).
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
+k_vs_chunk_coop(const uint32_t* __restrict__ chunk_off, const uint8_t* __restrict__ status, const Fp12* __restrict__ f,
+                const G2J* __restrict__ rS, uint8_t* __restrict__ chunk_valid) {
+  __shared__ Fp ws[SEG_WS];
+  __shared__ int flags[2];
+  Fp* ml = ws;
+  Fp* fe = ws + coop::MILLER_WS;
+  unsigned lane = threadIdx.x;
+  uint32_t c = blockIdx.x;
+  uint32_t b = chunk_off[c], e = chunk_off[c + 1];
+  int bad = b == e;
+  int any = 0;
+  Fp12 acc = fp12_one();
+  G2J s = jac_infinity<Fp2>();
+  for (uint32_t i = b + lane; i < e; i += 64) {
+    if (status[i] != SET_OK) {
+      bad = 1;
+      continue;
+    }
+    acc = any ? fp12_mul(acc, f[i]) : f[i];
+    s = any ? g2_add(s, rS[i]) : rS[i];
+    any = 1;
+  }
+  if (__any(bad)) {
+    if (lane == 0) chunk_valid[c] = 0;
+    return;
+  }
+  wave_reduce_fs_coop(acc, s, any);
+  if (lane == 0) {
+    G2A sa;
+    flags[0] = jac_to_aff(sa, s) ? 1 : 0;
+    store12(fe + coop::E_F, acc);
+    G1A ng = g1_neg_generator();
+    fe[coop::E_TMP2 + 0] = ng.x;
+    fe[coop::E_TMP2 + 1] = ng.y;
+    fe[coop::E_TMP2 + 2] = sa.x.c0;
+    fe[coop::E_TMP2 + 3] = sa.x.c1;
+    fe[coop::E_TMP2 + 4] = sa.y.c0;
+    fe[coop::E_TMP2 + 5] = sa.y.c1;
+  }
+  coop::barrier();
+  if (flags[0]) {
+    const Fp* st = fe + coop::E_TMP2;
+    coop::miller_load_pair(ml, 0, G1A{st[0], st[1]}, G2A{Fp2{st[2], st[3]}, Fp2{st[4], st[5]}});
+    coop::miller_loop(ml, 1);
+    coop::mul12(ws, coop::MILLER_WS + coop::E_Z, coop::MILLER_WS + coop::E_F, coop::M_F, coop::MILLER_WS + coop::E_F);
+  }
+  bool ok = coop::final_exp_is_one(fe);
+  if (lane == 0) chunk_valid[c] = ok ? 1 : 0;
+}
+
+void launch_fp12_check(LaunchCfg c, uint32_t k, const Fp12* parts, uint8_t* out) {
+  hipLaunchKernelGGL(k_fp12_check, dim3(1), dim3(64), 0, c.stream, k, parts, out);
+  debug_sync(c.stream, "k_fp12_check");
+}
+void launch_vs_chunk_coop(LaunchCfg c, uint32_t C, const uint32_t* chunk_off, const uint8_t* status, const Fp12* f, const G2J* rS,
+                          uint8_t* chunk_valid) {
+  hipLaunchKernelGGL(k_vs_chunk_coop, dim3(C), dim3(64), 0, c.stream, chunk_off, status, f, rS, chunk_valid);
+  debug_sync(c.stream, "k_vs_chunk_coop");
 }
 }  // namespace gbv

@@ -50,33 +50,6 @@ __global__ void GBV_KERNEL_ATTR k_vs_prepare(uint32_t n, const uint32_t* __restr
   f_out[i] = miller_loop_1j(rp, h);
 }
 
-__global__ void GBV_KERNEL_ATTR k_vs_chunk(uint32_t C, const uint32_t* __restrict__ chunk_off, const uint8_t* __restrict__ status,
-                                                 const Fp12* __restrict__ f, const G2J* __restrict__ rS, uint8_t* __restrict__ chunk_valid) {
-  uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  uint32_t b = chunk_off[c], e = chunk_off[c + 1];
-  bool ok = b < e;
-  for (uint32_t i = b; i < e; ++i) ok &= status[i] == SET_OK;
-  if (!ok) {
-    chunk_valid[c] = 0;
-    return;
-  }
-  Fp12 acc = f[b];
-  G2J s = rS[b];
-  for (uint32_t i = b + 1; i < e; ++i) {
-    acc = fp12_mul(acc, f[i]);
-    s = jac_add(s, rS[i]);
-  }
-  G2A sa;
-  if (!jac_to_aff(sa, s)) {
-    chunk_valid[c] = 0;
-    return;
-  }
-  acc = fp12_mul(acc, miller_loop_1(g1_neg_generator(), sa));
-  chunk_valid[c] = fp12_is_one(final_exponentiation(acc)) ? 1 : 0;
-}
-
-
 void launch_vs_prepare(LaunchCfg c, uint32_t n, const uint32_t* set_idx_off, const uint32_t* idx, const uint8_t* raw_flag,
                        const uint8_t* raw_pk48, const uint8_t* msgs32, const uint8_t* sig, uint32_t sig_stride, const uint32_t* sig_len,
                        const G1A* table, const uint8_t* table_ok, const Seed& seed, uint32_t nonce, Fp12* f_out, G2J* rS_out,
@@ -84,10 +57,5 @@ void launch_vs_prepare(LaunchCfg c, uint32_t n, const uint32_t* set_idx_off, con
   hipLaunchKernelGGL(k_vs_prepare, dim3(c.blocks), dim3(c.threads), 0, c.stream, n, set_idx_off, idx, raw_flag, raw_pk48, msgs32, sig,
                      sig_stride, sig_len, table, table_ok, seed, nonce, f_out, rS_out, status);
   debug_sync(c.stream, "k_vs_prepare");
-}
-void launch_vs_chunk(LaunchCfg c, uint32_t C, const uint32_t* chunk_off, const uint8_t* status, const Fp12* f, const G2J* rS,
-                     uint8_t* chunk_valid) {
-  hipLaunchKernelGGL(k_vs_chunk, dim3(c.blocks), dim3(c.threads), 0, c.stream, C, chunk_off, status, f, rS, chunk_valid);
-  debug_sync(c.stream, "k_vs_chunk");
 }
 }  // namespace gbv

@@ -15,7 +15,9 @@
 //   k_sm_fallback       retry each set individually (jobItem.ts:93-125)
 //   k_vs_prepare        per-set part of verifyMultipleAggregateSignatures (+ aggregatePublicKeys
 //                       of index lists, bls/utils.ts:5-20)
-//   k_vs_chunk          per-chunk multi-pairing product + one final exponentiation (maybeBatch.ts:17-26)
+//   k_vs_chunk_coop     per-chunk multi-pairing product + one final exponentiation, one wave per chunk
+//                       (maybeBatch.ts:17-26)
+//   k_fp12_check        product of per-GPU Miller partials + one final exponentiation (multi-GPU)
 #pragma once
 #include "hash_to_curve.h"
 #include "pairing.h"

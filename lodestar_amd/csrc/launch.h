@@ -22,7 +22,10 @@ void launch_sm_miller(LaunchCfg c, uint32_t g0, uint32_t G, const uint32_t* grp_
 uint32_t launch_sm_seg_reduce(LaunchCfg c, uint32_t g0, uint32_t G, const uint8_t* grp_state, const Fp12* F, const G2J* SgJ, Fp12* Fpart,
                               G2J* Spart, uint8_t* has, uint32_t* n_out);
 void launch_sm_seg_check(LaunchCfg c, uint32_t g0, uint32_t G, uint8_t* grp_state, const Fp12* F, const G2J* SgJ, Fp12* Fpart, G2J* Spart,
-                         uint8_t* has, uint8_t* seg_ok);
+                         uint8_t* has, uint8_t* seg_ok, Fp12* miller_out = nullptr);
+void launch_fp12_check(LaunchCfg c, uint32_t k, const Fp12* parts, uint8_t* out);
+void launch_vs_chunk_coop(LaunchCfg c, uint32_t C, const uint32_t* chunk_off, const uint8_t* status, const Fp12* f, const G2J* rS,
+                          uint8_t* chunk_valid);
 void launch_sm_group_pairing(LaunchCfg c, uint32_t g0, uint32_t G, const uint32_t* grp_msg, const G1J* PgJ, const G2J* SgJ, const G2A* H,
                              const uint8_t* seg_ok, uint8_t* grp_state, uint32_t* n_fallback);
 void launch_sm_fallback(LaunchCfg c, uint32_t n, const uint32_t* set_grp, const uint32_t* grp_msg, const uint8_t* grp_state,
@@ -40,8 +43,6 @@ void launch_vs_prepare(LaunchCfg c, uint32_t n, const uint32_t* set_idx_off, con
                        const uint8_t* raw_pk48, const uint8_t* msgs32, const uint8_t* sig, uint32_t sig_stride, const uint32_t* sig_len,
                        const G1A* table, const uint8_t* table_ok, const Seed& seed, uint32_t nonce, Fp12* f_out, G2J* rS_out,
                        uint8_t* status);
-void launch_vs_chunk(LaunchCfg c, uint32_t C, const uint32_t* chunk_off, const uint8_t* status, const Fp12* f, const G2J* rS,
-                     uint8_t* chunk_valid);
 }  // namespace gbv
 
 namespace gbv {

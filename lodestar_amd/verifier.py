@@ -136,8 +136,8 @@ class GpuBlsVerifier:
         return out.raw
 
     # ---- synchronous device calls (also the verifyOnMainThread path) ---------------------------
-    def verify_signature_sets_sync(self, sets: Sequence[ISignatureSet]) -> bool:
-        self._check_open()
+    def _marshal_sets(self, sets: Sequence[ISignatureSet]):
+        """ISignatureSet list -> (gbv_set array, index arena, keep-alive list) for the C ABI."""
         n = len(sets)
         arena: List[int] = []
         keep = []
@@ -166,11 +166,38 @@ class GpuBlsVerifier:
                 e.idx_off, e.idx_len = len(arena), 1
                 arena.append(int(s.index))
         ar = (ctypes.c_uint32 * max(len(arena), 1))(*arena)
+        return arr, ar, keep
+
+    def verify_signature_sets_sync(self, sets: Sequence[ISignatureSet]) -> bool:
+        self._check_open()
+        arr, ar, keep = self._marshal_sets(sets)
         allv = ctypes.c_uint8(0)
-        rc = self._lib.gbv_verify_sets(self._ctx, arr, n, ar, ctypes.byref(allv), None)
+        rc = self._lib.gbv_verify_sets(self._ctx, arr, len(sets), ar, ctypes.byref(allv), None)
         _native.check(self._lib, self._ctx, rc)
         self.metrics["device_passes"] += 1
         return bool(allv.value)
+
+    # ---- multi-GPU shards (lodestar_amd/sharded.py) --------------------------------------------
+    def vs_partial(self, sets: Sequence[ISignatureSet]) -> Tuple[bytes, bool]:
+        """This device's Fp12 Miller product over a shard of a verifySignatureSets call
+        (gbv_vs_partial): (opaque 576-byte blob, shard_ok)."""
+        self._check_open()
+        arr, ar, keep = self._marshal_sets(sets)
+        out = ctypes.create_string_buffer(576)
+        ok = ctypes.c_uint8(0)
+        rc = self._lib.gbv_vs_partial(self._ctx, arr, len(sets), ar, out, ctypes.byref(ok))
+        _native.check(self._lib, self._ctx, rc)
+        self.metrics["device_passes"] += 1
+        return out.raw, bool(ok.value)
+
+    def fp12_check(self, partials: Sequence[bytes]) -> bool:
+        """prod(partials) after one final exponentiation == 1 (gbv_fp12_check)."""
+        self._check_open()
+        blob = b"".join(bytes(p) for p in partials)
+        ok = ctypes.c_uint8(0)
+        rc = self._lib.gbv_fp12_check(self._ctx, blob or bytes(576), len(partials), ctypes.byref(ok))
+        _native.check(self._lib, self._ctx, rc)
+        return bool(ok.value)
 
     def verify_same_message_multi_sync(self, calls: Sequence[Tuple[Sequence[Tuple[int, bytes]], bytes]]) -> List[List[bool]]:
         """Many verifySignatureSetsSameMessage calls in one device pass."""

@@ -117,3 +117,66 @@ def test_verify_sets_large_chunks(world):
     assert v.verify_signature_sets_sync(sets) is True
     sets[150] = SingleSignatureSet(idx[150], msgs[151], sigs[150])
     assert v.verify_signature_sets_sync(sets) is False
+
+
+def _vs_sets(v, sks, n, tag):
+    from lodestar_amd import AggregatedSignatureSet, SingleSignatureSet
+    msgs = [hashlib.sha256(tag + i.to_bytes(4, "little")).digest() for i in range(n)]
+    out = []
+    for i in range(n):
+        if i % 5 == 0:  # a 128-member committee aggregate (C3 shape) from the HBM table
+            idx = [(13 * i + 7 * j) % N_TABLE for j in range(128)]
+            agg = sum(int.from_bytes(sks[k % N_KEYS], "big") for k in idx) % R_ORDER
+            sig = v.util_sign([agg.to_bytes(32, "big")], [0], [msgs[i]])[0]
+            out.append(AggregatedSignatureSet(idx, msgs[i], sig))
+        else:
+            k = (11 * i) % N_TABLE
+            out.append(SingleSignatureSet(k, msgs[i], v.util_sign([sks[k % N_KEYS]], [0], [msgs[i]])[0]))
+    return out
+
+
+def test_vs_shard_partials_combine(world):
+    """8(e): per-shard Fp12 Miller partials (gbv_vs_partial) + one final exponentiation over all
+    of them (gbv_fp12_check) agree with the single-device verifySignatureSets."""
+    from lodestar_amd import SingleSignatureSet
+    v, sks, _ = world
+    sets = _vs_sets(v, sks, 150, b"shard")
+    assert v.verify_signature_sets_sync(sets) is True
+    cuts = [0, 37, 101, 150]
+    parts = [v.vs_partial(sets[a:b]) for a, b in zip(cuts, cuts[1:])]
+    assert all(ok for _, ok in parts) and all(len(p) == 576 for p, _ in parts)
+    assert v.fp12_check([p for p, _ in parts]) is True
+    # a valid point over the wrong message in the middle shard: every shard decodes, product fails
+    bad = list(sets)
+    bad[61] = SingleSignatureSet(bad[61].index, bad[62].signing_root, bad[61].signature)
+    parts = [v.vs_partial(bad[a:b]) for a, b in zip(cuts, cuts[1:])]
+    assert all(ok for _, ok in parts)
+    assert v.fp12_check([p for p, _ in parts]) is False
+    assert v.verify_signature_sets_sync(bad) is False
+    # malformed signature: that shard reports shard_ok = False
+    bad = list(sets)
+    bad[121] = SingleSignatureSet(bad[121].index, bad[121].signing_root, bytes([10]) * 96)
+    assert v.vs_partial(bad[101:150])[1] is False
+
+
+def test_sharded_verifier_single_rank(world):
+    """ShardedVerifier over a 1-rank gloo group on the GPU box (the N>1 collective path itself is
+    covered by tests/test_sharded.py with 2 gloo ranks)."""
+    import socket
+    import torch.distributed as dist
+    from lodestar_amd.sharded import ShardedVerifier
+    v, sks, _ = world
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=0, world_size=1)
+    try:
+        sv = ShardedVerifier(v)
+        sets = _vs_sets(v, sks, 40, b"rank1")
+        assert sv.verify_signature_sets(sets) is True
+        msg = hashlib.sha256(b"sm").digest()
+        sigs = v.util_sign([sks[k] for k in range(8)], [0] * 8, [msg])
+        calls = [([(k, sigs[k]) for k in range(5)], msg), ([(5, sigs[5]), (6, sigs[0])], msg)]
+        assert sv.verify_same_message_multi(calls) == [[True] * 5, [True, False]]
+    finally:
+        dist.destroy_process_group()

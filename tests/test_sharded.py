@@ -1,0 +1,164 @@
+"""Multi-GPU host logic (lodestar_amd/sharded.py) on CPU: world_size-2 gloo process groups over
+127.0.0.1, with an oracle-backed stand-in for the device (test infrastructure only) so the
+sharding, the 577-byte all-gather of Fp12 Miller partials, the combined final exponentiation and
+the per-set boolean gather are exercised without a GPU.  Expected answers come from the oracle's
+restatement of the reference pool (oracle.bls_oracle.pool_verify_*).
+"""
+import os
+import random
+import socket
+
+import pytest
+import torch.multiprocessing as mp
+
+from lodestar_amd.sharded import PARTIAL_BYTES, balanced_ranges, set_weight
+from lodestar_amd.verifier import AggregatedSignatureSet, SingleSignatureSet
+from oracle import bls_oracle as O
+
+N_KEYS = 6
+
+
+def _keys():
+    sks = [O.interop_secret_key(i) for i in range(N_KEYS)]
+    return sks, [O.sk_to_pk(sk) for sk in sks]
+
+
+def _f12_to_bytes(f):
+    out = b""
+    for six in f:
+        for two in six:
+            out += two[0].to_bytes(48, "big") + two[1].to_bytes(48, "big")
+    return out
+
+
+def _f12_from_bytes(b):
+    v = [int.from_bytes(b[48 * i:48 * i + 48], "big") for i in range(12)]
+    f2 = [(v[2 * k], v[2 * k + 1]) for k in range(6)]
+    return ((f2[0], f2[1], f2[2]), (f2[3], f2[4], f2[5]))
+
+
+class OracleDevice:
+    """CPU stand-in with the GpuBlsVerifier methods ShardedVerifier uses (oracle arithmetic)."""
+
+    def __init__(self, pks):
+        self.pks = pks
+        self.rng = random.Random(os.getpid())
+
+    def _pk(self, s):
+        if isinstance(s, AggregatedSignatureSet):
+            return O.aggregate_pubkeys([self.pks[i] for i in s.indices])
+        return self.pks[s.index]
+
+    def vs_partial(self, sets):
+        f, sig_acc, ok = O.F12_ONE, None, True
+        for s in sets:
+            try:
+                sig = O.signature_from_bytes(bytes(s.signature), True)
+            except O.DecodeError:
+                ok = False
+                continue
+            pk = self._pk(s)
+            if pk is None or sig is None:
+                ok = False
+                continue
+            r = self.rng.getrandbits(64) | 1
+            f = O.f12_mul(f, O.miller_loop(O.g1_mul(pk, r), O.hash_to_g2(bytes(s.signing_root))))
+            sig_acc = O.g2_add(sig_acc, O.g2_mul(sig, r))
+        if sig_acc is not None:
+            f = O.f12_mul(f, O.miller_loop(O.g1_neg(O.G1_GEN), sig_acc))
+        blob = _f12_to_bytes(f)
+        assert len(blob) == PARTIAL_BYTES
+        return blob, ok
+
+    def fp12_check(self, partials):
+        f = O.F12_ONE
+        for b in partials:
+            f = O.f12_mul(f, _f12_from_bytes(b))
+        return O.final_exponentiation(f) == O.F12_ONE
+
+    def verify_same_message_multi_sync(self, calls):
+        return [O.pool_verify_same_message([(self.pks[i], sig) for i, sig in sets], msg) for sets, msg in calls]
+
+
+def _sets(sks, bad=None):
+    msgs = [bytes([i + 1]) * 32 for i in range(5)]
+    sets = [SingleSignatureSet(i, msgs[i], O.g2_compress(O.sign(sks[i], msgs[i]))) for i in range(3)]
+    agg_sk = (sks[3] + sks[4]) % O.R
+    sets.append(AggregatedSignatureSet([3, 4], msgs[3], O.g2_compress(O.sign(agg_sk, msgs[3]))))
+    sets.append(SingleSignatureSet(5, msgs[4], O.g2_compress(O.sign(sks[5], msgs[4]))))
+    if bad == "wrong_msg":
+        sets[4] = SingleSignatureSet(5, msgs[4], O.g2_compress(O.sign(sks[5], msgs[0])))
+    elif bad == "malformed":
+        sets[1] = SingleSignatureSet(1, msgs[1], bytes([10]) * 96)
+    return sets
+
+
+def _worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from lodestar_amd import EmptyAggregateError
+        from lodestar_amd.sharded import ShardedVerifier
+        sks, pks = _keys()
+        sv = ShardedVerifier(OracleDevice(pks))
+        res = {"shard": sv.shard_of(_sets(sks))}
+        res["valid"] = sv.verify_signature_sets(_sets(sks))
+        res["wrong_msg"] = sv.verify_signature_sets(_sets(sks, "wrong_msg"))
+        res["malformed"] = sv.verify_signature_sets(_sets(sks, "malformed"))
+        res["empty"] = sv.verify_signature_sets([])
+        try:
+            sv.verify_signature_sets(_sets(sks) + [AggregatedSignatureSet([], bytes(32), bytes(96))])
+            res["empty_agg"] = "no error"
+        except EmptyAggregateError:
+            res["empty_agg"] = "rejected"
+        msg = bytes([7]) * 32
+        good = [(i, O.g2_compress(O.sign(sks[i], msg))) for i in range(4)]
+        calls = [(good[:2], msg), ([good[2], (3, bytes([10]) * 96)], msg), ([(0, good[1][1])], msg)]
+        res["sm"] = sv.verify_same_message_multi(calls)
+        q.put((rank, res))
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_balanced_ranges_cover_and_balance():
+    w = [set_weight(AggregatedSignatureSet(list(range(k)), bytes(32), bytes(96))) for k in (1, 128, 1, 1, 512, 1, 128)]
+    for parts in (1, 2, 3, 8):
+        r = balanced_ranges(w, parts)
+        assert len(r) == parts and r[0][0] == 0 and r[-1][1] == len(w)
+        assert all(r[i][1] == r[i + 1][0] for i in range(parts - 1))
+
+
+def test_sharded_world2_gloo():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=600) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    sks, pks = _keys()
+    table_sets = lambda sets: [{"pubkeys": [pks[i] for i in s.indices]} if isinstance(s, AggregatedSignatureSet)
+                               else {"pubkey": pks[s.index]} for s in sets]
+    for rank in (0, 1):
+        r = out[rank]
+        assert r["valid"] is True and r["wrong_msg"] is False and r["malformed"] is False
+        assert r["empty"] is False and r["empty_agg"] == "rejected"
+        assert r["sm"] == [[True, True], [True, False], [False]]
+    # the two shards partition the call
+    assert out[0]["shard"][0] == 0 and out[0]["shard"][1] == out[1]["shard"][0] and out[1]["shard"][1] == 5
+    # and the answers match the oracle's restatement of the reference pool
+    for bad, want in ((None, True), ("wrong_msg", False), ("malformed", False)):
+        sets = _sets(sks, bad)
+        d = [dict(t, msg=bytes(s.signing_root), sig=bytes(s.signature)) for t, s in zip(table_sets(sets), sets)]
+        assert O.pool_verify_signature_sets(d) is want

@@ -14,7 +14,9 @@ Fp2/Fp6/Fp12, Granger-Scott cyclotomic squaring, sparse line multiplication, hom
 projective doubling/addition steps with line coefficients, Frobenius), executed symbolically.
 tests/test_coop_tables.py re-executes every program in Python against the oracle.
 
-Program encoding (all indices small):
+Program encoding (all indices small; emitted as fixed-size per-lane records -- 20 terms per
+product (A: 0..9, B: 10..19), 8 per partial sum / output, padding coef 0 -- so a lane fetches its
+whole record with a few 16-byte loads, one memory latency per phase):
   operands 0..5 -> base pointers given at run time (program-specific signature below)
   SRC_Z = 6  -> Z[k], the k-th product of this program (then the partial sums)
   SRC_C = 7  -> CONSTS[k] (Montgomery Fp constants emitted below)
@@ -30,6 +32,7 @@ sys.path.insert(0, ROOT)
 P = 0x1A0111EA397FE69A4B1BA7B6434BACD764774B84F38512BF6730D2A0F6B0F6241EABFFFEB153FFFFB9FEFFFFFFFFAAAB
 SRC_Z, SRC_C = 6, 7
 PART_TERMS = 6
+OPW = 10  # terms per product operand record (A: 0..9, B: 10..19); 20 x 4 B = five 16-byte loads
 
 
 # ---- symbolic Fp: linear forms over symbols ----------------------------------------------------
@@ -413,18 +416,31 @@ def emit(progs, path):
         L.append("// %s: operands %s; %d products in %d rounds, %d outputs, %d terms" % (
             n, ", ".join("%d=%s[%d] %s" % (i, s[0], s[1], s[2]) for i, s in enumerate(p["signature"])),
             len(p["prods"]), len(p["round_end"]), len(p["outs"]), len(p["terms"])))
-        L.append("GBV_COOP_TABLE Term %s_TERMS[%d] = {%s};" % (n, len(p["terms"]), ", ".join(
-            "{%d, %d, %d}" % t for t in p["terms"])))
-        L.append("GBV_COOP_TABLE Prod %s_PRODS[%d] = {%s};" % (n, max(1, len(p["prods"])), ", ".join(
-            "{%d, %d, %d, %d}" % q for q in p["prods"]) or "{0, 0, 0, 0}"))
-        L.append("GBV_COOP_TABLE Part %s_PARTS[%d] = {%s};" % (n, max(1, len(p["parts"])), ", ".join(
-            "{%d, %d, %d}" % q for q in p["parts"]) or "{0, 0, 0}"))
-        L.append("GBV_COOP_TABLE Out %s_OUTS[%d] = {%s};" % (n, len(p["outs"]), ", ".join(
-            "{%d, %d, %d, %d}" % o for o in p["outs"])))
+        T = p["terms"]
+        pad = (SRC_Z, 0, 0)
+
+        def rec(t0, tn, width):
+            assert tn <= width, (n, tn, width)
+            return list(T[t0:t0 + tn]) + [pad] * (width - tn)
+
+        prod_recs = [rec(a0, an, OPW) + rec(b0, bn, OPW) for (a0, an, b0, bn) in p["prods"]] or [[pad] * (2 * OPW)]
+        part_recs = [rec(t0, tn, 8) for (t0, tn, _) in p["parts"]] or [[pad] * 8]
+        out_recs = [rec(t0, tn, 8) for (t0, tn, _, _) in p["outs"]]
+        for j, (_, _, z) in enumerate(p["parts"]):
+            assert z == len(p["prods"]) + j
+        fmt = lambda recs: ",\n    ".join(", ".join("{%d, %d, %d}" % t for t in r) for r in recs)
+        L.append("GBV_COOP_TABLE Term %s_PRODS[%d][%d] __attribute__((aligned(16))) = {\n    %s};" % (
+            n, len(prod_recs), 2 * OPW, ",\n    ".join("{" + ", ".join("{%d, %d, %d}" % t for t in r) + "}" for r in prod_recs)))
+        L.append("GBV_COOP_TABLE Term %s_PARTS[%d][8] __attribute__((aligned(16))) = {\n    %s};" % (
+            n, len(part_recs), ",\n    ".join("{" + ", ".join("{%d, %d, %d}" % t for t in r) + "}" for r in part_recs)))
+        L.append("GBV_COOP_TABLE Term %s_OUTS[%d][8] __attribute__((aligned(16))) = {\n    %s};" % (
+            n, len(out_recs), ",\n    ".join("{" + ", ".join("{%d, %d, %d}" % t for t in r) + "}" for r in out_recs)))
+        L.append("GBV_COOP_TABLE uint8_t %s_OUT_DST[%d] = {%s};" % (n, len(p["outs"]), ", ".join(str(o[2]) for o in p["outs"])))
+        L.append("GBV_COOP_TABLE uint8_t %s_OUT_IDX[%d] = {%s};" % (n, len(p["outs"]), ", ".join(str(o[3]) for o in p["outs"])))
         re = p["round_end"] + [0] * (6 - len(p["round_end"]))
         assert len(p["round_end"]) <= 6
-        L.append("GBV_COOP_TABLE Prog %s = {%d, %d, %d, {%s}, %s_PRODS, %s_PARTS, %s_OUTS, %s_TERMS};" % (
-            n, len(p["round_end"]), len(p["parts"]), len(p["outs"]), ", ".join(map(str, re)), n, n, n, n))
+        L.append("GBV_COOP_TABLE Prog %s = {%d, %d, %d, {%s}, &%s_PRODS[0][0], &%s_PARTS[0][0], &%s_OUTS[0][0], %s_OUT_DST, %s_OUT_IDX};" % (
+            n, len(p["round_end"]), len(p["parts"]), len(p["outs"]), ", ".join(map(str, re)), n, n, n, n, n))
     L += ["", "}  // namespace coop", "}  // namespace gbv", ""]
     open(path, "w").write("\n".join(L))
 

@@ -16,6 +16,8 @@ def main(root, out):
             for row in csv.DictReader(f):
                 short = row.get("Kernel_Name", "").split("(")[0].replace("gbv::", "")
                 rows[short].append((float(row["Grid_Size"]), row["Counter_Name"], float(row["Counter_Value"])))
+                dur = (int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) * 1e-6
+                rows[short].append((float(row["Grid_Size"]), "duration_ms", dur))
     res = {}
     for k, rs in rows.items():
         gmax = max(g for g, _, _ in rs)
