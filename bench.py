@@ -174,8 +174,13 @@ def main():
         if dist is not None:
             dist.barrier()
 
+    slow_path = [0, 0]
+
     def collect(b):
         r = b.wait(True)
+        fb, seg = v.last_stats()
+        slow_path[0] += fb
+        slow_path[1] += seg
         ms, cnt = v.last_kernel_ms()
         kms[:] += np.array(ms)
         kcnt[:] += np.array(cnt)
@@ -204,6 +209,8 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     assert n_valid == [args.sets] * args.steps, n_valid
+    if slow_path != [0, 0]:
+        log("WARNING: fast path fell back (chunks, segments) = %s on an all-valid workload" % slow_path)
     avg_launch_ms = kms / np.maximum(kcnt, 1)
     kms /= max(args.steps, 1)
     prep_launches_per_step = kcnt[1] / max(args.steps, 1)
@@ -225,7 +232,8 @@ def main():
                 "traffic": round(traffic) if traffic is not None else None, "pmc": pmc,
                 "work_per_unit_fme": W_PREPARE_FME, "units_per_launch": round(units_per_launch, 1),
                 "avg_launch_ms": round(float(avg_launch_ms[1]), 3),
-                "kernel_ms_per_step": {k: round(float(x), 3) for k, x in zip(KERNELS, kms)}}
+                "kernel_ms_per_step": {k: round(float(x), 3) for k, x in zip(KERNELS, kms)},
+                "slow_path_chunks_segments": slow_path}
 
     cpu = None
     if rank == 0 and not args.no_cpu_baseline:

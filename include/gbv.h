@@ -134,6 +134,10 @@ int gbv_fp12_check(gbv_ctx* ctx, const uint8_t* partials576, size_t k, uint8_t* 
  * [hash, prepare, chunk_finish, miller, seg_check, group_pairing, fallback]; returns the number of
  * entries written (at most 7). */
 int gbv_last_kernel_ms(gbv_ctx* ctx, float* ms_out, int* launches_out, int max);
+/* Fast-path health of the last waited same-message verification: chunks that went to the per-set
+ * retry (malformed sets or failing chunk checks) and segments whose combined check failed.  Both
+ * are 0 for an all-valid batch (up to the 2^-64 batch-verification error). */
+int gbv_last_stats(gbv_ctx* ctx, uint32_t* fallback_chunks, uint32_t* failed_segments);
 
 /* ---- utilities for tests and synthetic workloads (not on the verification path) ----------- */
 /* sk32 (big-endian scalars) -> compressed pubkeys, on the device. */

@@ -7,7 +7,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libgbv.so")
+# LODESTAR_AMD_LIB selects an alternative in-tree build (A/B experiments with tools/build_variant.sh)
+LIB_PATH = os.environ.get("LODESTAR_AMD_LIB") or os.path.join(_HERE, "libgbv.so")
 
 GBV_OK = 0
 GBV_E_ARG = -1
@@ -20,7 +21,7 @@ EXPORTED_SYMBOLS = (
     "gbv_init", "gbv_destroy", "gbv_last_error", "gbv_pubkeys_append", "gbv_pubkeys_count",
     "gbv_verify_sets", "gbv_verify_same_message", "gbv_verify_same_message_multi",
     "gbv_aggregate_pubkeys", "gbv_sm_batch_create", "gbv_sm_batch_verify", "gbv_sm_batch_destroy",
-    "gbv_sm_batch_submit", "gbv_sm_batch_wait", "gbv_vs_partial", "gbv_fp12_check",
+    "gbv_sm_batch_submit", "gbv_sm_batch_wait", "gbv_vs_partial", "gbv_fp12_check", "gbv_last_stats",
     "gbv_last_kernel_ms", "gbv_util_sk_to_pk", "gbv_util_sign", "gbv_util_hash_to_g2",
     "gbv_pubkeys_replicate",
 )
@@ -80,6 +81,7 @@ def load_library(path=LIB_PATH):
         "gbv_sm_batch_submit": (i32, [vp, vp]),
         "gbv_vs_partial": (i32, [vp, P(GbvSet), sz, vp, vp, vp]),
         "gbv_fp12_check": (i32, [vp, vp, sz, vp]),
+        "gbv_last_stats": (i32, [vp, vp, vp]),
         "gbv_sm_batch_wait": (i32, [vp, vp, vp]),
         "gbv_sm_batch_destroy": (None, [vp, vp]),
         "gbv_last_kernel_ms": (i32, [vp, P(ctypes.c_float), P(ctypes.c_int), i32]),

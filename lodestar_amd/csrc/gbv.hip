@@ -53,6 +53,7 @@ struct gbv_ctx {
   static constexpr int NK = 7;  // hash, prepare, chunk_reduce, miller, seg_check, group_pairing, fallback
   float last_ms[NK] = {};
   int last_launches[NK] = {};
+  uint32_t last_fallback_chunks = 0, last_failed_segments = 0;
   bool closed = false;
 };
 
@@ -63,6 +64,7 @@ struct gbv_sm_batch {
   uint8_t *sig = nullptr, *msgs = nullptr, *status = nullptr, *grp_state = nullptr, *valid = nullptr, *seg_ok = nullptr;
   uint8_t* seg_ok_host = nullptr;  // pinned
   uint8_t* valid_host = nullptr;   // pinned, n bytes: results of the last submitted verify
+  uint32_t* nfb_host = nullptr;    // pinned: fallback chunk count of the last submitted verify
   size_t seg_cap = 0;
   // in-flight state of the last gbv_sm_batch_submit
   bool in_flight = false;
@@ -281,6 +283,7 @@ void gbv_sm_batch_destroy(gbv_ctx* c, gbv_sm_batch* b) {
   for (auto& e : b->ev) hipEventDestroy(e);
   if (b->done) hipEventDestroy(b->done);
   hipHostFree(b->valid_host);
+  hipHostFree(b->nfb_host);
   hipFree(b->F); hipFree(b->seg_ok); hipHostFree(b->seg_ok_host);
   hipFree(b->Fpart); hipFree(b->Spart); hipFree(b->has);
   delete b;
@@ -333,6 +336,7 @@ int gbv_sm_batch_create(gbv_ctx* c, size_t n_calls, const uint32_t* call_off, co
   chk(dalloc(&b->seg_ok, b->seg_cap));
   chk(hipHostMalloc((void**)&b->seg_ok_host, b->seg_cap, hipHostMallocDefault));
   chk(hipHostMalloc((void**)&b->valid_host, std::max<size_t>(n, 1), hipHostMallocDefault));
+  chk(hipHostMalloc((void**)&b->nfb_host, sizeof(uint32_t), hipHostMallocDefault));
   chk(hipEventCreateWithFlags(&b->done, hipEventDisableTiming));
   if (e != hipSuccess) {
     gbv_sm_batch_destroy(c, b);
@@ -441,6 +445,8 @@ int gbv_sm_batch_submit(gbv_ctx* c, gbv_sm_batch* b) {
                      c->table, b->S, b->H, b->valid, 1);
   hipEventRecord(ep[1], sbs[0]);
   HIP_CHECK(c, hipMemcpyAsync(b->valid_host, b->valid, b->n, hipMemcpyDeviceToHost, sbs[0]));
+  HIP_CHECK(c, hipMemcpyAsync(b->nfb_host, b->n_fallback, sizeof(uint32_t), hipMemcpyDeviceToHost, sbs[0]));
+  HIP_CHECK(c, hipMemcpyAsync(b->seg_ok_host, b->seg_ok, S, hipMemcpyDeviceToHost, sbs[0]));
   HIP_CHECK(c, hipEventRecord(b->done, sbs[0]));
   HIP_CHECK(c, hipGetLastError());
   b->in_flight = true;
@@ -455,6 +461,9 @@ int gbv_sm_batch_wait(gbv_ctx* c, gbv_sm_batch* b, uint8_t* valid) {
   b->in_flight = false;
   HIP_CHECK(c, hipEventSynchronize(b->done));
   if (valid) memcpy(valid, b->valid_host, b->n);
+  c->last_fallback_chunks = *b->nfb_host;
+  c->last_failed_segments = 0;
+  for (size_t s = 0; s < b->n_seg; ++s) c->last_failed_segments += b->seg_ok_host[s] ? 0 : 1;
   for (auto& x : c->last_ms) x = 0.f;
   for (auto& x : c->last_launches) x = 0;
   hipEvent_t* ev = b->ev.data();
@@ -479,6 +488,13 @@ int gbv_sm_batch_verify(gbv_ctx* c, gbv_sm_batch* b, uint8_t* valid) {
   int rc = gbv_sm_batch_submit(c, b);
   if (rc) return rc;
   return gbv_sm_batch_wait(c, b, valid);
+}
+
+int gbv_last_stats(gbv_ctx* c, uint32_t* fallback_chunks, uint32_t* failed_segments) {
+  if (!c) return GBV_E_ARG;
+  if (fallback_chunks) *fallback_chunks = c->last_fallback_chunks;
+  if (failed_segments) *failed_segments = c->last_failed_segments;
+  return GBV_OK;
 }
 
 int gbv_last_kernel_ms(gbv_ctx* c, float* out, int* launches, int max) {

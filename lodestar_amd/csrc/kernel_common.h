@@ -25,7 +25,10 @@
 // One wave per workgroup; the register budget is capped so that two waves share each SIMD
 // (measured on MI355X, tools/ubench_fp.hip: 2 waves/SIMD beat 1 and 3 for the point kernels,
 // whose live state -- a Jacobian G2 point plus its operand -- does not fit the 128 VGPRs of 4).
-#define GBV_KERNEL_ATTR __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
+#ifndef GBV_WAVES_PER_EU
+#define GBV_WAVES_PER_EU 2
+#endif
+#define GBV_KERNEL_ATTR __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GBV_WAVES_PER_EU)))
 
 namespace gbv {
 

@@ -247,6 +247,12 @@ class GpuBlsVerifier:
         _native.check(self._lib, self._ctx, rc)
         return StagedSameMessage(self, h, int(off[-1]))
 
+    def last_stats(self):
+        """(fallback_chunks, failed_segments) of the last waited same-message verification."""
+        a, b = ctypes.c_uint32(0), ctypes.c_uint32(0)
+        _native.check(self._lib, self._ctx, self._lib.gbv_last_stats(self._ctx, ctypes.byref(a), ctypes.byref(b)))
+        return a.value, b.value
+
     def last_kernel_ms(self):
         """(total device ms, launches) of each kernel of the last staged verify:
         [hash, prepare, chunk_finish, miller, seg_check, group_pairing, fallback]."""

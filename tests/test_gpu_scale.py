@@ -71,6 +71,8 @@ def test_same_message_all_valid_multi_segment(world, segments):
     assert all(res)
     ms, cnt = v.last_kernel_ms()
     assert cnt[4] >= 2, "expected several pipeline segments"
+    # the fast path alone must carry an all-valid stream: no failed segment, no retried chunk
+    assert v.last_stats() == (0, 0)
 
 
 def test_same_message_injected_invalid(world, segments):
@@ -90,6 +92,8 @@ def test_same_message_injected_invalid(world, segments):
     for i, s in bad.items():
         sigs[i] = s
     res = _run_staged(v, off, idx, sigs, msgs)
+    fb, seg = v.last_stats()
+    assert fb >= 6 and seg >= 1  # the injected sets' chunks, and at least one failing segment
     expected = [True] * n
     for i in bad:
         expected[i] = False
