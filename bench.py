@@ -114,6 +114,54 @@ def build_workload(v, n_sets, rank, log):
     return call_off, idx, b"".join(sigs), b"".join(msgs), pks
 
 
+# Signing-root row: getAttestationDataSigningRoot = 9 SHA-256 digests of 64 bytes
+# (8 AttestationData nodes + the SigningData node), 2 compressions each.  Algorithmic VALU ops per
+# digest with gfx950's 3-input ops (v_alignbit rotates, v_bitop3 xor3/maj/ch, v_add3): 64 rounds x 14
+# per compression x 2 + 48 schedule words x 10 + 16 state adds = 2288 (the second block's schedule is
+# constant).  Peak: 256 CU x 64 lanes x 2.4 GHz = 39.3 T lane-ops/s (full-rate 32-bit VALU).
+SSZ_DIGESTS_PER_ROOT = 9
+SSZ_OPS_PER_DIGEST = 2288
+SSZ_PEAK_OPS = 256 * 64 * 2.4e9
+SSZ_BYTES_PER_ROOT = 128 + 32 + 4  # AttestationData in, root out, domain index
+
+
+def signing_roots_bench(v, n=1 << 20, reps=5, cpu_sample=20000):
+    """Secondary line for the signing-root row: AttestationData signing roots per second with the
+    inputs resident in HBM (kernel time from HIP events on the launch stream), the PCIe-inclusive rate
+    of the host-buffer call, and the hashlib oracle on one host core over a bounded sample."""
+    rng = np.random.default_rng(11)
+    datas = rng.integers(0, 256, size=(n, 128), dtype=np.uint8).tobytes()
+    doms = rng.integers(0, 256, size=(4, 32), dtype=np.uint8).tobytes()
+    dom_idx = rng.integers(0, 4, size=n).tolist()
+    v.attestation_data_signing_roots(datas[:128 * 1024], doms, dom_idx[:1024])
+    kms, walls = [], []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        roots = v.attestation_data_signing_roots(datas, doms, dom_idx)
+        walls.append(time.perf_counter() - t0)
+        kms.append(v.ssz_last_kernel_ms())
+    assert len(roots) == n
+    k_ms = float(np.mean(kms))
+    achieved = n * SSZ_DIGESTS_PER_ROOT * SSZ_OPS_PER_DIGEST / (k_ms * 1e-3)
+    out = {"metric": "AttestationData signing roots/sec", "value": round(n / (k_ms * 1e-3), 1), "unit": "roots/s",
+           "roots_per_launch": n, "kernel": "k_ssz_att_signing_roots", "avg_launch_ms": round(k_ms, 4),
+           "pcie_inclusive_roots_per_s": round(n / float(np.median(walls)), 1),
+           "roofline": {"bound": "valu-int", "achieved": round(achieved / 1e12, 4), "peak": round(SSZ_PEAK_OPS / 1e12, 2),
+                        "unit": "T lane-ops/s", "frac": round(achieved / SSZ_PEAK_OPS, 4),
+                        "work_per_unit": "%d digest64 x %d ops" % (SSZ_DIGESTS_PER_ROOT, SSZ_OPS_PER_DIGEST),
+                        "hbm_GBps": round(n * SSZ_BYTES_PER_ROOT / (k_ms * 1e-3) / 1e9, 1)}}
+    if cpu_sample:
+        from oracle import ssz_oracle
+        d0 = doms[:32]
+        t0 = time.perf_counter()
+        for i in range(cpu_sample):
+            ssz_oracle.attestation_signing_root(datas[128 * i:128 * i + 128], d0)
+        dt = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": round(cpu_sample / dt, 1), "unit": "roots/s", "cores": 1, "kind": "port",
+                               "sample": "%d roots, oracle/ssz_oracle.py (hashlib SHA-256), %.2fs" % (cpu_sample, dt)}
+    return out
+
+
 def p50_batch_latency(v, call_off, idx, sigs, msgs, reps=20):
     """Latency of one gossip batch (one verifySignatureSetsSameMessage call of 64 sets) alone."""
     n = 64
@@ -133,6 +181,7 @@ def main():
     ap.add_argument("--sets", type=int, default=1 << 20)
     ap.add_argument("--cpu-sample", type=int, default=None, help="sets in the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-signing-roots", action="store_true", help="skip the signing-root secondary line")
     ap.add_argument("--no-stream", dest="stream", action="store_false",
                     help="one batch at a time (no overlap of consecutive verifications)")
     args = ap.parse_args()
@@ -235,6 +284,11 @@ def main():
                 "kernel_ms_per_step": {k: round(float(x), 3) for k, x in zip(KERNELS, kms)},
                 "slow_path_chunks_segments": slow_path}
 
+    ssz = None
+    if rank == 0 and not args.no_signing_roots:
+        ssz = signing_roots_bench(v, cpu_sample=0 if args.no_cpu_baseline else 20000)
+        log("signing roots: %s" % ssz)
+
     cpu = None
     if rank == 0 and not args.no_cpu_baseline:
         from oracle import cpu_baseline
@@ -262,6 +316,7 @@ def main():
                    "submission": "streamed: 2 batches in flight" if args.stream else "one batch at a time"},
         "roofline": roofline,
         "cpu_baseline": cpu,
+        "signing_roots": ssz,
     }
     if rank == 0:
         print(json.dumps(line), flush=True)

@@ -139,6 +139,29 @@ int gbv_last_kernel_ms(gbv_ctx* ctx, float* ms_out, int* launches_out, int max);
  * are 0 for an all-valid batch (up to the 2^-64 batch-verification error). */
 int gbv_last_stats(gbv_ctx* ctx, uint32_t* fallback_chunks, uint32_t* failed_segments);
 
+/* ---- signing roots: batched SHA-256 over SSZ nodes ------------------
+ * The builders hash a signing root for every set they hand the verifier (signatureSets/*.ts via
+ * computeSigningRoot, state-transition/src/util/signingRoot.ts:7-13).  Inputs and outputs are host
+ * buffers; n = 0 is a no-op.  Each call records its kernel time (HIP events, gbv_ssz_last_kernel_ms). */
+/* out32[i] = sha256(in64[i]): persistent-merkle-tree hasher.digest64(a, b) = sha256(a || b)
+ * (@chainsafe/as-sha256 0.5.0; light-client/src/utils/verifyMerkleBranch.ts:23). */
+int gbv_sha256_digest64(gbv_ctx* ctx, const uint8_t* in64, size_t n, uint8_t* out32);
+/* Merkle roots of n objects of 2^depth 32-byte chunks each (object-major, zero padding already in
+ * place): ContainerType.hashTreeRoot over the field roots of a container (@chainsafe/ssz 0.11.1).
+ * depth <= 24; depth 0 copies the single chunk. */
+int gbv_merkle_roots(gbv_ctx* ctx, const uint8_t* chunks32, size_t n, uint32_t depth, uint8_t* out32);
+/* computeSigningRoot from object roots: out32[i] = sha256(object_roots32[i] || domains32[d]) with
+ * d = dom_idx ? dom_idx[i] : 0 (signingRoot.ts:7-13).  dom_idx[i] >= n_domains is GBV_E_ARG. */
+int gbv_signing_roots(gbv_ctx* ctx, const uint8_t* object_roots32, size_t n, const uint8_t* domains32, size_t n_domains,
+                      const uint32_t* dom_idx, uint8_t* out32);
+/* getAttestationDataSigningRoot (beacon-node/src/chain/validation/attestation.ts:657-665):
+ * computeSigningRoot(ssz.phase0.AttestationData, data, domain) from the 128-byte SSZ serialisation of
+ * each AttestationData (types/src/phase0/sszTypes.ts:247-256); domains as in gbv_signing_roots. */
+int gbv_attestation_signing_roots(gbv_ctx* ctx, const uint8_t* data128, size_t n, const uint8_t* domains32, size_t n_domains,
+                                  const uint32_t* dom_idx, uint8_t* out32);
+/* Device time (ms) of the kernels of the last signing-root call above. */
+int gbv_ssz_last_kernel_ms(gbv_ctx* ctx, float* ms_out);
+
 /* ---- utilities for tests and synthetic workloads (not on the verification path) ----------- */
 /* sk32 (big-endian scalars) -> compressed pubkeys, on the device. */
 int gbv_util_sk_to_pk(gbv_ctx* ctx, const uint8_t* sk32, size_t n, uint8_t* pk48);

@@ -23,7 +23,8 @@ EXPORTED_SYMBOLS = (
     "gbv_aggregate_pubkeys", "gbv_sm_batch_create", "gbv_sm_batch_verify", "gbv_sm_batch_destroy",
     "gbv_sm_batch_submit", "gbv_sm_batch_wait", "gbv_vs_partial", "gbv_fp12_check", "gbv_last_stats",
     "gbv_last_kernel_ms", "gbv_util_sk_to_pk", "gbv_util_sign", "gbv_util_hash_to_g2",
-    "gbv_pubkeys_replicate",
+    "gbv_pubkeys_replicate", "gbv_sha256_digest64", "gbv_merkle_roots", "gbv_signing_roots",
+    "gbv_attestation_signing_roots", "gbv_ssz_last_kernel_ms",
 )
 
 
@@ -89,6 +90,11 @@ def load_library(path=LIB_PATH):
         "gbv_util_sign": (i32, [vp, vp, sz, vp, vp, sz, vp]),
         "gbv_util_hash_to_g2": (i32, [vp, vp, sz, vp]),
         "gbv_pubkeys_replicate": (i32, [vp, u32, u32, u32, sz]),
+        "gbv_sha256_digest64": (i32, [vp, vp, sz, vp]),
+        "gbv_merkle_roots": (i32, [vp, vp, sz, u32, vp]),
+        "gbv_signing_roots": (i32, [vp, vp, sz, vp, sz, vp, vp]),
+        "gbv_attestation_signing_roots": (i32, [vp, vp, sz, vp, sz, vp, vp]),
+        "gbv_ssz_last_kernel_ms": (i32, [vp, P(ctypes.c_float)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

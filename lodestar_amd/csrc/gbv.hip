@@ -55,6 +55,11 @@ struct gbv_ctx {
   int last_launches[NK] = {};
   uint32_t last_fallback_chunks = 0, last_failed_segments = 0;
   bool closed = false;
+  // signing-root (SSZ) calls: grow-only device buffers [input, output, domains, domain indices]
+  uint8_t* ssz_buf[4] = {};
+  size_t ssz_cap[4] = {};
+  hipEvent_t ssz_ev[2] = {};
+  float last_ssz_ms = 0.f;
 };
 
 struct gbv_sm_batch {
@@ -172,6 +177,9 @@ void gbv_destroy(gbv_ctx* c) {
   if (c->stream) hipStreamSynchronize(c->stream);
   hipFree(c->table);
   hipFree(c->table_ok);
+  for (auto* p : c->ssz_buf) hipFree(p);
+  for (auto e : c->ssz_ev)
+    if (e) hipEventDestroy(e);
   if (c->stream2) hipStreamSynchronize(c->stream2);
   if (c->stream3) hipStreamSynchronize(c->stream3);
   if (c->stream4) hipStreamSynchronize(c->stream4);
@@ -696,6 +704,126 @@ int gbv_fp12_check(gbv_ctx* c, const uint8_t* partials, size_t k, uint8_t* is_on
 }
 
 // ---- utilities -----------------------------------------------------------------------------
+// ---- signing roots (SSZ) --------------------------------------------------------------------
+static int ssz_buf(gbv_ctx* c, int k, size_t bytes, uint8_t** out) {
+  if (c->ssz_cap[k] < bytes) {
+    hipFree(c->ssz_buf[k]);
+    c->ssz_buf[k] = nullptr;
+    c->ssz_cap[k] = 0;
+    size_t cap = std::max<size_t>(bytes, 1u << 20);
+    HIP_CHECK(c, hipMalloc((void**)&c->ssz_buf[k], cap));
+    c->ssz_cap[k] = cap;
+  }
+  *out = c->ssz_buf[k];
+  return GBV_OK;
+}
+
+static int ssz_begin(gbv_ctx* c) {
+  if (!c) return GBV_E_ARG;
+  if (c->closed) return GBV_E_CLOSED;
+  HIP_CHECK(c, hipSetDevice(c->device));
+  for (auto& e : c->ssz_ev)
+    if (!e) HIP_CHECK(c, hipEventCreate(&e));
+  c->last_ssz_ms = 0.f;
+  return GBV_OK;
+}
+
+// Copy n results back, wait, and record the device time between the two events.
+static int ssz_finish(gbv_ctx* c, const uint8_t* d_out, size_t n, uint8_t* out32) {
+  HIP_CHECK(c, hipGetLastError());
+  HIP_CHECK(c, hipEventRecord(c->ssz_ev[1], c->stream));
+  HIP_CHECK(c, hipMemcpyAsync(out32, d_out, 32 * n, hipMemcpyDeviceToHost, c->stream));
+  HIP_CHECK(c, hipStreamSynchronize(c->stream));
+  HIP_CHECK(c, hipEventElapsedTime(&c->last_ssz_ms, c->ssz_ev[0], c->ssz_ev[1]));
+  return GBV_OK;
+}
+
+// Stage domains (and per-item indices) for the signing-root kernels.
+static int ssz_domains(gbv_ctx* c, size_t n, const uint8_t* domains32, size_t n_domains, const uint32_t* dom_idx, uint8_t** d_dom,
+                       uint32_t** d_idx) {
+  if (!domains32 || n_domains == 0) return fail(c, GBV_E_ARG, "no domain");
+  if (dom_idx)
+    for (size_t i = 0; i < n; ++i)
+      if (dom_idx[i] >= n_domains) return fail(c, GBV_E_ARG, "domain index out of range");
+  int rc = ssz_buf(c, 2, 32 * n_domains, d_dom);
+  if (rc) return rc;
+  HIP_CHECK(c, hipMemcpyAsync(*d_dom, domains32, 32 * n_domains, hipMemcpyHostToDevice, c->stream));
+  *d_idx = nullptr;
+  if (dom_idx) {
+    uint8_t* p = nullptr;
+    if ((rc = ssz_buf(c, 3, 4 * n, &p))) return rc;
+    HIP_CHECK(c, hipMemcpyAsync(p, dom_idx, 4 * n, hipMemcpyHostToDevice, c->stream));
+    *d_idx = (uint32_t*)p;
+  }
+  return GBV_OK;
+}
+
+int gbv_sha256_digest64(gbv_ctx* c, const uint8_t* in64, size_t n, uint8_t* out32) { return gbv_merkle_roots(c, in64, n, 1, out32); }
+
+int gbv_merkle_roots(gbv_ctx* c, const uint8_t* chunks32, size_t n, uint32_t depth, uint8_t* out32) {
+  int rc = ssz_begin(c);
+  if (rc) return rc;
+  if (n == 0) return GBV_OK;
+  if (!chunks32 || !out32) return fail(c, GBV_E_ARG, "null argument");
+  if (depth > 24 || (n << depth) >> depth != n || (n << depth) > 0xFFFFFFFFull) return fail(c, GBV_E_ARG, "tree too large");
+  size_t leaves = n << depth;
+  uint8_t *a = nullptr, *b = nullptr;
+  if ((rc = ssz_buf(c, 0, 32 * leaves, &a))) return rc;
+  if ((rc = ssz_buf(c, 1, 32 * std::max<size_t>(leaves / 2, n), &b))) return rc;
+  HIP_CHECK(c, hipMemcpyAsync(a, chunks32, 32 * leaves, hipMemcpyHostToDevice, c->stream));
+  HIP_CHECK(c, hipEventRecord(c->ssz_ev[0], c->stream));
+  // one launch per tree level: sibling chunks are adjacent, so a level is a digest64 over pairs
+  for (uint32_t lvl = 0; lvl < depth; ++lvl) {
+    leaves /= 2;
+    launch_ssz_digest64(c->stream, a, (uint32_t)leaves, b);
+    debug_sync(c->stream, "k_ssz_digest64");
+    std::swap(a, b);
+  }
+  return ssz_finish(c, a, n, out32);
+}
+
+int gbv_signing_roots(gbv_ctx* c, const uint8_t* roots32, size_t n, const uint8_t* domains32, size_t n_domains, const uint32_t* dom_idx,
+                      uint8_t* out32) {
+  int rc = ssz_begin(c);
+  if (rc) return rc;
+  if (n == 0) return GBV_OK;
+  if (!roots32 || !out32) return fail(c, GBV_E_ARG, "null argument");
+  if (n > 0xFFFFFFFFull) return fail(c, GBV_E_ARG, "too many roots");
+  uint8_t *d_in = nullptr, *d_out = nullptr, *d_dom = nullptr;
+  uint32_t* d_idx = nullptr;
+  if ((rc = ssz_domains(c, n, domains32, n_domains, dom_idx, &d_dom, &d_idx))) return rc;
+  if ((rc = ssz_buf(c, 0, 32 * n, &d_in)) || (rc = ssz_buf(c, 1, 32 * n, &d_out))) return rc;
+  HIP_CHECK(c, hipMemcpyAsync(d_in, roots32, 32 * n, hipMemcpyHostToDevice, c->stream));
+  HIP_CHECK(c, hipEventRecord(c->ssz_ev[0], c->stream));
+  launch_ssz_signing_roots(c->stream, d_in, (uint32_t)n, d_dom, d_idx, d_out);
+  debug_sync(c->stream, "k_ssz_signing_roots");
+  return ssz_finish(c, d_out, n, out32);
+}
+
+int gbv_attestation_signing_roots(gbv_ctx* c, const uint8_t* data128, size_t n, const uint8_t* domains32, size_t n_domains,
+                                  const uint32_t* dom_idx, uint8_t* out32) {
+  int rc = ssz_begin(c);
+  if (rc) return rc;
+  if (n == 0) return GBV_OK;
+  if (!data128 || !out32) return fail(c, GBV_E_ARG, "null argument");
+  if (n > 0xFFFFFFFFull) return fail(c, GBV_E_ARG, "too many objects");
+  uint8_t *d_in = nullptr, *d_out = nullptr, *d_dom = nullptr;
+  uint32_t* d_idx = nullptr;
+  if ((rc = ssz_domains(c, n, domains32, n_domains, dom_idx, &d_dom, &d_idx))) return rc;
+  if ((rc = ssz_buf(c, 0, 128 * n, &d_in)) || (rc = ssz_buf(c, 1, 32 * n, &d_out))) return rc;
+  HIP_CHECK(c, hipMemcpyAsync(d_in, data128, 128 * n, hipMemcpyHostToDevice, c->stream));
+  HIP_CHECK(c, hipEventRecord(c->ssz_ev[0], c->stream));
+  launch_ssz_att_signing_roots(c->stream, d_in, (uint32_t)n, d_dom, d_idx, d_out);
+  debug_sync(c->stream, "k_ssz_att_signing_roots");
+  return ssz_finish(c, d_out, n, out32);
+}
+
+int gbv_ssz_last_kernel_ms(gbv_ctx* c, float* ms) {
+  if (!c || !ms) return GBV_E_ARG;
+  *ms = c->last_ssz_ms;
+  return GBV_OK;
+}
+
 int gbv_util_sk_to_pk(gbv_ctx* c, const uint8_t* sk32, size_t n, uint8_t* pk48) {
   if (!c || (n && (!sk32 || !pk48))) return GBV_E_ARG;
   if (n == 0) return GBV_OK;

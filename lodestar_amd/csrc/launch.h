@@ -43,6 +43,12 @@ void launch_vs_prepare(LaunchCfg c, uint32_t n, const uint32_t* set_idx_off, con
                        const uint8_t* raw_pk48, const uint8_t* msgs32, const uint8_t* sig, uint32_t sig_stride, const uint32_t* sig_len,
                        const G1A* table, const uint8_t* table_ok, const Seed& seed, uint32_t nonce, Fp12* f_out, G2J* rS_out,
                        uint8_t* status);
+
+void launch_ssz_digest64(hipStream_t s, const uint8_t* in64, uint32_t n, uint8_t* out32);
+void launch_ssz_signing_roots(hipStream_t s, const uint8_t* roots32, uint32_t n, const uint8_t* domains32, const uint32_t* dom_idx,
+                              uint8_t* out32);
+void launch_ssz_att_signing_roots(hipStream_t s, const uint8_t* data128, uint32_t n, const uint8_t* domains32, const uint32_t* dom_idx,
+                                  uint8_t* out32);
 }  // namespace gbv
 
 namespace gbv {

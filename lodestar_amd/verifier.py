@@ -177,6 +177,19 @@ class GpuBlsVerifier:
         self.metrics["device_passes"] += 1
         return bool(allv.value)
 
+    def verify_signature_set(self, s: ISignatureSet) -> bool:
+        """Synchronous single-set verification used inside the state transition
+        (state-transition/src/util/signatureSets.ts:25-39): verify for a single set,
+        fastAggregateVerify for an aggregate one, the signature group-checked in both.
+
+        The reference throws from Signature.fromBytes on a malformed signature; its callers turn
+        either a throw or false into the same rejection, so both are False here.  An aggregate set
+        with no pubkeys is False (blst's fast_aggregate_verify reports an error code rather than
+        throwing; unpinned at the blst boundary)."""
+        if isinstance(s, AggregatedSignatureSet) and len(s.indices) == 0:
+            return False
+        return self.verify_signature_sets_sync([s])
+
     # ---- multi-GPU shards (lodestar_amd/sharded.py) --------------------------------------------
     def vs_partial(self, sets: Sequence[ISignatureSet]) -> Tuple[bytes, bool]:
         """This device's Fp12 Miller product over a shard of a verifySignatureSets call
@@ -381,6 +394,74 @@ class GpuBlsVerifier:
             self._busy -= 1
         if self._jobs:
             self._schedule()
+
+    # ---- signing roots (SSZ hashing on the device) ------------------------
+    @staticmethod
+    def _blob(items, size, what):
+        blob = items if isinstance(items, (bytes, bytearray, memoryview)) else b"".join(bytes(x) for x in items)
+        blob = bytes(blob)
+        if len(blob) % size:
+            raise ValueError("%s must be %d-byte items" % (what, size))
+        return blob, len(blob) // size
+
+    @staticmethod
+    def _roots(out, n):
+        raw = out.raw
+        return [raw[32 * i:32 * i + 32] for i in range(n)]
+
+    def _domains(self, domains, dom_idx, n):
+        dblob, nd = self._blob([domains] if isinstance(domains, (bytes, bytearray)) and len(domains) == 32 else domains, 32, "domains")
+        idx = None
+        if dom_idx is not None:
+            if len(dom_idx) != n:
+                raise ValueError("one domain index per item")
+            idx = (ctypes.c_uint32 * max(n, 1))(*dom_idx)
+        return dblob, nd, idx
+
+    def sha256_digest64(self, inputs) -> List[bytes]:
+        """hasher.digest64 over 64-byte inputs (persistent-merkle-tree; as-sha256 digest64)."""
+        self._check_open()
+        blob, n = self._blob(inputs, 64, "inputs")
+        out = ctypes.create_string_buffer(max(32 * n, 1))
+        _native.check(self._lib, self._ctx, self._lib.gbv_sha256_digest64(self._ctx, blob, n, out))
+        return self._roots(out, n)
+
+    def merkle_roots(self, chunks, depth: int) -> List[bytes]:
+        """Roots of objects of 2**depth 32-byte chunks each (ContainerType.hashTreeRoot over the
+        field roots, zero padding in place)."""
+        self._check_open()
+        blob, nchunks = self._blob(chunks, 32, "chunks")
+        if nchunks % (1 << depth):
+            raise ValueError("chunk count must be a multiple of 2**depth")
+        n = nchunks >> depth
+        out = ctypes.create_string_buffer(max(32 * n, 1))
+        _native.check(self._lib, self._ctx, self._lib.gbv_merkle_roots(self._ctx, blob, n, depth, out))
+        return self._roots(out, n)
+
+    def compute_signing_roots(self, object_roots, domains, dom_idx: Optional[Sequence[int]] = None) -> List[bytes]:
+        """computeSigningRoot(type, obj, domain) from hash_tree_root(obj) (util/signingRoot.ts:7-13).
+        domains: one 32-byte domain, or a list indexed by dom_idx."""
+        self._check_open()
+        blob, n = self._blob(object_roots, 32, "object roots")
+        dblob, nd, idx = self._domains(domains, dom_idx, n)
+        out = ctypes.create_string_buffer(max(32 * n, 1))
+        _native.check(self._lib, self._ctx, self._lib.gbv_signing_roots(self._ctx, blob, n, dblob, nd, idx, out))
+        return self._roots(out, n)
+
+    def attestation_data_signing_roots(self, datas, domains, dom_idx: Optional[Sequence[int]] = None) -> List[bytes]:
+        """getAttestationDataSigningRoot (chain/validation/attestation.ts:657-665) for 128-byte SSZ
+        phase0 AttestationData values."""
+        self._check_open()
+        blob, n = self._blob(datas, 128, "AttestationData")
+        dblob, nd, idx = self._domains(domains, dom_idx, n)
+        out = ctypes.create_string_buffer(max(32 * n, 1))
+        _native.check(self._lib, self._ctx, self._lib.gbv_attestation_signing_roots(self._ctx, blob, n, dblob, nd, idx, out))
+        return self._roots(out, n)
+
+    def ssz_last_kernel_ms(self) -> float:
+        ms = ctypes.c_float(0)
+        _native.check(self._lib, self._ctx, self._lib.gbv_ssz_last_kernel_ms(self._ctx, ctypes.byref(ms)))
+        return float(ms.value)
 
     # ---- utilities (synthetic workloads / tests; not on the verification path) ----------------
     def util_sk_to_pk(self, sks32: Sequence[bytes]) -> List[bytes]:

@@ -5,6 +5,7 @@
 #include "../../lodestar_amd/csrc/pairing.h"
 #include "../../lodestar_amd/csrc/hash_to_curve.h"
 #include "../../lodestar_amd/csrc/coop.h"
+#include "../../lodestar_amd/csrc/ssz.h"
 #include <vector>
 
 using namespace gbv;
@@ -123,5 +124,20 @@ int ht_randomize(uint8_t* outp, uint8_t* outq, const uint8_t* p96, const uint8_t
   store_canon(outp, pa.x); store_canon(outp + 48, pa.y);
   store_fp2(outq, qa.x); store_fp2(outq + 96, qa.y);
   return 1;
+}
+// SSZ hashing (sha256.h / ssz.h): 64 bytes -> sha256, and the AttestationData signing root.
+static u32x8 ht_chunk_be(const uint8_t* p) {
+  u32x8 r;
+  for (int i = 0; i < 8; ++i) r[i] = ((uint32_t)p[4*i] << 24) | ((uint32_t)p[4*i+1] << 16) | ((uint32_t)p[4*i+2] << 8) | p[4*i+3];
+  return r;
+}
+static void ht_store_be(uint8_t* o, u32x8 r) {
+  for (int i = 0; i < 8; ++i) { o[4*i] = r[i] >> 24; o[4*i+1] = r[i] >> 16; o[4*i+2] = r[i] >> 8; o[4*i+3] = r[i]; }
+}
+void ht_digest64(uint8_t* out32, const uint8_t* in64) { ht_store_be(out32, sha256_digest64(sha256_cat(ht_chunk_be(in64), ht_chunk_be(in64 + 32)))); }
+void ht_att_signing_root(uint8_t* out32, const uint8_t* data128, const uint8_t* domain32) {
+  uint32_t d[32];
+  for (int i = 0; i < 32; ++i) d[i] = (uint32_t)data128[4*i] | ((uint32_t)data128[4*i+1] << 8) | ((uint32_t)data128[4*i+2] << 16) | ((uint32_t)data128[4*i+3] << 24);
+  ht_store_be(out32, ssz_signing_root(ssz_attestation_data_root(d), ht_chunk_be(domain32)));
 }
 }
