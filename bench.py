@@ -162,6 +162,23 @@ def signing_roots_bench(v, n=1 << 20, reps=5, cpu_sample=20000):
     return out
 
 
+def inject_invalid(sigs, call_off, n_sets, frac):
+    """SURVEY 8(d) C5 recipe: `frac` of the sets chosen by PCG64(0xC0FFEE); 90 % of them get a valid
+    point signed over another message (the signature of a set in a later call, bls.test.ts:73 pattern),
+    10 % the malformed bytes([10]*96) (bls.test.ts:79).  Returns (sigs, expected valid count)."""
+    rng = np.random.Generator(np.random.PCG64(0xC0FFEE))
+    bad = np.sort(rng.choice(n_sets, size=int(round(frac * n_sets)), replace=False))
+    buf = bytearray(sigs)
+    shift = int(call_off[-1] - call_off[-2]) + 256  # lands in another call, so another message
+    for k, i in enumerate(bad.tolist()):
+        if k % 10 == 9:
+            buf[96 * i:96 * i + 96] = bytes([10]) * 96
+        else:
+            j = (i + shift) % n_sets
+            buf[96 * i:96 * i + 96] = sigs[96 * j:96 * j + 96]
+    return bytes(buf), n_sets - len(bad)
+
+
 def p50_batch_latency(v, call_off, idx, sigs, msgs, reps=20):
     """Latency of one gossip batch (one verifySignatureSetsSameMessage call of 64 sets) alone."""
     n = 64
@@ -181,6 +198,8 @@ def main():
     ap.add_argument("--sets", type=int, default=1 << 20)
     ap.add_argument("--cpu-sample", type=int, default=None, help="sets in the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--invalid-frac", type=float, default=0.0,
+                    help="C5: fraction of invalid sets (90%% wrong-message signatures, 10%% malformed bytes)")
     ap.add_argument("--no-signing-roots", action="store_true", help="skip the signing-root secondary line")
     ap.add_argument("--no-stream", dest="stream", action="store_false",
                     help="one batch at a time (no overlap of consecutive verifications)")
@@ -204,6 +223,10 @@ def main():
     build()
     v = GpuBlsVerifier(local_rank)
     call_off, idx, sigs, msgs, key_pks = build_workload(v, args.sets, rank, log)
+    expect_valid = args.sets
+    if args.invalid_frac > 0:
+        sigs, expect_valid = inject_invalid(sigs, call_off, args.sets, args.invalid_frac)
+        log("injected %d invalid sets (C5 recipe)" % (args.sets - expect_valid))
     staged = v.stage_same_message(call_off, idx, sigs, msgs)
     # streaming submission: two staged copies of the workload so that one batch's chunk-level tail
     # overlaps the next batch's per-set kernel (each verification still runs start to finish)
@@ -213,8 +236,8 @@ def main():
         res = staged.verify(True)
     if args.warmup:
         ok = res.count(1)
-        assert ok == args.sets, "warmup: %d of %d sets verified" % (ok, args.sets)
-        log("warmup ok: all %d sets valid" % ok)
+        assert ok == expect_valid, "warmup: %d of %d sets verified" % (ok, expect_valid)
+        log("warmup ok: %d of %d sets valid" % (ok, args.sets))
 
     kms = np.zeros(len(KERNELS))
     kcnt = np.zeros(len(KERNELS))
@@ -257,8 +280,8 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    assert n_valid == [args.sets] * args.steps, n_valid
-    if slow_path != [0, 0]:
+    assert n_valid == [expect_valid] * args.steps, n_valid
+    if slow_path != [0, 0] and not args.invalid_frac:
         log("WARNING: fast path fell back (chunks, segments) = %s on an all-valid workload" % slow_path)
     avg_launch_ms = kms / np.maximum(kcnt, 1)
     kms /= max(args.steps, 1)
@@ -313,7 +336,8 @@ def main():
         "config": {"workload": "C2 gossip attestation stream: 1M single-pubkey sets, same-message calls of 32-128",
                    "sets_per_gpu": args.sets, "calls_per_gpu": n_chunks, "table": N_VALIDATORS,
                    "parallelism": "replicas/dp%d" % world,
-                   "submission": "streamed: 2 batches in flight" if args.stream else "one batch at a time"},
+                   "submission": "streamed: 2 batches in flight" if args.stream else "one batch at a time",
+                   "invalid_frac": args.invalid_frac},
         "roofline": roofline,
         "cpu_baseline": cpu,
         "signing_roots": ssz,

@@ -19,6 +19,10 @@ namespace {
 
 constexpr uint32_t MAX_SIGNATURE_SETS_PER_JOB = 128;  // multithread/index.ts:56
 constexpr int TPB = 64;
+constexpr unsigned FB_GRID = 2048;
+// a failing segment with at least this many chunks checks them one thread each (throughput), below
+// it one wave each (latency); see k_sm_group_check / k_sm_group_pairing
+constexpr uint32_t GROUP_CHECK_THREAD_MIN = 512;  // persistent failure-path grids: 2 waves per SIMD
 
 // chunkifyMaximizeChunkSize (multithread/utils.ts:4-18): returns chunk start offsets + end.
 std::vector<uint32_t> chunk_offsets(uint32_t len, uint32_t min_per_chunk) {
@@ -84,6 +88,11 @@ struct gbv_sm_batch {
   uint8_t* has = nullptr;
   G1J* rP = nullptr;
   G1J* PgJ = nullptr;
+  // failure path lists: runs of failed chunks (head, end, chunk), then sets of failing runs
+  uint4* fb_runs = nullptr;
+  uint32_t* fb_list = nullptr;
+  uint32_t* fb_cnt = nullptr;  // [runs, listed sets]
+  size_t fb_cap = 0;
 };
 
 static int fail(gbv_ctx* c, int code, const std::string& msg) {
@@ -294,6 +303,7 @@ void gbv_sm_batch_destroy(gbv_ctx* c, gbv_sm_batch* b) {
   hipHostFree(b->nfb_host);
   hipFree(b->F); hipFree(b->seg_ok); hipHostFree(b->seg_ok_host);
   hipFree(b->Fpart); hipFree(b->Spart); hipFree(b->has);
+  hipFree(b->fb_runs); hipFree(b->fb_list); hipFree(b->fb_cnt);
   delete b;
 }
 
@@ -340,6 +350,8 @@ int gbv_sm_batch_create(gbv_ctx* c, size_t n_calls, const uint32_t* call_off, co
   // block partials: one region per segment stream (two segments' reductions can be in flight)
   chk(dalloc(&b->Fpart, 2 * (G / 64 + G / 4096 + 4))); chk(dalloc(&b->Spart, 2 * (G / 64 + G / 4096 + 4)));
   chk(dalloc(&b->has, 2 * (G / 64 + G / 4096 + 4)));
+  b->fb_cap = n / 8 + G + 64;  // runs: at most one per 8-set window plus one per chunk start
+  chk(dalloc(&b->fb_runs, b->fb_cap)); chk(dalloc(&b->fb_list, n)); chk(dalloc(&b->fb_cnt, 2));
   b->seg_cap = 64;
   chk(dalloc(&b->seg_ok, b->seg_cap));
   chk(hipHostMalloc((void**)&b->seg_ok_host, b->seg_cap, hipHostMallocDefault));
@@ -412,6 +424,7 @@ int gbv_sm_batch_submit(gbv_ctx* c, gbv_sm_batch* b) {
   hipEvent_t* ev = b->ev.data();
   const size_t part_stride = b->G / 64 + b->G / 4096 + 4;
   HIP_CHECK(c, hipMemsetAsync(b->n_fallback, 0, 4, sh));
+  HIP_CHECK(c, hipMemsetAsync(b->fb_cnt, 0, 8, sh));
   hipEventRecord(ev[0], sh);
   launch_hash_msgs(LaunchCfg{blocks_for(b->n_calls), TPB, sh}, b->msgs, (uint32_t)b->n_calls, b->H);
   hipEventRecord(ev[1], sh);
@@ -439,7 +452,10 @@ int gbv_sm_batch_submit(gbv_ctx* c, gbv_sm_batch* b) {
                         b->seg_ok + s);
     hipEventRecord(e[7], sb);
     hipEventRecord(e[8], sb);
-    launch_sm_group_pairing(LaunchCfg{G, 64, sb}, g0, G, b->grp_msg, b->PgJ, b->SgJ, b->H, b->seg_ok + s, b->grp_state, b->n_fallback);
+    if (G >= GROUP_CHECK_THREAD_MIN)
+      launch_sm_group_check(LaunchCfg{0, 64, sb}, g0, G, b->F, b->SgJ, b->seg_ok + s, b->grp_state, b->n_fallback);
+    else
+      launch_sm_group_pairing(LaunchCfg{G, 64, sb}, g0, G, b->grp_msg, b->PgJ, b->SgJ, b->H, b->seg_ok + s, b->grp_state, b->n_fallback);
     hipEventRecord(e[9], sb);
   }
   hipEvent_t* ep = ev + 2 + 10 * S;
@@ -449,8 +465,18 @@ int gbv_sm_batch_submit(gbv_ctx* c, gbv_sm_batch* b) {
     HIP_CHECK(c, hipStreamWaitEvent(sbs[0], ev[2 + 10 * last_b1 + 9], 0));
   }
   hipEventRecord(ep[0], sbs[0]);
+  // valid = 1 for the sets of passing chunks; the sets of failed chunks go through 8-set run
+  // checks and, for failing runs only, per-set checks (compacted lists, persistent grids)
   launch_sm_fallback(LaunchCfg{blocks_for(b->n), TPB, sbs[0]}, (uint32_t)b->n, b->set_grp, b->grp_msg, b->grp_state, b->status, b->idx,
-                     c->table, b->S, b->H, b->valid, 1);
+                     c->table, b->S, b->H, b->valid, 0);
+  for (size_t s = 0; s < S; ++s) {
+    uint32_t s0 = b->grp_off_host[gcut[s]], s1 = b->grp_off_host[gcut[s + 1]];
+    launch_sm_fb_runs(LaunchCfg{0, 64, sbs[0]}, s0, s1 - s0, b->set_grp, b->grp_state, b->fb_runs, b->fb_cnt, (uint32_t)b->fb_cap);
+  }
+  launch_sm_fb_blocks(LaunchCfg{FB_GRID, 64, sbs[0]}, b->fb_runs, b->fb_cnt, (uint32_t)b->fb_cap, b->status, b->grp_msg, b->rS, b->rP, b->H,
+                      b->valid, b->fb_list, b->fb_cnt + 1);
+  launch_sm_fb_sets(LaunchCfg{FB_GRID, 64, sbs[0]}, b->fb_list, b->fb_cnt + 1, b->set_grp, b->grp_msg, b->idx, c->table, b->S, b->H,
+                    b->valid);
   hipEventRecord(ep[1], sbs[0]);
   HIP_CHECK(c, hipMemcpyAsync(b->valid_host, b->valid, b->n, hipMemcpyDeviceToHost, sbs[0]));
   HIP_CHECK(c, hipMemcpyAsync(b->nfb_host, b->n_fallback, sizeof(uint32_t), hipMemcpyDeviceToHost, sbs[0]));
