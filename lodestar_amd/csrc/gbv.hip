@@ -19,10 +19,12 @@ namespace {
 
 constexpr uint32_t MAX_SIGNATURE_SETS_PER_JOB = 128;  // multithread/index.ts:56
 constexpr int TPB = 64;
-constexpr unsigned FB_GRID = 2048;
+constexpr unsigned FB_GRID = 2048;  // persistent failure-path grids: 2 waves per SIMD
 // a failing segment with at least this many chunks checks them one thread each (throughput), below
 // it one wave each (latency); see k_sm_group_check / k_sm_group_pairing
-constexpr uint32_t GROUP_CHECK_THREAD_MIN = 512;  // persistent failure-path grids: 2 waves per SIMD
+constexpr uint32_t GROUP_CHECK_THREAD_MIN = 512;
+// segments of at most this many chunks skip the combined segment check (latency of small calls)
+constexpr uint32_t DIRECT_CHUNK_MAX = 32;
 
 // chunkifyMaximizeChunkSize (multithread/utils.ts:4-18): returns chunk start offsets + end.
 std::vector<uint32_t> chunk_offsets(uint32_t len, uint32_t min_per_chunk) {
@@ -75,6 +77,7 @@ struct gbv_sm_batch {
   uint8_t* valid_host = nullptr;   // pinned, n bytes: results of the last submitted verify
   uint32_t* nfb_host = nullptr;    // pinned: fallback chunk count of the last submitted verify
   size_t seg_cap = 0;
+  std::vector<uint8_t> seg_direct = std::vector<uint8_t>(64);  // per segment: combined check skipped
   // in-flight state of the last gbv_sm_batch_submit
   bool in_flight = false;
   size_t n_seg = 0;
@@ -443,13 +446,19 @@ int gbv_sm_batch_submit(gbv_ctx* c, gbv_sm_batch* b) {
     launch_sm_chunk_finish(LaunchCfg{0, 64, sb}, g0, G, s0, b->grp_off, b->status, b->rS, b->rP, b->PgJ, b->SgJ, b->grp_state,
                            b->n_fallback);
     hipEventRecord(e[3], sb);
+    // a segment of a few chunks (a lone gossip call) skips the combined check: each chunk goes
+    // straight to its own one-wave check, which is the shorter dependency chain
+    b->seg_direct[s] = G <= DIRECT_CHUNK_MAX;
     hipEventRecord(e[4], sb);
-    launch_sm_miller(LaunchCfg{0, 64, sb}, g0, G, b->grp_msg, b->grp_state, b->PgJ, b->H, b->F);
+    if (!b->seg_direct[s]) launch_sm_miller(LaunchCfg{0, 64, sb}, g0, G, b->grp_msg, b->grp_state, b->PgJ, b->H, b->F);
     hipEventRecord(e[5], sb);
     hipEventRecord(e[6], sb);
     size_t po = (s & 1) * part_stride;
-    launch_sm_seg_check(LaunchCfg{1, 64, sb}, g0, G, b->grp_state, b->F, b->SgJ, b->Fpart + po, b->Spart + po, b->has + po,
-                        b->seg_ok + s);
+    if (b->seg_direct[s])
+      HIP_CHECK(c, hipMemsetAsync(b->seg_ok + s, 0, 1, sb));
+    else
+      launch_sm_seg_check(LaunchCfg{1, 64, sb}, g0, G, b->grp_state, b->F, b->SgJ, b->Fpart + po, b->Spart + po, b->has + po,
+                          b->seg_ok + s);
     hipEventRecord(e[7], sb);
     hipEventRecord(e[8], sb);
     if (G >= GROUP_CHECK_THREAD_MIN)
@@ -473,8 +482,13 @@ int gbv_sm_batch_submit(gbv_ctx* c, gbv_sm_batch* b) {
     uint32_t s0 = b->grp_off_host[gcut[s]], s1 = b->grp_off_host[gcut[s + 1]];
     launch_sm_fb_runs(LaunchCfg{0, 64, sbs[0]}, s0, s1 - s0, b->set_grp, b->grp_state, b->fb_runs, b->fb_cnt, (uint32_t)b->fb_cap);
   }
+  // few items: one wave each (latency); many: one thread each (throughput) -- one of each pair exits
+  launch_sm_fb_blocks_coop(LaunchCfg{0, 64, sbs[0]}, b->fb_runs, b->fb_cnt, (uint32_t)b->fb_cap, b->status, b->grp_msg, b->rS, b->rP,
+                           b->H, b->valid, b->fb_list, b->fb_cnt + 1);
   launch_sm_fb_blocks(LaunchCfg{FB_GRID, 64, sbs[0]}, b->fb_runs, b->fb_cnt, (uint32_t)b->fb_cap, b->status, b->grp_msg, b->rS, b->rP, b->H,
                       b->valid, b->fb_list, b->fb_cnt + 1);
+  launch_sm_fb_sets_coop(LaunchCfg{0, 64, sbs[0]}, b->fb_list, b->fb_cnt + 1, b->set_grp, b->grp_msg, b->idx, c->table, b->S, b->H,
+                         b->valid);
   launch_sm_fb_sets(LaunchCfg{FB_GRID, 64, sbs[0]}, b->fb_list, b->fb_cnt + 1, b->set_grp, b->grp_msg, b->idx, c->table, b->S, b->H,
                     b->valid);
   hipEventRecord(ep[1], sbs[0]);
@@ -497,7 +511,7 @@ int gbv_sm_batch_wait(gbv_ctx* c, gbv_sm_batch* b, uint8_t* valid) {
   if (valid) memcpy(valid, b->valid_host, b->n);
   c->last_fallback_chunks = *b->nfb_host;
   c->last_failed_segments = 0;
-  for (size_t s = 0; s < b->n_seg; ++s) c->last_failed_segments += b->seg_ok_host[s] ? 0 : 1;
+  for (size_t s = 0; s < b->n_seg; ++s) c->last_failed_segments += (b->seg_ok_host[s] || b->seg_direct[s]) ? 0 : 1;
   for (auto& x : c->last_ms) x = 0.f;
   for (auto& x : c->last_launches) x = 0;
   hipEvent_t* ev = b->ev.data();

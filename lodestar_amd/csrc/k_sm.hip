@@ -255,6 +255,7 @@ __global__ void GBV_KERNEL_ATTR k_sm_fb_blocks(const uint4* __restrict__ runs, c
                                                const G2J* __restrict__ Sh, const G1J* __restrict__ Ph, const G2A* __restrict__ H,
                                                uint8_t* __restrict__ valid, uint32_t* __restrict__ set_list, uint32_t* __restrict__ n_list) {
   uint32_t cnt = min(*n_runs, cap);
+  if (cnt <= FB_COOP_MAX) return;  // k_sm_fb_blocks_coop has them
   for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < cnt; k += gridDim.x * blockDim.x) {
     uint4 r = runs[k];
     bool any = false;
@@ -285,6 +286,7 @@ __global__ void GBV_KERNEL_ATTR k_sm_fb_sets(const uint32_t* __restrict__ set_li
                                              const uint32_t* __restrict__ idx, const G1A* __restrict__ table, const G2A* __restrict__ S,
                                              const G2A* __restrict__ H, uint8_t* __restrict__ valid) {
   uint32_t cnt = *n_list;
+  if (cnt <= FB_COOP_MAX) return;  // k_sm_fb_sets_coop has them
   for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < cnt; k += gridDim.x * blockDim.x) {
     uint32_t i = set_list[k];
     valid[i] = pairing_check_2(table[idx[i]], false, H[grp_msg[set_grp[i]]], g1_neg_generator(), false, S[i]) ? 1 : 0;

@@ -149,6 +149,100 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
 }
 
 
+// e(P, Q) * e(-g1, S) == 1 by one wave (S = infinity drops the second pair).  Arguments must be
+// wave-uniform (the callers stage them in LDS).
+__device__ inline bool coop_pair_check(Fp* ws, const G1A& P, const G2A& Q, bool s_inf, const G2A& S) {
+  coop::miller_load_pair(ws, 0, P, Q);
+  int np = 1;
+  if (!s_inf) {
+    coop::miller_load_pair(ws, 1, g1_neg_generator(), S);
+    np = 2;
+  }
+  coop::miller_loop(ws, np);
+  Fp* fe = ws + coop::MILLER_WS;
+  coop::copy(fe + coop::E_F, ws + coop::M_F, 12);
+  return coop::final_exp_is_one(fe);
+}
+
+// Failure path for few items (<= FB_COOP_MAX): the run checks and per-set checks of
+// k_sm_fb_blocks / k_sm_fb_sets with one wave per item, for latency.  Both variants are launched;
+// the one that does not own the item count exits at once.
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
+k_sm_fb_blocks_coop(const uint4* __restrict__ runs, const uint32_t* __restrict__ n_runs, uint32_t cap, const uint8_t* __restrict__ status,
+                    const uint32_t* __restrict__ grp_msg, const G2J* __restrict__ Sh, const G1J* __restrict__ Ph, const G2A* __restrict__ H,
+                    uint8_t* __restrict__ valid, uint32_t* __restrict__ set_list, uint32_t* __restrict__ n_list) {
+  __shared__ Fp ws[SEG_WS];
+  __shared__ Fp st[6];
+  __shared__ int flags[3];
+  uint32_t cnt = min(*n_runs, cap);
+  if (cnt > FB_COOP_MAX) return;
+  unsigned lane = threadIdx.x;
+  for (uint32_t k = blockIdx.x; k < cnt; k += gridDim.x) {
+    uint4 r = runs[k];
+    if (lane == 0) {
+      bool any = false;
+      for (uint32_t i = r.x; i < r.y; ++i) any |= status[i] == SET_OK;
+      G1A pa = G1A{fp_zero(), fp_zero()};
+      G2A sa = G2A{fp2_zero(), fp2_zero()};
+      flags[0] = any;
+      flags[1] = any && jac_to_aff(pa, Ph[r.x]);
+      flags[2] = any && jac_to_aff(sa, Sh[r.x]);
+      st[0] = pa.x;
+      st[1] = pa.y;
+      st[2] = sa.x.c0;
+      st[3] = sa.x.c1;
+      st[4] = sa.y.c0;
+      st[5] = sa.y.c1;
+    }
+    coop::barrier();
+    bool ok = true;
+    if (flags[0]) {
+      ok = false;
+      if (flags[1])
+        ok = coop_pair_check(ws, G1A{st[0], st[1]}, H[grp_msg[r.z]], !flags[2], G2A{Fp2{st[2], st[3]}, Fp2{st[4], st[5]}});
+    }
+    if (lane == 0)
+      for (uint32_t i = r.x; i < r.y; ++i) {
+        if (status[i] != SET_OK)
+          valid[i] = 0;
+        else if (ok)
+          valid[i] = 1;
+        else
+          set_list[atomicAdd(n_list, 1u)] = i;
+      }
+    coop::barrier();
+  }
+}
+
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
+k_sm_fb_sets_coop(const uint32_t* __restrict__ set_list, const uint32_t* __restrict__ n_list, const uint32_t* __restrict__ set_grp,
+                  const uint32_t* __restrict__ grp_msg, const uint32_t* __restrict__ idx, const G1A* __restrict__ table,
+                  const G2A* __restrict__ S, const G2A* __restrict__ H, uint8_t* __restrict__ valid) {
+  __shared__ Fp ws[SEG_WS];
+  uint32_t cnt = *n_list;
+  if (cnt > FB_COOP_MAX) return;
+  for (uint32_t k = blockIdx.x; k < cnt; k += gridDim.x) {
+    uint32_t i = set_list[k];
+    bool ok = coop_pair_check(ws, table[idx[i]], H[grp_msg[set_grp[i]]], false, S[i]);
+    if (threadIdx.x == 0) valid[i] = ok ? 1 : 0;
+    coop::barrier();
+  }
+}
+
+void launch_sm_fb_blocks_coop(LaunchCfg c, const uint4* runs, const uint32_t* n_runs, uint32_t cap, const uint8_t* status,
+                              const uint32_t* grp_msg, const G2J* Sh, const G1J* Ph, const G2A* H, uint8_t* valid, uint32_t* set_list,
+                              uint32_t* n_list) {
+  hipLaunchKernelGGL(k_sm_fb_blocks_coop, dim3(FB_COOP_MAX), dim3(64), 0, c.stream, runs, n_runs, cap, status, grp_msg, Sh, Ph, H, valid,
+                     set_list, n_list);
+  debug_sync(c.stream, "k_sm_fb_blocks_coop");
+}
+void launch_sm_fb_sets_coop(LaunchCfg c, const uint32_t* set_list, const uint32_t* n_list, const uint32_t* set_grp, const uint32_t* grp_msg,
+                            const uint32_t* idx, const G1A* table, const G2A* S, const G2A* H, uint8_t* valid) {
+  hipLaunchKernelGGL(k_sm_fb_sets_coop, dim3(FB_COOP_MAX), dim3(64), 0, c.stream, set_list, n_list, set_grp, grp_msg, idx, table, S, H,
+                     valid);
+  debug_sync(c.stream, "k_sm_fb_sets_coop");
+}
+
 void launch_sm_seg_check(LaunchCfg c, uint32_t g0, uint32_t G, uint8_t* grp_state, const Fp12* F, const G2J* SgJ, Fp12* Fpart, G2J* Spart,
                          uint8_t* has, uint8_t* seg_ok, Fp12* miller_out) {
   uint32_t nb = 0;

@@ -36,6 +36,9 @@ struct Seed { uint32_t w[8]; };
 
 enum : uint8_t { SET_OK = 0, SET_BAD_SIG = 1, SET_BAD_PK = 2 };
 enum : uint8_t { GRP_PENDING = 0, GRP_FALLBACK = 1, GRP_OK = 2 };
+// Failure-path item counts up to which one wave per item (k_sm_fb_*_coop, latency) beats one
+// thread per item (k_sm_fb_blocks / k_sm_fb_sets, throughput).
+constexpr uint32_t FB_COOP_MAX = 256;
 
 // Per-set random 64-bit scalar r_i = SHA-256(seed || i || nonce)[0..8), forced non-zero.
 // blst draws 64-bit random scalars for the same purpose; only the booleans are compared.

@@ -41,6 +41,12 @@ void launch_sm_fb_blocks(LaunchCfg c, const uint4* runs, const uint32_t* n_runs,
 void launch_sm_fb_sets(LaunchCfg c, const uint32_t* set_list, const uint32_t* n_list, const uint32_t* set_grp, const uint32_t* grp_msg,
                        const uint32_t* idx, const G1A* table, const G2A* S, const G2A* H, uint8_t* valid);
 
+void launch_sm_fb_blocks_coop(LaunchCfg c, const uint4* runs, const uint32_t* n_runs, uint32_t cap, const uint8_t* status,
+                              const uint32_t* grp_msg, const G2J* Sh, const G1J* Ph, const G2A* H, uint8_t* valid, uint32_t* set_list,
+                              uint32_t* n_list);
+void launch_sm_fb_sets_coop(LaunchCfg c, const uint32_t* set_list, const uint32_t* n_list, const uint32_t* set_grp, const uint32_t* grp_msg,
+                            const uint32_t* idx, const G1A* table, const G2A* S, const G2A* H, uint8_t* valid);
+
 void launch_pk_decompress(LaunchCfg c, uint32_t n, const uint8_t* pk48, int validate, G1A* table, uint8_t* table_ok, uint8_t* status);
 void launch_pk_replicate(LaunchCfg c, G1A* table, uint8_t* table_ok, uint32_t src_first, uint32_t src_n, uint32_t dst_first, uint32_t n);
 void launch_aggregate(LaunchCfg c, const uint32_t* idx, uint32_t k, const G1A* table, const uint8_t* table_ok, uint8_t* out48,

@@ -100,6 +100,32 @@ def test_same_message_injected_invalid(world, segments):
     assert res == expected
 
 
+def test_same_message_one_percent_invalid(world):
+    """C5-style density: 1 % of 60 000 sets invalid, so hundreds of chunks fail.  The
+    failure path then runs its thread-per-item kernels (group checks, 8-set run checks, per-set
+    checks: more than FB_COOP_MAX items each) and must still return exactly the per-set booleans."""
+    v, sks, _ = world
+    off, idx, grp, sigs, msgs = _workload(v, sks, 60000, 14)
+    n = len(sigs)
+    rng = np.random.Generator(np.random.PCG64(0xC0FFEE))
+    bad = sorted(rng.choice(n, size=n // 100, replace=False).tolist())
+    sigs = list(sigs)
+    for k, i in enumerate(bad):
+        if k % 10 == 9:
+            sigs[i] = bytes([10]) * 96
+        else:
+            j = (i + 300) % n
+            assert grp[j] != grp[i]
+            sigs[i] = sigs[j]
+    res = _run_staged(v, off, idx, sigs, msgs)
+    fb, seg = v.last_stats()
+    assert fb > 256 and seg >= 1
+    expected = [True] * n
+    for i in bad:
+        expected[i] = False
+    assert res == expected
+
+
 def test_same_message_spot_check_oracle(world):
     """A few GPU-signed sets re-verified by the CPU oracle (pins util_sign beyond K1)."""
     from oracle import bls_oracle as O
