@@ -39,6 +39,10 @@ N_KEYS = 1024
 #     the shared inversion is a binary GCD: no multiplications, so it counts 1)
 #   + per-group chunk scan 177 (3 levels x (43 + 16))  = 4387 per set.
 W_PREPARE_FME = 4387
+# With the G2 sum of a segment formed by the bucket MSM (k_msm.hip; segments >= 131072 sets, the
+# bench's 1M-set batch), k_sm_prepare keeps decompress 952 + subgroup 1170 + the G1 half of the
+# randomisation 593 (2 table madds x 11 + affine tables 13 + ladder 31 x 18) + G1 scan 48 (3 x 16).
+W_PREPARE_FME_MSM = 2763
 MAC_PER_FME = 300
 # Integer VALU peak: v_mad_u64_u32 measured at 37.0 T lane-ops/s on MI355X
 # (tools/ubench_int.hip, profiles/r01_ubench_int.txt); theoretical 256 CU x 4 SIMD x 16 lanes x 2.4 GHz = 39.3 T.
@@ -70,7 +74,7 @@ def pmc_evidence(units_per_launch):
 
 
 # device kernels of one same-message verify, in gbv_last_kernel_ms order
-KERNELS = ["hash", "prepare", "chunk_finish", "miller", "seg_check", "group_pairing", "fallback"]
+KERNELS = ["hash", "prepare", "chunk_finish", "miller", "seg_check", "group_pairing", "fallback", "msm"]
 
 
 def interop_sk_bytes(i):
@@ -203,6 +207,7 @@ def main():
     ap.add_argument("--no-signing-roots", action="store_true", help="skip the signing-root secondary line")
     ap.add_argument("--no-stream", dest="stream", action="store_false",
                     help="one batch at a time (no overlap of consecutive verifications)")
+    ap.add_argument("--inflight", type=int, default=3, help="staged batches queued on the device at once")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -228,12 +233,14 @@ def main():
         sigs, expect_valid = inject_invalid(sigs, call_off, args.sets, args.invalid_frac)
         log("injected %d invalid sets (C5 recipe)" % (args.sets - expect_valid))
     staged = v.stage_same_message(call_off, idx, sigs, msgs)
-    # streaming submission: two staged copies of the workload so that one batch's chunk-level tail
+    # streaming submission: staged copies of the workload so that one batch's chunk-level tail
     # overlaps the next batch's per-set kernel (each verification still runs start to finish)
-    stages = [staged, v.stage_same_message(call_off, idx, sigs, msgs)] if args.stream else [staged]
+    depth = max(1, args.inflight) if args.stream else 1
+    stages = [staged] + [v.stage_same_message(call_off, idx, sigs, msgs) for _ in range(depth - 1)]
 
     for _ in range(args.warmup):
-        res = staged.verify(True)
+        for st in stages:  # every staged copy once: first-use costs stay out of the timed region
+            res = st.verify(True)
     if args.warmup:
         ok = res.count(1)
         assert ok == expect_valid, "warmup: %d of %d sets verified" % (ok, expect_valid)
@@ -250,6 +257,7 @@ def main():
 
     def collect(b):
         r = b.wait(True)
+        log("  step done at %.1f ms" % ((time.perf_counter() - t0) * 1e3))
         fb, seg = v.last_stats()
         slow_path[0] += fb
         slow_path[1] += seg
@@ -261,18 +269,15 @@ def main():
     n_valid = []
     barrier()
     t0 = time.perf_counter()
-    pending = None
+    # batch k is submitted once batch k - depth (the same staged copy) has been collected, so up to
+    # `depth` verifications are queued on the device at any time
     for k in range(args.steps):
-        b = stages[k % len(stages)]
-        if pending is b:  # one stage only: finish it before resubmitting
+        b = stages[k % depth]
+        if k >= depth:
             n_valid.append(collect(b))
-            pending = None
         b.submit()
-        if pending is not None:
-            n_valid.append(collect(pending))
-        pending = b
-    if pending is not None:
-        n_valid.append(collect(pending))
+    for k in range(max(0, args.steps - depth), args.steps):
+        n_valid.append(collect(stages[k % depth]))
     barrier()
     elapsed = time.perf_counter() - t0
     if dist is not None:
@@ -296,13 +301,14 @@ def main():
     # per launch: algorithmic MACs of the sets one k_sm_prepare launch processes / its average duration
     units_per_launch = args.sets / max(prep_launches_per_step, 1)
     t_launch = avg_launch_ms[1] * 1e-3
-    achieved = units_per_launch * W_PREPARE_FME * MAC_PER_FME / t_launch / 1e12 if t_launch > 0 else 0.0
+    w_fme = W_PREPARE_FME_MSM if kcnt[7] > 0 else W_PREPARE_FME
+    achieved = units_per_launch * w_fme * MAC_PER_FME / t_launch / 1e12 if t_launch > 0 else 0.0
     peak = PEAK_MAC_PER_S / 1e12
     traffic, pmc = pmc_evidence(units_per_launch)
     roofline = {"bound": "valu-int", "kernel": "k_sm_prepare", "achieved": round(achieved, 4), "peak": peak,
                 "unit": "T u32-MAC/s", "frac": round(achieved / peak, 5),
                 "traffic": round(traffic) if traffic is not None else None, "pmc": pmc,
-                "work_per_unit_fme": W_PREPARE_FME, "units_per_launch": round(units_per_launch, 1),
+                "work_per_unit_fme": w_fme, "units_per_launch": round(units_per_launch, 1),
                 "avg_launch_ms": round(float(avg_launch_ms[1]), 3),
                 "kernel_ms_per_step": {k: round(float(x), 3) for k, x in zip(KERNELS, kms)},
                 "slow_path_chunks_segments": slow_path}
@@ -336,7 +342,7 @@ def main():
         "config": {"workload": "C2 gossip attestation stream: 1M single-pubkey sets, same-message calls of 32-128",
                    "sets_per_gpu": args.sets, "calls_per_gpu": n_chunks, "table": N_VALIDATORS,
                    "parallelism": "replicas/dp%d" % world,
-                   "submission": "streamed: 2 batches in flight" if args.stream else "one batch at a time",
+                   "submission": "streamed: %d batches in flight" % depth if depth > 1 else "one batch at a time",
                    "invalid_frac": args.invalid_frac},
         "roofline": roofline,
         "cpu_baseline": cpu,

@@ -428,5 +428,31 @@ GBV_NI bool randomize_pair(G1A P, G2A Q, uint64_t r64, G1J* rP, G2J* rQ) {
   return randomize_pair_tab(P, Q, r64, rP, rQ, t1, t2);
 }
 
+// [r] P in one group only (same r = a - b x^2 as randomize_pair): the same-message path's G1 term
+// when the G2 sum of a large segment comes from the bucket MSM (k_msm.hip), and the G2 term when
+// a failing segment needs its per-set r_i sig_i after all.  E(P) = phi(P) or -psi^2(P).
+template <class F> GBV_HD bool randomize_one(const Aff<F>& P, const Aff<F>& E, uint64_t r64, Jac<F>* rP) {
+  Jac<F> a1 = jac_add_aff(jac_from_aff(P), E);
+  Jac<F> a2 = jac_add_aff(jac_from_aff(P), Aff<F>{E.x, f_neg(E.y)});
+  F z = f_mul(a1.z, a2.z);
+  if (f_is_zero(z)) return false;
+  F inv = f_inv(z);
+  RegTab2<Aff<F>> t;
+  t.store(0, aff_from_jac_inv(a1, f_mul(a2.z, inv)));
+  t.store(1, aff_from_jac_inv(a2, f_mul(a1.z, inv)));
+  *rP = jac_mul_2d_signed_tab<F>(t, (uint32_t)r64, (uint32_t)(r64 >> 32));
+  return true;
+}
+GBV_NI bool randomize_g1(G1A P, uint64_t r64, G1J* rP) { return randomize_one<Fp>(P, g1_phi(P), r64, rP); }
+GBV_NI bool randomize_g2(G2A Q, uint64_t r64, G2J* rQ) { return randomize_one<Fp2>(Q, g2_neg_psi2(Q), r64, rQ); }
+
+// Batch-scalar halves for the bucket MSM: r P = a P + b E(P) with a = 2 sa - (2^32 - 1),
+// b = 2 sb - (2^32 - 1) (odd, |a|, |b| < 2^32).  Returns |a| or |b| and the sign.
+GBV_HD uint32_t scalar_half_mag(uint32_t s, bool* neg) {
+  // 2s - (2^32-1) >= 0  <=>  s >= 2^31
+  *neg = s < 0x80000000u;
+  return *neg ? (0xffffffffu - 2u * s) : (2u * s - 0xffffffffu);
+}
+
 }  // namespace gbv
 

@@ -25,6 +25,9 @@ constexpr unsigned FB_GRID = 2048;  // persistent failure-path grids: 2 waves pe
 constexpr uint32_t GROUP_CHECK_THREAD_MIN = 512;
 // segments of at most this many chunks skip the combined segment check (latency of small calls)
 constexpr uint32_t DIRECT_CHUNK_MAX = 32;
+// segments of at least this many sets form their G2 sum sum r_i sig_i with the bucket MSM
+// (k_msm.hip) instead of per-set ladders; GBV_MSM_MIN overrides (0 = never)
+constexpr uint32_t MSM_MIN_SETS = 131072;
 
 // chunkifyMaximizeChunkSize (multithread/utils.ts:4-18): returns chunk start offsets + end.
 std::vector<uint32_t> chunk_offsets(uint32_t len, uint32_t min_per_chunk) {
@@ -55,8 +58,9 @@ struct gbv_ctx {
   std::string err;
   uint32_t nonce = 0;
   hipStream_t stream2 = nullptr, stream3 = nullptr, stream4 = nullptr;
+  uint32_t sm_submits = 0;  // parity picks which of stream2/stream3 carries a batch's chunk tail
   std::vector<hipEvent_t> events;
-  static constexpr int NK = 7;  // hash, prepare, chunk_reduce, miller, seg_check, group_pairing, fallback
+  static constexpr int NK = 8;  // hash, prepare, chunk_reduce, miller, seg_check, group_pairing, fallback, msm
   float last_ms[NK] = {};
   int last_launches[NK] = {};
   uint32_t last_fallback_chunks = 0, last_failed_segments = 0;
@@ -81,8 +85,11 @@ struct gbv_sm_batch {
   // in-flight state of the last gbv_sm_batch_submit
   bool in_flight = false;
   size_t n_seg = 0;
-  std::vector<hipEvent_t> ev;
-  hipEvent_t done = nullptr;
+  // two event sets, one per tail stream (gbv_ctx::sm_submits parity): an event is only ever
+  // recorded on one stream
+  std::vector<hipEvent_t> evs[2];
+  hipEvent_t dones[2] = {};
+  int cur = 0;  // event set of the last submit
   G2A *H = nullptr, *S = nullptr;
   G2J *rS = nullptr, *SgJ = nullptr;
   Fp12* F = nullptr;
@@ -96,7 +103,28 @@ struct gbv_sm_batch {
   uint32_t* fb_list = nullptr;
   uint32_t* fb_cnt = nullptr;  // [runs, listed sets]
   size_t fb_cap = 0;
+  // bucket MSM scratch (allocated on the first submit that uses it): two sets, by segment parity
+  uint32_t *msm_cnt[2] = {}, *msm_off[2] = {}, *msm_cur[2] = {};
+  G2J *msm_buckets[2] = {}, *msm_part[2] = {};
+  uint32_t* msm_ent = nullptr;  // 4 per set, segment s at 4 * s0
+  G2J* msm_total = nullptr;     // one per segment
+  std::vector<uint8_t> seg_msm = std::vector<uint8_t>(64);
 };
+
+static size_t msm_min_sets() { return getenv("GBV_MSM_MIN") ? (size_t)atol(getenv("GBV_MSM_MIN")) : MSM_MIN_SETS; }
+
+template <class T> static hipError_t dalloc(T** p, size_t count);
+
+static hipError_t msm_alloc(gbv_sm_batch* b) {
+  hipError_t e = hipSuccess;
+  auto chk = [&](hipError_t x) { if (x != hipSuccess && e == hipSuccess) e = x; };
+  for (int k = 0; k < 2; ++k) {
+    chk(dalloc(&b->msm_cnt[k], MSM_KEYS)); chk(dalloc(&b->msm_off[k], MSM_KEYS)); chk(dalloc(&b->msm_cur[k], MSM_KEYS));
+    chk(dalloc(&b->msm_buckets[k], MSM_KEYS)); chk(dalloc(&b->msm_part[k], MSM_PARTS + 130));
+  }
+  chk(dalloc(&b->msm_ent, 4 * b->n)); chk(dalloc(&b->msm_total, b->seg_cap));
+  return e;
+}
 
 static int fail(gbv_ctx* c, int code, const std::string& msg) {
   if (c) c->err = msg;
@@ -165,13 +193,17 @@ int gbv_init(int device, gbv_ctx** out) {
   if (device < 0 || device >= ndev) return GBV_E_ARG;
   gbv_ctx* c = new gbv_ctx();
   c->device = device;
-  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+  // stream A (k_sm_prepare, throughput) at the lowest priority, the latency-bound chunk tails, hash
+  // and MSM streams at the highest: their few waves then dispatch ahead of k_sm_prepare's
+  int prio_lo = 0, prio_hi = 0;
+  if (hipSetDevice(device) != hipSuccess || hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess ||
+      hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, prio_lo) != hipSuccess) {
     delete c;
     return GBV_E_DEVICE;
   }
-  if (hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&c->stream3, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&c->stream4, hipStreamNonBlocking) != hipSuccess) {
+  if (hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, prio_hi) != hipSuccess ||
+      hipStreamCreateWithPriority(&c->stream3, hipStreamNonBlocking, prio_hi) != hipSuccess ||
+      hipStreamCreateWithPriority(&c->stream4, hipStreamNonBlocking, prio_hi) != hipSuccess) {
     hipStreamDestroy(c->stream);
     if (c->stream2) hipStreamDestroy(c->stream2);
   if (c->stream3) hipStreamDestroy(c->stream3);
@@ -299,14 +331,20 @@ void gbv_sm_batch_destroy(gbv_ctx* c, gbv_sm_batch* b) {
   hipFree(b->idx); hipFree(b->grp_off); hipFree(b->grp_msg); hipFree(b->set_grp); hipFree(b->n_fallback);
   hipFree(b->sig); hipFree(b->msgs); hipFree(b->status); hipFree(b->grp_state); hipFree(b->valid);
   hipFree(b->H); hipFree(b->S); hipFree(b->SgJ); hipFree(b->rS); hipFree(b->rP); hipFree(b->PgJ);
-  if (b->in_flight && b->done) hipEventSynchronize(b->done);
-  for (auto& e : b->ev) hipEventDestroy(e);
-  if (b->done) hipEventDestroy(b->done);
+  if (b->in_flight && b->dones[b->cur]) hipEventSynchronize(b->dones[b->cur]);
+  for (int k = 0; k < 2; ++k) {
+    for (auto& e : b->evs[k]) hipEventDestroy(e);
+    if (b->dones[k]) hipEventDestroy(b->dones[k]);
+  }
   hipHostFree(b->valid_host);
   hipHostFree(b->nfb_host);
   hipFree(b->F); hipFree(b->seg_ok); hipHostFree(b->seg_ok_host);
   hipFree(b->Fpart); hipFree(b->Spart); hipFree(b->has);
   hipFree(b->fb_runs); hipFree(b->fb_list); hipFree(b->fb_cnt);
+  for (int k = 0; k < 2; ++k) {
+    hipFree(b->msm_cnt[k]); hipFree(b->msm_off[k]); hipFree(b->msm_cur[k]); hipFree(b->msm_buckets[k]); hipFree(b->msm_part[k]);
+  }
+  hipFree(b->msm_ent); hipFree(b->msm_total);
   delete b;
 }
 
@@ -360,7 +398,9 @@ int gbv_sm_batch_create(gbv_ctx* c, size_t n_calls, const uint32_t* call_off, co
   chk(hipHostMalloc((void**)&b->seg_ok_host, b->seg_cap, hipHostMallocDefault));
   chk(hipHostMalloc((void**)&b->valid_host, std::max<size_t>(n, 1), hipHostMallocDefault));
   chk(hipHostMalloc((void**)&b->nfb_host, sizeof(uint32_t), hipHostMallocDefault));
-  chk(hipEventCreateWithFlags(&b->done, hipEventDisableTiming));
+  chk(hipEventCreateWithFlags(&b->dones[0], hipEventDisableTiming));
+  chk(hipEventCreateWithFlags(&b->dones[1], hipEventDisableTiming));
+  if (msm_min_sets() && n >= msm_min_sets()) chk(msm_alloc(b));
   if (e != hipSuccess) {
     gbv_sm_batch_destroy(c, b);
     return fail(c, GBV_E_OOM, std::string("hipMalloc: ") + hipGetErrorString(e));
@@ -401,7 +441,14 @@ int gbv_sm_batch_submit(gbv_ctx* c, gbv_sm_batch* b) {
   if (b->n == 0) return GBV_OK;
   Seed seed = fresh_seed();
   uint32_t nonce = c->nonce++;
-  hipStream_t sa = c->stream, sh = c->stream4, sbs[2] = {c->stream2, c->stream3};
+  // consecutive batches put their chunk-level tails on different streams, so that the tail of
+  // batch k and of batch k+1 overlap (each beside the next batch's k_sm_prepare on stream A)
+  // GBV_FLIP=1: alternate the tail stream per batch (lets consecutive tails overlap, but together
+  // with the MSM launches it stalled the device for seconds at a time on ROCm 7.2 -- off by default)
+  static const bool use_flip = getenv("GBV_FLIP") != nullptr;
+  const bool flip = use_flip && (c->sm_submits++ & 1) != 0;
+  hipStream_t sa = c->stream, sh = c->stream4;
+  hipStream_t sbs[2] = {flip ? c->stream3 : c->stream2, flip ? c->stream2 : c->stream3};
   const size_t max_seg = b->seg_cap;
   const size_t n_seg = getenv("GBV_SEGMENTS") ? (size_t)std::max(1, atoi(getenv("GBV_SEGMENTS"))) : 1;
   size_t sub_sets = std::max<size_t>((b->n + n_seg - 1) / n_seg, 16384);
@@ -417,14 +464,29 @@ int gbv_sm_batch_submit(gbv_ctx* c, gbv_sm_batch* b) {
   gcut.push_back((uint32_t)b->G);
   size_t S = gcut.size() - 1;
   b->n_seg = S;
-  // events: [0,1] hash; per segment 10 (prep, finish, miller, check, group); then [tail] 2 fallback
-  size_t need = 2 + 10 * S + 2;
-  if (b->ev.size() < need) {
-    size_t old = b->ev.size();
-    b->ev.resize(need);
-    for (size_t k = old; k < need; ++k) HIP_CHECK(c, hipEventCreateWithFlags(&b->ev[k], hipEventDefault));
+  const size_t msm_min = msm_min_sets();
+  bool any_msm = false;
+  for (size_t s = 0; s < S; ++s) {
+    uint32_t G = gcut[s + 1] - gcut[s];
+    size_t ns = b->grp_off_host[gcut[s + 1]] - b->grp_off_host[gcut[s]];
+    b->seg_direct[s] = G <= DIRECT_CHUNK_MAX;
+    b->seg_msm[s] = msm_min && ns >= msm_min && !b->seg_direct[s];
+    any_msm |= b->seg_msm[s] != 0;
   }
-  hipEvent_t* ev = b->ev.data();
+  if (any_msm && !b->msm_ent) {  // normally allocated by gbv_sm_batch_create (no hipMalloc while work is queued)
+    hipError_t e = msm_alloc(b);
+    if (e != hipSuccess) return fail(c, GBV_E_OOM, std::string("hipMalloc (msm): ") + hipGetErrorString(e));
+  }
+  // events: [0,1] hash; per segment 12 (prep, finish, miller, check, group, msm); then [tail] 2 fallback
+  size_t need = 2 + 12 * S + 2;
+  b->cur = flip ? 1 : 0;
+  std::vector<hipEvent_t>& evv = b->evs[b->cur];
+  if (evv.size() < need) {
+    size_t old = evv.size();
+    evv.resize(need);
+    for (size_t k = old; k < need; ++k) HIP_CHECK(c, hipEventCreateWithFlags(&evv[k], hipEventDefault));
+  }
+  hipEvent_t* ev = evv.data();
   const size_t part_stride = b->G / 64 + b->G / 4096 + 4;
   HIP_CHECK(c, hipMemsetAsync(b->n_fallback, 0, 4, sh));
   HIP_CHECK(c, hipMemsetAsync(b->fb_cnt, 0, 8, sh));
@@ -432,46 +494,63 @@ int gbv_sm_batch_submit(gbv_ctx* c, gbv_sm_batch* b) {
   launch_hash_msgs(LaunchCfg{blocks_for(b->n_calls), TPB, sh}, b->msgs, (uint32_t)b->n_calls, b->H);
   hipEventRecord(ev[1], sh);
   for (size_t s = 0; s < S; ++s) {
-    hipEvent_t* e = ev + 2 + 10 * s;
+    hipEvent_t* e = ev + 2 + 12 * s;
     hipStream_t sb = sbs[s & 1];
     uint32_t g0 = gcut[s], G = gcut[s + 1] - gcut[s];
     uint32_t s0 = b->grp_off_host[g0], s1 = b->grp_off_host[gcut[s + 1]];
+    const bool msm = b->seg_msm[s];
+    G2J* Sh = msm ? nullptr : b->rS;  // MSM segment: k_sm_prepare forms the G1 terms only
     hipEventRecord(e[0], sa);
     launch_sm_prepare(LaunchCfg{0, 64, sa}, s0, s1 - s0, b->idx, b->sig, b->set_grp, c->table, c->table_ok, (uint32_t)c->table_n, seed,
-                      nonce, b->S, b->rS, b->rP, b->status);
+                      nonce, b->S, Sh, b->rP, b->status);
     hipEventRecord(e[1], sa);
-    HIP_CHECK(c, hipStreamWaitEvent(sb, e[1], 0));
-    HIP_CHECK(c, hipStreamWaitEvent(sb, ev[1], 0));
-    hipEventRecord(e[2], sb);
-    launch_sm_chunk_finish(LaunchCfg{0, 64, sb}, g0, G, s0, b->grp_off, b->status, b->rS, b->rP, b->PgJ, b->SgJ, b->grp_state,
+    // A segment of a few chunks (a lone gossip call) skips the combined check (seg_direct): each
+    // chunk goes straight to its own one-wave check, which is the shorter dependency chain.
+    // An MSM segment runs its chunk sums and the bucket MSM on stream A right after its
+    // k_sm_prepare (the MSM's bucket pass then has the whole device instead of fighting the next
+    // k_sm_prepare for CUs); the tail stream waits for them.  Other segments sum their chunks on
+    // the tail stream.
+    hipStream_t scf = msm ? sa : sb;
+    if (!msm) HIP_CHECK(c, hipStreamWaitEvent(sb, e[1], 0));
+    HIP_CHECK(c, hipStreamWaitEvent(scf, ev[1], 0));
+    hipEventRecord(e[2], scf);
+    launch_sm_chunk_finish(LaunchCfg{0, 64, scf}, g0, G, s0, b->grp_off, b->status, Sh, b->rP, b->PgJ, b->SgJ, b->grp_state,
                            b->n_fallback);
-    hipEventRecord(e[3], sb);
-    // a segment of a few chunks (a lone gossip call) skips the combined check: each chunk goes
-    // straight to its own one-wave check, which is the shorter dependency chain
-    b->seg_direct[s] = G <= DIRECT_CHUNK_MAX;
+    hipEventRecord(e[3], scf);
+    hipEventRecord(e[10], scf);
+    if (msm)
+      launch_msm_g2_segment(sa, s0, s1 - s0, b->set_grp, b->status, b->grp_state, b->S, seed, nonce, b->msm_cnt[s & 1], b->msm_off[s & 1],
+                            b->msm_cur[s & 1], b->msm_ent + 4ull * s0, b->msm_buckets[s & 1], b->msm_part[s & 1], b->msm_total + s);
+    hipEventRecord(e[11], scf);
+    if (msm) HIP_CHECK(c, hipStreamWaitEvent(sb, e[3], 0));
     hipEventRecord(e[4], sb);
     if (!b->seg_direct[s]) launch_sm_miller(LaunchCfg{0, 64, sb}, g0, G, b->grp_msg, b->grp_state, b->PgJ, b->H, b->F);
     hipEventRecord(e[5], sb);
+    if (msm) HIP_CHECK(c, hipStreamWaitEvent(sb, e[11], 0));
     hipEventRecord(e[6], sb);
     size_t po = (s & 1) * part_stride;
     if (b->seg_direct[s])
       HIP_CHECK(c, hipMemsetAsync(b->seg_ok + s, 0, 1, sb));
     else
       launch_sm_seg_check(LaunchCfg{1, 64, sb}, g0, G, b->grp_state, b->F, b->SgJ, b->Fpart + po, b->Spart + po, b->has + po,
-                          b->seg_ok + s);
+                          b->seg_ok + s, nullptr, msm ? b->msm_total + s : nullptr);
     hipEventRecord(e[7], sb);
     hipEventRecord(e[8], sb);
+    if (msm) {  // failure path of an MSM segment needs the per-set / per-chunk G2 sums (exit at once on pass)
+      launch_sm_redo_g2(LaunchCfg{0, 64, sb}, s0, s1 - s0, b->set_grp, b->status, b->S, seed, nonce, b->seg_ok + s, b->rS);
+      launch_sm_chunk_finish_s(LaunchCfg{0, 64, sb}, g0, G, s0, b->grp_off, b->grp_state, b->rS, b->seg_ok + s, b->SgJ);
+    }
     if (G >= GROUP_CHECK_THREAD_MIN)
       launch_sm_group_check(LaunchCfg{0, 64, sb}, g0, G, b->F, b->SgJ, b->seg_ok + s, b->grp_state, b->n_fallback);
     else
       launch_sm_group_pairing(LaunchCfg{G, 64, sb}, g0, G, b->grp_msg, b->PgJ, b->SgJ, b->H, b->seg_ok + s, b->grp_state, b->n_fallback);
     hipEventRecord(e[9], sb);
   }
-  hipEvent_t* ep = ev + 2 + 10 * S;
+  hipEvent_t* ep = ev + 2 + 12 * S;
   // the tail runs on B0 after everything of this batch (B1's last segment included)
   if (S > 1) {
     size_t last_b1 = (S - 1) & 1 ? S - 1 : S - 2;  // last segment that ran on B1
-    HIP_CHECK(c, hipStreamWaitEvent(sbs[0], ev[2 + 10 * last_b1 + 9], 0));
+    HIP_CHECK(c, hipStreamWaitEvent(sbs[0], ev[2 + 12 * last_b1 + 9], 0));
   }
   hipEventRecord(ep[0], sbs[0]);
   // valid = 1 for the sets of passing chunks; the sets of failed chunks go through 8-set run
@@ -495,7 +574,7 @@ int gbv_sm_batch_submit(gbv_ctx* c, gbv_sm_batch* b) {
   HIP_CHECK(c, hipMemcpyAsync(b->valid_host, b->valid, b->n, hipMemcpyDeviceToHost, sbs[0]));
   HIP_CHECK(c, hipMemcpyAsync(b->nfb_host, b->n_fallback, sizeof(uint32_t), hipMemcpyDeviceToHost, sbs[0]));
   HIP_CHECK(c, hipMemcpyAsync(b->seg_ok_host, b->seg_ok, S, hipMemcpyDeviceToHost, sbs[0]));
-  HIP_CHECK(c, hipEventRecord(b->done, sbs[0]));
+  HIP_CHECK(c, hipEventRecord(b->dones[b->cur], sbs[0]));
   HIP_CHECK(c, hipGetLastError());
   b->in_flight = true;
   return GBV_OK;
@@ -507,14 +586,14 @@ int gbv_sm_batch_wait(gbv_ctx* c, gbv_sm_batch* b, uint8_t* valid) {
   if (!b->in_flight) return fail(c, GBV_E_ARG, "batch not submitted");
   HIP_CHECK(c, hipSetDevice(c->device));
   b->in_flight = false;
-  HIP_CHECK(c, hipEventSynchronize(b->done));
+  HIP_CHECK(c, hipEventSynchronize(b->dones[b->cur]));
   if (valid) memcpy(valid, b->valid_host, b->n);
   c->last_fallback_chunks = *b->nfb_host;
   c->last_failed_segments = 0;
   for (size_t s = 0; s < b->n_seg; ++s) c->last_failed_segments += (b->seg_ok_host[s] || b->seg_direct[s]) ? 0 : 1;
   for (auto& x : c->last_ms) x = 0.f;
   for (auto& x : c->last_launches) x = 0;
-  hipEvent_t* ev = b->ev.data();
+  hipEvent_t* ev = b->evs[b->cur].data();
   auto acc = [&](int k, hipEvent_t a0, hipEvent_t a1, bool count = true) {
     float ms = 0.f;
     if (hipEventElapsedTime(&ms, a0, a1) == hipSuccess) {
@@ -524,10 +603,11 @@ int gbv_sm_batch_wait(gbv_ctx* c, gbv_sm_batch* b, uint8_t* valid) {
   };
   acc(0, ev[0], ev[1]);
   for (size_t s = 0; s < b->n_seg; ++s) {
-    hipEvent_t* e = ev + 2 + 10 * s;
+    hipEvent_t* e = ev + 2 + 12 * s;
     for (int k = 0; k < 5; ++k) acc(1 + k, e[2 * k], e[2 * k + 1]);
+    if (b->seg_msm[s]) acc(7, e[10], e[11]);
   }
-  hipEvent_t* ep = ev + 2 + 10 * b->n_seg;
+  hipEvent_t* ep = ev + 2 + 12 * b->n_seg;
   acc(6, ep[0], ep[1]);
   return GBV_OK;
 }

@@ -30,6 +30,7 @@ constexpr unsigned SCAN_W = 8;  // lanes per scan group (power of two, <= 64)
 // then sums its terms per chunk with a segmented suffix scan (log2(SCAN_W) levels of point
 // additions) and the first lane of every chunk segment in the group writes the segment's sum at
 // its own set index; k_sm_chunk_finish adds the <= ceil(len/SCAN_W)+1 segment sums of a chunk.
+template <bool WITH_G2>
 __global__ void GBV_KERNEL_ATTR k_sm_prepare(uint32_t base, uint32_t n, const uint32_t* __restrict__ idx, const uint8_t* __restrict__ sig96,
                                              const uint32_t* __restrict__ set_grp, const G1A* __restrict__ table,
                                              const uint8_t* __restrict__ table_ok, uint32_t table_n, Seed seed, uint32_t nonce,
@@ -54,8 +55,12 @@ __global__ void GBV_KERNEL_ATTR k_sm_prepare(uint32_t base, uint32_t n, const ui
       S_out[i] = s;
       uint64_t r = prf_scalar(seed, i, nonce);
       G1A pk = table[k];
-      if (!randomize_pair(pk, s, r, &rp, &rs)) {  // unreachable for subgroup points; plain 64-bit r then
-        rs = g2_mul_u64(s, r);
+      if (WITH_G2) {
+        if (!randomize_pair(pk, s, r, &rp, &rs)) {  // unreachable for subgroup points; plain 64-bit r then
+          rs = g2_mul_u64(s, r);
+          rp = g1_mul_u64(pk, r);
+        }
+      } else if (!randomize_g1(pk, r, &rp)) {
         rp = g1_mul_u64(pk, r);
       }
     }
@@ -63,19 +68,62 @@ __global__ void GBV_KERNEL_ATTR k_sm_prepare(uint32_t base, uint32_t n, const ui
   // segmented suffix scan inside each group of SCAN_W lanes (3 levels: the whole wave pays every
   // level, so fewer levels = less work here; k_sm_chunk_finish adds the group sums of a chunk)
   for (unsigned d = 1; d < SCAN_W; d <<= 1) {
-    G2J so = shfl_down_jac(rs, d);
     G1J po = shfl_down_jac(rp, d);
     uint32_t ko = __shfl_down(key, d, 64);
-    if ((lane & (SCAN_W - 1)) + d < SCAN_W && ko == key) {
-      rs = g2_add(rs, so);
-      rp = g1_add(rp, po);
+    bool take = (lane & (SCAN_W - 1)) + d < SCAN_W && ko == key;
+    if (WITH_G2) {
+      G2J so = shfl_down_jac(rs, d);
+      if (take) rs = g2_add(rs, so);
     }
+    if (take) rp = g1_add(rp, po);
   }
   uint32_t kprev = __shfl_up(key, 1, 64);
   if (act && ((lane & (SCAN_W - 1)) == 0 || kprev != key)) {
-    Sh_out[i] = rs;
+    if (WITH_G2) Sh_out[i] = rs;
     Ph_out[i] = rp;
   }
+}
+
+// The G2 half of k_sm_prepare for a segment whose fast check used the bucket MSM (k_msm.hip) and
+// FAILED: the failure path needs the per-set r_i sig_i group sums (Sh) and the chunk sums S_g
+// after all.  Same r_i (prf_scalar of the same seed/nonce/index), same 8-lane scan, so Sh/S_g are
+// exactly what k_sm_prepare<true> would have written.  Exits at once when the segment passed.
+__global__ void GBV_KERNEL_ATTR k_sm_redo_g2(uint32_t base, uint32_t n, const uint32_t* __restrict__ set_grp,
+                                             const uint8_t* __restrict__ status, const G2A* __restrict__ S, Seed seed, uint32_t nonce,
+                                             const uint8_t* __restrict__ seg_ok, G2J* __restrict__ Sh_out) {
+  if (*seg_ok) return;
+  unsigned lane = threadIdx.x;
+  uint32_t t = blockIdx.x * 64 + lane;
+  bool act = t < n;
+  uint32_t i = base + t;
+  uint32_t key = act ? set_grp[i] : 0xffffffffu;
+  G2J rs = jac_infinity<Fp2>();
+  if (act && status[i] == SET_OK) {
+    G2A s = S[i];
+    uint64_t r = prf_scalar(seed, i, nonce);
+    if (!randomize_g2(s, r, &rs)) rs = g2_mul_u64(s, r);
+  }
+  for (unsigned d = 1; d < SCAN_W; d <<= 1) {
+    G2J so = shfl_down_jac(rs, d);
+    uint32_t ko = __shfl_down(key, d, 64);
+    if ((lane & (SCAN_W - 1)) + d < SCAN_W && ko == key) rs = g2_add(rs, so);
+  }
+  uint32_t kprev = __shfl_up(key, 1, 64);
+  if (act && ((lane & (SCAN_W - 1)) == 0 || kprev != key)) Sh_out[i] = rs;
+}
+
+// S_g of every pending chunk of a failed MSM segment from the Sh written by k_sm_redo_g2.
+__global__ void GBV_KERNEL_ATTR k_sm_chunk_finish_s(uint32_t g0, uint32_t G, uint32_t s0, const uint32_t* __restrict__ grp_off,
+                                                    const uint8_t* __restrict__ grp_state, const G2J* __restrict__ Sh,
+                                                    const uint8_t* __restrict__ seg_ok, G2J* __restrict__ SgJ) {
+  uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (*seg_ok || g >= G) return;
+  g += g0;
+  if (grp_state[g] != GRP_PENDING) return;
+  uint32_t b = grp_off[g], e = grp_off[g + 1];
+  G2J s = Sh[b];
+  for (uint32_t q = s0 + ((b - s0) / SCAN_W + 1) * SCAN_W; q < e; q += SCAN_W) s = g2_add(s, Sh[q]);
+  SgJ[g] = s;
 }
 
 // Per chunk (one thread): P_g = sum r_i pk_i, S_g = sum r_i sig_i from the segment sums at the
@@ -95,10 +143,10 @@ __global__ void GBV_KERNEL_ATTR k_sm_chunk_finish(uint32_t g0, uint32_t G, uint3
   for (uint32_t i = b; i < e; ++i) bad |= status[i] != SET_OK;
   if (!bad) {
     G1J p = Ph[b];
-    G2J s = Sh[b];
+    G2J s = Sh ? Sh[b] : jac_infinity<Fp2>();  // Sh == nullptr: the segment's G2 sum is the MSM's
     for (uint32_t q = s0 + ((b - s0) / SCAN_W + 1) * SCAN_W; q < e; q += SCAN_W) {
       p = g1_add(p, Ph[q]);
-      s = g2_add(s, Sh[q]);
+      if (Sh) s = g2_add(s, Sh[q]);
     }
     bad = jac_is_inf(p);
     PgJ[g] = p;
@@ -314,9 +362,24 @@ void launch_sm_fb_sets(LaunchCfg c, const uint32_t* set_list, const uint32_t* n_
 void launch_sm_prepare(LaunchCfg c, uint32_t base, uint32_t n, const uint32_t* idx, const uint8_t* sig96, const uint32_t* set_grp,
                        const G1A* table, const uint8_t* table_ok, uint32_t table_n, const Seed& seed, uint32_t nonce, G2A* S_out, G2J* Sh,
                        G1J* Ph, uint8_t* status) {
-  hipLaunchKernelGGL(k_sm_prepare, dim3((n + 63) / 64), dim3(64), 0, c.stream, base, n, idx, sig96, set_grp, table, table_ok, table_n, seed,
-                     nonce, S_out, Sh, Ph, status);
+  // Sh == nullptr: G1 terms only (the segment's G2 sum comes from the bucket MSM)
+  if (Sh)
+    hipLaunchKernelGGL(k_sm_prepare<true>, dim3((n + 63) / 64), dim3(64), 0, c.stream, base, n, idx, sig96, set_grp, table, table_ok, table_n,
+                       seed, nonce, S_out, Sh, Ph, status);
+  else
+    hipLaunchKernelGGL(k_sm_prepare<false>, dim3((n + 63) / 64), dim3(64), 0, c.stream, base, n, idx, sig96, set_grp, table, table_ok,
+                       table_n, seed, nonce, S_out, Sh, Ph, status);
   debug_sync(c.stream, "k_sm_prepare");
+}
+void launch_sm_redo_g2(LaunchCfg c, uint32_t base, uint32_t n, const uint32_t* set_grp, const uint8_t* status, const G2A* S, const Seed& seed,
+                       uint32_t nonce, const uint8_t* seg_ok, G2J* Sh) {
+  hipLaunchKernelGGL(k_sm_redo_g2, dim3((n + 63) / 64), dim3(64), 0, c.stream, base, n, set_grp, status, S, seed, nonce, seg_ok, Sh);
+  debug_sync(c.stream, "k_sm_redo_g2");
+}
+void launch_sm_chunk_finish_s(LaunchCfg c, uint32_t g0, uint32_t G, uint32_t s0, const uint32_t* grp_off, const uint8_t* grp_state,
+                              const G2J* Sh, const uint8_t* seg_ok, G2J* SgJ) {
+  hipLaunchKernelGGL(k_sm_chunk_finish_s, dim3((G + 63) / 64), dim3(64), 0, c.stream, g0, G, s0, grp_off, grp_state, Sh, seg_ok, SgJ);
+  debug_sync(c.stream, "k_sm_chunk_finish_s");
 }
 void launch_sm_chunk_finish(LaunchCfg c, uint32_t g0, uint32_t G, uint32_t s0, const uint32_t* grp_off, const uint8_t* status, const G2J* Sh,
                             const G1J* Ph, G1J* PgJ, G2J* SgJ, uint8_t* grp_state, uint32_t* n_fallback) {

@@ -53,7 +53,7 @@ constexpr int SEG_WS = coop::MILLER_WS + coop::FINAL_EXP_WS;
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_sm_seg_check(uint32_t g0, uint32_t G, uint32_t nb, const Fp12* __restrict__ Fpart,
                                                      const G2J* __restrict__ Spart, const uint8_t* __restrict__ has,
                                                      uint8_t* __restrict__ grp_state, uint8_t* __restrict__ seg_ok,
-                                                     Fp12* __restrict__ miller_out) {
+                                                     Fp12* __restrict__ miller_out, const G2J* __restrict__ S_extra) {
   __shared__ Fp ws[SEG_WS];
   __shared__ int flags[2];
   Fp* ml = ws;
@@ -62,7 +62,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
   // fe[E_F] = product of the (<= 4) final partials (cooperative, one after another), S = their sum
   if (lane == 0) flags[0] = 0;
   coop::set_one12(fe + coop::E_F);
-  G2J s = jac_infinity<Fp2>();
+  // S_extra: the segment's sum r_i sig_i from the bucket MSM (k_msm.hip) when the chunks carry none
+  G2J s = S_extra ? S_extra[0] : jac_infinity<Fp2>();
   for (uint32_t k = 0; k < nb; ++k) {
     if (!has[k]) continue;
     if (lane < 12) fe[coop::E_TMP + lane] = ((const Fp*)&Fpart[k])[lane];
@@ -244,11 +245,11 @@ void launch_sm_fb_sets_coop(LaunchCfg c, const uint32_t* set_list, const uint32_
 }
 
 void launch_sm_seg_check(LaunchCfg c, uint32_t g0, uint32_t G, uint8_t* grp_state, const Fp12* F, const G2J* SgJ, Fp12* Fpart, G2J* Spart,
-                         uint8_t* has, uint8_t* seg_ok, Fp12* miller_out) {
+                         uint8_t* has, uint8_t* seg_ok, Fp12* miller_out, const G2J* S_extra) {
   uint32_t nb = 0;
   uint32_t off = launch_sm_seg_reduce(c, g0, G, grp_state, F, SgJ, Fpart, Spart, has, &nb);
   hipLaunchKernelGGL(k_sm_seg_check, dim3(1), dim3(64), 0, c.stream, g0, G, nb, Fpart + off, Spart + off, has + off, grp_state, seg_ok,
-                     miller_out);
+                     miller_out, S_extra);
   debug_sync(c.stream, "k_sm_seg_check");
 }
 void launch_sm_group_pairing(LaunchCfg c, uint32_t g0, uint32_t G, const uint32_t* grp_msg, const G1J* PgJ, const G2J* SgJ, const G2A* H,

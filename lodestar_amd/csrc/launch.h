@@ -22,7 +22,18 @@ void launch_sm_miller(LaunchCfg c, uint32_t g0, uint32_t G, const uint32_t* grp_
 uint32_t launch_sm_seg_reduce(LaunchCfg c, uint32_t g0, uint32_t G, const uint8_t* grp_state, const Fp12* F, const G2J* SgJ, Fp12* Fpart,
                               G2J* Spart, uint8_t* has, uint32_t* n_out);
 void launch_sm_seg_check(LaunchCfg c, uint32_t g0, uint32_t G, uint8_t* grp_state, const Fp12* F, const G2J* SgJ, Fp12* Fpart, G2J* Spart,
-                         uint8_t* has, uint8_t* seg_ok, Fp12* miller_out = nullptr);
+                         uint8_t* has, uint8_t* seg_ok, Fp12* miller_out = nullptr, const G2J* S_extra = nullptr);
+void launch_sm_redo_g2(LaunchCfg c, uint32_t base, uint32_t n, const uint32_t* set_grp, const uint8_t* status, const G2A* S, const Seed& seed,
+                       uint32_t nonce, const uint8_t* seg_ok, G2J* Sh);
+void launch_sm_chunk_finish_s(LaunchCfg c, uint32_t g0, uint32_t G, uint32_t s0, const uint32_t* grp_off, const uint8_t* grp_state,
+                              const G2J* Sh, const uint8_t* seg_ok, G2J* SgJ);
+// Bucket MSM of a same-message segment: total = sum over its sets with status OK in pending chunks
+// of r_i sig_i (k_msm.hip).  Scratch: cnt/off/cur MSM_KEYS u32 each, ent 4 u32 per set, buckets
+// MSM_KEYS G2J, part MSM_PARTS + 130 G2J.
+constexpr uint32_t MSM_C = 16, MSM_WINDOWS = 2, MSM_KEYS = MSM_WINDOWS << MSM_C, MSM_SLICE = 16, MSM_PARTS = MSM_KEYS / MSM_SLICE;
+void launch_msm_g2_segment(hipStream_t s, uint32_t s0, uint32_t n, const uint32_t* set_grp, const uint8_t* status, const uint8_t* grp_state,
+                           const G2A* S, const Seed& seed, uint32_t nonce, uint32_t* cnt, uint32_t* off, uint32_t* cur, uint32_t* ent,
+                           G2J* buckets, G2J* part, G2J* total);
 void launch_fp12_check(LaunchCfg c, uint32_t k, const Fp12* parts, uint8_t* out);
 void launch_vs_chunk_coop(LaunchCfg c, uint32_t C, const uint32_t* chunk_off, const uint8_t* status, const Fp12* f, const G2J* rS,
                           uint8_t* chunk_valid);

@@ -268,10 +268,10 @@ class GpuBlsVerifier:
 
     def last_kernel_ms(self):
         """(total device ms, launches) of each kernel of the last staged verify:
-        [hash, prepare, chunk_finish, miller, seg_check, group_pairing, fallback]."""
-        buf = (ctypes.c_float * 7)()
-        cnt = (ctypes.c_int * 7)()
-        k = self._lib.gbv_last_kernel_ms(self._ctx, buf, cnt, 7)
+        [hash, prepare, chunk_finish, miller, seg_check, group_pairing, fallback, msm]."""
+        buf = (ctypes.c_float * 8)()
+        cnt = (ctypes.c_int * 8)()
+        k = self._lib.gbv_last_kernel_ms(self._ctx, buf, cnt, 8)
         return [buf[i] for i in range(k)], [cnt[i] for i in range(k)]
 
     # ---- IBlsVerifier (async) -------------------------------------------------------------------

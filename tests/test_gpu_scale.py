@@ -59,9 +59,13 @@ def _run_staged(v, off, idx, sigs, msgs):
         st.close()
 
 
-@pytest.fixture
-def segments(monkeypatch):
+@pytest.fixture(params=["ladder", "msm"])
+def segments(monkeypatch, request):
     monkeypatch.setenv("GBV_SEGMENTS", "4")  # read by gbv_sm_batch_verify on every call
+    # G2 terms per set (32-step ladders) or per segment (bucket MSM, k_msm.hip): both must give the
+    # same booleans, and an all-valid stream must pass the segment checks either way
+    monkeypatch.setenv("GBV_MSM_MIN", "0" if request.param == "ladder" else "1000")
+    return request.param
 
 
 def test_same_message_all_valid_multi_segment(world, segments):
@@ -100,10 +104,13 @@ def test_same_message_injected_invalid(world, segments):
     assert res == expected
 
 
-def test_same_message_one_percent_invalid(world):
+@pytest.mark.parametrize("mode", ["ladder", "msm"])
+def test_same_message_one_percent_invalid(world, monkeypatch, mode):
     """C5-style density: 1 % of 60 000 sets invalid, so hundreds of chunks fail.  The
     failure path then runs its thread-per-item kernels (group checks, 8-set run checks, per-set
-    checks: more than FB_COOP_MAX items each) and must still return exactly the per-set booleans."""
+    checks: more than FB_COOP_MAX items each) and must still return exactly the per-set booleans.
+    In MSM mode the failing segment first recomputes its per-set G2 terms (k_sm_redo_g2)."""
+    monkeypatch.setenv("GBV_MSM_MIN", "0" if mode == "ladder" else "1000")
     v, sks, _ = world
     off, idx, grp, sigs, msgs = _workload(v, sks, 60000, 14)
     n = len(sigs)
@@ -210,3 +217,25 @@ def test_sharded_verifier_single_rank(world):
         assert sv.verify_same_message_multi(calls) == [[True] * 5, [True, False]]
     finally:
         dist.destroy_process_group()
+
+
+def test_same_message_msm_single_segment(world, monkeypatch):
+    """One 100 000-set segment through the bucket MSM at its default size threshold (the bench's
+    shape at 1/10 scale): the segment check must pass on the MSM's sum alone, and the MSM kernels
+    must have run (their time is reported in slot 7 of last_kernel_ms)."""
+    monkeypatch.setenv("GBV_SEGMENTS", "1")
+    monkeypatch.setenv("GBV_MSM_MIN", "65536")
+    v, sks, _ = world
+    off, idx, grp, sigs, msgs = _workload(v, sks, 100000, 15)
+    res = _run_staged(v, off, idx, sigs, msgs)
+    assert all(res)
+    assert v.last_stats() == (0, 0)
+    ms, cnt = v.last_kernel_ms()
+    assert len(cnt) == 8 and cnt[7] == 1
+    # one wrong-message signature: the MSM segment fails, the redo + per-chunk path finds the set
+    sigs = list(sigs)
+    sigs[77777] = sigs[(77777 + 300) % len(sigs)]
+    res = _run_staged(v, off, idx, sigs, msgs)
+    assert res == [i != 77777 for i in range(len(sigs))]
+    fb, seg = v.last_stats()
+    assert fb == 1 and seg == 1
