@@ -477,8 +477,10 @@ int gbv_sm_batch_submit(gbv_ctx* c, gbv_sm_batch* b) {
     hipError_t e = msm_alloc(b);
     if (e != hipSuccess) return fail(c, GBV_E_OOM, std::string("hipMalloc (msm): ") + hipGetErrorString(e));
   }
-  // events: [0,1] hash; per segment 12 (prep, finish, miller, check, group, msm); then [tail] 2 fallback
-  size_t need = 2 + 12 * S + 2;
+  // events: [0,1] hash; per segment 13 (prep, finish, miller, check, group, msm, msm reduce done);
+  // then [tail] 2 fallback
+  constexpr size_t EPS = 13;
+  size_t need = 2 + EPS * S + 2;
   b->cur = flip ? 1 : 0;
   std::vector<hipEvent_t>& evv = b->evs[b->cur];
   if (evv.size() < need) {
@@ -494,7 +496,7 @@ int gbv_sm_batch_submit(gbv_ctx* c, gbv_sm_batch* b) {
   launch_hash_msgs(LaunchCfg{blocks_for(b->n_calls), TPB, sh}, b->msgs, (uint32_t)b->n_calls, b->H);
   hipEventRecord(ev[1], sh);
   for (size_t s = 0; s < S; ++s) {
-    hipEvent_t* e = ev + 2 + 12 * s;
+    hipEvent_t* e = ev + 2 + EPS * s;
     hipStream_t sb = sbs[s & 1];
     uint32_t g0 = gcut[s], G = gcut[s + 1] - gcut[s];
     uint32_t s0 = b->grp_off_host[g0], s1 = b->grp_off_host[gcut[s + 1]];
@@ -518,15 +520,21 @@ int gbv_sm_batch_submit(gbv_ctx* c, gbv_sm_batch* b) {
                            b->n_fallback);
     hipEventRecord(e[3], scf);
     hipEventRecord(e[10], scf);
+    // segment s-2 shares this segment's bucket buffers: its reduction (tail stream) must be done
+    if (msm && s >= 2 && b->seg_msm[s - 2]) HIP_CHECK(c, hipStreamWaitEvent(sa, ev[2 + EPS * (s - 2) + 12], 0));
     if (msm)
-      launch_msm_g2_segment(sa, s0, s1 - s0, b->set_grp, b->status, b->grp_state, b->S, seed, nonce, b->msm_cnt[s & 1], b->msm_off[s & 1],
-                            b->msm_cur[s & 1], b->msm_ent + 4ull * s0, b->msm_buckets[s & 1], b->msm_part[s & 1], b->msm_total + s);
+      launch_msm_g2_buckets(sa, s0, s1 - s0, b->set_grp, b->status, b->grp_state, b->S, seed, nonce, b->msm_cnt[s & 1], b->msm_off[s & 1],
+                            b->msm_cur[s & 1], b->msm_ent + 4ull * s0, b->msm_buckets[s & 1]);
     hipEventRecord(e[11], scf);
     if (msm) HIP_CHECK(c, hipStreamWaitEvent(sb, e[3], 0));
     hipEventRecord(e[4], sb);
     if (!b->seg_direct[s]) launch_sm_miller(LaunchCfg{0, 64, sb}, g0, G, b->grp_msg, b->grp_state, b->PgJ, b->H, b->F);
     hipEventRecord(e[5], sb);
-    if (msm) HIP_CHECK(c, hipStreamWaitEvent(sb, e[11], 0));
+    if (msm) {  // the latency-bound bucket reduction overlaps the next k_sm_prepare
+      HIP_CHECK(c, hipStreamWaitEvent(sb, e[11], 0));
+      launch_msm_g2_reduce(sb, b->msm_buckets[s & 1], b->msm_part[s & 1], b->msm_total + s);
+    }
+    hipEventRecord(e[12], sb);
     hipEventRecord(e[6], sb);
     size_t po = (s & 1) * part_stride;
     if (b->seg_direct[s])
@@ -546,11 +554,11 @@ int gbv_sm_batch_submit(gbv_ctx* c, gbv_sm_batch* b) {
       launch_sm_group_pairing(LaunchCfg{G, 64, sb}, g0, G, b->grp_msg, b->PgJ, b->SgJ, b->H, b->seg_ok + s, b->grp_state, b->n_fallback);
     hipEventRecord(e[9], sb);
   }
-  hipEvent_t* ep = ev + 2 + 12 * S;
+  hipEvent_t* ep = ev + 2 + EPS * S;
   // the tail runs on B0 after everything of this batch (B1's last segment included)
   if (S > 1) {
     size_t last_b1 = (S - 1) & 1 ? S - 1 : S - 2;  // last segment that ran on B1
-    HIP_CHECK(c, hipStreamWaitEvent(sbs[0], ev[2 + 12 * last_b1 + 9], 0));
+    HIP_CHECK(c, hipStreamWaitEvent(sbs[0], ev[2 + EPS * last_b1 + 9], 0));
   }
   hipEventRecord(ep[0], sbs[0]);
   // valid = 1 for the sets of passing chunks; the sets of failed chunks go through 8-set run
@@ -603,11 +611,11 @@ int gbv_sm_batch_wait(gbv_ctx* c, gbv_sm_batch* b, uint8_t* valid) {
   };
   acc(0, ev[0], ev[1]);
   for (size_t s = 0; s < b->n_seg; ++s) {
-    hipEvent_t* e = ev + 2 + 12 * s;
+    hipEvent_t* e = ev + 2 + 13 * s;
     for (int k = 0; k < 5; ++k) acc(1 + k, e[2 * k], e[2 * k + 1]);
     if (b->seg_msm[s]) acc(7, e[10], e[11]);
   }
-  hipEvent_t* ep = ev + 2 + 12 * b->n_seg;
+  hipEvent_t* ep = ev + 2 + 13 * b->n_seg;
   acc(6, ep[0], ep[1]);
   return GBV_OK;
 }

@@ -152,9 +152,9 @@ __global__ void GBV_KERNEL_ATTR k_msm_sum64(uint32_t n, const G2J* __restrict__ 
   if (threadIdx.x == 0) out[blockIdx.x] = s;
 }
 
-void launch_msm_g2_segment(hipStream_t s, uint32_t s0, uint32_t n, const uint32_t* set_grp, const uint8_t* status, const uint8_t* grp_state,
+void launch_msm_g2_buckets(hipStream_t s, uint32_t s0, uint32_t n, const uint32_t* set_grp, const uint8_t* status, const uint8_t* grp_state,
                            const G2A* S, const Seed& seed, uint32_t nonce, uint32_t* cnt, uint32_t* off, uint32_t* cur, uint32_t* ent,
-                           G2J* buckets, G2J* part, G2J* total) {
+                           G2J* buckets) {
   static_assert(MSM_KEYS % 4096 == 0 && MSM_PARTS % 64 == 0, "MSM shape");
   hipLaunchKernelGGL(k_msm_zero, dim3(MSM_KEYS / 256), dim3(256), 0, s, cnt);
   unsigned eb = (n + 63) / 64;
@@ -170,6 +170,9 @@ void launch_msm_g2_segment(hipStream_t s, uint32_t s0, uint32_t n, const uint32_
   debug_sync(s, "k_msm_entries<scatter>");
   hipLaunchKernelGGL(k_msm_buckets, dim3(MSM_KEYS / 64), dim3(64), 0, s, s0, off, cur, ent, S, buckets);
   debug_sync(s, "k_msm_buckets");
+}
+
+void launch_msm_g2_reduce(hipStream_t s, const G2J* buckets, G2J* part, G2J* total) {
   hipLaunchKernelGGL(k_msm_slices, dim3(MSM_PARTS / 64), dim3(64), 0, s, buckets, part);
   debug_sync(s, "k_msm_slices");
   // MSM_PARTS -> MSM_PARTS/64 -> ... -> 1
