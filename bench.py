@@ -56,17 +56,19 @@ PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_latest.json")  # tools/pmc.sh 
 ALG_BYTES_PER_SET = 4 + 96 + 4 + 128 + 1 + 1 + 256 + round((1 / 8 + 1 / 80) * (384 + 192))
 
 
-def pmc_evidence(units_per_launch):
+def pmc_evidence(units_per_launch, kernel="k_sm_prepare<false>"):
     """HBM traffic per launch and VALU issue utilisation of k_sm_prepare from the committed
     rocprofv3 --pmc summary (separate passes; FETCH_SIZE doubled per the gfx950 calibration in the
     MI355X guide: it counts 64 B per 128-B request; rocprofv3 reports kilobytes)."""
     try:
-        d = json.load(open(PMC_SUMMARY))["k_sm_prepare"]
+        summary = json.load(open(PMC_SUMMARY))
+        d = summary.get(kernel) or summary["k_sm_prepare"]
     except (OSError, KeyError, ValueError):
         return None, None
     per_set = (2 * d["FETCH_SIZE"] + d["WRITE_SIZE"]) * 1024.0 / d["grid_size"]
     valu = d["SQ_INSTS_VALU"] / (d["duration_ms"] * 1e-3 * PEAK_VALU_WAVE_INSTR_PER_S)
-    ev = {"source": os.path.relpath(PMC_SUMMARY, ROOT), "pmc_grid_sets": int(d["grid_size"]),
+    ev = {"source": os.path.relpath(PMC_SUMMARY, ROOT), "kernel": kernel if kernel in summary else "k_sm_prepare",
+          "pmc_grid_sets": int(d["grid_size"]),
           "hbm_bytes_per_set": round(per_set, 1), "algorithmic_bytes_per_set": ALG_BYTES_PER_SET, "valu_wave_instr_per_set": round(d["SQ_INSTS_VALU"] / d["SQ_WAVES"]),
           "valu_issue_utilisation": round(valu, 4),
           "valu_lane_utilisation": round(d["SQ_THREAD_CYCLES_VALU"] / (64.0 * d["SQ_ACTIVE_INST_VALU"]), 4)}
@@ -304,7 +306,7 @@ def main():
     w_fme = W_PREPARE_FME_MSM if kcnt[7] > 0 else W_PREPARE_FME
     achieved = units_per_launch * w_fme * MAC_PER_FME / t_launch / 1e12 if t_launch > 0 else 0.0
     peak = PEAK_MAC_PER_S / 1e12
-    traffic, pmc = pmc_evidence(units_per_launch)
+    traffic, pmc = pmc_evidence(units_per_launch, "k_sm_prepare<false>" if kcnt[7] > 0 else "k_sm_prepare<true>")
     roofline = {"bound": "valu-int", "kernel": "k_sm_prepare", "achieved": round(achieved, 4), "peak": peak,
                 "unit": "T u32-MAC/s", "frac": round(achieved / peak, 5),
                 "traffic": round(traffic) if traffic is not None else None, "pmc": pmc,

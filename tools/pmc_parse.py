@@ -15,6 +15,8 @@ def main(root, out):
         with open(path) as f:
             for row in csv.DictReader(f):
                 short = row.get("Kernel_Name", "").split("(")[0].replace("gbv::", "")
+                if short.startswith("void "):  # template instances: "void gbv::k_sm_prepare<false>"
+                    short = short[5:]
                 rows[short].append((float(row["Grid_Size"]), row["Counter_Name"], float(row["Counter_Value"])))
                 dur = (int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) * 1e-6
                 rows[short].append((float(row["Grid_Size"]), "duration_ms", dur))
