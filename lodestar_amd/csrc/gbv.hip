@@ -105,7 +105,7 @@ struct gbv_sm_batch {
   size_t fb_cap = 0;
   // bucket MSM scratch (allocated on the first submit that uses it): two sets, by segment parity
   uint32_t *msm_cnt[2] = {}, *msm_off[2] = {}, *msm_cur[2] = {};
-  G2J *msm_buckets[2] = {}, *msm_part[2] = {};
+  G2J *msm_buckets[2] = {}, *msm_part[2] = {}, *msm_head[2] = {}, *msm_tail[2] = {};
   uint32_t* msm_ent = nullptr;  // 4 per set, segment s at 4 * s0
   G2J* msm_total = nullptr;     // one per segment
   std::vector<uint8_t> seg_msm = std::vector<uint8_t>(64);
@@ -121,6 +121,7 @@ static hipError_t msm_alloc(gbv_sm_batch* b) {
   for (int k = 0; k < 2; ++k) {
     chk(dalloc(&b->msm_cnt[k], MSM_KEYS)); chk(dalloc(&b->msm_off[k], MSM_KEYS)); chk(dalloc(&b->msm_cur[k], MSM_KEYS));
     chk(dalloc(&b->msm_buckets[k], MSM_KEYS)); chk(dalloc(&b->msm_part[k], MSM_PARTS + 130));
+    chk(dalloc(&b->msm_head[k], 4 * b->n / MSM_RUN + 64)); chk(dalloc(&b->msm_tail[k], 4 * b->n / MSM_RUN + 64));
   }
   chk(dalloc(&b->msm_ent, 4 * b->n)); chk(dalloc(&b->msm_total, b->seg_cap));
   return e;
@@ -343,6 +344,7 @@ void gbv_sm_batch_destroy(gbv_ctx* c, gbv_sm_batch* b) {
   hipFree(b->fb_runs); hipFree(b->fb_list); hipFree(b->fb_cnt);
   for (int k = 0; k < 2; ++k) {
     hipFree(b->msm_cnt[k]); hipFree(b->msm_off[k]); hipFree(b->msm_cur[k]); hipFree(b->msm_buckets[k]); hipFree(b->msm_part[k]);
+    hipFree(b->msm_head[k]); hipFree(b->msm_tail[k]);
   }
   hipFree(b->msm_ent); hipFree(b->msm_total);
   delete b;
@@ -524,7 +526,7 @@ int gbv_sm_batch_submit(gbv_ctx* c, gbv_sm_batch* b) {
     if (msm && s >= 2 && b->seg_msm[s - 2]) HIP_CHECK(c, hipStreamWaitEvent(sa, ev[2 + EPS * (s - 2) + 12], 0));
     if (msm)
       launch_msm_g2_buckets(sa, s0, s1 - s0, b->set_grp, b->status, b->grp_state, b->S, seed, nonce, b->msm_cnt[s & 1], b->msm_off[s & 1],
-                            b->msm_cur[s & 1], b->msm_ent + 4ull * s0, b->msm_buckets[s & 1]);
+                            b->msm_cur[s & 1], b->msm_ent + 4ull * s0, b->msm_buckets[s & 1], b->msm_head[s & 1], b->msm_tail[s & 1]);
     hipEventRecord(e[11], scf);
     if (msm) HIP_CHECK(c, hipStreamWaitEvent(sb, e[3], 0));
     hipEventRecord(e[4], sb);

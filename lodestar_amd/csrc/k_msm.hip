@@ -14,6 +14,8 @@
 // sum_w 2^(16 w) sum_d d B_{w,d} is formed by slices of 16 buckets (running sums + one 16-bit
 // scalar multiple of the slice total) and a tree sum.  The segment's failure path does not use
 // the MSM: k_sm_redo_g2 recomputes the per-set terms with the same r_i (k_sm.hip).
+#include <cstdlib>
+
 #include "launch.h"
 #include "kernel_common.h"
 
@@ -21,7 +23,6 @@ namespace gbv {
 
 GBV_NI G2J msm_add(G2J a, G2J b) { return jac_add(a, b); }
 GBV_NI G2J msm_dbl(G2J a) { return jac_dbl(a); }
-GBV_NI G2J msm_madd(G2J a, G2A q) { return jac_add_aff(a, q); }
 
 __device__ inline bool msm_member(uint32_t i, const uint32_t* set_grp, const uint8_t* status, const uint8_t* grp_state) {
   return status[i] == SET_OK && grp_state[set_grp[i]] == GRP_PENDING;
@@ -88,20 +89,77 @@ __global__ void __launch_bounds__(64) k_msm_scan_apply(const uint32_t* __restric
   cur[k] = e;
 }
 
-// One thread per bucket: B_key = sum of its entries' (signed) points.
+__device__ inline G2A msm_entry_point(uint32_t v, uint32_t s0, const G2A* __restrict__ S) {
+  G2A q = S[s0 + (v >> 2)];
+  if (v & 2u) q = g2_neg_psi2(q);
+  if (v & 1u) q.y = fp2_neg(q.y);
+  return q;
+}
+
+// One thread per bucket: B_key = sum of its entries' (signed) points (GBV_MSM_RUNS=0 variant).
 __global__ void GBV_KERNEL_ATTR k_msm_buckets(uint32_t s0, const uint32_t* __restrict__ off, const uint32_t* __restrict__ end,
                                               const uint32_t* __restrict__ ent, const G2A* __restrict__ S, G2J* __restrict__ B) {
   uint32_t key = blockIdx.x * blockDim.x + threadIdx.x;
   if (key >= MSM_KEYS) return;
   G2J acc = jac_infinity<Fp2>();
-  for (uint32_t e = off[key], e1 = end[key]; e < e1; ++e) {
-    uint32_t v = ent[e];
-    G2A q = S[s0 + (v >> 2)];
-    if (v & 2u) q = g2_neg_psi2(q);
-    if (v & 1u) q.y = fp2_neg(q.y);
-    acc = msm_madd(acc, q);
-  }
+  for (uint32_t e = off[key], e1 = end[key]; e < e1; ++e)
+    acc = jac_add_aff(acc, msm_entry_point(ent[e], s0, S));  // inlined: a call would move acc through scratch
   B[key] = acc;
+}
+
+// One thread per run of MSM_RUN consecutive sorted entries, so every lane does the same number of
+// additions whatever the bucket sizes (window-0 digits are all odd: half those buckets are empty,
+// the others hold twice the mean).  A bucket lying inside the run is written to B directly; a
+// bucket continuing from the previous run goes to head[t], one continuing into the next run to
+// tail[t], and k_msm_fixup adds the pieces.
+__global__ void GBV_KERNEL_ATTR k_msm_runs(uint32_t s0, const uint32_t* __restrict__ off, const uint32_t* __restrict__ end,
+                                           const uint32_t* __restrict__ ent, const G2A* __restrict__ S, G2J* __restrict__ B,
+                                           G2J* __restrict__ head, G2J* __restrict__ tail) {
+  const uint32_t E = end[MSM_KEYS - 1];  // total entries (the last key's end)
+  uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t p = t * MSM_RUN;
+  if (p >= E) return;
+  uint32_t pe = min(p + MSM_RUN, E), r0 = p;
+  // bucket holding entry p: the largest key with off[key] <= p (then end[key] = off[key+1] > p)
+  uint32_t lo = 0, hi = MSM_KEYS - 1;
+  while (lo < hi) {
+    uint32_t mid = (lo + hi + 1) >> 1;
+    if (off[mid] <= p) lo = mid; else hi = mid - 1;
+  }
+  uint32_t k = lo, kend = end[k];
+  G2J acc = jac_infinity<Fp2>();
+  for (; p < pe; ++p) {
+    acc = jac_add_aff(acc, msm_entry_point(ent[p], s0, S));
+    if (p + 1 == kend || p + 1 == pe) {
+      bool starts_here = off[k] >= r0, ends_here = kend <= pe;
+      if (starts_here && ends_here) B[k] = acc;
+      else if (!starts_here) head[t] = acc;
+      else tail[t] = acc;
+      acc = jac_infinity<Fp2>();
+      if (p + 1 < pe) {
+        do { ++k; } while (end[k] == off[k]);
+        kend = end[k];
+      }
+    }
+  }
+}
+
+// One thread per bucket: empty buckets become infinity, buckets split over runs t0..t1 are
+// tail[t0] + head[t0+1] + ... + head[t1].
+__global__ void GBV_KERNEL_ATTR k_msm_fixup(const uint32_t* __restrict__ off, const uint32_t* __restrict__ end,
+                                            const G2J* __restrict__ head, const G2J* __restrict__ tail, G2J* __restrict__ B) {
+  uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= MSM_KEYS) return;
+  uint32_t b = off[k], e = end[k];
+  if (b == e) {
+    B[k] = jac_infinity<Fp2>();
+    return;
+  }
+  uint32_t t0 = b / MSM_RUN, t1 = (e - 1) / MSM_RUN;
+  if (t0 == t1) return;
+  G2J acc = tail[t0];
+  for (uint32_t t = t0 + 1; t <= t1; ++t) acc = msm_add(acc, head[t]);
+  B[k] = acc;
 }
 
 // One thread per slice of MSM_SLICE buckets of one window:
@@ -154,7 +212,7 @@ __global__ void GBV_KERNEL_ATTR k_msm_sum64(uint32_t n, const G2J* __restrict__ 
 
 void launch_msm_g2_buckets(hipStream_t s, uint32_t s0, uint32_t n, const uint32_t* set_grp, const uint8_t* status, const uint8_t* grp_state,
                            const G2A* S, const Seed& seed, uint32_t nonce, uint32_t* cnt, uint32_t* off, uint32_t* cur, uint32_t* ent,
-                           G2J* buckets) {
+                           G2J* buckets, G2J* head, G2J* tail) {
   static_assert(MSM_KEYS % 4096 == 0 && MSM_PARTS % 64 == 0, "MSM shape");
   hipLaunchKernelGGL(k_msm_zero, dim3(MSM_KEYS / 256), dim3(256), 0, s, cnt);
   unsigned eb = (n + 63) / 64;
@@ -168,8 +226,17 @@ void launch_msm_g2_buckets(hipStream_t s, uint32_t s0, uint32_t n, const uint32_
   debug_sync(s, "k_msm_scan");
   hipLaunchKernelGGL(k_msm_entries<true>, dim3(eb), dim3(64), 0, s, s0, n, set_grp, status, grp_state, seed, nonce, cur, ent);
   debug_sync(s, "k_msm_entries<scatter>");
-  hipLaunchKernelGGL(k_msm_buckets, dim3(MSM_KEYS / 64), dim3(64), 0, s, s0, off, cur, ent, S, buckets);
-  debug_sync(s, "k_msm_buckets");
+  static const bool per_bucket = getenv("GBV_MSM_RUNS") && atoi(getenv("GBV_MSM_RUNS")) == 0;
+  if (per_bucket) {
+    hipLaunchKernelGGL(k_msm_buckets, dim3(MSM_KEYS / 64), dim3(64), 0, s, s0, off, cur, ent, S, buckets);
+    debug_sync(s, "k_msm_buckets");
+  } else {
+    uint32_t runs = (uint32_t)((4ull * n + MSM_RUN - 1) / MSM_RUN);  // upper bound; runs past the end exit
+    hipLaunchKernelGGL(k_msm_runs, dim3((runs + 63) / 64), dim3(64), 0, s, s0, off, cur, ent, S, buckets, head, tail);
+    debug_sync(s, "k_msm_runs");
+    hipLaunchKernelGGL(k_msm_fixup, dim3(MSM_KEYS / 64), dim3(64), 0, s, off, cur, head, tail, buckets);
+    debug_sync(s, "k_msm_fixup");
+  }
 }
 
 void launch_msm_g2_reduce(hipStream_t s, const G2J* buckets, G2J* part, G2J* total) {

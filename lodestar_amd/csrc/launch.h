@@ -30,11 +30,12 @@ void launch_sm_chunk_finish_s(LaunchCfg c, uint32_t g0, uint32_t G, uint32_t s0,
 // Bucket MSM of a same-message segment: total = sum over its sets with status OK in pending chunks
 // of r_i sig_i (k_msm.hip).  Scratch: cnt/off/cur MSM_KEYS u32 each, ent 4 u32 per set, buckets
 // MSM_KEYS G2J, part MSM_PARTS + 130 G2J.
+constexpr uint32_t MSM_RUN = 32;  // sorted entries per thread of k_msm_runs (head/tail: 4n/MSM_RUN + 1 G2J each)
 constexpr uint32_t MSM_C = 16, MSM_WINDOWS = 2, MSM_KEYS = MSM_WINDOWS << MSM_C, MSM_SLICE = 16, MSM_PARTS = MSM_KEYS / MSM_SLICE;
 // throughput part (stream A): entries, counting sort, bucket sums
 void launch_msm_g2_buckets(hipStream_t s, uint32_t s0, uint32_t n, const uint32_t* set_grp, const uint8_t* status, const uint8_t* grp_state,
                            const G2A* S, const Seed& seed, uint32_t nonce, uint32_t* cnt, uint32_t* off, uint32_t* cur, uint32_t* ent,
-                           G2J* buckets);
+                           G2J* buckets, G2J* head, G2J* tail);
 // latency part (tail stream): slice running sums and the tree sum into *total
 void launch_msm_g2_reduce(hipStream_t s, const G2J* buckets, G2J* part, G2J* total);
 void launch_fp12_check(LaunchCfg c, uint32_t k, const Fp12* parts, uint8_t* out);

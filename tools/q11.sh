@@ -7,6 +7,7 @@ run() { # tag env...
 }
 timeout -k 10 300 python3 -u -m pytest tests/test_gpu_scale.py -x -q --timeout 120 --timeout-method thread > gpurun_out/q11/scale.log 2>&1 || { tail -30 gpurun_out/q11/scale.log; exit 1; }
 tail -1 gpurun_out/q11/scale.log
-for r in 1 2 3; do
-  run E$r
+for r in 1 2; do
+  run R$r
+  run P$r GBV_MSM_RUNS=0
 done
