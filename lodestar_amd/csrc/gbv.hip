@@ -521,13 +521,18 @@ int gbv_sm_batch_submit(gbv_ctx* c, gbv_sm_batch* b) {
     launch_sm_chunk_finish(LaunchCfg{0, 64, scf}, g0, G, s0, b->grp_off, b->status, Sh, b->rP, b->PgJ, b->SgJ, b->grp_state,
                            b->n_fallback);
     hipEventRecord(e[3], scf);
-    hipEventRecord(e[10], scf);
+    // the bucket pass runs on stream A (default) or, with GBV_MSM_STREAM=h, on the hash stream beside
+    // the tail's Miller values
+    static const bool msm_on_hash = getenv("GBV_MSM_STREAM") && getenv("GBV_MSM_STREAM")[0] == 'h';
+    hipStream_t smsm = msm ? (msm_on_hash ? sh : sa) : scf;
+    if (msm && msm_on_hash) HIP_CHECK(c, hipStreamWaitEvent(sh, e[3], 0));
+    hipEventRecord(e[10], smsm);
     // segment s-2 shares this segment's bucket buffers: its reduction (tail stream) must be done
-    if (msm && s >= 2 && b->seg_msm[s - 2]) HIP_CHECK(c, hipStreamWaitEvent(sa, ev[2 + EPS * (s - 2) + 12], 0));
+    if (msm && s >= 2 && b->seg_msm[s - 2]) HIP_CHECK(c, hipStreamWaitEvent(smsm, ev[2 + EPS * (s - 2) + 12], 0));
     if (msm)
-      launch_msm_g2_buckets(sa, s0, s1 - s0, b->set_grp, b->status, b->grp_state, b->S, seed, nonce, b->msm_cnt[s & 1], b->msm_off[s & 1],
+      launch_msm_g2_buckets(smsm, s0, s1 - s0, b->set_grp, b->status, b->grp_state, b->S, seed, nonce, b->msm_cnt[s & 1], b->msm_off[s & 1],
                             b->msm_cur[s & 1], b->msm_ent + 4ull * s0, b->msm_buckets[s & 1], b->msm_head[s & 1], b->msm_tail[s & 1]);
-    hipEventRecord(e[11], scf);
+    hipEventRecord(e[11], smsm);
     if (msm) HIP_CHECK(c, hipStreamWaitEvent(sb, e[3], 0));
     hipEventRecord(e[4], sb);
     if (!b->seg_direct[s]) launch_sm_miller(LaunchCfg{0, 64, sb}, g0, G, b->grp_msg, b->grp_state, b->PgJ, b->H, b->F);
