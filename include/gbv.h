@@ -131,8 +131,9 @@ int gbv_fp12_check(gbv_ctx* ctx, const uint8_t* partials576, size_t k, uint8_t* 
 
 /* Device time (ms, summed over launches) and launch count of each kernel of the last
  * gbv_sm_batch_verify, measured with HIP events on the stream each kernel runs on:
- * [hash, prepare, chunk_finish, miller, seg_check, group_pairing, fallback]; returns the number of
- * entries written (at most 7). */
+ * [hash, prepare, chunk_finish, miller, seg_check, group_pairing, fallback, msm] (msm: the bucket
+ * pass of segments whose G2 sum comes from the bucket MSM); returns the number of entries written
+ * (at most 8). */
 int gbv_last_kernel_ms(gbv_ctx* ctx, float* ms_out, int* launches_out, int max);
 /* Fast-path health of the last waited same-message verification: chunks that went to the per-set
  * retry (malformed sets or failing chunk checks) and segments whose combined check failed.  Both
