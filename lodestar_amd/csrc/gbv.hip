@@ -28,6 +28,7 @@ constexpr uint32_t DIRECT_CHUNK_MAX = 32;
 // segments of at least this many sets form their G2 sum sum r_i sig_i with the bucket MSM
 // (k_msm.hip) instead of per-set ladders; GBV_MSM_MIN overrides (0 = never)
 constexpr uint32_t MSM_MIN_SETS = 131072;
+constexpr uint32_t MSM_COOLDOWN = 16;
 
 // chunkifyMaximizeChunkSize (multithread/utils.ts:4-18): returns chunk start offsets + end.
 std::vector<uint32_t> chunk_offsets(uint32_t len, uint32_t min_per_chunk) {
@@ -59,6 +60,9 @@ struct gbv_ctx {
   uint32_t nonce = 0;
   hipStream_t stream2 = nullptr, stream3 = nullptr, stream4 = nullptr;
   uint32_t sm_submits = 0;  // parity picks which of stream2/stream3 carries a batch's chunk tail
+  // A failing MSM segment pays the per-set G2 terms after all (k_sm_redo_g2) on top of the MSM, so
+  // after one the next MSM_COOLDOWN submits use the per-set ladders (invalid-dense streams, C5)
+  uint32_t msm_cooldown = 0;
   std::vector<hipEvent_t> events;
   static constexpr int NK = 8;  // hash, prepare, chunk_reduce, miller, seg_check, group_pairing, fallback, msm
   float last_ms[NK] = {};
@@ -466,7 +470,8 @@ int gbv_sm_batch_submit(gbv_ctx* c, gbv_sm_batch* b) {
   gcut.push_back((uint32_t)b->G);
   size_t S = gcut.size() - 1;
   b->n_seg = S;
-  const size_t msm_min = msm_min_sets();
+  const size_t msm_min = c->msm_cooldown ? 0 : msm_min_sets();
+  if (c->msm_cooldown) --c->msm_cooldown;
   bool any_msm = false;
   for (size_t s = 0; s < S; ++s) {
     uint32_t G = gcut[s + 1] - gcut[s];
@@ -605,7 +610,12 @@ int gbv_sm_batch_wait(gbv_ctx* c, gbv_sm_batch* b, uint8_t* valid) {
   if (valid) memcpy(valid, b->valid_host, b->n);
   c->last_fallback_chunks = *b->nfb_host;
   c->last_failed_segments = 0;
-  for (size_t s = 0; s < b->n_seg; ++s) c->last_failed_segments += (b->seg_ok_host[s] || b->seg_direct[s]) ? 0 : 1;
+  for (size_t s = 0; s < b->n_seg; ++s) {
+    bool failed = !(b->seg_ok_host[s] || b->seg_direct[s]);
+    c->last_failed_segments += failed ? 1 : 0;
+    if (failed && b->seg_msm[s])
+      c->msm_cooldown = getenv("GBV_MSM_COOLDOWN") ? (uint32_t)atoi(getenv("GBV_MSM_COOLDOWN")) : MSM_COOLDOWN;
+  }
   for (auto& x : c->last_ms) x = 0.f;
   for (auto& x : c->last_launches) x = 0;
   hipEvent_t* ev = b->evs[b->cur].data();

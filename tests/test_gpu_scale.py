@@ -65,6 +65,7 @@ def segments(monkeypatch, request):
     # G2 terms per set (32-step ladders) or per segment (bucket MSM, k_msm.hip): both must give the
     # same booleans, and an all-valid stream must pass the segment checks either way
     monkeypatch.setenv("GBV_MSM_MIN", "0" if request.param == "ladder" else "1000")
+    monkeypatch.setenv("GBV_MSM_COOLDOWN", "0")  # keep the MSM on after a failing segment
     return request.param
 
 
@@ -111,6 +112,7 @@ def test_same_message_one_percent_invalid(world, monkeypatch, mode):
     checks: more than FB_COOP_MAX items each) and must still return exactly the per-set booleans.
     In MSM mode the failing segment first recomputes its per-set G2 terms (k_sm_redo_g2)."""
     monkeypatch.setenv("GBV_MSM_MIN", "0" if mode == "ladder" else "1000")
+    monkeypatch.setenv("GBV_MSM_COOLDOWN", "0")
     v, sks, _ = world
     off, idx, grp, sigs, msgs = _workload(v, sks, 60000, 14)
     n = len(sigs)
@@ -225,6 +227,7 @@ def test_same_message_msm_single_segment(world, monkeypatch):
     must have run (their time is reported in slot 7 of last_kernel_ms)."""
     monkeypatch.setenv("GBV_SEGMENTS", "1")
     monkeypatch.setenv("GBV_MSM_MIN", "65536")
+    monkeypatch.setenv("GBV_MSM_COOLDOWN", "0")
     v, sks, _ = world
     off, idx, grp, sigs, msgs = _workload(v, sks, 100000, 15)
     res = _run_staged(v, off, idx, sigs, msgs)
@@ -239,3 +242,31 @@ def test_same_message_msm_single_segment(world, monkeypatch):
     assert res == [i != 77777 for i in range(len(sigs))]
     fb, seg = v.last_stats()
     assert fb == 1 and seg == 1
+
+
+def test_msm_cooldown_after_failing_segment(world, monkeypatch):
+    """After an MSM segment fails, the next submits use the per-set ladders (an invalid-dense stream
+    would otherwise pay the MSM and the G2 recomputation); booleans are the same either way."""
+    monkeypatch.setenv("GBV_SEGMENTS", "1")
+    monkeypatch.setenv("GBV_MSM_MIN", "1000")
+    monkeypatch.setenv("GBV_MSM_COOLDOWN", "2")
+    v, sks, _ = world
+    off, idx, grp, sigs, msgs = _workload(v, sks, 5000, 16)
+    bad = list(sigs)
+    bad[123] = bytes([10]) * 96
+    want = [i != 123 for i in range(len(sigs))]
+    st = v.stage_same_message(off, idx, b"".join(bad), b"".join(msgs))
+    try:
+        # a chunk holding a malformed set is excluded from the segment check, so this one passes;
+        # a wrong-message signature makes the segment fail
+        bad[4000] = sigs[(4000 + 300) % len(sigs)]
+        want[4000] = False
+        st.close()
+        st = v.stage_same_message(off, idx, b"".join(bad), b"".join(msgs))
+        msm_runs = []
+        for _ in range(4):
+            assert [b == 1 for b in st.verify(True)] == want
+            msm_runs.append(v.last_kernel_ms()[1][7])
+        assert msm_runs == [1, 0, 0, 1]  # MSM, cooldown x2, MSM again
+    finally:
+        st.close()
