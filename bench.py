@@ -199,7 +199,7 @@ def p50_batch_latency(v, call_off, idx, sigs, msgs, reps=20):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=12)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--sets", type=int, default=1 << 20)
     ap.add_argument("--cpu-sample", type=int, default=None, help="sets in the CPU baseline sample")

@@ -5,7 +5,7 @@
 set -o pipefail
 TAG=${1:-r01}
 shift || true
-BENCH_ARGS=${*:-"--steps 3 --warmup 1"}
+BENCH_ARGS=${*:-""}
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
