@@ -30,7 +30,10 @@ void launch_sm_chunk_finish_s(LaunchCfg c, uint32_t g0, uint32_t G, uint32_t s0,
 // Bucket MSM of a same-message segment: total = sum over its sets with status OK in pending chunks
 // of r_i sig_i (k_msm.hip).  Scratch: cnt/off/cur MSM_KEYS u32 each, ent 4 u32 per set, buckets
 // MSM_KEYS G2J, part MSM_PARTS + 130 G2J.
-constexpr uint32_t MSM_RUN = 32;  // sorted entries per thread of k_msm_runs (head/tail: 4n/MSM_RUN + 1 G2J each)
+#ifndef GBV_MSM_RUN
+#define GBV_MSM_RUN 32
+#endif
+constexpr uint32_t MSM_RUN = GBV_MSM_RUN;  // sorted entries per thread of k_msm_runs (head/tail: 4n/MSM_RUN + 1 G2J each)
 constexpr uint32_t MSM_C = 16, MSM_WINDOWS = 2, MSM_KEYS = MSM_WINDOWS << MSM_C, MSM_SLICE = 16, MSM_PARTS = MSM_KEYS / MSM_SLICE;
 // throughput part (stream A): entries, counting sort, bucket sums
 void launch_msm_g2_buckets(hipStream_t s, uint32_t s0, uint32_t n, const uint32_t* set_grp, const uint8_t* status, const uint8_t* grp_state,
