@@ -165,6 +165,7 @@ __global__ void GBV_KERNEL_ATTR k_msm_fixup(const uint32_t* __restrict__ off, co
 // One thread per slice of MSM_SLICE buckets of one window:
 //   part = 2^(16 w) (sum_{q>=1} q B_{d0+q} + d0 sum_q B_{d0+q}),  d0 = slice * MSM_SLICE.
 __global__ void GBV_KERNEL_ATTR k_msm_slices(const G2J* __restrict__ B, G2J* __restrict__ part) {
+  GBV_TAIL_WAVE_PRIO();
   constexpr uint32_t PER_WIN = (1u << MSM_C) / MSM_SLICE;
   uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= MSM_PARTS) return;
@@ -198,6 +199,7 @@ __device__ inline Fp shfl_down_fp_m(const Fp& a, unsigned d) {
 
 // Tree sum of 64 points per workgroup: out[blk] = sum in[blk*64 .. blk*64+63] (< n).
 __global__ void GBV_KERNEL_ATTR k_msm_sum64(uint32_t n, const G2J* __restrict__ in, G2J* __restrict__ out) {
+  GBV_TAIL_WAVE_PRIO();
   uint32_t k = blockIdx.x * 64 + threadIdx.x;
   G2J s = k < n ? in[k] : jac_infinity<Fp2>();
   for (unsigned d = 32; d >= 1; d >>= 1) {

@@ -160,6 +160,7 @@ __global__ void GBV_KERNEL_ATTR k_sm_chunk_finish(uint32_t g0, uint32_t G, uint3
 // chunk count (~1/80 of the sets) is small, so these waves take few slots beside k_sm_prepare.
 __global__ void GBV_KERNEL_ATTR k_sm_miller(uint32_t g0, uint32_t G, const uint32_t* __restrict__ grp_msg, const uint8_t* __restrict__ grp_state,
                                             const G1J* __restrict__ PgJ, const G2A* __restrict__ H, Fp12* __restrict__ F) {
+  GBV_TAIL_WAVE_PRIO();
   uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= G) return;
   g += g0;
@@ -189,6 +190,7 @@ __device__ inline void wave_reduce_fs(Fp12& f, G2J& s, int& any) {
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
 k_sm_seg_reduce(uint32_t g0, uint32_t G, const uint8_t* __restrict__ grp_state, const Fp12* __restrict__ F, const G2J* __restrict__ SgJ,
                 Fp12* __restrict__ Fpart, G2J* __restrict__ Spart, uint8_t* __restrict__ has) {
+  GBV_TAIL_WAVE_PRIO();
   uint32_t g = g0 + blockIdx.x * 64 + threadIdx.x;
   int any = g < g0 + G && grp_state[g] == GRP_PENDING;
   Fp12 f = any ? F[g] : fp12_one();
@@ -207,6 +209,7 @@ k_sm_seg_reduce(uint32_t g0, uint32_t G, const uint8_t* __restrict__ grp_state, 
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
 k_sm_part_reduce(uint32_t n, const uint8_t* __restrict__ has_in, const Fp12* __restrict__ Fin, const G2J* __restrict__ Sin,
                  Fp12* __restrict__ Fout, G2J* __restrict__ Sout, uint8_t* __restrict__ has_out) {
+  GBV_TAIL_WAVE_PRIO();
   uint32_t k = blockIdx.x * 64 + threadIdx.x;
   int any = k < n && has_in[k];
   Fp12 f = any ? Fin[k] : fp12_one();

@@ -54,6 +54,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
                                                      const G2J* __restrict__ Spart, const uint8_t* __restrict__ has,
                                                      uint8_t* __restrict__ grp_state, uint8_t* __restrict__ seg_ok,
                                                      Fp12* __restrict__ miller_out, const G2J* __restrict__ S_extra) {
+  GBV_TAIL_WAVE_PRIO();
   __shared__ Fp ws[SEG_WS];
   __shared__ int flags[2];
   Fp* ml = ws;

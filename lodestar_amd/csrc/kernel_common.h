@@ -30,6 +30,17 @@
 #endif
 #define GBV_KERNEL_ATTR __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GBV_WAVES_PER_EU)))
 
+// Tail kernels (chunk Miller values, MSM reduction, segment reduction and check) share SIMDs with
+// the next batch's k_sm_prepare; GBV_TAIL_PRIO > 0 raises their waves' issue priority (s_setprio)
+// so the tail of a batch finishes sooner.  0 = hardware default.
+#ifndef GBV_TAIL_PRIO
+#define GBV_TAIL_PRIO 0
+#endif
+#define GBV_TAIL_WAVE_PRIO() \
+  do {                       \
+    if (GBV_TAIL_PRIO > 0) __builtin_amdgcn_s_setprio(GBV_TAIL_PRIO); \
+  } while (0)
+
 namespace gbv {
 
 struct Seed { uint32_t w[8]; };
