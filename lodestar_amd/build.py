@@ -32,9 +32,21 @@ def _compile(src, obj, verbose):
 
 
 def build(force=False, verbose=False, jobs=None):
-    """Compile each kernel family (lodestar_amd/csrc/*.hip) in parallel and link libgbv.so."""
+    """Compile each kernel family (lodestar_amd/csrc/*.hip) in parallel and link libgbv.so.
+
+    Serialised across processes with a file lock (bench.py ranks all call it): the first caller
+    builds, the others find the library fresh once they hold the lock."""
     if not force and not needs_build():
         return LIB
+    import fcntl
+    with open(os.path.join(HERE, ".build.lock"), "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        if not force and not needs_build():
+            return LIB
+        return _build_locked(force, verbose, jobs)
+
+
+def _build_locked(force, verbose, jobs):
     from concurrent.futures import ThreadPoolExecutor
     objdir = os.path.join(HERE, "build")
     os.makedirs(objdir, exist_ok=True)
