@@ -15,6 +15,8 @@
  *                             multithread/index.ts:498-507)
  *   GBV_E_CLOSED           -- context destroyed / closed (QueueError QUEUE_ABORTED, index.ts:303-305)
  *   GBV_E_ARG              -- invalid argument (null pointer, index out of table range)
+ *   GBV_E_BAD_POINT        -- a serialized point failed to deserialize where the reference throws
+ *                             (aggregateSerializedPublicKeys over a malformed key)
  */
 #ifndef GBV_H
 #define GBV_H
@@ -32,6 +34,11 @@ extern "C" {
 #define GBV_E_EMPTY_AGGREGATE (-3)
 #define GBV_E_CLOSED (-4)
 #define GBV_E_OOM (-5)
+#define GBV_E_BAD_POINT (-6)
+
+/* Per-call result byte of the multi-call entry points: 0 false, 1 true, GBV_CALL_REJECTED when the
+ * call's promise rejects (an aggregate set without pubkeys: EMPTY_AGGREGATE_ARRAY). */
+#define GBV_CALL_REJECTED 2
 
 /* Point status codes written by gbv_pubkeys_append (blst BLST_ERROR equivalents). */
 #define GBV_PT_OK 0
@@ -82,6 +89,29 @@ size_t gbv_pubkeys_count(gbv_ctx* ctx);
 int gbv_verify_sets(gbv_ctx* ctx, const gbv_set* sets, size_t n, const uint32_t* index_arena,
                     uint8_t* all_valid, uint8_t* chunk_valid);
 
+/* Many independent verifySignatureSets calls in ONE device pass -- the pool's dispatch of several
+ * jobs (multithread/index.ts:357-514) and the worker's grouping of batchable requests
+ * (worker.ts:29-107): call c covers sets [call_off[c], call_off[c+1]), call_off[0] == 0.  Every
+ * call is chunked with chunkifyMaximizeChunkSize(128) and each chunk verified as one randomised
+ * batch (verifyMultipleAggregateSignatures semantics, maybeBatch.ts:15-45); call_valid[c] is the
+ * AND over the call's chunks (0 for an empty call) or GBV_CALL_REJECTED.  A failing call does not
+ * affect the others (multithread.test.ts:109-129: an invalid set fails only its own request). */
+int gbv_verify_sets_multi(gbv_ctx* ctx, size_t n_calls, const uint32_t* call_off, const gbv_set* sets,
+                          const uint32_t* index_arena, uint8_t* call_valid);
+
+/* Device-resident form of gbv_verify_sets_multi (inputs staged in HBM once, verified many times:
+ * range sync / replay benches).  submit enqueues the whole verification and returns; wait blocks and
+ * writes call_valid.  Per-set kernels run on the context's throughput stream and the chunk checks on
+ * a tail stream, so consecutive batches overlap. */
+typedef struct gbv_vs_batch gbv_vs_batch;
+int gbv_vs_batch_create(gbv_ctx* ctx, size_t n_calls, const uint32_t* call_off, const gbv_set* sets,
+                        const uint32_t* index_arena, gbv_vs_batch** out);
+int gbv_vs_batch_submit(gbv_ctx* ctx, gbv_vs_batch* b);
+int gbv_vs_batch_wait(gbv_ctx* ctx, gbv_vs_batch* b, uint8_t* call_valid);
+void gbv_vs_batch_destroy(gbv_ctx* ctx, gbv_vs_batch* b);
+/* Device ms of the last waited verifySignatureSets pass: [aggregate, hash+signature, miller, chunk checks]. */
+int gbv_vs_last_kernel_ms(gbv_ctx* ctx, float* ms4);
+
 /* IBlsVerifier.verifySignatureSetsSameMessage (interface.ts:55-59; multithread/index.ts:212-236):
  * n sets {validator index, 96-byte signature} over one 32-byte message.  valid[i] receives the
  * per-set boolean in input order (all-true on a passing randomised aggregate check, otherwise
@@ -99,6 +129,18 @@ int gbv_verify_same_message_multi(gbv_ctx* ctx, size_t n_calls, const uint32_t* 
 /* aggregatePublicKeys(index2pubkey[idx[0..k)]).toBytes() (bls/utils.ts:5-20), byte-identical.
  * k == 0 returns GBV_E_EMPTY_AGGREGATE. */
 int gbv_aggregate_pubkeys(gbv_ctx* ctx, const uint32_t* idx, size_t k, uint8_t out48[48]);
+
+/* aggregateSerializedPublicKeys(pk48[0..k)).toBytes() (state-transition/src/util/syncCommittee.ts:37,
+ * epoch/processSyncCommitteeUpdates.ts:35): the 512-key sync-committee aggregate, byte-identical.
+ * The keys are decompressed on the device (validate != 0 adds the subgroup/infinity check); a key
+ * that fails to deserialize returns GBV_E_BAD_POINT, k == 0 GBV_E_EMPTY_AGGREGATE. */
+int gbv_aggregate_serialized_pubkeys(gbv_ctx* ctx, const uint8_t* pk48, size_t k, int validate, uint8_t out48[48]);
+
+/* Signature.fromBytes(sig, true) over n signatures of sig_len (96 or 192) bytes: status[i] = GBV_PT_*
+ * (decode, on-curve, subgroup, infinity), out96 (optional) the recompressed accepted points (the
+ * compressed infinity encoding for rejected inputs).  The "BLS deserializing signatures" perf id
+ * (beacon-node/test/perf/bls/bls.test.ts:89-100). */
+int gbv_signatures_validate(gbv_ctx* ctx, const uint8_t* sigs, size_t n, uint32_t sig_len, uint8_t* status, uint8_t* out96);
 
 /* ---- device-resident batches (inputs staged in HBM once, verified many times) ------------- */
 typedef struct gbv_sm_batch gbv_sm_batch;

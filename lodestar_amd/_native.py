@@ -16,6 +16,8 @@ GBV_E_DEVICE = -2
 GBV_E_EMPTY_AGGREGATE = -3
 GBV_E_CLOSED = -4
 GBV_E_OOM = -5
+GBV_E_BAD_POINT = -6
+GBV_CALL_REJECTED = 2
 
 EXPORTED_SYMBOLS = (
     "gbv_init", "gbv_destroy", "gbv_last_error", "gbv_pubkeys_append", "gbv_pubkeys_count",
@@ -24,7 +26,9 @@ EXPORTED_SYMBOLS = (
     "gbv_sm_batch_submit", "gbv_sm_batch_wait", "gbv_vs_partial", "gbv_fp12_check", "gbv_last_stats",
     "gbv_last_kernel_ms", "gbv_util_sk_to_pk", "gbv_util_sign", "gbv_util_hash_to_g2",
     "gbv_pubkeys_replicate", "gbv_sha256_digest64", "gbv_merkle_roots", "gbv_signing_roots",
-    "gbv_attestation_signing_roots", "gbv_ssz_last_kernel_ms",
+    "gbv_attestation_signing_roots", "gbv_ssz_last_kernel_ms", "gbv_verify_sets_multi", "gbv_vs_batch_create",
+    "gbv_vs_batch_submit", "gbv_vs_batch_wait", "gbv_vs_batch_destroy", "gbv_vs_last_kernel_ms",
+    "gbv_aggregate_serialized_pubkeys", "gbv_signatures_validate",
 )
 
 
@@ -52,6 +56,11 @@ class EmptyAggregateError(GbvError):
 
 class QueueAbortedError(GbvError):
     """QueueError(QUEUE_ABORTED) (multithread/index.ts:303-305)."""
+
+
+class BadPointError(GbvError):
+    """A serialized point failed to deserialize where blst throws (BLST_BAD_ENCODING,
+    BLST_POINT_NOT_ON_CURVE, ...), e.g. aggregateSerializedPublicKeys over a malformed key."""
 
 
 _lib = None
@@ -95,6 +104,14 @@ def load_library(path=LIB_PATH):
         "gbv_signing_roots": (i32, [vp, vp, sz, vp, sz, vp, vp]),
         "gbv_attestation_signing_roots": (i32, [vp, vp, sz, vp, sz, vp, vp]),
         "gbv_ssz_last_kernel_ms": (i32, [vp, P(ctypes.c_float)]),
+        "gbv_verify_sets_multi": (i32, [vp, sz, vp, P(GbvSet), vp, vp]),
+        "gbv_vs_batch_create": (i32, [vp, sz, vp, P(GbvSet), vp, P(vp)]),
+        "gbv_vs_batch_submit": (i32, [vp, vp]),
+        "gbv_vs_batch_wait": (i32, [vp, vp, vp]),
+        "gbv_vs_batch_destroy": (None, [vp, vp]),
+        "gbv_vs_last_kernel_ms": (i32, [vp, P(ctypes.c_float)]),
+        "gbv_aggregate_serialized_pubkeys": (i32, [vp, vp, sz, i32, vp]),
+        "gbv_signatures_validate": (i32, [vp, vp, sz, u32, vp, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -113,4 +130,6 @@ def check(lib, ctx, rc):
         raise EmptyAggregateError(rc, msg)
     if rc == GBV_E_CLOSED:
         raise QueueAbortedError(rc, msg)
+    if rc == GBV_E_BAD_POINT:
+        raise BadPointError(rc, msg)
     raise GbvError(rc, msg)

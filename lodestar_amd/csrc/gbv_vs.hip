@@ -1,0 +1,424 @@
+// Host side of verifySignatureSets (IBlsVerifier.verifySignatureSets, interface.ts:47;
+// BlsMultiThreadWorkerPool.verifySignatureSets, multithread/index.ts:157-207) and of its multi-GPU
+// shard form.  Many calls (the pool's jobs) go through ONE device pass:
+//
+//   stream A : k_vs_agg        one wave per aggregate set: coalesced gather of the set's validator
+//                              pubkeys from the HBM table + cross-lane tree sum (aggregatePublicKeys,
+//                              bls/utils.ts:5-20; jobItem.ts:55-62)
+//              k_vs_hash_sig   two block roles in one launch: hash_to_G2 of every set's signing root,
+//                              and per set Signature.fromBytes(sig, true) + pubkey + the randomised
+//                              terms r_i pk_i, r_i sig_i (maybeBatch.ts:17-26)
+//              k_vs_miller     Miller value f(r_i pk_i, H(m_i)) per set
+//   tail     : k_vs_chunk_coop one wave per <=128-set chunk (chunkifyMaximizeChunkSize,
+//                              multithread/utils.ts:4-18): product of its Miller values, the
+//                              (-g1, sum r_i sig_i) pair and ONE final exponentiation
+//
+// A call is true iff every chunk is (the AND over jobs, index.ts:185-206); a call with an empty
+// aggregate is rejected (aggregatePublicKeys throws EMPTY_AGGREGATE_ARRAY, index.ts:398-412); an
+// empty call is false (verifySignatureSetsMaybeBatch([]), maybeBatch.ts:29-31).
+#include "ctx.h"
+
+using namespace gbv;
+
+namespace {
+size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+}  // namespace
+
+struct gbv_vs_batch {
+  size_t n = 0, n_calls = 0, C = 0, n_agg = 0, A = 0;
+  uint32_t sig_stride = 96;
+  size_t cap_n = 0, cap_C = 0;
+  bool allocated = false;
+  std::vector<uint32_t> call_chunk;  // chunks of call c: [call_chunk[c], call_chunk[c+1])
+  std::vector<uint8_t> call_reject;  // call holds an empty aggregate
+  std::vector<uint32_t> chunk_off_host;
+  uint8_t *in_dev = nullptr, *in_host = nullptr;
+  size_t in_cap = 0;
+  // inputs (views into in_dev)
+  uint32_t *set_off = nullptr, *arena = nullptr, *agg_list = nullptr, *chunk_off = nullptr, *siglen = nullptr;
+  uint8_t *raw_flag = nullptr, *raw_pk = nullptr, *msgs = nullptr, *sig = nullptr;
+  // work
+  G1A* pk = nullptr;
+  uint8_t* pk_st = nullptr;
+  G2A* H = nullptr;
+  G1J* rP = nullptr;
+  G2J* rS = nullptr;
+  uint8_t* status = nullptr;
+  Fp12* F = nullptr;
+  uint8_t* chunk_valid = nullptr;
+  uint8_t* chunk_valid_host = nullptr;  // pinned
+  // shard mode (gbv_vs_partial): reduction scratch
+  Fp12 *Fpart = nullptr, *f_out = nullptr;
+  G2J* Spart = nullptr;
+  uint8_t *has = nullptr, *flag = nullptr;
+  size_t part_cap = 0;
+  hipEvent_t ev[6] = {};
+  hipEvent_t done = nullptr;
+  bool in_flight = false;
+  int tail = 0;
+};
+
+static void vs_free_work(gbv_vs_batch* b) {
+  hipFree(b->pk); hipFree(b->pk_st); hipFree(b->H); hipFree(b->rP); hipFree(b->rS); hipFree(b->status); hipFree(b->F);
+  hipFree(b->chunk_valid); hipHostFree(b->chunk_valid_host);
+  b->pk = nullptr; b->pk_st = nullptr; b->H = nullptr; b->rP = nullptr; b->rS = nullptr; b->status = nullptr; b->F = nullptr;
+  b->chunk_valid = nullptr; b->chunk_valid_host = nullptr;
+  b->allocated = false;
+}
+
+void vs_batch_free(gbv_vs_batch* b) {
+  if (!b) return;
+  if (b->in_flight && b->done) hipEventSynchronize(b->done);
+  vs_free_work(b);
+  hipFree(b->in_dev);
+  hipHostFree(b->in_host);
+  hipFree(b->Fpart); hipFree(b->Spart); hipFree(b->has); hipFree(b->f_out); hipFree(b->flag);
+  for (auto e : b->ev)
+    if (e) hipEventDestroy(e);
+  if (b->done) hipEventDestroy(b->done);
+  delete b;
+}
+
+static int vs_reserve(gbv_ctx* c, gbv_vs_batch* b, size_t n, size_t C) {
+  if (b->allocated && n <= b->cap_n && C <= b->cap_C) return GBV_OK;
+  if (b->allocated) {
+    n = std::max(n, b->cap_n);
+    C = std::max(C, b->cap_C);
+    vs_free_work(b);
+  }
+  hipError_t e = hipSuccess;
+  auto chk = [&](hipError_t x) { if (x != hipSuccess && e == hipSuccess) e = x; };
+  chk(dalloc(&b->pk, n)); chk(dalloc(&b->pk_st, n)); chk(dalloc(&b->H, n)); chk(dalloc(&b->rP, n)); chk(dalloc(&b->rS, n));
+  chk(dalloc(&b->status, n)); chk(dalloc(&b->F, n)); chk(dalloc(&b->chunk_valid, C));
+  chk(hipHostMalloc((void**)&b->chunk_valid_host, std::max<size_t>(C, 1), hipHostMallocDefault));
+  for (auto& ev : b->ev)
+    if (!ev) chk(hipEventCreate(&ev));
+  if (!b->done) chk(hipEventCreateWithFlags(&b->done, hipEventDisableTiming));
+  if (e != hipSuccess) {
+    vs_free_work(b);
+    return gbv_fail(c, GBV_E_OOM, std::string("hipMalloc: ") + hipGetErrorString(e));
+  }
+  b->allocated = true;
+  b->cap_n = n;
+  b->cap_C = C;
+  return GBV_OK;
+}
+
+// Stage n_calls calls (CSR call_off over sets) in b.  Argument errors fail the whole fill;
+// empty aggregates only mark their call rejected.
+static int vs_fill(gbv_ctx* c, gbv_vs_batch* b, size_t n_calls, const uint32_t* call_off, const gbv_set* sets, const uint32_t* arena) {
+  if (b->in_flight) return gbv_fail(c, GBV_E_ARG, "batch in flight");
+  if (n_calls && !call_off) return gbv_fail(c, GBV_E_ARG, "null call offsets");
+  size_t n = n_calls ? call_off[n_calls] : 0;
+  if (call_off && call_off[0] != 0) return gbv_fail(c, GBV_E_ARG, "call offsets must start at 0");
+  for (size_t g = 0; g < n_calls; ++g)
+    if (call_off[g + 1] < call_off[g]) return gbv_fail(c, GBV_E_ARG, "call offsets not monotone");
+  if (n && !sets) return gbv_fail(c, GBV_E_ARG, "null sets");
+  if (n > 0x7FFFFFFFull) return gbv_fail(c, GBV_E_ARG, "too many sets");
+  std::vector<uint8_t> reject(n_calls, 0);
+  size_t A = 0, n_agg = 0;
+  uint32_t stride = 96;
+  for (size_t g = 0; g < n_calls; ++g)
+    for (uint32_t i = call_off[g]; i < call_off[g + 1]; ++i) {
+      const gbv_set& s = sets[i];
+      if (!s.msg32 || (!s.sig && s.sig_len)) return gbv_fail(c, GBV_E_ARG, "null msg/sig");
+      if (s.sig_len == 192) stride = 192;
+      if (s.raw_pk48) continue;
+      if (s.idx_len == 0) {
+        reject[g] = 1;
+        continue;
+      }
+      if (!arena) return gbv_fail(c, GBV_E_ARG, "null index arena");
+      for (uint32_t j = 0; j < s.idx_len; ++j)
+        if (arena[s.idx_off + j] >= c->table_n) return gbv_fail(c, GBV_E_ARG, "validator index out of range");
+      A += s.idx_len;
+      n_agg += s.idx_len >= 2 ? 1 : 0;
+    }
+  // chunks: chunkifyMaximizeChunkSize(call, 128) per non-empty, non-rejected call
+  std::vector<uint32_t> chunk_off, call_chunk(n_calls + 1, 0);
+  for (size_t g = 0; g < n_calls; ++g) {
+    call_chunk[g] = (uint32_t)chunk_off.size();
+    uint32_t len = call_off[g + 1] - call_off[g];
+    if (len == 0 || reject[g]) continue;
+    std::vector<uint32_t> co = chunk_offsets(len, MAX_SIGNATURE_SETS_PER_JOB);
+    for (size_t j = 0; j + 1 < co.size(); ++j) chunk_off.push_back(call_off[g] + co[j]);
+  }
+  call_chunk[n_calls] = (uint32_t)chunk_off.size();
+  size_t C = chunk_off.size();
+  // chunk ends: chunk k ends where the next chunk of the same call starts, or at its call's end
+  std::vector<uint32_t> chunk_end(C);
+  for (size_t g = 0; g < n_calls; ++g)
+    for (uint32_t k = call_chunk[g]; k < call_chunk[g + 1]; ++k) chunk_end[k] = k + 1 < call_chunk[g + 1] ? chunk_off[k + 1] : call_off[g + 1];
+  HIP_CHECK(c, hipSetDevice(c->device));
+  int rc = vs_reserve(c, b, n, C);
+  if (rc) return rc;
+  // input blob: set_off 4(n+1) | arena 4A | agg_list 4 n_agg | chunk (begin,end) 8C | siglen 4n | raw_flag n |
+  //             raw_pk 48n | msgs 32n | sig stride*n
+  size_t o_so = 0, o_ar = align256(4 * (n + 1)), o_al = o_ar + align256(4 * A), o_co = o_al + align256(4 * n_agg);
+  size_t o_sl = o_co + align256(8 * C), o_rf = o_sl + align256(4 * n), o_rp = o_rf + align256(n), o_m = o_rp + align256(48 * n);
+  size_t o_sig = o_m + align256(32 * n), total = o_sig + align256((size_t)stride * n);
+  if (b->in_cap < total) {
+    hipFree(b->in_dev);
+    hipHostFree(b->in_host);
+    b->in_dev = b->in_host = nullptr;
+    size_t cap = std::max(total, b->in_cap + b->in_cap / 2);
+    b->in_cap = 0;
+    HIP_CHECK(c, hipMalloc((void**)&b->in_dev, cap));
+    HIP_CHECK(c, hipHostMalloc((void**)&b->in_host, cap, hipHostMallocDefault));
+    b->in_cap = cap;
+  }
+  uint8_t* h = b->in_host;
+  uint32_t* so = (uint32_t*)(h + o_so);
+  uint32_t* ar = (uint32_t*)(h + o_ar);
+  uint32_t* al = (uint32_t*)(h + o_al);
+  uint32_t* co = (uint32_t*)(h + o_co);
+  uint32_t* sl = (uint32_t*)(h + o_sl);
+  uint8_t* rf = h + o_rf;
+  size_t a = 0, na = 0;
+  for (size_t i = 0; i < n; ++i) {
+    const gbv_set& s = sets[i];
+    so[i] = (uint32_t)a;
+    rf[i] = s.raw_pk48 ? 1 : 0;
+    if (s.raw_pk48) {
+      memcpy(h + o_rp + 48 * i, s.raw_pk48, 48);
+    } else if (s.idx_len) {
+      memcpy(ar + a, arena + s.idx_off, 4 * (size_t)s.idx_len);
+      a += s.idx_len;
+      if (s.idx_len >= 2) al[na++] = (uint32_t)i;
+    }
+    memcpy(h + o_m + 32 * i, s.msg32, 32);
+    uint32_t L = s.sig_len;
+    sl[i] = (L == 96 || L == 192) ? L : 0;  // other lengths: BAD_ENCODING -> false
+    uint8_t* dst = h + o_sig + (size_t)stride * i;
+    if (sl[i]) memcpy(dst, s.sig, L);
+    if (sl[i] < stride) memset(dst + sl[i], 0, stride - sl[i]);
+  }
+  so[n] = (uint32_t)a;
+  for (size_t k = 0; k < C; ++k) {
+    co[2 * k] = chunk_off[k];
+    co[2 * k + 1] = chunk_end[k];
+  }
+  b->set_off = (uint32_t*)(b->in_dev + o_so);
+  b->arena = (uint32_t*)(b->in_dev + o_ar);
+  b->agg_list = (uint32_t*)(b->in_dev + o_al);
+  b->chunk_off = (uint32_t*)(b->in_dev + o_co);
+  b->siglen = (uint32_t*)(b->in_dev + o_sl);
+  b->raw_flag = b->in_dev + o_rf;
+  b->raw_pk = b->in_dev + o_rp;
+  b->msgs = b->in_dev + o_m;
+  b->sig = b->in_dev + o_sig;
+  HIP_CHECK(c, hipMemcpyAsync(b->in_dev, h, total, hipMemcpyHostToDevice, c->stream));
+  HIP_CHECK(c, hipStreamSynchronize(c->stream));  // the pinned blob is reused by the next fill
+  b->n = n;
+  b->n_calls = n_calls;
+  b->C = C;
+  b->n_agg = n_agg;
+  b->A = A;
+  b->sig_stride = stride;
+  b->call_chunk.swap(call_chunk);
+  b->call_reject.swap(reject);
+  b->chunk_off_host.swap(chunk_off);
+  return GBV_OK;
+}
+
+// Per-set kernels (aggregate, hash + signature + randomisation, Miller values) on stream A.
+static int vs_enqueue_sets(gbv_ctx* c, gbv_vs_batch* b) {
+  hipStream_t s = c->stream;
+  Seed seed = fresh_seed();
+  uint32_t nonce = c->nonce++;
+  HIP_CHECK(c, hipEventRecord(b->ev[0], s));
+  if (b->n_agg) launch_vs_agg(LaunchCfg{(unsigned)b->n_agg, 64, s}, b->agg_list, b->set_off, b->arena, c->table, c->table_ok, b->pk, b->pk_st);
+  HIP_CHECK(c, hipEventRecord(b->ev[1], s));
+  launch_vs_hash_sig(s, (uint32_t)b->n, b->msgs, b->set_off, b->arena, b->raw_flag, b->raw_pk, b->sig, b->sig_stride, b->siglen, c->table,
+                     c->table_ok, b->pk, b->pk_st, seed, nonce, b->H, b->rP, b->rS, b->status);
+  HIP_CHECK(c, hipEventRecord(b->ev[2], s));
+  launch_vs_miller(LaunchCfg{blocks_for(b->n), TPB, s}, (uint32_t)b->n, b->status, b->rP, b->H, b->F);
+  HIP_CHECK(c, hipEventRecord(b->ev[3], s));
+  HIP_CHECK(c, hipGetLastError());
+  return GBV_OK;
+}
+
+extern "C" {
+
+int gbv_vs_batch_create(gbv_ctx* c, size_t n_calls, const uint32_t* call_off, const gbv_set* sets, const uint32_t* arena,
+                        gbv_vs_batch** out) {
+  if (!c || !out) return GBV_E_ARG;
+  if (c->closed) return GBV_E_CLOSED;
+  *out = nullptr;
+  gbv_vs_batch* b = new gbv_vs_batch();
+  int rc = vs_fill(c, b, n_calls, call_off, sets, arena);
+  if (rc) {
+    vs_batch_free(b);
+    return rc;
+  }
+  *out = b;
+  return GBV_OK;
+}
+
+void gbv_vs_batch_destroy(gbv_ctx* c, gbv_vs_batch* b) {
+  (void)c;
+  vs_batch_free(b);
+}
+
+// Enqueue the whole verification without a host round trip: the per-set kernels on stream A, the
+// chunk checks on a tail stream (alternating per submit) so that they overlap the next batch's
+// per-set kernels.
+int gbv_vs_batch_submit(gbv_ctx* c, gbv_vs_batch* b) {
+  if (!c || !b) return GBV_E_ARG;
+  if (c->closed) return GBV_E_CLOSED;
+  if (b->in_flight) return gbv_fail(c, GBV_E_ARG, "batch already in flight");
+  HIP_CHECK(c, hipSetDevice(c->device));
+  if (b->n == 0 || b->C == 0) return GBV_OK;
+  int rc = vs_enqueue_sets(c, b);
+  if (rc) return rc;
+  b->tail = (int)(c->sm_submits++ & 1);
+  hipStream_t t = b->tail ? c->stream3 : c->stream2;
+  HIP_CHECK(c, hipStreamWaitEvent(t, b->ev[3], 0));
+  HIP_CHECK(c, hipEventRecord(b->ev[4], t));
+  launch_vs_chunk_coop(LaunchCfg{(unsigned)b->C, 64, t}, (uint32_t)b->C, b->chunk_off, b->status, b->F, b->rS, b->chunk_valid);
+  HIP_CHECK(c, hipEventRecord(b->ev[5], t));
+  HIP_CHECK(c, hipMemcpyAsync(b->chunk_valid_host, b->chunk_valid, b->C, hipMemcpyDeviceToHost, t));
+  HIP_CHECK(c, hipEventRecord(b->done, t));
+  HIP_CHECK(c, hipGetLastError());
+  b->in_flight = true;
+  return GBV_OK;
+}
+
+int gbv_vs_batch_wait(gbv_ctx* c, gbv_vs_batch* b, uint8_t* call_valid) {
+  if (!c || !b) return GBV_E_ARG;
+  HIP_CHECK(c, hipSetDevice(c->device));
+  if (b->in_flight) {
+    b->in_flight = false;
+    HIP_CHECK(c, hipEventSynchronize(b->done));
+    float ms[4] = {};
+    for (int k = 0; k < 4; ++k) {
+      int a = k < 3 ? k : 4;
+      if (hipEventElapsedTime(&ms[k], b->ev[a], b->ev[a + 1]) != hipSuccess) ms[k] = 0.f;
+    }
+    memcpy(c->last_vs_ms, ms, sizeof ms);
+  } else if (b->n && b->C) {
+    return gbv_fail(c, GBV_E_ARG, "batch not submitted");
+  }
+  if (call_valid)
+    for (size_t g = 0; g < b->n_calls; ++g) {
+      uint32_t k0 = b->call_chunk[g], k1 = b->call_chunk[g + 1];
+      uint8_t all = k1 > k0 ? 1 : 0;  // an empty call is false
+      for (uint32_t k = k0; k < k1; ++k) all &= b->chunk_valid_host[k];
+      call_valid[g] = b->call_reject[g] ? GBV_CALL_REJECTED : all;
+    }
+  return GBV_OK;
+}
+
+int gbv_vs_last_kernel_ms(gbv_ctx* c, float* ms4) {
+  if (!c || !ms4) return GBV_E_ARG;
+  memcpy(ms4, c->last_vs_ms, sizeof c->last_vs_ms);
+  return GBV_OK;
+}
+
+static gbv_vs_batch* scratch(gbv_ctx* c) {
+  if (!c->vs_scratch) c->vs_scratch = new gbv_vs_batch();
+  return c->vs_scratch;
+}
+
+int gbv_verify_sets_multi(gbv_ctx* c, size_t n_calls, const uint32_t* call_off, const gbv_set* sets, const uint32_t* arena,
+                          uint8_t* call_valid) {
+  if (!c || (n_calls && !call_valid)) return GBV_E_ARG;
+  if (c->closed) return GBV_E_CLOSED;
+  gbv_vs_batch* b = scratch(c);
+  int rc = vs_fill(c, b, n_calls, call_off, sets, arena);
+  if (rc) return rc;
+  if ((rc = gbv_vs_batch_submit(c, b))) return rc;
+  return gbv_vs_batch_wait(c, b, call_valid);
+}
+
+int gbv_verify_sets(gbv_ctx* c, const gbv_set* sets, size_t n, const uint32_t* arena, uint8_t* all_valid, uint8_t* chunk_valid) {
+  if (!c || !all_valid) return GBV_E_ARG;
+  if (c->closed) return GBV_E_CLOSED;
+  *all_valid = 0;
+  uint32_t off[2] = {0, (uint32_t)n};
+  gbv_vs_batch* b = scratch(c);
+  int rc = vs_fill(c, b, 1, off, sets, arena);
+  if (rc) return rc;
+  // aggregatePublicKeys([]) throws before any verification: the call rejects (index.ts:398-412)
+  if (b->call_reject[0]) return gbv_fail(c, GBV_E_EMPTY_AGGREGATE, "EMPTY_AGGREGATE_ARRAY");
+  if ((rc = gbv_vs_batch_submit(c, b))) return rc;
+  uint8_t v = 0;
+  if ((rc = gbv_vs_batch_wait(c, b, &v))) return rc;
+  *all_valid = v;
+  if (chunk_valid) {
+    if (b->C)
+      memcpy(chunk_valid, b->chunk_valid_host, b->C);
+    else
+      chunk_valid[0] = 0;  // verifySignatureSetsMaybeBatch([]) throws -> false (maybeBatch.ts:29-31,39-44)
+  }
+  return GBV_OK;
+}
+
+// One shard of a verifySignatureSets call spread over several GPUs: the shard's sets
+// reduce to ONE Fp12 Miller product (its pairs and its own (-g1, sum r_i sig_i) pair).
+int gbv_vs_partial(gbv_ctx* c, const gbv_set* sets, size_t n, const uint32_t* arena, uint8_t out576[GBV_FP12_PARTIAL_BYTES],
+                   uint8_t* shard_ok) {
+  if (!c || !out576 || !shard_ok) return GBV_E_ARG;
+  if (c->closed) return GBV_E_CLOSED;
+  *shard_ok = 1;
+  uint32_t off[2] = {0, (uint32_t)n};
+  gbv_vs_batch* b = scratch(c);
+  int rc = vs_fill(c, b, 1, off, sets, arena);
+  if (rc) return rc;
+  if (b->call_reject[0]) return gbv_fail(c, GBV_E_EMPTY_AGGREGATE, "EMPTY_AGGREGATE_ARRAY");
+  if (n == 0) {
+    fp12_pack(out576, fp12_one_host());
+    return GBV_OK;
+  }
+  size_t np = seg_reduce_scratch(n);
+  if (b->part_cap < np) {
+    hipFree(b->Fpart); hipFree(b->Spart); hipFree(b->has); hipFree(b->f_out); hipFree(b->flag);
+    b->Fpart = nullptr; b->Spart = nullptr; b->has = nullptr; b->f_out = nullptr; b->flag = nullptr;
+    b->part_cap = 0;
+    HIP_CHECK(c, dalloc(&b->Fpart, np)); HIP_CHECK(c, dalloc(&b->Spart, np)); HIP_CHECK(c, dalloc(&b->has, np));
+    HIP_CHECK(c, dalloc(&b->f_out, 1)); HIP_CHECK(c, dalloc(&b->flag, 1));
+    b->part_cap = np;
+  }
+  HIP_CHECK(c, hipSetDevice(c->device));
+  if ((rc = vs_enqueue_sets(c, b))) return rc;
+  hipStream_t s = c->stream;
+  // status doubles as the per-"chunk" state: SET_OK == GRP_PENDING (every valid set takes part);
+  // the reduction is a tree over 64-set blocks (k_sm_seg_reduce, k_sm_part_reduce)
+  launch_sm_seg_check(LaunchCfg{1, 64, s}, 0, (uint32_t)n, b->status, b->F, b->rS, b->Fpart, b->Spart, b->has, b->flag, b->f_out);
+  HIP_CHECK(c, hipGetLastError());
+  uint8_t* h = nullptr;
+  if ((rc = ctx_small_host(c, sizeof(Fp12) + n, &h))) return rc;
+  HIP_CHECK(c, hipMemcpyAsync(h, b->f_out, sizeof(Fp12), hipMemcpyDeviceToHost, s));
+  HIP_CHECK(c, hipMemcpyAsync(h + sizeof(Fp12), b->status, n, hipMemcpyDeviceToHost, s));
+  HIP_CHECK(c, hipStreamSynchronize(s));
+  Fp12 f;
+  memcpy((void*)&f, h, sizeof(Fp12));
+  fp12_pack(out576, f);
+  for (size_t i = 0; i < n; ++i)
+    if (h[sizeof(Fp12) + i] != SET_OK) *shard_ok = 0;
+  return GBV_OK;
+}
+
+int gbv_fp12_check(gbv_ctx* c, const uint8_t* partials, size_t k, uint8_t* is_one) {
+  if (!c || !is_one || (k && !partials)) return GBV_E_ARG;
+  if (c->closed) return GBV_E_CLOSED;
+  HIP_CHECK(c, hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  uint8_t *d = nullptr, *h = nullptr;
+  size_t o_o = align256(sizeof(Fp12) * std::max<size_t>(k, 1));
+  int rc;
+  if ((rc = ctx_small_dev(c, o_o + 256, &d)) || (rc = ctx_small_host(c, o_o + 256, &h))) return rc;
+  for (size_t j = 0; j < k; ++j) {
+    Fp12 f = fp12_unpack(partials + GBV_FP12_PARTIAL_BYTES * j);
+    memcpy(h + sizeof(Fp12) * j, (const void*)&f, sizeof(Fp12));
+  }
+  if (k) HIP_CHECK(c, hipMemcpyAsync(d, h, sizeof(Fp12) * k, hipMemcpyHostToDevice, s));
+  launch_fp12_check(LaunchCfg{1, 64, s}, (uint32_t)k, (const Fp12*)d, d + o_o);
+  HIP_CHECK(c, hipGetLastError());
+  HIP_CHECK(c, hipMemcpyAsync(h + o_o, d + o_o, 1, hipMemcpyDeviceToHost, s));
+  HIP_CHECK(c, hipStreamSynchronize(s));
+  *is_one = h[o_o];
+  return GBV_OK;
+}
+
+}  // extern "C"

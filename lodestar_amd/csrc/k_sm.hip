@@ -85,13 +85,16 @@ __global__ void GBV_KERNEL_ATTR k_sm_prepare(uint32_t base, uint32_t n, const ui
 }
 
 // The G2 half of k_sm_prepare for a segment whose fast check used the bucket MSM (k_msm.hip) and
-// FAILED: the failure path needs the per-set r_i sig_i group sums (Sh) and the chunk sums S_g
-// after all.  Same r_i (prf_scalar of the same seed/nonce/index), same 8-lane scan, so Sh/S_g are
+// FAILED (or holds a chunk bound for the per-set path): the failure path needs the per-set
+// r_i sig_i group sums (Sh) and the chunk sums S_g after all.  Same r_i (prf_scalar of the same seed/nonce/index), same 8-lane scan, so Sh/S_g are
 // exactly what k_sm_prepare<true> would have written.  Exits at once when the segment passed.
 __global__ void GBV_KERNEL_ATTR k_sm_redo_g2(uint32_t base, uint32_t n, const uint32_t* __restrict__ set_grp,
                                              const uint8_t* __restrict__ status, const G2A* __restrict__ S, Seed seed, uint32_t nonce,
-                                             const uint8_t* __restrict__ seg_ok, G2J* __restrict__ Sh_out) {
-  if (*seg_ok) return;
+                                             const uint8_t* __restrict__ seg_ok, const uint32_t* __restrict__ n_fallback,
+                                             G2J* __restrict__ Sh_out) {
+  // a passing segment still needs the per-set terms when one of its chunks went to the per-set
+  // path (malformed / non-subgroup signature): the run checks read Sh (k_sm_fb_blocks*)
+  if (*seg_ok && *n_fallback == 0) return;
   unsigned lane = threadIdx.x;
   uint32_t t = blockIdx.x * 64 + lane;
   bool act = t < n;
@@ -375,8 +378,9 @@ void launch_sm_prepare(LaunchCfg c, uint32_t base, uint32_t n, const uint32_t* i
   debug_sync(c.stream, "k_sm_prepare");
 }
 void launch_sm_redo_g2(LaunchCfg c, uint32_t base, uint32_t n, const uint32_t* set_grp, const uint8_t* status, const G2A* S, const Seed& seed,
-                       uint32_t nonce, const uint8_t* seg_ok, G2J* Sh) {
-  hipLaunchKernelGGL(k_sm_redo_g2, dim3((n + 63) / 64), dim3(64), 0, c.stream, base, n, set_grp, status, S, seed, nonce, seg_ok, Sh);
+                       uint32_t nonce, const uint8_t* seg_ok, const uint32_t* n_fallback, G2J* Sh) {
+  hipLaunchKernelGGL(k_sm_redo_g2, dim3((n + 63) / 64), dim3(64), 0, c.stream, base, n, set_grp, status, S, seed, nonce, seg_ok, n_fallback,
+                     Sh);
   debug_sync(c.stream, "k_sm_redo_g2");
 }
 void launch_sm_chunk_finish_s(LaunchCfg c, uint32_t g0, uint32_t G, uint32_t s0, const uint32_t* grp_off, const uint8_t* grp_state,

@@ -273,11 +273,11 @@ k_fp12_check(uint32_t k, const Fp12* __restrict__ parts, uint8_t* __restrict__ o
   if (lane == 0) out[0] = ok ? 1 : 0;
 }
 
-// verifySignatureSets chunks (<= 255 sets each, chunkifyMaximizeChunkSize): one wave per chunk
+// verifySignatureSets chunks (<= 255 sets each, chunkifyMaximizeChunkSize; (begin, end) pairs): one wave per chunk
 // multiplies its sets' Miller values and sums r_i sig_i (cross-lane tree), then runs the
 // (-g1, sum) pair and the final exponentiation cooperatively (maybeBatch.ts:17-26).
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
-k_vs_chunk_coop(const uint32_t* __restrict__ chunk_off, const uint8_t* __restrict__ status, const Fp12* __restrict__ f,
+k_vs_chunk_coop(const uint32_t* __restrict__ chunk_be, const uint8_t* __restrict__ status, const Fp12* __restrict__ f,
                 const G2J* __restrict__ rS, uint8_t* __restrict__ chunk_valid) {
   __shared__ Fp ws[SEG_WS];
   __shared__ int flags[2];
@@ -285,7 +285,7 @@ k_vs_chunk_coop(const uint32_t* __restrict__ chunk_off, const uint8_t* __restric
   Fp* fe = ws + coop::MILLER_WS;
   unsigned lane = threadIdx.x;
   uint32_t c = blockIdx.x;
-  uint32_t b = chunk_off[c], e = chunk_off[c + 1];
+  uint32_t b = chunk_be[2 * c], e = chunk_be[2 * c + 1];
   int bad = b == e;
   int any = 0;
   Fp12 acc = fp12_one();
@@ -331,9 +331,9 @@ void launch_fp12_check(LaunchCfg c, uint32_t k, const Fp12* parts, uint8_t* out)
   hipLaunchKernelGGL(k_fp12_check, dim3(1), dim3(64), 0, c.stream, k, parts, out);
   debug_sync(c.stream, "k_fp12_check");
 }
-void launch_vs_chunk_coop(LaunchCfg c, uint32_t C, const uint32_t* chunk_off, const uint8_t* status, const Fp12* f, const G2J* rS,
+void launch_vs_chunk_coop(LaunchCfg c, uint32_t C, const uint32_t* chunk_be, const uint8_t* status, const Fp12* f, const G2J* rS,
                           uint8_t* chunk_valid) {
-  hipLaunchKernelGGL(k_vs_chunk_coop, dim3(C), dim3(64), 0, c.stream, chunk_off, status, f, rS, chunk_valid);
+  hipLaunchKernelGGL(k_vs_chunk_coop, dim3(C), dim3(64), 0, c.stream, chunk_be, status, f, rS, chunk_valid);
   debug_sync(c.stream, "k_vs_chunk_coop");
 }
 }  // namespace gbv

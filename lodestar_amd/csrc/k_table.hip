@@ -31,7 +31,8 @@ __global__ void k_pk_replicate(G1A* __restrict__ table, uint8_t* __restrict__ ta
   table_ok[dst_first + i] = table_ok[s];
 }
 
-// aggregatePublicKeys over an index list: one 256-thread block, strided partial sums + LDS tree.
+// aggregatePublicKeys over an index list (idx == nullptr: table slots 0..k-1, the serialized-key
+// form): one 256-thread block, strided partial sums + LDS tree.
 __global__ void __launch_bounds__(256) k_aggregate(const uint32_t* __restrict__ idx, uint32_t k, const G1A* __restrict__ table,
                                                    const uint8_t* __restrict__ table_ok, uint8_t* __restrict__ out48,
                                                    uint32_t* __restrict__ bad) {
@@ -39,8 +40,11 @@ __global__ void __launch_bounds__(256) k_aggregate(const uint32_t* __restrict__ 
   uint32_t t = threadIdx.x;
   G1J acc = jac_infinity<Fp>();
   for (uint32_t i = t; i < k; i += 256) {
-    uint32_t j = idx[i];
-    if (!table_ok[j]) atomicOr(bad, 1u);
+    uint32_t j = idx ? idx[i] : i;
+    if (!table_ok[j]) {
+      if (idx) atomicOr(bad, 1u);
+      if (!idx) continue;  // serialized key that decoded to infinity: contributes nothing
+    }
     acc = jac_add_aff(acc, table[j]);
   }
   part[t] = acc;

@@ -1,36 +1,92 @@
-// Distinct-message path kernels (verifySignatureSets).
+// Distinct-message path kernels (verifySignatureSets, maybeBatch.ts:15-45), batched over many calls.
 #include "launch.h"
 #include "kernel_common.h"
 
 namespace gbv {
 
-// ---- distinct-message path (verifySignatureSets) ------------------------------------------------
-__global__ void GBV_KERNEL_ATTR k_vs_prepare(uint32_t n, const uint32_t* __restrict__ set_idx_off, const uint32_t* __restrict__ idx,
-                                                   const uint8_t* __restrict__ raw_flag, const uint8_t* __restrict__ raw_pk48,
-                                                   const uint8_t* __restrict__ msgs32, const uint8_t* __restrict__ sig, uint32_t sig_stride,
-                                                   const uint32_t* __restrict__ sig_len, const G1A* __restrict__ table,
-                                                   const uint8_t* __restrict__ table_ok, Seed seed, uint32_t nonce,
-                                                   Fp12* __restrict__ f_out, G2J* __restrict__ rS_out, uint8_t* __restrict__ status) {
-  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+GBV_NI G1J vs_g1_add(G1J a, G1J b) { return jac_add(a, b); }
+GBV_NI G1J vs_g1_add_aff(G1J a, G1A b) { return jac_add_aff(a, b); }
+
+__device__ inline Fp vs_shfl_down(const Fp& a, unsigned d) {
+  Fp r;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) r.v[i] = __shfl_down((unsigned)a.v[i], d, 64);
+  return r;
+}
+
+// aggregatePublicKeys over one set's validator indices (bls/utils.ts:5-20, jobItem.ts:55-62): one
+// wave per aggregate set.  Lane l gathers table entries l, l+64, ... (each lane reads its own
+// 128-byte affine record; a 128-member committee is two records per lane) and adds them, then a
+// 6-level cross-lane tree (ds_bpermute shuffles) sums the lanes.  Critical path for k = 128: 2
+// mixed additions + 6 full additions + 1 inversion, instead of 128 serial additions in one lane.
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
+k_vs_agg(const uint32_t* __restrict__ agg_list, const uint32_t* __restrict__ set_off, const uint32_t* __restrict__ arena,
+         const G1A* __restrict__ table, const uint8_t* __restrict__ table_ok, G1A* __restrict__ pk_out, uint8_t* __restrict__ pk_st) {
+  const uint32_t s = agg_list[blockIdx.x];
+  const uint32_t b = set_off[s], e = set_off[s + 1];
+  const unsigned lane = threadIdx.x;
+  G1J acc = jac_infinity<Fp>();
+  int bad = 0;
+  for (uint32_t j = b + lane; j < e; j += 64) {
+    uint32_t k = arena[j];
+    bad |= table_ok[k] ? 0 : 1;
+    acc = vs_g1_add_aff(acc, table[k]);
+  }
+  for (unsigned d = 32; d >= 1; d >>= 1) {
+    G1J o{vs_shfl_down(acc.x, d), vs_shfl_down(acc.y, d), vs_shfl_down(acc.z, d)};
+    if (lane < d) acc = vs_g1_add(acc, o);
+  }
+  bad = __any(bad);
+  if (lane == 0) {
+    G1A a;
+    bool fin = jac_to_aff(a, acc);
+    pk_out[s] = a;
+    // an infinity aggregate fails verification in blst; an invalid table slot never verifies
+    pk_st[s] = (bad || !fin) ? SET_BAD_PK : SET_OK;
+  }
+}
+
+// Two block roles in one launch (wave-uniform, no divergence): blocks [0, nb) hash the signing
+// roots; blocks [nb, 2 nb) decode and group-check the signatures (Signature.fromBytes(sig, true),
+// maybeBatch.ts:23), fetch the pubkey (table slot, the k_vs_agg result, or a raw key validated like
+// PublicKey.fromBytes(pk, true), blsToExecutionChange.ts:31) and form r_i pk_i and r_i sig_i.
+// The two roles are independent, so hashing (the longest per-set chain) overlaps the rest.
+__global__ void GBV_KERNEL_ATTR k_vs_hash_sig(uint32_t n, uint32_t nb, const uint8_t* __restrict__ msgs32,
+                                              const uint32_t* __restrict__ set_off, const uint32_t* __restrict__ arena,
+                                              const uint8_t* __restrict__ raw_flag, const uint8_t* __restrict__ raw_pk48,
+                                              const uint8_t* __restrict__ sig, uint32_t sig_stride, const uint32_t* __restrict__ sig_len,
+                                              const G1A* __restrict__ table, const uint8_t* __restrict__ table_ok,
+                                              const G1A* __restrict__ pk_agg, const uint8_t* __restrict__ pk_st, Seed seed, uint32_t nonce,
+                                              G2A* __restrict__ H, G1J* __restrict__ rP_out, G2J* __restrict__ rS_out,
+                                              uint8_t* __restrict__ status) {
+  if (blockIdx.x < nb) {
+    uint32_t i = blockIdx.x * 64 + threadIdx.x;
+    if (i >= n) return;
+    uint32_t w[8];
+    load_msg_words(w, msgs32 + 32ull * i);
+    H[i] = hash_to_g2(w);
+    return;
+  }
+  uint32_t i = (blockIdx.x - nb) * 64 + threadIdx.x;
   if (i >= n) return;
   uint8_t st = SET_OK;
-  // public key: raw (validated like PublicKey.fromBytes(pk, true)) or aggregate of table entries
   G1A pk;
-  bool pk_inf = false;
   if (raw_flag[i]) {
     uint8_t ds = g1_decompress(pk, raw_pk48 + 48ull * i);
     if (ds != PT_OK || !g1_in_subgroup(pk)) st = SET_BAD_PK;
   } else {
-    uint32_t b = set_idx_off[i], e = set_idx_off[i + 1];
-    G1J acc = jac_infinity<Fp>();
-    for (uint32_t j = b; j < e; ++j) {
-      uint32_t k = idx[j];
+    uint32_t b = set_off[i], e = set_off[i + 1];
+    if (e - b == 1) {
+      uint32_t k = arena[b];
+      pk = table[k];
       if (!table_ok[k]) st = SET_BAD_PK;
-      acc = jac_add_aff(acc, table[k]);
+    } else if (e == b) {
+      st = SET_BAD_PK;  // empty aggregate: its call is rejected on the host, never verified
+    } else {
+      pk = pk_agg[i];
+      if (pk_st[i] != SET_OK) st = SET_BAD_PK;
     }
-    pk_inf = !jac_to_aff(pk, acc);
   }
-  if (pk_inf) st = SET_BAD_PK;  // verify with an infinity pubkey fails in blst
   G2A s;
   uint8_t ds = g2_decode(s, sig + (size_t)sig_stride * i, sig_len[i]);
   if (ds != PT_OK || !g2_in_subgroup(s)) st = SET_BAD_SIG;
@@ -43,19 +99,59 @@ __global__ void GBV_KERNEL_ATTR k_vs_prepare(uint32_t n, const uint32_t* __restr
     rs = g2_mul_u64(s, r);
     rp = g1_mul_u64(pk, r);
   }
+  rP_out[i] = rp;
   rS_out[i] = rs;
-  uint32_t w[8];
-  load_msg_words(w, msgs32 + 32ull * i);
-  G2A h = hash_to_g2(w);
-  f_out[i] = miller_loop_1j(rp, h);
 }
 
-void launch_vs_prepare(LaunchCfg c, uint32_t n, const uint32_t* set_idx_off, const uint32_t* idx, const uint8_t* raw_flag,
-                       const uint8_t* raw_pk48, const uint8_t* msgs32, const uint8_t* sig, uint32_t sig_stride, const uint32_t* sig_len,
-                       const G1A* table, const uint8_t* table_ok, const Seed& seed, uint32_t nonce, Fp12* f_out, G2J* rS_out,
-                       uint8_t* status) {
-  hipLaunchKernelGGL(k_vs_prepare, dim3(c.blocks), dim3(c.threads), 0, c.stream, n, set_idx_off, idx, raw_flag, raw_pk48, msgs32, sig,
-                     sig_stride, sig_len, table, table_ok, seed, nonce, f_out, rS_out, status);
-  debug_sync(c.stream, "k_vs_prepare");
+// Miller value f_{|x|, H(m_i)}(r_i pk_i) of every set that decoded (P Jacobian: the lines carry a
+// Z^3 factor that the final exponentiation removes).
+__global__ void GBV_KERNEL_ATTR k_vs_miller(uint32_t n, const uint8_t* __restrict__ status, const G1J* __restrict__ rP,
+                                            const G2A* __restrict__ H, Fp12* __restrict__ F) {
+  uint32_t i = blockIdx.x * 64 + threadIdx.x;
+  if (i >= n || status[i] != SET_OK) return;
+  F[i] = miller_loop_1j(rP[i], H[i]);
+}
+
+// Signature.fromBytes(sig, true) (maybeBatch.ts:23; the "BLS deserializing signatures" perf id,
+// test/perf/bls/bls.test.ts:89-100): decode + subgroup check, and the recompressed encoding of
+// every accepted point (byte-identical to the input for canonical compressed signatures).
+__global__ void GBV_KERNEL_ATTR k_sig_validate(uint32_t n, const uint8_t* __restrict__ sig, uint32_t sig_len, uint8_t* __restrict__ status,
+                                               uint8_t* __restrict__ out96) {
+  uint32_t i = blockIdx.x * 64 + threadIdx.x;
+  if (i >= n) return;
+  G2A s;
+  uint8_t st = g2_decode(s, sig + (size_t)sig_len * i, sig_len);
+  if (st == PT_OK && !g2_in_subgroup(s)) st = PT_NOT_IN_GROUP;
+  status[i] = st;
+  if (st == PT_OK)
+    g2_compress(out96 + 96ull * i, s, false);
+  else
+    g2_compress(out96 + 96ull * i, s, true);  // infinity encoding as the placeholder of a rejected input
+}
+
+void launch_vs_agg(LaunchCfg c, const uint32_t* agg_list, const uint32_t* set_off, const uint32_t* arena, const G1A* table,
+                   const uint8_t* table_ok, G1A* pk_out, uint8_t* pk_st) {
+  hipLaunchKernelGGL(k_vs_agg, dim3(c.blocks), dim3(64), 0, c.stream, agg_list, set_off, arena, table, table_ok, pk_out, pk_st);
+  debug_sync(c.stream, "k_vs_agg");
+}
+
+void launch_vs_hash_sig(hipStream_t s, uint32_t n, const uint8_t* msgs32, const uint32_t* set_off, const uint32_t* arena,
+                        const uint8_t* raw_flag, const uint8_t* raw_pk48, const uint8_t* sig, uint32_t sig_stride, const uint32_t* sig_len,
+                        const G1A* table, const uint8_t* table_ok, const G1A* pk_agg, const uint8_t* pk_st, const Seed& seed,
+                        uint32_t nonce, G2A* H, G1J* rP, G2J* rS, uint8_t* status) {
+  uint32_t nb = (n + 63) / 64;
+  hipLaunchKernelGGL(k_vs_hash_sig, dim3(2 * nb), dim3(64), 0, s, n, nb, msgs32, set_off, arena, raw_flag, raw_pk48, sig, sig_stride,
+                     sig_len, table, table_ok, pk_agg, pk_st, seed, nonce, H, rP, rS, status);
+  debug_sync(s, "k_vs_hash_sig");
+}
+
+void launch_vs_miller(LaunchCfg c, uint32_t n, const uint8_t* status, const G1J* rP, const G2A* H, Fp12* F) {
+  hipLaunchKernelGGL(k_vs_miller, dim3(c.blocks), dim3(64), 0, c.stream, n, status, rP, H, F);
+  debug_sync(c.stream, "k_vs_miller");
+}
+
+void launch_sig_validate(LaunchCfg c, uint32_t n, const uint8_t* sig, uint32_t sig_len, uint8_t* status, uint8_t* out96) {
+  hipLaunchKernelGGL(k_sig_validate, dim3(c.blocks), dim3(64), 0, c.stream, n, sig, sig_len, status, out96);
+  debug_sync(c.stream, "k_sig_validate");
 }
 }  // namespace gbv

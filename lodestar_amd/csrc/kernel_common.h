@@ -13,8 +13,10 @@
 //   k_sm_group_pairing  verify(msg, aggPk, aggSig) of the chunk (worker.ts:29-107 -> maybeBatch n = 1),
 //                       only for chunks of a failing segment
 //   k_sm_fallback       retry each set individually (jobItem.ts:93-125)
-//   k_vs_prepare        per-set part of verifyMultipleAggregateSignatures (+ aggregatePublicKeys
-//                       of index lists, bls/utils.ts:5-20)
+//   k_vs_agg            aggregatePublicKeys of index lists (bls/utils.ts:5-20), one wave per set
+//   k_vs_hash_sig       per-set part of verifyMultipleAggregateSignatures: hash_to_G2 | decode,
+//                       subgroup check, randomisation (two block roles of one launch)
+//   k_vs_miller         per-set Miller values
 //   k_vs_chunk_coop     per-chunk multi-pairing product + one final exponentiation, one wave per chunk
 //                       (maybeBatch.ts:17-26)
 //   k_fp12_check        product of per-GPU Miller partials + one final exponentiation (multi-GPU)

@@ -23,8 +23,9 @@ uint32_t launch_sm_seg_reduce(LaunchCfg c, uint32_t g0, uint32_t G, const uint8_
                               G2J* Spart, uint8_t* has, uint32_t* n_out);
 void launch_sm_seg_check(LaunchCfg c, uint32_t g0, uint32_t G, uint8_t* grp_state, const Fp12* F, const G2J* SgJ, Fp12* Fpart, G2J* Spart,
                          uint8_t* has, uint8_t* seg_ok, Fp12* miller_out = nullptr, const G2J* S_extra = nullptr);
+// runs when the segment check failed or any chunk went to the per-set path (n_fallback > 0)
 void launch_sm_redo_g2(LaunchCfg c, uint32_t base, uint32_t n, const uint32_t* set_grp, const uint8_t* status, const G2A* S, const Seed& seed,
-                       uint32_t nonce, const uint8_t* seg_ok, G2J* Sh);
+                       uint32_t nonce, const uint8_t* seg_ok, const uint32_t* n_fallback, G2J* Sh);
 void launch_sm_chunk_finish_s(LaunchCfg c, uint32_t g0, uint32_t G, uint32_t s0, const uint32_t* grp_off, const uint8_t* grp_state,
                               const G2J* Sh, const uint8_t* seg_ok, G2J* SgJ);
 // Bucket MSM of a same-message segment: total = sum over its sets with status OK in pending chunks
@@ -42,7 +43,8 @@ void launch_msm_g2_buckets(hipStream_t s, uint32_t s0, uint32_t n, const uint32_
 // latency part (tail stream): slice running sums and the tree sum into *total
 void launch_msm_g2_reduce(hipStream_t s, const G2J* buckets, G2J* part, G2J* total);
 void launch_fp12_check(LaunchCfg c, uint32_t k, const Fp12* parts, uint8_t* out);
-void launch_vs_chunk_coop(LaunchCfg c, uint32_t C, const uint32_t* chunk_off, const uint8_t* status, const Fp12* f, const G2J* rS,
+// chunk_be: (begin, end) set range of each of the C chunks
+void launch_vs_chunk_coop(LaunchCfg c, uint32_t C, const uint32_t* chunk_be, const uint8_t* status, const Fp12* f, const G2J* rS,
                           uint8_t* chunk_valid);
 void launch_sm_group_pairing(LaunchCfg c, uint32_t g0, uint32_t G, const uint32_t* grp_msg, const G1J* PgJ, const G2J* SgJ, const G2A* H,
                              const uint8_t* seg_ok, uint8_t* grp_state, uint32_t* n_fallback);
@@ -67,15 +69,22 @@ void launch_sm_fb_sets_coop(LaunchCfg c, const uint32_t* set_list, const uint32_
 
 void launch_pk_decompress(LaunchCfg c, uint32_t n, const uint8_t* pk48, int validate, G1A* table, uint8_t* table_ok, uint8_t* status);
 void launch_pk_replicate(LaunchCfg c, G1A* table, uint8_t* table_ok, uint32_t src_first, uint32_t src_n, uint32_t dst_first, uint32_t n);
+// idx == nullptr: entries 0..k-1 of table (serialized keys decompressed into scratch slots; slots
+// with table_ok == 0 -- infinity keys -- are skipped rather than flagged)
 void launch_aggregate(LaunchCfg c, const uint32_t* idx, uint32_t k, const G1A* table, const uint8_t* table_ok, uint8_t* out48,
                       uint32_t* bad);
 void launch_util_sk_to_pk(LaunchCfg c, uint32_t n, const uint8_t* sk32, uint8_t* pk48);
 void launch_util_sign(LaunchCfg c, uint32_t n, const uint8_t* sk32, const uint32_t* grp, const G2A* H, uint8_t* sig96);
 
-void launch_vs_prepare(LaunchCfg c, uint32_t n, const uint32_t* set_idx_off, const uint32_t* idx, const uint8_t* raw_flag,
-                       const uint8_t* raw_pk48, const uint8_t* msgs32, const uint8_t* sig, uint32_t sig_stride, const uint32_t* sig_len,
-                       const G1A* table, const uint8_t* table_ok, const Seed& seed, uint32_t nonce, Fp12* f_out, G2J* rS_out,
-                       uint8_t* status);
+// verifySignatureSets batches (k_vs.hip)
+void launch_vs_agg(LaunchCfg c, const uint32_t* agg_list, const uint32_t* set_off, const uint32_t* arena, const G1A* table,
+                   const uint8_t* table_ok, G1A* pk_out, uint8_t* pk_st);
+void launch_vs_hash_sig(hipStream_t s, uint32_t n, const uint8_t* msgs32, const uint32_t* set_off, const uint32_t* arena,
+                        const uint8_t* raw_flag, const uint8_t* raw_pk48, const uint8_t* sig, uint32_t sig_stride, const uint32_t* sig_len,
+                        const G1A* table, const uint8_t* table_ok, const G1A* pk_agg, const uint8_t* pk_st, const Seed& seed,
+                        uint32_t nonce, G2A* H, G1J* rP, G2J* rS, uint8_t* status);
+void launch_vs_miller(LaunchCfg c, uint32_t n, const uint8_t* status, const G1J* rP, const G2A* H, Fp12* F);
+void launch_sig_validate(LaunchCfg c, uint32_t n, const uint8_t* sig, uint32_t sig_len, uint8_t* status, uint8_t* out96);
 
 void launch_ssz_digest64(hipStream_t s, const uint8_t* in64, uint32_t n, uint8_t* out32);
 void launch_ssz_signing_roots(hipStream_t s, const uint8_t* roots32, uint32_t n, const uint8_t* domains32, const uint32_t* dom_idx,

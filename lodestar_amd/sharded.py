@@ -110,14 +110,24 @@ class ShardedVerifier:
         return min(self.rank * per, n_calls), min((self.rank + 1) * per, n_calls)
 
     def verify_same_message_multi(self, calls: Sequence[Tuple[Sequence[Tuple[int, bytes]], bytes]]) -> List[List[bool]]:
+        from ._native import GbvError
         lo, hi = self.calls_of(len(calls))
-        mine = self.device.verify_same_message_multi_sync(list(calls[lo:hi])) if hi > lo else []
-        # gather per-set booleans: fixed-size payload = all sets of the widest rank's slice
+        # gather per-set booleans: fixed-size payload = all sets of the widest rank's slice, plus a
+        # status byte (1 ok, 2 this rank raised) so a rank whose device call raises still joins the
+        # collective and every rank raises together instead of the others blocking in all_gather
         sizes = [len(c[0]) for c in calls]
         per = (len(calls) + self.world - 1) // self.world
         width = max((sum(sizes[r * per:(r + 1) * per]) for r in range(self.world)), default=0)
-        flat = bytes(1 if b else 0 for res in mine for b in res)
-        blobs = self._all_gather_bytes(flat + bytes(width - len(flat)), width) if width else [b""] * self.world
+        flat, status = b"", 2
+        try:
+            mine = self.device.verify_same_message_multi_sync(list(calls[lo:hi])) if hi > lo else []
+            flat = bytes(1 if b else 0 for res in mine for b in res)
+            status = 1
+        finally:
+            blobs = self._all_gather_bytes(bytes([status]) + flat + bytes(width - len(flat)), width + 1)
+        if any(b[0] != 1 for b in blobs):
+            raise GbvError(-2, "device error on a peer rank")
+        blobs = [b[1:] for b in blobs]
         out: List[List[bool]] = []
         for r in range(self.world):
             clo, chi = min(r * per, len(calls)), min((r + 1) * per, len(calls))

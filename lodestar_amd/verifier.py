@@ -35,6 +35,13 @@ MAX_BUFFERED_SIGS = 32             # multithread/index.ts:65
 MAX_BUFFER_WAIT_MS = 100           # multithread/index.ts:74
 MAX_JOBS_CAN_ACCEPT_WORK = 512     # multithread/index.ts:79
 
+# struct gbv_set as a numpy record (include/gbv.h; 40 bytes on LP64, checked against ctypes below)
+import numpy as _np  # noqa: E402
+_GBVSET_DTYPE = _np.dtype({"names": ["idx_off", "idx_len", "raw", "msg", "sig", "sig_len"],
+                           "formats": ["<u4", "<u4", "<u8", "<u8", "<u8", "<u4"],
+                           "offsets": [0, 4, 8, 16, 24, 32], "itemsize": 40})
+assert ctypes.sizeof(GbvSet) == _GBVSET_DTYPE.itemsize
+
 
 @dataclass
 class SingleSignatureSet:
@@ -102,6 +109,7 @@ class GpuBlsVerifier:
         self._jobs: List[_Job] = []
         self._buffered: Optional[dict] = None
         self._busy = 0
+        self._idle: Optional[asyncio.Event] = None  # set when a running device pass ends (close())
         self._run_scheduled = False
         self.metrics = {"total_sig_sets": 0, "batchable_sig_sets": 0, "same_message_sets": 0,
                         "device_passes": 0, "same_message_retry_sets": 0}
@@ -137,36 +145,58 @@ class GpuBlsVerifier:
 
     # ---- synchronous device calls (also the verifyOnMainThread path) ---------------------------
     def _marshal_sets(self, sets: Sequence[ISignatureSet]):
-        """ISignatureSet list -> (gbv_set array, index arena, keep-alive list) for the C ABI."""
+        """ISignatureSet list -> (gbv_set array, index arena, keep-alive list) for the C ABI.
+
+        The gbv_set records are written as one numpy structured array whose pointer fields point
+        into three concatenated byte buffers (roots, signatures, raw pubkeys): linear in the set
+        count, so 10^5-set calls marshal in well under a second."""
+        import numpy as np
         n = len(sets)
         arena: List[int] = []
-        keep = []
-        arr = (GbvSet * max(n, 1))()
+        roots, sigs, raws = [], [], []
+        sig_off = np.zeros(n, dtype=np.uint64)
+        sig_len = np.zeros(n, dtype=np.uint32)
+        raw_off = np.full(n, -1, dtype=np.int64)
+        idx_off = np.zeros(n, dtype=np.uint32)
+        idx_len = np.zeros(n, dtype=np.uint32)
+        pos = 0
         for i, s in enumerate(sets):
             root = bytes(s.signing_root)
-            sig = bytes(s.signature)
             if len(root) != 32:
                 raise ValueError("signing root must be 32 bytes")
-            keep.extend([root, sig])
-            e = arr[i]
-            e.msg32 = ctypes.cast(ctypes.c_char_p(root), ctypes.c_void_p)
-            e.sig = ctypes.cast(ctypes.c_char_p(sig), ctypes.c_void_p) if sig else None
-            e.sig_len = len(sig)
+            roots.append(root)
+            sig = bytes(s.signature)
+            sig_off[i] = pos
+            sig_len[i] = len(sig)
+            sigs.append(sig)
+            pos += len(sig)
             if isinstance(s, AggregatedSignatureSet):
-                e.idx_off, e.idx_len = len(arena), len(s.indices)
+                idx_off[i], idx_len[i] = len(arena), len(s.indices)
                 arena.extend(int(x) for x in s.indices)
             elif s.pubkey is not None:
                 pk = bytes(s.pubkey)
                 if len(pk) != 48:
                     raise ValueError("raw pubkey must be 48 bytes")
-                keep.append(pk)
-                e.raw_pk48 = ctypes.cast(ctypes.c_char_p(pk), ctypes.c_void_p)
-                e.idx_off, e.idx_len = len(arena), 0
+                raw_off[i] = 48 * len(raws)
+                raws.append(pk)
+                idx_off[i], idx_len[i] = len(arena), 0
             else:
-                e.idx_off, e.idx_len = len(arena), 1
+                idx_off[i], idx_len[i] = len(arena), 1
                 arena.append(int(s.index))
-        ar = (ctypes.c_uint32 * max(len(arena), 1))(*arena)
-        return arr, ar, keep
+        rbuf = ctypes.create_string_buffer(b"".join(roots) or b"\0")
+        sbuf = ctypes.create_string_buffer(b"".join(sigs) or b"\0")
+        pbuf = ctypes.create_string_buffer(b"".join(raws) or b"\0")
+        rec = np.zeros(max(n, 1), dtype=_GBVSET_DTYPE)
+        if n:
+            rec["idx_off"][:n] = idx_off
+            rec["idx_len"][:n] = idx_len
+            rec["msg"][:n] = ctypes.addressof(rbuf) + 32 * np.arange(n, dtype=np.uint64)
+            rec["sig"][:n] = np.where(sig_len > 0, ctypes.addressof(sbuf) + sig_off, 0)
+            rec["sig_len"][:n] = sig_len
+            rec["raw"][:n] = np.where(raw_off >= 0, ctypes.addressof(pbuf) + np.maximum(raw_off, 0).astype(np.uint64), 0)
+        ar = np.ascontiguousarray(np.asarray(arena if arena else [0], dtype=np.uint32))
+        keep = [rbuf, sbuf, pbuf, rec, ar]
+        return ctypes.cast(rec.ctypes.data, ctypes.POINTER(GbvSet)), ar.ctypes.data, keep
 
     def verify_signature_sets_sync(self, sets: Sequence[ISignatureSet]) -> bool:
         self._check_open()
@@ -176,6 +206,70 @@ class GpuBlsVerifier:
         _native.check(self._lib, self._ctx, rc)
         self.metrics["device_passes"] += 1
         return bool(allv.value)
+
+    def _marshal_calls(self, calls: Sequence[Sequence[ISignatureSet]]):
+        import numpy as np
+        off = np.zeros(len(calls) + 1, dtype=np.uint32)
+        off[1:] = np.cumsum([len(c) for c in calls]) if calls else []
+        arr, ar, keep = self._marshal_sets([s for c in calls for s in c])
+        return off, arr, ar, keep
+
+    def verify_signature_sets_multi_sync(self, calls: Sequence[Sequence[ISignatureSet]]) -> List[Union[bool, Exception]]:
+        """Many verifySignatureSets calls in ONE device pass (gbv_verify_sets_multi).  Per call: its
+        boolean, or an EmptyAggregateError instance when the call rejects (only that call)."""
+        self._check_open()
+        off, arr, ar, keep = self._marshal_calls(calls)
+        out = ctypes.create_string_buffer(max(len(calls), 1))
+        rc = self._lib.gbv_verify_sets_multi(self._ctx, len(calls), off.ctypes.data, arr, ar, out)
+        _native.check(self._lib, self._ctx, rc)
+        self.metrics["device_passes"] += 1
+        res: List[Union[bool, Exception]] = []
+        for b in out.raw[:len(calls)]:
+            res.append(EmptyAggregateError(_native.GBV_E_EMPTY_AGGREGATE, "EMPTY_AGGREGATE_ARRAY")
+                       if b == _native.GBV_CALL_REJECTED else b == 1)
+        return res
+
+    def stage_signature_sets(self, calls: Sequence[Sequence[ISignatureSet]]) -> "StagedSignatureSets":
+        """Stage many verifySignatureSets calls in HBM (gbv_vs_batch_create) for repeated
+        verification (range-sync / replay benches)."""
+        self._check_open()
+        off, arr, ar, keep = self._marshal_calls(calls)
+        h = ctypes.c_void_p()
+        rc = self._lib.gbv_vs_batch_create(self._ctx, len(calls), off.ctypes.data, arr, ar, ctypes.byref(h))
+        _native.check(self._lib, self._ctx, rc)
+        return StagedSignatureSets(self, h, len(calls))
+
+    def vs_last_kernel_ms(self) -> List[float]:
+        """Device ms of the last verifySignatureSets pass: [aggregate, hash+signature, miller, chunk checks]."""
+        buf = (ctypes.c_float * 4)()
+        _native.check(self._lib, self._ctx, self._lib.gbv_vs_last_kernel_ms(self._ctx, buf))
+        return [buf[i] for i in range(4)]
+
+    def aggregate_serialized_pubkeys(self, pubkeys: Union[bytes, Sequence[bytes]], validate: bool = False) -> bytes:
+        """aggregateSerializedPublicKeys(pubkeys).toBytes() (util/syncCommittee.ts:37), on the device."""
+        self._check_open()
+        blob = pubkeys if isinstance(pubkeys, (bytes, bytearray)) else b"".join(bytes(p) for p in pubkeys)
+        if len(blob) % 48:
+            raise ValueError("pubkeys must be 48-byte compressed points")
+        out = ctypes.create_string_buffer(48)
+        rc = self._lib.gbv_aggregate_serialized_pubkeys(self._ctx, bytes(blob) or b"\0", len(blob) // 48, 1 if validate else 0, out)
+        _native.check(self._lib, self._ctx, rc)
+        return out.raw
+
+    def signatures_validate(self, sigs: Sequence[bytes], sig_len: int = 96) -> Tuple[bytes, List[bytes]]:
+        """Signature.fromBytes(sig, true) for each signature: (GBV_PT_* status bytes, recompressed
+        96-byte encodings)."""
+        self._check_open()
+        blob = b"".join(bytes(x) for x in sigs)
+        n = len(sigs)
+        if len(blob) != n * sig_len:
+            raise ValueError("every signature must be %d bytes" % sig_len)
+        st = ctypes.create_string_buffer(max(n, 1))
+        out = ctypes.create_string_buffer(max(96 * n, 1))
+        rc = self._lib.gbv_signatures_validate(self._ctx, blob or b"\0", n, sig_len, st, out)
+        _native.check(self._lib, self._ctx, rc)
+        raw = out.raw
+        return st.raw[:n], [raw[96 * i:96 * i + 96] for i in range(n)]
 
     def verify_signature_set(self, s: ISignatureSet) -> bool:
         """Synchronous single-set verification used inside the state transition
@@ -307,16 +401,23 @@ class GpuBlsVerifier:
         return [b for r in results for b in r]
 
     async def close(self):
+        """close() of the pool (multithread/index.ts:238-259): queued and buffered jobs reject with
+        QUEUE_ABORTED; a device pass already running on the worker thread is awaited (its jobs
+        resolve normally) before the context -- streams, HBM table, buffers -- is destroyed."""
         if self._closed:
             return
         self._closed = True
         if self._buffered and self._buffered["timer"]:
             self._buffered["timer"].cancel()
-        for job in self._jobs + (self._buffered["jobs"] if self._buffered else []):
+        for job in self._jobs + (self._buffered["jobs"] + self._buffered["prio"] if self._buffered else []):
             if not job.future.done():
                 job.future.set_exception(QueueAbortedError(_native.GBV_E_CLOSED, "QUEUE_ABORTED"))
         self._jobs = []
         self._buffered = None
+        while self._busy:
+            if self._idle is None:
+                self._idle = asyncio.Event()
+            await self._idle.wait()
         self._lib.gbv_destroy(self._ctx)
         self._ctx = None
 
@@ -382,17 +483,27 @@ class GpuBlsVerifier:
                     for j in sm:
                         if not j.future.done():
                             j.future.set_exception(e)
-            for j in df:
+            if df:
+                # every queued default job in ONE device pass; each keeps its own result (a job
+                # with an invalid set fails alone, worker.ts:73-95 / multithread.test.ts:109-129)
                 try:
-                    r = await asyncio.to_thread(self.verify_signature_sets_sync, j.sets)
-                    if not j.future.done():
-                        j.future.set_result(r)
-                except Exception as e:
-                    if not j.future.done():
-                        j.future.set_exception(e)
+                    res = await asyncio.to_thread(self.verify_signature_sets_multi_sync, [j.sets for j in df])
+                    for j, r in zip(df, res):
+                        if j.future.done():
+                            continue
+                        if isinstance(r, Exception):
+                            j.future.set_exception(r)
+                        else:
+                            j.future.set_result(r)
+                except Exception as e:  # device failure rejects the whole group (index.ts:498-507)
+                    for j in df:
+                        if not j.future.done():
+                            j.future.set_exception(e)
         finally:
             self._busy -= 1
-        if self._jobs:
+            if self._busy == 0 and self._idle is not None:
+                self._idle.set()
+        if self._jobs and not self._closed:
             self._schedule()
 
     # ---- signing roots (SSZ hashing on the device) ------------------------
@@ -486,6 +597,42 @@ class GpuBlsVerifier:
         _native.check(self._lib, self._ctx, self._lib.gbv_util_hash_to_g2(self._ctx, b"".join(msgs32), n, out))
         raw = out.raw
         return [raw[192 * i:192 * i + 192] for i in range(n)]
+
+
+class StagedSignatureSets:
+    """Handle of a gbv_vs_batch (device-resident verifySignatureSets calls)."""
+
+    def __init__(self, verifier: GpuBlsVerifier, handle: ctypes.c_void_p, n_calls: int):
+        self._v = verifier
+        self._h = handle
+        self.n_calls = n_calls
+
+    def submit(self):
+        v = self._v
+        _native.check(v._lib, v._ctx, v._lib.gbv_vs_batch_submit(v._ctx, self._h))
+
+    def wait(self) -> List[int]:
+        """Per call: 1 true, 0 false, 2 (GBV_CALL_REJECTED) rejected."""
+        v = self._v
+        out = ctypes.create_string_buffer(max(self.n_calls, 1))
+        _native.check(v._lib, v._ctx, v._lib.gbv_vs_batch_wait(v._ctx, self._h, out))
+        v.metrics["device_passes"] += 1
+        return list(out.raw[:self.n_calls])
+
+    def verify(self) -> List[int]:
+        self.submit()
+        return self.wait()
+
+    def close(self):
+        if self._h:
+            self._v._lib.gbv_vs_batch_destroy(self._v._ctx, self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class StagedSameMessage:

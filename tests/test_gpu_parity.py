@@ -104,3 +104,66 @@ def test_async_interface(v):
         return await asyncio.gather(a, b)
     ra, rb = asyncio.run(go())
     assert ra == case["expected"] and rb == sm["expected"]
+
+
+def test_verify_sets_multi_one_pass(v):
+    """Every verify_sets fixture as one call of ONE device pass (gbv_verify_sets_multi): each call
+    keeps its own answer, and the call with an empty aggregate rejects alone."""
+    from lodestar_amd import EmptyAggregateError
+    cases = FIX["verify_sets"]
+    res = v.verify_signature_sets_multi_sync([_sets(c) for c in cases])
+    for c, r in zip(cases, res):
+        if c["expected"] == "reject":
+            assert isinstance(r, EmptyAggregateError), c["name"]
+        else:
+            assert r == c["expected"], c["name"]
+
+
+def test_staged_signature_sets_reverify(v):
+    """gbv_vs_batch: the same staged calls verified three times (fresh random scalars each time)."""
+    cases = [c for c in FIX["verify_sets"] if c["expected"] != "reject"]
+    st = v.stage_signature_sets([_sets(c) for c in cases])
+    try:
+        want = [1 if c["expected"] else 0 for c in cases]
+        for _ in range(3):
+            assert st.verify() == want
+        ms = v.vs_last_kernel_ms()
+        assert len(ms) == 4 and ms[1] > 0
+    finally:
+        st.close()
+
+
+@pytest.mark.parametrize("case", FIX["aggregate_pubkeys"], ids=lambda c: str(c["indices"]))
+def test_aggregate_serialized_pubkeys_fixture(v, case):
+    """aggregateSerializedPublicKeys (syncCommittee.ts:37) over the same keys as bytes."""
+    pks = [bytes.fromhex(FIX["keys"]["pks"][i]) for i in case["indices"]]
+    assert v.aggregate_serialized_pubkeys(pks).hex() == case["expected"]
+    assert v.aggregate_serialized_pubkeys(pks, validate=True).hex() == case["expected"]
+
+
+def test_aggregate_serialized_pubkeys_errors(v):
+    from lodestar_amd import EmptyAggregateError
+    from lodestar_amd._native import BadPointError
+    pk0 = bytes.fromhex(FIX["keys"]["pks"][0])
+    with pytest.raises(EmptyAggregateError):
+        v.aggregate_serialized_pubkeys([])
+    with pytest.raises(BadPointError):
+        v.aggregate_serialized_pubkeys([pk0, bytes(48)])  # no compression flag
+    inf = bytes([0xC0]) + bytes(47)
+    # infinity deserializes without validation and contributes nothing; validation rejects it
+    assert v.aggregate_serialized_pubkeys([pk0, inf]) == pk0
+    with pytest.raises(BadPointError):
+        v.aggregate_serialized_pubkeys([pk0, inf], validate=True)
+
+
+def test_signatures_validate_recompresses(v):
+    """Signature.fromBytes(sig, true): accepted signatures recompress byte-identically; the
+    malformed / infinity encodings of the fixtures are rejected with their blst error class."""
+    sigs = [bytes.fromhex(s["sig"]) for c in FIX["verify_sets"] for s in c["sets"] if len(s["sig"]) == 192]
+    st, out = v.signatures_validate(sigs)
+    good = [i for i in range(len(sigs)) if st[i] == 0]
+    assert len(good) >= len(sigs) // 2
+    for i in good:
+        assert out[i] == sigs[i]
+    st, _ = v.signatures_validate([bytes([10]) * 96, bytes([0xC0]) + bytes(95), bytes(96)])
+    assert list(st) == [1, 4, 1]  # GBV_PT_BAD_ENCODING, GBV_PT_INFINITY, GBV_PT_BAD_ENCODING

@@ -117,6 +117,20 @@ def _worker(rank, world, port, q):
         good = [(i, O.g2_compress(O.sign(sks[i], msg))) for i in range(4)]
         calls = [(good[:2], msg), ([good[2], (3, bytes([10]) * 96)], msg), ([(0, good[1][1])], msg)]
         res["sm"] = sv.verify_same_message_multi(calls)
+        # a device error on ONE rank (e.g. an index out of range there) must raise on every rank,
+        # not leave the other rank blocked in the all-gather
+        from lodestar_amd import GbvError
+
+        class RaisingOnRank1(OracleDevice):
+            def verify_same_message_multi_sync(self, calls):
+                if rank == 1:
+                    raise GbvError(-1, "validator index out of range")
+                return super().verify_same_message_multi_sync(calls)
+        try:
+            ShardedVerifier(RaisingOnRank1(pks)).verify_same_message_multi(calls)
+            res["sm_err"] = "no error"
+        except GbvError:
+            res["sm_err"] = "raised"
         q.put((rank, res))
     finally:
         dist.destroy_process_group()
@@ -155,6 +169,7 @@ def test_sharded_world2_gloo():
         assert r["valid"] is True and r["wrong_msg"] is False and r["malformed"] is False
         assert r["empty"] is False and r["empty_agg"] == "rejected"
         assert r["sm"] == [[True, True], [True, False], [False]]
+        assert r["sm_err"] == "raised"
     # the two shards partition the call
     assert out[0]["shard"][0] == 0 and out[0]["shard"][1] == out[1]["shard"][0] and out[1]["shard"][1] == 5
     # and the answers match the oracle's restatement of the reference pool

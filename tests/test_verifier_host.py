@@ -21,20 +21,28 @@ class Recorder(GpuBlsVerifier):
         self._jobs = []
         self._buffered = None
         self._busy = 0
+        self._idle = None
         self._run_scheduled = False
+        self.destroyed_after = None
         self.metrics = {"total_sig_sets": 0, "batchable_sig_sets": 0, "same_message_sets": 0,
                         "device_passes": 0, "same_message_retry_sets": 0}
         self.passes = []
 
+        rec = self
+
         class _Lib:
             def gbv_destroy(self, ctx):
-                pass
+                rec.destroyed_after = list(rec.passes)
         self._lib = _Lib()
         self._ctx = None
 
     def verify_signature_sets_sync(self, sets):
         self.passes.append(("sets", len(sets)))
         return len(sets) > 0 and all(bytes(s.signature)[:1] == b"\x01" for s in sets)
+
+    def verify_signature_sets_multi_sync(self, calls):
+        self.passes.append(("multi", [len(c) for c in calls]))
+        return [len(c) > 0 and all(bytes(s.signature)[:1] == b"\x01" for s in c) for c in calls]
 
     def verify_same_message_multi_sync(self, calls):
         self.passes.append(("sm", [len(c[0]) for c in calls]))
@@ -76,7 +84,8 @@ def test_large_call_is_chunked_into_jobs_and_anded():
         return v, ok, bad
     v, ok, bad = run(go())
     assert ok is True and bad is False
-    assert ("sets", 150) in v.passes
+    # the call's two 150-set jobs (chunkifyMaximizeChunkSize) go to the device in one pass
+    assert ("multi", [150, 150]) in v.passes
 
 
 def test_batchable_requests_are_buffered_then_flushed_together():
@@ -89,7 +98,8 @@ def test_batchable_requests_are_buffered_then_flushed_together():
         res = await asyncio.gather(*futs)
         return v, res
     v, res = run(go())
-    assert res == [True, True, True] and len(v.passes) == 3
+    # the three buffered requests are one device pass (the worker's batchable grouping, worker.ts:51-86)
+    assert res == [True, True, True] and v.passes == [("multi", [1, 1, 1])]
 
 
 def test_batchable_buffer_flushes_past_max_buffered_sigs():
@@ -163,3 +173,38 @@ def test_verify_on_main_thread_is_synchronous():
         return v, r
     v, r = run(go())
     assert r is True and v.passes == [("sets", 1)] and v._jobs == []
+
+
+def test_close_waits_for_the_running_device_pass():
+    """close() while a device pass runs on the worker thread: the pass finishes (its job resolves)
+    before gbv_destroy frees the context; queued jobs reject with QUEUE_ABORTED."""
+    import threading
+
+    class Slow(Recorder):
+        def __init__(self):
+            super().__init__()
+            self.started = threading.Event()
+            self.release = threading.Event()
+
+        def verify_signature_sets_multi_sync(self, calls):
+            self.started.set()
+            assert self.release.wait(5)
+            return super().verify_signature_sets_multi_sync(calls)
+
+    async def go():
+        v = Slow()
+        running = asyncio.ensure_future(v.verify_signature_sets([_set()]))
+        while not v.started.is_set():
+            await asyncio.sleep(0.001)
+        queued = asyncio.ensure_future(v.verify_signature_sets([_set()]))
+        await asyncio.sleep(0)
+        closing = asyncio.ensure_future(v.close())
+        await asyncio.sleep(0.02)
+        assert v.destroyed_after is None  # still waiting for the pass in flight
+        v.release.set()
+        await closing
+        assert v.destroyed_after == [("multi", [1])]
+        assert await running is True
+        with pytest.raises(QueueAbortedError):
+            await queued
+    run(go())
