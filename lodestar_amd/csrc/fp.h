@@ -143,7 +143,15 @@ GBV_HD void mac96(uint64_t& acc, uint32_t& top, uint32_t a, uint32_t b) {
 // a*b and of m*p accumulate into one 96-bit accumulator, m_k is derived from the column's low
 // word.  2 VALU instructions per limb product (288 products), no carry propagation passes.
 // Inputs < p, output < p.
+#if defined(GBV_HOST_TEST)
+// Host build only (tests/native/hosttest.cpp): every Fp product is counted, so the algorithmic work
+// per signature set that bench.py's roofline uses is measured on the code, not estimated.
+inline unsigned long long g_fme_count = 0;
+#endif
 GBV_HD Fp fp_mul_inl(const Fp& a, const Fp& b) {
+#if defined(GBV_HOST_TEST)
+  ++g_fme_count;
+#endif
   uint32_t m[12], r[12];
   uint64_t acc = 0;
   uint32_t top = 0;

@@ -141,3 +141,63 @@ void ht_att_signing_root(uint8_t* out32, const uint8_t* data128, const uint8_t* 
   ht_store_be(out32, ssz_signing_root(ssz_attestation_data_root(d), ht_chunk_be(domain32)));
 }
 }
+
+// ---- Fp-product counts of the per-unit work of each kernel path (bench.py roofline numerators) ----
+// Each returns the number of Fp multiplications/squarings (FME) one unit costs on the code path the
+// device runs; inputs are the caller's valid points/messages (data-independent control flow except
+// for the rare exceptional additions, which valid random inputs never hit).
+extern "C" {
+unsigned long long ht_count_hash_to_g2(const uint8_t* msg32) {
+  uint32_t w[8];
+  for (int i = 0; i < 8; ++i) w[i] = ((uint32_t)msg32[4*i] << 24) | ((uint32_t)msg32[4*i+1] << 16) | ((uint32_t)msg32[4*i+2] << 8) | msg32[4*i+3];
+  g_fme_count = 0;
+  (void)hash_to_g2(w);
+  return g_fme_count;
+}
+// G2 decompress + subgroup check of a 96-byte signature (Signature.fromBytes(sig, true))
+unsigned long long ht_count_sig_validate(const uint8_t* sig96) {
+  G2A s;
+  g_fme_count = 0;
+  if (g2_decode(s, sig96, 96) == PT_OK) (void)g2_in_subgroup(s);
+  return g_fme_count;
+}
+// randomize_pair (r pk and r sig) / randomize_g1 (r pk only)
+unsigned long long ht_count_randomize(const uint8_t* p96, const uint8_t* q192, uint64_t r64, int g1_only) {
+  G1A P{load_mont(p96), load_mont(p96 + 48)};
+  G2A Q{load_fp2(q192), load_fp2(q192 + 96)};
+  G1J rp;
+  G2J rq;
+  g_fme_count = 0;
+  if (g1_only) randomize_g1(P, r64, &rp);
+  else randomize_pair(P, Q, r64, &rp, &rq);
+  return g_fme_count;
+}
+// Miller value with Jacobian P (k_vs_miller / k_sm_miller)
+unsigned long long ht_count_miller_1j(const uint8_t* p96, const uint8_t* q192) {
+  G1J P = jac_from_aff(G1A{load_mont(p96), load_mont(p96 + 48)});
+  G2A Q{load_fp2(q192), load_fp2(q192 + 96)};
+  g_fme_count = 0;
+  (void)miller_loop_1j(P, Q);
+  return g_fme_count;
+}
+// one mixed G1 addition (the gather-aggregate step), one full G1 addition (tree step),
+// one Fp12 product, one Jacobian G2 addition, one final exponentiation
+unsigned long long ht_count_op(int which, const uint8_t* p96, const uint8_t* q192) {
+  G1A P{load_mont(p96), load_mont(p96 + 48)};
+  G2A Q{load_fp2(q192), load_fp2(q192 + 96)};
+  G1J J = jac_dbl(jac_from_aff(P));
+  G2J JQ = jac_dbl(jac_from_aff(Q));
+  Fp12 f = miller_loop_1(P, Q);
+  g_fme_count = 0;
+  switch (which) {
+    case 0: (void)jac_add_aff(J, P); break;
+    case 1: (void)jac_add(J, jac_dbl(J)); g_fme_count -= 0; break;
+    case 2: (void)fp12_mul(f, f); break;
+    case 3: (void)jac_add(JQ, jac_dbl(JQ)); break;
+    case 4: (void)final_exponentiation(f); break;
+    case 5: { G1A a; (void)jac_to_aff(a, J); break; }
+    default: break;
+  }
+  return g_fme_count;
+}
+}
