@@ -1,0 +1,698 @@
+/*
+ * gbv_addon.c -- Node-API addon (C) over the C ABI of include/gbv.h: the binding a Lodestar
+ * GpuBlsVerifier (TypeScript, beside BlsMultiThreadWorkerPool; selected at
+ * beacon-node/src/chain/chain.ts:223-225) calls.  It mirrors IBlsVerifier
+ * (beacon-node/src/chain/bls/interface.ts:25-68) with index-form signature sets:
+ *
+ *   open(device)                                  -> ctx             (gbv_init)
+ *   addPubkeys(ctx, firstIndex, pk48s, validate)  -> Uint8Array      (gbv_pubkeys_append; syncPubkeys /
+ *                                                                      addFinalizedPubkey, pubkeyCache.ts:50-69)
+ *   verifySets(ctx, sets)                         -> Promise<boolean> (gbv_verify_sets; verifySignatureSets)
+ *   verifySetsMulti(ctx, calls)                   -> Promise<Array<boolean | Error>> (gbv_verify_sets_multi:
+ *                                                                      several calls in one device pass)
+ *   verifySameMessageMulti(ctx, calls)            -> Promise<boolean[][]> (gbv_verify_same_message_multi;
+ *                                                                      verifySignatureSetsSameMessage)
+ *   aggregatePubkeys(ctx, indices)                -> Uint8Array(48)  (gbv_aggregate_pubkeys)
+ *   aggregateSerializedPubkeys(ctx, pk48s, validate) -> Uint8Array(48) (syncCommittee.ts:37)
+ *   close(ctx)                                    -> Promise<void>   (waits for in-flight work, gbv_destroy)
+ *
+ * A set is {index: number} or {indices: Uint32Array | number[]} or {pubkey: Uint8Array(48)}, plus
+ * {signingRoot: Uint8Array(32), signature: Uint8Array}.  JS buffers are only borrowed during the
+ * synchronous part of a call: everything is copied into C-owned memory before the work is queued
+ * on the libuv pool (napi_async_work), and results are delivered on the JS thread.  One context is
+ * used by one device call at a time (include/gbv.h): a per-context mutex serialises the pool threads.
+ *
+ * Error mapping: per-set false results are values, never errors; an aggregate set
+ * without pubkeys rejects with code "EMPTY_AGGREGATE_ARRAY" (bls/utils.ts:12 -> index.ts:398-412),
+ * a closed context with "QUEUE_ABORTED" (index.ts:303-305), device failures with "GBV_E_DEVICE",
+ * malformed arguments with "GBV_E_ARG" (or a TypeError for a wrong JS type).
+ */
+#define NAPI_VERSION 6
+#include <node_api.h>
+#include <pthread.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../include/gbv.h"
+
+typedef struct {
+  gbv_ctx* ctx;
+  pthread_mutex_t mu;
+  int closed;
+  int inflight;
+} addon_ctx;
+
+/* ---- helpers ------------------------------------------------------------------------------ */
+#define NAPI_OK(env, call)                                                   \
+  do {                                                                       \
+    if ((call) != napi_ok) {                                                 \
+      napi_throw_error((env), "GBV_E_NAPI", "Node-API call failed: " #call); \
+      return NULL;                                                           \
+    }                                                                        \
+  } while (0)
+
+static const char* code_of(int rc) {
+  switch (rc) {
+    case GBV_E_EMPTY_AGGREGATE: return "EMPTY_AGGREGATE_ARRAY";
+    case GBV_E_CLOSED: return "QUEUE_ABORTED";
+    case GBV_E_DEVICE: return "GBV_E_DEVICE";
+    case GBV_E_OOM: return "GBV_E_OOM";
+    case GBV_E_BAD_POINT: return "GBV_E_BAD_POINT";
+    default: return "GBV_E_ARG";
+  }
+}
+
+static napi_value make_error(napi_env env, int rc, const char* msg) {
+  napi_value code, text, err;
+  napi_create_string_utf8(env, code_of(rc), NAPI_AUTO_LENGTH, &code);
+  napi_create_string_utf8(env, msg && *msg ? msg : code_of(rc), NAPI_AUTO_LENGTH, &text);
+  napi_create_error(env, code, text, &err);
+  return err;
+}
+
+static void throw_rc(napi_env env, int rc, const char* msg) { napi_throw(env, make_error(env, rc, msg)); }
+
+static addon_ctx* get_ctx(napi_env env, napi_value v) {
+  napi_valuetype t;
+  if (napi_typeof(env, v, &t) != napi_ok || t != napi_external) {
+    napi_throw_type_error(env, "GBV_E_ARG", "expected a context from open()");
+    return NULL;
+  }
+  void* p = NULL;
+  napi_get_value_external(env, v, &p);
+  return (addon_ctx*)p;
+}
+
+/* Borrow the bytes of a Uint8Array / Buffer (only valid during the synchronous part). */
+static int get_bytes(napi_env env, napi_value v, const uint8_t** data, size_t* len) {
+  bool is_ta = false;
+  napi_is_typedarray(env, v, &is_ta);
+  if (is_ta) {
+    napi_typedarray_type type;
+    size_t n, off;
+    void* d;
+    napi_value ab;
+    if (napi_get_typedarray_info(env, v, &type, &n, &d, &ab, &off) != napi_ok || type != napi_uint8_array) return 0;
+    *data = (const uint8_t*)d;
+    *len = n;
+    return 1;
+  }
+  bool is_buf = false;
+  napi_is_buffer(env, v, &is_buf);
+  if (is_buf) {
+    void* d;
+    if (napi_get_buffer_info(env, v, &d, len) != napi_ok) return 0;
+    *data = (const uint8_t*)d;
+    return 1;
+  }
+  return 0;
+}
+
+static int get_prop(napi_env env, napi_value obj, const char* name, napi_value* out) {
+  bool has = false;
+  if (napi_has_named_property(env, obj, name, &has) != napi_ok || !has) return 0;
+  if (napi_get_named_property(env, obj, name, out) != napi_ok) return 0;
+  napi_valuetype t;
+  napi_typeof(env, *out, &t);
+  return t != napi_undefined && t != napi_null;
+}
+
+static int get_u32(napi_env env, napi_value v, uint32_t* out) {
+  napi_valuetype t;
+  if (napi_typeof(env, v, &t) != napi_ok || t != napi_number) return 0;
+  return napi_get_value_uint32(env, v, out) == napi_ok;
+}
+
+/* growable byte / u32 vectors (C-owned copies of JS inputs) */
+typedef struct { uint8_t* p; size_t n, cap; } bvec;
+typedef struct { uint32_t* p; size_t n, cap; } uvec;
+static void bv_push(bvec* v, const void* d, size_t n) {
+  if (v->n + n > v->cap) {
+    v->cap = (v->n + n) * 2 + 64;
+    v->p = (uint8_t*)realloc(v->p, v->cap);
+  }
+  memcpy(v->p + v->n, d, n);
+  v->n += n;
+}
+static void uv_push(uvec* v, uint32_t x) {
+  if (v->n == v->cap) {
+    v->cap = v->cap * 2 + 64;
+    v->p = (uint32_t*)realloc(v->p, v->cap * sizeof(uint32_t));
+  }
+  v->p[v->n++] = x;
+}
+
+/* ---- signature-set marshalling ---------------------------------------------------------- */
+/* Copied sets: per set (arena offset/len, raw-pk offset or -1, msg offset, sig offset/len). */
+typedef struct {
+  uvec call_off;
+  uvec idx_off, idx_len, arena;
+  uvec raw_off; /* 0xFFFFFFFF: none */
+  uvec sig_off, sig_len;
+  bvec bytes; /* roots, signatures, raw pubkeys */
+  uvec msg_off;
+} sets_buf;
+
+static void sets_free(sets_buf* s) {
+  free(s->call_off.p); free(s->idx_off.p); free(s->idx_len.p); free(s->arena.p); free(s->raw_off.p);
+  free(s->sig_off.p); free(s->sig_len.p); free(s->bytes.p); free(s->msg_off.p);
+  memset(s, 0, sizeof *s);
+}
+
+/* Append the sets of one JS array; returns 0 (and throws) on a malformed argument. */
+static int marshal_sets(napi_env env, napi_value arr, sets_buf* s) {
+  bool is_arr = false;
+  napi_is_array(env, arr, &is_arr);
+  if (!is_arr) {
+    napi_throw_type_error(env, "GBV_E_ARG", "sets must be an array");
+    return 0;
+  }
+  uint32_t n = 0;
+  napi_get_array_length(env, arr, &n);
+  for (uint32_t i = 0; i < n; ++i) {
+    napi_value e, v;
+    napi_get_element(env, arr, i, &e);
+    napi_valuetype t;
+    napi_typeof(env, e, &t);
+    if (t != napi_object) {
+      napi_throw_type_error(env, "GBV_E_ARG", "a signature set must be an object");
+      return 0;
+    }
+    const uint8_t* d;
+    size_t len;
+    if (!get_prop(env, e, "signingRoot", &v) || !get_bytes(env, v, &d, &len) || len != 32) {
+      napi_throw_type_error(env, "GBV_E_ARG", "signingRoot must be a 32-byte Uint8Array");
+      return 0;
+    }
+    uv_push(&s->msg_off, (uint32_t)s->bytes.n);
+    bv_push(&s->bytes, d, 32);
+    if (!get_prop(env, e, "signature", &v) || !get_bytes(env, v, &d, &len)) {
+      napi_throw_type_error(env, "GBV_E_ARG", "signature must be a Uint8Array");
+      return 0;
+    }
+    uv_push(&s->sig_off, (uint32_t)s->bytes.n);
+    uv_push(&s->sig_len, (uint32_t)len);
+    bv_push(&s->bytes, d, len);
+    uv_push(&s->idx_off, (uint32_t)s->arena.n);
+    if (get_prop(env, e, "pubkey", &v)) {
+      if (!get_bytes(env, v, &d, &len) || len != 48) {
+        napi_throw_type_error(env, "GBV_E_ARG", "pubkey must be a 48-byte Uint8Array");
+        return 0;
+      }
+      uv_push(&s->raw_off, (uint32_t)s->bytes.n);
+      bv_push(&s->bytes, d, 48);
+      uv_push(&s->idx_len, 0);
+    } else if (get_prop(env, e, "indices", &v)) {
+      uv_push(&s->raw_off, 0xFFFFFFFFu);
+      bool ta = false, ja = false;
+      napi_is_typedarray(env, v, &ta);
+      napi_is_array(env, v, &ja);
+      uint32_t k = 0;
+      if (ta) {
+        napi_typedarray_type type;
+        size_t cnt, off;
+        void* p;
+        napi_value ab;
+        napi_get_typedarray_info(env, v, &type, &cnt, &p, &ab, &off);
+        if (type != napi_uint32_array) {
+          napi_throw_type_error(env, "GBV_E_ARG", "indices must be a Uint32Array or an array of numbers");
+          return 0;
+        }
+        for (size_t j = 0; j < cnt; ++j) uv_push(&s->arena, ((const uint32_t*)p)[j]);
+        k = (uint32_t)cnt;
+      } else if (ja) {
+        napi_get_array_length(env, v, &k);
+        for (uint32_t j = 0; j < k; ++j) {
+          napi_value x;
+          uint32_t u;
+          napi_get_element(env, v, j, &x);
+          if (!get_u32(env, x, &u)) {
+            napi_throw_type_error(env, "GBV_E_ARG", "indices must be numbers");
+            return 0;
+          }
+          uv_push(&s->arena, u);
+        }
+      } else {
+        napi_throw_type_error(env, "GBV_E_ARG", "indices must be a Uint32Array or an array of numbers");
+        return 0;
+      }
+      uv_push(&s->idx_len, k);
+    } else if (get_prop(env, e, "index", &v)) {
+      uint32_t u;
+      if (!get_u32(env, v, &u)) {
+        napi_throw_type_error(env, "GBV_E_ARG", "index must be a number");
+        return 0;
+      }
+      uv_push(&s->raw_off, 0xFFFFFFFFu);
+      uv_push(&s->arena, u);
+      uv_push(&s->idx_len, 1);
+    } else {
+      napi_throw_type_error(env, "GBV_E_ARG", "a set needs index, indices or pubkey");
+      return 0;
+    }
+  }
+  return 1;
+}
+
+/* gbv_set records pointing into the copied bytes (built on the pool thread, after all pushes). */
+static gbv_set* sets_records(sets_buf* s) {
+  size_t n = s->msg_off.n;
+  gbv_set* r = (gbv_set*)calloc(n ? n : 1, sizeof(gbv_set));
+  for (size_t i = 0; i < n; ++i) {
+    r[i].idx_off = s->idx_off.p[i];
+    r[i].idx_len = s->idx_len.p[i];
+    r[i].raw_pk48 = s->raw_off.p[i] == 0xFFFFFFFFu ? NULL : s->bytes.p + s->raw_off.p[i];
+    r[i].msg32 = s->bytes.p + s->msg_off.p[i];
+    r[i].sig = s->sig_len.p[i] ? s->bytes.p + s->sig_off.p[i] : NULL;
+    r[i].sig_len = s->sig_len.p[i];
+  }
+  return r;
+}
+
+/* ---- async work ------------------------------------------------------------------------------ */
+enum { OP_VERIFY_SETS, OP_VERIFY_SETS_MULTI, OP_SAME_MESSAGE_MULTI, OP_CLOSE };
+
+typedef struct {
+  int op;
+  addon_ctx* ac;
+  napi_deferred deferred;
+  napi_async_work work;
+  sets_buf sets;
+  /* same-message: per set index + 96-byte signature, per call a message */
+  uvec sm_idx;
+  bvec sm_sigs, sm_msgs;
+  uint8_t* out;
+  size_t n_out;
+  int rc;
+  char err[256];
+} job;
+
+static void lock_begin(addon_ctx* ac) {
+  pthread_mutex_lock(&ac->mu);
+}
+static void lock_end(addon_ctx* ac) { pthread_mutex_unlock(&ac->mu); }
+
+static void execute(napi_env env, void* data) {
+  (void)env;
+  job* j = (job*)data;
+  addon_ctx* ac = j->ac;
+  lock_begin(ac);
+  if (!ac->ctx) {
+    j->rc = GBV_E_CLOSED;
+    lock_end(ac);
+    return;
+  }
+  switch (j->op) {
+    case OP_VERIFY_SETS: {
+      gbv_set* r = sets_records(&j->sets);
+      j->out = (uint8_t*)calloc(1, 1);
+      j->rc = gbv_verify_sets(ac->ctx, r, j->sets.msg_off.n, j->sets.arena.p, j->out, NULL);
+      free(r);
+      break;
+    }
+    case OP_VERIFY_SETS_MULTI: {
+      gbv_set* r = sets_records(&j->sets);
+      size_t nc = j->sets.call_off.n ? j->sets.call_off.n - 1 : 0;
+      j->out = (uint8_t*)calloc(nc ? nc : 1, 1);
+      j->n_out = nc;
+      j->rc = gbv_verify_sets_multi(ac->ctx, nc, j->sets.call_off.p, r, j->sets.arena.p, j->out);
+      free(r);
+      break;
+    }
+    case OP_SAME_MESSAGE_MULTI: {
+      size_t nc = j->sets.call_off.n ? j->sets.call_off.n - 1 : 0;
+      j->n_out = j->sm_idx.n;
+      j->out = (uint8_t*)calloc(j->n_out ? j->n_out : 1, 1);
+      j->rc = gbv_verify_same_message_multi(ac->ctx, nc, j->sets.call_off.p, j->sm_idx.p, j->sm_sigs.p, j->sm_msgs.p, j->out);
+      break;
+    }
+    case OP_CLOSE:
+      gbv_destroy(ac->ctx);
+      ac->ctx = NULL;
+      j->rc = GBV_OK;
+      break;
+  }
+  if (j->rc && ac->ctx) snprintf(j->err, sizeof j->err, "%s", gbv_last_error(ac->ctx));
+  lock_end(ac);
+}
+
+static void complete(napi_env env, napi_status status, void* data) {
+  job* j = (job*)data;
+  napi_value result = NULL;
+  j->ac->inflight--;
+  if (status != napi_ok) {
+    napi_reject_deferred(env, j->deferred, make_error(env, GBV_E_DEVICE, "async work cancelled"));
+  } else if (j->rc != GBV_OK) {
+    napi_reject_deferred(env, j->deferred, make_error(env, j->rc, j->err));
+  } else {
+    switch (j->op) {
+      case OP_VERIFY_SETS:
+        napi_get_boolean(env, j->out[0] == 1, &result);
+        break;
+      case OP_VERIFY_SETS_MULTI:
+        napi_create_array_with_length(env, j->n_out, &result);
+        for (size_t c = 0; c < j->n_out; ++c) {
+          napi_value x;
+          if (j->out[c] == GBV_CALL_REJECTED)
+            x = make_error(env, GBV_E_EMPTY_AGGREGATE, "EMPTY_AGGREGATE_ARRAY");
+          else
+            napi_get_boolean(env, j->out[c] == 1, &x);
+          napi_set_element(env, result, (uint32_t)c, x);
+        }
+        break;
+      case OP_SAME_MESSAGE_MULTI: {
+        size_t nc = j->sets.call_off.n ? j->sets.call_off.n - 1 : 0;
+        napi_create_array_with_length(env, nc, &result);
+        for (size_t c = 0; c < nc; ++c) {
+          uint32_t a = j->sets.call_off.p[c], b = j->sets.call_off.p[c + 1];
+          napi_value arr;
+          napi_create_array_with_length(env, b - a, &arr);
+          for (uint32_t i = a; i < b; ++i) {
+            napi_value x;
+            napi_get_boolean(env, j->out[i] == 1, &x);
+            napi_set_element(env, arr, i - a, x);
+          }
+          napi_set_element(env, result, (uint32_t)c, arr);
+        }
+        break;
+      }
+      case OP_CLOSE:
+        napi_get_undefined(env, &result);
+        break;
+    }
+    napi_resolve_deferred(env, j->deferred, result);
+  }
+  napi_delete_async_work(env, j->work);
+  sets_free(&j->sets);
+  free(j->sm_idx.p); free(j->sm_sigs.p); free(j->sm_msgs.p);
+  free(j->out);
+  free(j);
+}
+
+static napi_value queue(napi_env env, job* j, const char* name) {
+  napi_value promise, res_name;
+  napi_create_promise(env, &j->deferred, &promise);
+  napi_create_string_utf8(env, name, NAPI_AUTO_LENGTH, &res_name);
+  napi_create_async_work(env, NULL, res_name, execute, complete, j, &j->work);
+  j->ac->inflight++;
+  napi_queue_async_work(env, j->work);
+  return promise;
+}
+
+/* A promise already rejected with QUEUE_ABORTED: work submitted after close() (the pool's
+ * verifySignatureSets is async, so its QueueError surfaces as a rejection, index.ts:303-305). */
+static napi_value rejected_closed(napi_env env) {
+  napi_value p;
+  napi_deferred d;
+  napi_create_promise(env, &d, &p);
+  napi_reject_deferred(env, d, make_error(env, GBV_E_CLOSED, "QUEUE_ABORTED"));
+  return p;
+}
+
+static job* new_job(napi_env env, addon_ctx* ac, int op) {
+  (void)env;
+  job* j = (job*)calloc(1, sizeof(job));
+  j->op = op;
+  j->ac = ac;
+  return j;
+}
+
+static void drop_job(job* j) {
+  sets_free(&j->sets);
+  free(j->sm_idx.p); free(j->sm_sigs.p); free(j->sm_msgs.p);
+  free(j);
+}
+
+/* ---- exported functions ------------------------------------------------------------------- */
+static void ctx_finalize(napi_env env, void* data, void* hint) {
+  (void)env; (void)hint;
+  addon_ctx* ac = (addon_ctx*)data;
+  if (ac->ctx) gbv_destroy(ac->ctx);
+  pthread_mutex_destroy(&ac->mu);
+  free(ac);
+}
+
+static napi_value js_open(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  NAPI_OK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  uint32_t dev = 0;
+  if (argc >= 1 && !get_u32(env, argv[0], &dev)) {
+    napi_throw_type_error(env, "GBV_E_ARG", "device must be a number");
+    return NULL;
+  }
+  gbv_ctx* c = NULL;
+  int rc = gbv_init((int)dev, &c);
+  if (rc != GBV_OK) {
+    throw_rc(env, rc, "gbv_init failed: no usable HIP device");
+    return NULL;
+  }
+  addon_ctx* ac = (addon_ctx*)calloc(1, sizeof(addon_ctx));
+  ac->ctx = c;
+  pthread_mutex_init(&ac->mu, NULL);
+  napi_value ext;
+  NAPI_OK(env, napi_create_external(env, ac, ctx_finalize, NULL, &ext));
+  return ext;
+}
+
+static napi_value js_add_pubkeys(napi_env env, napi_callback_info info) {
+  size_t argc = 4;
+  napi_value argv[4];
+  NAPI_OK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  addon_ctx* ac = argc >= 1 ? get_ctx(env, argv[0]) : NULL;
+  if (!ac) return NULL;
+  uint32_t first;
+  const uint8_t* d;
+  size_t len;
+  if (argc < 3 || !get_u32(env, argv[1], &first) || !get_bytes(env, argv[2], &d, &len) || len % 48) {
+    napi_throw_type_error(env, "GBV_E_ARG", "addPubkeys(ctx, firstIndex, pk48s: Uint8Array of n*48 bytes, validate)");
+    return NULL;
+  }
+  bool validate = false;
+  if (argc >= 4) napi_get_value_bool(env, argv[3], &validate);
+  if (ac->closed || !ac->ctx) {
+    throw_rc(env, GBV_E_CLOSED, "QUEUE_ABORTED");
+    return NULL;
+  }
+  size_t n = len / 48;
+  void* st_data = NULL;
+  napi_value ab, st;
+  NAPI_OK(env, napi_create_arraybuffer(env, n ? n : 1, &st_data, &ab));
+  NAPI_OK(env, napi_create_typedarray(env, napi_uint8_array, n, ab, 0, &st));
+  lock_begin(ac);
+  int rc = gbv_pubkeys_append(ac->ctx, first, d, n, validate ? 1 : 0, (uint8_t*)st_data);
+  const char* msg = rc ? gbv_last_error(ac->ctx) : "";
+  if (rc) throw_rc(env, rc, msg);
+  lock_end(ac);
+  return rc ? NULL : st;
+}
+
+static napi_value aggregate_impl(napi_env env, napi_callback_info info, int serialized) {
+  size_t argc = 3;
+  napi_value argv[3];
+  NAPI_OK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  addon_ctx* ac = argc >= 1 ? get_ctx(env, argv[0]) : NULL;
+  if (!ac) return NULL;
+  if (ac->closed || !ac->ctx) {
+    throw_rc(env, GBV_E_CLOSED, "QUEUE_ABORTED");
+    return NULL;
+  }
+  uint8_t out[48];
+  int rc;
+  if (serialized) {
+    const uint8_t* d;
+    size_t len;
+    if (argc < 2 || !get_bytes(env, argv[1], &d, &len) || len % 48) {
+      napi_throw_type_error(env, "GBV_E_ARG", "aggregateSerializedPubkeys(ctx, pk48s: Uint8Array of n*48 bytes, validate)");
+      return NULL;
+    }
+    bool validate = false;
+    if (argc >= 3) napi_get_value_bool(env, argv[2], &validate);
+    lock_begin(ac);
+    rc = gbv_aggregate_serialized_pubkeys(ac->ctx, d, len / 48, validate ? 1 : 0, out);
+  } else {
+    sets_buf tmp;
+    memset(&tmp, 0, sizeof tmp);
+    bool ja = false;
+    if (argc >= 2) napi_is_array(env, argv[1], &ja);
+    if (!ja) {
+      napi_throw_type_error(env, "GBV_E_ARG", "aggregatePubkeys(ctx, indices: number[])");
+      return NULL;
+    }
+    uint32_t k = 0;
+    napi_get_array_length(env, argv[1], &k);
+    for (uint32_t i = 0; i < k; ++i) {
+      napi_value x;
+      uint32_t u;
+      napi_get_element(env, argv[1], i, &x);
+      if (!get_u32(env, x, &u)) {
+        sets_free(&tmp);
+        napi_throw_type_error(env, "GBV_E_ARG", "indices must be numbers");
+        return NULL;
+      }
+      uv_push(&tmp.arena, u);
+    }
+    lock_begin(ac);
+    rc = gbv_aggregate_pubkeys(ac->ctx, tmp.arena.p, k, out);
+    sets_free(&tmp);
+  }
+  if (rc) {
+    throw_rc(env, rc, gbv_last_error(ac->ctx));
+    lock_end(ac);
+    return NULL;
+  }
+  lock_end(ac);
+  void* p;
+  napi_value ab, res;
+  NAPI_OK(env, napi_create_arraybuffer(env, 48, &p, &ab));
+  memcpy(p, out, 48);
+  NAPI_OK(env, napi_create_typedarray(env, napi_uint8_array, 48, ab, 0, &res));
+  return res;
+}
+
+static napi_value js_aggregate_pubkeys(napi_env env, napi_callback_info info) { return aggregate_impl(env, info, 0); }
+static napi_value js_aggregate_serialized(napi_env env, napi_callback_info info) { return aggregate_impl(env, info, 1); }
+
+static napi_value js_verify_sets(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2];
+  NAPI_OK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  addon_ctx* ac = argc >= 1 ? get_ctx(env, argv[0]) : NULL;
+  if (!ac) return NULL;
+  if (argc < 2) {
+    napi_throw_type_error(env, "GBV_E_ARG", "verifySets(ctx, sets)");
+    return NULL;
+  }
+  if (ac->closed) return rejected_closed(env);
+  job* j = new_job(env, ac, OP_VERIFY_SETS);
+  if (!j) return NULL;
+  if (!marshal_sets(env, argv[1], &j->sets)) {
+    drop_job(j);
+    return NULL;
+  }
+  return queue(env, j, "gbvVerifySets");
+}
+
+static napi_value js_verify_sets_multi(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2];
+  NAPI_OK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  addon_ctx* ac = argc >= 1 ? get_ctx(env, argv[0]) : NULL;
+  if (!ac) return NULL;
+  bool ja = false;
+  if (argc >= 2) napi_is_array(env, argv[1], &ja);
+  if (!ja) {
+    napi_throw_type_error(env, "GBV_E_ARG", "verifySetsMulti(ctx, calls: sets[][])");
+    return NULL;
+  }
+  if (ac->closed) return rejected_closed(env);
+  job* j = new_job(env, ac, OP_VERIFY_SETS_MULTI);
+  if (!j) return NULL;
+  uint32_t nc = 0;
+  napi_get_array_length(env, argv[1], &nc);
+  uv_push(&j->sets.call_off, 0);
+  for (uint32_t c = 0; c < nc; ++c) {
+    napi_value call;
+    napi_get_element(env, argv[1], c, &call);
+    if (!marshal_sets(env, call, &j->sets)) {
+      drop_job(j);
+      return NULL;
+    }
+    uv_push(&j->sets.call_off, (uint32_t)j->sets.msg_off.n);
+  }
+  return queue(env, j, "gbvVerifySetsMulti");
+}
+
+static napi_value js_verify_same_message_multi(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2];
+  NAPI_OK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  addon_ctx* ac = argc >= 1 ? get_ctx(env, argv[0]) : NULL;
+  if (!ac) return NULL;
+  bool ja = false;
+  if (argc >= 2) napi_is_array(env, argv[1], &ja);
+  if (!ja) {
+    napi_throw_type_error(env, "GBV_E_ARG", "verifySameMessageMulti(ctx, calls: {sets: {index, signature}[], message}[])");
+    return NULL;
+  }
+  if (ac->closed) return rejected_closed(env);
+  job* j = new_job(env, ac, OP_SAME_MESSAGE_MULTI);
+  if (!j) return NULL;
+  uint32_t nc = 0;
+  napi_get_array_length(env, argv[1], &nc);
+  uv_push(&j->sets.call_off, 0);
+  static const uint8_t zero96[96] = {0};
+  for (uint32_t c = 0; c < nc; ++c) {
+    napi_value call, sets, msg;
+    napi_get_element(env, argv[1], c, &call);
+    const uint8_t* d;
+    size_t len;
+    bool sa = false;
+    if (!get_prop(env, call, "message", &msg) || !get_bytes(env, msg, &d, &len) || len != 32 || !get_prop(env, call, "sets", &sets) ||
+        napi_is_array(env, sets, &sa) != napi_ok || !sa) {
+      drop_job(j);
+      napi_throw_type_error(env, "GBV_E_ARG", "each call needs sets: array and message: 32-byte Uint8Array");
+      return NULL;
+    }
+    bv_push(&j->sm_msgs, d, 32);
+    uint32_t n = 0;
+    napi_get_array_length(env, sets, &n);
+    for (uint32_t i = 0; i < n; ++i) {
+      napi_value e, v;
+      uint32_t idx;
+      napi_get_element(env, sets, i, &e);
+      if (!get_prop(env, e, "index", &v) || !get_u32(env, v, &idx) || !get_prop(env, e, "signature", &v) || !get_bytes(env, v, &d, &len)) {
+        drop_job(j);
+        napi_throw_type_error(env, "GBV_E_ARG", "a same-message set is {index: number, signature: Uint8Array}");
+        return NULL;
+      }
+      uv_push(&j->sm_idx, idx);
+      /* SSZ Bytes96 on the wire; another length throws in fromBytes -> that set is false: the
+       * all-zero encoding (no compression flag) is rejected the same way */
+      bv_push(&j->sm_sigs, len == 96 ? d : zero96, 96);
+    }
+    uv_push(&j->sets.call_off, (uint32_t)j->sm_idx.n);
+  }
+  return queue(env, j, "gbvVerifySameMessageMulti");
+}
+
+static napi_value js_close(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  NAPI_OK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  addon_ctx* ac = argc >= 1 ? get_ctx(env, argv[0]) : NULL;
+  if (!ac) return NULL;
+  if (ac->closed) {  // idempotent, like the pool's close()
+    napi_value p;
+    napi_deferred d;
+    napi_create_promise(env, &d, &p);
+    napi_value u;
+    napi_get_undefined(env, &u);
+    napi_resolve_deferred(env, d, u);
+    return p;
+  }
+  job* j = (job*)calloc(1, sizeof(job));
+  j->op = OP_CLOSE;
+  j->ac = ac;
+  ac->closed = 1;  // new calls reject with QUEUE_ABORTED; queued ones run before the destroy (mutex order)
+  return queue(env, j, "gbvClose");
+}
+
+static napi_value init(napi_env env, napi_value exports) {
+  napi_property_descriptor props[] = {
+      {"open", NULL, js_open, NULL, NULL, NULL, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), NULL},
+      {"addPubkeys", NULL, js_add_pubkeys, NULL, NULL, NULL, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), NULL},
+      {"verifySets", NULL, js_verify_sets, NULL, NULL, NULL, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), NULL},
+      {"verifySetsMulti", NULL, js_verify_sets_multi, NULL, NULL, NULL, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), NULL},
+      {"verifySameMessageMulti", NULL, js_verify_same_message_multi, NULL, NULL, NULL, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), NULL},
+      {"aggregatePubkeys", NULL, js_aggregate_pubkeys, NULL, NULL, NULL, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), NULL},
+      {"aggregateSerializedPubkeys", NULL, js_aggregate_serialized, NULL, NULL, NULL, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), NULL},
+      {"close", NULL, js_close, NULL, NULL, NULL, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), NULL},
+  };
+  napi_define_properties(env, exports, sizeof props / sizeof props[0], props);
+  return exports;
+}
+
+NAPI_MODULE(gbv_addon, init)

@@ -1,0 +1,93 @@
+// Exercises the Node-API addon (addon/gbv_addon.node) from JavaScript, as a Lodestar GpuBlsVerifier
+// would call it.  Used by tests/test_addon.py.
+//   node addon/test_addon.js cpu               exports, argument and error mapping (no GPU needed)
+//   node addon/test_addon.js gpu <fixtures>    every golden case through the addon on device 0
+"use strict";
+const path = require("path");
+const fs = require("fs");
+const addon = require(path.join(__dirname, "gbv_addon.node"));
+
+const EXPORTS = ["open", "addPubkeys", "verifySets", "verifySetsMulti", "verifySameMessageMulti", "aggregatePubkeys",
+  "aggregateSerializedPubkeys", "close"];
+const hex = (h) => Uint8Array.from(Buffer.from(h, "hex"));
+const report = {};
+
+function expectThrow(fn, code) {
+  try {
+    fn();
+  } catch (e) {
+    return e.code === code ? "ok" : "wrong code " + e.code;
+  }
+  return "no throw";
+}
+
+function toSets(c) {
+  return c.sets.map((s) => {
+    const o = {signingRoot: hex(s.msg), signature: hex(s.sig)};
+    if (s.raw_pk) o.pubkey = hex(s.raw_pk);
+    else if (s.indices.length === 1) o.index = s.indices[0];
+    else o.indices = Uint32Array.from(s.indices);
+    return o;
+  });
+}
+
+async function cpu() {
+  report.exports = EXPORTS.filter((k) => typeof addon[k] === "function");
+  report.open = expectThrow(() => addon.open(0), "GBV_E_DEVICE");
+  report.badCtx = expectThrow(() => addon.verifySets({}, []), "GBV_E_ARG");
+  report.badArg = expectThrow(() => addon.open("x"), "GBV_E_ARG");
+}
+
+async function gpu(fixPath) {
+  const fix = JSON.parse(fs.readFileSync(fixPath, "utf8"));
+  const ctx = addon.open(0);
+  const pks = Buffer.concat(fix.keys.pks.map((p) => Buffer.from(p, "hex")));
+  const st = addon.addPubkeys(ctx, 0, Uint8Array.from(pks), true);
+  report.ingest = Array.from(st).every((x) => x === 0);
+  // verifySets, one call per fixture case (rejections carry EMPTY_AGGREGATE_ARRAY)
+  const vs = [];
+  for (const c of fix.verify_sets) {
+    try {
+      const r = await addon.verifySets(ctx, toSets(c));
+      vs.push(r === c.expected);
+    } catch (e) {
+      vs.push(c.expected === "reject" && e.code === "EMPTY_AGGREGATE_ARRAY");
+    }
+  }
+  report.verifySets = vs;
+  // all cases in one device pass
+  const multi = await addon.verifySetsMulti(ctx, fix.verify_sets.map(toSets));
+  report.verifySetsMulti = multi.map((r, i) => {
+    const want = fix.verify_sets[i].expected;
+    return want === "reject" ? r instanceof Error && r.code === "EMPTY_AGGREGATE_ARRAY" : r === want;
+  });
+  const calls = fix.same_message.map((c) => ({
+    message: hex(c.msg),
+    sets: c.indices.map((idx, k) => ({index: idx, signature: hex(c.sigs[k])})),
+  }));
+  const sm = await addon.verifySameMessageMulti(ctx, calls);
+  report.sameMessage = sm.map((r, i) => JSON.stringify(r) === JSON.stringify(fix.same_message[i].expected));
+  report.aggregate = fix.aggregate_pubkeys.map((c) => Buffer.from(addon.aggregatePubkeys(ctx, c.indices)).toString("hex") === c.expected);
+  report.aggregateSerialized = fix.aggregate_pubkeys.map((c) => {
+    const ser = Buffer.concat(c.indices.map((i) => Buffer.from(fix.keys.pks[i], "hex")));
+    return Buffer.from(addon.aggregateSerializedPubkeys(ctx, Uint8Array.from(ser), false)).toString("hex") === c.expected;
+  });
+  report.emptyAggregate = expectThrow(() => addon.aggregatePubkeys(ctx, []), "EMPTY_AGGREGATE_ARRAY");
+  // concurrent submissions are serialised per context and all resolve
+  const conc = await Promise.all([0, 1, 2, 3].map(() => addon.verifySets(ctx, toSets(fix.verify_sets[0]))));
+  report.concurrent = conc.every((r) => r === fix.verify_sets[0].expected);
+  const pending = addon.verifySets(ctx, toSets(fix.verify_sets[0]));
+  await addon.close(ctx);
+  report.inflightBeforeClose = await pending.then((r) => r === fix.verify_sets[0].expected, (e) => e.code === "QUEUE_ABORTED");
+  report.afterClose = await addon.verifySets(ctx, toSets(fix.verify_sets[0])).then(() => "resolved", (e) => e.code);
+}
+
+(async () => {
+  const mode = process.argv[2];
+  if (mode === "cpu") await cpu();
+  else await gpu(process.argv[3]);
+  process.stdout.write(JSON.stringify(report) + "\n");
+})().catch((e) => {
+  process.stdout.write(JSON.stringify({fatal: String(e && e.stack || e), code: e && e.code}) + "\n");
+  process.exit(1);
+});

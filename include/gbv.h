@@ -183,7 +183,7 @@ int gbv_last_kernel_ms(gbv_ctx* ctx, float* ms_out, int* launches_out, int max);
 int gbv_last_stats(gbv_ctx* ctx, uint32_t* fallback_chunks, uint32_t* failed_segments);
 
 /* ---- signing roots: batched SHA-256 over SSZ nodes ------------------
- * The builders hash a signing root for every set they hand the verifier (signatureSets/*.ts via
+ * The builders hash a signing root for every set they hand the verifier (the signatureSets builders via
  * computeSigningRoot, state-transition/src/util/signingRoot.ts:7-13).  Inputs and outputs are host
  * buffers; n = 0 is a no-op.  Each call records its kernel time (HIP events, gbv_ssz_last_kernel_ms). */
 /* out32[i] = sha256(in64[i]): persistent-merkle-tree hasher.digest64(a, b) = sha256(a || b)

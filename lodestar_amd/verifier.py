@@ -337,6 +337,24 @@ class GpuBlsVerifier:
             out.append([raw[i] == 1 for i in range(off[g], off[g + 1])])
         return out
 
+    def verify_same_message_raw(self, call_off, idx, sigs96: bytes, msgs32: bytes) -> bytes:
+        """verifySignatureSetsSameMessage calls from flat buffers -- CSR call offsets, validator
+        indices, concatenated 96-byte signatures and 32-byte messages -- in one device pass
+        (gbv_verify_same_message_multi); returns one validity byte per set."""
+        self._check_open()
+        import numpy as np
+        off = np.ascontiguousarray(call_off, dtype=np.uint32)
+        ix = np.ascontiguousarray(idx, dtype=np.uint32)
+        n = int(off[-1]) if len(off) else 0
+        if len(sigs96) != 96 * n or len(msgs32) != 32 * (len(off) - 1):
+            raise ValueError("buffer sizes do not match the call offsets")
+        valid = ctypes.create_string_buffer(max(n, 1))
+        rc = self._lib.gbv_verify_same_message_multi(self._ctx, len(off) - 1, off.ctypes.data, ix.ctypes.data, bytes(sigs96) or b"\0",
+                                                     bytes(msgs32) or bytes(32), valid)
+        _native.check(self._lib, self._ctx, rc)
+        self.metrics["device_passes"] += 1
+        return valid.raw[:n]
+
     def verify_signature_sets_same_message_sync(self, sets: Sequence[Tuple[int, bytes]], message: bytes) -> List[bool]:
         return self.verify_same_message_multi_sync([(sets, message)])[0]
 

@@ -1033,3 +1033,150 @@ void port_hash_to_g2(const uint8_t* msg32, uint8_t* out192) {
   fp_to_raw(v, &h.y.c1); raw_to_be48(out192 + 96, v);
   fp_to_raw(v, &h.y.c0); raw_to_be48(out192 + 144, v);
 }
+
+/* ---------------- verifySignatureSets (distinct messages, aggregate pubkeys) ----------------
+ * BlsMultiThreadWorkerPool.verifySignatureSets (multithread/index.ts:157-207): every call is split
+ * with chunkifyMaximizeChunkSize(128) into jobs; a job's sets get their aggregate pubkey
+ * (aggregatePublicKeys, jobItem.ts:55-62), and the worker verifies the job as ONE randomised batch
+ * (verifyMultipleAggregateSignatures, maybeBatch.ts:17-26): per set decompress + subgroup check,
+ * 64-bit random r, hash_to_G2; then prod e(r_i pk_i, H(m_i)) * e(-g1, sum r_i sig_i) with a
+ * multi-Miller loop sharing its Fp12 squarings, and one final exponentiation.  A call is the AND
+ * over its jobs.  Workers pull jobs, as the pool's workers do. */
+typedef struct {
+  g2p T;
+  g2a Q;
+  fp nx, y;
+} mpair;
+
+static int multi_pairing_is_one(mpair* pr, size_t n) {
+  fp12 f;
+  fp12_one(&f);
+  fp2 c0, c2, c3;
+  for (int i = 62; i >= 0; --i) {
+    if (i != 62) fp12_sqr(&f, &f);
+    for (size_t j = 0; j < n; ++j) { dbl_step(&pr[j].T, &c0, &c2, &c3, &pr[j].nx, &pr[j].y); fp12_mul_line(&f, &c0, &c2, &c3); }
+    if ((X_ABS >> i) & 1)
+      for (size_t j = 0; j < n; ++j) { add_step(&pr[j].T, &pr[j].Q, &c0, &c2, &c3, &pr[j].nx, &pr[j].y); fp12_mul_line(&f, &c0, &c2, &c3); }
+  }
+  fp12_conj(&f, &f);
+  fp12 e;
+  final_exp(&e, &f);
+  return fp12_is_one(&e);
+}
+
+/* one job: sets [a, b) -> 1 valid / 0 invalid */
+static int vs_job(size_t a, size_t b, const uint32_t* pk_off, const uint32_t* pk_idx, const uint8_t* pk_aff, const uint8_t* msgs,
+                  const uint8_t* sigs, uint64_t* rng) {
+  size_t n = b - a;
+  if (n == 0) return 0; /* verifySignatureSetsMaybeBatch([]) -> false */
+  mpair* pr = (mpair*)malloc(sizeof(mpair) * (n + 1));
+  g2j acc;
+  memset(&acc, 0, sizeof acc);
+  int ok = 1;
+  for (size_t s = a; s < b && ok; ++s) {
+    g1j agg;
+    memset(&agg, 0, sizeof agg);
+    for (uint32_t k = pk_off[s]; k < pk_off[s + 1]; ++k) {
+      g1a p;
+      load_g1_aff96(&p, pk_aff + 96ull * pk_idx[k]);
+      g1_add_aff(&agg, &agg, &p);
+    }
+    g1a pk;
+    g2a sg;
+    if (!g1_to_aff(&pk, &agg) || g2_decompress(&sg, sigs + 96 * s) || !g2_in_subgroup(&sg)) { ok = 0; break; }
+    uint64_t r = 0;
+    while (!r) r = splitmix(rng);
+    g1j rp;
+    g2j rs;
+    g1_mul_u64(&rp, &pk, r);
+    g2_mul_u64(&rs, &sg, r);
+    g2_add(&acc, &acc, &rs);
+    g1a rpa;
+    g1_to_aff(&rpa, &rp);
+    mpair* m = &pr[s - a];
+    hash_to_g2(&m->Q, msgs + 32 * s);
+    m->T.x = m->Q.x; m->T.y = m->Q.y; m->T.z.c0 = R1; memset(&m->T.z.c1, 0, sizeof(fp));
+    fp_neg(&m->nx, &rpa.x);
+    m->y = rpa.y;
+  }
+  if (ok) {
+    g2a sa;
+    if (!g2_to_aff(&sa, &acc)) ok = 0;
+    else {
+      mpair* m = &pr[n];
+      m->Q = sa;
+      m->T.x = sa.x; m->T.y = sa.y; m->T.z.c0 = R1; memset(&m->T.z.c1, 0, sizeof(fp));
+      fp_neg(&m->nx, &G1X_M);
+      m->y = NEG_G1Y;
+      ok = multi_pairing_is_one(pr, n + 1);
+    }
+  }
+  free(pr);
+  return ok;
+}
+
+typedef struct {
+  const uint32_t* job_be; /* (begin, end) set range per job */
+  const uint32_t *pk_off, *pk_idx;
+  size_t n_jobs;
+  const uint8_t *pk_aff, *msgs, *sigs;
+  uint8_t* job_ok;
+  atomic_size_t next;
+  uint64_t seed;
+} vsjob_t;
+
+static void* vs_worker(void* arg) {
+  vsjob_t* j = (vsjob_t*)arg;
+  uint64_t rng = j->seed ^ (uint64_t)(uintptr_t)&rng;
+  for (;;) {
+    size_t c = atomic_fetch_add(&j->next, 1);
+    if (c >= j->n_jobs) break;
+    j->job_ok[c] = (uint8_t)vs_job(j->job_be[2 * c], j->job_be[2 * c + 1], j->pk_off, j->pk_idx, j->pk_aff, j->msgs, j->sigs, &rng);
+  }
+  return NULL;
+}
+
+/* n_calls verifySignatureSets calls on `nthreads` workers.  call_off: n_calls+1 set offsets; set s
+ * aggregates the 96-byte affine pubkeys pk_aff[pk_idx[pk_off[s] .. pk_off[s+1])]; msgs 32 B and
+ * sigs 96 B per set.  out[c] = AND over the call's <=128-set jobs (0 for an empty call). */
+int port_verify_sets_batch(int nthreads, size_t n_calls, const uint32_t* call_off, const uint32_t* pk_off, const uint32_t* pk_idx,
+                           const uint8_t* pk_aff, const uint8_t* msgs, const uint8_t* sigs, uint8_t* out, uint64_t seed) {
+  port_init();
+  size_t cap = 16, nj = 0;
+  uint32_t* be = (uint32_t*)malloc(sizeof(uint32_t) * 2 * cap);
+  uint32_t* jc = (uint32_t*)malloc(sizeof(uint32_t) * cap);
+  for (size_t g = 0; g < n_calls; ++g) {
+    uint32_t len = call_off[g + 1] - call_off[g];
+    if (!len) continue;
+    uint32_t cc = len / 128, per = len; /* chunkifyMaximizeChunkSize(call, 128) */
+    if (cc > 1) per = (len + cc - 1) / cc;
+    for (uint32_t s = 0; s < len; s += per) {
+      if (nj == cap) {
+        cap *= 2;
+        be = (uint32_t*)realloc(be, sizeof(uint32_t) * 2 * cap);
+        jc = (uint32_t*)realloc(jc, sizeof(uint32_t) * cap);
+      }
+      be[2 * nj] = call_off[g] + s;
+      be[2 * nj + 1] = call_off[g] + (s + per < len ? s + per : len);
+      jc[nj] = (uint32_t)g;
+      ++nj;
+    }
+  }
+  uint8_t* job_ok = (uint8_t*)malloc(nj + 1);
+  vsjob_t j;
+  memset(&j, 0, sizeof j);
+  j.job_be = be; j.pk_off = pk_off; j.pk_idx = pk_idx; j.pk_aff = pk_aff; j.msgs = msgs; j.sigs = sigs;
+  j.n_jobs = nj; j.job_ok = job_ok; j.seed = seed;
+  atomic_init(&j.next, 0);
+  if (nthreads < 1) nthreads = 1;
+  pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * (size_t)nthreads);
+  for (int t = 0; t < nthreads; ++t) pthread_create(&th[t], NULL, vs_worker, &j);
+  for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
+  for (size_t g = 0; g < n_calls; ++g) out[g] = call_off[g + 1] > call_off[g] ? 1 : 0;
+  for (size_t k = 0; k < nj; ++k) out[jc[k]] &= job_ok[k];
+  free(th);
+  free(job_ok);
+  free(be);
+  free(jc);
+  return 0;
+}

@@ -65,3 +65,56 @@ def measure_same_message(call_off, idx, sigs96, msgs32, table_pk48, n_keys, targ
             "sample": "%d sets in %d same-message calls (first calls of the bench workload), %.2fs wall, "
                       "%d/%d valid; oracle/c/blsport.c, C port not blst, %d worker threads" % (n, k, dt, ok, n, threads),
             "all_valid": ok == n}
+
+
+def _declare_vs(lib):
+    lib.port_verify_sets_batch.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                           ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_void_p, ctypes.c_uint64]
+
+
+def affine_rows(lib, pks48):
+    """96-byte affine rows (x||y) of compressed pubkeys -- the deserialized index2pubkey the
+    reference already holds (not timed)."""
+    rows = []
+    for pk in pks48:
+        out = ctypes.create_string_buffer(96)
+        assert lib.port_g1_decompress(bytes(pk), out) == 0
+        rows.append(out.raw)
+    return b"".join(rows)
+
+
+def run_verify_sets(lib, calls, pk_rows, threads=1, seed=None):
+    """verifySignatureSets calls on the port.  calls: list of lists of (pk row indices, msg32, sig96);
+    pk_rows: concatenated 96-byte affine rows.  Returns (per-call booleans, seconds)."""
+    _declare_vs(lib)
+    call_off, pk_off, pk_idx, msgs, sigs = [0], [0], [], [], []
+    for c in calls:
+        for rows, m, s in c:
+            pk_idx.extend(rows)
+            pk_off.append(len(pk_idx))
+            msgs.append(bytes(m))
+            sigs.append(bytes(s) if len(s) == 96 else bytes(96))
+        call_off.append(len(pk_off) - 1)
+    co = np.array(call_off, dtype=np.uint32)
+    po = np.array(pk_off, dtype=np.uint32)
+    pi = np.array(pk_idx or [0], dtype=np.uint32)
+    out = (ctypes.c_uint8 * max(len(calls), 1))()
+    seed = seed if seed is not None else int.from_bytes(os.urandom(8), "little")
+    t = time.perf_counter()
+    lib.port_verify_sets_batch(threads, len(calls), co.ctypes.data, po.ctypes.data, pi.ctypes.data, pk_rows, b"".join(msgs) or b"\0",
+                               b"".join(sigs) or b"\0", out, seed)
+    dt = time.perf_counter() - t
+    return [bool(out[i]) for i in range(len(calls))], dt
+
+
+def measure_verify_sets(calls, pk_rows, threads=None, label=""):
+    """`cpu_baseline` dict of a verifySignatureSets config: the port through the pool shape
+    (threads workers pulling <=128-set jobs) on the given bounded sample of calls."""
+    lib = load()
+    threads = threads or pool_threads()
+    res, dt = run_verify_sets(lib, calls, pk_rows, threads)
+    n = sum(len(c) for c in calls)
+    return {"value": round(n / dt, 1), "unit": "sets/s", "cores": threads, "kind": "port",
+            "sample": "%d sets in %d verifySignatureSets calls%s, %.2fs wall, %d/%d calls true; oracle/c/blsport.c "
+                      "(C port, not blst), %d worker threads" % (n, len(calls), label, dt, sum(res), len(calls), threads),
+            "all_valid": all(res)}

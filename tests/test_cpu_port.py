@@ -54,3 +54,37 @@ def test_port_hash_to_g2(lib):
         out = ctypes.create_string_buffer(192)
         lib.port_hash_to_g2(bytes.fromhex(c["msg"]), out)
         assert out.raw.hex() == c["expected"]
+
+
+def test_port_verify_sets_c4_block(lib):
+    """The port's verifySignatureSets (cpu_baseline of C1/C3/C4) on the oracle's C4 block fixture:
+    the clean block true, every corruption false (one call each, pool shape, 4 workers)."""
+    import sys
+    sys.path.insert(0, os.path.join(HERE, "golden"))
+    import c4_block as C
+    from oracle import block_oracle as BO
+    from oracle import cpu_baseline
+    fix = C.load()
+    rows = cpu_baseline.affine_rows(lib, [bytes.fromhex(p) for p in fix["pubkeys"]])
+    extra = []
+
+    def to_call(sets):
+        call = []
+        for kind, key, root, sig in sets:
+            if kind == "raw":
+                extra.append(key)
+                call.append(([C.N_KEYS + len(extra) - 1], root, sig))
+            elif kind == "single":
+                call.append(([key % C.N_KEYS], root, sig))
+            else:
+                call.append(([v % C.N_KEYS for v in key], root, sig))
+        return call
+    calls = [to_call(BO.block_signature_sets(fix))]
+    for kind in C.CORRUPTIONS:
+        b2, com2, _ = C.corrupt(fix, kind)
+        calls.append(to_call(BO.block_signature_sets(fix, b2, com2)))
+    rows += cpu_baseline.affine_rows(lib, extra)
+    res, _ = cpu_baseline.run_verify_sets(lib, calls, rows, threads=4)
+    assert res == [True] + [False] * len(C.CORRUPTIONS)
+    # empty call false, as verifySignatureSetsMaybeBatch([])
+    assert cpu_baseline.run_verify_sets(lib, [[]], rows)[0] == [False]

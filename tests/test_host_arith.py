@@ -207,3 +207,31 @@ def test_randomize_pair(lib, r64):
     assert (int.from_bytes(op.raw[:48], "big"), int.from_bytes(op.raw[48:], "big")) == o.g1_mul(P, r)
     assert (b2fp2(oq.raw[:96]), b2fp2(oq.raw[96:])) == o.g2_mul(Q, r)
 
+
+
+def test_roofline_work_constants_are_counted(lib):
+    """bench.py's algorithmic work per set (FME = Fp products) equals what the device code path
+    executes, counted by the host build of the same arithmetic -- the roofline numerators are
+    measured, not estimated."""
+    import sys
+    sys.path.insert(0, os.path.join(HERE, ".."))
+    import bench
+    for f in ("ht_count_hash_to_g2", "ht_count_sig_validate", "ht_count_randomize", "ht_count_miller_1j", "ht_count_op"):
+        getattr(lib, f).restype = ctypes.c_ulonglong
+    rng = random.Random(5)
+    for trial in range(3):
+        msg = bytes(rng.randrange(256) for _ in range(32))
+        sk = rng.randrange(1, o.R)
+        pk = o.sk_to_pk(sk)
+        sig_pt = o.sign(sk, msg)
+        h = o.hash_to_g2(msg)
+        p96 = be(pk[0]) + be(pk[1])
+        q192 = fp2b(h[0]) + fp2b(h[1])
+        r64 = ctypes.c_uint64(rng.getrandbits(64) | 1)
+        assert lib.ht_count_hash_to_g2(msg) == bench.FME_HASH_TO_G2
+        assert lib.ht_count_sig_validate(o.g2_compress(sig_pt)) == bench.FME_SIG_VALIDATE
+        assert lib.ht_count_randomize(p96, q192, r64, 0) == bench.FME_RANDOMIZE_PAIR
+        assert lib.ht_count_randomize(p96, q192, r64, 1) == bench.FME_RANDOMIZE_G1
+        assert lib.ht_count_miller_1j(p96, q192) == bench.FME_MILLER_1J
+        assert 3 * (lib.ht_count_op(1, p96, q192) - 7) == bench.FME_G1_SCAN  # full G1 addition (minus the doubling)
+    assert bench.W_VS_HASH_SIG == bench.FME_HASH_TO_G2 + bench.FME_SIG_VALIDATE + bench.FME_RANDOMIZE_PAIR
