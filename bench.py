@@ -53,6 +53,7 @@ MAC_PER_FME = 300  # u32 x u32 -> u64 MACs per Fp product (12-limb Montgomery: 1
 FME_SIG_VALIDATE = 2111     # Signature.fromBytes(sig, true): G2 decompress + subgroup check
 FME_RANDOMIZE_G1 = 593      # r_i pk_i (endomorphism-split 32-step ladder + affine tables)
 FME_RANDOMIZE_PAIR = 2086   # r_i pk_i and r_i sig_i with one shared inversion
+FME_RANDOMIZE_PAIR_JAC = 2096  # the same with P Jacobian (aggregate pubkeys straight from k_vs_agg)
 FME_HASH_TO_G2 = 6658       # RFC 9380 hash_to_G2 (SSWU + 3-isogeny + h_eff + to affine)
 FME_MILLER_1J = 7244        # Miller value of one pair, Jacobian P
 FME_G1_SCAN = 48            # 3-level 8-lane chunk scan of r_i pk_i (3 Jacobian G1 additions)
@@ -60,7 +61,7 @@ FME_G1_SCAN = 48            # 3-level 8-lane chunk scan of r_i pk_i (3 Jacobian 
 W_PREPARE_FME_MSM = FME_SIG_VALIDATE + FME_RANDOMIZE_G1 + FME_G1_SCAN
 W_PREPARE_FME = FME_SIG_VALIDATE + FME_RANDOMIZE_PAIR + 177
 # k_vs_hash_sig: both block roles per set
-W_VS_HASH_SIG = FME_HASH_TO_G2 + FME_SIG_VALIDATE + FME_RANDOMIZE_PAIR
+W_VS_HASH_SIG = FME_HASH_TO_G2 + FME_SIG_VALIDATE + FME_RANDOMIZE_PAIR_JAC
 # SURVEY.md 8(d)'s algorithm-independent counts for the same-message per-set work (decompress 1.8k +
 # subgroup 1.25k + r*pk 0.8k), reported beside ours
 W_SURVEY_SAME_MESSAGE = 1800 + 1250 + 800
@@ -527,7 +528,7 @@ def main():
         expect = expect_all[s0:s1]
         n_mine = s1 - s0
         widths = [int(call_off_all[min((r + 1) * per, n_calls)] - call_off_all[min(r * per, n_calls)]) for r in range(world)]
-        gather = (max(widths), widths, int(expect_all.sum()))
+        gather = (max(widths), widths, int(expect_all.sum())) if world > 1 else None
     if invalid_frac > 0:
         log("injected %d invalid sets on rank 0 (C5 recipe)" % int((expect == 0).sum()))
     staged = v.stage_same_message(call_off, idx, sigs, msgs)

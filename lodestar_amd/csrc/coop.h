@@ -2,13 +2,17 @@
 // verification (per-chunk Miller values, the shared final exponentiation, per-chunk retries).
 //
 // One workgroup = one wave (64 lanes) = one pairing job.  Field elements live in a per-wave LDS
-// workspace (Ws); a program from coop_tables.h (tools/gen_coop.py) runs as
+// workspace of Slots -- each Fp stored next to its negation, so a signed term of a linear
+// combination is ONE LDS load and ONE modular add; a program from coop_tables.h
+// (tools/gen_coop.py) runs as
 //   product rounds : lane k computes Z[k] = (sum of its A terms) * (sum of its B terms)
 //   partial sums   : lane j sums <= 6 terms of a long output into Z
 //   outputs        : lane o computes output coordinate o, then every lane stores after a barrier
-// so an Fp12 product costs ~1 Fp product of latency instead of 54.  The same drivers compile for
-// the host (GBV_HOST_TEST: the 64 lanes run one after another) and are checked against the
-// oracle in tests/test_host_arith.py; tests/test_coop_tables.py checks the programs themselves.
+// with term lists of their true length (records carry the counts; positive terms first), so an
+// Fp12 multiplication costs about one Fp product plus a few dozen adds of latency instead of 54
+// products.  The same drivers compile for the host (GBV_HOST_TEST: the 64 lanes run one after
+// another) and are checked against the oracle in tests/test_host_arith.py;
+// tests/test_coop_tables.py checks the programs themselves.
 #pragma once
 #include "pairing.h"
 
@@ -21,21 +25,24 @@
 namespace gbv {
 namespace coop {
 
-struct Term { uint8_t src, idx; int16_t coef; };
-// Fixed-size per-lane records (tools/gen_coop.py): product k = prods[20k .. 20k+19]
-// (A terms 0..9, B terms 10..19), partial j = parts[8j ..] -> Z[n_prod + j], output o = outs[8o ..]
-// -> operand out_dst[o], coordinate out_idx[o].  Padding terms have coef 0.
+// Per-lane records (tools/gen_coop.py): a product record is PROD_WORDS u32 -- header
+// (npos_A | nneg_A << 8 | npos_B << 16 | nneg_B << 24), OPW A terms, OPW B terms, padding --
+// a partial-sum / output record is SUM_WORDS u32 -- header (npos | nneg << 8), SUM_TERMS terms.
+// A term is src (bits 0-3) | idx << 8 | magnitude << 16; its sign is its position (positives first).
 struct Prog {
   uint8_t n_rounds, n_part, n_out;
   uint16_t round_end[6];
-  const Term* prods;
-  const Term* parts;
-  const Term* outs;
+  const uint32_t* prods;
+  const uint32_t* parts;
+  const uint32_t* outs;
   const uint8_t* out_dst;
   const uint8_t* out_idx;
 };
 constexpr int OPW = 10;
+constexpr int PROD_WORDS = 24;
+constexpr int SUM_WORDS = 8, SUM_TERMS = 7;
 enum { SRC_Z = 6, SRC_C = 7 };
+constexpr int N_CONSTS_MAX = 16;
 
 }  // namespace coop
 }  // namespace gbv
@@ -48,51 +55,67 @@ namespace coop {
 constexpr int LANES = 64;
 constexpr int ZSLOTS = 128;
 
+// A workspace slot: the value and its negation (p - v, and 0 for 0).
+struct Slot {
+  Fp v, n;
+};
+
 // LDS-typed pointers so workspace accesses compile to ds_read/ds_write (a generic pointer would
 // give flat instructions, which wait on both the vector-memory and LDS counters).
 #if defined(GBV_HOST_TEST)
-typedef Fp LFp;
+typedef Slot LSlot;
 #define GBV_LDS(p) (p)
 #else
-typedef __attribute__((address_space(3))) Fp LFp;
-#define GBV_LDS(p) ((LFp*)(p))
+typedef __attribute__((address_space(3))) Slot LSlot;
+#define GBV_LDS(p) ((LSlot*)(p))
 #endif
 
-GBV_HD Fp ld(const LFp* p) {
+GBV_HD Fp get(const LSlot* s) {
   Fp r;
-  r.v = p->v;
+  r.v = s->v.v;
   return r;
 }
-GBV_HD void st(LFp* p, const Fp& a) { p->v = a.v; }
+GBV_HD Fp get_signed(const LSlot* s, bool neg) {
+  Fp r;
+  r.v = neg ? s->n.v : s->v.v;
+  return r;
+}
+GBV_HD void put(LSlot* s, const Fp& a) {
+  s->v.v = a.v;
+  s->n.v = fp_neg(a).v;
+}
+GBV_HD void put_pair(LSlot* s, const Fp& a, const Fp& na) {
+  s->v.v = a.v;
+  s->n.v = na.v;
+}
+#if !defined(GBV_HOST_TEST)
+// generic-pointer forms for callers holding a plain Slot* into __shared__ memory
+__device__ inline Fp get(const Slot* s) { return get(GBV_LDS(s)); }
+__device__ inline void put(Slot* s, const Fp& a) { put(GBV_LDS(s), a); }
+#endif
 
-// Per-wave workspace: mem[] is LDS on the device; operand k of a program lives at mem + op[k].
+// The constant pool, in LDS so that every term source is a workspace load.
+#if defined(GBV_HOST_TEST)
+inline Slot g_consts[N_CONSTS_MAX];
+#define GBV_CONSTS_LDS (g_consts)
+#else
+__shared__ Slot g_consts[N_CONSTS_MAX];
+#define GBV_CONSTS_LDS GBV_LDS(g_consts)
+#endif
+
+// Per-wave workspace: mem is LDS on the device; operand k of a program lives at mem + op[k].
 struct Ws {
-  LFp* mem;
+  LSlot* mem;
   uint16_t op[6];
   uint16_t z;
 };
 
-GBV_HD Term term_of(uint32_t u) { return Term{(uint8_t)u, (uint8_t)(u >> 8), (int16_t)(u >> 16)}; }
-
-// Copy n (multiple of 4) terms into registers with 16-byte loads: one memory latency per record.
-template <int N> GBV_HD void load_terms(uint32_t (&r)[N], const Term* t) {
-  static_assert(N % 4 == 0, "records are whole 16-byte units");
-  const uint4* q = (const uint4*)t;
-#pragma unroll
-  for (int i = 0; i < N / 4; ++i) {
-    uint4 x = q[i];
-    r[4 * i] = x.x;
-    r[4 * i + 1] = x.y;
-    r[4 * i + 2] = x.z;
-    r[4 * i + 3] = x.w;
-  }
-}
-
-GBV_HD Fp ws_get(const Ws& w, Term t) {
-  if (t.src == SRC_C) return CONSTS[t.idx];
-  uint32_t base = t.src == SRC_Z ? w.z : t.src == 0 ? w.op[0] : t.src == 1 ? w.op[1] : t.src == 2 ? w.op[2]
-                 : t.src == 3 ? w.op[3] : t.src == 4 ? w.op[4] : w.op[5];
-  return ld(w.mem + base + t.idx);
+GBV_HD const LSlot* term_slot(const Ws& w, uint32_t t) {
+  uint32_t src = t & 0xF, idx = (t >> 8) & 0xFF;
+  if (src == SRC_C) return GBV_CONSTS_LDS + idx;
+  uint32_t base = src == SRC_Z ? w.z : src == 0 ? w.op[0] : src == 1 ? w.op[1] : src == 2 ? w.op[2]
+                 : src == 3 ? w.op[3] : src == 4 ? w.op[4] : w.op[5];
+  return w.mem + base + idx;
 }
 
 // c * v for a small integer c >= 2 (rare: scaled terms of the doubling/cyclotomic formulas)
@@ -110,103 +133,114 @@ GBV_NI Fp scale_small(Fp v, int c) {
   return s;
 }
 
-// p - s for s < p, without reduction (s = 0 gives p, which every consumer below accepts: it only
-// ever enters fp_add next to a value < p).
-GBV_HD Fp fp_neg_raw(const Fp& s) {
-  Fp d;
-  raw_sub(d, P_RAW, s);
-  return d;
-}
-
-// sum of coef * value over N packed terms: all N operand loads are issued first, then each term is
-// conditionally negated / zeroed with selects and added -- no divergent branch per term (a lane's
-// term count and signs differ from its neighbours').
-template <int N> GBV_HD Fp lin_eval(const Ws& w, const uint32_t* r) {
-  Fp v[N];
-#pragma unroll
-  for (int i = 0; i < N; ++i) v[i] = ws_get(w, term_of(r[i]));
+// Signed sum of the first npos (+) then nneg (-) terms of r[0 .. N): each term one slot load of
+// the value or its stored negation, then one modular add.  The loop is unrolled over the record's
+// maximum length; lanes with fewer terms are simply masked off for the tail.
+template <int N> GBV_HD Fp lin_eval(const Ws& w, const uint32_t* r, uint32_t npos, uint32_t nneg) {
+  const uint32_t n = npos + nneg;
   Fp acc = fp_zero();
 #pragma unroll
   for (int i = 0; i < N; ++i) {
-    int c = (int16_t)(r[i] >> 16);
-    int m = c < 0 ? -c : c;
-    Fp s = v[i];
-    if (m > 1) s = scale_small(s, m);  // rare (doubling / cyclotomic constants)
-    Fp t = fp_sel(c < 0, fp_neg_raw(s), s);
-    t = fp_sel(c == 0, fp_zero(), t);
-    acc = fp_add(acc, t);
+    if ((uint32_t)i < n) {
+      uint32_t t = r[i];
+      Fp v = get_signed(term_slot(w, t), (uint32_t)i >= npos);
+      uint32_t m = t >> 16;
+      if (m > 1) v = scale_small(v, (int)m);  // rare (doubling / cyclotomic constants)
+      acc = i == 0 ? v : fp_add(acc, v);
+    }
   }
   return acc;
 }
 
-GBV_HD void prod_lane(const uint32_t (&r)[2 * OPW], int k, const Ws& w) {
-  Fp x = lin_eval<OPW>(w, r);
-  Fp y = lin_eval<OPW>(w, r + OPW);
-  st(w.mem + w.z + k, fp_mul(x, y));
+// Copy n (multiple of 4) words into registers with 16-byte loads: one memory latency per record.
+template <int N> GBV_HD void load_words(uint32_t (&r)[N], const uint32_t* t) {
+  static_assert(N % 4 == 0, "records are whole 16-byte units");
+  const uint4* q = (const uint4*)t;
+#pragma unroll
+  for (int i = 0; i < N / 4; ++i) {
+    uint4 x = q[i];
+    r[4 * i] = x.x;
+    r[4 * i + 1] = x.y;
+    r[4 * i + 2] = x.z;
+    r[4 * i + 3] = x.w;
+  }
 }
 
-GBV_HD void part_lane(const Prog& P, const uint32_t (&r)[8], int j, const Ws& w) {
-  st(w.mem + w.z + P.round_end[P.n_rounds - 1] + j, lin_eval<8>(w, r));
+GBV_HD void prod_lane(const uint32_t (&r)[PROD_WORDS], int k, const Ws& w) {
+  uint32_t h = r[0];
+  Fp x = lin_eval<OPW>(w, r + 1, h & 0xFF, (h >> 8) & 0xFF);
+  Fp y = lin_eval<OPW>(w, r + 1 + OPW, (h >> 16) & 0xFF, h >> 24);
+  put(w.mem + w.z + k, fp_mul(x, y));
 }
+
+GBV_HD Fp sum_lane(const uint32_t (&r)[SUM_WORDS], const Ws& w) { return lin_eval<SUM_TERMS>(w, r + 1, r[0] & 0xFF, (r[0] >> 8) & 0xFF); }
 
 #if defined(GBV_HOST_TEST)
 inline unsigned lane_id() { return 0; }
 inline void barrier() {}
+inline void load_consts() {
+  for (int i = 0; i < N_CONSTS_MAX && i < N_CONSTS; ++i) put(g_consts + i, CONSTS[i]);
+}
 
 // Host: the lanes of each phase run one after another.
 inline void run(const Prog& P, const Ws& w) {
   int p0 = 0;
-  uint32_t rec[2 * OPW], r8[8];
+  uint32_t rec[PROD_WORDS], r8[SUM_WORDS];
   for (int r = 0; r < P.n_rounds; ++r) {
     for (int k = p0; k < P.round_end[r]; ++k) {
-      load_terms(rec, P.prods + 2 * OPW * k);
+      load_words(rec, P.prods + PROD_WORDS * k);
       prod_lane(rec, k, w);
     }
     p0 = P.round_end[r];
   }
   for (int j = 0; j < P.n_part; ++j) {
-    load_terms(r8, P.parts + 8 * j);
-    part_lane(P, r8, j, w);
+    load_words(r8, P.parts + SUM_WORDS * j);
+    put(w.mem + w.z + P.round_end[P.n_rounds - 1] + j, sum_lane(r8, w));
   }
   Fp o[LANES];
   for (int k = 0; k < P.n_out; ++k) {
-    load_terms(r8, P.outs + 8 * k);
-    o[k] = lin_eval<8>(w, r8);
+    load_words(r8, P.outs + SUM_WORDS * k);
+    o[k] = sum_lane(r8, w);
   }
-  for (int k = 0; k < P.n_out; ++k) st(w.mem + w.op[P.out_dst[k]] + P.out_idx[k], o[k]);
+  for (int k = 0; k < P.n_out; ++k) put(w.mem + w.op[P.out_dst[k]] + P.out_idx[k], o[k]);
 }
 #define COOP_LANES(l) for (unsigned l = 0; l < (unsigned)LANES; ++l)
 #define COOP_LANE0 if (true)
 #else
 __device__ inline unsigned lane_id() { return threadIdx.x; }
 __device__ inline void barrier() { __syncthreads(); }
+// Every kernel that runs programs calls this first (lane-parallel copy of the constant pool).
+__device__ inline void load_consts() {
+  if (threadIdx.x < N_CONSTS) put(GBV_CONSTS_LDS + threadIdx.x, CONSTS[threadIdx.x]);
+  __syncthreads();
+}
 
 // All of a lane's records for this program are fetched up front (one memory latency), the next
 // round's while the current round computes.
-__device__ __noinline__ void run_ni(const Prog* PP, LFp* mem, uint32_t op01, uint32_t op23, uint32_t op45, uint32_t z) {
+__device__ __noinline__ void run_ni(const Prog* PP, LSlot* mem, uint32_t op01, uint32_t op23, uint32_t op45, uint32_t z) {
   const Prog& P = *PP;
   const Ws w{mem, {(uint16_t)op01, (uint16_t)(op01 >> 16), (uint16_t)op23, (uint16_t)(op23 >> 16), (uint16_t)op45, (uint16_t)(op45 >> 16)},
              (uint16_t)z};
   const int lane = (int)threadIdx.x;
-  uint32_t rec[2 * OPW], rpart[8], rout[8];
+  uint32_t rec[PROD_WORDS], rpart[SUM_WORDS], rout[SUM_WORDS];
   bool have_part = lane < P.n_part, have_out = lane < P.n_out;
   int p0 = 0;
-  if (lane < P.round_end[0]) load_terms(rec, P.prods + 2 * OPW * lane);
-  if (have_part) load_terms(rpart, P.parts + 8 * lane);
-  if (have_out) load_terms(rout, P.outs + 8 * lane);
+  if (lane < P.round_end[0]) load_words(rec, P.prods + PROD_WORDS * lane);
+  if (have_part) load_words(rpart, P.parts + SUM_WORDS * lane);
+  if (have_out) load_words(rout, P.outs + SUM_WORDS * lane);
   for (int r = 0; r < P.n_rounds; ++r) {
     int p1 = P.round_end[r];
     if (p0 + lane < p1) prod_lane(rec, p0 + lane, w);  // every round has <= 64 products
-    if (r + 1 < P.n_rounds && p1 + lane < P.round_end[r + 1]) load_terms(rec, P.prods + 2 * OPW * (p1 + lane));
+    if (r + 1 < P.n_rounds && p1 + lane < P.round_end[r + 1]) load_words(rec, P.prods + PROD_WORDS * (p1 + lane));
     p0 = p1;
     __syncthreads();
   }
-  if (have_part) part_lane(P, rpart, lane, w);
+  if (have_part) put(w.mem + w.z + P.round_end[P.n_rounds - 1] + lane, sum_lane(rpart, w));
   if (P.n_part) __syncthreads();
   Fp o;
-  if (have_out) o = lin_eval<8>(w, rout);
+  if (have_out) o = sum_lane(rout, w);
   __syncthreads();
-  if (have_out) st(w.mem + w.op[P.out_dst[lane]] + P.out_idx[lane], o);
+  if (have_out) put(w.mem + w.op[P.out_dst[lane]] + P.out_idx[lane], o);
   __syncthreads();
 }
 // One out-of-line copy of the interpreter serves every call site (the drivers make hundreds).
@@ -218,44 +252,61 @@ __device__ inline void run(const Prog& P, const Ws& w) {
 #endif
 
 // ---- operand helpers (lane-parallel, end with a barrier) ------------------------------------
-GBV_HD void set_one12(Fp* fg) {
-  LFp* f = GBV_LDS(fg);
-  COOP_LANES(l) if (l < 12) st(f + l, l == 0 ? FP_ONE : fp_zero());
+GBV_HD void set_one12(Slot* fg) {
+  LSlot* f = GBV_LDS(fg);
+  COOP_LANES(l) if (l < 12) put(f + l, l == 0 ? FP_ONE : fp_zero());
   barrier();
 }
-GBV_HD void copy(Fp* dstg, const Fp* srcg, unsigned n) {
-  LFp* dst = GBV_LDS(dstg);
-  const LFp* src = GBV_LDS(srcg);
-  COOP_LANES(l) if (l < n) st(dst + l, ld(src + l));
+GBV_HD void copy(Slot* dstg, const Slot* srcg, unsigned n) {
+  LSlot* dst = GBV_LDS(dstg);
+  const LSlot* src = GBV_LDS(srcg);
+  COOP_LANES(l) if (l < n) put_pair(dst + l, get_signed(src + l, false), get_signed(src + l, true));
   barrier();
 }
-GBV_HD void conj12(Fp* fg) {  // negate the w-odd half (coordinates 6..11)
-  LFp* f = GBV_LDS(fg);
-  COOP_LANES(l) if (l >= 6 && l < 12) st(f + l, fp_neg(ld(f + l)));
+GBV_HD void conj12(Slot* fg) {  // negate the w-odd half (coordinates 6..11): swap value and negation
+  LSlot* f = GBV_LDS(fg);
+  COOP_LANES(l) if (l >= 6 && l < 12) {
+    Fp a = get_signed(f + l, false), na = get_signed(f + l, true);
+    put_pair(f + l, na, a);
+  }
   barrier();
 }
-GBV_HD bool is_one12(const Fp* f) {
+// Fp12 <-> 12 consecutive slots
+GBV_HD Fp12 load12(const Slot* fg) {
+  const LSlot* f = GBV_LDS(fg);
+  Fp12 r;
+  Fp* d = (Fp*)&r;
+  for (int i = 0; i < 12; ++i) d[i] = get(f + i);
+  return r;
+}
+GBV_HD void store12(Slot* fg, const Fp12& a) {
+  LSlot* f = GBV_LDS(fg);
+  const Fp* s = (const Fp*)&a;
+  for (int i = 0; i < 12; ++i) put(f + i, s[i]);
+}
+GBV_HD bool is_one12(const Slot* fg) {
+  const LSlot* f = GBV_LDS(fg);
   bool ok = true;
-  for (int i = 0; i < 12; ++i) ok = ok && fp_eq(f[i], i == 0 ? FP_ONE : fp_zero());
+  for (int i = 0; i < 12; ++i) ok = ok && fp_eq(get(f + i), i == 0 ? FP_ONE : fp_zero());
   return ok;
 }
 
-GBV_HD Ws ws2(Fp* mem, uint16_t z, uint16_t a, uint16_t b) { return Ws{GBV_LDS(mem), {a, b, 0, 0, 0, 0}, z}; }
-GBV_HD Ws ws3(Fp* mem, uint16_t z, uint16_t a, uint16_t b, uint16_t c) { return Ws{GBV_LDS(mem), {a, b, c, 0, 0, 0}, z}; }
+GBV_HD Ws ws2(Slot* mem, uint16_t z, uint16_t a, uint16_t b) { return Ws{GBV_LDS(mem), {a, b, 0, 0, 0, 0}, z}; }
+GBV_HD Ws ws3(Slot* mem, uint16_t z, uint16_t a, uint16_t b, uint16_t c) { return Ws{GBV_LDS(mem), {a, b, c, 0, 0, 0}, z}; }
 
-GBV_HD void mul12(Fp* mem, uint16_t z, uint16_t a, uint16_t b, uint16_t c) { run(FP12_MUL, ws3(mem, z, a, b, c)); }
-GBV_HD void cyc_sqr12(Fp* mem, uint16_t z, uint16_t a, uint16_t c) { run(FP12_CYC_SQR, ws2(mem, z, a, c)); }
-GBV_HD void frob12(Fp* mem, uint16_t z, int n, uint16_t a, uint16_t c) { run(n == 1 ? FP12_FROB1 : FP12_FROB2, ws2(mem, z, a, c)); }
+GBV_HD void mul12(Slot* mem, uint16_t z, uint16_t a, uint16_t b, uint16_t c) { run(FP12_MUL, ws3(mem, z, a, b, c)); }
+GBV_HD void cyc_sqr12(Slot* mem, uint16_t z, uint16_t a, uint16_t c) { run(FP12_CYC_SQR, ws2(mem, z, a, c)); }
+GBV_HD void frob12(Slot* mem, uint16_t z, int n, uint16_t a, uint16_t c) { run(n == 1 ? FP12_FROB1 : FP12_FROB2, ws2(mem, z, a, c)); }
 
 // ---- Miller loop over up to 2 pairs ---------------------------------------------------------
-// Workspace layout (Fp offsets), MILLER_WS Fp in total:
+// Workspace layout (slot offsets), MILLER_WS slots in total:
 //   F 0..11 | L 12..17 | per pair j: T 18+12j (6), Q 24+12j (4), P 28+12j (2: -xP, yP) | Z 42..169
 constexpr uint16_t M_F = 0, M_L = 12, M_PAIR = 18, M_Z = 42;
 constexpr int MILLER_WS = M_Z + ZSLOTS;
 
 // Load pair j: P affine G1, Q affine G2 (neither infinity).  Lane-parallel, ends with a barrier.
-GBV_HD void miller_load_pair(Fp* mem, int j, const G1A& P, const G2A& Q) {
-  LFp* b = GBV_LDS(mem + M_PAIR + 12 * j);
+GBV_HD void miller_load_pair(Slot* mem, int j, const G1A& P, const G2A& Q) {
+  LSlot* b = GBV_LDS(mem + M_PAIR + 12 * j);
   COOP_LANES(l) {
     if (l < 12) {
       Fp v;
@@ -273,14 +324,14 @@ GBV_HD void miller_load_pair(Fp* mem, int j, const G1A& P, const G2A& Q) {
         case 10: v = fp_neg(P.x); break;
         default: v = P.y; break;
       }
-      st(b + l, v);
+      put(b + l, v);
     }
   }
   barrier();
 }
 
 // F = prod_j f_{|x|, Q_j}(P_j), conjugated (x < 0).  Pairs must be loaded first.
-GBV_HD void miller_loop(Fp* mem, int npairs) {
+GBV_HD void miller_loop(Slot* mem, int npairs) {
   set_one12(mem + M_F);
   for (int i = 62; i >= 0; --i) {
     if (i != 62) run(FP12_SQR, ws2(mem, M_Z, M_F, M_F));
@@ -301,24 +352,13 @@ GBV_HD void miller_loop(Fp* mem, int npairs) {
 }
 
 // ---- final exponentiation: f^(3 (p^12 - 1)/r) == 1 ? -----------------------------------------
-// Workspace (Fp offsets): F 0..11 (input, clobbered) | INV 12 | T 24 | A 36 | B 48 | C 60 |
+// Workspace (slot offsets): F 0..11 (input, clobbered) | INV 12 | T 24 | A 36 | B 48 | C 60 |
 // TMP 72 | TMP2 84 | Z 96..223
 constexpr uint16_t E_F = 0, E_INV = 12, E_T = 24, E_A = 36, E_B = 48, E_C = 60, E_TMP = 72, E_TMP2 = 84, E_Z = 96;
 constexpr int FINAL_EXP_WS = E_Z + ZSLOTS;
 
-GBV_HD Fp12 load12(const Fp* f) {
-  Fp12 r;
-  Fp* d = (Fp*)&r;
-  for (int i = 0; i < 12; ++i) d[i] = f[i];
-  return r;
-}
-GBV_HD void store12(Fp* f, const Fp12& a) {
-  const Fp* s = (const Fp*)&a;
-  for (int i = 0; i < 12; ++i) f[i] = s[i];
-}
-
 // r = a^x (a in the cyclotomic subgroup)
-GBV_HD void exp_x(Fp* mem, uint16_t a, uint16_t r) {
+GBV_HD void exp_x(Slot* mem, uint16_t a, uint16_t r) {
   copy(mem + r, mem + a, 12);
   for (int i = 62; i >= 0; --i) {
     cyc_sqr12(mem, E_Z, r, r);
@@ -328,7 +368,7 @@ GBV_HD void exp_x(Fp* mem, uint16_t a, uint16_t r) {
 }
 
 // f (at mem + E_F) -> returns f^(3 (p^12-1)/r) == 1 (same value on every lane)
-GBV_HD bool final_exp_is_one(Fp* mem) {
+GBV_HD bool final_exp_is_one(Slot* mem) {
   COOP_LANE0 store12(mem + E_INV, fp12_inv(load12(mem + E_F)));  // one scalar inversion
   barrier();
   conj12(mem + E_F);

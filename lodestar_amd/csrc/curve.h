@@ -428,6 +428,37 @@ GBV_NI bool randomize_pair(G1A P, G2A Q, uint64_t r64, G1J* rP, G2J* rQ) {
   return randomize_pair_tab(P, Q, r64, rP, rQ, t1, t2);
 }
 
+// randomize_pair with P in Jacobian coordinates (an aggregate pubkey straight from the gather-sum,
+// never normalised): phi(X : Y : Z) = (beta X : Y : Z), so P +- phi(P) are two full additions and
+// the tables are normalised by the same single shared inversion -- no inversion for P itself.
+GBV_NI bool randomize_pair_jac(G1J P, G2A Q, uint64_t r64, G1J* rP, G2J* rQ) {
+  G1J ph{fp_mul(P.x, FP_BETA), P.y, P.z};
+  G2A qh = g2_neg_psi2(Q);
+  G1J a1 = jac_add(P, ph);
+  G1J a2 = jac_add(P, jac_neg(ph));
+  G2J b1 = jac_add_aff(jac_from_aff(Q), qh);
+  G2J b2 = jac_add_aff(jac_from_aff(Q), G2A{qh.x, fp2_neg(qh.y)});
+  Fp2 W = fp2_mul(b1.z, b2.z);
+  Fp nW = fp_add(fp_sqr(W.c0), fp_sqr(W.c1));
+  Fp u = fp_mul(a1.z, a2.z);
+  Fp tot = fp_mul(u, nW);
+  if (fp_is_zero(tot)) return false;
+  Fp inv = fp_inv(tot);
+  Fp inv_u = fp_mul(inv, nW);
+  Fp inv_nW = fp_mul(inv, u);
+  Fp2 Winv = fp2_mul_fp(fp2_conj(W), inv_nW);
+  RegTab2<G1A> t1;
+  RegTab2<G2A> t2;
+  t1.store(0, aff_from_jac_inv(a1, fp_mul(a2.z, inv_u)));
+  t1.store(1, aff_from_jac_inv(a2, fp_mul(a1.z, inv_u)));
+  t2.store(0, aff_from_jac_inv(b1, fp2_mul(b2.z, Winv)));
+  t2.store(1, aff_from_jac_inv(b2, fp2_mul(b1.z, Winv)));
+  uint32_t sa = (uint32_t)r64, sb = (uint32_t)(r64 >> 32);
+  *rP = jac_mul_2d_signed_tab<Fp>(t1, sa, sb);
+  *rQ = jac_mul_2d_signed_tab<Fp2>(t2, sa, sb);
+  return true;
+}
+
 // [r] P in one group only (same r = a - b x^2 as randomize_pair): the same-message path's G1 term
 // when the G2 sum of a large segment comes from the bucket MSM (k_msm.hip), and the G2 term when
 // a failing segment needs its per-set r_i sig_i after all.  E(P) = phi(P) or -psi^2(P).

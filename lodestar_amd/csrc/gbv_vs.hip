@@ -38,7 +38,7 @@ struct gbv_vs_batch {
   uint32_t *set_off = nullptr, *arena = nullptr, *agg_list = nullptr, *chunk_off = nullptr, *siglen = nullptr;
   uint8_t *raw_flag = nullptr, *raw_pk = nullptr, *msgs = nullptr, *sig = nullptr;
   // work
-  G1A* pk = nullptr;
+  G1J* pk = nullptr;  // aggregate pubkeys (Jacobian, k_vs_agg)
   uint8_t* pk_st = nullptr;
   G2A* H = nullptr;
   G1J* rP = nullptr;
@@ -221,8 +221,10 @@ static int vs_fill(gbv_ctx* c, gbv_vs_batch* b, size_t n_calls, const uint32_t* 
   return GBV_OK;
 }
 
-// Per-set kernels (aggregate, hash + signature + randomisation, Miller values) on stream A.
-static int vs_enqueue_sets(gbv_ctx* c, gbv_vs_batch* b) {
+// Per-set kernels: aggregate and hash + signature + randomisation on stream A, the Miller values on
+// stream m (a tail stream, so that they overlap the next batch's stream-A kernels; or stream A).
+// Events: ev0 agg ev1 hash_sig ev2 | (m) ev3 miller ev4.
+static int vs_enqueue_sets(gbv_ctx* c, gbv_vs_batch* b, hipStream_t m) {
   hipStream_t s = c->stream;
   Seed seed = fresh_seed();
   uint32_t nonce = c->nonce++;
@@ -232,8 +234,10 @@ static int vs_enqueue_sets(gbv_ctx* c, gbv_vs_batch* b) {
   launch_vs_hash_sig(s, (uint32_t)b->n, b->msgs, b->set_off, b->arena, b->raw_flag, b->raw_pk, b->sig, b->sig_stride, b->siglen, c->table,
                      c->table_ok, b->pk, b->pk_st, seed, nonce, b->H, b->rP, b->rS, b->status);
   HIP_CHECK(c, hipEventRecord(b->ev[2], s));
-  launch_vs_miller(LaunchCfg{blocks_for(b->n), TPB, s}, (uint32_t)b->n, b->status, b->rP, b->H, b->F);
-  HIP_CHECK(c, hipEventRecord(b->ev[3], s));
+  if (m != s) HIP_CHECK(c, hipStreamWaitEvent(m, b->ev[2], 0));
+  HIP_CHECK(c, hipEventRecord(b->ev[3], m));
+  launch_vs_miller(LaunchCfg{blocks_for(b->n), TPB, m}, (uint32_t)b->n, b->status, b->rP, b->H, b->F);
+  HIP_CHECK(c, hipEventRecord(b->ev[4], m));
   HIP_CHECK(c, hipGetLastError());
   return GBV_OK;
 }
@@ -269,12 +273,10 @@ int gbv_vs_batch_submit(gbv_ctx* c, gbv_vs_batch* b) {
   if (b->in_flight) return gbv_fail(c, GBV_E_ARG, "batch already in flight");
   HIP_CHECK(c, hipSetDevice(c->device));
   if (b->n == 0 || b->C == 0) return GBV_OK;
-  int rc = vs_enqueue_sets(c, b);
-  if (rc) return rc;
   b->tail = (int)(c->sm_submits++ & 1);
   hipStream_t t = b->tail ? c->stream3 : c->stream2;
-  HIP_CHECK(c, hipStreamWaitEvent(t, b->ev[3], 0));
-  HIP_CHECK(c, hipEventRecord(b->ev[4], t));
+  int rc = vs_enqueue_sets(c, b, t);
+  if (rc) return rc;
   launch_vs_chunk_coop(LaunchCfg{(unsigned)b->C, 64, t}, (uint32_t)b->C, b->chunk_off, b->status, b->F, b->rS, b->chunk_valid);
   HIP_CHECK(c, hipEventRecord(b->ev[5], t));
   HIP_CHECK(c, hipMemcpyAsync(b->chunk_valid_host, b->chunk_valid, b->C, hipMemcpyDeviceToHost, t));
@@ -291,10 +293,9 @@ int gbv_vs_batch_wait(gbv_ctx* c, gbv_vs_batch* b, uint8_t* call_valid) {
     b->in_flight = false;
     HIP_CHECK(c, hipEventSynchronize(b->done));
     float ms[4] = {};
-    for (int k = 0; k < 4; ++k) {
-      int a = k < 3 ? k : 4;
-      if (hipEventElapsedTime(&ms[k], b->ev[a], b->ev[a + 1]) != hipSuccess) ms[k] = 0.f;
-    }
+    const int from[4] = {0, 1, 3, 4};  // agg, hash_sig, miller, chunk checks
+    for (int k = 0; k < 4; ++k)
+      if (hipEventElapsedTime(&ms[k], b->ev[from[k]], b->ev[from[k] + 1]) != hipSuccess) ms[k] = 0.f;
     memcpy(c->last_vs_ms, ms, sizeof ms);
   } else if (b->n && b->C) {
     return gbv_fail(c, GBV_E_ARG, "batch not submitted");
@@ -380,8 +381,8 @@ int gbv_vs_partial(gbv_ctx* c, const gbv_set* sets, size_t n, const uint32_t* ar
     b->part_cap = np;
   }
   HIP_CHECK(c, hipSetDevice(c->device));
-  if ((rc = vs_enqueue_sets(c, b))) return rc;
   hipStream_t s = c->stream;
+  if ((rc = vs_enqueue_sets(c, b, s))) return rc;
   // status doubles as the per-"chunk" state: SET_OK == GRP_PENDING (every valid set takes part);
   // the reduction is a tree over 64-set blocks (k_sm_seg_reduce, k_sm_part_reduce)
   launch_sm_seg_check(LaunchCfg{1, 64, s}, 0, (uint32_t)n, b->status, b->F, b->rS, b->Fpart, b->Spart, b->has, b->flag, b->f_out);

@@ -38,11 +38,6 @@ __device__ inline void wave_reduce_fs_coop(Fp12& f, G2J& s, int& any) {
   }
 }
 
-__device__ inline void store12(Fp* dst, const Fp12& a) {
-  const Fp* s = (const Fp*)&a;
-  for (int i = 0; i < 12; ++i) dst[i] = s[i];
-}
-
 // One wave per segment: the randomised chunk equations of the whole segment are folded into one
 // check  prod_g e(P_g, H(m_g)) * e(-g1, sum_g S_g) == 1  with ONE final exponentiation.  Every
 // set carries its own random 64-bit scalar, so this is blst's verifyMultipleAggregateSignatures
@@ -55,11 +50,13 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
                                                      uint8_t* __restrict__ grp_state, uint8_t* __restrict__ seg_ok,
                                                      Fp12* __restrict__ miller_out, const G2J* __restrict__ S_extra) {
   GBV_TAIL_WAVE_PRIO();
-  __shared__ Fp ws[SEG_WS];
+  __shared__ coop::Slot ws[SEG_WS];
   __shared__ int flags[2];
-  Fp* ml = ws;
-  Fp* fe = ws + coop::MILLER_WS;
+  __shared__ Fp stage[6];  // the (-g1, S) pair, staged by lane 0
+  coop::Slot* ml = ws;
+  coop::Slot* fe = ws + coop::MILLER_WS;
   unsigned lane = threadIdx.x;
+  coop::load_consts();
   // fe[E_F] = product of the (<= 4) final partials (cooperative, one after another), S = their sum
   if (lane == 0) flags[0] = 0;
   coop::set_one12(fe + coop::E_F);
@@ -67,7 +64,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
   G2J s = S_extra ? S_extra[0] : jac_infinity<Fp2>();
   for (uint32_t k = 0; k < nb; ++k) {
     if (!has[k]) continue;
-    if (lane < 12) fe[coop::E_TMP + lane] = ((const Fp*)&Fpart[k])[lane];
+    if (lane < 12) coop::put(fe + coop::E_TMP + lane, ((const Fp*)&Fpart[k])[lane]);
     if (lane == 0) {
       s = g2_add(s, Spart[k]);
       flags[0] = 1;
@@ -83,18 +80,18 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
       flags[1] = jac_to_aff(sa, s) ? 1 : 0;
       if (flags[1]) {
         G1A ng = g1_neg_generator();
-        // stage the pair for miller_load_pair (lane-parallel) through the Fp12 temp slots
-        ws[coop::MILLER_WS + coop::E_TMP2 + 0] = ng.x;
-        ws[coop::MILLER_WS + coop::E_TMP2 + 1] = ng.y;
-        ws[coop::MILLER_WS + coop::E_TMP2 + 2] = sa.x.c0;
-        ws[coop::MILLER_WS + coop::E_TMP2 + 3] = sa.x.c1;
-        ws[coop::MILLER_WS + coop::E_TMP2 + 4] = sa.y.c0;
-        ws[coop::MILLER_WS + coop::E_TMP2 + 5] = sa.y.c1;
+        // stage the pair for miller_load_pair (lane-parallel)
+        stage[0] = ng.x;
+        stage[1] = ng.y;
+        stage[2] = sa.x.c0;
+        stage[3] = sa.x.c1;
+        stage[4] = sa.y.c0;
+        stage[5] = sa.y.c1;
       }
     }
     coop::barrier();
     if (flags[1]) {
-      const Fp* st = fe + coop::E_TMP2;
+      const Fp* st = stage;
       coop::miller_load_pair(ml, 0, G1A{st[0], st[1]}, G2A{Fp2{st[2], st[3]}, Fp2{st[4], st[5]}});
       coop::miller_loop(ml, 1);
       coop::mul12(ws, coop::MILLER_WS + coop::E_Z, coop::MILLER_WS + coop::E_F, coop::M_F, coop::MILLER_WS + coop::E_F);
@@ -102,7 +99,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     if (!miller_out) ok = coop::final_exp_is_one(fe) ? 1 : 0;
   }
   if (miller_out) {  // shard mode: hand out the Miller product, the caller combines shards
-    if (lane < 12) ((Fp*)miller_out)[lane] = fe[coop::E_F + lane];
+    if (lane < 12) ((Fp*)miller_out)[lane] = coop::get(fe + coop::E_F + lane);
     if (lane == 0) seg_ok[0] = (uint8_t)flags[0];
     return;
   }
@@ -117,12 +114,13 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_sm_group_pairing(uint32_t g0, const uint32_t* __restrict__ grp_msg, const G1J* __restrict__ PgJ,
                                                          const G2J* __restrict__ SgJ, const G2A* __restrict__ H, const uint8_t* __restrict__ seg_ok,
                                                          uint8_t* __restrict__ grp_state, uint32_t* __restrict__ n_fallback) {
-  __shared__ Fp ws[SEG_WS];
+  __shared__ coop::Slot ws[SEG_WS];
   __shared__ Fp sa_lds[6];
   __shared__ int sa_ok;
   uint32_t g = g0 + blockIdx.x;
   if (*seg_ok || grp_state[g] != GRP_PENDING) return;  // launched unconditionally: no host round trip
   unsigned lane = threadIdx.x;
+  coop::load_consts();
   if (lane == 0) {
     G2A sa;
     G1A pa;
@@ -140,7 +138,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     coop::miller_load_pair(ws, 0, G1A{sa_lds[4], sa_lds[5]}, H[grp_msg[g]]);
     coop::miller_load_pair(ws, 1, g1_neg_generator(), G2A{Fp2{sa_lds[0], sa_lds[1]}, Fp2{sa_lds[2], sa_lds[3]}});
     coop::miller_loop(ws, 2);
-    Fp* fe = ws + coop::MILLER_WS;
+    coop::Slot* fe = ws + coop::MILLER_WS;
     coop::copy(fe + coop::E_F, ws + coop::M_F, 12);
     ok = coop::final_exp_is_one(fe);
   }
@@ -153,7 +151,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
 
 // e(P, Q) * e(-g1, S) == 1 by one wave (S = infinity drops the second pair).  Arguments must be
 // wave-uniform (the callers stage them in LDS).
-__device__ inline bool coop_pair_check(Fp* ws, const G1A& P, const G2A& Q, bool s_inf, const G2A& S) {
+__device__ inline bool coop_pair_check(coop::Slot* ws, const G1A& P, const G2A& Q, bool s_inf, const G2A& S) {
   coop::miller_load_pair(ws, 0, P, Q);
   int np = 1;
   if (!s_inf) {
@@ -161,7 +159,7 @@ __device__ inline bool coop_pair_check(Fp* ws, const G1A& P, const G2A& Q, bool 
     np = 2;
   }
   coop::miller_loop(ws, np);
-  Fp* fe = ws + coop::MILLER_WS;
+  coop::Slot* fe = ws + coop::MILLER_WS;
   coop::copy(fe + coop::E_F, ws + coop::M_F, 12);
   return coop::final_exp_is_one(fe);
 }
@@ -173,12 +171,13 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
 k_sm_fb_blocks_coop(const uint4* __restrict__ runs, const uint32_t* __restrict__ n_runs, uint32_t cap, const uint8_t* __restrict__ status,
                     const uint32_t* __restrict__ grp_msg, const G2J* __restrict__ Sh, const G1J* __restrict__ Ph, const G2A* __restrict__ H,
                     uint8_t* __restrict__ valid, uint32_t* __restrict__ set_list, uint32_t* __restrict__ n_list) {
-  __shared__ Fp ws[SEG_WS];
+  __shared__ coop::Slot ws[SEG_WS];
   __shared__ Fp st[6];
   __shared__ int flags[3];
   uint32_t cnt = min(*n_runs, cap);
   if (cnt > FB_COOP_MAX) return;
   unsigned lane = threadIdx.x;
+  if (blockIdx.x < cnt) coop::load_consts();
   for (uint32_t k = blockIdx.x; k < cnt; k += gridDim.x) {
     uint4 r = runs[k];
     if (lane == 0) {
@@ -220,9 +219,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
 k_sm_fb_sets_coop(const uint32_t* __restrict__ set_list, const uint32_t* __restrict__ n_list, const uint32_t* __restrict__ set_grp,
                   const uint32_t* __restrict__ grp_msg, const uint32_t* __restrict__ idx, const G1A* __restrict__ table,
                   const G2A* __restrict__ S, const G2A* __restrict__ H, uint8_t* __restrict__ valid) {
-  __shared__ Fp ws[SEG_WS];
+  __shared__ coop::Slot ws[SEG_WS];
   uint32_t cnt = *n_list;
   if (cnt > FB_COOP_MAX) return;
+  if (blockIdx.x < cnt) coop::load_consts();
   for (uint32_t k = blockIdx.x; k < cnt; k += gridDim.x) {
     uint32_t i = set_list[k];
     bool ok = coop_pair_check(ws, table[idx[i]], H[grp_msg[set_grp[i]]], false, S[i]);
@@ -261,11 +261,12 @@ void launch_sm_group_pairing(LaunchCfg c, uint32_t g0, uint32_t G, const uint32_
 // Product of k Fp12 Miller partials (one per shard / GPU) and ONE final exponentiation == 1?
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
 k_fp12_check(uint32_t k, const Fp12* __restrict__ parts, uint8_t* __restrict__ out) {
-  __shared__ Fp ws[coop::FINAL_EXP_WS];
+  __shared__ coop::Slot ws[coop::FINAL_EXP_WS];
   unsigned lane = threadIdx.x;
+  coop::load_consts();
   coop::set_one12(ws + coop::E_F);
   for (uint32_t j = 0; j < k; ++j) {
-    if (lane < 12) ws[coop::E_TMP + lane] = ((const Fp*)&parts[j])[lane];
+    if (lane < 12) coop::put(ws + coop::E_TMP + lane, ((const Fp*)&parts[j])[lane]);
     coop::barrier();
     coop::mul12(ws, coop::E_Z, coop::E_F, coop::E_TMP, coop::E_F);
   }
@@ -279,10 +280,11 @@ k_fp12_check(uint32_t k, const Fp12* __restrict__ parts, uint8_t* __restrict__ o
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
 k_vs_chunk_coop(const uint32_t* __restrict__ chunk_be, const uint8_t* __restrict__ status, const Fp12* __restrict__ f,
                 const G2J* __restrict__ rS, uint8_t* __restrict__ chunk_valid) {
-  __shared__ Fp ws[SEG_WS];
+  __shared__ coop::Slot ws[SEG_WS];
   __shared__ int flags[2];
-  Fp* ml = ws;
-  Fp* fe = ws + coop::MILLER_WS;
+  __shared__ Fp stage[6];
+  coop::Slot* ml = ws;
+  coop::Slot* fe = ws + coop::MILLER_WS;
   unsigned lane = threadIdx.x;
   uint32_t c = blockIdx.x;
   uint32_t b = chunk_be[2 * c], e = chunk_be[2 * c + 1];
@@ -304,21 +306,22 @@ k_vs_chunk_coop(const uint32_t* __restrict__ chunk_be, const uint8_t* __restrict
     return;
   }
   wave_reduce_fs_coop(acc, s, any);
+  coop::load_consts();
   if (lane == 0) {
     G2A sa;
     flags[0] = jac_to_aff(sa, s) ? 1 : 0;
-    store12(fe + coop::E_F, acc);
+    coop::store12(fe + coop::E_F, acc);
     G1A ng = g1_neg_generator();
-    fe[coop::E_TMP2 + 0] = ng.x;
-    fe[coop::E_TMP2 + 1] = ng.y;
-    fe[coop::E_TMP2 + 2] = sa.x.c0;
-    fe[coop::E_TMP2 + 3] = sa.x.c1;
-    fe[coop::E_TMP2 + 4] = sa.y.c0;
-    fe[coop::E_TMP2 + 5] = sa.y.c1;
+    stage[0] = ng.x;
+    stage[1] = ng.y;
+    stage[2] = sa.x.c0;
+    stage[3] = sa.x.c1;
+    stage[4] = sa.y.c0;
+    stage[5] = sa.y.c1;
   }
   coop::barrier();
   if (flags[0]) {
-    const Fp* st = fe + coop::E_TMP2;
+    const Fp* st = stage;
     coop::miller_load_pair(ml, 0, G1A{st[0], st[1]}, G2A{Fp2{st[2], st[3]}, Fp2{st[4], st[5]}});
     coop::miller_loop(ml, 1);
     coop::mul12(ws, coop::MILLER_WS + coop::E_Z, coop::MILLER_WS + coop::E_F, coop::M_F, coop::MILLER_WS + coop::E_F);

@@ -14,35 +14,49 @@ __device__ inline Fp vs_shfl_down(const Fp& a, unsigned d) {
   return r;
 }
 
-// aggregatePublicKeys over one set's validator indices (bls/utils.ts:5-20, jobItem.ts:55-62): one
-// wave per aggregate set.  Lane l gathers table entries l, l+64, ... (each lane reads its own
-// 128-byte affine record; a 128-member committee is two records per lane) and adds them, then a
-// 6-level cross-lane tree (ds_bpermute shuffles) sums the lanes.  Critical path for k = 128: 2
-// mixed additions + 6 full additions + 1 inversion, instead of 128 serial additions in one lane.
+// aggregatePublicKeys over one set's validator indices (bls/utils.ts:5-20, jobItem.ts:55-62):
+// AGG_LANES lanes per aggregate set, 64 / AGG_LANES sets per wave.  Lane j of a set gathers table
+// entries j, j + AGG_LANES, ... (each lane reads its own 128-byte affine record) and adds them
+// serially, then a log2(AGG_LANES)-level cross-lane tree (ds_bpermute shuffles inside the lane
+// group) sums the group.  For a 128-member committee: 16 mixed additions + 3 full additions of
+// latency per set, and every lane of the wave busy for all but the short tree.  The sum stays
+// Jacobian: the randomisation (randomize_pair_jac) normalises its tables with the one inversion it
+// does anyway, so no per-set inversion is spent here.
+constexpr unsigned AGG_LANES = 8;
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
-k_vs_agg(const uint32_t* __restrict__ agg_list, const uint32_t* __restrict__ set_off, const uint32_t* __restrict__ arena,
-         const G1A* __restrict__ table, const uint8_t* __restrict__ table_ok, G1A* __restrict__ pk_out, uint8_t* __restrict__ pk_st) {
-  const uint32_t s = agg_list[blockIdx.x];
-  const uint32_t b = set_off[s], e = set_off[s + 1];
-  const unsigned lane = threadIdx.x;
+k_vs_agg(uint32_t n_agg, const uint32_t* __restrict__ agg_list, const uint32_t* __restrict__ set_off, const uint32_t* __restrict__ arena,
+         const G1A* __restrict__ table, const uint8_t* __restrict__ table_ok, G1J* __restrict__ pk_out, uint8_t* __restrict__ pk_st) {
+  const unsigned lane = threadIdx.x, sub = lane % AGG_LANES;
+  const uint32_t a = blockIdx.x * (64 / AGG_LANES) + lane / AGG_LANES;
+  const bool act = a < n_agg;
+  const uint32_t s = act ? agg_list[a] : 0;
+  const uint32_t b = act ? set_off[s] : 0, e = act ? set_off[s + 1] : 0;
   G1J acc = jac_infinity<Fp>();
   int bad = 0;
-  for (uint32_t j = b + lane; j < e; j += 64) {
+  uint32_t j = b + sub;
+  if (j < e) {  // the first member starts the sum: no addition to infinity
+    uint32_t k = arena[j];
+    bad |= table_ok[k] ? 0 : 1;
+    acc = jac_from_aff(table[k]);
+    j += AGG_LANES;
+  }
+  for (; j < e; j += AGG_LANES) {
     uint32_t k = arena[j];
     bad |= table_ok[k] ? 0 : 1;
     acc = vs_g1_add_aff(acc, table[k]);
   }
-  for (unsigned d = 32; d >= 1; d >>= 1) {
+  for (unsigned d = AGG_LANES / 2; d >= 1; d >>= 1) {
     G1J o{vs_shfl_down(acc.x, d), vs_shfl_down(acc.y, d), vs_shfl_down(acc.z, d)};
-    if (lane < d) acc = vs_g1_add(acc, o);
+    int ob = __shfl_down(bad, d, 64);
+    if (sub < d) {
+      acc = vs_g1_add(acc, o);
+      bad |= ob;
+    }
   }
-  bad = __any(bad);
-  if (lane == 0) {
-    G1A a;
-    bool fin = jac_to_aff(a, acc);
-    pk_out[s] = a;
+  if (act && sub == 0) {
+    pk_out[s] = acc;
     // an infinity aggregate fails verification in blst; an invalid table slot never verifies
-    pk_st[s] = (bad || !fin) ? SET_BAD_PK : SET_OK;
+    pk_st[s] = (bad || jac_is_inf(acc)) ? SET_BAD_PK : SET_OK;
   }
 }
 
@@ -56,7 +70,7 @@ __global__ void GBV_KERNEL_ATTR k_vs_hash_sig(uint32_t n, uint32_t nb, const uin
                                               const uint8_t* __restrict__ raw_flag, const uint8_t* __restrict__ raw_pk48,
                                               const uint8_t* __restrict__ sig, uint32_t sig_stride, const uint32_t* __restrict__ sig_len,
                                               const G1A* __restrict__ table, const uint8_t* __restrict__ table_ok,
-                                              const G1A* __restrict__ pk_agg, const uint8_t* __restrict__ pk_st, Seed seed, uint32_t nonce,
+                                              const G1J* __restrict__ pk_agg, const uint8_t* __restrict__ pk_st, Seed seed, uint32_t nonce,
                                               G2A* __restrict__ H, G1J* __restrict__ rP_out, G2J* __restrict__ rS_out,
                                               uint8_t* __restrict__ status) {
   if (blockIdx.x < nb) {
@@ -70,15 +84,17 @@ __global__ void GBV_KERNEL_ATTR k_vs_hash_sig(uint32_t n, uint32_t nb, const uin
   uint32_t i = (blockIdx.x - nb) * 64 + threadIdx.x;
   if (i >= n) return;
   uint8_t st = SET_OK;
-  G1A pk;
+  G1J pk;
   if (raw_flag[i]) {
-    uint8_t ds = g1_decompress(pk, raw_pk48 + 48ull * i);
-    if (ds != PT_OK || !g1_in_subgroup(pk)) st = SET_BAD_PK;
+    G1A a;
+    uint8_t ds = g1_decompress(a, raw_pk48 + 48ull * i);
+    if (ds != PT_OK || !g1_in_subgroup(a)) st = SET_BAD_PK;
+    pk = jac_from_aff(a);
   } else {
     uint32_t b = set_off[i], e = set_off[i + 1];
     if (e - b == 1) {
       uint32_t k = arena[b];
-      pk = table[k];
+      pk = jac_from_aff(table[k]);
       if (!table_ok[k]) st = SET_BAD_PK;
     } else if (e == b) {
       st = SET_BAD_PK;  // empty aggregate: its call is rejected on the host, never verified
@@ -95,9 +111,11 @@ __global__ void GBV_KERNEL_ATTR k_vs_hash_sig(uint32_t n, uint32_t nb, const uin
   uint64_t r = prf_scalar(seed, i, nonce);
   G1J rp;
   G2J rs;
-  if (!randomize_pair(pk, s, r, &rp, &rs)) {  // unreachable for subgroup points; plain 64-bit r then
+  if (!randomize_pair_jac(pk, s, r, &rp, &rs)) {  // unreachable for subgroup points; plain 64-bit r then
+    G1A pa;
+    jac_to_aff(pa, pk);
     rs = g2_mul_u64(s, r);
-    rp = g1_mul_u64(pk, r);
+    rp = g1_mul_u64(pa, r);
   }
   rP_out[i] = rp;
   rS_out[i] = rs;
@@ -130,14 +148,16 @@ __global__ void GBV_KERNEL_ATTR k_sig_validate(uint32_t n, const uint8_t* __rest
 }
 
 void launch_vs_agg(LaunchCfg c, const uint32_t* agg_list, const uint32_t* set_off, const uint32_t* arena, const G1A* table,
-                   const uint8_t* table_ok, G1A* pk_out, uint8_t* pk_st) {
-  hipLaunchKernelGGL(k_vs_agg, dim3(c.blocks), dim3(64), 0, c.stream, agg_list, set_off, arena, table, table_ok, pk_out, pk_st);
+                   const uint8_t* table_ok, G1J* pk_out, uint8_t* pk_st) {
+  const uint32_t n_agg = c.blocks;  // c.blocks carries the aggregate-set count
+  hipLaunchKernelGGL(k_vs_agg, dim3((n_agg + 64 / AGG_LANES - 1) / (64 / AGG_LANES)), dim3(64), 0, c.stream, n_agg, agg_list, set_off, arena,
+                     table, table_ok, pk_out, pk_st);
   debug_sync(c.stream, "k_vs_agg");
 }
 
 void launch_vs_hash_sig(hipStream_t s, uint32_t n, const uint8_t* msgs32, const uint32_t* set_off, const uint32_t* arena,
                         const uint8_t* raw_flag, const uint8_t* raw_pk48, const uint8_t* sig, uint32_t sig_stride, const uint32_t* sig_len,
-                        const G1A* table, const uint8_t* table_ok, const G1A* pk_agg, const uint8_t* pk_st, const Seed& seed,
+                        const G1A* table, const uint8_t* table_ok, const G1J* pk_agg, const uint8_t* pk_st, const Seed& seed,
                         uint32_t nonce, G2A* H, G1J* rP, G2J* rS, uint8_t* status) {
   uint32_t nb = (n + 63) / 64;
   hipLaunchKernelGGL(k_vs_hash_sig, dim3(2 * nb), dim3(64), 0, s, n, nb, msgs32, set_off, arena, raw_flag, raw_pk48, sig, sig_stride,

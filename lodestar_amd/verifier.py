@@ -439,6 +439,25 @@ class GpuBlsVerifier:
         self._lib.gbv_destroy(self._ctx)
         self._ctx = None
 
+    def close_sync(self):
+        """Synchronous close for non-async owners (tests, benches): destroys the context -- its
+        streams, HBM table and buffers -- once no device pass is running."""
+        if self._closed:
+            return
+        if self._busy:
+            raise RuntimeError("close_sync() while a device pass is running: use await close()")
+        self._closed = True
+        self._jobs = []
+        self._buffered = None
+        self._lib.gbv_destroy(self._ctx)
+        self._ctx = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close_sync()
+
     def can_accept_work(self) -> bool:
         """index.ts:149-155: a device pass in flight counts as the busy pool."""
         return self._busy == 0 and len(self._jobs) < MAX_JOBS_CAN_ACCEPT_WORK

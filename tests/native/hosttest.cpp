@@ -97,17 +97,18 @@ int ht_verify(const uint8_t* pk48, const uint8_t* msg32, const uint8_t* sig, uin
 // Wave-cooperative drivers (coop.h) run lane by lane: Miller loop over 1 or 2 pairs, then the
 // final exponentiation; out = the FE value (12 canonical Fp, tower order); returns is_one.
 int ht_coop_pairing(uint8_t* out, const uint8_t* p96, const uint8_t* q192, int npairs) {
-  std::vector<Fp> mem(coop::MILLER_WS + coop::FINAL_EXP_WS);
+  coop::load_consts();
+  std::vector<coop::Slot> mem(coop::MILLER_WS + coop::FINAL_EXP_WS);
   for (int j = 0; j < npairs; ++j) {
     G1A P{load_mont(p96 + 96 * j), load_mont(p96 + 96 * j + 48)};
     G2A Q{load_fp2(q192 + 192 * j), load_fp2(q192 + 192 * j + 96)};
     coop::miller_load_pair(mem.data(), j, P, Q);
   }
   coop::miller_loop(mem.data(), npairs);
-  Fp* fe = mem.data() + coop::MILLER_WS;
+  coop::Slot* fe = mem.data() + coop::MILLER_WS;
   coop::copy(fe + coop::E_F, mem.data() + coop::M_F, 12);
   int ok = coop::final_exp_is_one(fe) ? 1 : 0;
-  for (int i = 0; i < 12; ++i) store_canon(out + 48 * i, fe[coop::E_C + i]);
+  for (int i = 0; i < 12; ++i) store_canon(out + 48 * i, coop::get(fe + coop::E_C + i));
   return ok;
 }
 // [r] P, [r] Q for the batch scalar r = a - b x^2 of the 64-bit digit word r64 (curve.h)
@@ -117,6 +118,23 @@ int ht_randomize(uint8_t* outp, uint8_t* outq, const uint8_t* p96, const uint8_t
   G1J rp;
   G2J rq;
   if (!randomize_pair(P, Q, r64, &rp, &rq)) return 0;
+  G1A pa;
+  G2A qa;
+  jac_to_aff(pa, rp);
+  jac_to_aff(qa, rq);
+  store_canon(outp, pa.x); store_canon(outp + 48, pa.y);
+  store_fp2(outq, qa.x); store_fp2(outq + 96, qa.y);
+  return 1;
+}
+// randomize_pair_jac with P given in Jacobian coordinates scaled by z (X z^2, Y z^3, z)
+int ht_randomize_jac(uint8_t* outp, uint8_t* outq, const uint8_t* p96, const uint8_t* q192, uint64_t r64, const uint8_t* z48) {
+  G1A P{load_mont(p96), load_mont(p96 + 48)};
+  G2A Q{load_fp2(q192), load_fp2(q192 + 96)};
+  Fp z = load_mont(z48), z2 = fp_sqr(z);
+  G1J PJ{fp_mul(P.x, z2), fp_mul(P.y, fp_mul(z2, z)), z};
+  G1J rp;
+  G2J rq;
+  if (!randomize_pair_jac(PJ, Q, r64, &rp, &rq)) return 0;
   G1A pa;
   G2A qa;
   jac_to_aff(pa, rp);
@@ -167,8 +185,10 @@ unsigned long long ht_count_randomize(const uint8_t* p96, const uint8_t* q192, u
   G2A Q{load_fp2(q192), load_fp2(q192 + 96)};
   G1J rp;
   G2J rq;
+  G1J PJ = jac_from_aff(P);
   g_fme_count = 0;
-  if (g1_only) randomize_g1(P, r64, &rp);
+  if (g1_only == 1) randomize_g1(P, r64, &rp);
+  else if (g1_only == 2) randomize_pair_jac(PJ, Q, r64, &rp, &rq);
   else randomize_pair(P, Q, r64, &rp, &rq);
   return g_fme_count;
 }

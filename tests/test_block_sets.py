@@ -114,6 +114,7 @@ def gpu():
     v.replicate_pubkeys(0, C.N_KEYS, C.N_KEYS, C.N_VALIDATORS - C.N_KEYS)
     assert v.pubkey_count == C.N_VALIDATORS
     yield v
+    v.close_sync()
 
 
 @pytest.mark.gpu

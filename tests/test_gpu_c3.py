@@ -40,6 +40,7 @@ def c3():
     sigs = v.util_sign(agg_sk, list(range(N_SETS)), msgs)
     sets = [AggregatedSignatureSet(c.tolist(), msgs[i], sigs[i]) for i, c in enumerate(committees)]
     yield v, sets, pks
+    v.close_sync()
 
 
 def test_c3_all_valid_and_injected(c3):

@@ -21,6 +21,7 @@ def v():
     st = ver.add_pubkeys(0, [bytes.fromhex(p) for p in FIX["keys"]["pks"]], validate=True)
     assert st == bytes(len(FIX["keys"]["pks"]))
     yield ver
+    ver.close_sync()
 
 
 def _sets(case):

@@ -34,6 +34,7 @@ def world():
     assert v.add_pubkeys(0, pks, validate=True) == bytes(N_KEYS)
     v.replicate_pubkeys(0, N_KEYS, N_KEYS, N_TABLE - N_KEYS)
     yield v, sks, pks
+    v.close_sync()
 
 
 def _workload(v, sks, n_sets, seed):

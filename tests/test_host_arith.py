@@ -206,6 +206,12 @@ def test_randomize_pair(lib, r64):
     r = _digits_scalar(r64)
     assert (int.from_bytes(op.raw[:48], "big"), int.from_bytes(op.raw[48:], "big")) == o.g1_mul(P, r)
     assert (b2fp2(oq.raw[:96]), b2fp2(oq.raw[96:])) == o.g2_mul(Q, r)
+    # the Jacobian-input variant (aggregate pubkeys, k_vs_hash_sig) with a non-trivial Z
+    lib.ht_randomize_jac.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint64, ctypes.c_char_p]
+    op, oq = buf(96), buf(192)
+    assert lib.ht_randomize_jac(op, oq, be(P[0]) + be(P[1]), fp2b(Q[0]) + fp2b(Q[1]), r64, be(0x1234567890ABCDEF << 200)) == 1
+    assert (int.from_bytes(op.raw[:48], "big"), int.from_bytes(op.raw[48:], "big")) == o.g1_mul(P, r)
+    assert (b2fp2(oq.raw[:96]), b2fp2(oq.raw[96:])) == o.g2_mul(Q, r)
 
 
 
@@ -232,6 +238,7 @@ def test_roofline_work_constants_are_counted(lib):
         assert lib.ht_count_sig_validate(o.g2_compress(sig_pt)) == bench.FME_SIG_VALIDATE
         assert lib.ht_count_randomize(p96, q192, r64, 0) == bench.FME_RANDOMIZE_PAIR
         assert lib.ht_count_randomize(p96, q192, r64, 1) == bench.FME_RANDOMIZE_G1
+        assert lib.ht_count_randomize(p96, q192, r64, 2) == bench.FME_RANDOMIZE_PAIR_JAC
         assert lib.ht_count_miller_1j(p96, q192) == bench.FME_MILLER_1J
         assert 3 * (lib.ht_count_op(1, p96, q192) - 7) == bench.FME_G1_SCAN  # full G1 addition (minus the doubling)
-    assert bench.W_VS_HASH_SIG == bench.FME_HASH_TO_G2 + bench.FME_SIG_VALIDATE + bench.FME_RANDOMIZE_PAIR
+    assert bench.W_VS_HASH_SIG == bench.FME_HASH_TO_G2 + bench.FME_SIG_VALIDATE + bench.FME_RANDOMIZE_PAIR_JAC

@@ -51,7 +51,9 @@ def test_oracle_reject_cases_and_k6():
 @pytest.fixture(scope="module")
 def v():
     from lodestar_amd import GpuBlsVerifier
-    return GpuBlsVerifier(0)
+    v = GpuBlsVerifier(0)
+    yield v
+    v.close_sync()
 
 
 @pytest.mark.gpu

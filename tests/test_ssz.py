@@ -111,7 +111,9 @@ def test_host_attestation_signing_root(hostlib):
 @pytest.fixture(scope="module")
 def v():
     from lodestar_amd import GpuBlsVerifier
-    return GpuBlsVerifier(0)
+    v = GpuBlsVerifier(0)
+    yield v
+    v.close_sync()
 
 
 @pytest.mark.gpu

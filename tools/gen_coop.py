@@ -14,9 +14,11 @@ Fp2/Fp6/Fp12, Granger-Scott cyclotomic squaring, sparse line multiplication, hom
 projective doubling/addition steps with line coefficients, Frobenius), executed symbolically.
 tests/test_coop_tables.py re-executes every program in Python against the oracle.
 
-Program encoding (all indices small; emitted as fixed-size per-lane records -- 20 terms per
-product (A: 0..9, B: 10..19), 8 per partial sum / output, padding coef 0 -- so a lane fetches its
-whole record with a few 16-byte loads, one memory latency per phase):
+Program encoding (all indices small; emitted as fixed-size per-lane u32 records -- a product is a
+header (term counts) + up to 10 A terms + up to 10 B terms, a partial sum / output a header + up to
+7 terms; within a linear form the positive terms come first, so the sign of a term is its position
+and the device reads the value or its stored negation -- a lane fetches its whole record with a few
+16-byte loads, one memory latency per phase, and evaluates only its true number of terms):
   operands 0..5 -> base pointers given at run time (program-specific signature below)
   SRC_Z = 6  -> Z[k], the k-th product of this program (then the partial sums)
   SRC_C = 7  -> CONSTS[k] (Montgomery Fp constants emitted below)
@@ -402,10 +404,32 @@ def limbs(v):
     return ["0x%08xu" % ((v >> (32 * i)) & 0xFFFFFFFF) for i in range(12)]
 
 
+PROD_WORDS, SUM_WORDS, SUM_TERMS = 24, 8, 7
+
+
+def term_word(t):
+    src, idx, c = t
+    assert 0 <= src < 16 and idx < 256 and 0 < abs(c) < 65536
+    return src | (idx << 8) | (abs(c) << 16)
+
+
+def signed_record(T, t0, tn, width):
+    """(npos, nneg, words): the terms of T[t0:t0+tn] with positive coefficients first, each term a
+    u32 (src | idx << 8 | |coef| << 16); padded to `width` words."""
+    ts = list(T[t0:t0 + tn])
+    pos = [t for t in ts if t[2] > 0]
+    neg = [t for t in ts if t[2] < 0]
+    assert len(pos) + len(neg) == len(ts) and len(ts) <= width and len(pos) < 256 and len(neg) < 256
+    words = [term_word(t) for t in pos + neg]
+    return len(pos), len(neg), words + [0] * (width - len(words))
+
+
 def emit(progs, path):
     L = ["// GENERATED by tools/gen_coop.py -- do not edit.",
          "// Wave-cooperative programs (see tools/gen_coop.py for the encoding); run by coop.h.",
          "#pragma once", '#include "fp_types.h"', "", "namespace gbv {", "namespace coop {", ""]
+    assert len(CONSTS.vals) <= 16
+    L.append("constexpr int N_CONSTS = %d;" % len(CONSTS.vals))
     L.append("GBV_COOP_TABLE Fp CONSTS[%d] = {" % max(1, len(CONSTS.vals)))
     for v in CONSTS.vals or [0]:
         L.append("    {{%s}}," % ", ".join(limbs(mont(v))))
@@ -413,28 +437,32 @@ def emit(progs, path):
     for p in progs:
         n = p["name"]
         L.append("")
-        L.append("// %s: operands %s; %d products in %d rounds, %d outputs, %d terms" % (
+        L.append("// %s: operands %s; %d products in %d rounds, %d partial sums, %d outputs, %d terms" % (
             n, ", ".join("%d=%s[%d] %s" % (i, s[0], s[1], s[2]) for i, s in enumerate(p["signature"])),
-            len(p["prods"]), len(p["round_end"]), len(p["outs"]), len(p["terms"])))
+            len(p["prods"]), len(p["round_end"]), len(p["parts"]), len(p["outs"]), len(p["terms"])))
         T = p["terms"]
-        pad = (SRC_Z, 0, 0)
+        prod_recs = []
+        for (a0, an, b0, bn) in p["prods"]:
+            pa, na, wa = signed_record(T, a0, an, OPW)
+            pb, nb, wb = signed_record(T, b0, bn, OPW)
+            hdr = pa | (na << 8) | (pb << 16) | (nb << 24)
+            prod_recs.append([hdr] + wa + wb + [0] * (PROD_WORDS - 1 - 2 * OPW))
+        prod_recs = prod_recs or [[0] * PROD_WORDS]
 
-        def rec(t0, tn, width):
-            assert tn <= width, (n, tn, width)
-            return list(T[t0:t0 + tn]) + [pad] * (width - tn)
-
-        prod_recs = [rec(a0, an, OPW) + rec(b0, bn, OPW) for (a0, an, b0, bn) in p["prods"]] or [[pad] * (2 * OPW)]
-        part_recs = [rec(t0, tn, 8) for (t0, tn, _) in p["parts"]] or [[pad] * 8]
-        out_recs = [rec(t0, tn, 8) for (t0, tn, _, _) in p["outs"]]
+        def sum_rec(t0, tn):
+            ps, ns, w = signed_record(T, t0, tn, SUM_TERMS)
+            return [ps | (ns << 8)] + w
+        part_recs = [sum_rec(t0, tn) for (t0, tn, _) in p["parts"]] or [[0] * SUM_WORDS]
+        out_recs = [sum_rec(t0, tn) for (t0, tn, _, _) in p["outs"]]
         for j, (_, _, z) in enumerate(p["parts"]):
             assert z == len(p["prods"]) + j
-        fmt = lambda recs: ",\n    ".join(", ".join("{%d, %d, %d}" % t for t in r) for r in recs)
-        L.append("GBV_COOP_TABLE Term %s_PRODS[%d][%d] __attribute__((aligned(16))) = {\n    %s};" % (
-            n, len(prod_recs), 2 * OPW, ",\n    ".join("{" + ", ".join("{%d, %d, %d}" % t for t in r) + "}" for r in prod_recs)))
-        L.append("GBV_COOP_TABLE Term %s_PARTS[%d][8] __attribute__((aligned(16))) = {\n    %s};" % (
-            n, len(part_recs), ",\n    ".join("{" + ", ".join("{%d, %d, %d}" % t for t in r) + "}" for r in part_recs)))
-        L.append("GBV_COOP_TABLE Term %s_OUTS[%d][8] __attribute__((aligned(16))) = {\n    %s};" % (
-            n, len(out_recs), ",\n    ".join("{" + ", ".join("{%d, %d, %d}" % t for t in r) + "}" for r in out_recs)))
+        fmt = lambda recs: ",\n    ".join("{" + ", ".join("0x%xu" % w for w in r) + "}" for r in recs)
+        L.append("GBV_COOP_TABLE uint32_t %s_PRODS[%d][%d] __attribute__((aligned(16))) = {\n    %s};" % (
+            n, len(prod_recs), PROD_WORDS, fmt(prod_recs)))
+        L.append("GBV_COOP_TABLE uint32_t %s_PARTS[%d][%d] __attribute__((aligned(16))) = {\n    %s};" % (
+            n, len(part_recs), SUM_WORDS, fmt(part_recs)))
+        L.append("GBV_COOP_TABLE uint32_t %s_OUTS[%d][%d] __attribute__((aligned(16))) = {\n    %s};" % (
+            n, len(out_recs), SUM_WORDS, fmt(out_recs)))
         L.append("GBV_COOP_TABLE uint8_t %s_OUT_DST[%d] = {%s};" % (n, len(p["outs"]), ", ".join(str(o[2]) for o in p["outs"])))
         L.append("GBV_COOP_TABLE uint8_t %s_OUT_IDX[%d] = {%s};" % (n, len(p["outs"]), ", ".join(str(o[3]) for o in p["outs"])))
         re = p["round_end"] + [0] * (6 - len(p["round_end"]))

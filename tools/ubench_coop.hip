@@ -8,22 +8,28 @@
 using namespace gbv;
 
 // one wave: ITER cooperative Fp12 products, in place
+__device__ inline Fp seed_fp(unsigned k) {
+  Fp a = FP_ONE;
+  a.v[1] += k;
+  return a;
+}
+
 __global__ void __launch_bounds__(64) k_coop_mul(Fp* out, int iters) {
-  __shared__ Fp ws[36 + coop::ZSLOTS];
-  if (threadIdx.x < 24) ws[threadIdx.x] = fp_add(FP_ONE, fp_zero());
-  if (threadIdx.x < 24) ws[threadIdx.x].v[1] += threadIdx.x;
+  __shared__ coop::Slot ws[36 + coop::ZSLOTS];
+  coop::load_consts();
+  if (threadIdx.x < 24) coop::put(ws + threadIdx.x, seed_fp(threadIdx.x));
   __syncthreads();
   for (int i = 0; i < iters; ++i) coop::mul12(ws, 36, 0, 12, 0);
-  if (threadIdx.x < 12) out[blockIdx.x * 12 + threadIdx.x] = ws[threadIdx.x];
+  if (threadIdx.x < 12) out[blockIdx.x * 12 + threadIdx.x] = coop::get(ws + threadIdx.x);
 }
 
 __global__ void __launch_bounds__(64) k_coop_cyc(Fp* out, int iters) {
-  __shared__ Fp ws[36 + coop::ZSLOTS];
-  if (threadIdx.x < 24) ws[threadIdx.x] = FP_ONE;
-  if (threadIdx.x < 24) ws[threadIdx.x].v[1] += threadIdx.x;
+  __shared__ coop::Slot ws[36 + coop::ZSLOTS];
+  coop::load_consts();
+  if (threadIdx.x < 24) coop::put(ws + threadIdx.x, seed_fp(threadIdx.x));
   __syncthreads();
   for (int i = 0; i < iters; ++i) coop::cyc_sqr12(ws, 36, 0, 0);
-  if (threadIdx.x < 12) out[blockIdx.x * 12 + threadIdx.x] = ws[threadIdx.x];
+  if (threadIdx.x < 12) out[blockIdx.x * 12 + threadIdx.x] = coop::get(ws + threadIdx.x);
 }
 
 // one wave, one lane: dependent Fp products (latency of the thread-level primitive)
@@ -46,7 +52,8 @@ __global__ void __launch_bounds__(64) k_fp12_mul_lat(Fp* out, int iters) {
 
 // one wave: cooperative Miller loop (1 pair) + final exponentiation, iters times
 __global__ void __launch_bounds__(64) k_coop_pairing(Fp* out, int iters) {
-  __shared__ Fp ws[coop::MILLER_WS + coop::FINAL_EXP_WS];
+  __shared__ coop::Slot ws[coop::MILLER_WS + coop::FINAL_EXP_WS];
+  coop::load_consts();
   G1A P = g1_neg_generator();
   G2A Q{Fp2{FP_ONE, FP_ONE}, Fp2{FP_B1, FP_ONE}};
   bool ok = false;
@@ -56,19 +63,20 @@ __global__ void __launch_bounds__(64) k_coop_pairing(Fp* out, int iters) {
     coop::copy(ws + coop::MILLER_WS + coop::E_F, ws + coop::M_F, 12);
     ok ^= coop::final_exp_is_one(ws + coop::MILLER_WS);
   }
-  if (threadIdx.x < 12) out[blockIdx.x * 12 + threadIdx.x] = ws[threadIdx.x];
+  if (threadIdx.x < 12) out[blockIdx.x * 12 + threadIdx.x] = coop::get(ws + threadIdx.x);
   if (threadIdx.x == 0) out[0].v[0] += ok;
 }
 
 __global__ void __launch_bounds__(64) k_coop_miller(Fp* out, int iters) {
-  __shared__ Fp ws[coop::MILLER_WS];
+  __shared__ coop::Slot ws[coop::MILLER_WS];
+  coop::load_consts();
   G1A P = g1_neg_generator();
   G2A Q{Fp2{FP_ONE, FP_ONE}, Fp2{FP_B1, FP_ONE}};
   for (int i = 0; i < iters; ++i) {
     coop::miller_load_pair(ws, 0, P, Q);
     coop::miller_loop(ws, 1);
   }
-  if (threadIdx.x < 12) out[blockIdx.x * 12 + threadIdx.x] = ws[threadIdx.x];
+  if (threadIdx.x < 12) out[blockIdx.x * 12 + threadIdx.x] = coop::get(ws + threadIdx.x);
 }
 
 // one lane: thread-level pieces that run on lane 0 inside the cooperative kernels
