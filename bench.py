@@ -52,6 +52,7 @@ MAC_PER_FME = 300  # u32 x u32 -> u64 MACs per Fp product (12-limb Montgomery: 1
 # tests/test_host_arith.py::test_roofline_work_constants_are_counted):
 FME_SIG_VALIDATE = 2111     # Signature.fromBytes(sig, true): G2 decompress + subgroup check
 FME_RANDOMIZE_G1 = 593      # r_i pk_i (endomorphism-split 32-step ladder + affine tables)
+FME_COMB_G1 = 126           # r_i pk_i from the validator's comb table (7 doublings + 7 mixed additions)
 FME_RANDOMIZE_PAIR = 2086   # r_i pk_i and r_i sig_i with one shared inversion
 FME_RANDOMIZE_PAIR_JAC = 2096  # the same with P Jacobian (aggregate pubkeys straight from k_vs_agg)
 FME_HASH_TO_G2 = 6658       # RFC 9380 hash_to_G2 (SSWU + 3-isogeny + h_eff + to affine)
@@ -59,6 +60,7 @@ FME_MILLER_1J = 7244        # Miller value of one pair, Jacobian P
 FME_G1_SCAN = 48            # 3-level 8-lane chunk scan of r_i pk_i (3 Jacobian G1 additions)
 # k_sm_prepare<false> (bench: G2 sum by bucket MSM) and <true> (per-set G2 ladders)
 W_PREPARE_FME_MSM = FME_SIG_VALIDATE + FME_RANDOMIZE_G1 + FME_G1_SCAN
+W_PREPARE_FME_MSM_COMB = FME_SIG_VALIDATE + FME_COMB_G1 + FME_G1_SCAN
 W_PREPARE_FME = FME_SIG_VALIDATE + FME_RANDOMIZE_PAIR + 177
 # k_vs_hash_sig: both block roles per set
 W_VS_HASH_SIG = FME_HASH_TO_G2 + FME_SIG_VALIDATE + FME_RANDOMIZE_PAIR_JAC
@@ -75,6 +77,8 @@ PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_latest.json")  # tools/pmc.sh 
 # (G1 affine, two 64-byte Fp slots) + table_ok 1; writes status 1 + affine signature 256 + chunk
 # group sums ((1/8 + 1/80) x (384 + 192)).  The measured traffic above this is scratch spilling.
 ALG_BYTES_PER_SET = 4 + 96 + 4 + 128 + 1 + 1 + 256 + round((1 / 8 + 1 / 80) * (384 + 192))
+# with comb tables the 128-byte table record is replaced by 8 comb entries (96 B) + the 1-byte flag
+ALG_BYTES_PER_SET_COMB = ALG_BYTES_PER_SET - 128 + 8 * 96 + 1
 # k_vs_agg gather: per member a 4-byte index + the 128-byte affine table record + its 1-byte flag
 AGG_BYTES_PER_MEMBER = 4 + 128 + 1
 
@@ -599,14 +603,15 @@ def main():
     # per launch: algorithmic MACs of the sets one k_sm_prepare launch processes / its average duration
     units_per_launch = n_mine / max(prep_launches_per_step, 1)
     t_launch = avg_launch_ms[1] * 1e-3
-    w_fme = W_PREPARE_FME_MSM if kcnt[7] > 0 else W_PREPARE_FME
+    comb = v.comb_enabled()
+    w_fme = (W_PREPARE_FME_MSM_COMB if comb else W_PREPARE_FME_MSM) if kcnt[7] > 0 else W_PREPARE_FME
     achieved = units_per_launch * w_fme * MAC_PER_FME / t_launch / 1e12 if t_launch > 0 else 0.0
     peak = PEAK_MAC_PER_S / 1e12
     traffic, pmc = pmc_evidence(units_per_launch, "k_sm_prepare<false>" if kcnt[7] > 0 else "k_sm_prepare<true>")
     roofline = {"bound": "valu-int", "kernel": "k_sm_prepare", "achieved": round(achieved, 4), "peak": peak,
                 "unit": "T u32-MAC/s", "frac": round(achieved / peak, 5),
                 "traffic": round(traffic) if traffic is not None else None, "pmc": pmc,
-                "work_per_unit_fme": w_fme, "work_per_unit_fme_survey": W_SURVEY_SAME_MESSAGE,
+                "work_per_unit_fme": w_fme, "work_per_unit_fme_survey": W_SURVEY_SAME_MESSAGE, "comb_tables": comb,
                 "frac_at_survey_work": round(achieved / peak * W_SURVEY_SAME_MESSAGE / w_fme, 5),
                 "units_per_launch": round(units_per_launch, 1),
                 "avg_launch_ms": round(float(avg_launch_ms[1]), 3),

@@ -80,6 +80,10 @@ int gbv_pubkeys_append(gbv_ctx* ctx, uint32_t first_index, const uint8_t* pk48, 
                        uint8_t* status);
 /* Number of table slots currently allocated (max index + 1). */
 size_t gbv_pubkeys_count(gbv_ctx* ctx);
+/* 1 when the per-slot comb tables for r*pk are built and used by the same-message path (default;
+ * GBV_COMB=0 in the environment at gbv_init, or a failed allocation, selects the ladder; results are
+ * identical either way).  No reference counterpart: an accelerator of index2pubkey. */
+int gbv_comb_enabled(gbv_ctx* ctx);
 
 /* IBlsVerifier.verifySignatureSets (interface.ts:47; multithread/index.ts:157-207).
  * The sets are split with chunkifyMaximizeChunkSize(sets, 128) (multithread/utils.ts:4-18) and
@@ -213,6 +217,10 @@ int gbv_util_sign(gbv_ctx* ctx, const uint8_t* sk32, size_t n, const uint32_t* g
                   size_t n_msgs, uint8_t* sig96);
 /* hash_to_G2 of n 32-byte messages, uncompressed 192-byte affine output. */
 int gbv_util_hash_to_g2(gbv_ctx* ctx, const uint8_t* msgs32, size_t n, uint8_t* out192);
+/* [r] index2pubkey[slot] (compressed) for the batch scalar r = a - b*x^2 of each 64-bit digit word,
+ * through the slot's comb table (use_comb = 1) or the endomorphism ladder (0): test hook for the
+ * tables k_sm_prepare reads. */
+int gbv_util_g1_mul_rand(gbv_ctx* ctx, const uint32_t* slots, const uint64_t* r64, size_t n, int use_comb, uint8_t* out48);
 /* Duplicate table slots: slot[dst_first + i] = slot[src_first + (i % src_n)], i < n (synthetic tables). */
 int gbv_pubkeys_replicate(gbv_ctx* ctx, uint32_t src_first, uint32_t src_n, uint32_t dst_first, size_t n);
 

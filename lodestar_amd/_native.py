@@ -20,11 +20,11 @@ GBV_E_BAD_POINT = -6
 GBV_CALL_REJECTED = 2
 
 EXPORTED_SYMBOLS = (
-    "gbv_init", "gbv_destroy", "gbv_last_error", "gbv_pubkeys_append", "gbv_pubkeys_count",
+    "gbv_init", "gbv_destroy", "gbv_last_error", "gbv_pubkeys_append", "gbv_pubkeys_count", "gbv_comb_enabled",
     "gbv_verify_sets", "gbv_verify_same_message", "gbv_verify_same_message_multi",
     "gbv_aggregate_pubkeys", "gbv_sm_batch_create", "gbv_sm_batch_verify", "gbv_sm_batch_destroy",
     "gbv_sm_batch_submit", "gbv_sm_batch_wait", "gbv_vs_partial", "gbv_fp12_check", "gbv_last_stats",
-    "gbv_last_kernel_ms", "gbv_util_sk_to_pk", "gbv_util_sign", "gbv_util_hash_to_g2",
+    "gbv_last_kernel_ms", "gbv_util_sk_to_pk", "gbv_util_sign", "gbv_util_hash_to_g2", "gbv_util_g1_mul_rand",
     "gbv_pubkeys_replicate", "gbv_sha256_digest64", "gbv_merkle_roots", "gbv_signing_roots",
     "gbv_attestation_signing_roots", "gbv_ssz_last_kernel_ms", "gbv_verify_sets_multi", "gbv_vs_batch_create",
     "gbv_vs_batch_submit", "gbv_vs_batch_wait", "gbv_vs_batch_destroy", "gbv_vs_last_kernel_ms",
@@ -82,6 +82,7 @@ def load_library(path=LIB_PATH):
         "gbv_last_error": (cp, [vp]),
         "gbv_pubkeys_append": (i32, [vp, u32, vp, sz, i32, vp]),
         "gbv_pubkeys_count": (sz, [vp]),
+        "gbv_comb_enabled": (ctypes.c_int, [vp]),
         "gbv_verify_sets": (i32, [vp, P(GbvSet), sz, vp, vp, vp]),
         "gbv_verify_same_message": (i32, [vp, vp, vp, sz, vp, vp]),
         "gbv_verify_same_message_multi": (i32, [vp, sz, vp, vp, vp, vp, vp]),
@@ -98,6 +99,7 @@ def load_library(path=LIB_PATH):
         "gbv_util_sk_to_pk": (i32, [vp, vp, sz, vp]),
         "gbv_util_sign": (i32, [vp, vp, sz, vp, vp, sz, vp]),
         "gbv_util_hash_to_g2": (i32, [vp, vp, sz, vp]),
+        "gbv_util_g1_mul_rand": (i32, [vp, vp, vp, sz, ctypes.c_int, vp]),
         "gbv_pubkeys_replicate": (i32, [vp, u32, u32, u32, sz]),
         "gbv_sha256_digest64": (i32, [vp, vp, sz, vp]),
         "gbv_merkle_roots": (i32, [vp, vp, sz, u32, vp]),

@@ -24,6 +24,7 @@ def needs_build():
 
 def _compile(src, obj, verbose):
     cmd = ["hipcc", "--offload-arch=%s" % ARCH, "-O3", "-fPIC", "-std=c++17", "-c", src, "-o", obj + ".tmp"]
+    cmd[1:1] = os.environ.get("GBV_EXTRA_CFLAGS", "").split()  # experiments only (e.g. -mllvm options)
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.check_call(cmd)

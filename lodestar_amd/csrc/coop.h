@@ -26,9 +26,11 @@ namespace gbv {
 namespace coop {
 
 // Per-lane records (tools/gen_coop.py): a product record is PROD_WORDS u32 -- header
-// (npos_A | nneg_A << 8 | npos_B << 16 | nneg_B << 24), OPW A terms, OPW B terms, padding --
-// a partial-sum / output record is SUM_WORDS u32 -- header (npos | nneg << 8), SUM_TERMS terms.
-// A term is src (bits 0-3) | idx << 8 | magnitude << 16; its sign is its position (positives first).
+// (npos_A | nneg_A << 8 | npos_B << 16 | nneg_B << 24), OPW A terms, OPW B terms, scaled-term
+// counts (nsc_A | nsc_B << 8), padding -- a partial-sum / output record is SUM_WORDS u32 -- header
+// (npos | nneg << 8 | nsc << 16), SUM_TERMS terms.  A term is src (bits 0-2) | neg << 4 | idx << 8 |
+// magnitude << 16.  Unit terms come first (+1 then -1: the sign is the position), the rare scaled
+// terms (|coefficient| > 1, sign in bit 4) last.
 struct Prog {
   uint8_t n_rounds, n_part, n_out;
   uint16_t round_end[6];
@@ -103,51 +105,84 @@ __shared__ Slot g_consts[N_CONSTS_MAX];
 #define GBV_CONSTS_LDS GBV_LDS(g_consts)
 #endif
 
-// Per-wave workspace: mem is LDS on the device; operand k of a program lives at mem + op[k].
+// Per-wave workspace addressing.  Operand k of a program lives at workspace slot op[k], the
+// program's scratch Z at slot z, the constant pool in g_consts.
+#if defined(GBV_HOST_TEST)
 struct Ws {
   LSlot* mem;
   uint16_t op[6];
   uint16_t z;
 };
-
-GBV_HD const LSlot* term_slot(const Ws& w, uint32_t t) {
-  uint32_t src = t & 0xF, idx = (t >> 8) & 0xFF;
+inline Ws make_ws(Slot* mem, uint16_t z, uint16_t o0, uint16_t o1 = 0, uint16_t o2 = 0, uint16_t o3 = 0, uint16_t o4 = 0,
+                  uint16_t o5 = 0) {
+  return Ws{mem, {o0, o1, o2, o3, o4, o5}, z};
+}
+inline LSlot* ws_slot(const Ws& w, uint32_t src, uint32_t idx) {
   if (src == SRC_C) return GBV_CONSTS_LDS + idx;
-  uint32_t base = src == SRC_Z ? w.z : src == 0 ? w.op[0] : src == 1 ? w.op[1] : src == 2 ? w.op[2]
-                 : src == 3 ? w.op[3] : src == 4 ? w.op[4] : w.op[5];
-  return w.mem + base + idx;
+  return w.mem + (src == SRC_Z ? w.z : w.op[src]) + idx;
 }
-
-// c * v for a small integer c >= 2 (rare: scaled terms of the doubling/cyclotomic formulas)
-GBV_NI Fp scale_small(Fp v, int c) {
-  Fp s = v;
-  bool have = false;
-  while (c) {
-    if (c & 1) {
-      s = have ? fp_add(s, v) : v;
-      have = true;
-    }
-    c >>= 1;
-    if (c) v = fp_dbl(v);
-  }
-  return s;
+inline Fp term_load(const Ws& w, uint32_t t, uint32_t neg) {
+  const LSlot* s = ws_slot(w, t & 7, (t >> 8) & 0xFF);
+  return neg ? s->n : s->v;
 }
+inline void ws_put(const Ws& w, uint32_t src, uint32_t idx, const Fp& a) { put(ws_slot(w, src, idx), a); }
+#else
+// Device: every source is an absolute LDS address in 64-byte units (a Slot is two units: the value,
+// then its negation), packed as 16-bit bases -- op0|op1, op2|op3, op4|op5, Z|consts -- so a term's
+// address is two selects, a shift and an add, and the load reads exactly one Fp.
+typedef __attribute__((address_space(3))) Fp LFp;
+struct Ws {
+  uint32_t b[4];
+};
+__device__ inline uint32_t lds_unit(const LSlot* p) { return (uint32_t)(size_t)p >> 6; }
+__device__ inline Ws make_ws(Slot* mem, uint16_t z, uint16_t o0, uint16_t o1 = 0, uint16_t o2 = 0, uint16_t o3 = 0, uint16_t o4 = 0,
+                             uint16_t o5 = 0) {
+  const uint32_t m = lds_unit(GBV_LDS(mem));
+  auto u = [m](uint16_t o) { return m + 2u * o; };
+  return Ws{{u(o0) | u(o1) << 16, u(o2) | u(o3) << 16, u(o4) | u(o5) << 16, u(z) | lds_unit(GBV_CONSTS_LDS) << 16}};
+}
+__device__ inline uint32_t ws_unit(const Ws& w, uint32_t src, uint32_t idx) {
+  const uint32_t pr = src >> 1;
+  const uint32_t word = pr == 0 ? w.b[0] : pr == 1 ? w.b[1] : pr == 2 ? w.b[2] : w.b[3];
+  return ((src & 1) ? word >> 16 : word & 0xFFFFu) + 2u * idx;
+}
+__device__ inline Fp term_load(const Ws& w, uint32_t t, uint32_t neg) {
+  const LFp* q = (const LFp*)(size_t)((ws_unit(w, t & 7, (t >> 8) & 0xFF) + neg) << 6);
+  Fp r;
+  r.v = q->v;
+  return r;
+}
+__device__ inline void ws_put(const Ws& w, uint32_t src, uint32_t idx, const Fp& a) {
+  LFp* q = (LFp*)(size_t)(ws_unit(w, src, idx) << 6);
+  q[0].v = a.v;
+  q[1].v = fp_neg(a).v;
+}
+#endif
 
-// Signed sum of the first npos (+) then nneg (-) terms of r[0 .. N): each term one slot load of
-// the value or its stored negation, then one modular add.  The loop is unrolled over the record's
-// maximum length; lanes with fewer terms are simply masked off for the tail.
-template <int N> GBV_HD Fp lin_eval(const Ws& w, const uint32_t* r, uint32_t npos, uint32_t nneg) {
-  const uint32_t n = npos + nneg;
+// Signed sum of a record's terms: the npos (+1) and nneg (-1) unit terms of r[0 .. N) -- each one
+// slot load of the value or its stored negation, then one modular add, unrolled over the record's
+// maximum length (lanes with fewer terms are masked off for the tail) -- then the nsc scaled terms
+// (|c| > 1: doubling / cyclotomic coefficients), read from the record in memory (rg) by a rolled
+// double-and-add loop.  No calls: the interpreter keeps its registers across the whole program.
+template <int N> GBV_HD Fp lin_eval(const Ws& w, const uint32_t* r, uint32_t npos, uint32_t nneg, uint32_t nsc, const uint32_t* rg) {
+  const uint32_t nu = npos + nneg;
   Fp acc = fp_zero();
 #pragma unroll
   for (int i = 0; i < N; ++i) {
-    if ((uint32_t)i < n) {
-      uint32_t t = r[i];
-      Fp v = get_signed(term_slot(w, t), (uint32_t)i >= npos);
-      uint32_t m = t >> 16;
-      if (m > 1) v = scale_small(v, (int)m);  // rare (doubling / cyclotomic constants)
+    if ((uint32_t)i < nu) {
+      Fp v = term_load(w, r[i], (uint32_t)i >= npos ? 1u : 0u);
       acc = i == 0 ? v : fp_add(acc, v);
     }
+  }
+  for (uint32_t j = 0; j < nsc; ++j) {
+    const uint32_t t = rg[nu + j], m = t >> 16;
+    const Fp v = term_load(w, t, (t >> 4) & 1);
+    Fp s = v;
+    for (int bit = 30 - __builtin_clz(m); bit >= 0; --bit) {  // m >= 2: below the top bit
+      s = fp_dbl(s);
+      if ((m >> bit) & 1) s = fp_add(s, v);
+    }
+    acc = (nu == 0 && j == 0) ? s : fp_add(acc, s);
   }
   return acc;
 }
@@ -166,14 +201,17 @@ template <int N> GBV_HD void load_words(uint32_t (&r)[N], const uint32_t* t) {
   }
 }
 
-GBV_HD void prod_lane(const uint32_t (&r)[PROD_WORDS], int k, const Ws& w) {
-  uint32_t h = r[0];
-  Fp x = lin_eval<OPW>(w, r + 1, h & 0xFF, (h >> 8) & 0xFF);
-  Fp y = lin_eval<OPW>(w, r + 1 + OPW, (h >> 16) & 0xFF, h >> 24);
-  put(w.mem + w.z + k, fp_mul(x, y));
+// product k: Z[k] = A * B (rg: the record in memory, for the scaled terms)
+GBV_HD void prod_lane(const uint32_t (&r)[PROD_WORDS], const uint32_t* rg, int k, const Ws& w) {
+  const uint32_t h = r[0], hs = r[1 + 2 * OPW];
+  Fp x = lin_eval<OPW>(w, r + 1, h & 0xFF, (h >> 8) & 0xFF, hs & 0xFF, rg + 1);
+  Fp y = lin_eval<OPW>(w, r + 1 + OPW, (h >> 16) & 0xFF, h >> 24, (hs >> 8) & 0xFF, rg + 1 + OPW);
+  ws_put(w, SRC_Z, (uint32_t)k, fp_mul_inl(x, y));
 }
 
-GBV_HD Fp sum_lane(const uint32_t (&r)[SUM_WORDS], const Ws& w) { return lin_eval<SUM_TERMS>(w, r + 1, r[0] & 0xFF, (r[0] >> 8) & 0xFF); }
+GBV_HD Fp sum_lane(const uint32_t (&r)[SUM_WORDS], const uint32_t* rg, const Ws& w) {
+  return lin_eval<SUM_TERMS>(w, r + 1, r[0] & 0xFF, (r[0] >> 8) & 0xFF, (r[0] >> 16) & 0xFF, rg + 1);
+}
 
 #if defined(GBV_HOST_TEST)
 inline unsigned lane_id() { return 0; }
@@ -189,20 +227,20 @@ inline void run(const Prog& P, const Ws& w) {
   for (int r = 0; r < P.n_rounds; ++r) {
     for (int k = p0; k < P.round_end[r]; ++k) {
       load_words(rec, P.prods + PROD_WORDS * k);
-      prod_lane(rec, k, w);
+      prod_lane(rec, P.prods + PROD_WORDS * k, k, w);
     }
     p0 = P.round_end[r];
   }
   for (int j = 0; j < P.n_part; ++j) {
     load_words(r8, P.parts + SUM_WORDS * j);
-    put(w.mem + w.z + P.round_end[P.n_rounds - 1] + j, sum_lane(r8, w));
+    ws_put(w, SRC_Z, P.round_end[P.n_rounds - 1] + j, sum_lane(r8, P.parts + SUM_WORDS * j, w));
   }
   Fp o[LANES];
   for (int k = 0; k < P.n_out; ++k) {
     load_words(r8, P.outs + SUM_WORDS * k);
-    o[k] = sum_lane(r8, w);
+    o[k] = sum_lane(r8, P.outs + SUM_WORDS * k, w);
   }
-  for (int k = 0; k < P.n_out; ++k) put(w.mem + w.op[P.out_dst[k]] + P.out_idx[k], o[k]);
+  for (int k = 0; k < P.n_out; ++k) ws_put(w, P.out_dst[k], P.out_idx[k], o[k]);
 }
 #define COOP_LANES(l) for (unsigned l = 0; l < (unsigned)LANES; ++l)
 #define COOP_LANE0 if (true)
@@ -217,36 +255,35 @@ __device__ inline void load_consts() {
 
 // All of a lane's records for this program are fetched up front (one memory latency), the next
 // round's while the current round computes.
-__device__ __noinline__ void run_ni(const Prog* PP, LSlot* mem, uint32_t op01, uint32_t op23, uint32_t op45, uint32_t z) {
+__device__ __noinline__ void run_ni(const Prog* PP, uint32_t b0, uint32_t b1, uint32_t b2, uint32_t b3) {
   const Prog& P = *PP;
-  const Ws w{mem, {(uint16_t)op01, (uint16_t)(op01 >> 16), (uint16_t)op23, (uint16_t)(op23 >> 16), (uint16_t)op45, (uint16_t)(op45 >> 16)},
-             (uint16_t)z};
+  const Ws w{{b0, b1, b2, b3}};
   const int lane = (int)threadIdx.x;
   uint32_t rec[PROD_WORDS], rpart[SUM_WORDS], rout[SUM_WORDS];
-  bool have_part = lane < P.n_part, have_out = lane < P.n_out;
+  const bool have_part = lane < P.n_part, have_out = lane < P.n_out;
+  const uint32_t* gpart = P.parts + SUM_WORDS * lane;
+  const uint32_t* gout = P.outs + SUM_WORDS * lane;
   int p0 = 0;
   if (lane < P.round_end[0]) load_words(rec, P.prods + PROD_WORDS * lane);
-  if (have_part) load_words(rpart, P.parts + SUM_WORDS * lane);
-  if (have_out) load_words(rout, P.outs + SUM_WORDS * lane);
+  if (have_part) load_words(rpart, gpart);
+  if (have_out) load_words(rout, gout);
   for (int r = 0; r < P.n_rounds; ++r) {
     int p1 = P.round_end[r];
-    if (p0 + lane < p1) prod_lane(rec, p0 + lane, w);  // every round has <= 64 products
+    if (p0 + lane < p1) prod_lane(rec, P.prods + PROD_WORDS * (p0 + lane), p0 + lane, w);  // every round has <= 64 products
     if (r + 1 < P.n_rounds && p1 + lane < P.round_end[r + 1]) load_words(rec, P.prods + PROD_WORDS * (p1 + lane));
     p0 = p1;
     __syncthreads();
   }
-  if (have_part) put(w.mem + w.z + P.round_end[P.n_rounds - 1] + lane, sum_lane(rpart, w));
+  if (have_part) ws_put(w, SRC_Z, P.round_end[P.n_rounds - 1] + lane, sum_lane(rpart, gpart, w));
   if (P.n_part) __syncthreads();
   Fp o;
-  if (have_out) o = sum_lane(rout, w);
+  if (have_out) o = sum_lane(rout, gout, w);
   __syncthreads();
-  if (have_out) put(w.mem + w.op[P.out_dst[lane]] + P.out_idx[lane], o);
+  if (have_out) ws_put(w, P.out_dst[lane], P.out_idx[lane], o);
   __syncthreads();
 }
 // One out-of-line copy of the interpreter serves every call site (the drivers make hundreds).
-__device__ inline void run(const Prog& P, const Ws& w) {
-  run_ni(&P, w.mem, w.op[0] | ((uint32_t)w.op[1] << 16), w.op[2] | ((uint32_t)w.op[3] << 16), w.op[4] | ((uint32_t)w.op[5] << 16), w.z);
-}
+__device__ inline void run(const Prog& P, const Ws& w) { run_ni(&P, w.b[0], w.b[1], w.b[2], w.b[3]); }
 #define COOP_LANES(l) for (unsigned l = threadIdx.x; l == threadIdx.x; l = ~0u)
 #define COOP_LANE0 if (threadIdx.x == 0)
 #endif
@@ -291,8 +328,8 @@ GBV_HD bool is_one12(const Slot* fg) {
   return ok;
 }
 
-GBV_HD Ws ws2(Slot* mem, uint16_t z, uint16_t a, uint16_t b) { return Ws{GBV_LDS(mem), {a, b, 0, 0, 0, 0}, z}; }
-GBV_HD Ws ws3(Slot* mem, uint16_t z, uint16_t a, uint16_t b, uint16_t c) { return Ws{GBV_LDS(mem), {a, b, c, 0, 0, 0}, z}; }
+GBV_HD Ws ws2(Slot* mem, uint16_t z, uint16_t a, uint16_t b) { return make_ws(mem, z, a, b); }
+GBV_HD Ws ws3(Slot* mem, uint16_t z, uint16_t a, uint16_t b, uint16_t c) { return make_ws(mem, z, a, b, c); }
 
 GBV_HD void mul12(Slot* mem, uint16_t z, uint16_t a, uint16_t b, uint16_t c) { run(FP12_MUL, ws3(mem, z, a, b, c)); }
 GBV_HD void cyc_sqr12(Slot* mem, uint16_t z, uint16_t a, uint16_t c) { run(FP12_CYC_SQR, ws2(mem, z, a, c)); }
@@ -337,13 +374,13 @@ GBV_HD void miller_loop(Slot* mem, int npairs) {
     if (i != 62) run(FP12_SQR, ws2(mem, M_Z, M_F, M_F));
     for (int j = 0; j < npairs; ++j) {
       uint16_t t = M_PAIR + 12 * j;
-      run(G2_DBL_STEP, Ws{GBV_LDS(mem), {t, (uint16_t)(t + 10), t, M_L, 0, 0}, M_Z});
+      run(G2_DBL_STEP, make_ws(mem, M_Z, t, (uint16_t)(t + 10), t, M_L));
       run(FP12_MUL_LINE, ws3(mem, M_Z, M_F, M_L, M_F));
     }
     if ((X_ABS >> i) & 1ull) {
       for (int j = 0; j < npairs; ++j) {
         uint16_t t = M_PAIR + 12 * j;
-        run(G2_ADD_STEP, Ws{GBV_LDS(mem), {t, (uint16_t)(t + 6), (uint16_t)(t + 10), t, M_L, 0}, M_Z});
+        run(G2_ADD_STEP, make_ws(mem, M_Z, t, (uint16_t)(t + 6), (uint16_t)(t + 10), t, M_L));
         run(FP12_MUL_LINE, ws3(mem, M_Z, M_F, M_L, M_F));
       }
     }

@@ -97,6 +97,12 @@ struct gbv_ctx {
   uint8_t* table_ok = nullptr;
   size_t table_cap = 0;
   size_t table_n = 0;
+  // per-slot comb tables for r pk (curve.h comb_mul; 128 affine entries = 12 KB per slot), built on
+  // append / replicate; comb_on = false (GBV_COMB=0, or an allocation that failed) -> the ladder
+  uint4* comb = nullptr;
+  uint8_t* comb_ok = nullptr;
+  size_t comb_cap = 0;
+  bool comb_on = true;
   std::string err;
   uint32_t nonce = 0;
   uint32_t sm_submits = 0;  // parity picks the tail stream of a batch

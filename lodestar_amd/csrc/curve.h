@@ -477,6 +477,114 @@ template <class F> GBV_HD bool randomize_one(const Aff<F>& P, const Aff<F>& E, u
 GBV_NI bool randomize_g1(G1A P, uint64_t r64, G1J* rP) { return randomize_one<Fp>(P, g1_phi(P), r64, rP); }
 GBV_NI bool randomize_g2(G2A Q, uint64_t r64, G2J* rQ) { return randomize_one<Fp2>(Q, g2_neg_psi2(Q), r64, rQ); }
 
+// ---- per-validator comb tables for r pk (the same-message path's G1 term) ---------------------
+// r P = a P + b phi(P) with the signed digits of randomize_pair (a_i = 2 s_i - 1, b_i = 2 t_i - 1,
+// 32 each).  An 8-row comb over the 64 digits -- column i (0..7) holds digits 8j + i (j = 0..3) of
+// a and of b --
+//   r P = sum_{i<8} 2^i G_i,   G_i = sum_{j<4} 2^{8j} (a_{8j+i} P + b_{8j+i} phi(P)),
+// so G_i is one of the 256 signed sums of the bases B = (P, 2^8 P, 2^16 P, 2^24 P, phi of those).
+// The table keeps the 128 with a positive B_7 coefficient (the others are their negatives), affine:
+// entry e has sign +B_b iff bit b of e is set (b < 7).  Evaluation is 7 doublings + 7 mixed
+// additions (~126 Fp products) against the 31 + 31 ladder steps and table inversion of
+// randomize_g1 (~593).  The table is built once per validator (k_comb_* in k_table.hip), 12 KB
+// each: index2pubkey laid out for HBM capacity instead of recomputed per signature.
+constexpr int COMB_ENTRIES = 128;
+constexpr int COMB_U4 = 6;  // one entry: x, y limbs (96 bytes) = six 16-byte words
+
+GBV_HD uint32_t comb_digits(uint32_t sa, uint32_t sb, int i) {
+  uint32_t d = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    d |= ((sa >> (8 * j + i)) & 1u) << j;
+    d |= ((sb >> (8 * j + i)) & 1u) << (4 + j);
+  }
+  return d;
+}
+
+GBV_HD G1A comb_entry_load(const uint4* p) {
+  G1A a;
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    uint4 x = p[q], y = p[3 + q];
+    a.x.v[4 * q] = x.x, a.x.v[4 * q + 1] = x.y, a.x.v[4 * q + 2] = x.z, a.x.v[4 * q + 3] = x.w;
+    a.y.v[4 * q] = y.x, a.y.v[4 * q + 1] = y.y, a.y.v[4 * q + 2] = y.z, a.y.v[4 * q + 3] = y.w;
+  }
+  return a;
+}
+
+GBV_HD void comb_entry_store(uint4* p, const G1A& a) {
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    p[q] = uint4{a.x.v[4 * q], a.x.v[4 * q + 1], a.x.v[4 * q + 2], a.x.v[4 * q + 3]};
+    p[3 + q] = uint4{a.y.v[4 * q], a.y.v[4 * q + 1], a.y.v[4 * q + 2], a.y.v[4 * q + 3]};
+  }
+}
+
+GBV_HD G1A comb_pick(const uint4* tab, uint32_t sa, uint32_t sb, int i) {
+  const uint32_t d = comb_digits(sa, sb, i);
+  const bool pos = (d >> 7) & 1u;
+  G1A t = comb_entry_load(tab + COMB_U4 * ((pos ? d : ~d) & 127u));
+  t.y = fp_sel(pos, t.y, fp_neg(t.y));
+  return t;
+}
+
+// One comb column: R = 2 R + G_c.  Out of line, and the driver below is a plain sequence of calls:
+// with the evaluation written as one loop, the gfx950 backend (ROCm 7.2) software-pipelines the
+// next column's table loads across the loop back-edge and miscompiles the loop-carried 12-limb
+// values (tests/test_gpu_scale.py::test_comb_tables_match_ladder caught it); a call per column
+// keeps every load and its use inside one straight-line body.
+GBV_NI G1J comb_step(G1J R, const uint4* tab, uint32_t sa, uint32_t sb, int c) {
+  const G1A t = comb_pick(tab, sa, sb, c);
+  return jac_add_aff(jac_dbl(R), t);
+}
+
+// [r] P from P's comb table (r = a - b x^2 of the digit word, exactly randomize_g1's scalar)
+GBV_NI G1J comb_mul(const uint4* tab, uint32_t sa, uint32_t sb) {
+  G1J R = jac_from_aff(comb_pick(tab, sa, sb, 7));
+  R = comb_step(R, tab, sa, sb, 6);
+  R = comb_step(R, tab, sa, sb, 5);
+  R = comb_step(R, tab, sa, sb, 4);
+  R = comb_step(R, tab, sa, sb, 3);
+  R = comb_step(R, tab, sa, sb, 2);
+  R = comb_step(R, tab, sa, sb, 1);
+  return comb_step(R, tab, sa, sb, 0);
+}
+
+// The comb bases B[0..7] (affine) and D = 2 P, with one shared inversion.  P affine, in G1.
+GBV_HD void comb_bases(const G1A& P, G1A B[8], G1A& D) {
+  G1J J[4];  // 2P, 2^8 P, 2^16 P, 2^24 P
+  G1J t = jac_dbl(jac_from_aff(P));
+  J[0] = t;
+  for (int k = 1; k < 4; ++k) {
+    for (int q = 0; q < (k == 1 ? 7 : 8); ++q) t = jac_dbl(t);
+    J[k] = t;
+  }
+  Fp p01 = fp_mul(J[0].z, J[1].z), p012 = fp_mul(p01, J[2].z);
+  Fp inv = fp_inv(fp_mul(p012, J[3].z));
+  Fp i3 = fp_mul(inv, p012);
+  inv = fp_mul(inv, J[3].z);  // (z0 z1 z2)^-1
+  Fp i2 = fp_mul(inv, p01);
+  inv = fp_mul(inv, J[2].z);  // (z0 z1)^-1
+  Fp i1 = fp_mul(inv, J[0].z), i0 = fp_mul(inv, J[1].z);
+  D = aff_from_jac_inv(J[0], i0);
+  B[0] = P;
+  B[1] = aff_from_jac_inv(J[1], i1);
+  B[2] = aff_from_jac_inv(J[2], i2);
+  B[3] = aff_from_jac_inv(J[3], i3);
+  for (int j = 0; j < 4; ++j) B[4 + j] = g1_phi(B[j]);
+}
+
+// entry e of the table, Jacobian (bit b of e: sign of B_b for b < 7; B_7 positive)
+GBV_HD G1J comb_entry_jac(const G1A B[8], uint32_t e) {
+  G1J R = jac_from_aff(B[7]);
+  for (int b = 6; b >= 0; --b) {
+    G1A t = B[b];
+    t.y = fp_sel((e >> b) & 1u, t.y, fp_neg(t.y));
+    R = jac_add_aff(R, t);
+  }
+  return R;
+}
+
 // Batch-scalar halves for the bucket MSM: r P = a P + b E(P) with a = 2 sa - (2^32 - 1),
 // b = 2 sb - (2^32 - 1) (odd, |a|, |b| < 2^32).  Returns |a| or |b| and the sign.
 GBV_HD uint32_t scalar_half_mag(uint32_t s, bool* neg) {

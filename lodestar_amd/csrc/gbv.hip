@@ -212,6 +212,8 @@ int gbv_init(int device, gbv_ctx** out) {
     delete c;
     return GBV_E_DEVICE;
   }
+  const char* comb_env = getenv("GBV_COMB");
+  c->comb_on = !(comb_env && comb_env[0] == '0');
   *out = c;
   return GBV_OK;
 }
@@ -227,6 +229,8 @@ void gbv_destroy(gbv_ctx* c) {
   vs_batch_free(c->vs_scratch);
   hipFree(c->table);
   hipFree(c->table_ok);
+  hipFree(c->comb);
+  hipFree(c->comb_ok);
   hipFree(c->small_dev);
   hipHostFree(c->small_host);
   for (auto* p : c->ssz_buf) hipFree(p);
@@ -240,6 +244,7 @@ void gbv_destroy(gbv_ctx* c) {
 const char* gbv_last_error(gbv_ctx* c) { return c ? c->err.c_str() : "null context"; }
 
 size_t gbv_pubkeys_count(gbv_ctx* c) { return c ? c->table_n : 0; }
+int gbv_comb_enabled(gbv_ctx* c) { return c && c->comb_on ? 1 : 0; }
 
 static int table_reserve(gbv_ctx* c, size_t need) {
   if (need <= c->table_cap) return GBV_OK;
@@ -270,6 +275,72 @@ static int table_reserve(gbv_ctx* c, size_t need) {
   return GBV_OK;
 }
 
+// ---- comb tables (curve.h comb_mul): one per table slot, grown with the table -------------------
+static constexpr size_t COMB_SLOT_BYTES = (size_t)COMB_ENTRIES * COMB_U4 * sizeof(uint4);
+
+static void comb_disable(gbv_ctx* c) {
+  hipFree(c->comb);
+  hipFree(c->comb_ok);
+  c->comb = nullptr;
+  c->comb_ok = nullptr;
+  c->comb_cap = 0;
+  c->comb_on = false;
+}
+
+// Room for `need` slots, slots [0, keep) preserved.  The tables are an accelerator, not state: when
+// HBM cannot hold them the context drops them and k_sm_prepare runs the ladder (same results).
+static int comb_reserve(gbv_ctx* c, size_t need, size_t keep) {
+  if (need <= c->comb_cap) return GBV_OK;
+  size_t cap = std::max(need, c->comb_cap * 2);
+  uint4* t = nullptr;
+  uint8_t* ok = nullptr;
+  if (hipMalloc(&t, cap * COMB_SLOT_BYTES) != hipSuccess || hipMalloc(&ok, cap) != hipSuccess) {
+    (void)hipGetLastError();
+    hipFree(t);
+    comb_disable(c);
+    return GBV_OK;
+  }
+  hipError_t e = hipMemsetAsync(ok, 0, cap, c->stream);
+  keep = std::min(keep, c->comb_cap);
+  if (e == hipSuccess && keep) {
+    e = hipMemcpyAsync(t, c->comb, keep * COMB_SLOT_BYTES, hipMemcpyDeviceToDevice, c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(ok, c->comb_ok, keep, hipMemcpyDeviceToDevice, c->stream);
+  }
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  if (e != hipSuccess) {
+    hipFree(t);
+    hipFree(ok);
+    return gbv_fail(c, GBV_E_DEVICE, std::string("comb grow: ") + hipGetErrorString(e));
+  }
+  hipFree(c->comb);
+  hipFree(c->comb_ok);
+  c->comb = t;
+  c->comb_ok = ok;
+  c->comb_cap = cap;
+  return GBV_OK;
+}
+
+// comb tables of slots [first, first + n) from their (final) table entries
+static int comb_build(gbv_ctx* c, uint32_t first, size_t n, size_t keep) {
+  if (!c->comb_on) return GBV_OK;
+  int rc = comb_reserve(c, (size_t)first + n, keep);
+  if (rc || !c->comb_on) return rc;
+  constexpr size_t CH = 65536;  // slots per pass: 9 affine bases each in scratch (75 MB)
+  G1A* bases = nullptr;
+  if (dalloc(&bases, 9 * std::min(n, CH)) != hipSuccess) {
+    (void)hipGetLastError();
+    comb_disable(c);
+    return GBV_OK;
+  }
+  for (size_t off = 0; off < n; off += CH)
+    launch_comb_build(c->stream, first + (uint32_t)off, (uint32_t)std::min(CH, n - off), c->table, c->table_ok, bases, c->comb, c->comb_ok);
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  hipFree(bases);
+  if (e != hipSuccess) return gbv_fail(c, GBV_E_DEVICE, std::string("comb build: ") + hipGetErrorString(e));
+  return GBV_OK;
+}
+
 int gbv_pubkeys_append(gbv_ctx* c, uint32_t first, const uint8_t* pk48, size_t n, int validate, uint8_t* status) {
   if (!c) return GBV_E_ARG;
   if (c->closed) return GBV_E_CLOSED;
@@ -290,8 +361,9 @@ int gbv_pubkeys_append(gbv_ctx* c, uint32_t first, const uint8_t* pk48, size_t n
   HIP_CHECK(c, hipMemcpyAsync(h, d + st_off, n, hipMemcpyDeviceToHost, c->stream));
   HIP_CHECK(c, hipStreamSynchronize(c->stream));
   if (status) memcpy(status, h, n);
+  const size_t keep = c->table_n;
   c->table_n = std::max(c->table_n, (size_t)first + n);
-  return GBV_OK;
+  return comb_build(c, first, n, keep);
 }
 
 int gbv_pubkeys_replicate(gbv_ctx* c, uint32_t src_first, uint32_t src_n, uint32_t dst_first, size_t n) {
@@ -303,7 +375,14 @@ int gbv_pubkeys_replicate(gbv_ctx* c, uint32_t src_first, uint32_t src_n, uint32
                       dst_first, (uint32_t)n);
   HIP_CHECK(c, hipGetLastError());
   HIP_CHECK(c, hipStreamSynchronize(c->stream));
+  const size_t keep = c->table_n;
   c->table_n = std::max(c->table_n, (size_t)dst_first + n);
+  if (c->comb_on && (rc = comb_reserve(c, (size_t)dst_first + n, keep)) != GBV_OK) return rc;
+  if (c->comb_on) {  // the source slots' tables are built: copy them like the table entries
+    launch_comb_replicate(c->stream, c->comb, c->comb_ok, src_first, src_n, dst_first, (uint32_t)n);
+    HIP_CHECK(c, hipGetLastError());
+    HIP_CHECK(c, hipStreamSynchronize(c->stream));
+  }
   return GBV_OK;
 }
 
@@ -560,7 +639,8 @@ int gbv_sm_batch_submit(gbv_ctx* c, gbv_sm_batch* b) {
     const bool msm = b->seg_msm[s];
     G2J* Sh = msm ? nullptr : b->rS;  // MSM segment: k_sm_prepare forms the G1 terms only
     HIP_CHECK(c, hipEventRecord(e[0], sa));
-    launch_sm_prepare(LaunchCfg{0, 64, sa}, s0, s1 - s0, b->idx, b->sig, b->set_grp, c->table, c->table_ok, (uint32_t)c->table_n, seed,
+    launch_sm_prepare(LaunchCfg{0, 64, sa}, s0, s1 - s0, b->idx, b->sig, b->set_grp, c->table, c->table_ok, (uint32_t)c->table_n,
+                      c->comb_on ? c->comb : nullptr, c->comb_ok, seed,
                       nonce, b->S, Sh, b->rP, b->status);
     HIP_CHECK(c, hipEventRecord(e[1], sa));
     // A segment of a few chunks (a lone gossip call) skips the combined check (seg_direct): each
@@ -860,6 +940,26 @@ int gbv_util_sk_to_pk(gbv_ctx* c, const uint8_t* sk32, size_t n, uint8_t* pk48) 
   launch_util_sk_to_pk(LaunchCfg{blocks_for(n), TPB, c->stream}, (uint32_t)n, d, d + o_pk);
   HIP_CHECK(c, hipGetLastError());
   HIP_CHECK(c, hipMemcpyAsync(pk48, d + o_pk, 48 * n, hipMemcpyDeviceToHost, c->stream));
+  HIP_CHECK(c, hipStreamSynchronize(c->stream));
+  return GBV_OK;
+}
+
+int gbv_util_g1_mul_rand(gbv_ctx* c, const uint32_t* slots, const uint64_t* r64, size_t n, int use_comb, uint8_t* out48) {
+  if (!c || (n && (!slots || !r64 || !out48))) return GBV_E_ARG;
+  if (n == 0) return GBV_OK;
+  if (use_comb && !c->comb_on) return gbv_fail(c, GBV_E_ARG, "comb tables disabled");
+  for (size_t i = 0; i < n; ++i)
+    if (slots[i] >= c->table_n) return gbv_fail(c, GBV_E_ARG, "slot out of range");
+  HIP_CHECK(c, hipSetDevice(c->device));
+  uint8_t* d = nullptr;
+  size_t o_r = align256(4 * n), o_o = o_r + align256(8 * n);
+  int rc = ctx_small_dev(c, o_o + 48 * n, &d);
+  if (rc) return rc;
+  HIP_CHECK(c, hipMemcpyAsync(d, slots, 4 * n, hipMemcpyHostToDevice, c->stream));
+  HIP_CHECK(c, hipMemcpyAsync(d + o_r, r64, 8 * n, hipMemcpyHostToDevice, c->stream));
+  launch_util_g1_mul_rand(c->stream, (uint32_t)n, (const uint32_t*)d, (const uint64_t*)(d + o_r), c->table, c->comb, use_comb, d + o_o);
+  HIP_CHECK(c, hipGetLastError());
+  HIP_CHECK(c, hipMemcpyAsync(out48, d + o_o, 48 * n, hipMemcpyDeviceToHost, c->stream));
   HIP_CHECK(c, hipStreamSynchronize(c->stream));
   return GBV_OK;
 }

@@ -33,9 +33,9 @@ constexpr unsigned SCAN_W = 8;  // lanes per scan group (power of two, <= 64)
 template <bool WITH_G2>
 __global__ void GBV_KERNEL_ATTR k_sm_prepare(uint32_t base, uint32_t n, const uint32_t* __restrict__ idx, const uint8_t* __restrict__ sig96,
                                              const uint32_t* __restrict__ set_grp, const G1A* __restrict__ table,
-                                             const uint8_t* __restrict__ table_ok, uint32_t table_n, Seed seed, uint32_t nonce,
-                                             G2A* __restrict__ S_out, G2J* __restrict__ Sh_out, G1J* __restrict__ Ph_out,
-                                             uint8_t* __restrict__ status) {
+                                             const uint8_t* __restrict__ table_ok, uint32_t table_n, const uint4* __restrict__ comb,
+                                             const uint8_t* __restrict__ comb_ok, Seed seed, uint32_t nonce, G2A* __restrict__ S_out,
+                                             G2J* __restrict__ Sh_out, G1J* __restrict__ Ph_out, uint8_t* __restrict__ status) {
   unsigned lane = threadIdx.x;
   uint32_t t = blockIdx.x * 64 + lane;
   bool act = t < n;
@@ -54,14 +54,21 @@ __global__ void GBV_KERNEL_ATTR k_sm_prepare(uint32_t base, uint32_t n, const ui
     if (st == SET_OK) {
       S_out[i] = s;
       uint64_t r = prf_scalar(seed, i, nonce);
-      G1A pk = table[k];
-      if (WITH_G2) {
+      if (comb && comb_ok[k]) {  // r pk from the validator's comb table (curve.h comb_mul)
+        rp = comb_mul(comb + (size_t)k * (COMB_ENTRIES * COMB_U4), (uint32_t)r, (uint32_t)(r >> 32));
+        if (WITH_G2 && !randomize_g2(s, r, &rs)) {  // unreachable for subgroup points: both terms with plain r
+          rs = g2_mul_u64(s, r);
+          rp = g1_mul_u64(table[k], r);
+        }
+      } else if (WITH_G2) {
+        G1A pk = table[k];
         if (!randomize_pair(pk, s, r, &rp, &rs)) {  // unreachable for subgroup points; plain 64-bit r then
           rs = g2_mul_u64(s, r);
           rp = g1_mul_u64(pk, r);
         }
-      } else if (!randomize_g1(pk, r, &rp)) {
-        rp = g1_mul_u64(pk, r);
+      } else {
+        G1A pk = table[k];
+        if (!randomize_g1(pk, r, &rp)) rp = g1_mul_u64(pk, r);
       }
     }
   }
@@ -366,15 +373,16 @@ void launch_sm_fb_sets(LaunchCfg c, const uint32_t* set_list, const uint32_t* n_
 }
 
 void launch_sm_prepare(LaunchCfg c, uint32_t base, uint32_t n, const uint32_t* idx, const uint8_t* sig96, const uint32_t* set_grp,
-                       const G1A* table, const uint8_t* table_ok, uint32_t table_n, const Seed& seed, uint32_t nonce, G2A* S_out, G2J* Sh,
-                       G1J* Ph, uint8_t* status) {
-  // Sh == nullptr: G1 terms only (the segment's G2 sum comes from the bucket MSM)
+                       const G1A* table, const uint8_t* table_ok, uint32_t table_n, const uint4* comb, const uint8_t* comb_ok,
+                       const Seed& seed, uint32_t nonce, G2A* S_out, G2J* Sh, G1J* Ph, uint8_t* status) {
+  // Sh == nullptr: G1 terms only (the segment's G2 sum comes from the bucket MSM); comb == nullptr:
+  // no comb tables (GBV_COMB=0 or not built), the ladder forms r pk
   if (Sh)
     hipLaunchKernelGGL(k_sm_prepare<true>, dim3((n + 63) / 64), dim3(64), 0, c.stream, base, n, idx, sig96, set_grp, table, table_ok, table_n,
-                       seed, nonce, S_out, Sh, Ph, status);
+                       comb, comb_ok, seed, nonce, S_out, Sh, Ph, status);
   else
     hipLaunchKernelGGL(k_sm_prepare<false>, dim3((n + 63) / 64), dim3(64), 0, c.stream, base, n, idx, sig96, set_grp, table, table_ok,
-                       table_n, seed, nonce, S_out, Sh, Ph, status);
+                       table_n, comb, comb_ok, seed, nonce, S_out, Sh, Ph, status);
   debug_sync(c.stream, "k_sm_prepare");
 }
 void launch_sm_redo_g2(LaunchCfg c, uint32_t base, uint32_t n, const uint32_t* set_grp, const uint8_t* status, const G2A* S, const Seed& seed,

@@ -44,7 +44,11 @@ __device__ inline void wave_reduce_fs_coop(Fp12& f, G2J& s, int& any) {
 // over the segment's sets: it passes iff every chunk would pass its own aggregate check, except
 // with probability ~2^-64 (the bound each chunk check has).  Pass -> every pending chunk is
 // valid; fail -> seg_ok = 0 and the host runs the per-chunk checks, then the per-set retries.
-constexpr int SEG_WS = coop::MILLER_WS + coop::FINAL_EXP_WS;
+// The Miller loop and the final exponentiation share one workspace (M_F == E_F): the (-g1, S)
+// Miller value is formed first, the partial products are multiplied into it, then the final
+// exponentiation runs in place -- 224 slots (28 KB of LDS) per wave.
+constexpr int SEG_WS = coop::MILLER_WS > coop::FINAL_EXP_WS ? coop::MILLER_WS : coop::FINAL_EXP_WS;
+static_assert(coop::M_F == coop::E_F, "shared Miller / final-exponentiation workspace");
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_sm_seg_check(uint32_t g0, uint32_t G, uint32_t nb, const Fp12* __restrict__ Fpart,
                                                      const G2J* __restrict__ Spart, const uint8_t* __restrict__ has,
                                                      uint8_t* __restrict__ grp_state, uint8_t* __restrict__ seg_ok,
@@ -53,53 +57,51 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
   __shared__ coop::Slot ws[SEG_WS];
   __shared__ int flags[2];
   __shared__ Fp stage[6];  // the (-g1, S) pair, staged by lane 0
-  coop::Slot* ml = ws;
-  coop::Slot* fe = ws + coop::MILLER_WS;
   unsigned lane = threadIdx.x;
   coop::load_consts();
-  // fe[E_F] = product of the (<= 4) final partials (cooperative, one after another), S = their sum
-  if (lane == 0) flags[0] = 0;
-  coop::set_one12(fe + coop::E_F);
-  // S_extra: the segment's sum r_i sig_i from the bucket MSM (k_msm.hip) when the chunks carry none
-  G2J s = S_extra ? S_extra[0] : jac_infinity<Fp2>();
-  for (uint32_t k = 0; k < nb; ++k) {
-    if (!has[k]) continue;
-    if (lane < 12) coop::put(fe + coop::E_TMP + lane, ((const Fp*)&Fpart[k])[lane]);
-    if (lane == 0) {
-      s = g2_add(s, Spart[k]);
-      flags[0] = 1;
+  // S = S_extra (the segment's sum r_i sig_i from the bucket MSM, k_msm.hip, when the chunks carry
+  // none) + the partial sums; flags[0]: any partial present
+  if (lane == 0) {
+    G2J s = S_extra ? S_extra[0] : jac_infinity<Fp2>();
+    int any = 0;
+    for (uint32_t k = 0; k < nb; ++k)
+      if (has[k]) {
+        s = g2_add(s, Spart[k]);
+        any = 1;
+      }
+    G2A sa;
+    flags[0] = any;
+    flags[1] = any && jac_to_aff(sa, s) ? 1 : 0;
+    if (flags[1]) {
+      G1A ng = g1_neg_generator();
+      stage[0] = ng.x;
+      stage[1] = ng.y;
+      stage[2] = sa.x.c0;
+      stage[3] = sa.x.c1;
+      stage[4] = sa.y.c0;
+      stage[5] = sa.y.c1;
     }
-    coop::barrier();
-    coop::mul12(fe, coop::E_Z, coop::E_F, coop::E_TMP, coop::E_F);
   }
   coop::barrier();
   int ok = 1;
   if (flags[0]) {
-    if (lane == 0) {
-      G2A sa;
-      flags[1] = jac_to_aff(sa, s) ? 1 : 0;
-      if (flags[1]) {
-        G1A ng = g1_neg_generator();
-        // stage the pair for miller_load_pair (lane-parallel)
-        stage[0] = ng.x;
-        stage[1] = ng.y;
-        stage[2] = sa.x.c0;
-        stage[3] = sa.x.c1;
-        stage[4] = sa.y.c0;
-        stage[5] = sa.y.c1;
-      }
-    }
-    coop::barrier();
     if (flags[1]) {
       const Fp* st = stage;
-      coop::miller_load_pair(ml, 0, G1A{st[0], st[1]}, G2A{Fp2{st[2], st[3]}, Fp2{st[4], st[5]}});
-      coop::miller_loop(ml, 1);
-      coop::mul12(ws, coop::MILLER_WS + coop::E_Z, coop::MILLER_WS + coop::E_F, coop::M_F, coop::MILLER_WS + coop::E_F);
+      coop::miller_load_pair(ws, 0, G1A{st[0], st[1]}, G2A{Fp2{st[2], st[3]}, Fp2{st[4], st[5]}});
+      coop::miller_loop(ws, 1);
+    } else {
+      coop::set_one12(ws + coop::E_F);
     }
-    if (!miller_out) ok = coop::final_exp_is_one(fe) ? 1 : 0;
+    for (uint32_t k = 0; k < nb; ++k) {  // F *= the (<= 4) final partials, one after another
+      if (!has[k]) continue;
+      if (lane < 12) coop::put(ws + coop::E_TMP + lane, ((const Fp*)&Fpart[k])[lane]);
+      coop::barrier();
+      coop::mul12(ws, coop::E_Z, coop::E_F, coop::E_TMP, coop::E_F);
+    }
+    if (!miller_out) ok = coop::final_exp_is_one(ws) ? 1 : 0;
   }
   if (miller_out) {  // shard mode: hand out the Miller product, the caller combines shards
-    if (lane < 12) ((Fp*)miller_out)[lane] = coop::get(fe + coop::E_F + lane);
+    if (lane < 12) ((Fp*)miller_out)[lane] = flags[0] ? coop::get(ws + coop::E_F + lane) : (lane == 0 ? FP_ONE : fp_zero());
     if (lane == 0) seg_ok[0] = (uint8_t)flags[0];
     return;
   }
@@ -138,9 +140,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     coop::miller_load_pair(ws, 0, G1A{sa_lds[4], sa_lds[5]}, H[grp_msg[g]]);
     coop::miller_load_pair(ws, 1, g1_neg_generator(), G2A{Fp2{sa_lds[0], sa_lds[1]}, Fp2{sa_lds[2], sa_lds[3]}});
     coop::miller_loop(ws, 2);
-    coop::Slot* fe = ws + coop::MILLER_WS;
-    coop::copy(fe + coop::E_F, ws + coop::M_F, 12);
-    ok = coop::final_exp_is_one(fe);
+    ok = coop::final_exp_is_one(ws);
   }
   if (lane == 0) {
     grp_state[g] = ok ? GRP_OK : GRP_FALLBACK;
@@ -159,9 +159,7 @@ __device__ inline bool coop_pair_check(coop::Slot* ws, const G1A& P, const G2A& 
     np = 2;
   }
   coop::miller_loop(ws, np);
-  coop::Slot* fe = ws + coop::MILLER_WS;
-  coop::copy(fe + coop::E_F, ws + coop::M_F, 12);
-  return coop::final_exp_is_one(fe);
+  return coop::final_exp_is_one(ws);
 }
 
 // Failure path for few items (<= FB_COOP_MAX): the run checks and per-set checks of
@@ -283,8 +281,6 @@ k_vs_chunk_coop(const uint32_t* __restrict__ chunk_be, const uint8_t* __restrict
   __shared__ coop::Slot ws[SEG_WS];
   __shared__ int flags[2];
   __shared__ Fp stage[6];
-  coop::Slot* ml = ws;
-  coop::Slot* fe = ws + coop::MILLER_WS;
   unsigned lane = threadIdx.x;
   uint32_t c = blockIdx.x;
   uint32_t b = chunk_be[2 * c], e = chunk_be[2 * c + 1];
@@ -310,7 +306,6 @@ k_vs_chunk_coop(const uint32_t* __restrict__ chunk_be, const uint8_t* __restrict
   if (lane == 0) {
     G2A sa;
     flags[0] = jac_to_aff(sa, s) ? 1 : 0;
-    coop::store12(fe + coop::E_F, acc);
     G1A ng = g1_neg_generator();
     stage[0] = ng.x;
     stage[1] = ng.y;
@@ -320,13 +315,18 @@ k_vs_chunk_coop(const uint32_t* __restrict__ chunk_be, const uint8_t* __restrict
     stage[5] = sa.y.c1;
   }
   coop::barrier();
-  if (flags[0]) {
+  if (flags[0]) {  // F = f_(-g1, sum r_i sig_i) * prod f_i (shared Miller / final-exp workspace)
     const Fp* st = stage;
-    coop::miller_load_pair(ml, 0, G1A{st[0], st[1]}, G2A{Fp2{st[2], st[3]}, Fp2{st[4], st[5]}});
-    coop::miller_loop(ml, 1);
-    coop::mul12(ws, coop::MILLER_WS + coop::E_Z, coop::MILLER_WS + coop::E_F, coop::M_F, coop::MILLER_WS + coop::E_F);
+    coop::miller_load_pair(ws, 0, G1A{st[0], st[1]}, G2A{Fp2{st[2], st[3]}, Fp2{st[4], st[5]}});
+    coop::miller_loop(ws, 1);
+    if (lane == 0) coop::store12(ws + coop::E_TMP, acc);
+    coop::barrier();
+    coop::mul12(ws, coop::E_Z, coop::E_F, coop::E_TMP, coop::E_F);
+  } else {
+    if (lane == 0) coop::store12(ws + coop::E_F, acc);
+    coop::barrier();
   }
-  bool ok = coop::final_exp_is_one(fe);
+  bool ok = coop::final_exp_is_one(ws);
   if (lane == 0) chunk_valid[c] = ok ? 1 : 0;
 }
 

@@ -13,8 +13,8 @@ void launch_hash_msgs(LaunchCfg c, const uint8_t* msgs32, uint32_t n, G2A* H);
 void launch_util_g2_out(LaunchCfg c, uint32_t n, const G2A* H, uint8_t* out192);
 
 void launch_sm_prepare(LaunchCfg c, uint32_t base, uint32_t n, const uint32_t* idx, const uint8_t* sig96, const uint32_t* set_grp,
-                       const G1A* table, const uint8_t* table_ok, uint32_t table_n, const Seed& seed, uint32_t nonce, G2A* S_out, G2J* Sh,
-                       G1J* Ph, uint8_t* status);
+                       const G1A* table, const uint8_t* table_ok, uint32_t table_n, const uint4* comb, const uint8_t* comb_ok,
+                       const Seed& seed, uint32_t nonce, G2A* S_out, G2J* Sh, G1J* Ph, uint8_t* status);
 void launch_sm_chunk_finish(LaunchCfg c, uint32_t g0, uint32_t G, uint32_t s0, const uint32_t* grp_off, const uint8_t* status, const G2J* Sh,
                             const G1J* Ph, G1J* PgJ, G2J* SgJ, uint8_t* grp_state, uint32_t* n_fallback);
 void launch_sm_miller(LaunchCfg c, uint32_t g0, uint32_t G, const uint32_t* grp_msg, const uint8_t* grp_state, const G1J* PgJ, const G2A* H,
@@ -68,6 +68,11 @@ void launch_sm_fb_sets_coop(LaunchCfg c, const uint32_t* set_list, const uint32_
                             const uint32_t* idx, const G1A* table, const G2A* S, const G2A* H, uint8_t* valid);
 
 void launch_pk_decompress(LaunchCfg c, uint32_t n, const uint8_t* pk48, int validate, G1A* table, uint8_t* table_ok, uint8_t* status);
+void launch_comb_build(hipStream_t s, uint32_t first, uint32_t n, const G1A* table, const uint8_t* table_ok, G1A* bases9, uint4* comb,
+                       uint8_t* comb_ok);
+void launch_util_g1_mul_rand(hipStream_t s, uint32_t n, const uint32_t* slots, const uint64_t* r64, const G1A* table, const uint4* comb,
+                             int use_comb, uint8_t* out48);
+void launch_comb_replicate(hipStream_t s, uint4* comb, uint8_t* comb_ok, uint32_t src_first, uint32_t src_n, uint32_t dst_first, uint32_t n);
 void launch_pk_replicate(LaunchCfg c, G1A* table, uint8_t* table_ok, uint32_t src_first, uint32_t src_n, uint32_t dst_first, uint32_t n);
 // idx == nullptr: entries 0..k-1 of table (serialized keys decompressed into scratch slots; slots
 // with table_ok == 0 -- infinity keys -- are skipped rather than flagged)

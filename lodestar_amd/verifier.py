@@ -135,6 +135,10 @@ class GpuBlsVerifier:
     def pubkey_count(self) -> int:
         return int(self._lib.gbv_pubkeys_count(self._ctx))
 
+    def comb_enabled(self):
+        """True when r*pk comes from the per-slot comb tables (12 KB of HBM per validator)."""
+        return bool(self._lib.gbv_comb_enabled(self._ctx))
+
     def aggregate_pubkeys(self, indices: Sequence[int]) -> bytes:
         """aggregatePublicKeys(index2pubkey[indices]).toBytes() (bls/utils.ts:5-20)."""
         self._check_open()
@@ -634,6 +638,17 @@ class GpuBlsVerifier:
         _native.check(self._lib, self._ctx, self._lib.gbv_util_hash_to_g2(self._ctx, b"".join(msgs32), n, out))
         raw = out.raw
         return [raw[192 * i:192 * i + 192] for i in range(n)]
+
+    def util_g1_mul_rand(self, slots: Sequence[int], r64: Sequence[int], use_comb: bool) -> List[bytes]:
+        """[a - b x^2] pubkey[slot] (compressed) for each 64-bit digit word, via the slot's comb table
+        or the ladder -- the check of the tables k_sm_prepare reads."""
+        n = len(slots)
+        s = _np.ascontiguousarray(slots, dtype=_np.uint32)
+        r = _np.ascontiguousarray(r64, dtype=_np.uint64)
+        out = ctypes.create_string_buffer(max(48 * n, 1))
+        _native.check(self._lib, self._ctx, self._lib.gbv_util_g1_mul_rand(self._ctx, s.ctypes.data, r.ctypes.data, n, int(bool(use_comb)), out))
+        raw = out.raw
+        return [raw[48 * i:48 * i + 48] for i in range(n)]
 
 
 class StagedSignatureSets:

@@ -143,6 +143,66 @@ int ht_randomize_jac(uint8_t* outp, uint8_t* outq, const uint8_t* p96, const uin
   store_fp2(outq, qa.x); store_fp2(outq + 96, qa.y);
   return 1;
 }
+// [r] P through a comb table built on the host (comb_bases + comb_entry_jac, one inversion per
+// entry here; the device normalises a slot's 128 entries with one inversion) -- k_sm_prepare's
+// comb path.  Also returns the Fp products of the evaluation alone (the per-set work).
+int ht_comb_mul(uint8_t* outp, const uint8_t* p96, uint64_t r64, unsigned long long* fme) {
+  G1A P{load_mont(p96), load_mont(p96 + 48)};
+  G1A B[8], D;
+  comb_bases(P, B, D);
+  std::vector<uint4> tab(COMB_ENTRIES * COMB_U4);
+  for (uint32_t e = 0; e < (uint32_t)COMB_ENTRIES; ++e) {
+    G1J j = (e & 1u) ? jac_add_aff(comb_entry_jac(B, e & ~1u), D) : comb_entry_jac(B, e);
+    G1A a;
+    if (!jac_to_aff(a, j)) return 0;
+    comb_entry_store(tab.data() + COMB_U4 * e, a);
+  }
+  g_fme_count = 0;
+  G1J rp = comb_mul(tab.data(), (uint32_t)r64, (uint32_t)(r64 >> 32));
+  *fme = g_fme_count;
+  G1A pa;
+  jac_to_aff(pa, rp);
+  store_canon(outp, pa.x); store_canon(outp + 48, pa.y);
+  return 1;
+}
+// k_comb_entries' wave normalisation replayed lane by lane (prefix / suffix products, one inversion):
+// returns the number of entries that differ from per-entry normalisation (expected 0).
+int ht_comb_wave_check(const uint8_t* p96) {
+  G1A P{load_mont(p96), load_mont(p96 + 48)};
+  G1A B[8], D;
+  comb_bases(P, B, D);
+  G1J J0[64], J1[64];
+  Fp zz[64], pre[64], suf[64];
+  for (int l = 0; l < 64; ++l) {
+    J0[l] = comb_entry_jac(B, 2u * l);
+    J1[l] = jac_add_aff(J0[l], D);
+    zz[l] = fp_mul(J0[l].z, J1[l].z);
+    pre[l] = suf[l] = zz[l];
+  }
+  for (int d = 1; d < 64; d <<= 1) {
+    Fp po[64], so[64];
+    for (int l = 0; l < 64; ++l) {
+      po[l] = pre[l - d >= 0 ? l - d : l];
+      so[l] = suf[l + d < 64 ? l + d : l];
+    }
+    for (int l = 0; l < 64; ++l) {
+      if (l - d >= 0) pre[l] = fp_mul(pre[l], po[l]);
+      if (l + d < 64) suf[l] = fp_mul(suf[l], so[l]);
+    }
+  }
+  Fp inv = fp_inv(pre[63]);
+  int bad = 0;
+  for (int l = 0; l < 64; ++l) {
+    Fp ex_pre = l > 0 ? pre[l - 1] : FP_ONE, ex_suf = l < 63 ? suf[l + 1] : FP_ONE;
+    Fp izz = fp_mul(inv, fp_mul(ex_pre, ex_suf));
+    G1A a0 = aff_from_jac_inv(J0[l], fp_mul(izz, J1[l].z)), a1 = aff_from_jac_inv(J1[l], fp_mul(izz, J0[l].z));
+    G1A r0, r1;
+    jac_to_aff(r0, J0[l]);
+    jac_to_aff(r1, J1[l]);
+    bad += !(fp_eq(a0.x, r0.x) && fp_eq(a0.y, r0.y)) + !(fp_eq(a1.x, r1.x) && fp_eq(a1.y, r1.y));
+  }
+  return bad;
+}
 // SSZ hashing (sha256.h / ssz.h): 64 bytes -> sha256, and the AttestationData signing root.
 static u32x8 ht_chunk_be(const uint8_t* p) {
   u32x8 r;

@@ -37,6 +37,52 @@ def world():
     v.close_sync()
 
 
+@pytest.mark.gpu
+def test_comb_tables_match_ladder(world):
+    """The per-slot comb tables k_sm_prepare reads (built on append, copied on replicate) give the
+    same [a - b x^2] pk as the endomorphism ladder, for appended and replicated slots; a few are
+    checked against the oracle."""
+    v, sks, pks = world
+    if not v.comb_enabled():
+        pytest.skip("comb tables disabled (GBV_COMB=0)")
+    rng = np.random.Generator(np.random.PCG64(77))
+    slots = [0, 1, N_KEYS - 1, N_KEYS, N_KEYS + 1, N_TABLE - 1] + [int(x) for x in rng.integers(0, N_TABLE, size=250)]
+    r64 = [0, 2**64 - 1, 0x0123456789ABCDEF, 1 << 63, 0xFFFFFFFF, 1 << 32] + [int(x) for x in rng.integers(0, 2**63, size=250)]
+    from oracle import bls_oracle as O
+    # raw entries of slot 0: T[e] = sum_b (bit b of e ? +1 : -1) B_b (b < 7) + B_7
+    pk0 = O.pubkey_from_bytes(pks[0], validate=False)
+    base = [O.g1_mul(pk0, 1 << (8 * j)) for j in range(4)]
+    lam = (-(O.X * O.X)) % O.R
+    base += [O.g1_mul(b, lam) for b in base]
+    ents = list(range(0, 128, 9)) + [127]
+    got = _util_raw(v, [0] * len(ents), ents)
+    for e, g in zip(ents, got):
+        acc = base[7]
+        for b in range(7):
+            acc = O.g1_add(acc, base[b] if (e >> b) & 1 else O.g1_neg(base[b]))
+        assert g == O.g1_compress(acc), e
+    comb = v.util_g1_mul_rand(slots, r64, True)
+    ladder = v.util_g1_mul_rand(slots, r64, False)
+    bad = [i for i in range(len(slots)) if comb[i] != ladder[i]]
+    assert not bad, (len(bad), bad[:8])
+    for i in range(4):
+        s, r = slots[i], r64[i]
+        a = sum(((1 if (r >> j) & 1 else -1) << j) for j in range(32))
+        b = sum(((1 if (r >> (32 + j)) & 1 else -1) << j) for j in range(32))
+        pk = O.pubkey_from_bytes(pks[s % N_KEYS], validate=False)
+        assert comb[i] == O.g1_compress(O.g1_mul(pk, (a - b * O.X * O.X) % O.R))
+
+
+def _util_raw(v, slots, ents):
+    import ctypes
+    from lodestar_amd import _native
+    s = np.ascontiguousarray(slots, dtype=np.uint32)
+    r = np.ascontiguousarray(ents, dtype=np.uint64)
+    out = ctypes.create_string_buffer(48 * len(slots))
+    _native.check(v._lib, v._ctx, v._lib.gbv_util_g1_mul_rand(v._ctx, s.ctypes.data, r.ctypes.data, len(slots), 2, out))
+    return [out.raw[48 * i:48 * i + 48] for i in range(len(slots))]
+
+
 def _workload(v, sks, n_sets, seed):
     rng = np.random.Generator(np.random.PCG64(seed))
     sizes = []

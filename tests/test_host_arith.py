@@ -215,6 +215,22 @@ def test_randomize_pair(lib, r64):
 
 
 
+@pytest.mark.parametrize("r64", [0, 0xFFFFFFFFFFFFFFFF, 0x0123456789ABCDEF, 0xDEADBEEF00C0FFEE, 0x8000000000000001])
+def test_comb_mul(lib, r64):
+    """Per-validator comb table (curve.h comb_bases / comb_entry_jac / comb_mul): [a - b x^2] P
+    equals the ladder's scalar for every digit pattern, in FME_COMB_G1 Fp products."""
+    import sys
+    sys.path.insert(0, os.path.join(HERE, ".."))
+    import bench
+    P = o.g1_mul(o.G1_GEN, 0x9876543)
+    lib.ht_comb_mul.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint64, ctypes.POINTER(ctypes.c_ulonglong)]
+    op, fme = buf(96), ctypes.c_ulonglong(0)
+    assert lib.ht_comb_mul(op, be(P[0]) + be(P[1]), r64, ctypes.byref(fme)) == 1
+    assert (int.from_bytes(op.raw[:48], "big"), int.from_bytes(op.raw[48:], "big")) == o.g1_mul(P, _digits_scalar(r64))
+    assert fme.value == bench.FME_COMB_G1
+    assert lib.ht_comb_wave_check(be(P[0]) + be(P[1])) == 0  # k_comb_entries' one-inversion normalisation
+
+
 def test_roofline_work_constants_are_counted(lib):
     """bench.py's algorithmic work per set (FME = Fp products) equals what the device code path
     executes, counted by the host build of the same arithmetic -- the roofline numerators are

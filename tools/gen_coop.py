@@ -16,9 +16,11 @@ tests/test_coop_tables.py re-executes every program in Python against the oracle
 
 Program encoding (all indices small; emitted as fixed-size per-lane u32 records -- a product is a
 header (term counts) + up to 10 A terms + up to 10 B terms, a partial sum / output a header + up to
-7 terms; within a linear form the positive terms come first, so the sign of a term is its position
-and the device reads the value or its stored negation -- a lane fetches its whole record with a few
-16-byte loads, one memory latency per phase, and evaluates only its true number of terms):
+7 terms; within a linear form the coefficient +1 terms come first, then the -1 terms (the sign of a
+unit term is its position and the device reads the value or its stored negation), then the rare
+scaled terms (|coefficient| > 1, sign in bit 4 of the term word) -- a lane fetches its whole record
+with a few 16-byte loads, one memory latency per phase, evaluates the unit terms in an unrolled
+chain and the scaled ones in a short rolled loop, i.e. only its true number of terms):
   operands 0..5 -> base pointers given at run time (program-specific signature below)
   SRC_Z = 6  -> Z[k], the k-th product of this program (then the partial sums)
   SRC_C = 7  -> CONSTS[k] (Montgomery Fp constants emitted below)
@@ -407,21 +409,23 @@ def limbs(v):
 PROD_WORDS, SUM_WORDS, SUM_TERMS = 24, 8, 7
 
 
-def term_word(t):
+def term_word(t, neg=False):
     src, idx, c = t
-    assert 0 <= src < 16 and idx < 256 and 0 < abs(c) < 65536
-    return src | (idx << 8) | (abs(c) << 16)
+    assert 0 <= src < 8 and idx < 256 and 0 < abs(c) < 65536
+    return src | (int(neg) << 4) | (idx << 8) | (abs(c) << 16)
 
 
 def signed_record(T, t0, tn, width):
-    """(npos, nneg, words): the terms of T[t0:t0+tn] with positive coefficients first, each term a
-    u32 (src | idx << 8 | |coef| << 16); padded to `width` words."""
+    """(npos, nneg, nsc, words): the terms of T[t0:t0+tn] -- coefficient +1 terms, then -1 terms,
+    then scaled terms (|c| > 1, sign bit 4) -- each a u32 (src | neg << 4 | idx << 8 | |c| << 16),
+    padded to `width` words."""
     ts = list(T[t0:t0 + tn])
-    pos = [t for t in ts if t[2] > 0]
-    neg = [t for t in ts if t[2] < 0]
-    assert len(pos) + len(neg) == len(ts) and len(ts) <= width and len(pos) < 256 and len(neg) < 256
-    words = [term_word(t) for t in pos + neg]
-    return len(pos), len(neg), words + [0] * (width - len(words))
+    pos = [t for t in ts if t[2] == 1]
+    neg = [t for t in ts if t[2] == -1]
+    sc = [t for t in ts if abs(t[2]) > 1]
+    assert len(pos) + len(neg) + len(sc) == len(ts) and len(ts) <= width
+    words = [term_word(t) for t in pos + neg] + [term_word(t, t[2] < 0) for t in sc]
+    return len(pos), len(neg), len(sc), words + [0] * (width - len(words))
 
 
 def emit(progs, path):
@@ -443,15 +447,15 @@ def emit(progs, path):
         T = p["terms"]
         prod_recs = []
         for (a0, an, b0, bn) in p["prods"]:
-            pa, na, wa = signed_record(T, a0, an, OPW)
-            pb, nb, wb = signed_record(T, b0, bn, OPW)
+            pa, na, sa, wa = signed_record(T, a0, an, OPW)
+            pb, nb, sb, wb = signed_record(T, b0, bn, OPW)
             hdr = pa | (na << 8) | (pb << 16) | (nb << 24)
-            prod_recs.append([hdr] + wa + wb + [0] * (PROD_WORDS - 1 - 2 * OPW))
+            prod_recs.append([hdr] + wa + wb + [sa | (sb << 8)] + [0] * (PROD_WORDS - 2 - 2 * OPW))
         prod_recs = prod_recs or [[0] * PROD_WORDS]
 
         def sum_rec(t0, tn):
-            ps, ns, w = signed_record(T, t0, tn, SUM_TERMS)
-            return [ps | (ns << 8)] + w
+            ps, ns, ss, w = signed_record(T, t0, tn, SUM_TERMS)
+            return [ps | (ns << 8) | (ss << 16)] + w
         part_recs = [sum_rec(t0, tn) for (t0, tn, _) in p["parts"]] or [[0] * SUM_WORDS]
         out_recs = [sum_rec(t0, tn) for (t0, tn, _, _) in p["outs"]]
         for j, (_, _, z) in enumerate(p["parts"]):
