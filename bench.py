@@ -55,7 +55,7 @@ FME_RANDOMIZE_G1 = 593      # r_i pk_i (endomorphism-split 32-step ladder + affi
 FME_COMB_G1 = 126           # r_i pk_i from the validator's comb table (7 doublings + 7 mixed additions)
 FME_RANDOMIZE_PAIR = 2086   # r_i pk_i and r_i sig_i with one shared inversion
 FME_RANDOMIZE_PAIR_JAC = 2096  # the same with P Jacobian (aggregate pubkeys straight from k_vs_agg)
-FME_HASH_TO_G2 = 6658       # RFC 9380 hash_to_G2 (SSWU + 3-isogeny + h_eff + to affine)
+FME_HASH_TO_G2 = 4808       # RFC 9380 hash_to_G2 (SSWU with one norm exponentiation per map + 3-isogeny + h_eff + to affine)
 FME_MILLER_1J = 7244        # Miller value of one pair, Jacobian P
 FME_G1_SCAN = 48            # 3-level 8-lane chunk scan of r_i pk_i (3 Jacobian G1 additions)
 # k_sm_prepare<false> (bench: G2 sum by bucket MSM) and <true> (per-set G2 ladders)

@@ -125,6 +125,8 @@ GBV_HD Fp fp_dbl(const Fp& a) { return fp_add(a, a); }
 
 // One multiply-accumulate into a 96-bit column accumulator {acc (64), top (32)}:
 //   acc += a * b  (v_mad_u64_u32 with carry-out in VCC),  top += carry  (v_addc_co_u32).
+// mac96_first starts a column (top = carry: no separate zeroing move); mac96_k takes the constant
+// operand (a limb of p) from an SGPR, so the 144 reduction products need no VGPR copies of p.
 GBV_HD void mac96(uint64_t& acc, uint32_t& top, uint32_t a, uint32_t b) {
 #if defined(__HIP_DEVICE_COMPILE__)
   asm("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\tv_addc_co_u32 %1, vcc, 0, %1, vcc"
@@ -136,6 +138,38 @@ GBV_HD void mac96(uint64_t& acc, uint32_t& top, uint32_t a, uint32_t b) {
   uint64_t s = acc + p;
   top += (s < acc) ? 1u : 0u;
   acc = s;
+#endif
+}
+GBV_HD void mac96_first(uint64_t& acc, uint32_t& top, uint32_t a, uint32_t b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\tv_addc_co_u32_e64 %1, vcc, 0, 0, vcc"
+      : "+v"(acc), "=v"(top)
+      : "v"(a), "v"(b)
+      : "vcc");
+#else
+  top = 0;
+  mac96(acc, top, a, b);
+#endif
+}
+GBV_HD void mac96_k(uint64_t& acc, uint32_t& top, uint32_t a, uint32_t k) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\tv_addc_co_u32 %1, vcc, 0, %1, vcc"
+      : "+v"(acc), "+v"(top)
+      : "v"(a), "s"(k)
+      : "vcc");
+#else
+  mac96(acc, top, a, k);
+#endif
+}
+GBV_HD void mac96_k_first(uint64_t& acc, uint32_t& top, uint32_t a, uint32_t k) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\tv_addc_co_u32_e64 %1, vcc, 0, 0, vcc"
+      : "+v"(acc), "=v"(top)
+      : "v"(a), "s"(k)
+      : "vcc");
+#else
+  top = 0;
+  mac96(acc, top, a, k);
 #endif
 }
 
@@ -157,25 +191,26 @@ GBV_HD Fp fp_mul_inl(const Fp& a, const Fp& b) {
   uint32_t top = 0;
 #pragma unroll
   for (int k = 0; k < 12; ++k) {
+    mac96_first(acc, top, a.v[0], b.v[k]);
 #pragma unroll
-    for (int i = 0; i <= k; ++i) mac96(acc, top, a.v[i], b.v[k - i]);
+    for (int i = 1; i <= k; ++i) mac96(acc, top, a.v[i], b.v[k - i]);
 #pragma unroll
-    for (int i = 0; i < k; ++i) mac96(acc, top, m[i], P_RAW.v[k - i]);
+    for (int i = 0; i < k; ++i) mac96_k(acc, top, m[i], P_RAW.v[k - i]);
     m[k] = (uint32_t)acc * NP0;
-    mac96(acc, top, m[k], P_RAW.v[0]);
+    mac96_k(acc, top, m[k], P_RAW.v[0]);
     acc = (acc >> 32) | ((uint64_t)top << 32);
-    top = 0;
   }
 #pragma unroll
   for (int k = 12; k < 23; ++k) {
+    mac96_first(acc, top, a.v[k - 11], b.v[11]);
+    mac96_k(acc, top, m[k - 11], P_RAW.v[11]);
 #pragma unroll
-    for (int i = k - 11; i < 12; ++i) {
+    for (int i = k - 10; i < 12; ++i) {
       mac96(acc, top, a.v[i], b.v[k - i]);
-      mac96(acc, top, m[i], P_RAW.v[k - i]);
+      mac96_k(acc, top, m[i], P_RAW.v[k - i]);
     }
     r[k - 12] = (uint32_t)acc;
     acc = (acc >> 32) | ((uint64_t)top << 32);
-    top = 0;
   }
   r[11] = (uint32_t)acc;
   Fp o;

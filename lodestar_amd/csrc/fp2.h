@@ -99,9 +99,9 @@ GBV_HD bool fp2_is_lexi_large(const Fp2& a) {
 //   alpha = sqrt(a0^2 + a1^2);  delta = (a0 + alpha)/2 (or (a0 - alpha)/2 if that is 0);
 //   t = delta^((p-3)/4);  x0 = t*delta;  if x0*t == 1: root = (x0, a1 t / 2) else (-a1 t / 2, x0).
 // Returns true iff a is a square (root^2 == a).  Prototype: tests/test_algorithm_prototypes.py.
-GBV_HD bool fp2_sqrt(Fp2& root, const Fp2& a) {
-  Fp n = fp_add(fp_sqr(a.c0), fp_sqr(a.c1));
-  Fp alpha = fp_pow_sched(n, SCHED_SQRT_NSQ, SCHED_SQRT_IDX, SCHED_SQRT_STEPS);
+// fp2_sqrt_with_norm_root is the second half, for callers that already hold a square root alpha
+// (either sign) of the norm a0^2 + a1^2.
+GBV_HD bool fp2_sqrt_with_norm_root(Fp2& root, const Fp2& a, const Fp& alpha) {
   Fp delta = fp_mul(fp_add(a.c0, alpha), FP_INV2);
   Fp delta2 = fp_mul(fp_sub(a.c0, alpha), FP_INV2);
   delta = fp_sel(fp_is_zero(delta), delta2, delta);
@@ -112,6 +112,13 @@ GBV_HD bool fp2_sqrt(Fp2& root, const Fp2& a) {
   root.c0 = fp_sel(qr, x0, fp_neg(h));
   root.c1 = fp_sel(qr, h, x0);
   return fp2_eq(fp2_sqr(root), a);
+}
+
+GBV_HD Fp fp2_norm(const Fp2& a) { return fp_add(fp_sqr(a.c0), fp_sqr(a.c1)); }
+
+GBV_HD bool fp2_sqrt(Fp2& root, const Fp2& a) {
+  Fp alpha = fp_pow_sched(fp2_norm(a), SCHED_SQRT_NSQ, SCHED_SQRT_IDX, SCHED_SQRT_STEPS);
+  return fp2_sqrt_with_norm_root(root, a, alpha);
 }
 
 // Frobenius / psi helpers -------------------------------------------------------------------

@@ -83,11 +83,19 @@ GBV_NI G2A map_to_curve_sswu(Fp2 u) {
   Fp2 gx1 = fp2_add(fp2_mul(fp2_add(fp2_sqr(x1), SSWU_A), x1), SSWU_B);
   Fp2 x2 = fp2_mul(zu2, x1);
   Fp2 gx2 = fp2_add(fp2_mul(fp2_add(fp2_sqr(x2), SSWU_A), x2), SSWU_B);
-  Fp2 y1, y2;
-  bool ok1 = fp2_sqrt(y1, gx1);
-  fp2_sqrt(y2, gx2);
-  Fp2 x = fp2_sel(ok1, x1, x2);
-  Fp2 y = fp2_sel(ok1, y1, y2);
+  // ONE norm exponentiation decides which of g(x1), g(x2) is the square and yields the norm root
+  // of that one: n1 = N(g(x1)); a1 = n1^((p+1)/4) is sqrt(n1) if n1 is a residue (then g(x1) is a
+  // square in Fp2), else sqrt(-n1); and g(x2) = Z^3 u^6 g(x1) gives
+  // sqrt(N(g(x2))) = N(u)^3 sqrt(-N(Z)^3) a1.  Then one fp2_sqrt_with_norm_root -- two Fp
+  // exponentiations per map instead of four.
+  Fp n1 = fp2_norm(gx1);
+  Fp a1 = fp_pow_sched(n1, SCHED_SQRT_NSQ, SCHED_SQRT_IDX, SCHED_SQRT_STEPS);
+  bool sq1 = fp_eq(fp_sqr(a1), n1);
+  Fp nu = fp2_norm(u);
+  Fp a2 = fp_mul(fp_mul(fp_mul(fp_sqr(nu), nu), SSWU_SQRT_MINUS_NZ3), a1);
+  Fp2 x = fp2_sel(sq1, x1, x2);
+  Fp2 y;
+  fp2_sqrt_with_norm_root(y, fp2_sel(sq1, gx1, gx2), fp_sel(sq1, a1, a2));
   if (fp2_sgn0(u) != fp2_sgn0(y)) y = fp2_neg(y);
   return G2A{x, y};
 }
