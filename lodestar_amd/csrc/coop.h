@@ -42,7 +42,7 @@ struct Prog {
 };
 constexpr int OPW = 10;
 constexpr int PROD_WORDS = 24;
-constexpr int SUM_WORDS = 8, SUM_TERMS = 7;
+constexpr int SUM_WORDS = 12, SUM_TERMS = 11;
 enum { SRC_Z = 6, SRC_C = 7 };
 constexpr int N_CONSTS_MAX = 16;
 

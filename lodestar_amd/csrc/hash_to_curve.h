@@ -130,18 +130,31 @@ GBV_NI G2J clear_cofactor_g2(G2J p) {
   return jac_add(t3, jac_neg(p));
 }
 
+// hash_to_field: u_j = expand_message_xmd(msg)[64 j .. 64 j + 64) as Fp2 (j = 0, 1)
+GBV_HD Fp2 hash_to_field_fp2(const uint32_t* msg, int j) {
+  uint32_t u[64];
+  expand_message_xmd_32(u, msg);
+  return Fp2{fp_from_be64_words(u + 32 * j), fp_from_be64_words(u + 32 * j + 16)};
+}
+
+// Q(u) = iso_map(map_to_curve(u)); the two halves of hash_to_G2 are independent
+GBV_NI G2J hash_map_iso(Fp2 u) { return iso_map(map_to_curve_sswu(u)); }
+
+// clear_cofactor(Q0 + Q1) as an affine point
+GBV_NI G2A hash_finish(G2J q0, G2J q1) {
+  G2J q = clear_cofactor_g2(jac_add(q0, q1));
+  G2A out;
+  jac_to_aff(out, q);
+  return out;
+}
+
 // hash_to_G2(msg32) as an affine point (Montgomery).  msg given as 8 big-endian words.
 GBV_NI G2A hash_to_g2(const uint32_t* msg) {
   uint32_t u[64];
   expand_message_xmd_32(u, msg);
   Fp2 u0{fp_from_be64_words(u), fp_from_be64_words(u + 16)};
   Fp2 u1{fp_from_be64_words(u + 32), fp_from_be64_words(u + 48)};
-  G2J q0 = iso_map(map_to_curve_sswu(u0));
-  G2J q1 = iso_map(map_to_curve_sswu(u1));
-  G2J q = clear_cofactor_g2(jac_add(q0, q1));
-  G2A out;
-  jac_to_aff(out, q);
-  return out;
+  return hash_finish(hash_map_iso(u0), hash_map_iso(u1));
 }
 
 }  // namespace gbv

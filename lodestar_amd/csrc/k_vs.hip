@@ -65,7 +65,7 @@ k_vs_agg(uint32_t n_agg, const uint32_t* __restrict__ agg_list, const uint32_t* 
 // maybeBatch.ts:23), fetch the pubkey (table slot, the k_vs_agg result, or a raw key validated like
 // PublicKey.fromBytes(pk, true), blsToExecutionChange.ts:31) and form r_i pk_i and r_i sig_i.
 // The two roles are independent, so hashing (the longest per-set chain) overlaps the rest.
-__global__ void GBV_KERNEL_ATTR k_vs_hash_sig(uint32_t n, uint32_t nb, const uint8_t* __restrict__ msgs32,
+__global__ void GBV_KERNEL_ATTR k_vs_hash_sig(uint32_t n, uint32_t nb, uint32_t pair, const uint8_t* __restrict__ msgs32,
                                               const uint32_t* __restrict__ set_off, const uint32_t* __restrict__ arena,
                                               const uint8_t* __restrict__ raw_flag, const uint8_t* __restrict__ raw_pk48,
                                               const uint8_t* __restrict__ sig, uint32_t sig_stride, const uint32_t* __restrict__ sig_len,
@@ -74,6 +74,15 @@ __global__ void GBV_KERNEL_ATTR k_vs_hash_sig(uint32_t n, uint32_t nb, const uin
                                               G2A* __restrict__ H, G1J* __restrict__ rP_out, G2J* __restrict__ rS_out,
                                               uint8_t* __restrict__ status) {
   if (blockIdx.x < nb) {
+    if (pair) {  // few sets: lane pairs (hash_to_g2_lane_pair), nb = ceil(2n / 64)
+      uint32_t i = (blockIdx.x * 64 + threadIdx.x) >> 1;
+      bool act = i < n;
+      uint32_t w[8] = {};
+      if (act) load_msg_words(w, msgs32 + 32ull * i);
+      G2A h;
+      if (hash_to_g2_lane_pair(w, act, &h)) H[i] = h;
+      return;
+    }
     uint32_t i = blockIdx.x * 64 + threadIdx.x;
     if (i >= n) return;
     uint32_t w[8];
@@ -159,8 +168,9 @@ void launch_vs_hash_sig(hipStream_t s, uint32_t n, const uint8_t* msgs32, const 
                         const uint8_t* raw_flag, const uint8_t* raw_pk48, const uint8_t* sig, uint32_t sig_stride, const uint32_t* sig_len,
                         const G1A* table, const uint8_t* table_ok, const G1J* pk_agg, const uint8_t* pk_st, const Seed& seed,
                         uint32_t nonce, G2A* H, G1J* rP, G2J* rS, uint8_t* status) {
-  uint32_t nb = (n + 63) / 64;
-  hipLaunchKernelGGL(k_vs_hash_sig, dim3(2 * nb), dim3(64), 0, s, n, nb, msgs32, set_off, arena, raw_flag, raw_pk48, sig, sig_stride,
+  const uint32_t pair = n <= HASH_PAIR_MAX ? 1u : 0u;
+  const uint32_t nb = pair ? (2 * n + 63) / 64 : (n + 63) / 64, nsig = (n + 63) / 64;
+  hipLaunchKernelGGL(k_vs_hash_sig, dim3(nb + nsig), dim3(64), 0, s, n, nb, pair, msgs32, set_off, arena, raw_flag, raw_pk48, sig, sig_stride,
                      sig_len, table, table_ok, pk_agg, pk_st, seed, nonce, H, rP, rS, status);
   debug_sync(s, "k_vs_hash_sig");
 }

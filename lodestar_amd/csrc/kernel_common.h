@@ -52,6 +52,8 @@ enum : uint8_t { GRP_PENDING = 0, GRP_FALLBACK = 1, GRP_OK = 2 };
 // Failure-path item counts up to which one wave per item (k_sm_fb_*_coop, latency) beats one
 // thread per item (k_sm_fb_blocks / k_sm_fb_sets, throughput).
 constexpr uint32_t FB_COOP_MAX = 256;
+// Message counts up to which hash_to_G2 runs on lane pairs (latency) instead of one lane each.
+constexpr uint32_t HASH_PAIR_MAX = 4096;
 
 // Per-set random 64-bit scalar r_i = SHA-256(seed || i || nonce)[0..8), forced non-zero.
 // blst draws 64-bit random scalars for the same purpose; only the booleans are compared.
@@ -68,6 +70,29 @@ __device__ inline uint64_t prf_scalar(const Seed& s, uint32_t i, uint32_t nonce)
   sha256_compress(st, blk);
   uint64_t r = ((uint64_t)st[0] << 32) | st[1];
   return r ? r : 1ull;
+}
+
+// Lane-pair hash_to_G2 for latency (few messages): lanes 2m and 2m+1 map u_0 and u_1 of message m
+// at the same time, the odd lane hands its point over (shuffles), the even lane clears the
+// cofactor.  Every lane of the wave must call it (the shuffles); returns true on the even lane.
+__device__ inline Fp shfl_fp(const Fp& a, int src) {
+  Fp r;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) r.v[i] = __shfl((unsigned)a.v[i], src, 64);
+  return r;
+}
+__device__ inline bool hash_to_g2_lane_pair(const uint32_t w[8], bool active, G2A* out) {
+  const int lane = (int)threadIdx.x, half = lane & 1;
+  G2J q = jac_infinity<Fp2>();
+  if (active) q = hash_map_iso(hash_to_field_fp2(w, half));
+  Fp* f = (Fp*)&q;
+  G2J o;
+  Fp* g = (Fp*)&o;
+#pragma unroll
+  for (int i = 0; i < 6; ++i) g[i] = shfl_fp(f[i], lane | 1);
+  if (!active || half) return false;
+  *out = hash_finish(q, o);
+  return true;
 }
 
 __device__ inline void load_msg_words(uint32_t w[8], const uint8_t* m) {

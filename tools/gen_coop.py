@@ -36,6 +36,7 @@ sys.path.insert(0, ROOT)
 P = 0x1A0111EA397FE69A4B1BA7B6434BACD764774B84F38512BF6730D2A0F6B0F6241EABFFFEB153FFFFB9FEFFFFFFFFAAAB
 SRC_Z, SRC_C = 6, 7
 PART_TERMS = 6
+OUT_MAX = 7  # longer outputs are split into partial sums of PART_TERMS (short add chains per phase)
 OPW = 10  # terms per product operand record (A: 0..9, B: 10..19); 20 x 4 B = five 16-byte loads
 
 
@@ -90,6 +91,13 @@ class Builder:
         self.signature = signature  # list of (operand name, n coords, role)
         self.prods = []  # (Lin, Lin)
         self.outs = []   # (dst operand, coord, Lin)
+        self.xparts = []  # explicit partial sums (Lin over products / inputs / constants)
+
+    def part(self, lin):
+        """An explicit partial sum: one lane of the partial-sum phase computes it into Z, so an
+        output can use it several times (3 t - 2 z as t + t + t - z - z: unit terms only)."""
+        self.xparts.append(lin)
+        return Lin({("p", len(self.xparts) - 1): 1})
 
     def mul(self, a, b):
         self.prods.append((a, b))
@@ -169,9 +177,13 @@ class Builder:
         t0, t1 = fp4_sqr(z0, z1)
         t2, t3 = fp4_sqr(z2, z3)
         t4, t5 = fp4_sqr(z4, z5)
+        # the t's become partial sums, so each output 3 t +- 2 z is five unit terms
+        t0, t1, t2, t3, t4 = [(self.part(t[0]), self.part(t[1])) for t in (t0, t1, t2, t3, t4)]
+        t5x = f2xi(t5)
+        t5x = (self.part(t5x[0]), self.part(t5x[1]))
         n0 = f2sub(f2scale(t0, 3), f2scale(z0, 2))
         n1 = f2add(f2scale(t1, 3), f2scale(z1, 2))
-        n2 = f2add(f2scale(f2xi(t5), 3), f2scale(z2, 2))
+        n2 = f2add(f2scale(t5x, 3), f2scale(z2, 2))
         n3 = f2sub(f2scale(t4, 3), f2scale(z3, 2))
         n4 = f2sub(f2scale(t2, 3), f2scale(z4, 2))
         n5 = f2add(f2scale(t3, 3), f2scale(z5, 2))
@@ -350,48 +362,80 @@ def schedule(b):
     return order, remap, round_end
 
 
+DUP_MAX = 3  # a term with |coefficient| <= DUP_MAX is emitted as |c| unit terms (no scaling loop)
+
+
 def encode(b):
     order, remap, round_end = schedule(b)
+    nprod = len(b.prods)
     terms = []
 
-    def enc(lin):
-        start = len(terms)
-        for s, c in sorted(lin.d.items(), key=lambda kv: str(kv[0])):
-            if s[0] == "in":
-                src, idx = s[1], s[2]
-            elif s[0] == "z":
-                src, idx = SRC_Z, remap[s[1]]
+    def expand(lin, width):
+        """(src, idx, coefficient) list of a linear form; terms with |c| <= DUP_MAX become |c| unit
+        copies (no scaling loop on the device) while the record width allows."""
+        items = []
+        for s_, c in sorted(lin.d.items(), key=lambda kv: str(kv[0])):
+            if s_[0] == "in":
+                src, idx = s_[1], s_[2]
+            elif s_[0] == "z":
+                src, idx = SRC_Z, remap[s_[1]]
+            elif s_[0] == "p":
+                src, idx = SRC_Z, nprod + s_[1]
+            elif s_[0] == "zraw":
+                src, idx = SRC_Z, s_[1]
             else:
-                src, idx = SRC_C, s[1]
+                src, idx = SRC_C, s_[1]
             assert -32768 < c < 32768 and idx < 256
-            terms.append((src, idx, c))
-        return start, len(terms) - start
+            items.append((src, idx, c))
+        budget = width - len(items)
+        out = []
+        for src, idx, c in items:
+            if 1 < abs(c) <= DUP_MAX and abs(c) - 1 <= budget:
+                budget -= abs(c) - 1
+                out += [(src, idx, 1 if c > 0 else -1)] * abs(c)
+            else:
+                out.append((src, idx, c))
+        return out
+
+    def put(tl):
+        start = len(terms)
+        terms.extend(tl)
+        return start, len(tl)
 
     prods = []
     for k in order:
-        a0, an = enc(b.prods[k][0])
-        b0, bn = enc(b.prods[k][1])
+        a0, an = put(expand(b.prods[k][0], OPW))
+        b0, bn = put(expand(b.prods[k][1], OPW))
+        assert an <= OPW and bn <= OPW, (b.name, an, bn)
         prods.append((a0, an, b0, bn))
-    # Long output sums are split into partial sums of <= PART_TERMS terms (one lane each, stored
-    # in Z after the products), so the output phase is two short adds chains, not one long one.
+    # Partial sums (one lane each, stored in Z after the products): the explicit ones, then the
+    # pieces of long outputs, so the output phase is two short add chains, not one long one.
     parts = []
+    nz = nprod
+    for lin in b.xparts:
+        tl = expand(lin, SUM_TERMS)
+        assert all(t[0] != SRC_Z or t[1] < nprod for t in tl), "a partial sum reads products only"
+        assert len(tl) <= SUM_TERMS, (b.name, len(tl))
+        t0, tn = put(tl)
+        parts.append((t0, tn, nz))
+        nz += 1
     outs = []
-    nz = len(prods)
     for op, i, lin in b.outs:
-        items = sorted(lin.d.items(), key=lambda kv: str(kv[0]))
-        if len(items) > PART_TERMS:
-            refs = {}
-            for j in range(0, len(items), PART_TERMS):
-                t0, tn = enc(Lin(dict(items[j:j + PART_TERMS])))
+        tl = expand(lin, OUT_MAX)
+        if len(tl) > OUT_MAX:  # split: expand freely inside the pieces
+            tl = expand(lin, 4 * SUM_TERMS * SUM_TERMS)
+        if len(tl) > OUT_MAX:
+            refs = []
+            for j in range(0, len(tl), PART_TERMS):
+                t0, tn = put(tl[j:j + PART_TERMS])
                 parts.append((t0, tn, nz))
-                refs[("zraw", nz)] = 1
+                refs.append((SRC_Z, nz, 1))
                 nz += 1
-            start = len(terms)
-            for s_, c in refs.items():
-                terms.append((SRC_Z, s_[1], c))
-            outs.append((start, len(terms) - start, op, i))
+            assert len(refs) <= SUM_TERMS, (b.name, len(refs))
+            t0, tn = put(refs)
+            outs.append((t0, tn, op, i))
         else:
-            t0, tn = enc(lin)
+            t0, tn = put(tl)
             outs.append((t0, tn, op, i))
     assert len(outs) <= 64 and len(prods) <= 64 and len(parts) <= 64 and nz <= 128, (b.name, len(outs), len(prods), nz)
     return {"name": b.name, "signature": b.signature, "round_end": round_end, "prods": prods, "parts": parts,
@@ -406,7 +450,7 @@ def limbs(v):
     return ["0x%08xu" % ((v >> (32 * i)) & 0xFFFFFFFF) for i in range(12)]
 
 
-PROD_WORDS, SUM_WORDS, SUM_TERMS = 24, 8, 7
+PROD_WORDS, SUM_WORDS, SUM_TERMS = 24, 12, 11
 
 
 def term_word(t, neg=False):

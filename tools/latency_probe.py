@@ -1,25 +1,28 @@
-"""Where the time of one small same-message call goes (create / submit+wait / destroy), on the GPU."""
+"""Where the time of one lone 64-set same-message call goes (bench.py's p50 path), on the GPU.
+
+    python tools/latency_probe.py            # per-call wall time and per-kernel event times
+    rocprofv3 --kernel-trace -d gpurun_out/lat -- python3 tools/latency_probe.py   # timeline
+"""
+import os
 import sys
 import time
 
 import numpy as np
 
-sys.path.insert(0, ".")
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import bench  # noqa: E402
 from lodestar_amd import GpuBlsVerifier  # noqa: E402
 
 v = GpuBlsVerifier(0)
-call_off, idx, sigs, msgs, _ = bench.build_workload(v, 4096, 0, lambda m: None)
+sks, _ = bench.build_table(v, lambda m: None)
+call_off, idx, sigs, msgs = bench.build_workload(v, sks, 4096, 0, lambda m: None)
 n = 64
-off = np.array([0, n], dtype=np.uint32)
-for rep in range(8):
+calls = [([(int(idx[i]), sigs[96 * i:96 * i + 96]) for i in range(n)], msgs[:32])]
+for rep in range(12):
     t0 = time.perf_counter()
-    st = v.stage_same_message(off, idx[:n], sigs[:96 * n], msgs[:32])
+    res = v.verify_same_message_multi_sync(calls)
     t1 = time.perf_counter()
-    res = st.verify(True)
-    t2 = time.perf_counter()
-    st.close()
-    t3 = time.perf_counter()
     kms, cnt = v.last_kernel_ms()
-    print("create %.2f ms  verify %.2f ms  destroy %.2f ms  kernels %s  valid %d" % (
-        (t1 - t0) * 1e3, (t2 - t1) * 1e3, (t3 - t2) * 1e3, [round(x, 2) for x in kms], res.count(1)), flush=True)
+    print("call %.2f ms  kernels %s  valid %d" % ((t1 - t0) * 1e3, dict(zip(bench.KERNELS, [round(float(x), 2) for x in kms])),
+                                                  sum(sum(r) for r in res)), flush=True)
+v.close_sync()
