@@ -236,7 +236,10 @@ static int vs_enqueue_sets(gbv_ctx* c, gbv_vs_batch* b, hipStream_t m) {
   HIP_CHECK(c, hipEventRecord(b->ev[2], s));
   if (m != s) HIP_CHECK(c, hipStreamWaitEvent(m, b->ev[2], 0));
   HIP_CHECK(c, hipEventRecord(b->ev[3], m));
-  launch_vs_miller(LaunchCfg{blocks_for(b->n), TPB, m}, (uint32_t)b->n, b->status, b->rP, b->H, b->F);
+  if (b->n <= VS_COOP_MILLER_MAX)  // latency: one wave per set (cooperative Miller loop)
+    launch_vs_miller_coop(m, (uint32_t)b->n, b->status, b->rP, b->H, b->F);
+  else
+    launch_vs_miller(LaunchCfg{blocks_for(b->n), TPB, m}, (uint32_t)b->n, b->status, b->rP, b->H, b->F);
   HIP_CHECK(c, hipEventRecord(b->ev[4], m));
   HIP_CHECK(c, hipGetLastError());
   return GBV_OK;

@@ -330,6 +330,39 @@ k_vs_chunk_coop(const uint32_t* __restrict__ chunk_be, const uint8_t* __restrict
   if (lane == 0) chunk_valid[c] = ok ? 1 : 0;
 }
 
+// Miller value f_{|x|, H(m_i)}(r_i pk_i) of one set per wave (latency: small verifySignatureSets
+// passes; k_vs_miller runs one thread per set for large ones).  Same value up to an Fp factor as the
+// thread version (the final exponentiation removes it): P is made affine by lane 0 first.
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
+k_vs_miller_coop(const uint8_t* __restrict__ status, const G1J* __restrict__ rP, const G2A* __restrict__ H, Fp12* __restrict__ F) {
+  __shared__ coop::Slot ws[coop::MILLER_WS];
+  __shared__ Fp stage[2];
+  __shared__ int ok;
+  const uint32_t i = blockIdx.x;
+  if (status[i] != SET_OK) return;
+  const unsigned lane = threadIdx.x;
+  coop::load_consts();
+  if (lane == 0) {
+    G1A pa;
+    ok = jac_to_aff(pa, rP[i]) ? 1 : 0;
+    stage[0] = pa.x;
+    stage[1] = pa.y;
+  }
+  coop::barrier();
+  if (!ok) {  // r_i pk_i at infinity cannot happen for a valid key (r_i != 0 mod r); F = 1 keeps the product defined
+    if (lane < 12) ((Fp*)&F[i])[lane] = lane == 0 ? FP_ONE : fp_zero();
+    return;
+  }
+  coop::miller_load_pair(ws, 0, G1A{stage[0], stage[1]}, H[i]);
+  coop::miller_loop(ws, 1);
+  if (lane < 12) ((Fp*)&F[i])[lane] = coop::get(ws + coop::M_F + lane);
+}
+
+void launch_vs_miller_coop(hipStream_t s, uint32_t n, const uint8_t* status, const G1J* rP, const G2A* H, Fp12* F) {
+  hipLaunchKernelGGL(k_vs_miller_coop, dim3(n), dim3(64), 0, s, status, rP, H, F);
+  debug_sync(s, "k_vs_miller_coop");
+}
+
 void launch_fp12_check(LaunchCfg c, uint32_t k, const Fp12* parts, uint8_t* out) {
   hipLaunchKernelGGL(k_fp12_check, dim3(1), dim3(64), 0, c.stream, k, parts, out);
   debug_sync(c.stream, "k_fp12_check");

@@ -54,6 +54,9 @@ enum : uint8_t { GRP_PENDING = 0, GRP_FALLBACK = 1, GRP_OK = 2 };
 constexpr uint32_t FB_COOP_MAX = 256;
 // Message counts up to which hash_to_G2 runs on lane pairs (latency) instead of one lane each.
 constexpr uint32_t HASH_PAIR_MAX = 4096;
+// verifySignatureSets passes up to this many sets compute their Miller values one wave per set
+// (cooperative, ~2.9 ms) instead of one thread per set (~16 ms of latency, far less VALU in total).
+constexpr uint32_t VS_COOP_MILLER_MAX = 2048;
 
 // Per-set random 64-bit scalar r_i = SHA-256(seed || i || nonce)[0..8), forced non-zero.
 // blst draws 64-bit random scalars for the same purpose; only the booleans are compared.

@@ -88,6 +88,7 @@ void launch_vs_hash_sig(hipStream_t s, uint32_t n, const uint8_t* msgs32, const 
                         const uint8_t* raw_flag, const uint8_t* raw_pk48, const uint8_t* sig, uint32_t sig_stride, const uint32_t* sig_len,
                         const G1A* table, const uint8_t* table_ok, const G1J* pk_agg, const uint8_t* pk_st, const Seed& seed,
                         uint32_t nonce, G2A* H, G1J* rP, G2J* rS, uint8_t* status);
+void launch_vs_miller_coop(hipStream_t s, uint32_t n, const uint8_t* status, const G1J* rP, const G2A* H, Fp12* F);
 void launch_vs_miller(LaunchCfg c, uint32_t n, const uint8_t* status, const G1J* rP, const G2A* H, Fp12* F);
 void launch_sig_validate(LaunchCfg c, uint32_t n, const uint8_t* sig, uint32_t sig_len, uint8_t* status, uint8_t* out96);
 

@@ -25,4 +25,13 @@ for rep in range(12):
     kms, cnt = v.last_kernel_ms()
     print("call %.2f ms  kernels %s  valid %d" % ((t1 - t0) * 1e3, dict(zip(bench.KERNELS, [round(float(x), 2) for x in kms])),
                                                   sum(sum(r) for r in res)), flush=True)
+# C1: one verifySignatureSets call of 128 distinct-message single-pubkey sets
+rng = np.random.Generator(np.random.PCG64(0xC1))
+sets = bench._single_sets(v, sks, 128, b"gbv-c1", rng)
+for rep in range(8):
+    t0 = time.perf_counter()
+    ok = v.verify_signature_sets_sync(sets)
+    t1 = time.perf_counter()
+    print("c1 call %.2f ms  kernels %s  ok %s" % ((t1 - t0) * 1e3, dict(zip(bench.VS_KERNELS, [round(float(x), 2) for x in v.vs_last_kernel_ms()])), ok),
+          flush=True)
 v.close_sync()
