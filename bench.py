@@ -83,7 +83,7 @@ ALG_BYTES_PER_SET_COMB = ALG_BYTES_PER_SET - 128 + 8 * 96 + 1
 AGG_BYTES_PER_MEMBER = 4 + 128 + 1
 
 
-def pmc_evidence(units_per_launch, kernel="k_sm_prepare<false>"):
+def pmc_evidence(units_per_launch, kernel="k_sm_prepare<false>", alg_bytes=ALG_BYTES_PER_SET):
     """HBM traffic per launch and VALU issue utilisation of k_sm_prepare from the committed
     rocprofv3 --pmc summary (separate passes; FETCH_SIZE doubled per the gfx950 calibration in the
     MI355X guide: it counts 64 B per 128-B request; rocprofv3 reports kilobytes)."""
@@ -96,7 +96,7 @@ def pmc_evidence(units_per_launch, kernel="k_sm_prepare<false>"):
     valu = d["SQ_INSTS_VALU"] / (d["duration_ms"] * 1e-3 * PEAK_VALU_WAVE_INSTR_PER_S)
     ev = {"source": os.path.relpath(PMC_SUMMARY, ROOT), "kernel": kernel if kernel in summary else "k_sm_prepare",
           "pmc_grid_sets": int(d["grid_size"]),
-          "hbm_bytes_per_set": round(per_set, 1), "algorithmic_bytes_per_set": ALG_BYTES_PER_SET, "valu_wave_instr_per_set": round(d["SQ_INSTS_VALU"] / d["SQ_WAVES"]),
+          "hbm_bytes_per_set": round(per_set, 1), "algorithmic_bytes_per_set": alg_bytes, "valu_wave_instr_per_set": round(d["SQ_INSTS_VALU"] / d["SQ_WAVES"]),
           "valu_issue_utilisation": round(valu, 4),
           "valu_lane_utilisation": round(d["SQ_THREAD_CYCLES_VALU"] / (64.0 * d["SQ_ACTIVE_INST_VALU"]), 4)}
     return per_set * units_per_launch, ev
@@ -607,7 +607,8 @@ def main():
     w_fme = (W_PREPARE_FME_MSM_COMB if comb else W_PREPARE_FME_MSM) if kcnt[7] > 0 else W_PREPARE_FME
     achieved = units_per_launch * w_fme * MAC_PER_FME / t_launch / 1e12 if t_launch > 0 else 0.0
     peak = PEAK_MAC_PER_S / 1e12
-    traffic, pmc = pmc_evidence(units_per_launch, "k_sm_prepare<false>" if kcnt[7] > 0 else "k_sm_prepare<true>")
+    traffic, pmc = pmc_evidence(units_per_launch, "k_sm_prepare<false>" if kcnt[7] > 0 else "k_sm_prepare<true>",
+                                ALG_BYTES_PER_SET_COMB if comb else ALG_BYTES_PER_SET)
     roofline = {"bound": "valu-int", "kernel": "k_sm_prepare", "achieved": round(achieved, 4), "peak": peak,
                 "unit": "T u32-MAC/s", "frac": round(achieved / peak, 5),
                 "traffic": round(traffic) if traffic is not None else None, "pmc": pmc,

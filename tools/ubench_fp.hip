@@ -85,7 +85,7 @@ int main() {
   printf("device %s CUs=%d clock=%d kHz\n", p.gcnArchName, p.multiProcessorCount, p.clockRate);
   Fp* out;
   hipMalloc(&out, sizeof(Fp) * 256 * 32768);
-  for (int bl : {1024, 4096, 16384}) {
+  for (int bl : {256, 512, 1024, 4096}) {
     run("fp_mul_inl x1", k_fp_mul_1, out, bl, 256, ITERS);
     run("fp_mul_inl x2", k_fp_mul_2, out, bl, 256, ITERS);
     run("fp_mul call", k_fp_mul_call, out, bl, 256, ITERS);
