@@ -90,9 +90,10 @@ struct gbv_sm_batch;
 
 struct gbv_ctx {
   int device = 0;
-  // stream A (per-set throughput kernels) at the lowest priority; the tail streams 2/3 (chunk-level
-  // latency-bound work of consecutive batches) and the hash stream 4 at the highest.
-  hipStream_t stream = nullptr, stream2 = nullptr, stream3 = nullptr, stream4 = nullptr;
+  // stream A (per-set throughput kernels) at the lowest priority; the tail stream 2 (chunk-level
+  // latency-bound work) and the hash stream 4 at the highest.  Three streams = three hardware
+  // queues (GPU_MAX_HW_QUEUES=4 leaves one for the runtime): no two streams share a queue.
+  hipStream_t stream = nullptr, stream2 = nullptr, stream4 = nullptr;
   gbv::G1A* table = nullptr;
   uint8_t* table_ok = nullptr;
   size_t table_cap = 0;
@@ -105,7 +106,7 @@ struct gbv_ctx {
   bool comb_on = true;
   std::string err;
   uint32_t nonce = 0;
-  uint32_t sm_submits = 0;  // parity picks the tail stream of a batch
+  uint32_t sm_submits = 0;  // batches submitted (statistics)
   // A failing MSM segment pays the per-set G2 terms after all (k_sm_redo_g2) on top of the MSM, so
   // after one the next MSM_COOLDOWN submits use the per-set ladders (invalid-dense streams, C5)
   uint32_t msm_cooldown = 0;

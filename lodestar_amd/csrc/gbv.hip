@@ -204,10 +204,9 @@ int gbv_init(int device, gbv_ctx** out) {
   bool ok = hipSetDevice(device) == hipSuccess && hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) == hipSuccess &&
             hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, prio_lo) == hipSuccess &&
             hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, prio_hi) == hipSuccess &&
-            hipStreamCreateWithPriority(&c->stream3, hipStreamNonBlocking, prio_hi) == hipSuccess &&
             hipStreamCreateWithPriority(&c->stream4, hipStreamNonBlocking, prio_hi) == hipSuccess;
   if (!ok) {
-    for (hipStream_t s : {c->stream, c->stream2, c->stream3, c->stream4})
+    for (hipStream_t s : {c->stream, c->stream2, c->stream4})
       if (s) hipStreamDestroy(s);
     delete c;
     return GBV_E_DEVICE;
@@ -223,7 +222,7 @@ void gbv_destroy(gbv_ctx* c) {
   hipSetDevice(c->device);
   c->closed = true;
   // every stream drains before anything it may still read or write is freed
-  for (hipStream_t s : {c->stream, c->stream2, c->stream3, c->stream4})
+  for (hipStream_t s : {c->stream, c->stream2, c->stream4})
     if (s) hipStreamSynchronize(s);
   sm_destroy(c->sm_scratch);
   vs_batch_free(c->vs_scratch);
@@ -236,7 +235,7 @@ void gbv_destroy(gbv_ctx* c) {
   for (auto* p : c->ssz_buf) hipFree(p);
   for (auto e : c->ssz_ev)
     if (e) hipEventDestroy(e);
-  for (hipStream_t s : {c->stream, c->stream2, c->stream3, c->stream4})
+  for (hipStream_t s : {c->stream, c->stream2, c->stream4})
     if (s) hipStreamDestroy(s);
   delete c;
 }
@@ -579,12 +578,16 @@ int gbv_sm_batch_submit(gbv_ctx* c, gbv_sm_batch* b) {
   if (b->n == 0) return GBV_OK;
   Seed seed = fresh_seed();
   uint32_t nonce = c->nonce++;
-  // GBV_FLIP=1: alternate the tail stream per batch so that the tails of consecutive batches
-  // overlap (each beside the next batch's k_sm_prepare on stream A)
-  static const bool use_flip = getenv("GBV_FLIP") != nullptr;
-  const bool flip = use_flip && (c->sm_submits++ & 1) != 0;
+  // Three streams, one hardware queue each: with GPU_MAX_HW_QUEUES=4 (HIP's default, and the
+  // box's), a fourth live stream shares a hardware queue with another, and a cross-stream wait
+  // (barrier packet) at the head of the shared queue blocks the other stream's packets behind it.
+  // Round 1's alternating tail streams (GBV_FLIP) hit exactly that: 3.37 M sets/s with stalls of
+  // 0.1-8 s at GPU_MAX_HW_QUEUES=4, 17.37 M at 8 (profiles/r02_flip_*), where it also no longer
+  // beats one tail stream (17.50 M): the flip is gone, every tail runs on stream 2.
+  const bool flip = false;
+  c->sm_submits++;
   hipStream_t sa = c->stream, sh = c->stream4;
-  hipStream_t sbs[2] = {flip ? c->stream3 : c->stream2, flip ? c->stream2 : c->stream3};
+  hipStream_t sbs[2] = {c->stream2, c->stream2};
   const size_t max_seg = b->seg_cap;
   const size_t n_seg = getenv("GBV_SEGMENTS") ? (size_t)std::max(1, atoi(getenv("GBV_SEGMENTS"))) : 1;
   size_t sub_sets = std::max<size_t>((b->n + n_seg - 1) / n_seg, 16384);

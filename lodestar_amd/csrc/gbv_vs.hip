@@ -268,8 +268,10 @@ void gbv_vs_batch_destroy(gbv_ctx* c, gbv_vs_batch* b) {
 }
 
 // Enqueue the whole verification without a host round trip: the per-set kernels on stream A, the
-// chunk checks on a tail stream (alternating per submit) so that they overlap the next batch's
-// per-set kernels.
+// Miller values and chunk checks on a tail stream, alternating per submit between stream 2 and the
+// hash stream (idle in this path), so that consecutive batches' tails overlap each other and the
+// next batch's per-set kernels -- still three streams in all (gbv_sm_batch_submit: a fourth live
+// stream oversubscribes GPU_MAX_HW_QUEUES=4).
 int gbv_vs_batch_submit(gbv_ctx* c, gbv_vs_batch* b) {
   if (!c || !b) return GBV_E_ARG;
   if (c->closed) return GBV_E_CLOSED;
@@ -277,7 +279,7 @@ int gbv_vs_batch_submit(gbv_ctx* c, gbv_vs_batch* b) {
   HIP_CHECK(c, hipSetDevice(c->device));
   if (b->n == 0 || b->C == 0) return GBV_OK;
   b->tail = (int)(c->sm_submits++ & 1);
-  hipStream_t t = b->tail ? c->stream3 : c->stream2;
+  hipStream_t t = b->tail ? c->stream4 : c->stream2;
   int rc = vs_enqueue_sets(c, b, t);
   if (rc) return rc;
   launch_vs_chunk_coop(LaunchCfg{(unsigned)b->C, 64, t}, (uint32_t)b->C, b->chunk_off, b->status, b->F, b->rS, b->chunk_valid);
