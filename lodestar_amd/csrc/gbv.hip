@@ -578,16 +578,19 @@ int gbv_sm_batch_submit(gbv_ctx* c, gbv_sm_batch* b) {
   if (b->n == 0) return GBV_OK;
   Seed seed = fresh_seed();
   uint32_t nonce = c->nonce++;
-  // Three streams, one hardware queue each: with GPU_MAX_HW_QUEUES=4 (HIP's default, and the
-  // box's), a fourth live stream shares a hardware queue with another, and a cross-stream wait
-  // (barrier packet) at the head of the shared queue blocks the other stream's packets behind it.
-  // Round 1's alternating tail streams (GBV_FLIP) hit exactly that: 3.37 M sets/s with stalls of
-  // 0.1-8 s at GPU_MAX_HW_QUEUES=4, 17.37 M at 8 (profiles/r02_flip_*), where it also no longer
-  // beats one tail stream (17.50 M): the flip is gone, every tail runs on stream 2.
-  const bool flip = false;
-  c->sm_submits++;
-  hipStream_t sa = c->stream, sh = c->stream4;
-  hipStream_t sbs[2] = {c->stream2, c->stream2};
+  // Same-message batches: hash on stream 4, tail on stream 2, every batch.  Alternating the tails
+  // of consecutive batches over two streams stalls the device for 0.1-8 s at a time at
+  // GPU_MAX_HW_QUEUES=4 (HIP's default and the box's) and never at 8 -- with four streams
+  // (round 1's GBV_FLIP: 3.37 M sets/s vs 17.37 M at 8 queues, profiles/r02_flip_*) and with three
+  // (hash and tail of a batch on the same alternating stream, GBV_ALT_TAIL=1: 1.14 M sets/s,
+  // profiles/r02s_alt_tail_hash_bench_STALL.json): the streams' cross-stream waits meet in shared
+  // hardware queues.  One tail stream leaves consecutive tails serialised, which costs nothing
+  // while the tail is shorter than k_sm_prepare (all-valid streams).
+  static const bool alt_tail = getenv("GBV_ALT_TAIL") != nullptr;  // diagnosis only
+  const bool flip = alt_tail && (c->sm_submits++ & 1) != 0;
+  hipStream_t sa = c->stream;
+  hipStream_t tail = flip ? c->stream4 : c->stream2, sh = alt_tail ? tail : c->stream4;
+  hipStream_t sbs[2] = {tail, tail};
   const size_t max_seg = b->seg_cap;
   const size_t n_seg = getenv("GBV_SEGMENTS") ? (size_t)std::max(1, atoi(getenv("GBV_SEGMENTS"))) : 1;
   size_t sub_sets = std::max<size_t>((b->n + n_seg - 1) / n_seg, 16384);
