@@ -272,6 +272,24 @@ GBV_HD Fp fp_mul_inl(const Fp& a, const Fp& b) {
   uint32_t m[12], r[12];
   uint64_t acc = 0;
   uint32_t top = 0;
+#if defined(__HIP_DEVICE_COMPILE__)
+  // device: each column's MACs are ONE generated asm block (fp_asm.h GBV_ASM_FIPS_COL*)
+#define GBV_COL_LO(K)                              \
+  GBV_ASM_FIPS_COL##K(acc, top, a, b, m);          \
+  m[K] = (uint32_t)acc * NP0;                      \
+  mac96_k(acc, top, m[K], P_RAW.v[0]);             \
+  acc = (acc >> 32) | ((uint64_t)top << 32);
+#define GBV_COL_HI(K)                              \
+  GBV_ASM_FIPS_COL##K(acc, top, a, b, m);          \
+  r[K - 12] = (uint32_t)acc;                       \
+  acc = (acc >> 32) | ((uint64_t)top << 32);
+  GBV_COL_LO(0) GBV_COL_LO(1) GBV_COL_LO(2) GBV_COL_LO(3) GBV_COL_LO(4) GBV_COL_LO(5)
+  GBV_COL_LO(6) GBV_COL_LO(7) GBV_COL_LO(8) GBV_COL_LO(9) GBV_COL_LO(10) GBV_COL_LO(11)
+  GBV_COL_HI(12) GBV_COL_HI(13) GBV_COL_HI(14) GBV_COL_HI(15) GBV_COL_HI(16) GBV_COL_HI(17)
+  GBV_COL_HI(18) GBV_COL_HI(19) GBV_COL_HI(20) GBV_COL_HI(21) GBV_COL_HI(22)
+#undef GBV_COL_LO
+#undef GBV_COL_HI
+#else
   fips_col_lo<0>(acc, top, a, b, m), fips_col_lo<1>(acc, top, a, b, m), fips_col_lo<2>(acc, top, a, b, m);
   fips_col_lo<3>(acc, top, a, b, m), fips_col_lo<4>(acc, top, a, b, m), fips_col_lo<5>(acc, top, a, b, m);
   fips_col_lo<6>(acc, top, a, b, m), fips_col_lo<7>(acc, top, a, b, m), fips_col_lo<8>(acc, top, a, b, m);
@@ -280,6 +298,7 @@ GBV_HD Fp fp_mul_inl(const Fp& a, const Fp& b) {
   fips_col_hi<15>(acc, top, a, b, m, r), fips_col_hi<16>(acc, top, a, b, m, r), fips_col_hi<17>(acc, top, a, b, m, r);
   fips_col_hi<18>(acc, top, a, b, m, r), fips_col_hi<19>(acc, top, a, b, m, r), fips_col_hi<20>(acc, top, a, b, m, r);
   fips_col_hi<21>(acc, top, a, b, m, r), fips_col_hi<22>(acc, top, a, b, m, r);
+#endif
   r[11] = (uint32_t)acc;
   Fp o;
 #pragma unroll
