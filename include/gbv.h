@@ -146,6 +146,14 @@ int gbv_aggregate_serialized_pubkeys(gbv_ctx* ctx, const uint8_t* pk48, size_t k
  * (beacon-node/test/perf/bls/bls.test.ts:89-100). */
 int gbv_signatures_validate(gbv_ctx* ctx, const uint8_t* sigs, size_t n, uint32_t sig_len, uint8_t* status, uint8_t* out96);
 
+/* aggregateSignatures(sigs.map(s => Signature.fromBytes(s, validate))).toBytes() -- the aggregate of
+ * BlsSingleThreadVerifier.verifySignatureSetsSameMessage (beacon-node/src/chain/bls/singleThread.ts:44-57),
+ * byte-identical.  validate != 0 applies Signature.fromBytes(sig, true) (infinity and subgroup
+ * rejected); validate == 0 lets an infinity signature contribute nothing.  A signature that fails
+ * to deserialize returns GBV_E_BAD_POINT (the reference's fromBytes throw), n == 0
+ * GBV_E_EMPTY_AGGREGATE. */
+int gbv_aggregate_signatures(gbv_ctx* ctx, const uint8_t* sigs, size_t n, uint32_t sig_len, int validate, uint8_t out96[96]);
+
 /* ---- device-resident batches (inputs staged in HBM once, verified many times) ------------- */
 typedef struct gbv_sm_batch gbv_sm_batch;
 /* Stage a same-message workload (as gbv_verify_same_message_multi) in HBM. */

@@ -28,7 +28,7 @@ EXPORTED_SYMBOLS = (
     "gbv_pubkeys_replicate", "gbv_sha256_digest64", "gbv_merkle_roots", "gbv_signing_roots",
     "gbv_attestation_signing_roots", "gbv_ssz_last_kernel_ms", "gbv_verify_sets_multi", "gbv_vs_batch_create",
     "gbv_vs_batch_submit", "gbv_vs_batch_wait", "gbv_vs_batch_destroy", "gbv_vs_last_kernel_ms",
-    "gbv_aggregate_serialized_pubkeys", "gbv_signatures_validate",
+    "gbv_aggregate_serialized_pubkeys", "gbv_signatures_validate", "gbv_aggregate_signatures",
 )
 
 
@@ -114,6 +114,7 @@ def load_library(path=LIB_PATH):
         "gbv_vs_last_kernel_ms": (i32, [vp, P(ctypes.c_float)]),
         "gbv_aggregate_serialized_pubkeys": (i32, [vp, vp, sz, i32, vp]),
         "gbv_signatures_validate": (i32, [vp, vp, sz, u32, vp, vp]),
+        "gbv_aggregate_signatures": (i32, [vp, vp, sz, u32, i32, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

@@ -467,6 +467,35 @@ int gbv_signatures_validate(gbv_ctx* c, const uint8_t* sigs, size_t n, uint32_t 
   return GBV_OK;
 }
 
+int gbv_aggregate_signatures(gbv_ctx* c, const uint8_t* sigs, size_t n, uint32_t sig_len, int validate, uint8_t out96[96]) {
+  if (!c) return GBV_E_ARG;
+  if (c->closed) return GBV_E_CLOSED;
+  if (n == 0) return gbv_fail(c, GBV_E_EMPTY_AGGREGATE, "EMPTY_AGGREGATE_ARRAY");
+  if (!sigs || !out96) return gbv_fail(c, GBV_E_ARG, "null argument");
+  if (sig_len != 96 && sig_len != 192) return gbv_fail(c, GBV_E_ARG, "sig_len must be 96 or 192");
+  if (n > 0xFFFFFFFFull) return gbv_fail(c, GBV_E_ARG, "too many signatures");
+  HIP_CHECK(c, hipSetDevice(c->device));
+  // device scratch: [sigs][bad u32][out 96][block partials]
+  size_t nb = (n + 63) / 64;
+  size_t o_bad = align256((size_t)sig_len * n), o_out = o_bad + 256, o_part = o_out + 256, total = o_part + sizeof(G2J) * nb;
+  uint8_t *d = nullptr, *h = nullptr;
+  int rc;
+  if ((rc = ctx_small_dev(c, total, &d)) || (rc = ctx_small_host(c, std::max<size_t>((size_t)sig_len * n, 512), &h))) return rc;
+  memcpy(h, sigs, (size_t)sig_len * n);
+  HIP_CHECK(c, hipMemcpyAsync(d, h, (size_t)sig_len * n, hipMemcpyHostToDevice, c->stream));
+  HIP_CHECK(c, hipMemsetAsync(d + o_bad, 0, 4, c->stream));
+  launch_sig_aggregate(c->stream, (uint32_t)n, d, sig_len, validate, (G2J*)(d + o_part), (uint32_t*)(d + o_bad), d + o_out);
+  HIP_CHECK(c, hipGetLastError());
+  HIP_CHECK(c, hipMemcpyAsync(h, d + o_bad, 4, hipMemcpyDeviceToHost, c->stream));
+  HIP_CHECK(c, hipMemcpyAsync(h + 256, d + o_out, 96, hipMemcpyDeviceToHost, c->stream));
+  HIP_CHECK(c, hipStreamSynchronize(c->stream));
+  uint32_t bad;
+  memcpy(&bad, h, 4);
+  if (bad) return gbv_fail(c, GBV_E_BAD_POINT, "signature failed to deserialize");
+  memcpy(out96, h + 256, 96);
+  return GBV_OK;
+}
+
 // ---- same-message batches ------------------------------------------------------------------
 void gbv_sm_batch_destroy(gbv_ctx* c, gbv_sm_batch* b) {
   (void)c;

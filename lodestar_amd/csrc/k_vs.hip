@@ -156,6 +156,56 @@ __global__ void GBV_KERNEL_ATTR k_sig_validate(uint32_t n, const uint8_t* __rest
     g2_compress(out96 + 96ull * i, s, true);  // infinity encoding as the placeholder of a rejected input
 }
 
+// aggregateSignatures(Signature.fromBytes(sig_i, validate)) (singleThread.ts:54-57): stage 1, one
+// thread per signature decodes (+ subgroup check), a 6-level shuffle tree sums the wave, lane 0
+// writes the block's Jacobian partial; any rejected input raises *bad.
+GBV_NI G2J vs_g2_add(G2J a, G2J b) { return jac_add(a, b); }
+__device__ inline Fp2 vs_shfl_down2(const Fp2& a, unsigned d) { return Fp2{vs_shfl_down(a.c0, d), vs_shfl_down(a.c1, d)}; }
+__device__ inline G2J wave_sum_g2(G2J acc) {
+  for (unsigned d = 32; d > 0; d >>= 1) {
+    G2J o{vs_shfl_down2(acc.x, d), vs_shfl_down2(acc.y, d), vs_shfl_down2(acc.z, d)};
+    acc = vs_g2_add(acc, o);
+  }
+  return acc;
+}
+
+__global__ void GBV_KERNEL_ATTR k_sig_aggregate(uint32_t n, const uint8_t* __restrict__ sig, uint32_t sig_len, int validate,
+                                                G2J* __restrict__ part, uint32_t* __restrict__ bad) {
+  uint32_t i = blockIdx.x * 64 + threadIdx.x;
+  G2J acc = jac_infinity<Fp2>();
+  if (i < n) {
+    G2A s;
+    uint8_t st = g2_decode(s, sig + (size_t)sig_len * i, sig_len);
+    if (validate && st == PT_OK && !g2_in_subgroup(s)) st = PT_NOT_IN_GROUP;
+    bool reject = st != PT_OK && (validate || st != PT_INFINITY);
+    if (reject) atomicOr(bad, 1u);
+    else if (st == PT_OK) acc = jac_from_aff(s);
+  }
+  acc = wave_sum_g2(acc);
+  if (threadIdx.x == 0) part[blockIdx.x] = acc;
+}
+
+// stage 2: one wave sums the nb block partials and writes the compressed aggregate.
+__global__ void __launch_bounds__(64) k_sig_aggregate_final(uint32_t nb, const G2J* __restrict__ part, uint8_t* __restrict__ out96) {
+  G2J acc = jac_infinity<Fp2>();
+  for (uint32_t b = threadIdx.x; b < nb; b += 64) acc = vs_g2_add(acc, part[b]);
+  acc = wave_sum_g2(acc);
+  if (threadIdx.x == 0) {
+    G2A a;
+    bool fin = jac_to_aff(a, acc);
+    g2_compress(out96, a, !fin);
+  }
+}
+
+void launch_sig_aggregate(hipStream_t s, uint32_t n, const uint8_t* sig, uint32_t sig_len, int validate, G2J* part, uint32_t* bad,
+                          uint8_t* out96) {
+  uint32_t nb = (n + 63) / 64;
+  hipLaunchKernelGGL(k_sig_aggregate, dim3(nb), dim3(64), 0, s, n, sig, sig_len, validate, part, bad);
+  debug_sync(s, "k_sig_aggregate");
+  hipLaunchKernelGGL(k_sig_aggregate_final, dim3(1), dim3(64), 0, s, nb, part, out96);
+  debug_sync(s, "k_sig_aggregate_final");
+}
+
 void launch_vs_agg(LaunchCfg c, const uint32_t* agg_list, const uint32_t* set_off, const uint32_t* arena, const G1A* table,
                    const uint8_t* table_ok, G1J* pk_out, uint8_t* pk_st) {
   const uint32_t n_agg = c.blocks;  // c.blocks carries the aggregate-set count

@@ -91,6 +91,8 @@ void launch_vs_hash_sig(hipStream_t s, uint32_t n, const uint8_t* msgs32, const 
 void launch_vs_miller_coop(hipStream_t s, uint32_t n, const uint8_t* status, const G1J* rP, const G2A* H, Fp12* F);
 void launch_vs_miller(LaunchCfg c, uint32_t n, const uint8_t* status, const G1J* rP, const G2A* H, Fp12* F);
 void launch_sig_validate(LaunchCfg c, uint32_t n, const uint8_t* sig, uint32_t sig_len, uint8_t* status, uint8_t* out96);
+void launch_sig_aggregate(hipStream_t s, uint32_t n, const uint8_t* sig, uint32_t sig_len, int validate, G2J* part, uint32_t* bad,
+                          uint8_t* out96);
 
 void launch_ssz_digest64(hipStream_t s, const uint8_t* in64, uint32_t n, uint8_t* out32);
 void launch_ssz_signing_roots(hipStream_t s, const uint8_t* roots32, uint32_t n, const uint8_t* domains32, const uint32_t* dom_idx,

@@ -275,6 +275,19 @@ class GpuBlsVerifier:
         raw = out.raw
         return st.raw[:n], [raw[96 * i:96 * i + 96] for i in range(n)]
 
+    def aggregate_signatures(self, sigs: Sequence[bytes], validate: bool = True, sig_len: int = 96) -> bytes:
+        """aggregateSignatures(sigs.map(s => Signature.fromBytes(s, validate))).toBytes()
+        (singleThread.ts:44-57), on the device.  Raises BadPointError when a signature fails to
+        deserialize, EmptyAggregateError on an empty list."""
+        self._check_open()
+        blob = b"".join(bytes(x) for x in sigs)
+        if len(blob) != len(sigs) * sig_len:
+            raise ValueError("every signature must be %d bytes" % sig_len)
+        out = ctypes.create_string_buffer(96)
+        rc = self._lib.gbv_aggregate_signatures(self._ctx, blob or b"\0", len(sigs), sig_len, 1 if validate else 0, out)
+        _native.check(self._lib, self._ctx, rc)
+        return out.raw
+
     def verify_signature_set(self, s: ISignatureSet) -> bool:
         """Synchronous single-set verification used inside the state transition
         (state-transition/src/util/signatureSets.ts:25-39): verify for a single set,

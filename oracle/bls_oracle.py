@@ -955,6 +955,31 @@ def pool_verify_same_message(sets, msg) -> list:
     return out
 
 
+def single_thread_verify_same_message(sets, msg) -> list:
+    """BlsSingleThreadVerifier.verifySignatureSetsSameMessage (singleThread.ts:36-80): the
+    UNRANDOMIZED aggregate verify(msg, aggregatePublicKeys(pks), aggregateSignatures(sigs)); all
+    true when it holds, else verify per set.  sets: list of (pk_point, sig_bytes).  Raises
+    ValueError on an empty list (aggregatePublicKeys throws, :41)."""
+    pk = aggregate_pubkeys([p for p, _ in sets])
+    sigs, all_valid = [], True
+    for _, sb in sets:                                   # :44-52, Signature.fromBytes(sig, true)
+        try:
+            sigs.append(signature_from_bytes(sb, True))
+        except DecodeError:
+            sigs.append(None)
+            all_valid = False
+    if all_valid:                                        # :54-57
+        agg = None
+        for sg in sigs:
+            agg = g2_add(agg, sg)
+        # blst verify: an infinite pubkey is rejected (PK_IS_INFINITY); an infinite aggregate
+        # signature leaves e(pk, H(m)) != 1.  core_verify answers False for both.
+        all_valid = core_verify(pk, msg, agg)
+    if all_valid:
+        return [True] * len(sets)
+    return [sg is not None and core_verify(p, msg, sg) for (p, _), sg in zip(sets, sigs)]   # :62-71
+
+
 def random_scalar(rng=None):
     rng = rng or _random.Random(0)
     return rng.randrange(1, R)

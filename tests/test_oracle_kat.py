@@ -144,3 +144,29 @@ def test_chunkify():
     assert c(list(range(6)), 3) == [[0, 1, 2], [3, 4, 5]]
     assert c(list(range(7)), 3) == [[0, 1, 2, 3], [4, 5, 6]]
     assert c(list(range(9)), 3) == [[0, 1, 2], [3, 4, 5], [6, 7, 8]]
+
+
+def test_single_thread_same_message_semantics():
+    """singleThread.ts:36-80 vs the pool (index.ts:212-236): the unrandomized aggregate accepts
+    signatures whose errors cancel (swapped_keys), so the single-thread verifier answers all true
+    where the pool's randomized check falls back to per-set results.  Pins the golden vectors of
+    tests/golden/single_thread.json against the live oracle on the cases that decide it."""
+    import json
+    import os
+    st = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "single_thread.json")))
+    fix = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "fixtures.json")))
+    pks = [o.g1_decompress(bytes.fromhex(p)) for p in fix["keys"]["pks"]]
+    by_name = {c["name"]: c for c in st["same_message"]}
+    sm = by_name["swapped_keys"]
+    sets = [(pks[i], bytes.fromhex(s)) for i, s in zip(sm["indices"], sm["sigs"])]
+    assert o.single_thread_verify_same_message(sets, bytes.fromhex(sm["msg"])) == [True, True, True] == sm["expected"]
+    assert sm["pool_expected"] == [True, False, False]
+    for name in ("all_valid", "one_wrong_message", "one_malformed", "six_two_bad"):  # bls.test.ts:68-82: both agree
+        assert by_name[name]["expected"] == by_name[name]["pool_expected"]
+    with pytest.raises(ValueError):
+        o.single_thread_verify_same_message([], bytes(32))
+    assert by_name["empty"]["expected"] == "reject"
+    # aggregateSignatures vectors: a two-signature sum matches the live oracle
+    a = [c for c in st["aggregate_signatures"] if c["name"] == "two"][0]
+    pts = [o.signature_from_bytes(bytes.fromhex(s), True) for s in a["sigs"]]
+    assert o.g2_compress(o.g2_add(pts[0], pts[1])).hex() == a["expected"]
