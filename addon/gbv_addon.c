@@ -555,6 +555,73 @@ static napi_value aggregate_impl(napi_env env, napi_callback_info info, int seri
 static napi_value js_aggregate_pubkeys(napi_env env, napi_callback_info info) { return aggregate_impl(env, info, 0); }
 static napi_value js_aggregate_serialized(napi_env env, napi_callback_info info) { return aggregate_impl(env, info, 1); }
 
+/* aggregateSignatures(ctx, sigs: Uint8Array of n*96 bytes, validate) -> Uint8Array(96), synchronous
+ * like blst's aggregateSignatures (singleThread.ts:55); gbv_aggregate_signatures. */
+static napi_value js_aggregate_signatures(napi_env env, napi_callback_info info) {
+  size_t argc = 3;
+  napi_value argv[3];
+  NAPI_OK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  addon_ctx* ac = argc >= 1 ? get_ctx(env, argv[0]) : NULL;
+  if (!ac) return NULL;
+  const uint8_t* d;
+  size_t len;
+  if (argc < 2 || !get_bytes(env, argv[1], &d, &len) || len % 96) {
+    napi_throw_type_error(env, "GBV_E_ARG", "aggregateSignatures(ctx, sig96s: Uint8Array of n*96 bytes, validate)");
+    return NULL;
+  }
+  bool validate = true;
+  if (argc >= 3) napi_get_value_bool(env, argv[2], &validate);
+  if (ac->closed || !ac->ctx) {
+    throw_rc(env, GBV_E_CLOSED, "QUEUE_ABORTED");
+    return NULL;
+  }
+  uint8_t out[96];
+  lock_begin(ac);
+  int rc = gbv_aggregate_signatures(ac->ctx, len ? d : (const uint8_t*)"", len / 96, 96, validate ? 1 : 0, out);
+  if (rc) {
+    throw_rc(env, rc, gbv_last_error(ac->ctx));
+    lock_end(ac);
+    return NULL;
+  }
+  lock_end(ac);
+  void* p;
+  napi_value ab, res;
+  NAPI_OK(env, napi_create_arraybuffer(env, 96, &p, &ab));
+  memcpy(p, out, 96);
+  NAPI_OK(env, napi_create_typedarray(env, napi_uint8_array, 96, ab, 0, &res));
+  return res;
+}
+
+/* validateSignatures(ctx, sigs: Uint8Array of n*96 bytes) -> Uint8Array(n) of GBV_PT_* codes:
+ * Signature.fromBytes(sig, true) per signature (singleThread.ts:44-52); gbv_signatures_validate. */
+static napi_value js_validate_signatures(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2];
+  NAPI_OK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  addon_ctx* ac = argc >= 1 ? get_ctx(env, argv[0]) : NULL;
+  if (!ac) return NULL;
+  const uint8_t* d;
+  size_t len;
+  if (argc < 2 || !get_bytes(env, argv[1], &d, &len) || len % 96) {
+    napi_throw_type_error(env, "GBV_E_ARG", "validateSignatures(ctx, sig96s: Uint8Array of n*96 bytes)");
+    return NULL;
+  }
+  if (ac->closed || !ac->ctx) {
+    throw_rc(env, GBV_E_CLOSED, "QUEUE_ABORTED");
+    return NULL;
+  }
+  size_t n = len / 96;
+  void* st_data = NULL;
+  napi_value ab, st;
+  NAPI_OK(env, napi_create_arraybuffer(env, n ? n : 1, &st_data, &ab));
+  NAPI_OK(env, napi_create_typedarray(env, napi_uint8_array, n, ab, 0, &st));
+  lock_begin(ac);
+  int rc = gbv_signatures_validate(ac->ctx, n ? d : (const uint8_t*)"", n, 96, (uint8_t*)st_data, NULL);
+  if (rc) throw_rc(env, rc, gbv_last_error(ac->ctx));
+  lock_end(ac);
+  return rc ? NULL : st;
+}
+
 static napi_value js_verify_sets(napi_env env, napi_callback_info info) {
   size_t argc = 2;
   napi_value argv[2];
@@ -689,6 +756,8 @@ static napi_value init(napi_env env, napi_value exports) {
       {"verifySameMessageMulti", NULL, js_verify_same_message_multi, NULL, NULL, NULL, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), NULL},
       {"aggregatePubkeys", NULL, js_aggregate_pubkeys, NULL, NULL, NULL, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), NULL},
       {"aggregateSerializedPubkeys", NULL, js_aggregate_serialized, NULL, NULL, NULL, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), NULL},
+      {"aggregateSignatures", NULL, js_aggregate_signatures, NULL, NULL, NULL, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), NULL},
+      {"validateSignatures", NULL, js_validate_signatures, NULL, NULL, NULL, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), NULL},
       {"close", NULL, js_close, NULL, NULL, NULL, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), NULL},
   };
   napi_define_properties(env, exports, sizeof props / sizeof props[0], props);

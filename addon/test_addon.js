@@ -8,7 +8,7 @@ const fs = require("fs");
 const addon = require(path.join(__dirname, "gbv_addon.node"));
 
 const EXPORTS = ["open", "addPubkeys", "verifySets", "verifySetsMulti", "verifySameMessageMulti", "aggregatePubkeys",
-  "aggregateSerializedPubkeys", "close"];
+  "aggregateSerializedPubkeys", "aggregateSignatures", "validateSignatures", "close"];
 const hex = (h) => Uint8Array.from(Buffer.from(h, "hex"));
 const report = {};
 
@@ -29,6 +29,26 @@ function toSets(c) {
     else o.indices = Uint32Array.from(s.indices);
     return o;
   });
+}
+
+// BlsSingleThreadVerifier.verifySignatureSetsSameMessage (singleThread.ts:36-80) written over the
+// addon, as the TypeScript side of a drop-in would: device aggregate pubkey, device signature
+// validation, device aggregateSignatures, one unrandomized verify, per-set retry in one pass.
+async function singleThreadSameMessage(ctx, sets, message) {
+  const pk = addon.aggregatePubkeys(ctx, sets.map((s) => s.index)); // throws EMPTY_AGGREGATE_ARRAY on []
+  const sigs = Buffer.concat(sets.map((s) => Buffer.from(s.signature.length === 96 ? s.signature : new Uint8Array(96))));
+  const st = addon.validateSignatures(ctx, Uint8Array.from(sigs));
+  let isAllValid = Array.from(st).every((x) => x === 0);
+  if (isAllValid) {
+    const agg = addon.aggregateSignatures(ctx, Uint8Array.from(sigs), true);
+    isAllValid = await addon.verifySets(ctx, [{pubkey: pk, signingRoot: message, signature: agg}]);
+  }
+  if (isAllValid) return sets.map(() => true);
+  const todo = sets.map((_, i) => i).filter((i) => st[i] === 0);
+  const res = await addon.verifySetsMulti(ctx, todo.map((i) => [{index: sets[i].index, signingRoot: message, signature: sets[i].signature}]));
+  const out = sets.map(() => false);
+  todo.forEach((i, k) => (out[i] = res[k] === true));
+  return out;
 }
 
 async function cpu() {
@@ -73,6 +93,27 @@ async function gpu(fixPath) {
     return Buffer.from(addon.aggregateSerializedPubkeys(ctx, Uint8Array.from(ser), false)).toString("hex") === c.expected;
   });
   report.emptyAggregate = expectThrow(() => addon.aggregatePubkeys(ctx, []), "EMPTY_AGGREGATE_ARRAY");
+  // single-thread semantics (tests/golden/single_thread.json) over the addon primitives
+  const stf = JSON.parse(fs.readFileSync(path.join(path.dirname(fixPath), "single_thread.json"), "utf8"));
+  addon.addPubkeys(ctx, stf.extra_index, hex(stf.extra_pk), true);
+  const single = [];
+  for (const c of stf.same_message) {
+    const sets = c.indices.map((idx, k) => ({index: idx, signature: hex(c.sigs[k])}));
+    try {
+      single.push(JSON.stringify(await singleThreadSameMessage(ctx, sets, hex(c.msg))) === JSON.stringify(c.expected));
+    } catch (e) {
+      single.push(c.expected === "reject" && e.code === "EMPTY_AGGREGATE_ARRAY");
+    }
+  }
+  report.singleThread = single;
+  report.aggregateSignatures = stf.aggregate_signatures.map((c) => {
+    const sigs = Uint8Array.from(Buffer.concat(c.sigs.map((x) => Buffer.from(x, "hex"))));
+    try {
+      return Buffer.from(addon.aggregateSignatures(ctx, sigs, c.validate)).toString("hex") === c.expected;
+    } catch (e) {
+      return (c.expected === "bad_point" && e.code === "GBV_E_BAD_POINT") || (c.expected === "empty" && e.code === "EMPTY_AGGREGATE_ARRAY");
+    }
+  });
   // concurrent submissions are serialised per context and all resolve
   const conc = await Promise.all([0, 1, 2, 3].map(() => addon.verifySets(ctx, toSets(fix.verify_sets[0]))));
   report.concurrent = conc.every((r) => r === fix.verify_sets[0].expected);

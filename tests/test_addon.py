@@ -48,7 +48,7 @@ def test_addon_builds_and_maps_errors_without_gpu():
         pytest.skip("this case checks the no-device error path")
     r = _run("cpu")
     assert r["exports"] == ["open", "addPubkeys", "verifySets", "verifySetsMulti", "verifySameMessageMulti", "aggregatePubkeys",
-                            "aggregateSerializedPubkeys", "close"]
+                            "aggregateSerializedPubkeys", "aggregateSignatures", "validateSignatures", "close"]
     assert r["open"] == "ok"      # gbv_init without a device -> Error code GBV_E_DEVICE
     assert r["badCtx"] == "ok"    # not a context -> TypeError code GBV_E_ARG
     assert r["badArg"] == "ok"
@@ -64,6 +64,8 @@ def test_addon_golden_cases_on_gpu():
     assert all(r["sameMessage"]) and r["sameMessage"]
     assert all(r["aggregate"]) and all(r["aggregateSerialized"])
     assert r["emptyAggregate"] == "ok"
+    assert all(r["singleThread"]) and len(r["singleThread"]) == 11   # singleThread.ts semantics, incl. swapped_keys
+    assert all(r["aggregateSignatures"]) and len(r["aggregateSignatures"]) == 7
     assert r["concurrent"] is True
     assert r["inflightBeforeClose"] is True
     assert r["afterClose"] == "QUEUE_ABORTED"
