@@ -59,8 +59,9 @@ struct gbv_vs_batch {
 };
 
 static void vs_free_work(gbv_vs_batch* b) {
-  hipFree(b->pk); hipFree(b->pk_st); hipFree(b->H); hipFree(b->rP); hipFree(b->rS); hipFree(b->status); hipFree(b->F);
-  hipFree(b->chunk_valid); hipHostFree(b->chunk_valid_host);
+  // teardown: a failing free has nothing left to report to
+  (void)hipFree(b->pk); (void)hipFree(b->pk_st); (void)hipFree(b->H); (void)hipFree(b->rP); (void)hipFree(b->rS);
+  (void)hipFree(b->status); (void)hipFree(b->F); (void)hipFree(b->chunk_valid); (void)hipHostFree(b->chunk_valid_host);
   b->pk = nullptr; b->pk_st = nullptr; b->H = nullptr; b->rP = nullptr; b->rS = nullptr; b->status = nullptr; b->F = nullptr;
   b->chunk_valid = nullptr; b->chunk_valid_host = nullptr;
   b->allocated = false;
@@ -68,7 +69,7 @@ static void vs_free_work(gbv_vs_batch* b) {
 
 void vs_batch_free(gbv_vs_batch* b) {
   if (!b) return;
-  if (b->in_flight && b->done) hipEventSynchronize(b->done);
+  if (b->in_flight && b->done) (void)hipEventSynchronize(b->done);
   vs_free_work(b);
   hipFree(b->in_dev);
   hipHostFree(b->in_host);
