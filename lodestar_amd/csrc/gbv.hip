@@ -617,9 +617,17 @@ int gbv_sm_batch_submit(gbv_ctx* c, gbv_sm_batch* b) {
   // while the tail is shorter than k_sm_prepare (all-valid streams).
   static const bool alt_tail = getenv("GBV_ALT_TAIL") != nullptr;  // diagnosis only
   const bool flip = alt_tail && (c->sm_submits++ & 1) != 0;
+  // Invalid-dense regime (a segment failed within the last MSM_COOLDOWN submits, e.g. C5's 1 %
+  // invalid stream): the failure path -- latency-bound run and per-set checks, ~170 ms per 1M
+  // sets at 1 % -- goes to stream 4 and the hash to stream A, so batch k's failure path runs
+  // beside batch k+1's chunk tail instead of in front of it (three streams either way).
+  // GBV_FB_STREAM=0 keeps the failure path on the tail stream.
+  static const bool fb_stream_env = !(getenv("GBV_FB_STREAM") && getenv("GBV_FB_STREAM")[0] == '0');
+  const bool dense = fb_stream_env && !alt_tail && c->msm_cooldown != 0;
   hipStream_t sa = c->stream;
-  hipStream_t tail = flip ? c->stream4 : c->stream2, sh = alt_tail ? tail : c->stream4;
+  hipStream_t tail = flip ? c->stream4 : c->stream2, sh = alt_tail ? tail : (dense ? sa : c->stream4);
   hipStream_t sbs[2] = {tail, tail};
+  hipStream_t sf = dense ? c->stream4 : tail;  // failure path + copy-out
   const size_t max_seg = b->seg_cap;
   const size_t n_seg = getenv("GBV_SEGMENTS") ? (size_t)std::max(1, atoi(getenv("GBV_SEGMENTS"))) : 1;
   size_t sub_sets = std::max<size_t>((b->n + n_seg - 1) / n_seg, 16384);
@@ -738,28 +746,29 @@ int gbv_sm_batch_submit(gbv_ctx* c, gbv_sm_batch* b) {
     HIP_CHECK(c, hipStreamWaitEvent(sbs[0], ev[2 + EPS * last_b1 + 9], 0));
   }
   HIP_CHECK(c, hipEventRecord(ep[0], sbs[0]));
+  if (sf != sbs[0]) HIP_CHECK(c, hipStreamWaitEvent(sf, ep[0], 0));
   // valid = 1 for the sets of passing chunks; the sets of failed chunks go through 8-set run
   // checks and, for failing runs only, per-set checks (compacted lists, persistent grids)
-  launch_sm_fallback(LaunchCfg{blocks_for(b->n), TPB, sbs[0]}, (uint32_t)b->n, b->set_grp, b->grp_msg, b->grp_state, b->status, b->idx,
+  launch_sm_fallback(LaunchCfg{blocks_for(b->n), TPB, sf}, (uint32_t)b->n, b->set_grp, b->grp_msg, b->grp_state, b->status, b->idx,
                      c->table, b->S, b->H, b->valid, 0);
   for (size_t s = 0; s < S; ++s) {
     uint32_t s0 = b->grp_off_host[gcut[s]], s1 = b->grp_off_host[gcut[s + 1]];
-    launch_sm_fb_runs(LaunchCfg{0, 64, sbs[0]}, s0, s1 - s0, b->set_grp, b->grp_state, b->fb_runs, b->fb_cnt, (uint32_t)b->fb_cap);
+    launch_sm_fb_runs(LaunchCfg{0, 64, sf}, s0, s1 - s0, b->set_grp, b->grp_state, b->fb_runs, b->fb_cnt, (uint32_t)b->fb_cap);
   }
   // few items: one wave each (latency); many: one thread each (throughput) -- one of each pair exits
-  launch_sm_fb_blocks_coop(LaunchCfg{0, 64, sbs[0]}, b->fb_runs, b->fb_cnt, (uint32_t)b->fb_cap, b->status, b->grp_msg, b->rS, b->rP,
+  launch_sm_fb_blocks_coop(LaunchCfg{0, 64, sf}, b->fb_runs, b->fb_cnt, (uint32_t)b->fb_cap, b->status, b->grp_msg, b->rS, b->rP,
                            b->H, b->valid, b->fb_list, b->fb_cnt + 1);
-  launch_sm_fb_blocks(LaunchCfg{FB_GRID, 64, sbs[0]}, b->fb_runs, b->fb_cnt, (uint32_t)b->fb_cap, b->status, b->grp_msg, b->rS, b->rP, b->H,
+  launch_sm_fb_blocks(LaunchCfg{FB_GRID, 64, sf}, b->fb_runs, b->fb_cnt, (uint32_t)b->fb_cap, b->status, b->grp_msg, b->rS, b->rP, b->H,
                       b->valid, b->fb_list, b->fb_cnt + 1);
-  launch_sm_fb_sets_coop(LaunchCfg{0, 64, sbs[0]}, b->fb_list, b->fb_cnt + 1, b->set_grp, b->grp_msg, b->idx, c->table, b->S, b->H,
+  launch_sm_fb_sets_coop(LaunchCfg{0, 64, sf}, b->fb_list, b->fb_cnt + 1, b->set_grp, b->grp_msg, b->idx, c->table, b->S, b->H,
                          b->valid);
-  launch_sm_fb_sets(LaunchCfg{FB_GRID, 64, sbs[0]}, b->fb_list, b->fb_cnt + 1, b->set_grp, b->grp_msg, b->idx, c->table, b->S, b->H,
+  launch_sm_fb_sets(LaunchCfg{FB_GRID, 64, sf}, b->fb_list, b->fb_cnt + 1, b->set_grp, b->grp_msg, b->idx, c->table, b->S, b->H,
                     b->valid);
-  HIP_CHECK(c, hipEventRecord(ep[1], sbs[0]));
-  HIP_CHECK(c, hipMemcpyAsync(b->valid_host, b->valid, b->n, hipMemcpyDeviceToHost, sbs[0]));
-  HIP_CHECK(c, hipMemcpyAsync(b->nfb_host, b->n_fallback, sizeof(uint32_t), hipMemcpyDeviceToHost, sbs[0]));
-  HIP_CHECK(c, hipMemcpyAsync(b->seg_ok_host, b->seg_ok, S, hipMemcpyDeviceToHost, sbs[0]));
-  HIP_CHECK(c, hipEventRecord(b->dones[b->cur], sbs[0]));
+  HIP_CHECK(c, hipEventRecord(ep[1], sf));
+  HIP_CHECK(c, hipMemcpyAsync(b->valid_host, b->valid, b->n, hipMemcpyDeviceToHost, sf));
+  HIP_CHECK(c, hipMemcpyAsync(b->nfb_host, b->n_fallback, sizeof(uint32_t), hipMemcpyDeviceToHost, sf));
+  HIP_CHECK(c, hipMemcpyAsync(b->seg_ok_host, b->seg_ok, S, hipMemcpyDeviceToHost, sf));
+  HIP_CHECK(c, hipEventRecord(b->dones[b->cur], sf));
   HIP_CHECK(c, hipGetLastError());
   b->in_flight = true;
   return GBV_OK;

@@ -10,8 +10,6 @@ namespace gbv {
 
 struct G2Proj { Fp2 x, y, z; };
 
-struct Line { Fp2 c0, c2, c3; };
-
 // Doubling step; P given as (-xP, yP)
 GBV_HD Line dbl_step(G2Proj& T, const Fp& neg_xP, const Fp& yP) {
   Fp2 A = fp2_mul_fp(fp2_mul(T.x, T.y), FP_INV2);
@@ -59,70 +57,88 @@ GBV_HD Line add_step(G2Proj& T, const G2A& Q, const Fp& neg_xP, const Fp& yP) {
   return l;
 }
 
+// The accumulator f lives in the frame and is updated in place through the pointer-taking Fp12
+// calls (fp12.h); the two G2 points T_j stay in VGPRs.
+
 // prod_{j<2} f_{|x|, Q_j}(P_j), conjugated.  A pair whose P or Q is infinity contributes 1.
-GBV_NI Fp12 miller_loop_2(G1A P0, bool inf0, G2A Q0, G1A P1, bool inf1, G2A Q1) {
+GBV_NI void miller_loop_2_to(Fp12* out, G1A P0, bool inf0, G2A Q0, G1A P1, bool inf1, G2A Q1) {
   Fp nx0 = fp_neg(P0.x), nx1 = fp_neg(P1.x);
   G2Proj T0{Q0.x, Q0.y, fp2_one()};
   G2Proj T1{Q1.x, Q1.y, fp2_one()};
   Fp12 f = fp12_one();
+  Line l;
   for (int i = 62; i >= 0; --i) {
-    if (i != 62) f = fp12_sqr(f);
-    Line l0 = dbl_step(T0, nx0, P0.y);
-    if (!inf0) f = fp12_mul_line(f, l0.c0, l0.c2, l0.c3);
-    Line l1 = dbl_step(T1, nx1, P1.y);
-    if (!inf1) f = fp12_mul_line(f, l1.c0, l1.c2, l1.c3);
+    if (i != 62) fp12_sqr_to(&f, &f);
+    l = dbl_step(T0, nx0, P0.y);
+    if (!inf0) fp12_mul_line_to(&f, &l);
+    l = dbl_step(T1, nx1, P1.y);
+    if (!inf1) fp12_mul_line_to(&f, &l);
     if ((X_ABS >> i) & 1ull) {
-      l0 = add_step(T0, Q0, nx0, P0.y);
-      if (!inf0) f = fp12_mul_line(f, l0.c0, l0.c2, l0.c3);
-      l1 = add_step(T1, Q1, nx1, P1.y);
-      if (!inf1) f = fp12_mul_line(f, l1.c0, l1.c2, l1.c3);
+      l = add_step(T0, Q0, nx0, P0.y);
+      if (!inf0) fp12_mul_line_to(&f, &l);
+      l = add_step(T1, Q1, nx1, P1.y);
+      if (!inf1) fp12_mul_line_to(&f, &l);
     }
   }
-  return fp12_conj(f);
+  fp12_conj_to(out, &f);
 }
 
 // single pair
-GBV_NI Fp12 miller_loop_1(G1A P0, G2A Q0) {
+GBV_NI void miller_loop_1_to(Fp12* out, G1A P0, G2A Q0) {
   Fp nx0 = fp_neg(P0.x);
   G2Proj T0{Q0.x, Q0.y, fp2_one()};
   Fp12 f = fp12_one();
+  Line l;
   for (int i = 62; i >= 0; --i) {
-    if (i != 62) f = fp12_sqr(f);
-    Line l0 = dbl_step(T0, nx0, P0.y);
-    f = fp12_mul_line(f, l0.c0, l0.c2, l0.c3);
+    if (i != 62) fp12_sqr_to(&f, &f);
+    l = dbl_step(T0, nx0, P0.y);
+    fp12_mul_line_to(&f, &l);
     if ((X_ABS >> i) & 1ull) {
-      l0 = add_step(T0, Q0, nx0, P0.y);
-      f = fp12_mul_line(f, l0.c0, l0.c2, l0.c3);
+      l = add_step(T0, Q0, nx0, P0.y);
+      fp12_mul_line_to(&f, &l);
     }
   }
-  return fp12_conj(f);
+  fp12_conj_to(out, &f);
 }
 
 // single pair with P in Jacobian coordinates (X : Y : Z), Z != 0: every line is the affine line
 // times Z^3 (c0 * Z^3, c2 from -X Z, c3 from Y), an Fp factor the final exponentiation removes,
 // so no inversion is needed to get P affine.
-GBV_NI Fp12 miller_loop_1j(G1J P, G2A Q0) {
+GBV_NI void miller_loop_1j_to(Fp12* out, G1J P, G2A Q0) {
   Fp z2 = fp_sqr(P.z);
   Fp z3 = fp_mul(z2, P.z);
   Fp nxz = fp_neg(fp_mul(P.x, P.z));
   G2Proj T0{Q0.x, Q0.y, fp2_one()};
   Fp12 f = fp12_one();
+  Line l;
   for (int i = 62; i >= 0; --i) {
-    if (i != 62) f = fp12_sqr(f);
-    Line l0 = dbl_step(T0, nxz, P.y);
-    f = fp12_mul_line(f, fp2_mul_fp(l0.c0, z3), l0.c2, l0.c3);
+    if (i != 62) fp12_sqr_to(&f, &f);
+    l = dbl_step(T0, nxz, P.y);
+    l.c0 = fp2_mul_fp(l.c0, z3);
+    fp12_mul_line_to(&f, &l);
     if ((X_ABS >> i) & 1ull) {
-      l0 = add_step(T0, Q0, nxz, P.y);
-      f = fp12_mul_line(f, fp2_mul_fp(l0.c0, z3), l0.c2, l0.c3);
+      l = add_step(T0, Q0, nxz, P.y);
+      l.c0 = fp2_mul_fp(l.c0, z3);
+      fp12_mul_line_to(&f, &l);
     }
   }
-  return fp12_conj(f);
+  fp12_conj_to(out, &f);
 }
+
+GBV_HD Fp12 miller_loop_2(const G1A& P0, bool inf0, const G2A& Q0, const G1A& P1, bool inf1, const G2A& Q1) {
+  Fp12 r;
+  miller_loop_2_to(&r, P0, inf0, Q0, P1, inf1, Q1);
+  return r;
+}
+GBV_HD Fp12 miller_loop_1(const G1A& P0, const G2A& Q0) { Fp12 r; miller_loop_1_to(&r, P0, Q0); return r; }
+GBV_HD Fp12 miller_loop_1j(const G1J& P, const G2A& Q0) { Fp12 r; miller_loop_1j_to(&r, P, Q0); return r; }
 
 // e(P0, Q0) * e(P1, Q1) == 1 ?
 GBV_HD bool pairing_check_2(const G1A& P0, bool inf0, const G2A& Q0, const G1A& P1, bool inf1, const G2A& Q1) {
-  Fp12 f = miller_loop_2(P0, inf0, Q0, P1, inf1, Q1);
-  return fp12_is_one(final_exponentiation(f));
+  Fp12 f;
+  miller_loop_2_to(&f, P0, inf0, Q0, P1, inf1, Q1);
+  final_exponentiation_to(&f, &f);
+  return fp12_is_one(f);
 }
 
 GBV_HD G1A g1_neg_generator() { return G1A{G1_GEN_X, G1_GEN_NEG_Y}; }
