@@ -608,13 +608,10 @@ int gbv_sm_batch_submit(gbv_ctx* c, gbv_sm_batch* b) {
   Seed seed = fresh_seed();
   uint32_t nonce = c->nonce++;
   // Same-message batches: hash on stream 4, tail on stream 2, every batch.  Alternating the tails
-  // of consecutive batches over two streams stalls the device for 0.1-8 s at a time at
-  // GPU_MAX_HW_QUEUES=4 (HIP's default and the box's) and never at 8 -- with four streams
-  // (round 1's GBV_FLIP: 3.37 M sets/s vs 17.37 M at 8 queues, profiles/r02_flip_*) and with three
-  // (hash and tail of a batch on the same alternating stream, GBV_ALT_TAIL=1: 1.14 M sets/s,
-  // profiles/r02s_alt_tail_hash_bench_STALL.json): the streams' cross-stream waits meet in shared
-  // hardware queues.  One tail stream leaves consecutive tails serialised, which costs nothing
-  // while the tail is shorter than k_sm_prepare (all-valid streams).
+  // of consecutive batches over two streams (GBV_ALT_TAIL=1, diagnosis) used to stall the device
+  // for 0.1-8 s at a time while the failure-path kernels needed 27-28 KB of scratch per lane and
+  // were dispatched from two hardware queues; with the pointer-based Fp12 layer (<= 8.7 KB) it runs
+  // clean, but buys nothing while the tail is shorter than k_sm_prepare.
   static const bool alt_tail = getenv("GBV_ALT_TAIL") != nullptr;  // diagnosis only
   const bool flip = alt_tail && (c->sm_submits++ & 1) != 0;
   // Invalid-dense regime (a segment failed within the last MSM_COOLDOWN submits, e.g. C5's 1 %
