@@ -66,18 +66,20 @@ template <class F> GBV_HD Jac<F> jac_sel(bool c, const Jac<F>& a, const Jac<F>& 
 template <class F> GBV_HD Jac<F> jac_neg(const Jac<F>& p) { return Jac<F>{p.x, f_neg(p.y), p.z}; }
 
 // dbl-2009-l, 2M + 5S.  Complete for a = 0 (2-torsion and infinity give z3 = 0).
+// Z3 first so that Z dies early: over Fp2 the live set then stays at five elements (120 VGPRs)
+// plus one product's operands, inside the registers an out-of-line Fp product leaves untouched.
 template <class F> GBV_HD Jac<F> jac_dbl(const Jac<F>& p) {
-  F A = f_sqr(p.x);
+  Jac<F> r;
+  r.z = f_dbl(f_mul(p.y, p.z));
   F B = f_sqr(p.y);
+  F A = f_sqr(p.x);
   F C = f_sqr(B);
   F D = f_dbl(f_sub(f_sub(f_sqr(f_add(p.x, B)), A), C));
   F E = f_add(f_dbl(A), A);
   F Fv = f_sqr(E);
-  Jac<F> r;
   r.x = f_sub(Fv, f_dbl(D));
   F C8 = f_dbl(f_dbl(f_dbl(C)));
   r.y = f_sub(f_mul(E, f_sub(D, r.x)), C8);
-  r.z = f_dbl(f_mul(p.y, p.z));
   return r;
 }
 
@@ -191,13 +193,23 @@ template <class F> GBV_HD Jac<F> jac_mul_xabs_jac(const Jac<F>& q) {
   return r;
 }
 
+// An out-of-line function that returns a named aggregate builds it in the caller's return slot
+// (NRVO), i.e. in memory: the loop-carried point of a scalar multiplication was stored in full
+// after every step (288 B per G2 doubling -- ~18 KB of the ~22 KB/set of scratch writes of
+// k_sm_prepare went to the 63 doublings of the G2 subgroup check).  ret_copy() keeps the loop
+// variable an ordinary (register) local and writes the return slot once.
+template <class T> GBV_HD T ret_copy(const T& v) {
+  T out = v;
+  return out;
+}
+
 // Out-of-line scalar multiplications (coarse: the point crosses the call once).
-GBV_NI G1J g1_mul_u64(G1A q, uint64_t k) { return jac_mul_u64(q, k); }
-GBV_NI G2J g2_mul_u64(G2A q, uint64_t k) { return jac_mul_u64(q, k); }
-GBV_NI G2J g2_mul_xabs(G2A q) { return jac_mul_xabs(q); }
-GBV_NI G2J g2_mul_xabs_jac(G2J q) { return jac_mul_xabs_jac(q); }
-GBV_NI G1J g1_mul_u256(G1A q, const uint32_t* k) { return jac_mul_u256(q, k); }
-GBV_NI G2J g2_mul_u256(G2A q, const uint32_t* k) { return jac_mul_u256(q, k); }
+GBV_NI G1J g1_mul_u64(G1A q, uint64_t k) { G1J r = jac_mul_u64(q, k); return ret_copy(r); }
+GBV_NI G2J g2_mul_u64(G2A q, uint64_t k) { G2J r = jac_mul_u64(q, k); return ret_copy(r); }
+GBV_NI G2J g2_mul_xabs(G2A q) { G2J r = jac_mul_xabs(q); return ret_copy(r); }
+GBV_NI G2J g2_mul_xabs_jac(G2J q) { G2J r = jac_mul_xabs_jac(q); return ret_copy(r); }
+GBV_NI G1J g1_mul_u256(G1A q, const uint32_t* k) { G1J r = jac_mul_u256(q, k); return ret_copy(r); }
+GBV_NI G2J g2_mul_u256(G2A q, const uint32_t* k) { G2J r = jac_mul_u256(q, k); return ret_copy(r); }
 
 // ---- curve constants & decoding -------------------------------------------------------------
 enum : uint8_t {
@@ -535,7 +547,8 @@ GBV_HD G1A comb_pick(const uint4* tab, uint32_t sa, uint32_t sb, int i) {
 // keeps every load and its use inside one straight-line body.
 GBV_NI G1J comb_step(G1J R, const uint4* tab, uint32_t sa, uint32_t sb, int c) {
   const G1A t = comb_pick(tab, sa, sb, c);
-  return jac_add_aff(jac_dbl(R), t);
+  G1J r = jac_add_aff(jac_dbl(R), t);
+  return ret_copy(r);
 }
 
 // [r] P from P's comb table (r = a - b x^2 of the digit word, exactly randomize_g1's scalar)

@@ -97,7 +97,7 @@ GBV_NI G2A map_to_curve_sswu(Fp2 u) {
   Fp2 y;
   fp2_sqrt_with_norm_root(y, fp2_sel(sq1, gx1, gx2), fp_sel(sq1, a1, a2));
   if (fp2_sgn0(u) != fp2_sgn0(y)) y = fp2_neg(y);
-  return G2A{x, y};
+  return ret_copy(G2A{x, y});
 }
 
 // 3-isogeny E2' -> E2 (RFC 9380 E.3), output in Jacobian coordinates (no inversion):
@@ -114,7 +114,7 @@ GBV_NI G2J iso_map(G2A p) {
   r.z = fp2_mul(xd, yd);
   r.x = fp2_mul(fp2_mul(xn, xd), yd2);
   r.y = fp2_mul(fp2_mul(fp2_mul(p.y, yn), fp2_mul(xd2, xd)), yd2);
-  return r;
+  return ret_copy(r);
 }
 
 // RFC 9380 G.3 clear_cofactor: h_eff P = [x^2-x-1]P + [x-1]psi(P) + psi^2(2P)
@@ -127,7 +127,8 @@ GBV_NI G2J clear_cofactor_g2(G2J p) {
   t2 = jac_neg(g2_mul_xabs_jac(t2));             // [x] t2
   t3 = jac_add(t3, t2);
   t3 = jac_add(t3, jac_neg(t1));
-  return jac_add(t3, jac_neg(p));
+  G2J r = jac_add(t3, jac_neg(p));
+  return ret_copy(r);
 }
 
 // hash_to_field: u_j = expand_message_xmd(msg)[64 j .. 64 j + 64) as Fp2 (j = 0, 1)
@@ -145,7 +146,7 @@ GBV_NI G2A hash_finish(G2J q0, G2J q1) {
   G2J q = clear_cofactor_g2(jac_add(q0, q1));
   G2A out;
   jac_to_aff(out, q);
-  return out;
+  return ret_copy(out);
 }
 
 // hash_to_G2(msg32) as an affine point (Montgomery).  msg given as 8 big-endian words.
