@@ -545,22 +545,24 @@ GBV_HD G1A comb_pick(const uint4* tab, uint32_t sa, uint32_t sb, int i) {
 // next column's table loads across the loop back-edge and miscompiles the loop-carried 12-limb
 // values (tests/test_gpu_scale.py::test_comb_tables_match_ladder caught it); a call per column
 // keeps every load and its use inside one straight-line body.
-GBV_NI G1J comb_step(G1J R, const uint4* tab, uint32_t sa, uint32_t sb, int c) {
+// The running point stays in comb_mul's frame and each column updates it in place (one 192-byte
+// store per column; by value it was an argument copy plus a returned copy).
+GBV_NI void comb_step_to(G1J* R, const uint4* tab, uint32_t sa, uint32_t sb, int c) {
   const G1A t = comb_pick(tab, sa, sb, c);
-  G1J r = jac_add_aff(jac_dbl(R), t);
-  return ret_copy(r);
+  *R = jac_add_aff(jac_dbl(*R), t);
 }
 
 // [r] P from P's comb table (r = a - b x^2 of the digit word, exactly randomize_g1's scalar)
 GBV_NI G1J comb_mul(const uint4* tab, uint32_t sa, uint32_t sb) {
   G1J R = jac_from_aff(comb_pick(tab, sa, sb, 7));
-  R = comb_step(R, tab, sa, sb, 6);
-  R = comb_step(R, tab, sa, sb, 5);
-  R = comb_step(R, tab, sa, sb, 4);
-  R = comb_step(R, tab, sa, sb, 3);
-  R = comb_step(R, tab, sa, sb, 2);
-  R = comb_step(R, tab, sa, sb, 1);
-  return comb_step(R, tab, sa, sb, 0);
+  comb_step_to(&R, tab, sa, sb, 6);
+  comb_step_to(&R, tab, sa, sb, 5);
+  comb_step_to(&R, tab, sa, sb, 4);
+  comb_step_to(&R, tab, sa, sb, 3);
+  comb_step_to(&R, tab, sa, sb, 2);
+  comb_step_to(&R, tab, sa, sb, 1);
+  comb_step_to(&R, tab, sa, sb, 0);
+  return ret_copy(R);
 }
 
 // The comb bases B[0..7] (affine) and D = 2 P, with one shared inversion.  P affine, in G1.

@@ -82,7 +82,7 @@ __global__ void GBV_KERNEL_ATTR k_sm_prepare(uint32_t base, uint32_t n, const ui
       G2J so = shfl_down_jac(rs, d);
       if (take) rs = g2_add(rs, so);
     }
-    if (take) rp = g1_add(rp, po);
+    if (take) rp = jac_add(rp, po);  // inline: an out-of-line G1 addition copies both points through scratch
   }
   uint32_t kprev = __shfl_up(key, 1, 64);
   if (act && ((lane & (SCAN_W - 1)) == 0 || kprev != key)) {
