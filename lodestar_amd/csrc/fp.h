@@ -230,11 +230,6 @@ template <int N> GBV_HD void mac_run(uint64_t& acc, uint32_t& top, const uint32_
 // a*b and of m*p accumulate into one 96-bit accumulator, m_k is derived from the column's low
 // word.  2 VALU instructions per limb product (288 products), no carry propagation passes.
 // Inputs < p, output < p.
-#if defined(GBV_HOST_TEST)
-// Host build only (tests/native/hosttest.cpp): every Fp product is counted, so the algorithmic work
-// per signature set that bench.py's roofline uses is measured on the code, not estimated.
-inline unsigned long long g_fme_count = 0;
-#endif
 // column K < 12: a_0 b_K (starts the carry word), a_i b_{K-i} (i = 1..K), m_i p_{K-i} (i < K),
 // then m_K from the low word and m_K p_0; the accumulator shifts down one word
 template <int K> GBV_HD void fips_col_lo(uint64_t& acc, uint32_t& top, const Fp& a, const Fp& b, uint32_t (&m)[12]) {
@@ -265,47 +260,87 @@ template <int K> GBV_HD void fips_col_hi(uint64_t& acc, uint32_t& top, const Fp&
   r[K - 12] = (uint32_t)acc;
   acc = (acc >> 32) | ((uint64_t)top << 32);
 }
-GBV_HD Fp fp_mul_inl(const Fp& a, const Fp& b) {
+// ---- the product: 14 x 28-bit limbs, Montgomery radix R = 2^392 ---------------------------------
+// An element is stored as 12 x 32-bit limbs (adds, subtracts and comparisons use the hardware carry
+// chain), but multiplied as 14 limbs of 28 bits: a column of up to 14 a_i b_j and 14 m_i p_j
+// products of 56 bits sums below 2^61, so each limb product is ONE v_mad_u64_u32 into a plain
+// 64-bit accumulator -- no carry word, no carry instruction -- where the 32-bit FIPS form needs a
+// v_addc per product to catch the 96-bit column's carry.  Counted on the gfx950 code: 479
+// instructions per product against 673 (288 mad + 288 addc + 97) for 32-bit limbs.
+// The output of mul28_inl is < 2p for inputs < 2p (4p^2 < R p); fp_mul_inl reduces it once.
+typedef uint32_t u32x14 __attribute__((ext_vector_type(14)));
+struct F28 { u32x14 v; };
+constexpr uint32_t M28 = 0xFFFFFFFu;
+
+GBV_HD F28 fp_to28(const Fp& a) {  // the same integer in 28-bit limbs
+  F28 r;
+#pragma unroll
+  for (int j = 0; j < 14; ++j) {
+    const int w = (28 * j) >> 5, o = (28 * j) & 31;
+    uint32_t v = a.v[w] >> o;
+    if (o > 4 && w + 1 < 12) v |= a.v[w + 1] << (32 - o);
+    r.v[j] = v & M28;
+  }
+  return r;
+}
+
+GBV_HD Fp fp_from28(const F28& z) {  // z < 2^384, limbs < 2^28
+  Fp r;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    const int j = (32 * i) / 28, o = (32 * i) % 28;
+    uint32_t v = z.v[j] >> o;
+    if (j + 1 < 14) v |= z.v[j + 1] << (28 - o);
+    if (j + 2 < 14 && 56 - o < 32) v |= z.v[j + 2] << (56 - o);
+    r.v[i] = v;
+  }
+  return r;
+}
+
+#if defined(GBV_HOST_TEST)
+// Host build only (tests/native/hosttest.cpp): every Fp product is counted, so the algorithmic work
+// per signature set that bench.py's roofline uses is measured on the code, not estimated.
+inline unsigned long long g_fme_count = 0;
+#endif
+
+// a b 2^-392 mod p (< 2p) by product scanning: column k of a*b and of m*p in one 64-bit
+// accumulator, m_k from the column's low 28 bits for k < 14, output limb k-14 for k >= 14.
+GBV_HD F28 mul28_inl(const F28& a, const F28& b) {
 #if defined(GBV_HOST_TEST)
   ++g_fme_count;
 #endif
-  uint32_t m[12], r[12];
+  uint32_t m[14], r[14];
   uint64_t acc = 0;
-  uint32_t top = 0;
-#if defined(__HIP_DEVICE_COMPILE__)
-  // device: each column's MACs are ONE generated asm block (fp_asm.h GBV_ASM_FIPS_COL*)
-#define GBV_COL_LO(K)                              \
-  GBV_ASM_FIPS_COL##K(acc, top, a, b, m);          \
-  m[K] = (uint32_t)acc * NP0;                      \
-  mac96_k(acc, top, m[K], P_RAW.v[0]);             \
-  acc = (acc >> 32) | ((uint64_t)top << 32);
-#define GBV_COL_HI(K)                              \
-  GBV_ASM_FIPS_COL##K(acc, top, a, b, m);          \
-  r[K - 12] = (uint32_t)acc;                       \
-  acc = (acc >> 32) | ((uint64_t)top << 32);
-  GBV_COL_LO(0) GBV_COL_LO(1) GBV_COL_LO(2) GBV_COL_LO(3) GBV_COL_LO(4) GBV_COL_LO(5)
-  GBV_COL_LO(6) GBV_COL_LO(7) GBV_COL_LO(8) GBV_COL_LO(9) GBV_COL_LO(10) GBV_COL_LO(11)
-  GBV_COL_HI(12) GBV_COL_HI(13) GBV_COL_HI(14) GBV_COL_HI(15) GBV_COL_HI(16) GBV_COL_HI(17)
-  GBV_COL_HI(18) GBV_COL_HI(19) GBV_COL_HI(20) GBV_COL_HI(21) GBV_COL_HI(22)
-#undef GBV_COL_LO
-#undef GBV_COL_HI
-#else
-  fips_col_lo<0>(acc, top, a, b, m), fips_col_lo<1>(acc, top, a, b, m), fips_col_lo<2>(acc, top, a, b, m);
-  fips_col_lo<3>(acc, top, a, b, m), fips_col_lo<4>(acc, top, a, b, m), fips_col_lo<5>(acc, top, a, b, m);
-  fips_col_lo<6>(acc, top, a, b, m), fips_col_lo<7>(acc, top, a, b, m), fips_col_lo<8>(acc, top, a, b, m);
-  fips_col_lo<9>(acc, top, a, b, m), fips_col_lo<10>(acc, top, a, b, m), fips_col_lo<11>(acc, top, a, b, m);
-  fips_col_hi<12>(acc, top, a, b, m, r), fips_col_hi<13>(acc, top, a, b, m, r), fips_col_hi<14>(acc, top, a, b, m, r);
-  fips_col_hi<15>(acc, top, a, b, m, r), fips_col_hi<16>(acc, top, a, b, m, r), fips_col_hi<17>(acc, top, a, b, m, r);
-  fips_col_hi<18>(acc, top, a, b, m, r), fips_col_hi<19>(acc, top, a, b, m, r), fips_col_hi<20>(acc, top, a, b, m, r);
-  fips_col_hi<21>(acc, top, a, b, m, r), fips_col_hi<22>(acc, top, a, b, m, r);
-#endif
-  r[11] = (uint32_t)acc;
-  Fp o;
 #pragma unroll
-  for (int i = 0; i < 12; ++i) o.v[i] = r[i];
-  return fp_reduce_once(o);
+  for (int k = 0; k < 27; ++k) {
+#pragma unroll
+    for (int i = 0; i < 14; ++i) {
+      const int j = k - i;
+      if (j >= 0 && j < 14) acc += (uint64_t)a.v[i] * b.v[j];
+    }
+#pragma unroll
+    for (int i = 0; i < 14; ++i) {
+      const int j = k - i;
+      if (i < k && j >= 0 && j < 14) acc += (uint64_t)m[i] * P28[j];
+    }
+    if (k < 14) {
+      m[k] = ((uint32_t)acc * NP28) & M28;
+      acc += (uint64_t)m[k] * P28[0];
+      acc >>= 28;
+    } else {
+      r[k - 14] = (uint32_t)acc & M28;
+      acc >>= 28;
+    }
+  }
+  r[13] = (uint32_t)acc;
+  F28 o;
+#pragma unroll
+  for (int i = 0; i < 14; ++i) o.v[i] = r[i];
+  return o;
 }
 
+// Montgomery product a b R^-1 mod p, R = 2^392.  Inputs < p, output < p.
+GBV_HD Fp fp_mul_inl(const Fp& a, const Fp& b) { return fp_reduce_once(fp_from28(mul28_inl(fp_to28(a), fp_to28(b)))); }
 GBV_HD Fp fp_sqr_inl(const Fp& a) { return fp_mul_inl(a, a); }
 
 // Out-of-line versions: keep the hot loops of the big kernels inside the instruction cache.
@@ -320,38 +355,49 @@ GBV_HD Fp fp_from_mont(const Fp& a) {
   return fp_mul(a, one);
 }
 
+// Exponentiations stay in the 28-bit limb form from the first product to the last: every step is
+// a bare mul28 (479 instructions, no repacking, no final reduction -- the values stay < 2p).
+GBV_NI F28 mul28(F28 a, F28 b) { return mul28_inl(a, b); }
+GBV_HD F28 f28_sel(bool c, const F28& a, const F28& b) {
+  F28 r;
+#pragma unroll
+  for (int i = 0; i < 14; ++i) r.v[i] = c ? a.v[i] : b.v[i];
+  return r;
+}
+
 // a^e for a fixed public exponent (12 little-endian words, top bit index nbits-1).
 // Square-and-multiply; the branch is on the public exponent so all lanes agree.
 GBV_NI Fp fp_pow(Fp a, const uint32_t* e, int nbits) {
-  Fp r = a;
+  const F28 x = fp_to28(a);
+  F28 r = x;
   for (int i = nbits - 2; i >= 0; --i) {
-    r = fp_sqr(r);
-    if ((e[i >> 5] >> (i & 31)) & 1) r = fp_mul(r, a);
+    r = mul28(r, r);
+    if ((e[i >> 5] >> (i & 31)) & 1) r = mul28(r, x);
   }
-  return r;
+  return fp_reduce_once(fp_from28(r));
 }
 
 // a^e for a fixed public exponent given as a sliding-window schedule (tools/gen_constants.py
 // c_sched): table of odd powers a^1..a^15, ~76 multiplications for a 379-bit exponent instead of
 // ~228 by square-and-multiply.  The table index is wave-uniform; picked with selects.
 GBV_NI Fp fp_pow_sched(Fp a, const uint8_t* nsq, const uint8_t* idx, int steps) {
-  Fp t[8];
-  t[0] = a;
-  Fp a2 = fp_sqr(a);
+  F28 t[8];
+  t[0] = fp_to28(a);
+  const F28 a2 = mul28(t[0], t[0]);
 #pragma unroll
-  for (int j = 1; j < 8; ++j) t[j] = fp_mul(t[j - 1], a2);
+  for (int j = 1; j < 8; ++j) t[j] = mul28(t[j - 1], a2);
   auto pick = [&](uint32_t k) {
-    Fp s = t[0];
+    F28 s = t[0];
 #pragma unroll
-    for (int j = 1; j < 8; ++j) s = fp_sel(k == (uint32_t)j, t[j], s);
+    for (int j = 1; j < 8; ++j) s = f28_sel(k == (uint32_t)j, t[j], s);
     return s;
   };
-  Fp r = pick(idx[0]);
+  F28 r = pick(idx[0]);
   for (int s = 1; s < steps; ++s) {
-    for (int q = 0; q < nsq[s]; ++q) r = fp_sqr(r);
-    if (idx[s] != 255) r = fp_mul(r, pick(idx[s]));
+    for (int q = 0; q < nsq[s]; ++q) r = mul28(r, r);
+    if (idx[s] != 255) r = mul28(r, pick(idx[s]));
   }
-  return r;
+  return fp_reduce_once(fp_from28(r));
 }
 
 GBV_HD Fp fp_inv_pow(const Fp& a) { return fp_pow(a, EXP_INV, EXP_INV_BITS); }  // 0 -> 0

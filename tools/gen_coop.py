@@ -443,7 +443,7 @@ def encode(b):
 
 
 def mont(v):
-    return v * (1 << 384) % P
+    return v * (1 << 392) % P  # Montgomery radix R = 2^392 (fp.h)
 
 
 def limbs(v):
