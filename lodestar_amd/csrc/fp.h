@@ -123,143 +123,6 @@ GBV_HD Fp fp_neg(const Fp& a) {
 
 GBV_HD Fp fp_dbl(const Fp& a) { return fp_add(a, a); }
 
-// One multiply-accumulate into a 96-bit column accumulator {acc (64), top (32)}:
-//   acc += a * b  (v_mad_u64_u32 with carry-out in VCC),  top += carry  (v_addc_co_u32).
-// mac96_first starts a column (top = carry: no separate zeroing move); mac96_k takes the constant
-// operand (a limb of p) from an SGPR, so the 144 reduction products need no VGPR copies of p.
-GBV_HD void mac96(uint64_t& acc, uint32_t& top, uint32_t a, uint32_t b) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  asm("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\tv_addc_co_u32 %1, vcc, 0, %1, vcc"
-      : "+v"(acc), "+v"(top)
-      : "v"(a), "v"(b)
-      : "vcc");
-#else  // host build used only by tests/native/hosttest.cpp
-  uint64_t p = (uint64_t)a * b;
-  uint64_t s = acc + p;
-  top += (s < acc) ? 1u : 0u;
-  acc = s;
-#endif
-}
-GBV_HD void mac96_first(uint64_t& acc, uint32_t& top, uint32_t a, uint32_t b) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  asm("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\tv_addc_co_u32_e64 %1, vcc, 0, 0, vcc"
-      : "+v"(acc), "=v"(top)
-      : "v"(a), "v"(b)
-      : "vcc");
-#else
-  top = 0;
-  mac96(acc, top, a, b);
-#endif
-}
-GBV_HD void mac96_k(uint64_t& acc, uint32_t& top, uint32_t a, uint32_t k) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  asm("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\tv_addc_co_u32 %1, vcc, 0, %1, vcc"
-      : "+v"(acc), "+v"(top)
-      : "v"(a), "s"(k)
-      : "vcc");
-#else
-  mac96(acc, top, a, k);
-#endif
-}
-GBV_HD void mac96_k_first(uint64_t& acc, uint32_t& top, uint32_t a, uint32_t k) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  asm("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\tv_addc_co_u32_e64 %1, vcc, 0, 0, vcc"
-      : "+v"(acc), "=v"(top)
-      : "v"(a), "s"(k)
-      : "vcc");
-#else
-  top = 0;
-  mac96(acc, top, a, k);
-#endif
-}
-
-// Several MACs of one column in ONE inline-asm block.  The compiler pads every boundary between
-// asm blocks with s_nop (it cannot see that the blocks hold no transcendental op whose result
-// needs a wait state), so fewer, longer blocks issue faster: 4 MACs per block measured +9 % Fp
-// products/s at 2 waves per SIMD, +24 % at 1 wave (profiles/ubench/r02_ubench_fp_mac_blocks.txt).
-#if defined(__HIP_DEVICE_COMPILE__)
-#define GBV_MAC_ASM(a, b) "v_mad_u64_u32 %0, vcc, " a ", " b ", %0\n\tv_addc_co_u32 %1, vcc, 0, %1, vcc\n\t"
-#endif
-GBV_HD void mac96x2(uint64_t& acc, uint32_t& top, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  asm(GBV_MAC_ASM("%2", "%3") GBV_MAC_ASM("%4", "%5") : "+v"(acc), "+v"(top) : "v"(a), "v"(b), "v"(c), "v"(d) : "vcc");
-#else
-  mac96(acc, top, a, b);
-  mac96(acc, top, c, d);
-#endif
-}
-GBV_HD void mac96x4(uint64_t& acc, uint32_t& top, const uint32_t* x, const uint32_t* y) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  asm(GBV_MAC_ASM("%2", "%3") GBV_MAC_ASM("%4", "%5") GBV_MAC_ASM("%6", "%7") GBV_MAC_ASM("%8", "%9")
-      : "+v"(acc), "+v"(top)
-      : "v"(x[0]), "v"(y[0]), "v"(x[1]), "v"(y[1]), "v"(x[2]), "v"(y[2]), "v"(x[3]), "v"(y[3])
-      : "vcc");
-#else
-  for (int i = 0; i < 4; ++i) mac96(acc, top, x[i], y[i]);
-#endif
-}
-GBV_HD void mac96x8(uint64_t& acc, uint32_t& top, const uint32_t* x, const uint32_t* y) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  asm(GBV_MAC_ASM("%2", "%3") GBV_MAC_ASM("%4", "%5") GBV_MAC_ASM("%6", "%7") GBV_MAC_ASM("%8", "%9")
-      GBV_MAC_ASM("%10", "%11") GBV_MAC_ASM("%12", "%13") GBV_MAC_ASM("%14", "%15") GBV_MAC_ASM("%16", "%17")
-      : "+v"(acc), "+v"(top)
-      : "v"(x[0]), "v"(y[0]), "v"(x[1]), "v"(y[1]), "v"(x[2]), "v"(y[2]), "v"(x[3]), "v"(y[3]),
-        "v"(x[4]), "v"(y[4]), "v"(x[5]), "v"(y[5]), "v"(x[6]), "v"(y[6]), "v"(x[7]), "v"(y[7])
-      : "vcc");
-#else
-  for (int i = 0; i < 8; ++i) mac96(acc, top, x[i], y[i]);
-#endif
-}
-// the N MACs x[i] * y[i] of a column, in blocks of 8, 4, 2, 1
-template <int N> GBV_HD void mac_run(uint64_t& acc, uint32_t& top, const uint32_t* x, const uint32_t* y) {
-  int j = 0;
-#pragma unroll
-  for (; j + 7 < N; j += 8) mac96x8(acc, top, x + j, y + j);
-  if (j + 3 < N) {
-    mac96x4(acc, top, x + j, y + j);
-    j += 4;
-  }
-  if (j + 1 < N) {
-    mac96x2(acc, top, x[j], y[j], x[j + 1], y[j + 1]);
-    j += 2;
-  }
-  if (j < N) mac96(acc, top, x[j], y[j]);
-}
-
-// Montgomery product a*b*2^-384 mod p by finely integrated product scanning (FIPS): column k of
-// a*b and of m*p accumulate into one 96-bit accumulator, m_k is derived from the column's low
-// word.  2 VALU instructions per limb product (288 products), no carry propagation passes.
-// Inputs < p, output < p.
-// column K < 12: a_0 b_K (starts the carry word), a_i b_{K-i} (i = 1..K), m_i p_{K-i} (i < K),
-// then m_K from the low word and m_K p_0; the accumulator shifts down one word
-template <int K> GBV_HD void fips_col_lo(uint64_t& acc, uint32_t& top, const Fp& a, const Fp& b, uint32_t (&m)[12]) {
-  mac96_first(acc, top, a.v[0], b.v[K]);
-  if (K > 0) {
-    uint32_t x[2 * K + 1], y[2 * K + 1];
-#pragma unroll
-    for (int i = 1; i <= K; ++i) x[i - 1] = a.v[i], y[i - 1] = b.v[K - i];
-#pragma unroll
-    for (int i = 0; i < K; ++i) x[K + i] = m[i], y[K + i] = P_RAW.v[K - i];
-    mac_run<2 * K>(acc, top, x, y);
-  }
-  m[K] = (uint32_t)acc * NP0;
-  mac96_k(acc, top, m[K], P_RAW.v[0]);
-  acc = (acc >> 32) | ((uint64_t)top << 32);
-}
-// column K >= 12: a_i b_{K-i} and m_i p_{K-i} for i = K-11 .. 11; its low word is result limb K-12
-template <int K> GBV_HD void fips_col_hi(uint64_t& acc, uint32_t& top, const Fp& a, const Fp& b, const uint32_t (&m)[12], uint32_t (&r)[12]) {
-  mac96_first(acc, top, a.v[K - 11], b.v[11]);
-  uint32_t x[2 * (23 - K)], y[2 * (23 - K)];
-  x[0] = m[K - 11], y[0] = P_RAW.v[11];
-#pragma unroll
-  for (int i = K - 10, n = 1; i < 12; ++i) {
-    x[n] = a.v[i], y[n++] = b.v[K - i];
-    x[n] = m[i], y[n++] = P_RAW.v[K - i];
-  }
-  mac_run<1 + 2 * (22 - K)>(acc, top, x, y);
-  r[K - 12] = (uint32_t)acc;
-  acc = (acc >> 32) | ((uint64_t)top << 32);
-}
 // ---- the product: 14 x 28-bit limbs, Montgomery radix R = 2^392 ---------------------------------
 // An element is stored as 12 x 32-bit limbs (adds, subtracts and comparisons use the hardware carry
 // chain), but multiplied as 14 limbs of 28 bits: a column of up to 14 a_i b_j and 14 m_i p_j
@@ -268,6 +131,7 @@ template <int K> GBV_HD void fips_col_hi(uint64_t& acc, uint32_t& top, const Fp&
 // v_addc per product to catch the 96-bit column's carry.  Counted on the gfx950 code: 479
 // instructions per product against 673 (288 mad + 288 addc + 97) for 32-bit limbs.
 // The output of mul28_inl is < 2p for inputs < 2p (4p^2 < R p); fp_mul_inl reduces it once.
+// (Splitting a column into two accumulation chains measured no faster at 2 waves/SIMD.)
 typedef uint32_t u32x14 __attribute__((ext_vector_type(14)));
 struct F28 { u32x14 v; };
 constexpr uint32_t M28 = 0xFFFFFFFu;
