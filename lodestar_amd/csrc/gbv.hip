@@ -1047,6 +1047,11 @@ int gbv_util_sign(gbv_ctx* c, const uint8_t* sk32, size_t n, const uint32_t* grp
 }  // extern "C"
 
 namespace gbv {
+uint32_t hash_pair_max() {
+  static const uint32_t v = getenv("GBV_HASH_PAIR_MAX") ? (uint32_t)atoi(getenv("GBV_HASH_PAIR_MAX")) : HASH_PAIR_MAX;
+  return v;
+}
+
 void debug_sync(hipStream_t s, const char* kernel) {
   static int on = getenv("GBV_SYNC_DEBUG") ? atoi(getenv("GBV_SYNC_DEBUG")) : 0;
   if (!on) return;

@@ -35,7 +35,7 @@ __global__ void GBV_KERNEL_ATTR k_util_g2_out(uint32_t n, const G2A* __restrict_
 
 
 void launch_hash_msgs(LaunchCfg c, const uint8_t* msgs32, uint32_t n, G2A* H) {
-  if (n <= HASH_PAIR_MAX)  // latency: lane pairs (grid sized here; c.blocks is for one lane per message)
+  if (n <= hash_pair_max())  // latency: lane pairs (grid sized here; c.blocks is for one lane per message)
     hipLaunchKernelGGL(k_hash_msgs_pair, dim3((2 * n + 63) / 64), dim3(64), 0, c.stream, msgs32, n, H);
   else
     hipLaunchKernelGGL(k_hash_msgs, dim3(c.blocks), dim3(c.threads), 0, c.stream, msgs32, n, H);

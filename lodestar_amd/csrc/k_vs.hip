@@ -218,7 +218,7 @@ void launch_vs_hash_sig(hipStream_t s, uint32_t n, const uint8_t* msgs32, const 
                         const uint8_t* raw_flag, const uint8_t* raw_pk48, const uint8_t* sig, uint32_t sig_stride, const uint32_t* sig_len,
                         const G1A* table, const uint8_t* table_ok, const G1J* pk_agg, const uint8_t* pk_st, const Seed& seed,
                         uint32_t nonce, G2A* H, G1J* rP, G2J* rS, uint8_t* status) {
-  const uint32_t pair = n <= HASH_PAIR_MAX ? 1u : 0u;
+  const uint32_t pair = n <= hash_pair_max() ? 1u : 0u;
   const uint32_t nb = pair ? (2 * n + 63) / 64 : (n + 63) / 64, nsig = (n + 63) / 64;
   hipLaunchKernelGGL(k_vs_hash_sig, dim3(nb + nsig), dim3(64), 0, s, n, nb, pair, msgs32, set_off, arena, raw_flag, raw_pk48, sig, sig_stride,
                      sig_len, table, table_ok, pk_agg, pk_st, seed, nonce, H, rP, rS, status);

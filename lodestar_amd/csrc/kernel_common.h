@@ -54,6 +54,8 @@ enum : uint8_t { GRP_PENDING = 0, GRP_FALLBACK = 1, GRP_OK = 2 };
 constexpr uint32_t FB_COOP_MAX = 256;
 // Message counts up to which hash_to_G2 runs on lane pairs (latency) instead of one lane each.
 constexpr uint32_t HASH_PAIR_MAX = 4096;
+// HASH_PAIR_MAX, overridable for A/B runs (GBV_HASH_PAIR_MAX); host side only
+uint32_t hash_pair_max();
 // verifySignatureSets passes up to this many sets compute their Miller values one wave per set
 // (cooperative, ~2.9 ms) instead of one thread per set (~16 ms of latency, far less VALU in total).
 constexpr uint32_t VS_COOP_MILLER_MAX = 2048;
