@@ -10,7 +10,7 @@ i=0
 for setting in "$@"; do
   i=$((i + 1))
   envs=""; [ "$setting" != "-" ] && envs="$setting"
-  env $envs timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-signing-roots ${AB_EXTRAS:---no-extras} > "$OUT/run$i.json" 2> "$OUT/run$i.err" || { echo "bench failed ($setting)"; tail -20 "$OUT/run$i.err"; exit 1; }
+  env $envs timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-signing-roots ${AB_EXTRAS:---no-extras} ${AB_ARGS:-} > "$OUT/run$i.json" 2> "$OUT/run$i.err" || { echo "bench failed ($setting)"; tail -20 "$OUT/run$i.err"; exit 1; }
   python3 - "$OUT/run$i.json" "$setting" <<'PY'
 import json, sys
 d = json.load(open(sys.argv[1]))
