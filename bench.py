@@ -469,6 +469,8 @@ def main():
     ap.add_argument("--no-stream", dest="stream", action="store_false",
                     help="one batch at a time (no overlap of consecutive verifications)")
     ap.add_argument("--inflight", type=int, default=3, help="staged batches queued on the device at once")
+    ap.add_argument("--c3-calls", type=int, default=512, help="128-set calls per C3 device pass")
+    ap.add_argument("--c4-blocks", type=int, default=64, help="blocks per C4 device pass (range-sync segment)")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -626,9 +628,10 @@ def main():
         if cpu_ok:
             from oracle import cpu_baseline
             pk_rows = cpu_baseline.affine_rows(cpu_baseline.load(), key_pks)
-        for name, fn, a in (("c1", c1_bench, sks), ("c3", c3_bench, sk_ints), ("c4", c4_bench, sk_ints)):
+        for name, fn, a, kw in (("c1", c1_bench, sks, {}), ("c3", c3_bench, sk_ints, {"n_calls": args.c3_calls}),
+                                ("c4", c4_bench, sk_ints, {"n_blocks": args.c4_blocks})):
             t = time.time()
-            extras[name] = fn(v, a, pk_rows, cpu_ok)
+            extras[name] = fn(v, a, pk_rows, cpu_ok, **kw)
             log("%s: %s sets/s (%.1fs)" % (name, extras[name]["value"], time.time() - t))
 
     ssz = None
