@@ -267,7 +267,9 @@ GBV_NI G2J g2_mul_xabs_lazy(G2A q) {
 // form.  In that form (ROCm 7.2, IPRA on) the ~60 SGPR constants of the lazy chain left
 // k_vs_hash_sig with a corrupted pointer after the call (illegal address on the GPU, reproduced
 // and gone with -mllvm -enable-ipra=false).
+#if GBV_LAZY_G2
 __device__ __attribute__((used)) static void* const g_keep_lazy_xabs_cc = (void*)&g2_mul_xabs_lazy;
+#endif
 GBV_NI G2J g2_mul_xabs_jac(G2J q) { G2J r = jac_mul_xabs_jac(q); return ret_copy(r); }
 GBV_NI G1J g1_mul_u256(G1A q, const uint32_t* k) { G1J r = jac_mul_u256(q, k); return ret_copy(r); }
 GBV_NI G2J g2_mul_u256(G2A q, const uint32_t* k) { G2J r = jac_mul_u256(q, k); return ret_copy(r); }
