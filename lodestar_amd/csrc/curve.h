@@ -21,6 +21,7 @@ GBV_HD Fp f_neg(const Fp& a) { return fp_neg(a); }
 GBV_HD Fp f_dbl(const Fp& a) { return fp_dbl(a); }
 GBV_HD Fp f_mul(const Fp& a, const Fp& b) { return fp_mul(a, b); }
 GBV_HD Fp f_sqr(const Fp& a) { return fp_sqr(a); }
+GBV_HD Fp f_add_lazy(const Fp& a, const Fp& b) { return fp_add_lazy(a, b); }  // feeds products only
 GBV_HD bool f_is_zero(const Fp& a) { return fp_is_zero(a); }
 GBV_HD bool f_eq(const Fp& a, const Fp& b) { return fp_eq(a, b); }
 GBV_HD Fp f_sel(bool c, const Fp& a, const Fp& b) { return fp_sel(c, a, b); }
@@ -34,6 +35,7 @@ GBV_HD Fp2 f_neg(const Fp2& a) { return fp2_neg(a); }
 GBV_HD Fp2 f_dbl(const Fp2& a) { return fp2_dbl(a); }
 GBV_HD Fp2 f_mul(const Fp2& a, const Fp2& b) { return fp2_mul(a, b); }
 GBV_HD Fp2 f_sqr(const Fp2& a) { return fp2_sqr(a); }
+GBV_HD Fp2 f_add_lazy(const Fp2& a, const Fp2& b) { return fp2_add_lazy(a, b); }
 GBV_HD bool f_is_zero(const Fp2& a) { return fp2_is_zero(a); }
 GBV_HD bool f_eq(const Fp2& a, const Fp2& b) { return fp2_eq(a, b); }
 GBV_HD Fp2 f_sel(bool c, const Fp2& a, const Fp2& b) { return fp2_sel(c, a, b); }
@@ -82,8 +84,8 @@ template <class F> GBV_HD Jac<F> jac_dbl(const Jac<F>& p) {
   F B = f_sqr(p.y);
   F A = f_sqr(p.x);
   F C = f_sqr(B);
-  F D = f_dbl(f_sub(f_sub(f_sqr(f_add(p.x, B)), A), C));
-  F E = f_add(f_dbl(A), A);
+  F D = f_dbl(f_sub(f_sub(f_sqr(f_add_lazy(p.x, B)), A), C));
+  F E = f_add_lazy(f_add_lazy(A, A), A);  // < 3p: feeds the two products below only
   F Fv = f_sqr(E);
   r.x = f_sub(Fv, f_dbl(D));
   F C8 = f_dbl(f_dbl(f_dbl(C)));
@@ -110,7 +112,7 @@ template <class F> GBV_HD Jac<F> jac_add_aff(const Jac<F>& p, const Aff<F>& q) {
   Jac<F> r;
   r.x = f_sub(f_sub(f_sqr(rr), J), f_dbl(V));
   r.y = f_sub(f_mul(rr, f_sub(V, r.x)), f_dbl(f_mul(p.y, J)));
-  r.z = f_sub(f_sub(f_sqr(f_add(p.z, H)), Z1Z1), HH);
+  r.z = f_sub(f_sub(f_sqr(f_add_lazy(p.z, H)), Z1Z1), HH);
   return jac_sel(p_inf, jac_from_aff(q), r);
 }
 

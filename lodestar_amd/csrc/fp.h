@@ -123,6 +123,37 @@ GBV_HD Fp fp_neg(const Fp& a) {
 
 GBV_HD Fp fp_dbl(const Fp& a) { return fp_add(a, a); }
 
+// Lazy forms for values that only feed a product: the product takes any input below 2^384 (fp_to28)
+// and its Montgomery output stays below 1.02 p for inputs below 7 p (7p x 7p / 2^392 < 0.02 p), so
+// the conditional subtraction of a modular add/sub is skipped.  fp_sub_lazy4: a + 4p - b for b < 4p.
+static constexpr Fp P4_RAW = {{0xfffeaaacu, 0xe7fbffffu, 0xc54ffffeu, 0x7aaffffau, 0xdac3d890u, 0x9cc34a83u, 0xce144afdu,
+                               0x91dd2e13u, 0x0d2eb35du, 0x2c6e9ed9u, 0xe5ff9a69u, 0x680447a8u}};  // 4 p < 2^383
+#if defined(__HIP_DEVICE_COMPILE__)
+GBV_HD Fp fp_add_lazy(const Fp& a, const Fp& b) {
+  Fp s;
+  GBV_ASM_ADD_RAW(s, a, b);
+  return s;
+}
+GBV_HD Fp fp_sub_lazy4(const Fp& a, const Fp& b) {
+  Fp t, d;
+  const Fp k = P4_RAW;
+  GBV_ASM_SUB_RAW_K(t, d, a, b, k);
+  return d;
+}
+#else
+GBV_HD Fp fp_add_lazy(const Fp& a, const Fp& b) {
+  Fp s;
+  raw_add(s, a, b);
+  return s;
+}
+GBV_HD Fp fp_sub_lazy4(const Fp& a, const Fp& b) {
+  Fp t, d;
+  raw_add(t, a, P4_RAW);
+  raw_sub(d, t, b);
+  return d;
+}
+#endif
+
 // ---- the product: 14 x 28-bit limbs, Montgomery radix R = 2^392 ---------------------------------
 // An element is stored as 12 x 32-bit limbs (adds, subtracts and comparisons use the hardware carry
 // chain), but multiplied as 14 limbs of 28 bits: a column of up to 14 a_i b_j and 14 m_i p_j

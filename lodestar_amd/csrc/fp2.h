@@ -54,19 +54,23 @@ GBV_HD Fp2 fp2_sqr(const Fp2& a) {
 #else
 // Karatsuba over out-of-line Fp products: the Fp2 layer is inlined into its caller and only the
 // 70-VGPR Fp product is a call, so occupancy (not in-thread ILP) hides the mad latency.
+// Inputs may be lazy (components below 4 p, fp_add_lazy): the Karatsuba sums and the (a0 - a1)
+// of the square are formed without reduction; outputs are canonical.
 GBV_HD Fp2 fp2_mul(const Fp2& a, const Fp2& b) {
   Fp t0 = fp_mul(a.c0, b.c0);
   Fp t1 = fp_mul(a.c1, b.c1);
-  Fp t2 = fp_mul(fp_add(a.c0, a.c1), fp_add(b.c0, b.c1));
+  Fp t2 = fp_mul(fp_add_lazy(a.c0, a.c1), fp_add_lazy(b.c0, b.c1));
   return Fp2{fp_sub(t0, t1), fp_sub(fp_sub(t2, t0), t1)};
 }
 
 GBV_HD Fp2 fp2_sqr(const Fp2& a) {
-  Fp t0 = fp_mul(fp_add(a.c0, a.c1), fp_sub(a.c0, a.c1));
+  Fp t0 = fp_mul(fp_add_lazy(a.c0, a.c1), fp_sub_lazy4(a.c0, a.c1));
   Fp t1 = fp_mul(a.c0, a.c1);
   return Fp2{t0, fp_dbl(t1)};
 }
 #endif
+
+GBV_HD Fp2 fp2_add_lazy(const Fp2& a, const Fp2& b) { return Fp2{fp_add_lazy(a.c0, b.c0), fp_add_lazy(a.c1, b.c1)}; }
 
 
 GBV_HD Fp2 fp2_mul_fp(const Fp2& a, const Fp& s) { return Fp2{fp_mul(a.c0, s), fp_mul(a.c1, s)}; }
