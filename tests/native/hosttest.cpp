@@ -17,6 +17,13 @@ static Fp2 load_fp2(const uint8_t* in) { return Fp2{load_mont(in), load_mont(in 
 
 extern "C" {
 void ht_fp_mul(uint8_t* out, const uint8_t* a, const uint8_t* b) { store_canon(out, fp_mul(load_mont(a), load_mont(b))); }
+// Lazy product inputs (fp.h fp_add_lazy / fp_sub_lazy4): raw 384-bit Montgomery-form operands, which
+// may be >= p; op 0: (a + b) * c, op 1: (a + 4p - b) * c, op 2: a * b.  Output raw (must be < p).
+void ht_fp_lazy(uint8_t* out, const uint8_t* a, const uint8_t* b, const uint8_t* c, int op) {
+  const Fp x = fp_load_be48(a, false), y = fp_load_be48(b, false), z = fp_load_be48(c, false);
+  Fp r = op == 0 ? fp_mul(fp_add_lazy(x, y), z) : op == 1 ? fp_mul(fp_sub_lazy4(x, y), z) : fp_mul(x, y);
+  fp_store_be48(out, r);
+}
 void ht_fp_inv(uint8_t* out, const uint8_t* a) { store_canon(out, fp_inv(load_mont(a))); }
 int ht_fp2_sqrt(uint8_t* out, const uint8_t* a) {
   Fp2 r;

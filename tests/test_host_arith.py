@@ -54,6 +54,32 @@ def test_fp_mul_inv(lib):
         assert int.from_bytes(out.raw, "big") * a % o.P == 1
 
 
+def test_fp_lazy_product_inputs(lib):
+    """Unreduced sums feed the product (fp.h fp_add_lazy / fp_sub_lazy4): inputs up to 7p give a
+    canonical output, a b 2^-392 mod p, at the extremes the callers reach (curve.h jac_dbl: 3A and
+    X + B; fp2.h: Karatsuba sums of lazy components < 3p, a0 + 4p - a1 < 7p)."""
+    rng = random.Random(7)
+    rinv = pow(2, -392, o.P)
+    out = buf(48)
+    raw = lambda x: x.to_bytes(48, "big")
+    edge = [0, 1, o.P - 1, 2 * o.P - 1, 3 * o.P - 1, 3 * o.P - 2]
+    for _ in range(40):
+        a = rng.choice(edge + [rng.randrange(3 * o.P)])
+        b = rng.choice(edge + [rng.randrange(3 * o.P)])
+        c = rng.choice(edge + [rng.randrange(7 * o.P)])
+        lib.ht_fp_lazy(out, raw(a), raw(b), raw(c), 0)  # (a + b) c, a + b < 6p
+        got = int.from_bytes(out.raw, "big")
+        assert got < o.P and got == (a + b) * c * rinv % o.P
+        bb = min(b, 4 * o.P - 1)
+        lib.ht_fp_lazy(out, raw(a), raw(bb), raw(c), 1)  # (a + 4p - b) c, < 7p
+        got = int.from_bytes(out.raw, "big")
+        assert got < o.P and got == (a + 4 * o.P - bb) * c * rinv % o.P
+    for a, b in ((7 * o.P - 1, 7 * o.P - 1), (7 * o.P - 1, 1), (6 * o.P + 5, 5 * o.P + 3)):
+        lib.ht_fp_lazy(out, raw(a), raw(b), raw(0), 2)
+        got = int.from_bytes(out.raw, "big")
+        assert got < o.P and got == a * b * rinv % o.P
+
+
 def test_fp_inv_edges(lib):
     """Binary-GCD inversion (fp.h fp_inv) at edge values; 0 maps to 0 like the exponentiation."""
     out = buf(48)
