@@ -88,6 +88,8 @@ struct gbv_sm_batch {
   G2A *H = nullptr, *S = nullptr;
   G2J *rS = nullptr, *SgJ = nullptr;
   Fp12* F = nullptr;
+  Fp12* Fpair = nullptr;     // 2 per chunk: the two Miller values of a chunk's own check (k_sm_group_miller2)
+  uint8_t* pair_ok = nullptr;
   Fp12* Fpart = nullptr;  // per 64-chunk block partials of a segment (reused segment after segment)
   G2J* Spart = nullptr;
   uint8_t* has = nullptr;
@@ -111,7 +113,7 @@ static void sm_free_work(gbv_sm_batch* b) {
   hipFree(b->n_fallback); hipFree(b->status); hipFree(b->grp_state); hipFree(b->valid);
   hipFree(b->H); hipFree(b->S); hipFree(b->SgJ); hipFree(b->rS); hipFree(b->rP); hipFree(b->PgJ);
   hipHostFree(b->valid_host); hipHostFree(b->nfb_host);
-  hipFree(b->F); hipFree(b->seg_ok); hipHostFree(b->seg_ok_host);
+  hipFree(b->F); hipFree(b->Fpair); hipFree(b->pair_ok); hipFree(b->seg_ok); hipHostFree(b->seg_ok_host);
   hipFree(b->Fpart); hipFree(b->Spart); hipFree(b->has);
   hipFree(b->fb_runs); hipFree(b->fb_list); hipFree(b->fb_cnt);
   for (int k = 0; k < 2; ++k) {
@@ -122,7 +124,7 @@ static void sm_free_work(gbv_sm_batch* b) {
   }
   hipFree(b->msm_ent); hipFree(b->msm_total);
   b->n_fallback = nullptr; b->status = b->grp_state = b->valid = b->seg_ok = b->seg_ok_host = b->valid_host = nullptr;
-  b->H = b->S = nullptr; b->SgJ = b->rS = nullptr; b->rP = b->PgJ = nullptr; b->F = b->Fpart = nullptr; b->Spart = nullptr;
+  b->H = b->S = nullptr; b->SgJ = b->rS = nullptr; b->rP = b->PgJ = nullptr; b->F = b->Fpart = b->Fpair = nullptr; b->pair_ok = nullptr; b->Spart = nullptr;
   b->has = nullptr; b->fb_runs = nullptr; b->fb_list = b->fb_cnt = b->nfb_host = nullptr; b->msm_ent = nullptr; b->msm_total = nullptr;
   b->allocated = false;
 }
@@ -154,6 +156,7 @@ static int sm_reserve(gbv_ctx* c, gbv_sm_batch* b, size_t n, size_t G, size_t ca
   chk(dalloc(&b->status, n)); chk(dalloc(&b->grp_state, G)); chk(dalloc(&b->valid, n));
   chk(dalloc(&b->H, calls)); chk(dalloc(&b->S, n)); chk(dalloc(&b->rS, n)); chk(dalloc(&b->rP, n));
   chk(dalloc(&b->PgJ, G)); chk(dalloc(&b->SgJ, G)); chk(dalloc(&b->F, G));
+  chk(dalloc(&b->Fpair, 2 * G)); chk(dalloc(&b->pair_ok, 2 * G));
   // block partials: one region per segment parity (two segments' reductions can be in flight)
   b->part_stride = seg_reduce_scratch(G);
   chk(dalloc(&b->Fpart, 2 * b->part_stride)); chk(dalloc(&b->Spart, 2 * b->part_stride)); chk(dalloc(&b->has, 2 * b->part_stride));
@@ -733,7 +736,8 @@ int gbv_sm_batch_submit(gbv_ctx* c, gbv_sm_batch* b) {
     if (G >= GROUP_CHECK_THREAD_MIN)
       launch_sm_group_check(LaunchCfg{0, 64, sb}, g0, G, b->F, b->SgJ, b->seg_ok + s, b->grp_state, b->n_fallback);
     else
-      launch_sm_group_pairing(LaunchCfg{G, 64, sb}, g0, G, b->grp_msg, b->PgJ, b->SgJ, b->H, b->seg_ok + s, b->grp_state, b->n_fallback);
+      launch_sm_group_pairing(LaunchCfg{G, 64, sb}, g0, G, b->grp_msg, b->PgJ, b->SgJ, b->H, b->seg_ok + s, b->grp_state, b->n_fallback,
+                              b->Fpair, b->pair_ok);
     HIP_CHECK(c, hipEventRecord(e[9], sb));
   }
   hipEvent_t* ep = ev + 2 + EPS * S;

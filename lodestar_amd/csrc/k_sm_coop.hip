@@ -1,6 +1,8 @@
 // Same-message path kernels built on the wave-cooperative pairing arithmetic (coop.h): one
 // workgroup = one wave = one pairing job.  Kept in their own translation unit so their small
 // register budget (one Fp product per lane) is not merged with the thread-per-set kernels'.
+#include <cstdlib>
+
 #include "launch.h"
 #include "kernel_common.h"
 #include "coop.h"
@@ -148,6 +150,72 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
   }
 }
 
+// The same check with its two Miller loops on two waves (latency: a lone gossip call ends here).
+// Block (g, j) forms the Miller value of pair j of chunk g -- j = 0: (P_g, H(m_g)), j = 1:
+// (-g1, S_g) -- so the chain is one Miller loop (Fp12 square + one line per bit) instead of the
+// 2-pair loop's square + two lines; k_sm_group_fe multiplies the two values and exponentiates.
+// pair_ok[2g + j] = 0 when the pair's point is at infinity (the chunk then goes to the per-set path,
+// as k_sm_group_pairing does).
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
+k_sm_group_miller2(uint32_t g0, const uint32_t* __restrict__ grp_msg, const G1J* __restrict__ PgJ, const G2J* __restrict__ SgJ,
+                   const G2A* __restrict__ H, const uint8_t* __restrict__ seg_ok, const uint8_t* __restrict__ grp_state,
+                   Fp12* __restrict__ Fpair, uint8_t* __restrict__ pair_ok) {
+  __shared__ coop::Slot ws[coop::MILLER_WS];
+  __shared__ Fp st[4];
+  __shared__ int ok;
+  const uint32_t g = g0 + blockIdx.x, j = blockIdx.y;
+  if (*seg_ok || grp_state[g] != GRP_PENDING) return;  // launched unconditionally: no host round trip
+  const unsigned lane = threadIdx.x;
+  coop::load_consts();
+  if (lane == 0) {
+    if (j == 0) {
+      G1A pa;
+      ok = jac_to_aff(pa, PgJ[g]) ? 1 : 0;
+      st[0] = pa.x;
+      st[1] = pa.y;
+    } else {
+      G2A sa;
+      ok = jac_to_aff(sa, SgJ[g]) ? 1 : 0;
+      st[0] = sa.x.c0;
+      st[1] = sa.x.c1;
+      st[2] = sa.y.c0;
+      st[3] = sa.y.c1;
+    }
+    pair_ok[2 * g + j] = (uint8_t)ok;
+  }
+  coop::barrier();
+  if (!ok) return;
+  if (j == 0)
+    coop::miller_load_pair(ws, 0, G1A{st[0], st[1]}, H[grp_msg[g]]);
+  else
+    coop::miller_load_pair(ws, 0, g1_neg_generator(), G2A{Fp2{st[0], st[1]}, Fp2{st[2], st[3]}});
+  coop::miller_loop(ws, 1);
+  if (lane < 12) ((Fp*)&Fpair[2 * g + j])[lane] = coop::get(ws + coop::M_F + lane);
+}
+
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
+k_sm_group_fe(uint32_t g0, const uint8_t* __restrict__ seg_ok, const Fp12* __restrict__ Fpair, const uint8_t* __restrict__ pair_ok,
+              uint8_t* __restrict__ grp_state, uint32_t* __restrict__ n_fallback) {
+  __shared__ coop::Slot ws[coop::FINAL_EXP_WS];
+  const uint32_t g = g0 + blockIdx.x;
+  if (*seg_ok || grp_state[g] != GRP_PENDING) return;
+  const unsigned lane = threadIdx.x;
+  bool ok = false;
+  if (pair_ok[2 * g] && pair_ok[2 * g + 1]) {
+    coop::load_consts();
+    if (lane < 12) {
+      coop::put(ws + coop::E_F + lane, ((const Fp*)&Fpair[2 * g])[lane]);
+      coop::put(ws + coop::E_TMP + lane, ((const Fp*)&Fpair[2 * g + 1])[lane]);
+    }
+    coop::barrier();
+    coop::mul12(ws, coop::E_Z, coop::E_F, coop::E_TMP, coop::E_F);
+    ok = coop::final_exp_is_one(ws);
+  }
+  if (lane == 0) {
+    grp_state[g] = ok ? GRP_OK : GRP_FALLBACK;
+    if (!ok) atomicAdd(n_fallback, 1u);
+  }
+}
 
 // e(P, Q) * e(-g1, S) == 1 by one wave (S = infinity drops the second pair).  Arguments must be
 // wave-uniform (the callers stage them in LDS).
@@ -252,9 +320,17 @@ void launch_sm_seg_check(LaunchCfg c, uint32_t g0, uint32_t G, uint8_t* grp_stat
   debug_sync(c.stream, "k_sm_seg_check");
 }
 void launch_sm_group_pairing(LaunchCfg c, uint32_t g0, uint32_t G, const uint32_t* grp_msg, const G1J* PgJ, const G2J* SgJ, const G2A* H,
-                             const uint8_t* seg_ok, uint8_t* grp_state, uint32_t* n_fallback) {
-  hipLaunchKernelGGL(k_sm_group_pairing, dim3(G), dim3(64), 0, c.stream, g0, grp_msg, PgJ, SgJ, H, seg_ok, grp_state, n_fallback);
-  debug_sync(c.stream, "k_sm_group_pairing");
+                             const uint8_t* seg_ok, uint8_t* grp_state, uint32_t* n_fallback, Fp12* Fpair, uint8_t* pair_ok) {
+  static const bool one_wave = getenv("GBV_GROUP_PAIRING_1W") && atoi(getenv("GBV_GROUP_PAIRING_1W")) != 0;
+  if (one_wave || !Fpair) {
+    hipLaunchKernelGGL(k_sm_group_pairing, dim3(G), dim3(64), 0, c.stream, g0, grp_msg, PgJ, SgJ, H, seg_ok, grp_state, n_fallback);
+    debug_sync(c.stream, "k_sm_group_pairing");
+    return;
+  }
+  hipLaunchKernelGGL(k_sm_group_miller2, dim3(G, 2), dim3(64), 0, c.stream, g0, grp_msg, PgJ, SgJ, H, seg_ok, grp_state, Fpair, pair_ok);
+  debug_sync(c.stream, "k_sm_group_miller2");
+  hipLaunchKernelGGL(k_sm_group_fe, dim3(G), dim3(64), 0, c.stream, g0, seg_ok, Fpair, pair_ok, grp_state, n_fallback);
+  debug_sync(c.stream, "k_sm_group_fe");
 }
 // Product of k Fp12 Miller partials (one per shard / GPU) and ONE final exponentiation == 1?
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
