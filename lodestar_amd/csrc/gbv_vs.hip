@@ -16,6 +16,8 @@
 // A call is true iff every chunk is (the AND over jobs, index.ts:185-206); a call with an empty
 // aggregate is rejected (aggregatePublicKeys throws EMPTY_AGGREGATE_ARRAY, index.ts:398-412); an
 // empty call is false (verifySignatureSetsMaybeBatch([]), maybeBatch.ts:29-31).
+#include <cstdlib>
+
 #include "ctx.h"
 
 using namespace gbv;
@@ -45,6 +47,8 @@ struct gbv_vs_batch {
   G2J* rS = nullptr;
   uint8_t* status = nullptr;
   Fp12* F = nullptr;
+  Fp12* Fs = nullptr;         // per chunk: Miller value of (-g1, sum r_i sig_i) (small passes, k_vs_miller_coop)
+  uint8_t* fs_flag = nullptr;
   uint8_t* chunk_valid = nullptr;
   uint8_t* chunk_valid_host = nullptr;  // pinned
   // shard mode (gbv_vs_partial): reduction scratch
@@ -52,7 +56,7 @@ struct gbv_vs_batch {
   G2J* Spart = nullptr;
   uint8_t *has = nullptr, *flag = nullptr;
   size_t part_cap = 0;
-  hipEvent_t ev[6] = {};
+  hipEvent_t ev[7] = {};
   hipEvent_t done = nullptr;
   bool in_flight = false;
   int tail = 0;
@@ -61,8 +65,8 @@ struct gbv_vs_batch {
 static void vs_free_work(gbv_vs_batch* b) {
   // teardown: a failing free has nothing left to report to
   (void)hipFree(b->pk); (void)hipFree(b->pk_st); (void)hipFree(b->H); (void)hipFree(b->rP); (void)hipFree(b->rS);
-  (void)hipFree(b->status); (void)hipFree(b->F); (void)hipFree(b->chunk_valid); (void)hipHostFree(b->chunk_valid_host);
-  b->pk = nullptr; b->pk_st = nullptr; b->H = nullptr; b->rP = nullptr; b->rS = nullptr; b->status = nullptr; b->F = nullptr;
+  (void)hipFree(b->status); (void)hipFree(b->F); (void)hipFree(b->Fs); (void)hipFree(b->fs_flag); (void)hipFree(b->chunk_valid); (void)hipHostFree(b->chunk_valid_host);
+  b->pk = nullptr; b->pk_st = nullptr; b->H = nullptr; b->rP = nullptr; b->rS = nullptr; b->status = nullptr; b->F = nullptr; b->Fs = nullptr; b->fs_flag = nullptr;
   b->chunk_valid = nullptr; b->chunk_valid_host = nullptr;
   b->allocated = false;
 }
@@ -91,6 +95,7 @@ static int vs_reserve(gbv_ctx* c, gbv_vs_batch* b, size_t n, size_t C) {
   auto chk = [&](hipError_t x) { if (x != hipSuccess && e == hipSuccess) e = x; };
   chk(dalloc(&b->pk, n)); chk(dalloc(&b->pk_st, n)); chk(dalloc(&b->H, n)); chk(dalloc(&b->rP, n)); chk(dalloc(&b->rS, n));
   chk(dalloc(&b->status, n)); chk(dalloc(&b->F, n)); chk(dalloc(&b->chunk_valid, C));
+  chk(dalloc(&b->Fs, C)); chk(dalloc(&b->fs_flag, C));
   chk(hipHostMalloc((void**)&b->chunk_valid_host, std::max<size_t>(C, 1), hipHostMallocDefault));
   for (auto& ev : b->ev)
     if (!ev) chk(hipEventCreate(&ev));
@@ -222,10 +227,19 @@ static int vs_fill(gbv_ctx* c, gbv_vs_batch* b, size_t n_calls, const uint32_t* 
   return GBV_OK;
 }
 
+static bool vs_fs_on() {  // GBV_VS_FS=0: the chunk check forms the (-g1, sum) Miller value itself (A/B)
+  static const bool on = !(getenv("GBV_VS_FS") && atoi(getenv("GBV_VS_FS")) == 0);
+  return on;
+}
+
+static bool vs_fs_small(const gbv_vs_batch* b) { return b->n <= VS_COOP_MILLER_MAX && vs_fs_on(); }
+
 // Per-set kernels: aggregate and hash + signature + randomisation on stream A, the Miller values on
 // stream m (a tail stream, so that they overlap the next batch's stream-A kernels; or stream A).
 // Events: ev0 agg ev1 hash_sig ev2 | (m) ev3 miller ev4.
-static int vs_enqueue_sets(gbv_ctx* c, gbv_vs_batch* b, hipStream_t m) {
+// with_fs: the chunk checks follow (gbv_vs_batch_submit), so a small pass also forms each chunk's
+// (-g1, sum r_i sig_i) Miller value beside the per-set ones.
+static int vs_enqueue_sets(gbv_ctx* c, gbv_vs_batch* b, hipStream_t m, bool with_fs) {
   hipStream_t s = c->stream;
   Seed seed = fresh_seed();
   uint32_t nonce = c->nonce++;
@@ -242,6 +256,11 @@ static int vs_enqueue_sets(gbv_ctx* c, gbv_vs_batch* b, hipStream_t m) {
   else
     launch_vs_miller(LaunchCfg{blocks_for(b->n), TPB, m}, (uint32_t)b->n, b->status, b->rP, b->H, b->F);
   HIP_CHECK(c, hipEventRecord(b->ev[4], m));
+  if (with_fs && vs_fs_small(b)) {  // beside the per-set Miller values, on stream A (free after hash_sig)
+    launch_vs_chunk_s_miller(s, (uint32_t)b->C, b->status, b->chunk_off, b->rS, b->Fs, b->fs_flag);
+    HIP_CHECK(c, hipEventRecord(b->ev[6], s));
+    if (m != s) HIP_CHECK(c, hipStreamWaitEvent(m, b->ev[6], 0));
+  }
   HIP_CHECK(c, hipGetLastError());
   return GBV_OK;
 }
@@ -281,9 +300,11 @@ int gbv_vs_batch_submit(gbv_ctx* c, gbv_vs_batch* b) {
   if (b->n == 0 || b->C == 0) return GBV_OK;
   b->tail = (int)(c->sm_submits++ & 1);
   hipStream_t t = b->tail ? c->stream4 : c->stream2;
-  int rc = vs_enqueue_sets(c, b, t);
+  int rc = vs_enqueue_sets(c, b, t, true);
   if (rc) return rc;
-  launch_vs_chunk_coop(LaunchCfg{(unsigned)b->C, 64, t}, (uint32_t)b->C, b->chunk_off, b->status, b->F, b->rS, b->chunk_valid);
+  const bool fs = vs_fs_small(b);
+  launch_vs_chunk_coop(LaunchCfg{(unsigned)b->C, 64, t}, (uint32_t)b->C, b->chunk_off, b->status, b->F, b->rS, b->chunk_valid,
+                       fs ? b->Fs : nullptr, b->fs_flag);
   HIP_CHECK(c, hipEventRecord(b->ev[5], t));
   HIP_CHECK(c, hipMemcpyAsync(b->chunk_valid_host, b->chunk_valid, b->C, hipMemcpyDeviceToHost, t));
   HIP_CHECK(c, hipEventRecord(b->done, t));
@@ -388,7 +409,7 @@ int gbv_vs_partial(gbv_ctx* c, const gbv_set* sets, size_t n, const uint32_t* ar
   }
   HIP_CHECK(c, hipSetDevice(c->device));
   hipStream_t s = c->stream;
-  if ((rc = vs_enqueue_sets(c, b, s))) return rc;
+  if ((rc = vs_enqueue_sets(c, b, s, false))) return rc;
   // status doubles as the per-"chunk" state: SET_OK == GRP_PENDING (every valid set takes part);
   // the reduction is a tree over 64-set blocks (k_sm_seg_reduce, k_sm_part_reduce)
   launch_sm_seg_check(LaunchCfg{1, 64, s}, 0, (uint32_t)n, b->status, b->F, b->rS, b->Fpart, b->Spart, b->has, b->flag, b->f_out);

@@ -40,6 +40,36 @@ __device__ inline void wave_reduce_fs_coop(Fp12& f, G2J& s, int& any) {
   }
 }
 
+// cross-lane trees over one of the two: lane 0 ends with the product of the f / the sum of the s
+__device__ inline void wave_reduce_f_coop(Fp12& f, int& any) {
+  unsigned lane = threadIdx.x;
+  for (unsigned d = 32; d >= 1; d >>= 1) {
+    Fp12 fo;
+    Fp* fd = (Fp*)&fo;
+    const Fp* fsrc = (const Fp*)&f;
+    for (int i = 0; i < 12; ++i) fd[i] = shfl_down_fp_c(fsrc[i], d);
+    int ao = __shfl_down(any, d, 64);
+    if (lane < d && ao) {
+      f = any ? fp12_mul(f, fo) : fo;
+      any = 1;
+    }
+  }
+}
+__device__ inline void wave_reduce_s_coop(G2J& s, int& any) {
+  unsigned lane = threadIdx.x;
+  for (unsigned d = 32; d >= 1; d >>= 1) {
+    G2J so;
+    Fp* sd = (Fp*)&so;
+    const Fp* ssrc = (const Fp*)&s;
+    for (int i = 0; i < 6; ++i) sd[i] = shfl_down_fp_c(ssrc[i], d);
+    int ao = __shfl_down(any, d, 64);
+    if (lane < d && ao) {
+      s = any ? g2_add(s, so) : so;
+      any = 1;
+    }
+  }
+}
+
 // One wave per segment: the randomised chunk equations of the whole segment are folded into one
 // check  prod_g e(P_g, H(m_g)) * e(-g1, sum_g S_g) == 1  with ONE final exponentiation.  Every
 // set carries its own random 64-bit scalar, so this is blst's verifyMultipleAggregateSignatures
@@ -351,9 +381,13 @@ k_fp12_check(uint32_t k, const Fp12* __restrict__ parts, uint8_t* __restrict__ o
 // verifySignatureSets chunks (<= 255 sets each, chunkifyMaximizeChunkSize; (begin, end) pairs): one wave per chunk
 // multiplies its sets' Miller values and sums r_i sig_i (cross-lane tree), then runs the
 // (-g1, sum) pair and the final exponentiation cooperatively (maybeBatch.ts:17-26).
+// With Fs (small passes): the (-g1, sum) Miller value was formed beside the per-set ones by
+// k_vs_miller_coop (fs_flag 1; 2: the sum is infinity, no pair), so this kernel only multiplies.
+template <bool FS>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
 k_vs_chunk_coop(const uint32_t* __restrict__ chunk_be, const uint8_t* __restrict__ status, const Fp12* __restrict__ f,
-                const G2J* __restrict__ rS, uint8_t* __restrict__ chunk_valid) {
+                const G2J* __restrict__ rS, uint8_t* __restrict__ chunk_valid, const Fp12* __restrict__ Fs,
+                const uint8_t* __restrict__ fs_flag) {
   __shared__ coop::Slot ws[SEG_WS];
   __shared__ int flags[2];
   __shared__ Fp stage[6];
@@ -370,11 +404,22 @@ k_vs_chunk_coop(const uint32_t* __restrict__ chunk_be, const uint8_t* __restrict
       continue;
     }
     acc = any ? fp12_mul(acc, f[i]) : f[i];
-    s = any ? g2_add(s, rS[i]) : rS[i];
+    if (!FS) s = any ? g2_add(s, rS[i]) : rS[i];
     any = 1;
   }
   if (__any(bad)) {
     if (lane == 0) chunk_valid[c] = 0;
+    return;
+  }
+  if (FS) {
+    wave_reduce_f_coop(acc, any);
+    coop::load_consts();
+    if (lane == 0) coop::store12(ws + coop::E_F, acc);
+    if (fs_flag[c] == 1 && lane < 12) coop::put(ws + coop::E_TMP + lane, ((const Fp*)&Fs[c])[lane]);
+    coop::barrier();
+    if (fs_flag[c] == 1) coop::mul12(ws, coop::E_Z, coop::E_F, coop::E_TMP, coop::E_F);
+    bool ok = fs_flag[c] != 0 && coop::final_exp_is_one(ws);
+    if (lane == 0) chunk_valid[c] = ok ? 1 : 0;
     return;
   }
   wave_reduce_fs_coop(acc, s, any);
@@ -406,6 +451,51 @@ k_vs_chunk_coop(const uint32_t* __restrict__ chunk_be, const uint8_t* __restrict
   if (lane == 0) chunk_valid[c] = ok ? 1 : 0;
 }
 
+// Chunk c's sum of r_i sig_i and the Miller value of (-g1, sum), one wave per chunk, on its own stream
+// beside k_vs_miller_coop (small passes), so that k_vs_chunk_coop's critical path loses that Miller
+// loop (fs_flag: 0 the chunk holds a rejected set, 1 Fs[c] set, 2 the sum is infinity).  A kernel of
+// its own: the serial G2 additions would otherwise raise k_vs_miller_coop's register budget.
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
+k_vs_chunk_s_miller(const uint8_t* __restrict__ status, const uint32_t* __restrict__ chunk_be, const G2J* __restrict__ rS,
+                    Fp12* __restrict__ Fs, uint8_t* __restrict__ fs_flag) {
+  __shared__ coop::Slot ws[coop::MILLER_WS];
+  __shared__ Fp stage[4];
+  __shared__ int ok;
+  const unsigned lane = threadIdx.x;
+  const uint32_t c = blockIdx.x;
+  const uint32_t b = chunk_be[2 * c], e = chunk_be[2 * c + 1];
+  int bad = b == e, any = 0;
+  G2J s = jac_infinity<Fp2>();
+  for (uint32_t i = b + lane; i < e; i += 64) {
+    if (status[i] != SET_OK) {
+      bad = 1;
+      continue;
+    }
+    s = any ? g2_add(s, rS[i]) : rS[i];
+    any = 1;
+  }
+  if (__any(bad)) {
+    if (lane == 0) fs_flag[c] = 0;
+    return;
+  }
+  wave_reduce_s_coop(s, any);
+  coop::load_consts();
+  if (lane == 0) {
+    G2A sa;
+    ok = jac_to_aff(sa, s) ? 1 : 0;
+    stage[0] = sa.x.c0;
+    stage[1] = sa.x.c1;
+    stage[2] = sa.y.c0;
+    stage[3] = sa.y.c1;
+    fs_flag[c] = ok ? 1 : 2;
+  }
+  coop::barrier();
+  if (!ok) return;
+  coop::miller_load_pair(ws, 0, g1_neg_generator(), G2A{Fp2{stage[0], stage[1]}, Fp2{stage[2], stage[3]}});
+  coop::miller_loop(ws, 1);
+  if (lane < 12) ((Fp*)&Fs[c])[lane] = coop::get(ws + coop::M_F + lane);
+}
+
 // Miller value f_{|x|, H(m_i)}(r_i pk_i) of one set per wave (latency: small verifySignatureSets
 // passes; k_vs_miller runs one thread per set for large ones).  Same value up to an Fp factor as the
 // thread version (the final exponentiation removes it): P is made affine by lane 0 first.
@@ -414,9 +504,9 @@ k_vs_miller_coop(const uint8_t* __restrict__ status, const G1J* __restrict__ rP,
   __shared__ coop::Slot ws[coop::MILLER_WS];
   __shared__ Fp stage[2];
   __shared__ int ok;
+  const unsigned lane = threadIdx.x;
   const uint32_t i = blockIdx.x;
   if (status[i] != SET_OK) return;
-  const unsigned lane = threadIdx.x;
   coop::load_consts();
   if (lane == 0) {
     G1A pa;
@@ -434,6 +524,11 @@ k_vs_miller_coop(const uint8_t* __restrict__ status, const G1J* __restrict__ rP,
   if (lane < 12) ((Fp*)&F[i])[lane] = coop::get(ws + coop::M_F + lane);
 }
 
+void launch_vs_chunk_s_miller(hipStream_t s, uint32_t C, const uint8_t* status, const uint32_t* chunk_be, const G2J* rS, Fp12* Fs,
+                              uint8_t* fs_flag) {
+  hipLaunchKernelGGL(k_vs_chunk_s_miller, dim3(C), dim3(64), 0, s, status, chunk_be, rS, Fs, fs_flag);
+  debug_sync(s, "k_vs_chunk_s_miller");
+}
 void launch_vs_miller_coop(hipStream_t s, uint32_t n, const uint8_t* status, const G1J* rP, const G2A* H, Fp12* F) {
   hipLaunchKernelGGL(k_vs_miller_coop, dim3(n), dim3(64), 0, s, status, rP, H, F);
   debug_sync(s, "k_vs_miller_coop");
@@ -444,8 +539,11 @@ void launch_fp12_check(LaunchCfg c, uint32_t k, const Fp12* parts, uint8_t* out)
   debug_sync(c.stream, "k_fp12_check");
 }
 void launch_vs_chunk_coop(LaunchCfg c, uint32_t C, const uint32_t* chunk_be, const uint8_t* status, const Fp12* f, const G2J* rS,
-                          uint8_t* chunk_valid) {
-  hipLaunchKernelGGL(k_vs_chunk_coop, dim3(C), dim3(64), 0, c.stream, chunk_be, status, f, rS, chunk_valid);
+                          uint8_t* chunk_valid, const Fp12* Fs, const uint8_t* fs_flag) {
+  if (Fs)
+    hipLaunchKernelGGL(k_vs_chunk_coop<true>, dim3(C), dim3(64), 0, c.stream, chunk_be, status, f, rS, chunk_valid, Fs, fs_flag);
+  else
+    hipLaunchKernelGGL(k_vs_chunk_coop<false>, dim3(C), dim3(64), 0, c.stream, chunk_be, status, f, rS, chunk_valid, Fs, fs_flag);
   debug_sync(c.stream, "k_vs_chunk_coop");
 }
 }  // namespace gbv
