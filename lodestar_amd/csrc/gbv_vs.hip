@@ -232,7 +232,12 @@ static bool vs_fs_on() {  // GBV_VS_FS=0: the chunk check forms the (-g1, sum) M
   return on;
 }
 
-static bool vs_fs_small(const gbv_vs_batch* b) { return b->n <= VS_COOP_MILLER_MAX && vs_fs_on(); }
+// Small passes, and passes of few chunks (a range-sync segment of blocks: 2 chunks per block), whose
+// chunk checks are latency-bound; GBV_VS_FS_MAXC sets the chunk bound (A/B).
+static bool vs_fs_small(const gbv_vs_batch* b) {
+  static const size_t maxc = getenv("GBV_VS_FS_MAXC") ? (size_t)atol(getenv("GBV_VS_FS_MAXC")) : 256;
+  return vs_fs_on() && (b->n <= VS_COOP_MILLER_MAX || b->C <= maxc);
+}
 
 // Per-set kernels: aggregate and hash + signature + randomisation on stream A, the Miller values on
 // stream m (a tail stream, so that they overlap the next batch's stream-A kernels; or stream A).
