@@ -1,4 +1,6 @@
 // Same-message path kernels (verifySignatureSetsSameMessage).
+#include <cstdlib>
+
 #include "launch.h"
 #include "kernel_common.h"
 
@@ -164,6 +166,52 @@ __global__ void GBV_KERNEL_ATTR k_sm_chunk_finish(uint32_t g0, uint32_t G, uint3
   }
   grp_state[g] = bad ? GRP_FALLBACK : GRP_PENDING;
   if (bad) atomicAdd(n_fallback, 1u);
+}
+
+// The same with one wave per chunk (segments of few chunks: a lone gossip call): lane k adds in the
+// k-th group sum of the chunk by a cross-lane tree (log2 of the group count levels instead of a
+// serial chain of group additions).  Same sums, same grp_state / n_fallback as k_sm_chunk_finish.
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
+k_sm_chunk_finish_wave(uint32_t g0, uint32_t s0, const uint32_t* __restrict__ grp_off, const uint8_t* __restrict__ status,
+                       const G2J* __restrict__ Sh, const G1J* __restrict__ Ph, G1J* __restrict__ PgJ, G2J* __restrict__ SgJ,
+                       uint8_t* __restrict__ grp_state, uint32_t* __restrict__ n_fallback) {
+  const uint32_t g = g0 + blockIdx.x;
+  const unsigned lane = threadIdx.x;
+  const uint32_t b = grp_off[g], e = grp_off[g + 1];
+  int bad = b == e;
+  for (uint32_t i = b + lane; i < e; i += 64) bad |= status[i] != SET_OK;
+  bad = __any(bad);
+  // group starts: the chunk start, then every SCAN_W-set boundary of the segment inside the chunk
+  // (lane k takes groups k, k + 64, ...: any chunk length)
+  int any = 0;
+  G1J p = jac_infinity<Fp>();
+  G2J s = jac_infinity<Fp2>();
+  for (uint32_t k = lane; !bad; k += 64) {
+    const uint32_t q = k == 0 ? b : s0 + ((b - s0) / SCAN_W + k) * SCAN_W;
+    if (q >= e) break;
+    p = any ? g1_add(p, Ph[q]) : Ph[q];
+    if (Sh) s = any ? g2_add(s, Sh[q]) : Sh[q];
+    any = 1;
+  }
+  for (unsigned d = 32; d >= 1; d >>= 1) {
+    G1J po = shfl_down_jac(p, d);
+    G2J so = shfl_down_jac(s, d);
+    int ao = __shfl_down(any, d, 64);
+    if (lane < d && ao) {
+      p = any ? g1_add(p, po) : po;
+      if (Sh) s = any ? g2_add(s, so) : so;
+      any = 1;
+    }
+  }
+  if (lane == 0) {
+    if (!bad) {
+      bad = jac_is_inf(p);
+      PgJ[g] = p;
+      SgJ[g] = s;
+    }
+    grp_state[g] = bad ? GRP_FALLBACK : GRP_PENDING;
+    if (bad) atomicAdd(n_fallback, 1u);
+  }
 }
 
 // Miller value f_g = f_{|x|, H(m_g)}(P_g) of every pending chunk, one thread per chunk: the
@@ -398,8 +446,13 @@ void launch_sm_chunk_finish_s(LaunchCfg c, uint32_t g0, uint32_t G, uint32_t s0,
 }
 void launch_sm_chunk_finish(LaunchCfg c, uint32_t g0, uint32_t G, uint32_t s0, const uint32_t* grp_off, const uint8_t* status, const G2J* Sh,
                             const G1J* Ph, G1J* PgJ, G2J* SgJ, uint8_t* grp_state, uint32_t* n_fallback) {
-  hipLaunchKernelGGL(k_sm_chunk_finish, dim3((G + 63) / 64), dim3(64), 0, c.stream, g0, G, s0, grp_off, status, Sh, Ph, PgJ, SgJ, grp_state,
-                     n_fallback);
+  static const uint32_t wave_max = getenv("GBV_CHUNK_FINISH_WAVE_MAX") ? (uint32_t)atoi(getenv("GBV_CHUNK_FINISH_WAVE_MAX")) : 32;
+  if (G <= wave_max)  // latency (a lone call): a wave per chunk, tree over its group sums
+    hipLaunchKernelGGL(k_sm_chunk_finish_wave, dim3(G), dim3(64), 0, c.stream, g0, s0, grp_off, status, Sh, Ph, PgJ, SgJ, grp_state,
+                       n_fallback);
+  else
+    hipLaunchKernelGGL(k_sm_chunk_finish, dim3((G + 63) / 64), dim3(64), 0, c.stream, g0, G, s0, grp_off, status, Sh, Ph, PgJ, SgJ,
+                       grp_state, n_fallback);
   debug_sync(c.stream, "k_sm_chunk_finish");
 }
 void launch_sm_miller(LaunchCfg c, uint32_t g0, uint32_t G, const uint32_t* grp_msg, const uint8_t* grp_state, const G1J* PgJ, const G2A* H,
