@@ -388,6 +388,26 @@ GBV_HD void miller_loop(Slot* mem, int npairs) {
   conj12(mem + M_F);
 }
 
+// [|x|] Q (Q affine, not infinity) by the Miller loop's point steps alone (the lines they also
+// write to M_L are ignored): T ends at mem + M_PAIR in homogeneous projective coordinates
+// (x = X/Z, y = Y/Z).  The mixed addition is incomplete only for T = +-Q, i.e. for Q of order
+// dividing k -+ 1 with k < 2^64: a point of a small-order subgroup of E'(Fp2), never a hash output
+// or a curve point that has a component in the order-r subgroup.
+GBV_HD void mul_xabs_point(Slot* mem, const G2A& Q) {
+  miller_load_pair(mem, 0, G1A{fp_zero(), fp_zero()}, Q);
+  const uint16_t t = M_PAIR;
+  for (int i = 62; i >= 0; --i) {
+    run(G2_DBL_STEP, make_ws(mem, M_Z, t, (uint16_t)(t + 10), t, M_L));
+    if ((X_ABS >> i) & 1ull) run(G2_ADD_STEP, make_ws(mem, M_Z, t, (uint16_t)(t + 6), (uint16_t)(t + 10), t, M_L));
+  }
+}
+// the point left by mul_xabs_point as a Jacobian point (X Z, Y Z^2, Z); one lane
+GBV_HD G2J point_jac(const Slot* mem) {
+  const LSlot* b = GBV_LDS(mem + M_PAIR);
+  const Fp2 X{get(b + 0), get(b + 1)}, Y{get(b + 2), get(b + 3)}, Z{get(b + 4), get(b + 5)};
+  return G2J{fp2_mul(X, Z), fp2_mul(Y, fp2_sqr(Z)), Z};
+}
+
 // ---- final exponentiation: f^(3 (p^12 - 1)/r) == 1 ? -----------------------------------------
 // Workspace (slot offsets): F 0..11 (input, clobbered) | INV 12 | T 24 | A 36 | B 48 | C 60 |
 // TMP 72 | TMP2 84 | Z 96..223

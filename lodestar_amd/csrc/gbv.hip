@@ -88,6 +88,7 @@ struct gbv_sm_batch {
   G2A *H = nullptr, *S = nullptr;
   G2J *rS = nullptr, *SgJ = nullptr;
   Fp12* F = nullptr;
+  G2J* Hpre = nullptr;       // per message: Q0 + Q1 before the cofactor clearing (few-message hashing)
   Fp12* Fpair = nullptr;     // 2 per chunk: the two Miller values of a chunk's own check (k_sm_group_miller2)
   uint8_t* pair_ok = nullptr;
   Fp12* Fpart = nullptr;  // per 64-chunk block partials of a segment (reused segment after segment)
@@ -113,7 +114,7 @@ static void sm_free_work(gbv_sm_batch* b) {
   hipFree(b->n_fallback); hipFree(b->status); hipFree(b->grp_state); hipFree(b->valid);
   hipFree(b->H); hipFree(b->S); hipFree(b->SgJ); hipFree(b->rS); hipFree(b->rP); hipFree(b->PgJ);
   hipHostFree(b->valid_host); hipHostFree(b->nfb_host);
-  hipFree(b->F); hipFree(b->Fpair); hipFree(b->pair_ok); hipFree(b->seg_ok); hipHostFree(b->seg_ok_host);
+  hipFree(b->F); hipFree(b->Fpair); hipFree(b->pair_ok); hipFree(b->Hpre); hipFree(b->seg_ok); hipHostFree(b->seg_ok_host);
   hipFree(b->Fpart); hipFree(b->Spart); hipFree(b->has);
   hipFree(b->fb_runs); hipFree(b->fb_list); hipFree(b->fb_cnt);
   for (int k = 0; k < 2; ++k) {
@@ -124,7 +125,7 @@ static void sm_free_work(gbv_sm_batch* b) {
   }
   hipFree(b->msm_ent); hipFree(b->msm_total);
   b->n_fallback = nullptr; b->status = b->grp_state = b->valid = b->seg_ok = b->seg_ok_host = b->valid_host = nullptr;
-  b->H = b->S = nullptr; b->SgJ = b->rS = nullptr; b->rP = b->PgJ = nullptr; b->F = b->Fpart = b->Fpair = nullptr; b->pair_ok = nullptr; b->Spart = nullptr;
+  b->H = b->S = nullptr; b->SgJ = b->rS = nullptr; b->rP = b->PgJ = nullptr; b->F = b->Fpart = b->Fpair = nullptr; b->pair_ok = nullptr; b->Hpre = nullptr; b->Spart = nullptr;
   b->has = nullptr; b->fb_runs = nullptr; b->fb_list = b->fb_cnt = b->nfb_host = nullptr; b->msm_ent = nullptr; b->msm_total = nullptr;
   b->allocated = false;
 }
@@ -154,7 +155,7 @@ static int sm_reserve(gbv_ctx* c, gbv_sm_batch* b, size_t n, size_t G, size_t ca
   auto chk = [&](hipError_t x) { if (x != hipSuccess && e == hipSuccess) e = x; };
   chk(dalloc(&b->n_fallback, 1));
   chk(dalloc(&b->status, n)); chk(dalloc(&b->grp_state, G)); chk(dalloc(&b->valid, n));
-  chk(dalloc(&b->H, calls)); chk(dalloc(&b->S, n)); chk(dalloc(&b->rS, n)); chk(dalloc(&b->rP, n));
+  chk(dalloc(&b->H, calls)); chk(dalloc(&b->Hpre, calls)); chk(dalloc(&b->S, n)); chk(dalloc(&b->rS, n)); chk(dalloc(&b->rP, n));
   chk(dalloc(&b->PgJ, G)); chk(dalloc(&b->SgJ, G)); chk(dalloc(&b->F, G));
   chk(dalloc(&b->Fpair, 2 * G)); chk(dalloc(&b->pair_ok, 2 * G));
   // block partials: one region per segment parity (two segments' reductions can be in flight)
@@ -672,7 +673,7 @@ int gbv_sm_batch_submit(gbv_ctx* c, gbv_sm_batch* b) {
   HIP_CHECK(c, hipMemsetAsync(b->n_fallback, 0, 4, sh));
   HIP_CHECK(c, hipMemsetAsync(b->fb_cnt, 0, 8, sh));
   HIP_CHECK(c, hipEventRecord(ev[0], sh));
-  launch_hash_msgs(LaunchCfg{blocks_for(b->n_calls), TPB, sh}, b->msgs, (uint32_t)b->n_calls, b->H);
+  launch_hash_msgs(LaunchCfg{blocks_for(b->n_calls), TPB, sh}, b->msgs, (uint32_t)b->n_calls, b->H, b->Hpre);
   HIP_CHECK(c, hipEventRecord(ev[1], sh));
   for (size_t s = 0; s < S; ++s) {
     hipEvent_t* e = ev + 2 + EPS * s;

@@ -23,6 +23,15 @@ __global__ void GBV_KERNEL_ATTR k_hash_msgs_pair(const uint8_t* __restrict__ msg
   if (hash_to_g2_lane_pair(w, act, &h)) H[i] = h;
 }
 
+__global__ void GBV_KERNEL_ATTR k_hash_msgs_pre(const uint8_t* __restrict__ msgs32, uint32_t n, G2J* __restrict__ Qpre) {
+  uint32_t i = (blockIdx.x * blockDim.x + threadIdx.x) >> 1;
+  bool act = i < n;
+  uint32_t w[8] = {};
+  if (act) load_msg_words(w, msgs32 + 32ull * i);
+  G2J q;
+  if (hash_to_g2_lane_pair_pre(w, act, &q)) Qpre[i] = q;
+}
+
 __global__ void GBV_KERNEL_ATTR k_util_g2_out(uint32_t n, const G2A* __restrict__ H, uint8_t* __restrict__ out192) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -34,7 +43,14 @@ __global__ void GBV_KERNEL_ATTR k_util_g2_out(uint32_t n, const G2A* __restrict_
 }
 
 
-void launch_hash_msgs(LaunchCfg c, const uint8_t* msgs32, uint32_t n, G2A* H) {
+void launch_hash_msgs(LaunchCfg c, const uint8_t* msgs32, uint32_t n, G2A* H, G2J* Qpre) {
+  static const uint32_t coop_max = getenv("GBV_HASH_COOP_MAX") ? (uint32_t)atoi(getenv("GBV_HASH_COOP_MAX")) : 256;
+  if (Qpre && n <= coop_max) {  // latency: lane-pair maps, then the cofactor clearing one wave per message
+    hipLaunchKernelGGL(k_hash_msgs_pre, dim3((2 * n + 63) / 64), dim3(64), 0, c.stream, msgs32, n, Qpre);
+    debug_sync(c.stream, "k_hash_msgs_pre");
+    launch_hash_clear_coop(c.stream, n, Qpre, H);
+    return;
+  }
   if (n <= hash_pair_max())  // latency: lane pairs (grid sized here; c.blocks is for one lane per message)
     hipLaunchKernelGGL(k_hash_msgs_pair, dim3((2 * n + 63) / 64), dim3(64), 0, c.stream, msgs32, n, H);
   else

@@ -93,6 +93,78 @@ __global__ void GBV_KERNEL_ATTR k_sm_prepare(uint32_t base, uint32_t n, const ui
   }
 }
 
+// Latency form of k_sm_prepare<true> for segments of few sets (a lone gossip call): TWO waves per 64
+// sets (a 128-thread block).  Both decode the signatures; wave 0 runs the subgroup checks while
+// wave 1 forms r pk and r sig (the two longest chains of a set, side by side on two SIMDs instead of
+// one after the other -- two lanes of ONE wave would only take turns); wave 0's verdicts reach
+// wave 1 through LDS and decide, exactly as in k_sm_prepare, whether a set's terms count.  Same
+// r_i, statuses, 8-set segmented scan (wave 1, lane = set) and outputs as k_sm_prepare<true>.
+__global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(GBV_WAVES_PER_EU)))
+k_sm_prepare_split(uint32_t base, uint32_t n, const uint32_t* __restrict__ idx, const uint8_t* __restrict__ sig96,
+                   const uint32_t* __restrict__ set_grp, const G1A* __restrict__ table, const uint8_t* __restrict__ table_ok,
+                   uint32_t table_n, const uint4* __restrict__ comb, const uint8_t* __restrict__ comb_ok, Seed seed, uint32_t nonce,
+                   G2A* __restrict__ S_out, G2J* __restrict__ Sh_out, G1J* __restrict__ Ph_out, uint8_t* __restrict__ status) {
+  __shared__ uint8_t sub_ok[64];
+  const unsigned lane = threadIdx.x & 63u, role = threadIdx.x >> 6;
+  const uint32_t t = blockIdx.x * 64 + lane;
+  const bool act = t < n;
+  const uint32_t i = base + t;
+  const uint32_t key = act ? set_grp[i] : 0xffffffffu;
+  G2J rs = jac_infinity<Fp2>();
+  G1J rp = jac_infinity<Fp>();
+  G2A s;
+  uint8_t st = SET_OK;
+  bool dec_ok = false;
+  uint32_t k = 0;
+  if (act) {
+    k = idx[i];
+    if (k >= table_n || !table_ok[k]) st = SET_BAD_PK;
+    dec_ok = g2_decode(s, sig96 + 96ull * i, 96) == PT_OK;
+  }
+  if (role == 0) {
+    sub_ok[lane] = (uint8_t)(act && dec_ok && g2_in_subgroup(s));
+  } else if (act && dec_ok && st == SET_OK) {  // (discarded below when wave 0 rejects the point)
+    const uint64_t r = prf_scalar(seed, i, nonce);
+    if (comb && comb_ok[k]) {
+      rp = comb_mul(comb + (size_t)k * (COMB_ENTRIES * COMB_U4), (uint32_t)r, (uint32_t)(r >> 32));
+      if (!randomize_g2(s, r, &rs)) {
+        rs = g2_mul_u64(s, r);
+        rp = g1_mul_u64(table[k], r);
+      }
+    } else {
+      G1A pk = table[k];
+      if (!randomize_pair(pk, s, r, &rp, &rs)) {
+        rs = g2_mul_u64(s, r);
+        rp = g1_mul_u64(pk, r);
+      }
+    }
+  }
+  __syncthreads();
+  if (role == 0) return;
+  if (act && !sub_ok[lane]) st = SET_BAD_SIG;  // as k_sm_prepare: a bad signature outranks a bad key
+  if (st != SET_OK) {
+    rp = jac_infinity<Fp>();
+    rs = jac_infinity<Fp2>();
+  }
+  if (act) {
+    status[i] = st;
+    if (st == SET_OK) S_out[i] = s;
+  }
+  for (unsigned d = 1; d < SCAN_W; d <<= 1) {
+    G1J po = shfl_down_jac(rp, d);
+    uint32_t ko = __shfl_down(key, d, 64);
+    bool take = (lane & (SCAN_W - 1)) + d < SCAN_W && ko == key;
+    G2J so = shfl_down_jac(rs, d);
+    if (take) rs = g2_add(rs, so);
+    if (take) rp = jac_add(rp, po);
+  }
+  uint32_t kprev = __shfl_up(key, 1, 64);
+  if (act && ((lane & (SCAN_W - 1)) == 0 || kprev != key)) {
+    Sh_out[i] = rs;
+    Ph_out[i] = rp;
+  }
+}
+
 // The G2 half of k_sm_prepare for a segment whose fast check used the bucket MSM (k_msm.hip) and
 // FAILED (or holds a chunk bound for the per-set path): the failure path needs the per-set
 // r_i sig_i group sums (Sh) and the chunk sums S_g after all.  Same r_i (prf_scalar of the same seed/nonce/index), same 8-lane scan, so Sh/S_g are
@@ -425,7 +497,11 @@ void launch_sm_prepare(LaunchCfg c, uint32_t base, uint32_t n, const uint32_t* i
                        const Seed& seed, uint32_t nonce, G2A* S_out, G2J* Sh, G1J* Ph, uint8_t* status) {
   // Sh == nullptr: G1 terms only (the segment's G2 sum comes from the bucket MSM); comb == nullptr:
   // no comb tables (GBV_COMB=0 or not built), the ladder forms r pk
-  if (Sh)
+  static const uint32_t split_max = getenv("GBV_PREPARE_SPLIT_MAX") ? (uint32_t)atoi(getenv("GBV_PREPARE_SPLIT_MAX")) : 2048;
+  if (Sh && n <= split_max)  // latency: two waves per 64 sets
+    hipLaunchKernelGGL(k_sm_prepare_split, dim3((n + 63) / 64), dim3(128), 0, c.stream, base, n, idx, sig96, set_grp, table, table_ok, table_n,
+                       comb, comb_ok, seed, nonce, S_out, Sh, Ph, status);
+  else if (Sh)
     hipLaunchKernelGGL(k_sm_prepare<true>, dim3((n + 63) / 64), dim3(64), 0, c.stream, base, n, idx, sig96, set_grp, table, table_ok, table_n,
                        comb, comb_ok, seed, nonce, S_out, Sh, Ph, status);
   else

@@ -247,6 +247,71 @@ k_sm_group_fe(uint32_t g0, const uint8_t* __restrict__ seg_ok, const Fp12* __res
   }
 }
 
+// hash_to_G2's cofactor clearing for few messages, one wave per message (latency: a lone gossip
+// call hashes one message).  clear_cofactor_g2 (RFC 9380 G.3) with its two [|x|] scalar
+// multiplications run by the Miller loop's cooperative point steps (coop::mul_xabs_point: each
+// doubling two rounds of independent products instead of 16 dependent ones); lane 0 does the
+// psi maps, the five additions and the affine conversions.  Qpre = Q0 + Q1 (k_hash_msgs_pre).
+// A base at infinity (never, for a hash) takes the thread-serial clear_cofactor_g2 on lane 0.
+__device__ inline G2A g2_aff_out(const G2J& q) {
+  G2A out;
+  jac_to_aff(out, q);
+  return out;
+}
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
+k_hash_clear_coop(const G2J* __restrict__ Qpre, G2A* __restrict__ H) {
+  __shared__ coop::Slot ws[coop::MILLER_WS];
+  __shared__ Fp st[4];
+  __shared__ int ok;
+  const uint32_t m = blockIdx.x;
+  const unsigned lane = threadIdx.x;
+  coop::load_consts();
+  G2J p, t1, t3;  // lane 0's
+  if (lane == 0) {
+    p = Qpre[m];
+    G2A a;
+    ok = jac_to_aff(a, p) ? 1 : 0;
+    if (!ok) H[m] = g2_aff_out(clear_cofactor_g2(p));
+    st[0] = a.x.c0;
+    st[1] = a.x.c1;
+    st[2] = a.y.c0;
+    st[3] = a.y.c1;
+  }
+  coop::barrier();
+  if (!ok) return;
+  coop::mul_xabs_point(ws, G2A{Fp2{st[0], st[1]}, Fp2{st[2], st[3]}});
+  if (lane == 0) {
+    t1 = jac_neg(coop::point_jac(ws));             // [x] P
+    G2J t2 = g2_psi_jac(p);                        // psi(P)
+    t3 = g2_psi_jac(g2_psi_jac(jac_dbl(p)));       // psi^2(2P)
+    t3 = g2_add(t3, jac_neg(t2));
+    t2 = g2_add(t1, t2);
+    G2A a;
+    ok = jac_to_aff(a, t2) ? 1 : 0;
+    if (!ok) {  // t2 at infinity: [x] t2 is infinity too
+      t3 = g2_add(t3, jac_neg(t1));
+      H[m] = g2_aff_out(g2_add(t3, jac_neg(p)));
+    }
+    st[0] = a.x.c0;
+    st[1] = a.x.c1;
+    st[2] = a.y.c0;
+    st[3] = a.y.c1;
+  }
+  coop::barrier();
+  if (!ok) return;
+  coop::mul_xabs_point(ws, G2A{Fp2{st[0], st[1]}, Fp2{st[2], st[3]}});
+  if (lane == 0) {
+    const G2J t2 = jac_neg(coop::point_jac(ws));  // [x] t2
+    t3 = g2_add(t3, t2);
+    t3 = g2_add(t3, jac_neg(t1));
+    H[m] = g2_aff_out(g2_add(t3, jac_neg(p)));
+  }
+}
+void launch_hash_clear_coop(hipStream_t s, uint32_t n, const G2J* Qpre, G2A* H) {
+  hipLaunchKernelGGL(k_hash_clear_coop, dim3(n), dim3(64), 0, s, Qpre, H);
+  debug_sync(s, "k_hash_clear_coop");
+}
+
 // e(P, Q) * e(-g1, S) == 1 by one wave (S = infinity drops the second pair).  Arguments must be
 // wave-uniform (the callers stage them in LDS).
 __device__ inline bool coop_pair_check(coop::Slot* ws, const G1A& P, const G2A& Q, bool s_inf, const G2A& S) {

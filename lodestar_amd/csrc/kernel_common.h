@@ -100,6 +100,22 @@ __device__ inline bool hash_to_g2_lane_pair(const uint32_t w[8], bool active, G2
   return true;
 }
 
+// The same lane pairs, stopping before the cofactor clearing: Q0 + Q1 (Jacobian) on the even lane
+// (k_hash_clear_coop then clears the cofactor with one wave per message).
+__device__ inline bool hash_to_g2_lane_pair_pre(const uint32_t w[8], bool active, G2J* out) {
+  const int lane = (int)threadIdx.x, half = lane & 1;
+  G2J q = jac_infinity<Fp2>();
+  if (active) q = hash_map_iso(hash_to_field_fp2(w, half));
+  Fp* f = (Fp*)&q;
+  G2J o;
+  Fp* g = (Fp*)&o;
+#pragma unroll
+  for (int i = 0; i < 6; ++i) g[i] = shfl_fp(f[i], lane | 1);
+  if (!active || half) return false;
+  *out = jac_add(q, o);
+  return true;
+}
+
 __device__ inline void load_msg_words(uint32_t w[8], const uint8_t* m) {
   for (int i = 0; i < 8; ++i)
     w[i] = ((uint32_t)m[4 * i] << 24) | ((uint32_t)m[4 * i + 1] << 16) | ((uint32_t)m[4 * i + 2] << 8) | m[4 * i + 3];

@@ -9,7 +9,9 @@ namespace gbv {
 struct Seed;
 struct LaunchCfg { unsigned blocks; unsigned threads; hipStream_t stream; };
 
-void launch_hash_msgs(LaunchCfg c, const uint8_t* msgs32, uint32_t n, G2A* H);
+// Qpre (optional, n entries): scratch of the latency form for few messages (k_hash_clear_coop)
+void launch_hash_msgs(LaunchCfg c, const uint8_t* msgs32, uint32_t n, G2A* H, G2J* Qpre = nullptr);
+void launch_hash_clear_coop(hipStream_t s, uint32_t n, const G2J* Qpre, G2A* H);
 void launch_util_g2_out(LaunchCfg c, uint32_t n, const G2A* H, uint8_t* out192);
 
 void launch_sm_prepare(LaunchCfg c, uint32_t base, uint32_t n, const uint32_t* idx, const uint8_t* sig96, const uint32_t* set_grp,

@@ -134,6 +134,30 @@ int ht_coop_pairing(uint8_t* out, const uint8_t* p96, const uint8_t* q192, int n
   for (int i = 0; i < 12; ++i) store_canon(out + 48 * i, coop::get(fe + coop::E_C + i));
   return ok;
 }
+// clear_cofactor_g2 with both [|x|] multiplications by the cooperative point steps
+// (coop::mul_xabs_point, as k_hash_clear_coop runs it); in: affine point of E2, out: affine
+void ht_coop_clear_cofactor(uint8_t* out, const uint8_t* xy) {
+  coop::load_consts();
+  std::vector<coop::Slot> mem(coop::MILLER_WS);
+  const G2A a{load_fp2(xy), load_fp2(xy + 96)};
+  const G2J p = jac_from_aff(a);
+  coop::mul_xabs_point(mem.data(), a);
+  const G2J t1 = jac_neg(coop::point_jac(mem.data()));
+  G2J t2 = g2_psi_jac(p);
+  G2J t3 = g2_psi_jac(g2_psi_jac(jac_dbl(p)));
+  t3 = jac_add(t3, jac_neg(t2));
+  t2 = jac_add(t1, t2);
+  G2A b;
+  jac_to_aff(b, t2);
+  coop::mul_xabs_point(mem.data(), b);
+  t2 = jac_neg(coop::point_jac(mem.data()));
+  t3 = jac_add(t3, t2);
+  t3 = jac_add(t3, jac_neg(t1));
+  G2A o;
+  jac_to_aff(o, jac_add(t3, jac_neg(p)));
+  store_fp2(out, o.x);
+  store_fp2(out + 96, o.y);
+}
 // [r] P, [r] Q for the batch scalar r = a - b x^2 of the 64-bit digit word r64 (curve.h)
 int ht_randomize(uint8_t* outp, uint8_t* outq, const uint8_t* p96, const uint8_t* q192, uint64_t r64) {
   G1A P{load_mont(p96), load_mont(p96 + 48)};

@@ -308,6 +308,21 @@ def test_g2_xabs_lazy_chain(lib):
         assert Z1 != (0, 0)
 
 
+def test_coop_clear_cofactor(lib):
+    """hash_to_G2's cofactor clearing with both [|x|] multiplications by the cooperative Miller-loop
+    point steps (coop.h mul_xabs_point, k_hash_clear_coop) equals the oracle's clear_cofactor_g2 on
+    points of E2 outside G2 (iso_map of SSWU outputs, the hash's own inputs)."""
+    rnd = random.Random(21)
+    lib.ht_coop_clear_cofactor.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+    for _ in range(4):
+        q = o.iso_map_g2(o.map_to_curve_sswu_g2((rnd.randrange(o.P), rnd.randrange(o.P))))
+        out = buf(192)
+        lib.ht_coop_clear_cofactor(out, be(q[0][0]) + be(q[0][1]) + be(q[1][0]) + be(q[1][1]))
+        got = [int.from_bytes(out.raw[48 * i:48 * i + 48], "big") for i in range(4)]
+        want = o.clear_cofactor_g2(q)
+        assert ((got[0], got[1]), (got[2], got[3])) == (want[0], want[1])
+
+
 def test_lazy_fp2_limb_bounds(lib):
     """l2_mul / l2_sqr at the limb and value bounds f28_lazy.h allows: every limb 2^28 - 1 and
     values up to 16 p (mul) / the K of the square, against exact Montgomery arithmetic."""
