@@ -47,6 +47,7 @@ struct gbv_vs_batch {
   G2J* rS = nullptr;
   uint8_t* status = nullptr;
   Fp12* F = nullptr;
+  G2J* Hpre = nullptr;        // per set: Q0 + Q1 before the cofactor clearing (small passes)
   Fp12* Fs = nullptr;         // per chunk: Miller value of (-g1, sum r_i sig_i) (small passes, k_vs_miller_coop)
   uint8_t* fs_flag = nullptr;
   uint8_t* chunk_valid = nullptr;
@@ -65,8 +66,8 @@ struct gbv_vs_batch {
 static void vs_free_work(gbv_vs_batch* b) {
   // teardown: a failing free has nothing left to report to
   (void)hipFree(b->pk); (void)hipFree(b->pk_st); (void)hipFree(b->H); (void)hipFree(b->rP); (void)hipFree(b->rS);
-  (void)hipFree(b->status); (void)hipFree(b->F); (void)hipFree(b->Fs); (void)hipFree(b->fs_flag); (void)hipFree(b->chunk_valid); (void)hipHostFree(b->chunk_valid_host);
-  b->pk = nullptr; b->pk_st = nullptr; b->H = nullptr; b->rP = nullptr; b->rS = nullptr; b->status = nullptr; b->F = nullptr; b->Fs = nullptr; b->fs_flag = nullptr;
+  (void)hipFree(b->status); (void)hipFree(b->F); (void)hipFree(b->Fs); (void)hipFree(b->Hpre); (void)hipFree(b->fs_flag); (void)hipFree(b->chunk_valid); (void)hipHostFree(b->chunk_valid_host);
+  b->pk = nullptr; b->pk_st = nullptr; b->H = nullptr; b->rP = nullptr; b->rS = nullptr; b->status = nullptr; b->F = nullptr; b->Fs = nullptr; b->fs_flag = nullptr; b->Hpre = nullptr;
   b->chunk_valid = nullptr; b->chunk_valid_host = nullptr;
   b->allocated = false;
 }
@@ -95,7 +96,7 @@ static int vs_reserve(gbv_ctx* c, gbv_vs_batch* b, size_t n, size_t C) {
   auto chk = [&](hipError_t x) { if (x != hipSuccess && e == hipSuccess) e = x; };
   chk(dalloc(&b->pk, n)); chk(dalloc(&b->pk_st, n)); chk(dalloc(&b->H, n)); chk(dalloc(&b->rP, n)); chk(dalloc(&b->rS, n));
   chk(dalloc(&b->status, n)); chk(dalloc(&b->F, n)); chk(dalloc(&b->chunk_valid, C));
-  chk(dalloc(&b->Fs, C)); chk(dalloc(&b->fs_flag, C));
+  chk(dalloc(&b->Fs, C)); chk(dalloc(&b->fs_flag, C)); chk(dalloc(&b->Hpre, n));
   chk(hipHostMalloc((void**)&b->chunk_valid_host, std::max<size_t>(C, 1), hipHostMallocDefault));
   for (auto& ev : b->ev)
     if (!ev) chk(hipEventCreate(&ev));
@@ -234,6 +235,11 @@ static bool vs_fs_on() {  // GBV_VS_FS=0: the chunk check forms the (-g1, sum) M
 
 // Small passes, and passes of few chunks (a range-sync segment of blocks: 2 chunks per block), whose
 // chunk checks are latency-bound; GBV_VS_FS_MAXC sets the chunk bound (A/B).
+static bool vs_split_on() {  // GBV_VS_SPLIT=0: hash and signature roles in one k_vs_hash_sig launch (A/B)
+  static const bool on = !(getenv("GBV_VS_SPLIT") && atoi(getenv("GBV_VS_SPLIT")) == 0);
+  return on;
+}
+
 static bool vs_fs_small(const gbv_vs_batch* b) {
   static const size_t maxc = getenv("GBV_VS_FS_MAXC") ? (size_t)atol(getenv("GBV_VS_FS_MAXC")) : 256;
   return vs_fs_on() && (b->n <= VS_COOP_MILLER_MAX || b->C <= maxc);
@@ -251,8 +257,12 @@ static int vs_enqueue_sets(gbv_ctx* c, gbv_vs_batch* b, hipStream_t m, bool with
   HIP_CHECK(c, hipEventRecord(b->ev[0], s));
   if (b->n_agg) launch_vs_agg(LaunchCfg{(unsigned)b->n_agg, 64, s}, b->agg_list, b->set_off, b->arena, c->table, c->table_ok, b->pk, b->pk_st);
   HIP_CHECK(c, hipEventRecord(b->ev[1], s));
+  // small passes (latency): the hash on stream m (lane-pair maps, cooperative cofactor clearing)
+  // beside the signature checks and the randomisation, which run as two block roles on stream A
+  const bool split = with_fs && m != s && vs_fs_small(b) && vs_split_on();
+  if (split) launch_hash_msgs(LaunchCfg{blocks_for(b->n), TPB, m}, b->msgs, (uint32_t)b->n, b->H, b->Hpre);
   launch_vs_hash_sig(s, (uint32_t)b->n, b->msgs, b->set_off, b->arena, b->raw_flag, b->raw_pk, b->sig, b->sig_stride, b->siglen, c->table,
-                     c->table_ok, b->pk, b->pk_st, seed, nonce, b->H, b->rP, b->rS, b->status);
+                     c->table_ok, b->pk, b->pk_st, seed, nonce, b->H, b->rP, b->rS, b->status, split);
   HIP_CHECK(c, hipEventRecord(b->ev[2], s));
   if (m != s) HIP_CHECK(c, hipStreamWaitEvent(m, b->ev[2], 0));
   HIP_CHECK(c, hipEventRecord(b->ev[3], m));

@@ -65,7 +65,12 @@ k_vs_agg(uint32_t n_agg, const uint32_t* __restrict__ agg_list, const uint32_t* 
 // maybeBatch.ts:23), fetch the pubkey (table slot, the k_vs_agg result, or a raw key validated like
 // PublicKey.fromBytes(pk, true), blsToExecutionChange.ts:31) and form r_i pk_i and r_i sig_i.
 // The two roles are independent, so hashing (the longest per-set chain) overlaps the rest.
-__global__ void GBV_KERNEL_ATTR k_vs_hash_sig(uint32_t n, uint32_t nb, uint32_t pair, const uint8_t* __restrict__ msgs32,
+//
+// split (small passes, the hash then runs on its own stream): the signature role is itself two
+// block roles side by side -- blocks [nb, nb + nsig) decode and group-check (status), blocks
+// [nb + nsig, nb + 2 nsig) decode and randomise (rP, rS, written whatever the checks say: every
+// consumer reads them only for sets whose status is SET_OK).
+__global__ void GBV_KERNEL_ATTR k_vs_hash_sig(uint32_t n, uint32_t nb, uint32_t pair, uint32_t split, const uint8_t* __restrict__ msgs32,
                                               const uint32_t* __restrict__ set_off, const uint32_t* __restrict__ arena,
                                               const uint8_t* __restrict__ raw_flag, const uint8_t* __restrict__ raw_pk48,
                                               const uint8_t* __restrict__ sig, uint32_t sig_stride, const uint32_t* __restrict__ sig_len,
@@ -90,14 +95,18 @@ __global__ void GBV_KERNEL_ATTR k_vs_hash_sig(uint32_t n, uint32_t nb, uint32_t 
     H[i] = hash_to_g2(w);
     return;
   }
-  uint32_t i = (blockIdx.x - nb) * 64 + threadIdx.x;
+  const uint32_t nsig = (n + 63) / 64;
+  uint32_t blk = blockIdx.x - nb;
+  const bool rand_only = split && blk >= nsig, check_only = split && blk < nsig;
+  if (rand_only) blk -= nsig;
+  uint32_t i = blk * 64 + threadIdx.x;
   if (i >= n) return;
   uint8_t st = SET_OK;
   G1J pk;
   if (raw_flag[i]) {
     G1A a;
     uint8_t ds = g1_decompress(a, raw_pk48 + 48ull * i);
-    if (ds != PT_OK || !g1_in_subgroup(a)) st = SET_BAD_PK;
+    if (ds != PT_OK || (!rand_only && !g1_in_subgroup(a))) st = SET_BAD_PK;
     pk = jac_from_aff(a);
   } else {
     uint32_t b = set_off[i], e = set_off[i + 1];
@@ -114,9 +123,9 @@ __global__ void GBV_KERNEL_ATTR k_vs_hash_sig(uint32_t n, uint32_t nb, uint32_t 
   }
   G2A s;
   uint8_t ds = g2_decode(s, sig + (size_t)sig_stride * i, sig_len[i]);
-  if (ds != PT_OK || !g2_in_subgroup(s)) st = SET_BAD_SIG;
-  status[i] = st;
-  if (st != SET_OK) return;
+  if (ds != PT_OK || (!rand_only && !g2_in_subgroup(s))) st = SET_BAD_SIG;
+  if (!rand_only) status[i] = st;
+  if (check_only || st != SET_OK) return;
   uint64_t r = prf_scalar(seed, i, nonce);
   G1J rp;
   G2J rs;
@@ -217,11 +226,12 @@ void launch_vs_agg(LaunchCfg c, const uint32_t* agg_list, const uint32_t* set_of
 void launch_vs_hash_sig(hipStream_t s, uint32_t n, const uint8_t* msgs32, const uint32_t* set_off, const uint32_t* arena,
                         const uint8_t* raw_flag, const uint8_t* raw_pk48, const uint8_t* sig, uint32_t sig_stride, const uint32_t* sig_len,
                         const G1A* table, const uint8_t* table_ok, const G1J* pk_agg, const uint8_t* pk_st, const Seed& seed,
-                        uint32_t nonce, G2A* H, G1J* rP, G2J* rS, uint8_t* status) {
+                        uint32_t nonce, G2A* H, G1J* rP, G2J* rS, uint8_t* status, bool split) {
   const uint32_t pair = n <= hash_pair_max() ? 1u : 0u;
-  const uint32_t nb = pair ? (2 * n + 63) / 64 : (n + 63) / 64, nsig = (n + 63) / 64;
-  hipLaunchKernelGGL(k_vs_hash_sig, dim3(nb + nsig), dim3(64), 0, s, n, nb, pair, msgs32, set_off, arena, raw_flag, raw_pk48, sig, sig_stride,
-                     sig_len, table, table_ok, pk_agg, pk_st, seed, nonce, H, rP, rS, status);
+  const uint32_t nsig = (n + 63) / 64;
+  const uint32_t nb = split ? 0u : pair ? (2 * n + 63) / 64 : (n + 63) / 64;  // split: the caller hashes
+  hipLaunchKernelGGL(k_vs_hash_sig, dim3(nb + (split ? 2 : 1) * nsig), dim3(64), 0, s, n, nb, pair, split ? 1u : 0u, msgs32, set_off,
+                     arena, raw_flag, raw_pk48, sig, sig_stride, sig_len, table, table_ok, pk_agg, pk_st, seed, nonce, H, rP, rS, status);
   debug_sync(s, "k_vs_hash_sig");
 }
 
