@@ -88,6 +88,7 @@ struct gbv_sm_batch {
   G2A *H = nullptr, *S = nullptr;
   G2J *rS = nullptr, *SgJ = nullptr;
   Fp12* F = nullptr;
+  Fp12* Ffb = nullptr;       // 2 * FB_COOP_MAX: the two Miller values of each few-item per-set check
   G2J* Hpre = nullptr;       // per message: Q0 + Q1 before the cofactor clearing (few-message hashing)
   Fp12* Fpair = nullptr;     // 2 per chunk: the two Miller values of a chunk's own check (k_sm_group_miller2)
   uint8_t* pair_ok = nullptr;
@@ -114,7 +115,7 @@ static void sm_free_work(gbv_sm_batch* b) {
   hipFree(b->n_fallback); hipFree(b->status); hipFree(b->grp_state); hipFree(b->valid);
   hipFree(b->H); hipFree(b->S); hipFree(b->SgJ); hipFree(b->rS); hipFree(b->rP); hipFree(b->PgJ);
   hipHostFree(b->valid_host); hipHostFree(b->nfb_host);
-  hipFree(b->F); hipFree(b->Fpair); hipFree(b->pair_ok); hipFree(b->Hpre); hipFree(b->seg_ok); hipHostFree(b->seg_ok_host);
+  hipFree(b->F); hipFree(b->Fpair); hipFree(b->pair_ok); hipFree(b->Hpre); hipFree(b->Ffb); hipFree(b->seg_ok); hipHostFree(b->seg_ok_host);
   hipFree(b->Fpart); hipFree(b->Spart); hipFree(b->has);
   hipFree(b->fb_runs); hipFree(b->fb_list); hipFree(b->fb_cnt);
   for (int k = 0; k < 2; ++k) {
@@ -125,7 +126,7 @@ static void sm_free_work(gbv_sm_batch* b) {
   }
   hipFree(b->msm_ent); hipFree(b->msm_total);
   b->n_fallback = nullptr; b->status = b->grp_state = b->valid = b->seg_ok = b->seg_ok_host = b->valid_host = nullptr;
-  b->H = b->S = nullptr; b->SgJ = b->rS = nullptr; b->rP = b->PgJ = nullptr; b->F = b->Fpart = b->Fpair = nullptr; b->pair_ok = nullptr; b->Hpre = nullptr; b->Spart = nullptr;
+  b->H = b->S = nullptr; b->SgJ = b->rS = nullptr; b->rP = b->PgJ = nullptr; b->F = b->Fpart = b->Fpair = nullptr; b->pair_ok = nullptr; b->Hpre = nullptr; b->Ffb = nullptr; b->Spart = nullptr;
   b->has = nullptr; b->fb_runs = nullptr; b->fb_list = b->fb_cnt = b->nfb_host = nullptr; b->msm_ent = nullptr; b->msm_total = nullptr;
   b->allocated = false;
 }
@@ -157,7 +158,7 @@ static int sm_reserve(gbv_ctx* c, gbv_sm_batch* b, size_t n, size_t G, size_t ca
   chk(dalloc(&b->status, n)); chk(dalloc(&b->grp_state, G)); chk(dalloc(&b->valid, n));
   chk(dalloc(&b->H, calls)); chk(dalloc(&b->Hpre, calls)); chk(dalloc(&b->S, n)); chk(dalloc(&b->rS, n)); chk(dalloc(&b->rP, n));
   chk(dalloc(&b->PgJ, G)); chk(dalloc(&b->SgJ, G)); chk(dalloc(&b->F, G));
-  chk(dalloc(&b->Fpair, 2 * G)); chk(dalloc(&b->pair_ok, 2 * G));
+  chk(dalloc(&b->Fpair, 2 * G)); chk(dalloc(&b->pair_ok, 2 * G)); chk(dalloc(&b->Ffb, 2 * FB_COOP_MAX));
   // block partials: one region per segment parity (two segments' reductions can be in flight)
   b->part_stride = seg_reduce_scratch(G);
   chk(dalloc(&b->Fpart, 2 * b->part_stride)); chk(dalloc(&b->Spart, 2 * b->part_stride)); chk(dalloc(&b->has, 2 * b->part_stride));
@@ -763,7 +764,7 @@ int gbv_sm_batch_submit(gbv_ctx* c, gbv_sm_batch* b) {
   launch_sm_fb_blocks(LaunchCfg{FB_GRID, 64, sf}, b->fb_runs, b->fb_cnt, (uint32_t)b->fb_cap, b->status, b->grp_msg, b->rS, b->rP, b->H,
                       b->valid, b->fb_list, b->fb_cnt + 1);
   launch_sm_fb_sets_coop(LaunchCfg{0, 64, sf}, b->fb_list, b->fb_cnt + 1, b->set_grp, b->grp_msg, b->idx, c->table, b->S, b->H,
-                         b->valid);
+                         b->valid, b->Ffb);
   launch_sm_fb_sets(LaunchCfg{FB_GRID, 64, sf}, b->fb_list, b->fb_cnt + 1, b->set_grp, b->grp_msg, b->idx, c->table, b->S, b->H,
                     b->valid);
   HIP_CHECK(c, hipEventRecord(ep[1], sf));

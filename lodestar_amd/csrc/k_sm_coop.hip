@@ -392,6 +392,49 @@ k_sm_fb_sets_coop(const uint32_t* __restrict__ set_list, const uint32_t* __restr
   }
 }
 
+// k_sm_fb_sets_coop with each check's two Miller loops on two waves (block (k, j): pair j of item
+// k, both points affine and finite as there), then product + final exponentiation by one wave.
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
+k_sm_fb_sets_miller2(const uint32_t* __restrict__ set_list, const uint32_t* __restrict__ n_list, const uint32_t* __restrict__ set_grp,
+                     const uint32_t* __restrict__ grp_msg, const uint32_t* __restrict__ idx, const G1A* __restrict__ table,
+                     const G2A* __restrict__ S, const G2A* __restrict__ H, Fp12* __restrict__ Fpair) {
+  __shared__ coop::Slot ws[coop::MILLER_WS];
+  const uint32_t cnt = *n_list;
+  if (cnt > FB_COOP_MAX) return;
+  if (blockIdx.x < cnt) coop::load_consts();
+  const uint32_t j = blockIdx.y;
+  for (uint32_t k = blockIdx.x; k < cnt; k += gridDim.x) {
+    const uint32_t i = set_list[k];
+    if (j == 0)
+      coop::miller_load_pair(ws, 0, table[idx[i]], H[grp_msg[set_grp[i]]]);
+    else
+      coop::miller_load_pair(ws, 0, g1_neg_generator(), S[i]);
+    coop::miller_loop(ws, 1);
+    if (threadIdx.x < 12) ((Fp*)&Fpair[2 * k + j])[threadIdx.x] = coop::get(ws + coop::M_F + threadIdx.x);
+    coop::barrier();
+  }
+}
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
+k_sm_fb_sets_fe(const uint32_t* __restrict__ set_list, const uint32_t* __restrict__ n_list, const Fp12* __restrict__ Fpair,
+                uint8_t* __restrict__ valid) {
+  __shared__ coop::Slot ws[coop::FINAL_EXP_WS];
+  const uint32_t cnt = *n_list;
+  if (cnt > FB_COOP_MAX) return;
+  if (blockIdx.x < cnt) coop::load_consts();
+  const unsigned lane = threadIdx.x;
+  for (uint32_t k = blockIdx.x; k < cnt; k += gridDim.x) {
+    if (lane < 12) {
+      coop::put(ws + coop::E_F + lane, ((const Fp*)&Fpair[2 * k])[lane]);
+      coop::put(ws + coop::E_TMP + lane, ((const Fp*)&Fpair[2 * k + 1])[lane]);
+    }
+    coop::barrier();
+    coop::mul12(ws, coop::E_Z, coop::E_F, coop::E_TMP, coop::E_F);
+    const bool ok = coop::final_exp_is_one(ws);
+    if (lane == 0) valid[set_list[k]] = ok ? 1 : 0;
+    coop::barrier();
+  }
+}
+
 void launch_sm_fb_blocks_coop(LaunchCfg c, const uint4* runs, const uint32_t* n_runs, uint32_t cap, const uint8_t* status,
                               const uint32_t* grp_msg, const G2J* Sh, const G1J* Ph, const G2A* H, uint8_t* valid, uint32_t* set_list,
                               uint32_t* n_list) {
@@ -400,7 +443,16 @@ void launch_sm_fb_blocks_coop(LaunchCfg c, const uint4* runs, const uint32_t* n_
   debug_sync(c.stream, "k_sm_fb_blocks_coop");
 }
 void launch_sm_fb_sets_coop(LaunchCfg c, const uint32_t* set_list, const uint32_t* n_list, const uint32_t* set_grp, const uint32_t* grp_msg,
-                            const uint32_t* idx, const G1A* table, const G2A* S, const G2A* H, uint8_t* valid) {
+                            const uint32_t* idx, const G1A* table, const G2A* S, const G2A* H, uint8_t* valid, Fp12* Fpair) {
+  static const bool one_wave = getenv("GBV_GROUP_PAIRING_1W") && atoi(getenv("GBV_GROUP_PAIRING_1W")) != 0;
+  if (Fpair && !one_wave) {  // 2 * FB_COOP_MAX Fp12 of scratch
+    hipLaunchKernelGGL(k_sm_fb_sets_miller2, dim3(FB_COOP_MAX, 2), dim3(64), 0, c.stream, set_list, n_list, set_grp, grp_msg, idx, table, S, H,
+                       Fpair);
+    debug_sync(c.stream, "k_sm_fb_sets_miller2");
+    hipLaunchKernelGGL(k_sm_fb_sets_fe, dim3(FB_COOP_MAX), dim3(64), 0, c.stream, set_list, n_list, Fpair, valid);
+    debug_sync(c.stream, "k_sm_fb_sets_fe");
+    return;
+  }
   hipLaunchKernelGGL(k_sm_fb_sets_coop, dim3(FB_COOP_MAX), dim3(64), 0, c.stream, set_list, n_list, set_grp, grp_msg, idx, table, S, H,
                      valid);
   debug_sync(c.stream, "k_sm_fb_sets_coop");

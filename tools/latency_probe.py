@@ -25,6 +25,17 @@ for rep in range(12):
     kms, cnt = v.last_kernel_ms()
     print("call %.2f ms  kernels %s  valid %d" % ((t1 - t0) * 1e3, dict(zip(bench.KERNELS, [round(float(x), 2) for x in kms])),
                                                   sum(sum(r) for r in res)), flush=True)
+# the same lone call with one invalid set (set 5 carries set 6's signature): chunk check fails, then
+# the run checks and the per-set checks (the few-item cooperative failure path)
+bad = [(calls[0][0][i][0], calls[0][0][6][1] if i == 5 else calls[0][0][i][1]) for i in range(n)]
+for rep in range(6):
+    t0 = time.perf_counter()
+    res = v.verify_same_message_multi_sync([(bad, calls[0][1])])
+    t1 = time.perf_counter()
+    kms, cnt = v.last_kernel_ms()
+    assert list(res[0]) == [i != 5 for i in range(n)], res
+    print("bad call %.2f ms  kernels %s  valid %d" % ((t1 - t0) * 1e3, dict(zip(bench.KERNELS, [round(float(x), 2) for x in kms])),
+                                                      sum(sum(r) for r in res)), flush=True)
 # C1: one verifySignatureSets call of 128 distinct-message single-pubkey sets
 rng = np.random.Generator(np.random.PCG64(0xC1))
 sets = bench._single_sets(v, sks, 128, b"gbv-c1", rng)
