@@ -81,24 +81,38 @@ ALG_BYTES_PER_SET = 4 + 96 + 4 + 128 + 1 + 1 + 256 + round((1 / 8 + 1 / 80) * (3
 ALG_BYTES_PER_SET_COMB = ALG_BYTES_PER_SET - 128 + 8 * 96 + 1
 # k_vs_agg gather: per member a 4-byte index + the 128-byte affine table record + its 1-byte flag
 AGG_BYTES_PER_MEMBER = 4 + 128 + 1
+# host-counted (tests/native/hosttest.cpp ht_count_op): mixed G1 addition, Fp12 product, Jacobian G2
+# addition, final exponentiation
+FME_G1_MADD = 11
+FME_FP12_MUL = 54
+FME_G2_ADD = 59
+FME_FINAL_EXP = 7709
+# verifySignatureSets kernels: algorithmic bytes per set (Fp in 64-byte slots: G1J 192, G2A 256,
+# G2J 384, Fp12 768).  hash_sig reads msg 32 + sig 96 + set_off 8 + index 4 + table record 128 + flag 1
+# and writes H 256 + rP 192 + rS 384 + status 1; miller reads rP 192 + H 256 + status 1, writes F 768.
+VS_ALG_BYTES = {"hash_sig": 32 + 96 + 8 + 4 + 128 + 1 + 256 + 192 + 384 + 1, "miller": 192 + 256 + 1 + 768}
 
 
-def pmc_evidence(units_per_launch, kernel="k_sm_prepare<false>", alg_bytes=ALG_BYTES_PER_SET):
-    """HBM traffic per launch and VALU issue utilisation of k_sm_prepare from the committed
-    rocprofv3 --pmc summary (separate passes; FETCH_SIZE doubled per the gfx950 calibration in the
-    MI355X guide: it counts 64 B per 128-B request; rocprofv3 reports kilobytes)."""
+def pmc_evidence(units_per_launch, kernel="k_sm_prepare<false>", alg_bytes=ALG_BYTES_PER_SET, threads_per_unit=1, exact=False):
+    """HBM traffic per launch and VALU issue utilisation of a kernel (default k_sm_prepare) from the
+    committed rocprofv3 --pmc summary (separate passes; FETCH_SIZE doubled per the gfx950 calibration
+    in the MI355X guide: it counts 64 B per 128-B request; rocprofv3 reports kilobytes).
+    threads_per_unit: lanes per unit of work (2 for the lane-pair Miller kernel); exact: no fallback
+    to k_sm_prepare when the summary lacks the kernel."""
     try:
         summary = json.load(open(PMC_SUMMARY))
-        d = summary.get(kernel) or summary["k_sm_prepare"]
+        d = summary.get(kernel) or (None if exact else summary["k_sm_prepare"])
     except (OSError, KeyError, ValueError):
         return None, None
-    per_set = (2 * d["FETCH_SIZE"] + d["WRITE_SIZE"]) * 1024.0 / d["grid_size"]
-    valu = d["SQ_INSTS_VALU"] / (d["duration_ms"] * 1e-3 * PEAK_VALU_WAVE_INSTR_PER_S)
+    if d is None or "FETCH_SIZE" not in d or "WRITE_SIZE" not in d:
+        return None, None
+    per_set = (2 * d["FETCH_SIZE"] + d["WRITE_SIZE"]) * 1024.0 * threads_per_unit / d["grid_size"]
+    valu = d["SQ_INSTS_VALU"] / (d["duration_ms"] * 1e-3 * PEAK_VALU_WAVE_INSTR_PER_S) if "SQ_INSTS_VALU" in d else None
     ev = {"source": os.path.relpath(PMC_SUMMARY, ROOT), "kernel": kernel if kernel in summary else "k_sm_prepare",
-          "pmc_grid_sets": int(d["grid_size"]),
-          "hbm_bytes_per_set": round(per_set, 1), "algorithmic_bytes_per_set": alg_bytes, "valu_wave_instr_per_set": round(d["SQ_INSTS_VALU"] / d["SQ_WAVES"]),
-          "valu_issue_utilisation": round(valu, 4),
-          "valu_lane_utilisation": round(d["SQ_THREAD_CYCLES_VALU"] / (64.0 * d["SQ_ACTIVE_INST_VALU"]), 4)}
+          "pmc_grid_sets": int(d["grid_size"] // threads_per_unit),
+          "hbm_bytes_per_set": round(per_set, 1), "algorithmic_bytes_per_set": alg_bytes, "valu_wave_instr_per_set": round(d["SQ_INSTS_VALU"] / d["SQ_WAVES"]) if "SQ_WAVES" in d else None,
+          "valu_issue_utilisation": None if valu is None else round(valu, 4),
+          "valu_lane_utilisation": round(d["SQ_THREAD_CYCLES_VALU"] / (64.0 * d["SQ_ACTIVE_INST_VALU"]), 4) if "SQ_ACTIVE_INST_VALU" in d else None}
     return per_set * units_per_launch, ev
 
 
@@ -249,16 +263,44 @@ def api_path_rate(v, call_off, idx, sigs, msgs, n_sets=1 << 18):
 
 
 # ---- verifySignatureSets configs (C1, C3, C4) ------------------------------------------------------
-def _vs_roofline(v, n_sets, ms, agg_members=0):
-    hs = ms[1]
-    achieved = n_sets * W_VS_HASH_SIG * MAC_PER_FME / (hs * 1e-3) / 1e12 if hs > 0 else 0.0
-    out = {"bound": "valu-int", "kernel": "k_vs_hash_sig", "achieved": round(achieved, 4), "peak": PEAK_MAC_PER_S / 1e12,
-           "unit": "T u32-MAC/s", "frac": round(achieved * 1e12 / PEAK_MAC_PER_S, 5), "traffic": None,
-           "work_per_unit_fme": W_VS_HASH_SIG, "units_per_launch": n_sets, "avg_launch_ms": round(hs, 3),
-           "kernel_ms_per_pass": {k: round(float(x), 3) for k, x in zip(VS_KERNELS, ms)},
+# device kernel name of each verifySignatureSets stage (the larger-pass forms) and its PMC key
+VS_KERNEL_NAMES = {"agg": "k_vs_agg", "hash_sig": "k_vs_hash_sig", "miller": "k_vs_miller_pair", "chunk_check": "k_vs_chunk_coop"}
+
+
+def _vs_roofline(v, n_sets, ms, agg_members=0, n_chunks=0):
+    """Roofline of the LONGEST kernel of a verifySignatureSets pass (ms: gbv_vs_last_kernel_ms, HIP
+    events on the stream each kernel runs on), with its algorithmic work per pass:
+      agg          11 FME per gathered member (mixed G1 addition)
+      hash_sig     hash_to_G2 + Signature.fromBytes + randomisation per set (W_VS_HASH_SIG)
+      miller       one Miller loop per set (FME_MILLER_1J)
+      chunk_check  per set an Fp12 product and a G2 addition, per chunk a final exponentiation and the
+                   (-g1, sum r sig) Miller loop
+    `traffic` is the kernel's HBM bytes per pass from the committed PMC summary when it holds the kernel."""
+    n_chunks = n_chunks or max(1, -(-n_sets // 128))
+    work = {"agg": agg_members * FME_G1_MADD, "hash_sig": n_sets * W_VS_HASH_SIG, "miller": n_sets * FME_MILLER_1J,
+            "chunk_check": n_sets * (FME_FP12_MUL + FME_G2_ADD) + n_chunks * (FME_FINAL_EXP + FME_MILLER_1J)}
+    k = max(range(len(VS_KERNELS)), key=lambda i: float(ms[i]))
+    name = VS_KERNELS[k]
+    t = float(ms[k])
+    achieved = work[name] * MAC_PER_FME / (t * 1e-3) / 1e12 if t > 0 else 0.0
+    if name == "miller" and os.environ.get("GBV_VS_MILLER", "").startswith("t"):
+        kname = "k_vs_miller"
+    else:
+        kname = VS_KERNEL_NAMES[name]
+    traffic, ev = None, None
+    if name in VS_ALG_BYTES:
+        pair = kname.endswith("_pair")
+        traffic, ev = pmc_evidence(n_sets, kname, VS_ALG_BYTES[name], threads_per_unit=2 if pair else 1, exact=True)
+    out = {"bound": "valu-int", "kernel": kname, "achieved": round(achieved, 4), "peak": PEAK_MAC_PER_S / 1e12,
+           "unit": "T u32-MAC/s", "frac": round(achieved * 1e12 / PEAK_MAC_PER_S, 5),
+           "traffic": None if traffic is None else round(traffic), "pmc": ev,
+           "work_per_pass_fme": int(work[name]), "units_per_launch": n_sets, "avg_launch_ms": round(t, 3),
+           "kernel_ms_per_pass": {kk: round(float(x), 3) for kk, x in zip(VS_KERNELS, ms)},
+           "frac_by_kernel": {kk: round(work[kk] * MAC_PER_FME / (float(x) * 1e-3) / PEAK_MAC_PER_S, 4) if float(x) > 0 else None
+                              for kk, x in zip(VS_KERNELS, ms)},
            "miller_fme_per_set": FME_MILLER_1J}
     if agg_members and ms[0] > 0:
-        out["agg_gather_GBps"] = round(agg_members * AGG_BYTES_PER_MEMBER / (ms[0] * 1e-3) / 1e9, 1)
+        out["agg_gather_GBps_formula"] = round(agg_members * AGG_BYTES_PER_MEMBER / (ms[0] * 1e-3) / 1e9, 1)
     return out
 
 

@@ -4,8 +4,13 @@
  * This is the drop-in boundary for Lodestar's IBlsVerifier hot path
  * (/root/reference/packages/beacon-node/src/chain/bls/interface.ts:25-68).  A Node-API addon
  *  or the Python host mirror (lodestar_amd/verifier.py) binds these symbols; no
- * torch or HIP types appear in the signatures.  All entry points are called from one host thread
- * per context; each context owns one GPU, one HIP stream and the HBM-resident pubkey table.
+ * torch or HIP types appear in the signatures.  Each context owns one GPU, three HIP streams
+ * (per-set throughput kernels, chunk-level tail, hashing) and the HBM-resident pubkey table.
+ * Entry points may be called from several host threads: each holds the context's lock while it
+ * touches the context (the one-shot calls share one scratch batch and run one at a time); the
+ * batch waits release it while they block on the device.  A batch object (gbv_sm_batch,
+ * gbv_vs_batch) belongs to one caller from fill/submit to wait.  gbv_last_error reports the last
+ * failure of the calling thread.
  *
  * Error convention: return 0 on success; per-set "false" results are carried
  * in the output byte arrays, never as errors.  Negative codes map to promise rejections:
@@ -110,6 +115,11 @@ int gbv_verify_sets_multi(gbv_ctx* ctx, size_t n_calls, const uint32_t* call_off
 typedef struct gbv_vs_batch gbv_vs_batch;
 int gbv_vs_batch_create(gbv_ctx* ctx, size_t n_calls, const uint32_t* call_off, const gbv_set* sets,
                         const uint32_t* index_arena, gbv_vs_batch** out);
+/* Refill an existing batch with a new workload (same rules as create), reusing its HBM and pinned
+ * buffers: the streamed verifier keeps a few batches and cycles them.  The batch must not be in
+ * flight.  The input copy is queued on the device, not waited for. */
+int gbv_vs_batch_fill(gbv_ctx* ctx, gbv_vs_batch* b, size_t n_calls, const uint32_t* call_off, const gbv_set* sets,
+                      const uint32_t* index_arena);
 int gbv_vs_batch_submit(gbv_ctx* ctx, gbv_vs_batch* b);
 int gbv_vs_batch_wait(gbv_ctx* ctx, gbv_vs_batch* b, uint8_t* call_valid);
 void gbv_vs_batch_destroy(gbv_ctx* ctx, gbv_vs_batch* b);
@@ -165,6 +175,9 @@ int gbv_sm_batch_verify(gbv_ctx* ctx, gbv_sm_batch* b, uint8_t* valid);
  * wait blocks until it is done and copies the per-set booleans.  Submitting batch k+1 before
  * waiting on batch k overlaps k's chunk-level tail with k+1's per-set kernel (gossip stream).
  * A batch can have one verification in flight at a time. */
+/* Refill an existing batch (as gbv_vs_batch_fill). */
+int gbv_sm_batch_fill(gbv_ctx* ctx, gbv_sm_batch* b, size_t n_calls, const uint32_t* call_off, const uint32_t* idx,
+                      const uint8_t* sigs96, const uint8_t* msgs32);
 int gbv_sm_batch_submit(gbv_ctx* ctx, gbv_sm_batch* b);
 int gbv_sm_batch_wait(gbv_ctx* ctx, gbv_sm_batch* b, uint8_t* valid);
 void gbv_sm_batch_destroy(gbv_ctx* ctx, gbv_sm_batch* b);

@@ -8,6 +8,7 @@ from .verifier import (  # noqa: F401
     EmptyAggregateError,
     GbvError,
     GpuBlsVerifier,
+    PackedSameMessageSets,
     QueueAbortedError,
     SingleSignatureSet,
     VerifySignatureOpts,

@@ -12,6 +12,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -130,7 +131,18 @@ struct gbv_ctx {
   hipEvent_t ssz_ev[2] = {};
   float last_ssz_ms = 0.f;
   float last_vs_ms[4] = {};  // agg, hash+sig, miller, chunk check of the last vs batch
+  // Every entry point holds this while it touches the context (its scratch batches, streams, table,
+  // counters), so host threads may share a context: the Python verifier's worker threads and its
+  // event-loop thread, the addon's libuv pool.  Recursive: one-shot calls nest submit + wait.  The
+  // batch waits release it while they block on the device.
+  std::recursive_mutex mu;
 };
+
+#define GBV_LOCK(c) std::lock_guard<std::recursive_mutex> gbv_lock_((c)->mu)
+
+// Synchronise the context's streams, ignoring errors: an enqueue that failed midway leaves
+// nothing queued that could still read buffers the caller is about to free or refill.
+void ctx_drain(gbv_ctx* c);
 
 int gbv_fail(gbv_ctx* c, int code, const std::string& msg);
 
@@ -139,6 +151,16 @@ int gbv_fail(gbv_ctx* c, int code, const std::string& msg);
     hipError_t e_ = (call);                                                                  \
     if (e_ != hipSuccess)                                                                    \
       return gbv_fail(ctx, GBV_E_DEVICE, std::string(#call) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+// HIP_CHECK for calls made after kernels were enqueued: drain the streams before returning
+#define HIP_CHECK_DRAIN(ctx, call)                                                           \
+  do {                                                                                       \
+    hipError_t e_ = (call);                                                                  \
+    if (e_ != hipSuccess) {                                                                  \
+      ctx_drain(ctx);                                                                        \
+      return gbv_fail(ctx, GBV_E_DEVICE, std::string(#call) + ": " + hipGetErrorString(e_)); \
+    }                                                                                        \
   } while (0)
 
 // grow-only small scratch (device / pinned host) owned by the context

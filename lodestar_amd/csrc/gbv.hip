@@ -27,9 +27,20 @@ size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 }  // namespace
 
+// The message of the last failure on the calling thread (gbv_last_error): with several host threads
+// on one context, each reads its own call's error.
+static thread_local std::string t_err;
+
 int gbv_fail(gbv_ctx* c, int code, const std::string& msg) {
   if (c) c->err = msg;
+  t_err = msg;
   return code;
+}
+
+void ctx_drain(gbv_ctx* c) {
+  for (hipStream_t s : {c->stream, c->stream2, c->stream4})
+    if (s) (void)hipStreamSynchronize(s);
+  (void)hipGetLastError();
 }
 
 int ctx_small_dev(gbv_ctx* c, size_t bytes, uint8_t** out) {
@@ -85,6 +96,9 @@ struct gbv_sm_batch {
   std::vector<hipEvent_t> evs[2];
   hipEvent_t dones[2] = {};
   int cur = 0;  // event set of the last submit
+  // the input blob's host-to-device copy (stream A) of the last fill: the pinned blob is rewritten
+  // only once it is done, and the streams other than A wait for it before reading the inputs
+  hipEvent_t copied = nullptr;
   G2A *H = nullptr, *S = nullptr;
   G2J *rS = nullptr, *SgJ = nullptr;
   Fp12* F = nullptr;
@@ -183,6 +197,10 @@ static int sm_reserve(gbv_ctx* c, gbv_sm_batch* b, size_t n, size_t G, size_t ca
 static void sm_destroy(gbv_sm_batch* b) {
   if (!b) return;
   if (b->in_flight && b->dones[b->cur]) hipEventSynchronize(b->dones[b->cur]);  // nothing is freed under a running pass
+  if (b->copied) {
+    hipEventSynchronize(b->copied);
+    hipEventDestroy(b->copied);
+  }
   sm_free_work(b);
   hipFree(b->in_dev);
   hipHostFree(b->in_host);
@@ -224,6 +242,9 @@ int gbv_init(int device, gbv_ctx** out) {
 
 void gbv_destroy(gbv_ctx* c) {
   if (!c) return;
+  {
+    GBV_LOCK(c);  // a call still running on another thread finishes first
+  }
   hipSetDevice(c->device);
   c->closed = true;
   // every stream drains before anything it may still read or write is freed
@@ -245,10 +266,18 @@ void gbv_destroy(gbv_ctx* c) {
   delete c;
 }
 
-const char* gbv_last_error(gbv_ctx* c) { return c ? c->err.c_str() : "null context"; }
+const char* gbv_last_error(gbv_ctx* c) { return c ? t_err.c_str() : "null context"; }
 
-size_t gbv_pubkeys_count(gbv_ctx* c) { return c ? c->table_n : 0; }
-int gbv_comb_enabled(gbv_ctx* c) { return c && c->comb_on ? 1 : 0; }
+size_t gbv_pubkeys_count(gbv_ctx* c) {
+  if (!c) return 0;
+  GBV_LOCK(c);
+  return c->table_n;
+}
+int gbv_comb_enabled(gbv_ctx* c) {
+  if (!c) return 0;
+  GBV_LOCK(c);
+  return c->comb_on ? 1 : 0;
+}
 
 static int table_reserve(gbv_ctx* c, size_t need) {
   if (need <= c->table_cap) return GBV_OK;
@@ -347,6 +376,7 @@ static int comb_build(gbv_ctx* c, uint32_t first, size_t n, size_t keep) {
 
 int gbv_pubkeys_append(gbv_ctx* c, uint32_t first, const uint8_t* pk48, size_t n, int validate, uint8_t* status) {
   if (!c) return GBV_E_ARG;
+  GBV_LOCK(c);
   if (c->closed) return GBV_E_CLOSED;
   if (n == 0) return GBV_OK;
   if (!pk48) return gbv_fail(c, GBV_E_ARG, "null pk48");
@@ -371,7 +401,9 @@ int gbv_pubkeys_append(gbv_ctx* c, uint32_t first, const uint8_t* pk48, size_t n
 }
 
 int gbv_pubkeys_replicate(gbv_ctx* c, uint32_t src_first, uint32_t src_n, uint32_t dst_first, size_t n) {
-  if (!c || src_n == 0 || (size_t)src_first + src_n > c->table_n) return gbv_fail(c, GBV_E_ARG, "bad replicate range");
+  if (!c) return GBV_E_ARG;
+  GBV_LOCK(c);
+  if (src_n == 0 || (size_t)src_first + src_n > c->table_n) return gbv_fail(c, GBV_E_ARG, "bad replicate range");
   HIP_CHECK(c, hipSetDevice(c->device));
   int rc = table_reserve(c, (size_t)dst_first + n);
   if (rc) return rc;
@@ -394,6 +426,7 @@ int gbv_pubkeys_replicate(gbv_ctx* c, uint32_t src_first, uint32_t src_n, uint32
 // aggregateSerializedPublicKeys, decompressed on the device first).
 static int aggregate_common(gbv_ctx* c, const uint32_t* idx, const uint8_t* pk48, size_t k, int validate, uint8_t out48[48]) {
   if (!c) return GBV_E_ARG;
+  GBV_LOCK(c);
   if (c->closed) return GBV_E_CLOSED;
   if (k == 0) return gbv_fail(c, GBV_E_EMPTY_AGGREGATE, "EMPTY_AGGREGATE_ARRAY");
   if ((!idx && !pk48) || !out48) return gbv_fail(c, GBV_E_ARG, "null argument");
@@ -451,6 +484,7 @@ int gbv_aggregate_serialized_pubkeys(gbv_ctx* c, const uint8_t* pk48, size_t k, 
 
 int gbv_signatures_validate(gbv_ctx* c, const uint8_t* sigs, size_t n, uint32_t sig_len, uint8_t* status, uint8_t* out96) {
   if (!c) return GBV_E_ARG;
+  GBV_LOCK(c);
   if (c->closed) return GBV_E_CLOSED;
   if (n == 0) return GBV_OK;
   if (!sigs || !status) return gbv_fail(c, GBV_E_ARG, "null argument");
@@ -474,6 +508,7 @@ int gbv_signatures_validate(gbv_ctx* c, const uint8_t* sigs, size_t n, uint32_t 
 
 int gbv_aggregate_signatures(gbv_ctx* c, const uint8_t* sigs, size_t n, uint32_t sig_len, int validate, uint8_t out96[96]) {
   if (!c) return GBV_E_ARG;
+  GBV_LOCK(c);
   if (c->closed) return GBV_E_CLOSED;
   if (n == 0) return gbv_fail(c, GBV_E_EMPTY_AGGREGATE, "EMPTY_AGGREGATE_ARRAY");
   if (!sigs || !out96) return gbv_fail(c, GBV_E_ARG, "null argument");
@@ -503,8 +538,12 @@ int gbv_aggregate_signatures(gbv_ctx* c, const uint8_t* sigs, size_t n, uint32_t
 
 // ---- same-message batches ------------------------------------------------------------------
 void gbv_sm_batch_destroy(gbv_ctx* c, gbv_sm_batch* b) {
-  (void)c;
-  sm_destroy(b);
+  if (c) {
+    GBV_LOCK(c);
+    sm_destroy(b);
+  } else {
+    sm_destroy(b);
+  }
 }
 
 // (Re)fill batch b with a workload: chunking on the host, inputs through one pinned blob and ONE
@@ -513,6 +552,7 @@ static int sm_fill(gbv_ctx* c, gbv_sm_batch* b, size_t n_calls, const uint32_t* 
                    const uint8_t* msgs32) {
   if (b->in_flight) return gbv_fail(c, GBV_E_ARG, "batch in flight");
   if (n_calls && (!call_off || !msgs32)) return gbv_fail(c, GBV_E_ARG, "null argument");
+  if (b->copied) HIP_CHECK(c, hipEventSynchronize(b->copied));  // the pinned blob is free again
   size_t n = n_calls ? call_off[n_calls] : 0;
   if (n && (!idx || !sigs96)) return gbv_fail(c, GBV_E_ARG, "null argument");
   if (call_off && call_off[0] != 0) return gbv_fail(c, GBV_E_ARG, "call offsets must start at 0");
@@ -569,8 +609,11 @@ static int sm_fill(gbv_ctx* c, gbv_sm_batch* b, size_t n_calls, const uint32_t* 
   b->grp_off = (uint32_t*)(b->in_dev + o_go);
   b->grp_msg = (uint32_t*)(b->in_dev + o_gm);
   b->msgs = b->in_dev + o_m;
+  // no host wait: stream A runs the copy ahead of this batch's kernels (and behind the previous
+  // batch's k_sm_prepare); the other streams wait for the event
+  if (!b->copied) HIP_CHECK(c, hipEventCreateWithFlags(&b->copied, hipEventDisableTiming));
   HIP_CHECK(c, hipMemcpyAsync(b->in_dev, h, total, hipMemcpyHostToDevice, c->stream));
-  HIP_CHECK(c, hipStreamSynchronize(c->stream));  // the pinned blob is reused by the next fill
+  HIP_CHECK(c, hipEventRecord(b->copied, c->stream));
   b->n = n;
   b->G = G;
   b->n_calls = n_calls;
@@ -581,6 +624,7 @@ static int sm_fill(gbv_ctx* c, gbv_sm_batch* b, size_t n_calls, const uint32_t* 
 int gbv_sm_batch_create(gbv_ctx* c, size_t n_calls, const uint32_t* call_off, const uint32_t* idx, const uint8_t* sigs96,
                         const uint8_t* msgs32, gbv_sm_batch** out) {
   if (!c || !out) return GBV_E_ARG;
+  GBV_LOCK(c);
   if (c->closed) return GBV_E_CLOSED;
   *out = nullptr;
   gbv_sm_batch* b = new gbv_sm_batch();
@@ -591,6 +635,29 @@ int gbv_sm_batch_create(gbv_ctx* c, size_t n_calls, const uint32_t* call_off, co
   }
   *out = b;
   return GBV_OK;
+}
+
+int gbv_sm_batch_fill(gbv_ctx* c, gbv_sm_batch* b, size_t n_calls, const uint32_t* call_off, const uint32_t* idx, const uint8_t* sigs96,
+                      const uint8_t* msgs32) {
+  if (!c || !b) return GBV_E_ARG;
+  GBV_LOCK(c);
+  if (c->closed) return GBV_E_CLOSED;
+  return sm_fill(c, b, n_calls, call_off, idx, sigs96, msgs32);
+}
+
+static int sm_submit_enqueue(gbv_ctx* c, gbv_sm_batch* b);
+
+int gbv_sm_batch_submit(gbv_ctx* c, gbv_sm_batch* b) {
+  if (!c || !b) return GBV_E_ARG;
+  GBV_LOCK(c);
+  if (c->closed) return GBV_E_CLOSED;
+  if (b->in_flight) return gbv_fail(c, GBV_E_ARG, "batch already in flight");
+  HIP_CHECK(c, hipSetDevice(c->device));
+  if (b->n == 0) return GBV_OK;
+  int rc = sm_submit_enqueue(c, b);
+  if (rc) ctx_drain(c);  // kernels enqueued before the failure finish before anything is freed
+  else b->in_flight = true;
+  return rc;
 }
 
 // Pipelined over segments of ~n/S sets (cut at chunk boundaries), all enqueued without a host
@@ -604,12 +671,7 @@ int gbv_sm_batch_create(gbv_ctx* c, size_t n_calls, const uint32_t* call_off, co
 //   stream B0     : wait(all) k_sm_fallback (per-set retry of failed chunks only), copy-out
 // Each segment ends in ONE randomised multi-pairing check over all its chunks; only a failing
 // segment pays per-chunk checks and only a failing chunk pays per-set retries.
-int gbv_sm_batch_submit(gbv_ctx* c, gbv_sm_batch* b) {
-  if (!c || !b) return GBV_E_ARG;
-  if (c->closed) return GBV_E_CLOSED;
-  if (b->in_flight) return gbv_fail(c, GBV_E_ARG, "batch already in flight");
-  HIP_CHECK(c, hipSetDevice(c->device));
-  if (b->n == 0) return GBV_OK;
+static int sm_submit_enqueue(gbv_ctx* c, gbv_sm_batch* b) {
   Seed seed = fresh_seed();
   uint32_t nonce = c->nonce++;
   // Same-message batches: hash on stream 4, tail on stream 2, every batch.  Alternating the tails
@@ -671,6 +733,7 @@ int gbv_sm_batch_submit(gbv_ctx* c, gbv_sm_batch* b) {
   }
   hipEvent_t* ev = evv.data();
   const size_t part_stride = b->part_stride;
+  if (sh != sa) HIP_CHECK(c, hipStreamWaitEvent(sh, b->copied, 0));  // the hash reads the staged messages
   HIP_CHECK(c, hipMemsetAsync(b->n_fallback, 0, 4, sh));
   HIP_CHECK(c, hipMemsetAsync(b->fb_cnt, 0, 8, sh));
   HIP_CHECK(c, hipEventRecord(ev[0], sh));
@@ -773,17 +836,25 @@ int gbv_sm_batch_submit(gbv_ctx* c, gbv_sm_batch* b) {
   HIP_CHECK(c, hipMemcpyAsync(b->seg_ok_host, b->seg_ok, S, hipMemcpyDeviceToHost, sf));
   HIP_CHECK(c, hipEventRecord(b->dones[b->cur], sf));
   HIP_CHECK(c, hipGetLastError());
-  b->in_flight = true;
   return GBV_OK;
 }
 
 int gbv_sm_batch_wait(gbv_ctx* c, gbv_sm_batch* b, uint8_t* valid) {
   if (!c || !b) return GBV_E_ARG;
-  if (b->n == 0) return GBV_OK;
-  if (!b->in_flight) return gbv_fail(c, GBV_E_ARG, "batch not submitted");
+  hipEvent_t done = nullptr;
+  {
+    GBV_LOCK(c);
+    if (b->n == 0) return GBV_OK;
+    if (!b->in_flight) return gbv_fail(c, GBV_E_ARG, "batch not submitted");
+    done = b->dones[b->cur];
+  }
   HIP_CHECK(c, hipSetDevice(c->device));
+  // block on the device without the context lock (other threads keep submitting); the batch itself
+  // belongs to this caller until the wait returns
+  hipError_t we = hipEventSynchronize(done);
+  GBV_LOCK(c);
   b->in_flight = false;
-  HIP_CHECK(c, hipEventSynchronize(b->dones[b->cur]));
+  if (we != hipSuccess) return gbv_fail(c, GBV_E_DEVICE, std::string("hipEventSynchronize: ") + hipGetErrorString(we));
   if (valid) memcpy(valid, b->valid_host, b->n);
   c->last_fallback_chunks = *b->nfb_host;
   c->last_failed_segments = 0;
@@ -815,6 +886,8 @@ int gbv_sm_batch_wait(gbv_ctx* c, gbv_sm_batch* b, uint8_t* valid) {
 }
 
 int gbv_sm_batch_verify(gbv_ctx* c, gbv_sm_batch* b, uint8_t* valid) {
+  if (!c) return GBV_E_ARG;
+  GBV_LOCK(c);
   int rc = gbv_sm_batch_submit(c, b);
   if (rc) return rc;
   return gbv_sm_batch_wait(c, b, valid);
@@ -822,6 +895,7 @@ int gbv_sm_batch_verify(gbv_ctx* c, gbv_sm_batch* b, uint8_t* valid) {
 
 int gbv_last_stats(gbv_ctx* c, uint32_t* fallback_chunks, uint32_t* failed_segments) {
   if (!c) return GBV_E_ARG;
+  GBV_LOCK(c);
   if (fallback_chunks) *fallback_chunks = c->last_fallback_chunks;
   if (failed_segments) *failed_segments = c->last_failed_segments;
   return GBV_OK;
@@ -829,6 +903,7 @@ int gbv_last_stats(gbv_ctx* c, uint32_t* fallback_chunks, uint32_t* failed_segme
 
 int gbv_last_kernel_ms(gbv_ctx* c, float* out, int* launches, int max) {
   if (!c || !out) return 0;
+  GBV_LOCK(c);
   int k = std::min(max, (int)gbv_ctx::NK);
   for (int i = 0; i < k; ++i) {
     out[i] = c->last_ms[i];
@@ -842,6 +917,7 @@ int gbv_last_kernel_ms(gbv_ctx* c, float* out, int* launches, int max) {
 int gbv_verify_same_message_multi(gbv_ctx* c, size_t n_calls, const uint32_t* call_off, const uint32_t* idx, const uint8_t* sigs96,
                                   const uint8_t* msgs32, uint8_t* valid) {
   if (!c) return GBV_E_ARG;
+  GBV_LOCK(c);  // the scratch batch is shared by every one-shot call on this context
   if (c->closed) return GBV_E_CLOSED;
   if (!c->sm_scratch) c->sm_scratch = new gbv_sm_batch();
   int rc = sm_fill(c, c->sm_scratch, n_calls, call_off, idx, sigs96, msgs32);
@@ -869,7 +945,6 @@ static int ssz_buf(gbv_ctx* c, int k, size_t bytes, uint8_t** out) {
 }
 
 static int ssz_begin(gbv_ctx* c) {
-  if (!c) return GBV_E_ARG;
   if (c->closed) return GBV_E_CLOSED;
   HIP_CHECK(c, hipSetDevice(c->device));
   for (auto& e : c->ssz_ev)
@@ -911,6 +986,8 @@ static int ssz_domains(gbv_ctx* c, size_t n, const uint8_t* domains32, size_t n_
 int gbv_sha256_digest64(gbv_ctx* c, const uint8_t* in64, size_t n, uint8_t* out32) { return gbv_merkle_roots(c, in64, n, 1, out32); }
 
 int gbv_merkle_roots(gbv_ctx* c, const uint8_t* chunks32, size_t n, uint32_t depth, uint8_t* out32) {
+  if (!c) return GBV_E_ARG;
+  GBV_LOCK(c);
   int rc = ssz_begin(c);
   if (rc) return rc;
   if (n == 0) return GBV_OK;
@@ -934,6 +1011,8 @@ int gbv_merkle_roots(gbv_ctx* c, const uint8_t* chunks32, size_t n, uint32_t dep
 
 int gbv_signing_roots(gbv_ctx* c, const uint8_t* roots32, size_t n, const uint8_t* domains32, size_t n_domains, const uint32_t* dom_idx,
                       uint8_t* out32) {
+  if (!c) return GBV_E_ARG;
+  GBV_LOCK(c);
   int rc = ssz_begin(c);
   if (rc) return rc;
   if (n == 0) return GBV_OK;
@@ -952,6 +1031,8 @@ int gbv_signing_roots(gbv_ctx* c, const uint8_t* roots32, size_t n, const uint8_
 
 int gbv_attestation_signing_roots(gbv_ctx* c, const uint8_t* data128, size_t n, const uint8_t* domains32, size_t n_domains,
                                   const uint32_t* dom_idx, uint8_t* out32) {
+  if (!c) return GBV_E_ARG;
+  GBV_LOCK(c);
   int rc = ssz_begin(c);
   if (rc) return rc;
   if (n == 0) return GBV_OK;
@@ -970,6 +1051,7 @@ int gbv_attestation_signing_roots(gbv_ctx* c, const uint8_t* data128, size_t n, 
 
 int gbv_ssz_last_kernel_ms(gbv_ctx* c, float* ms) {
   if (!c || !ms) return GBV_E_ARG;
+  GBV_LOCK(c);
   *ms = c->last_ssz_ms;
   return GBV_OK;
 }
@@ -977,6 +1059,7 @@ int gbv_ssz_last_kernel_ms(gbv_ctx* c, float* ms) {
 // ---- utilities (synthetic workloads, tests) -------------------------------------------------
 int gbv_util_sk_to_pk(gbv_ctx* c, const uint8_t* sk32, size_t n, uint8_t* pk48) {
   if (!c || (n && (!sk32 || !pk48))) return GBV_E_ARG;
+  GBV_LOCK(c);
   if (n == 0) return GBV_OK;
   HIP_CHECK(c, hipSetDevice(c->device));
   uint8_t* d = nullptr;
@@ -993,6 +1076,7 @@ int gbv_util_sk_to_pk(gbv_ctx* c, const uint8_t* sk32, size_t n, uint8_t* pk48) 
 
 int gbv_util_g1_mul_rand(gbv_ctx* c, const uint32_t* slots, const uint64_t* r64, size_t n, int use_comb, uint8_t* out48) {
   if (!c || (n && (!slots || !r64 || !out48))) return GBV_E_ARG;
+  GBV_LOCK(c);
   if (n == 0) return GBV_OK;
   if (use_comb && !c->comb_on) return gbv_fail(c, GBV_E_ARG, "comb tables disabled");
   for (size_t i = 0; i < n; ++i)
@@ -1013,6 +1097,7 @@ int gbv_util_g1_mul_rand(gbv_ctx* c, const uint32_t* slots, const uint64_t* r64,
 
 int gbv_util_hash_to_g2(gbv_ctx* c, const uint8_t* msgs32, size_t n, uint8_t* out192) {
   if (!c || (n && (!msgs32 || !out192))) return GBV_E_ARG;
+  GBV_LOCK(c);
   if (n == 0) return GBV_OK;
   HIP_CHECK(c, hipSetDevice(c->device));
   uint8_t* d = nullptr;
@@ -1030,6 +1115,7 @@ int gbv_util_hash_to_g2(gbv_ctx* c, const uint8_t* msgs32, size_t n, uint8_t* ou
 
 int gbv_util_sign(gbv_ctx* c, const uint8_t* sk32, size_t n, const uint32_t* grp, const uint8_t* msgs32, size_t n_msgs, uint8_t* sig96) {
   if (!c || (n && (!sk32 || !grp || !msgs32 || !sig96))) return GBV_E_ARG;
+  GBV_LOCK(c);
   if (n == 0) return GBV_OK;
   for (size_t i = 0; i < n; ++i)
     if (grp[i] >= n_msgs) return gbv_fail(c, GBV_E_ARG, "message index out of range");

@@ -27,7 +27,7 @@ size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 }  // namespace
 
 struct gbv_vs_batch {
-  size_t n = 0, n_calls = 0, C = 0, n_agg = 0, A = 0;
+  size_t n = 0, n_calls = 0, C = 0, n_agg = 0, A = 0, n_big = 0, n_slices = 0;
   uint32_t sig_stride = 96;
   size_t cap_n = 0, cap_C = 0;
   bool allocated = false;
@@ -38,10 +38,14 @@ struct gbv_vs_batch {
   size_t in_cap = 0;
   // inputs (views into in_dev)
   uint32_t *set_off = nullptr, *arena = nullptr, *agg_list = nullptr, *chunk_off = nullptr, *siglen = nullptr;
+  uint4 *big = nullptr, *slices = nullptr;  // large aggregates: (set, first slice, count), slice (begin, end)
   uint8_t *raw_flag = nullptr, *raw_pk = nullptr, *msgs = nullptr, *sig = nullptr;
   // work
-  G1J* pk = nullptr;  // aggregate pubkeys (Jacobian, k_vs_agg)
+  G1J* pk = nullptr;  // aggregate pubkeys (Jacobian, k_vs_agg / k_vs_agg_big)
   uint8_t* pk_st = nullptr;
+  G1J* agg_part = nullptr;  // slice sums of the large aggregates (grow-only)
+  uint8_t* agg_part_bad = nullptr;
+  size_t agg_part_cap = 0;
   G2A* H = nullptr;
   G1J* rP = nullptr;
   G2J* rS = nullptr;
@@ -59,6 +63,7 @@ struct gbv_vs_batch {
   size_t part_cap = 0;
   hipEvent_t ev[7] = {};
   hipEvent_t done = nullptr;
+  hipEvent_t copied = nullptr;  // the last fill's input copy (stream A); see gbv_sm_batch::copied
   bool in_flight = false;
   int tail = 0;
 };
@@ -75,10 +80,15 @@ static void vs_free_work(gbv_vs_batch* b) {
 void vs_batch_free(gbv_vs_batch* b) {
   if (!b) return;
   if (b->in_flight && b->done) (void)hipEventSynchronize(b->done);
+  if (b->copied) {
+    (void)hipEventSynchronize(b->copied);
+    (void)hipEventDestroy(b->copied);
+  }
   vs_free_work(b);
   hipFree(b->in_dev);
   hipHostFree(b->in_host);
   hipFree(b->Fpart); hipFree(b->Spart); hipFree(b->has); hipFree(b->f_out); hipFree(b->flag);
+  hipFree(b->agg_part); hipFree(b->agg_part_bad);
   for (auto e : b->ev)
     if (e) hipEventDestroy(e);
   if (b->done) hipEventDestroy(b->done);
@@ -116,6 +126,7 @@ static int vs_reserve(gbv_ctx* c, gbv_vs_batch* b, size_t n, size_t C) {
 static int vs_fill(gbv_ctx* c, gbv_vs_batch* b, size_t n_calls, const uint32_t* call_off, const gbv_set* sets, const uint32_t* arena) {
   if (b->in_flight) return gbv_fail(c, GBV_E_ARG, "batch in flight");
   if (n_calls && !call_off) return gbv_fail(c, GBV_E_ARG, "null call offsets");
+  if (b->copied) HIP_CHECK(c, hipEventSynchronize(b->copied));  // the pinned blob is free again
   size_t n = n_calls ? call_off[n_calls] : 0;
   if (call_off && call_off[0] != 0) return gbv_fail(c, GBV_E_ARG, "call offsets must start at 0");
   for (size_t g = 0; g < n_calls; ++g)
@@ -123,7 +134,7 @@ static int vs_fill(gbv_ctx* c, gbv_vs_batch* b, size_t n_calls, const uint32_t* 
   if (n && !sets) return gbv_fail(c, GBV_E_ARG, "null sets");
   if (n > 0x7FFFFFFFull) return gbv_fail(c, GBV_E_ARG, "too many sets");
   std::vector<uint8_t> reject(n_calls, 0);
-  size_t A = 0, n_agg = 0;
+  size_t A = 0, n_agg = 0, n_big = 0, n_slices = 0;
   uint32_t stride = 96;
   for (size_t g = 0; g < n_calls; ++g)
     for (uint32_t i = call_off[g]; i < call_off[g + 1]; ++i) {
@@ -139,7 +150,12 @@ static int vs_fill(gbv_ctx* c, gbv_vs_batch* b, size_t n_calls, const uint32_t* 
       for (uint32_t j = 0; j < s.idx_len; ++j)
         if (arena[s.idx_off + j] >= c->table_n) return gbv_fail(c, GBV_E_ARG, "validator index out of range");
       A += s.idx_len;
-      n_agg += s.idx_len >= 2 ? 1 : 0;
+      if (s.idx_len >= AGG_BIG_MIN) {
+        ++n_big;
+        n_slices += (s.idx_len + AGG_SLICE_MEMBERS - 1) / AGG_SLICE_MEMBERS;
+      } else if (s.idx_len >= 2) {
+        ++n_agg;
+      }
     }
   // chunks: chunkifyMaximizeChunkSize(call, 128) per non-empty, non-rejected call
   std::vector<uint32_t> chunk_off, call_chunk(n_calls + 1, 0);
@@ -159,11 +175,23 @@ static int vs_fill(gbv_ctx* c, gbv_vs_batch* b, size_t n_calls, const uint32_t* 
   HIP_CHECK(c, hipSetDevice(c->device));
   int rc = vs_reserve(c, b, n, C);
   if (rc) return rc;
+  if (b->agg_part_cap < n_slices) {
+    hipFree(b->agg_part);
+    hipFree(b->agg_part_bad);
+    b->agg_part = nullptr;
+    b->agg_part_bad = nullptr;
+    b->agg_part_cap = 0;
+    size_t cap = std::max(n_slices, 2 * b->agg_part_cap);
+    HIP_CHECK(c, dalloc(&b->agg_part, cap));
+    HIP_CHECK(c, dalloc(&b->agg_part_bad, cap));
+    b->agg_part_cap = cap;
+  }
   // input blob: set_off 4(n+1) | arena 4A | agg_list 4 n_agg | chunk (begin,end) 8C | siglen 4n | raw_flag n |
-  //             raw_pk 48n | msgs 32n | sig stride*n
+  //             raw_pk 48n | msgs 32n | sig stride*n | big 16 n_big | slices 16 n_slices
   size_t o_so = 0, o_ar = align256(4 * (n + 1)), o_al = o_ar + align256(4 * A), o_co = o_al + align256(4 * n_agg);
   size_t o_sl = o_co + align256(8 * C), o_rf = o_sl + align256(4 * n), o_rp = o_rf + align256(n), o_m = o_rp + align256(48 * n);
-  size_t o_sig = o_m + align256(32 * n), total = o_sig + align256((size_t)stride * n);
+  size_t o_sig = o_m + align256(32 * n), o_big = o_sig + align256((size_t)stride * n), o_slc = o_big + align256(16 * n_big);
+  size_t total = o_slc + align256(16 * n_slices);
   if (b->in_cap < total) {
     hipFree(b->in_dev);
     hipHostFree(b->in_host);
@@ -181,7 +209,9 @@ static int vs_fill(gbv_ctx* c, gbv_vs_batch* b, size_t n_calls, const uint32_t* 
   uint32_t* co = (uint32_t*)(h + o_co);
   uint32_t* sl = (uint32_t*)(h + o_sl);
   uint8_t* rf = h + o_rf;
-  size_t a = 0, na = 0;
+  uint4* bg = (uint4*)(h + o_big);
+  uint4* slc = (uint4*)(h + o_slc);
+  size_t a = 0, na = 0, nb = 0, ns = 0;
   for (size_t i = 0; i < n; ++i) {
     const gbv_set& s = sets[i];
     so[i] = (uint32_t)a;
@@ -190,8 +220,15 @@ static int vs_fill(gbv_ctx* c, gbv_vs_batch* b, size_t n_calls, const uint32_t* 
       memcpy(h + o_rp + 48 * i, s.raw_pk48, 48);
     } else if (s.idx_len) {
       memcpy(ar + a, arena + s.idx_off, 4 * (size_t)s.idx_len);
+      if (s.idx_len >= AGG_BIG_MIN) {
+        const uint32_t k = (s.idx_len + AGG_SLICE_MEMBERS - 1) / AGG_SLICE_MEMBERS;
+        bg[nb++] = make_uint4((uint32_t)i, (uint32_t)ns, k, 0);
+        for (uint32_t q = 0; q < k; ++q)
+          slc[ns++] = make_uint4((uint32_t)a + q * AGG_SLICE_MEMBERS, (uint32_t)a + std::min(s.idx_len, (q + 1) * AGG_SLICE_MEMBERS), 0, 0);
+      } else if (s.idx_len >= 2) {
+        al[na++] = (uint32_t)i;
+      }
       a += s.idx_len;
-      if (s.idx_len >= 2) al[na++] = (uint32_t)i;
     }
     memcpy(h + o_m + 32 * i, s.msg32, 32);
     uint32_t L = s.sig_len;
@@ -201,6 +238,9 @@ static int vs_fill(gbv_ctx* c, gbv_vs_batch* b, size_t n_calls, const uint32_t* 
     if (sl[i] < stride) memset(dst + sl[i], 0, stride - sl[i]);
   }
   so[n] = (uint32_t)a;
+  // k_vs_agg runs 8 sets per wave: sets of similar size share a wave (largest first), so a 512-member
+  // sync aggregate does not hold a wave of 128-member committees for 4x their time
+  std::stable_sort(al, al + na, [&](uint32_t x, uint32_t y) { return sets[x].idx_len > sets[y].idx_len; });
   for (size_t k = 0; k < C; ++k) {
     co[2 * k] = chunk_off[k];
     co[2 * k + 1] = chunk_end[k];
@@ -214,12 +254,18 @@ static int vs_fill(gbv_ctx* c, gbv_vs_batch* b, size_t n_calls, const uint32_t* 
   b->raw_pk = b->in_dev + o_rp;
   b->msgs = b->in_dev + o_m;
   b->sig = b->in_dev + o_sig;
+  b->big = (uint4*)(b->in_dev + o_big);
+  b->slices = (uint4*)(b->in_dev + o_slc);
+  // no host wait: stream A runs the copy ahead of the batch's kernels, other streams wait for the event
+  if (!b->copied) HIP_CHECK(c, hipEventCreateWithFlags(&b->copied, hipEventDisableTiming));
   HIP_CHECK(c, hipMemcpyAsync(b->in_dev, h, total, hipMemcpyHostToDevice, c->stream));
-  HIP_CHECK(c, hipStreamSynchronize(c->stream));  // the pinned blob is reused by the next fill
+  HIP_CHECK(c, hipEventRecord(b->copied, c->stream));
   b->n = n;
   b->n_calls = n_calls;
   b->C = C;
   b->n_agg = n_agg;
+  b->n_big = n_big;
+  b->n_slices = n_slices;
   b->A = A;
   b->sig_stride = stride;
   b->call_chunk.swap(call_chunk);
@@ -256,10 +302,13 @@ static int vs_enqueue_sets(gbv_ctx* c, gbv_vs_batch* b, hipStream_t m, bool with
   uint32_t nonce = c->nonce++;
   HIP_CHECK(c, hipEventRecord(b->ev[0], s));
   if (b->n_agg) launch_vs_agg(LaunchCfg{(unsigned)b->n_agg, 64, s}, b->agg_list, b->set_off, b->arena, c->table, c->table_ok, b->pk, b->pk_st);
+  launch_vs_agg_big(s, (uint32_t)b->n_slices, b->slices, (uint32_t)b->n_big, b->big, b->arena, c->table, c->table_ok, b->agg_part,
+                    b->agg_part_bad, b->pk, b->pk_st);
   HIP_CHECK(c, hipEventRecord(b->ev[1], s));
   // small passes (latency): the hash on stream m (lane-pair maps, cooperative cofactor clearing)
   // beside the signature checks and the randomisation, which run as two block roles on stream A
   const bool split = with_fs && m != s && vs_fs_small(b) && vs_split_on();
+  if (split) HIP_CHECK(c, hipStreamWaitEvent(m, b->copied, 0));
   if (split) launch_hash_msgs(LaunchCfg{blocks_for(b->n), TPB, m}, b->msgs, (uint32_t)b->n, b->H, b->Hpre);
   launch_vs_hash_sig(s, (uint32_t)b->n, b->msgs, b->set_off, b->arena, b->raw_flag, b->raw_pk, b->sig, b->sig_stride, b->siglen, c->table,
                      c->table_ok, b->pk, b->pk_st, seed, nonce, b->H, b->rP, b->rS, b->status, split);
@@ -285,6 +334,7 @@ extern "C" {
 int gbv_vs_batch_create(gbv_ctx* c, size_t n_calls, const uint32_t* call_off, const gbv_set* sets, const uint32_t* arena,
                         gbv_vs_batch** out) {
   if (!c || !out) return GBV_E_ARG;
+  GBV_LOCK(c);
   if (c->closed) return GBV_E_CLOSED;
   *out = nullptr;
   gbv_vs_batch* b = new gbv_vs_batch();
@@ -298,21 +348,22 @@ int gbv_vs_batch_create(gbv_ctx* c, size_t n_calls, const uint32_t* call_off, co
 }
 
 void gbv_vs_batch_destroy(gbv_ctx* c, gbv_vs_batch* b) {
-  (void)c;
-  vs_batch_free(b);
+  if (c) {
+    GBV_LOCK(c);
+    vs_batch_free(b);
+  } else {
+    vs_batch_free(b);
+  }
 }
 
-// Enqueue the whole verification without a host round trip: the per-set kernels on stream A, the
-// Miller values and chunk checks on a tail stream, alternating per submit between stream 2 and the
-// hash stream (idle in this path), so that consecutive batches' tails overlap each other and the
-// next batch's per-set kernels -- still three streams in all (gbv_sm_batch_submit: a fourth live
-// stream oversubscribes GPU_MAX_HW_QUEUES=4).
-int gbv_vs_batch_submit(gbv_ctx* c, gbv_vs_batch* b) {
+int gbv_vs_batch_fill(gbv_ctx* c, gbv_vs_batch* b, size_t n_calls, const uint32_t* call_off, const gbv_set* sets, const uint32_t* arena) {
   if (!c || !b) return GBV_E_ARG;
+  GBV_LOCK(c);
   if (c->closed) return GBV_E_CLOSED;
-  if (b->in_flight) return gbv_fail(c, GBV_E_ARG, "batch already in flight");
-  HIP_CHECK(c, hipSetDevice(c->device));
-  if (b->n == 0 || b->C == 0) return GBV_OK;
+  return vs_fill(c, b, n_calls, call_off, sets, arena);
+}
+
+static int vs_submit_enqueue(gbv_ctx* c, gbv_vs_batch* b) {
   b->tail = (int)(c->sm_submits++ & 1);
   hipStream_t t = b->tail ? c->stream4 : c->stream2;
   int rc = vs_enqueue_sets(c, b, t, true);
@@ -324,16 +375,41 @@ int gbv_vs_batch_submit(gbv_ctx* c, gbv_vs_batch* b) {
   HIP_CHECK(c, hipMemcpyAsync(b->chunk_valid_host, b->chunk_valid, b->C, hipMemcpyDeviceToHost, t));
   HIP_CHECK(c, hipEventRecord(b->done, t));
   HIP_CHECK(c, hipGetLastError());
-  b->in_flight = true;
   return GBV_OK;
+}
+
+// Enqueue the whole verification without a host round trip: the per-set kernels on stream A, the
+// Miller values and chunk checks on a tail stream, alternating per submit between stream 2 and the
+// hash stream (idle in this path), so that consecutive batches' tails overlap each other and the
+// next batch's per-set kernels -- still three streams in all (gbv_sm_batch_submit: a fourth live
+// stream oversubscribes GPU_MAX_HW_QUEUES=4).
+int gbv_vs_batch_submit(gbv_ctx* c, gbv_vs_batch* b) {
+  if (!c || !b) return GBV_E_ARG;
+  GBV_LOCK(c);
+  if (c->closed) return GBV_E_CLOSED;
+  if (b->in_flight) return gbv_fail(c, GBV_E_ARG, "batch already in flight");
+  HIP_CHECK(c, hipSetDevice(c->device));
+  if (b->n == 0 || b->C == 0) return GBV_OK;
+  int rc = vs_submit_enqueue(c, b);
+  if (rc) ctx_drain(c);  // kernels enqueued before the failure finish before anything is freed
+  else b->in_flight = true;
+  return rc;
 }
 
 int gbv_vs_batch_wait(gbv_ctx* c, gbv_vs_batch* b, uint8_t* call_valid) {
   if (!c || !b) return GBV_E_ARG;
   HIP_CHECK(c, hipSetDevice(c->device));
-  if (b->in_flight) {
+  bool flying;
+  {
+    GBV_LOCK(c);
+    flying = b->in_flight;
+  }
+  // the device wait runs without the context lock; the batch belongs to this caller
+  hipError_t we = flying ? hipEventSynchronize(b->done) : hipSuccess;
+  GBV_LOCK(c);
+  if (flying) {
     b->in_flight = false;
-    HIP_CHECK(c, hipEventSynchronize(b->done));
+    if (we != hipSuccess) return gbv_fail(c, GBV_E_DEVICE, std::string("hipEventSynchronize: ") + hipGetErrorString(we));
     float ms[4] = {};
     const int from[4] = {0, 1, 3, 4};  // agg, hash_sig, miller, chunk checks
     for (int k = 0; k < 4; ++k)
@@ -354,6 +430,7 @@ int gbv_vs_batch_wait(gbv_ctx* c, gbv_vs_batch* b, uint8_t* call_valid) {
 
 int gbv_vs_last_kernel_ms(gbv_ctx* c, float* ms4) {
   if (!c || !ms4) return GBV_E_ARG;
+  GBV_LOCK(c);
   memcpy(ms4, c->last_vs_ms, sizeof c->last_vs_ms);
   return GBV_OK;
 }
@@ -366,6 +443,7 @@ static gbv_vs_batch* scratch(gbv_ctx* c) {
 int gbv_verify_sets_multi(gbv_ctx* c, size_t n_calls, const uint32_t* call_off, const gbv_set* sets, const uint32_t* arena,
                           uint8_t* call_valid) {
   if (!c || (n_calls && !call_valid)) return GBV_E_ARG;
+  GBV_LOCK(c);  // the scratch batch is shared by every one-shot call on this context
   if (c->closed) return GBV_E_CLOSED;
   gbv_vs_batch* b = scratch(c);
   int rc = vs_fill(c, b, n_calls, call_off, sets, arena);
@@ -376,6 +454,7 @@ int gbv_verify_sets_multi(gbv_ctx* c, size_t n_calls, const uint32_t* call_off, 
 
 int gbv_verify_sets(gbv_ctx* c, const gbv_set* sets, size_t n, const uint32_t* arena, uint8_t* all_valid, uint8_t* chunk_valid) {
   if (!c || !all_valid) return GBV_E_ARG;
+  GBV_LOCK(c);
   if (c->closed) return GBV_E_CLOSED;
   *all_valid = 0;
   uint32_t off[2] = {0, (uint32_t)n};
@@ -402,6 +481,7 @@ int gbv_verify_sets(gbv_ctx* c, const gbv_set* sets, size_t n, const uint32_t* a
 int gbv_vs_partial(gbv_ctx* c, const gbv_set* sets, size_t n, const uint32_t* arena, uint8_t out576[GBV_FP12_PARTIAL_BYTES],
                    uint8_t* shard_ok) {
   if (!c || !out576 || !shard_ok) return GBV_E_ARG;
+  GBV_LOCK(c);
   if (c->closed) return GBV_E_CLOSED;
   *shard_ok = 1;
   uint32_t off[2] = {0, (uint32_t)n};
@@ -424,16 +504,22 @@ int gbv_vs_partial(gbv_ctx* c, const gbv_set* sets, size_t n, const uint32_t* ar
   }
   HIP_CHECK(c, hipSetDevice(c->device));
   hipStream_t s = c->stream;
-  if ((rc = vs_enqueue_sets(c, b, s, false))) return rc;
+  if ((rc = vs_enqueue_sets(c, b, s, false))) {
+    ctx_drain(c);
+    return rc;
+  }
   // status doubles as the per-"chunk" state: SET_OK == GRP_PENDING (every valid set takes part);
   // the reduction is a tree over 64-set blocks (k_sm_seg_reduce, k_sm_part_reduce)
   launch_sm_seg_check(LaunchCfg{1, 64, s}, 0, (uint32_t)n, b->status, b->F, b->rS, b->Fpart, b->Spart, b->has, b->flag, b->f_out);
-  HIP_CHECK(c, hipGetLastError());
+  HIP_CHECK_DRAIN(c, hipGetLastError());
   uint8_t* h = nullptr;
-  if ((rc = ctx_small_host(c, sizeof(Fp12) + n, &h))) return rc;
-  HIP_CHECK(c, hipMemcpyAsync(h, b->f_out, sizeof(Fp12), hipMemcpyDeviceToHost, s));
-  HIP_CHECK(c, hipMemcpyAsync(h + sizeof(Fp12), b->status, n, hipMemcpyDeviceToHost, s));
-  HIP_CHECK(c, hipStreamSynchronize(s));
+  if ((rc = ctx_small_host(c, sizeof(Fp12) + n, &h))) {
+    ctx_drain(c);
+    return rc;
+  }
+  HIP_CHECK_DRAIN(c, hipMemcpyAsync(h, b->f_out, sizeof(Fp12), hipMemcpyDeviceToHost, s));
+  HIP_CHECK_DRAIN(c, hipMemcpyAsync(h + sizeof(Fp12), b->status, n, hipMemcpyDeviceToHost, s));
+  HIP_CHECK_DRAIN(c, hipStreamSynchronize(s));
   Fp12 f;
   memcpy((void*)&f, h, sizeof(Fp12));
   fp12_pack(out576, f);
@@ -444,6 +530,7 @@ int gbv_vs_partial(gbv_ctx* c, const gbv_set* sets, size_t n, const uint32_t* ar
 
 int gbv_fp12_check(gbv_ctx* c, const uint8_t* partials, size_t k, uint8_t* is_one) {
   if (!c || !is_one || (k && !partials)) return GBV_E_ARG;
+  GBV_LOCK(c);
   if (c->closed) return GBV_E_CLOSED;
   HIP_CHECK(c, hipSetDevice(c->device));
   hipStream_t s = c->stream;

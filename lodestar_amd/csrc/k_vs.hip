@@ -1,6 +1,7 @@
 // Distinct-message path kernels (verifySignatureSets, maybeBatch.ts:15-45), batched over many calls.
 #include "launch.h"
 #include "kernel_common.h"
+#include "pair.h"
 
 namespace gbv {
 
@@ -57,6 +58,79 @@ k_vs_agg(uint32_t n_agg, const uint32_t* __restrict__ agg_list, const uint32_t* 
     pk_out[s] = acc;
     // an infinity aggregate fails verification in blst; an invalid table slot never verifies
     pk_st[s] = (bad || jac_is_inf(acc)) ? SET_BAD_PK : SET_OK;
+  }
+}
+
+// aggregatePublicKeys of LARGE sets (electra attestations: committee_bits name up to 64 committees,
+// so one aggregate holds thousands to tens of thousands of validators; epochCache.ts:953-973) by
+// slices of AGG_SLICE_MEMBERS members (launch.h): one 256-thread workgroup per slice.  Thread t reads index words
+// begin + t, begin + t + 256, ... (consecutive threads, consecutive words: coalesced) and gathers the
+// 128-byte table records; each thread sums its few records with mixed additions, a 6-level shuffle
+// tree sums each wave and the 4 wave sums meet in LDS.  part[w] is the slice's Jacobian sum,
+// part_bad[w] flags an unusable table slot.  k_vs_agg_big_fin then sums each set's slices.
+constexpr unsigned AGG_BIG_TPB = 256;
+__global__ void __launch_bounds__(AGG_BIG_TPB) k_vs_agg_big(const uint4* __restrict__ slices, const uint32_t* __restrict__ arena,
+                                                            const G1A* __restrict__ table, const uint8_t* __restrict__ table_ok,
+                                                            G1J* __restrict__ part, uint8_t* __restrict__ part_bad) {
+  __shared__ G1J wsum[AGG_BIG_TPB / 64];
+  __shared__ int wbad[AGG_BIG_TPB / 64];
+  const uint4 sl = slices[blockIdx.x];  // (begin, end) of the slice in the arena
+  const unsigned t = threadIdx.x, lane = t & 63, w = t >> 6;
+  G1J acc = jac_infinity<Fp>();
+  int bad = 0;
+  uint32_t j = sl.x + t;
+  if (j < sl.y) {
+    const uint32_t k = arena[j];
+    bad |= table_ok[k] ? 0 : 1;
+    acc = jac_from_aff(table[k]);
+    j += AGG_BIG_TPB;
+  }
+  for (; j < sl.y; j += AGG_BIG_TPB) {
+    const uint32_t k = arena[j];
+    bad |= table_ok[k] ? 0 : 1;
+    acc = vs_g1_add_aff(acc, table[k]);
+  }
+  for (unsigned d = 32; d >= 1; d >>= 1) {
+    G1J o{vs_shfl_down(acc.x, d), vs_shfl_down(acc.y, d), vs_shfl_down(acc.z, d)};
+    bad |= __shfl_down(bad, d, 64);
+    if (lane < d) acc = vs_g1_add(acc, o);
+  }
+  if (lane == 0) {
+    wsum[w] = acc;
+    wbad[w] = bad;
+  }
+  __syncthreads();
+  if (t == 0) {
+    for (unsigned q = 1; q < AGG_BIG_TPB / 64; ++q) {
+      acc = vs_g1_add(acc, wsum[q]);
+      bad |= wbad[q];
+    }
+    part[blockIdx.x] = acc;
+    part_bad[blockIdx.x] = (uint8_t)bad;
+  }
+}
+
+// One wave per large set: sum of its slice partials (lane-strided, then the shuffle tree).
+// big = (set, first slice, slice count).
+__global__ void __launch_bounds__(64) k_vs_agg_big_fin(uint32_t n_big, const uint4* __restrict__ big, const G1J* __restrict__ part,
+                                                       const uint8_t* __restrict__ part_bad, G1J* __restrict__ pk_out,
+                                                       uint8_t* __restrict__ pk_st) {
+  const uint4 b = big[blockIdx.x];
+  const unsigned lane = threadIdx.x;
+  G1J acc = jac_infinity<Fp>();
+  int bad = 0;
+  for (uint32_t q = lane; q < b.z; q += 64) {
+    acc = vs_g1_add(acc, part[b.y + q]);
+    bad |= part_bad[b.y + q];
+  }
+  for (unsigned d = 32; d >= 1; d >>= 1) {
+    G1J o{vs_shfl_down(acc.x, d), vs_shfl_down(acc.y, d), vs_shfl_down(acc.z, d)};
+    bad |= __shfl_down(bad, d, 64);
+    if (lane < d) acc = vs_g1_add(acc, o);
+  }
+  if (lane == 0) {
+    pk_out[b.x] = acc;
+    pk_st[b.x] = (bad || jac_is_inf(acc)) ? SET_BAD_PK : SET_OK;
   }
 }
 
@@ -141,11 +215,44 @@ __global__ void GBV_KERNEL_ATTR k_vs_hash_sig(uint32_t n, uint32_t nb, uint32_t 
 
 // Miller value f_{|x|, H(m_i)}(r_i pk_i) of every set that decoded (P Jacobian: the lines carry a
 // Z^3 factor that the final exponentiation removes).
-__global__ void GBV_KERNEL_ATTR k_vs_miller(uint32_t n, const uint8_t* __restrict__ status, const G1J* __restrict__ rP,
+// One wave per SIMD (512 registers, VGPRs + AGPRs): a C3 pass of 65 536 sets is 1024 waves, one per
+// SIMD anyway, and the 576-byte accumulator, T, the line and the operands then stay in registers
+// (at two waves per SIMD the accumulator lived in scratch: 775 KB of HBM traffic per set).
+#define GBV_MILLER_ATTR __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1)))
+__global__ void GBV_MILLER_ATTR k_vs_miller(uint32_t n, const uint8_t* __restrict__ status, const G1J* __restrict__ rP,
                                             const G2A* __restrict__ H, Fp12* __restrict__ F) {
   uint32_t i = blockIdx.x * 64 + threadIdx.x;
   if (i >= n || status[i] != SET_OK) return;
   F[i] = miller_loop_1j(rP[i], H[i]);
+}
+
+// The same Miller values on lane pairs (pair.h): set i on lanes 2(i mod 32), 2(i mod 32) + 1 of block
+// i / 32; lane 0 of the pair writes c0 of the conjugated value, lane 1 c1.  Every lane runs the loop
+// (the pair exchanges need both lanes); pairs past n or whose set did not decode write nothing.
+__global__ void GBV_MILLER_ATTR k_vs_miller_pair(uint32_t n, const uint8_t* __restrict__ status, const G1J* __restrict__ rP,
+                                                 const G2A* __restrict__ H, Fp12* __restrict__ F) {
+  const bool h = (threadIdx.x & 1) != 0;
+  const uint32_t i = blockIdx.x * 32 + (threadIdx.x >> 1);
+  const bool act = i < n && status[i] == SET_OK;
+  const uint32_t j = i < n ? i : n - 1;
+  const G1J p = rP[j];
+  PairP P;
+  P.z3 = fp_mul(fp_sqr(p.z), p.z);
+  P.nxz = fp_neg(fp_mul(p.x, p.z));
+  P.y = p.y;
+  const G2A Q = H[j];
+  PairT T{Q.x, Q.y, fp2_one()};
+  Fp6 M = fp6_sel(h, fp6_zero(), fp6_one());
+  for (int b = 62; b >= 0; --b) {
+    if (b != 62) pair_sqr(M, h);
+    Line l = pair_dbl(T, P, h);
+    pair_mul_line(M, l, h);
+    if ((X_ABS >> b) & 1ull) {
+      l = pair_add(T, Q, P, h);
+      pair_mul_line(M, l, h);
+    }
+  }
+  if (act) ((Fp6*)&F[i])[h ? 1 : 0] = h ? fp6_neg(M) : M;
 }
 
 // Signature.fromBytes(sig, true) (maybeBatch.ts:23; the "BLS deserializing signatures" perf id,
@@ -223,6 +330,15 @@ void launch_vs_agg(LaunchCfg c, const uint32_t* agg_list, const uint32_t* set_of
   debug_sync(c.stream, "k_vs_agg");
 }
 
+void launch_vs_agg_big(hipStream_t s, uint32_t n_slices, const uint4* slices, uint32_t n_big, const uint4* big, const uint32_t* arena,
+                       const G1A* table, const uint8_t* table_ok, G1J* part, uint8_t* part_bad, G1J* pk_out, uint8_t* pk_st) {
+  if (!n_big) return;
+  hipLaunchKernelGGL(k_vs_agg_big, dim3(n_slices), dim3(AGG_BIG_TPB), 0, s, slices, arena, table, table_ok, part, part_bad);
+  debug_sync(s, "k_vs_agg_big");
+  hipLaunchKernelGGL(k_vs_agg_big_fin, dim3(n_big), dim3(64), 0, s, n_big, big, part, part_bad, pk_out, pk_st);
+  debug_sync(s, "k_vs_agg_big_fin");
+}
+
 void launch_vs_hash_sig(hipStream_t s, uint32_t n, const uint8_t* msgs32, const uint32_t* set_off, const uint32_t* arena,
                         const uint8_t* raw_flag, const uint8_t* raw_pk48, const uint8_t* sig, uint32_t sig_stride, const uint32_t* sig_len,
                         const G1A* table, const uint8_t* table_ok, const G1J* pk_agg, const uint8_t* pk_st, const Seed& seed,
@@ -236,8 +352,16 @@ void launch_vs_hash_sig(hipStream_t s, uint32_t n, const uint8_t* msgs32, const 
 }
 
 void launch_vs_miller(LaunchCfg c, uint32_t n, const uint8_t* status, const G1J* rP, const G2A* H, Fp12* F) {
-  hipLaunchKernelGGL(k_vs_miller, dim3(c.blocks), dim3(64), 0, c.stream, n, status, rP, H, F);
-  debug_sync(c.stream, "k_vs_miller");
+  if (n == 0) return;
+  // lane pairs by default; GBV_VS_MILLER=thread selects one thread per set (A/B)
+  static const bool thread = getenv("GBV_VS_MILLER") && getenv("GBV_VS_MILLER")[0] == 't';
+  if (thread) {
+    hipLaunchKernelGGL(k_vs_miller, dim3((n + 63) / 64), dim3(64), 0, c.stream, n, status, rP, H, F);
+    debug_sync(c.stream, "k_vs_miller");
+  } else {
+    hipLaunchKernelGGL(k_vs_miller_pair, dim3((n + 31) / 32), dim3(64), 0, c.stream, n, status, rP, H, F);
+    debug_sync(c.stream, "k_vs_miller_pair");
+  }
 }
 
 void launch_sig_validate(LaunchCfg c, uint32_t n, const uint8_t* sig, uint32_t sig_len, uint8_t* status, uint8_t* out96) {

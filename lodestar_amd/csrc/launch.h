@@ -86,6 +86,11 @@ void launch_util_sign(LaunchCfg c, uint32_t n, const uint8_t* sk32, const uint32
 // verifySignatureSets batches (k_vs.hip)
 void launch_vs_agg(LaunchCfg c, const uint32_t* agg_list, const uint32_t* set_off, const uint32_t* arena, const G1A* table,
                    const uint8_t* table_ok, G1J* pk_out, uint8_t* pk_st);
+// large aggregate sets (>= AGG_BIG_MIN members): slices (begin, end) of AGG_SLICE members, one
+// 256-thread workgroup each, then one wave per set over its slices; big = (set, first slice, count)
+constexpr uint32_t AGG_BIG_MIN = 1024, AGG_SLICE_MEMBERS = 2048;
+void launch_vs_agg_big(hipStream_t s, uint32_t n_slices, const uint4* slices, uint32_t n_big, const uint4* big, const uint32_t* arena,
+                       const G1A* table, const uint8_t* table_ok, G1J* part, uint8_t* part_bad, G1J* pk_out, uint8_t* pk_st);
 void launch_vs_hash_sig(hipStream_t s, uint32_t n, const uint8_t* msgs32, const uint32_t* set_off, const uint32_t* arena,
                         const uint8_t* raw_flag, const uint8_t* raw_pk48, const uint8_t* sig, uint32_t sig_stride, const uint32_t* sig_len,
                         const G1A* table, const uint8_t* table_ok, const G1J* pk_agg, const uint8_t* pk_st, const Seed& seed,

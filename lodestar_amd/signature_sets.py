@@ -17,10 +17,13 @@ with hashlib, as the reference hashes them on its host; every AttestationData ro
 signing root (SigningData{object_root, domain}) is computed on the device in two batched calls
 (gbv_attestation_signing_roots, gbv_signing_roots) through the ``hasher`` -- a GpuBlsVerifier.
 
-Scope: pre-electra (phase0 .. deneb) attestations -- committee from getBeaconCommittee(slot, index)
-intersected with the aggregation bits (epochCache.ts:938-960).  ``BeaconBlock.body_root`` is the
-hash_tree_root of the block body, which the block-import pipeline computes anyway; the execution
-payload and the rest of the body are not re-hashed here.
+Attesting indices (epochCache.ts:938-973): before electra the committee of (data.slot, data.index)
+intersected with the aggregation bits; from electra on the committees named by ``committee_bits``
+(getBeaconCommittees, epochCache.ts:813-849), concatenated in committee order and intersected with
+the aggregation bits that span all of them -- up to MAX_COMMITTEES_PER_SLOT = 64 committees, i.e.
+aggregates of tens of thousands of pubkeys, which k_vs_agg_big sums on the device.
+``BeaconBlock.body_root`` is the hash_tree_root of the block body, which the block-import pipeline
+computes anyway; the execution payload and the rest of the body are not re-hashed here.
 """
 from __future__ import annotations
 
@@ -31,6 +34,8 @@ from typing import Callable, Dict, List, Optional, Sequence, Tuple
 from .verifier import AggregatedSignatureSet, ISignatureSet, SingleSignatureSet
 
 SLOTS_PER_EPOCH = 32                      # params/src/presets/mainnet.ts:38
+MAX_COMMITTEES_PER_SLOT = 64              # presets/mainnet.ts:10
+FORK_ORDER = ("phase0", "altair", "bellatrix", "capella", "deneb", "electra")  # ForkSeq (params/src/forkName.ts)
 SYNC_COMMITTEE_SIZE = 512                 # presets/mainnet.ts:90
 DOMAIN_BEACON_PROPOSER = bytes([0, 0, 0, 0])      # params/src/index.ts:139-149
 DOMAIN_BEACON_ATTESTER = bytes([1, 0, 0, 0])
@@ -115,9 +120,12 @@ class AttestationData:
 
 @dataclass
 class Attestation:
+    """phase0 Attestation, or electra's (types/src/electra/sszTypes.ts) when committee_bits is set:
+    aggregation_bits then span the committees named by committee_bits, data.index is 0."""
     aggregation_bits: Sequence[bool]
     data: AttestationData
     signature: bytes
+    committee_bits: Optional[Sequence[bool]] = None
 
 
 @dataclass
@@ -246,6 +254,10 @@ class BeaconConfig:
             self.by_name["deneb"].epoch if "deneb" in self.by_name else 2 ** 64 - 1)
         self._cache: Dict[Tuple[str, bytes], bytes] = {}
 
+    def fork_seq(self, slot: int) -> int:
+        """getForkSeq(slot): the position of the active fork in FORK_ORDER."""
+        return FORK_ORDER.index(self.fork_info(slot)[0].name)
+
     def fork_info(self, slot: int) -> Tuple[Fork, Fork]:
         """(fork at slot, the fork before it) -- chainForkConfig.getForkInfo + prevForkName."""
         epoch = compute_epoch_at_slot(slot)
@@ -288,10 +300,24 @@ class EpochState:
         self.get_beacon_committee = get_beacon_committee
         self.current_sync_committee = list(current_sync_committee)
 
-    def attesting_indices(self, att: Attestation) -> List[int]:
-        """getIndexedAttestation (epochCache.ts:938-960), pre-electra: committee intersected with the
-        aggregation bits, sorted."""
-        committee = self.get_beacon_committee(att.data.slot, att.data.index)
+    def attesting_indices(self, att: Attestation, fork_seq: Optional[int] = None) -> List[int]:
+        """getIndexedAttestation / getAttestingIndices (epochCache.ts:938-973), sorted.  Before electra
+        the committee of (slot, index); from electra on the committees of committee_bits concatenated
+        (getBeaconCommittees, :813-849).  Either way intersected with the aggregation bits, whose
+        length must match (BitArray.intersectValues)."""
+        if fork_seq is None or fork_seq < FORK_ORDER.index("electra"):
+            committee = self.get_beacon_committee(att.data.slot, att.data.index)
+        else:
+            if att.committee_bits is None:
+                raise ValueError("electra attestation without committee_bits")
+            indices = [i for i, bit in enumerate(att.committee_bits) if bit]
+            if not indices:
+                raise ValueError("Attempt to get committees without providing CommitteeIndex")
+            committee = []
+            for ci in indices:
+                if ci >= MAX_COMMITTEES_PER_SLOT:
+                    raise ValueError("COMMITTEE_INDEX_OUT_OF_RANGE %d" % ci)
+                committee.extend(self.get_beacon_committee(att.data.slot, ci))
         if len(att.aggregation_bits) != len(committee):
             raise ValueError("aggregation bits length %d != committee size %d" % (len(att.aggregation_bits), len(committee)))
         return sorted(v for v, bit in zip(committee, att.aggregation_bits) if bit)
@@ -370,8 +396,9 @@ def _block_pending(state: EpochState, signed: SignedBeaconBlock, skip_proposer_s
         out += _proposer_slashing(state, ps)
     for a_s in body.attester_slashings:
         out += [_indexed_attestation(state, a_s.attestation_1), _indexed_attestation(state, a_s.attestation_2)]
+    fork = state.config.fork_seq(b.slot)  # getForkSeq(signedBlock.message.slot), index.ts:35
     for att in body.attestations:
-        out.append(_indexed_attestation(state, IndexedAttestation(state.attesting_indices(att), att.data, att.signature)))
+        out.append(_indexed_attestation(state, IndexedAttestation(state.attesting_indices(att, fork), att.data, att.signature)))
     for se in body.voluntary_exits:
         out.append(_voluntary_exit(state, se))
     if not skip_proposer_signature:
@@ -449,5 +476,6 @@ def get_blocks_signature_sets(state: EpochState, signed_blocks: Sequence[SignedB
 
 def get_attestations_signature_sets(state: EpochState, signed_block: SignedBeaconBlock, hasher) -> List[ISignatureSet]:
     """getAttestationsSignatureSets (indexedAttestation.ts:39-51)."""
-    return _resolve([_indexed_attestation(state, IndexedAttestation(state.attesting_indices(a), a.data, a.signature))
+    fork = state.config.fork_seq(signed_block.message.slot)
+    return _resolve([_indexed_attestation(state, IndexedAttestation(state.attesting_indices(a, fork), a.data, a.signature))
                      for a in signed_block.message.body.attestations], hasher)

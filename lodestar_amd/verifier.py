@@ -10,10 +10,14 @@ Default implementation replaced: BlsMultiThreadWorkerPool (multithread/index.ts:
 The pool's scheduling semantics are kept (VerifySignatureOpts, interface.ts:4-23): batchable
 jobs wait at most MAX_BUFFER_WAIT_MS or until more than MAX_BUFFERED_SIGS signatures are buffered
 (index.ts:320-339), priority jobs go to the front (index.ts:343-349), verifyOnMainThread runs
-synchronously.  Work is dispatched to the device in groups: every queued same-message job of one
-dispatch becomes ONE device pass (gbv_verify_same_message_multi), which is what lets small gossip
-batches (32-128 sets) fill 256 CUs.  Device calls run on a worker thread (the analogue of the
-Node-API async work the addon would use), so the event loop never blocks on the GPU.
+synchronously.  Work is dispatched to the device in passes: every job queued when a pass starts
+goes into it -- the same-message jobs as ONE device batch (gbv_sm_batch_fill / submit), the
+default jobs as another (gbv_vs_batch_fill / submit) -- which is what lets small gossip batches
+(32-128 sets) fill 256 CUs.  Up to MAX_PASSES_IN_FLIGHT passes are on the device at once, each on
+its own pair of refillable batches, so the next pass's per-set kernels overlap the previous pass's
+chunk checks (the pool keeps all its workers busy the same way, index.ts:357-534).  Device calls
+run on worker threads (the analogue of the Node-API async work the addon uses), so the event
+loop never blocks on the GPU; the context's lock (include/gbv.h) makes that safe.
 
 Signature sets are in index form: pubkeys are validator indices into the HBM-resident
 index2pubkey table (state-transition/src/cache/epochCache.ts:126-133) fed by add_pubkeys()
@@ -24,16 +28,21 @@ from __future__ import annotations
 import asyncio
 import ctypes
 import time
+import weakref
 from dataclasses import dataclass, field
 from typing import List, Optional, Sequence, Tuple, Union
 
 from . import _native
 from ._native import EmptyAggregateError, GbvError, GbvSet, QueueAbortedError  # noqa: F401
+from .metrics import BlsPoolMetrics
 
 MAX_SIGNATURE_SETS_PER_JOB = 128   # multithread/index.ts:56
 MAX_BUFFERED_SIGS = 32             # multithread/index.ts:65
 MAX_BUFFER_WAIT_MS = 100           # multithread/index.ts:74
 MAX_JOBS_CAN_ACCEPT_WORK = 512     # multithread/index.ts:79
+# Device passes in flight at once (the GPU analogue of the pool's worker count, index.ts:46): with
+# three, pass k+1's per-set kernels run beside pass k's chunk tail and pass k+2 is staged.
+MAX_PASSES_IN_FLIGHT = 3
 
 # struct gbv_set as a numpy record (include/gbv.h; 40 bytes on LP64, checked against ctypes below)
 import numpy as _np  # noqa: E402
@@ -65,6 +74,23 @@ ISignatureSet = Union[SingleSignatureSet, AggregatedSignatureSet]
 
 
 @dataclass
+class PackedSameMessageSets:
+    """The ``sets`` argument of verifySignatureSetsSameMessage in packed form: validator indices
+    (u32) and their 96-byte signatures concatenated -- the layout the device stages, so large
+    gossip streams skip per-set Python objects.  The result is then a numpy bool array."""
+    indices: "_np.ndarray"
+    signatures: bytes
+
+    def __post_init__(self):
+        self.indices = _np.ascontiguousarray(self.indices, dtype=_np.uint32)
+        if len(self.signatures) != 96 * len(self.indices):
+            raise ValueError("signatures must be 96 bytes per index")
+
+    def __len__(self):
+        return len(self.indices)
+
+
+@dataclass
 class VerifySignatureOpts:
     """VerifySignatureOpts (interface.ts:4-23)."""
     batchable: bool = False
@@ -86,13 +112,25 @@ class _Job:
     kind: str  # "default" | "same_message"
     opts: VerifySignatureOpts
     future: asyncio.Future
-    sets: list
+    sets: list  # default: ISignatureSet list; same_message: (u32 index array, 96-byte signature blob)
     message: bytes = b""
+    packed: bool = False  # same_message: resolve with a numpy bool array
     added: float = field(default_factory=time.monotonic)
+
+    def n_sets(self):
+        return len(self.sets) if self.kind == "default" else len(self.sets[0])
 
     def sig_sets(self):
         # jobItemSigSets (jobItem.ts:38-45): a same-message job counts as one
         return len(self.sets) if self.kind == "default" else 1
+
+
+class _PassSlot:
+    """One device pass's pair of refillable batches (gbv_sm_batch, gbv_vs_batch)."""
+
+    def __init__(self, sm: ctypes.c_void_p, vs: ctypes.c_void_p):
+        self.sm = sm
+        self.vs = vs
 
 
 class GpuBlsVerifier:
@@ -105,14 +143,21 @@ class GpuBlsVerifier:
         if rc != _native.GBV_OK:
             raise GbvError(rc, "gbv_init(%d) failed: no usable HIP device" % device)
         self._ctx = ctx
+        self._device = int(device)
+        self._init_host_state()
+
+    def _init_host_state(self):
         self._closed = False
         self._jobs: List[_Job] = []
         self._buffered: Optional[dict] = None
-        self._busy = 0
-        self._idle: Optional[asyncio.Event] = None  # set when a running device pass ends (close())
+        self._busy = 0  # device passes in flight (the pool's workersBusy)
+        self._idle: Optional[asyncio.Event] = None  # set when the last running device pass ends (close())
         self._run_scheduled = False
-        self.metrics = {"total_sig_sets": 0, "batchable_sig_sets": 0, "same_message_sets": 0,
-                        "device_passes": 0, "same_message_retry_sets": 0}
+        self._slots: List[_PassSlot] = []  # free pass slots; a pass takes one, returns it when done
+        self._all_slots: List[_PassSlot] = []
+        self._staged = weakref.WeakSet()  # live StagedSignatureSets / StagedSameMessage handles
+        self.pool_metrics = BlsPoolMetrics()
+        self.device_passes = 0
 
     # ---- index2pubkey table ------------------------------------------------------------------
     def add_pubkeys(self, first_index: int, pubkeys: Union[bytes, Sequence[bytes]], validate: bool = False) -> bytes:
@@ -208,7 +253,7 @@ class GpuBlsVerifier:
         allv = ctypes.c_uint8(0)
         rc = self._lib.gbv_verify_sets(self._ctx, arr, len(sets), ar, ctypes.byref(allv), None)
         _native.check(self._lib, self._ctx, rc)
-        self.metrics["device_passes"] += 1
+        self.device_passes += 1
         return bool(allv.value)
 
     def _marshal_calls(self, calls: Sequence[Sequence[ISignatureSet]]):
@@ -226,7 +271,7 @@ class GpuBlsVerifier:
         out = ctypes.create_string_buffer(max(len(calls), 1))
         rc = self._lib.gbv_verify_sets_multi(self._ctx, len(calls), off.ctypes.data, arr, ar, out)
         _native.check(self._lib, self._ctx, rc)
-        self.metrics["device_passes"] += 1
+        self.device_passes += 1
         res: List[Union[bool, Exception]] = []
         for b in out.raw[:len(calls)]:
             res.append(EmptyAggregateError(_native.GBV_E_EMPTY_AGGREGATE, "EMPTY_AGGREGATE_ARRAY")
@@ -241,7 +286,9 @@ class GpuBlsVerifier:
         h = ctypes.c_void_p()
         rc = self._lib.gbv_vs_batch_create(self._ctx, len(calls), off.ctypes.data, arr, ar, ctypes.byref(h))
         _native.check(self._lib, self._ctx, rc)
-        return StagedSignatureSets(self, h, len(calls))
+        st = StagedSignatureSets(self, h, len(calls))
+        self._staged.add(st)
+        return st
 
     def vs_last_kernel_ms(self) -> List[float]:
         """Device ms of the last verifySignatureSets pass: [aggregate, hash+signature, miller, chunk checks]."""
@@ -311,7 +358,7 @@ class GpuBlsVerifier:
         ok = ctypes.c_uint8(0)
         rc = self._lib.gbv_vs_partial(self._ctx, arr, len(sets), ar, out, ctypes.byref(ok))
         _native.check(self._lib, self._ctx, rc)
-        self.metrics["device_passes"] += 1
+        self.device_passes += 1
         return out.raw, bool(ok.value)
 
     def fp12_check(self, partials: Sequence[bytes]) -> bool:
@@ -348,7 +395,7 @@ class GpuBlsVerifier:
         rc = self._lib.gbv_verify_same_message_multi(self._ctx, len(calls), offa, idxa, b"".join(sigs),
                                                      b"".join(msgs) or bytes(32), valid)
         _native.check(self._lib, self._ctx, rc)
-        self.metrics["device_passes"] += 1
+        self.device_passes += 1
         out, raw = [], valid.raw
         for g in range(len(calls)):
             out.append([raw[i] == 1 for i in range(off[g], off[g + 1])])
@@ -369,7 +416,7 @@ class GpuBlsVerifier:
         rc = self._lib.gbv_verify_same_message_multi(self._ctx, len(off) - 1, off.ctypes.data, ix.ctypes.data, bytes(sigs96) or b"\0",
                                                      bytes(msgs32) or bytes(32), valid)
         _native.check(self._lib, self._ctx, rc)
-        self.metrics["device_passes"] += 1
+        self.device_passes += 1
         return valid.raw[:n]
 
     def verify_signature_sets_same_message_sync(self, sets: Sequence[Tuple[int, bytes]], message: bytes) -> List[bool]:
@@ -387,7 +434,9 @@ class GpuBlsVerifier:
         rc = self._lib.gbv_sm_batch_create(self._ctx, len(off) - 1, off.ctypes.data, ix.ctypes.data, sigs96, msgs32,
                                            ctypes.byref(h))
         _native.check(self._lib, self._ctx, rc)
-        return StagedSameMessage(self, h, int(off[-1]))
+        st = StagedSameMessage(self, h, int(off[-1]))
+        self._staged.add(st)
+        return st
 
     def last_stats(self):
         """(fallback_chunks, failed_segments) of the last waited same-message verification."""
@@ -404,13 +453,44 @@ class GpuBlsVerifier:
         return [buf[i] for i in range(k)], [cnt[i] for i in range(k)]
 
     # ---- IBlsVerifier (async) -------------------------------------------------------------------
+    def _validate_sets(self, sets: Sequence[ISignatureSet]):
+        """Argument checks of one verifySignatureSets call, before it is queued, so that a bad call
+        rejects alone instead of failing the device pass it would share with other jobs (the
+        reference fails such a call while building its job: index2pubkey[i] / getAggregatedPubkey,
+        jobItem.ts:55-62)."""
+        n_keys = None
+        for s in sets:
+            if len(s.signing_root) != 32:
+                raise ValueError("signing root must be 32 bytes")
+            if isinstance(s, AggregatedSignatureSet):
+                idx = s.indices
+            elif s.pubkey is not None:
+                if len(s.pubkey) != 48:
+                    raise ValueError("raw pubkey must be 48 bytes")
+                continue
+            else:
+                idx = (s.index,)
+            if len(idx):
+                if n_keys is None:
+                    n_keys = self.pubkey_count
+                if min(idx) < 0 or max(idx) >= n_keys:
+                    raise GbvError(_native.GBV_E_ARG, "validator index out of range")
+
     async def verify_signature_sets(self, sets: Sequence[ISignatureSet], opts: Optional[VerifySignatureOpts] = None) -> bool:
         opts = opts or VerifySignatureOpts()
-        self.metrics["total_sig_sets"] += len(sets)
+        self._check_open()
+        m = self.pool_metrics
+        m.total_sig_sets.inc(len(sets))
+        if opts.priority:
+            m.prioritized_sig_sets.inc(len(sets))
         if opts.batchable:
-            self.metrics["batchable_sig_sets"] += len(sets)
+            m.batchable_sig_sets.inc(len(sets))
+        self._validate_sets(sets)
         if opts.verify_on_main_thread:
-            return self.verify_signature_sets_sync(sets)
+            t = time.monotonic()
+            r = self.verify_signature_sets_sync(sets)
+            m.main_thread_duration_in_thread_pool.observe(time.monotonic() - t)
+            return r
         loop = asyncio.get_running_loop()
         futs = []
         for chunk in chunkify_maximize_chunk_size(list(sets), MAX_SIGNATURE_SETS_PER_JOB):
@@ -420,28 +500,50 @@ class GpuBlsVerifier:
         results = await asyncio.gather(*futs)
         return all(r is True for r in results)
 
-    async def verify_signature_sets_same_message(self, sets: Sequence[Tuple[int, bytes]], message: bytes,
-                                                 opts: Optional[VerifySignatureOpts] = None) -> List[bool]:
+    def _pack_same_message(self, sets) -> Tuple[_np.ndarray, bytes, bool]:
+        if isinstance(sets, PackedSameMessageSets):
+            return sets.indices, bytes(sets.signatures), True
+        idx = _np.fromiter((int(i) for i, _ in sets), dtype=_np.int64, count=len(sets))
+        if len(idx) and (idx.min() < 0 or idx.max() > 0xFFFFFFFF):
+            raise GbvError(_native.GBV_E_ARG, "validator index out of range")
+        # SSZ Bytes96 on the wire; any other length throws in fromBytes -> that set is false.  It is
+        # mapped to the 96-byte all-0x00 encoding, which blst rejects (no compression bit).
+        sigs = b"".join(bytes(sig) if len(sig) == 96 else bytes(96) for _, sig in sets)
+        return idx.astype(_np.uint32), sigs, False
+
+    async def verify_signature_sets_same_message(self, sets, message: bytes,
+                                                 opts: Optional[VerifySignatureOpts] = None):
+        """verifySignatureSetsSameMessage (interface.ts:55-59): ``sets`` is a list of
+        (validator index, signature bytes) or a PackedSameMessageSets."""
         opts = opts or VerifySignatureOpts()
-        self.metrics["same_message_sets"] += len(sets)
+        self._check_open()
+        if len(message) != 32:
+            raise ValueError("message must be 32 bytes")
+        idx, sigs, packed = self._pack_same_message(sets)
+        n = len(idx)
+        if n and int(idx.max()) >= self.pubkey_count:
+            raise GbvError(_native.GBV_E_ARG, "validator index out of range")
+        m = self.pool_metrics
+        m.total_sig_sets.inc(n)
+        if opts.priority:
+            m.prioritized_sig_sets.inc(n)
+        if opts.batchable:
+            m.batchable_sig_sets.inc(n)
         loop = asyncio.get_running_loop()
         futs = []
         # chunkify here too so a job carries at most one reference chunk (index.ts:218-219); the
         # device re-applies the same chunk rule to the job it receives, which is then a no-op.
-        for chunk in chunkify_maximize_chunk_size(list(sets), MAX_SIGNATURE_SETS_PER_JOB):
+        for ch in chunkify_maximize_chunk_size(range(n), MAX_SIGNATURE_SETS_PER_JOB):
+            a, b = (ch[0], ch[-1] + 1) if ch else (0, 0)
             fut = loop.create_future()
-            self._queue(_Job("same_message", opts, fut, chunk, bytes(message)))
+            self._queue(_Job("same_message", opts, fut, (idx[a:b], sigs[96 * a:96 * b]), bytes(message), packed))
             futs.append(fut)
         results = await asyncio.gather(*futs)
+        if packed:
+            return _np.concatenate(results) if results else _np.zeros(0, dtype=bool)
         return [b for r in results for b in r]
 
-    async def close(self):
-        """close() of the pool (multithread/index.ts:238-259): queued and buffered jobs reject with
-        QUEUE_ABORTED; a device pass already running on the worker thread is awaited (its jobs
-        resolve normally) before the context -- streams, HBM table, buffers -- is destroyed."""
-        if self._closed:
-            return
-        self._closed = True
+    def _reject_pending(self):
         if self._buffered and self._buffered["timer"]:
             self._buffered["timer"].cancel()
         for job in self._jobs + (self._buffered["jobs"] + self._buffered["prio"] if self._buffered else []):
@@ -449,25 +551,44 @@ class GpuBlsVerifier:
                 job.future.set_exception(QueueAbortedError(_native.GBV_E_CLOSED, "QUEUE_ABORTED"))
         self._jobs = []
         self._buffered = None
-        while self._busy:
-            if self._idle is None:
-                self._idle = asyncio.Event()
-            await self._idle.wait()
+
+    def _destroy_device(self):
+        """Release the pass slots and staged batches, then the context (after every pass ended)."""
+        for h in list(self._staged):
+            h.close()
+        for sl in self._all_slots:
+            self._lib.gbv_sm_batch_destroy(self._ctx, sl.sm)
+            self._lib.gbv_vs_batch_destroy(self._ctx, sl.vs)
+        self._all_slots = []
+        self._slots = []
         self._lib.gbv_destroy(self._ctx)
         self._ctx = None
 
+    async def close(self):
+        """close() of the pool (multithread/index.ts:238-259): queued and buffered jobs reject with
+        QUEUE_ABORTED; device passes already running are awaited (their jobs resolve normally)
+        before the context -- streams, HBM table, buffers -- is destroyed."""
+        if self._closed:
+            return
+        self._closed = True
+        self._reject_pending()
+        while self._busy:
+            if self._idle is None:
+                self._idle = asyncio.Event()
+            self._idle.clear()
+            await self._idle.wait()
+        self._destroy_device()
+
     def close_sync(self):
-        """Synchronous close for non-async owners (tests, benches): destroys the context -- its
-        streams, HBM table and buffers -- once no device pass is running."""
+        """Synchronous close for non-async owners (tests, benches): pending jobs reject with
+        QUEUE_ABORTED like close(), then the context is destroyed (no device pass may be running)."""
         if self._closed:
             return
         if self._busy:
             raise RuntimeError("close_sync() while a device pass is running: use await close()")
         self._closed = True
-        self._jobs = []
-        self._buffered = None
-        self._lib.gbv_destroy(self._ctx)
-        self._ctx = None
+        self._reject_pending()
+        self._destroy_device()
 
     def __enter__(self):
         return self
@@ -476,10 +597,11 @@ class GpuBlsVerifier:
         self.close_sync()
 
     def can_accept_work(self) -> bool:
-        """index.ts:149-155: a device pass in flight counts as the busy pool."""
-        return self._busy == 0 and len(self._jobs) < MAX_JOBS_CAN_ACCEPT_WORK
+        """index.ts:149-155 (workersBusy < poolSize && jobs < 512): the device's passes in flight
+        play the busy workers."""
+        return self._busy < MAX_PASSES_IN_FLIGHT and len(self._jobs) < MAX_JOBS_CAN_ACCEPT_WORK
 
-    # ---- queueing (index.ts:302-352, 539-550) ------------------------------------------------
+    # ---- queueing (index.ts:302-352, 357-534, 539-550) ---------------------------------------
     def _check_open(self):
         if self._closed:
             raise QueueAbortedError(_native.GBV_E_CLOSED, "QUEUE_ABORTED")
@@ -502,6 +624,7 @@ class GpuBlsVerifier:
             else:
                 self._jobs.append(job)
             self._schedule()
+        self.pool_metrics.queue_length.set(len(self._jobs))
 
     def _run_buffered(self):
         b = self._buffered
@@ -516,49 +639,174 @@ class GpuBlsVerifier:
     def _schedule(self):
         if not self._run_scheduled:
             self._run_scheduled = True
-            asyncio.get_running_loop().call_soon(lambda: asyncio.ensure_future(self._run_jobs()))
+            asyncio.get_running_loop().call_soon(self._run_jobs)
 
-    async def _run_jobs(self):
+    def _run_jobs(self):
+        """Start device passes while jobs are queued and fewer than MAX_PASSES_IN_FLIGHT run: each
+        takes every job queued at that moment."""
         self._run_scheduled = False
-        if self._closed or self._busy or not self._jobs:
-            return
-        jobs, self._jobs = self._jobs, []
-        self._busy += 1
+        while self._jobs and not self._closed and self._busy < MAX_PASSES_IN_FLIGHT:
+            jobs, self._jobs = self._jobs, []
+            self._busy += 1
+            self.pool_metrics.workers_busy.set(self._busy)
+            self.pool_metrics.queue_length.set(0)
+            asyncio.ensure_future(self._run_pass(jobs))
+
+    def _new_slot(self) -> _PassSlot:
+        z = (ctypes.c_uint32 * 1)(0)
+        sm, vs = ctypes.c_void_p(), ctypes.c_void_p()
+        _native.check(self._lib, self._ctx, self._lib.gbv_sm_batch_create(self._ctx, 0, z, None, None, None, ctypes.byref(sm)))
+        rc = self._lib.gbv_vs_batch_create(self._ctx, 0, z, None, None, ctypes.byref(vs))
+        if rc != _native.GBV_OK:
+            self._lib.gbv_sm_batch_destroy(self._ctx, sm)
+            _native.check(self._lib, self._ctx, rc)
+        return _PassSlot(sm, vs)
+
+    @staticmethod
+    def _sm_group(jobs: Sequence[_Job]):
+        off = _np.zeros(len(jobs) + 1, dtype=_np.uint32)
+        off[1:] = _np.cumsum([len(j.sets[0]) for j in jobs])
+        idx = _np.ascontiguousarray(_np.concatenate([j.sets[0] for j in jobs]), dtype=_np.uint32)
+        return off, idx, b"".join(j.sets[1] for j in jobs) or b"\0", b"".join(j.message for j in jobs)
+
+    def _pass_submit(self, slot: Optional[_PassSlot], sm: Sequence[_Job], df: Sequence[_Job]):
+        """Worker thread: fill and submit both device batches of one pass.  Returns (slot, sm state,
+        df state), a state being None (submitted / nothing to do) or the exception of its group."""
+        lib, ctx = self._lib, self._ctx
+        if slot is None:
+            slot = self._new_slot()
+            self._all_slots.append(slot)
+        st_sm = st_df = None
+        if sm:
+            try:
+                off, idx, sigs, msgs = self._sm_group(sm)
+                _native.check(lib, ctx, lib.gbv_sm_batch_fill(ctx, slot.sm, len(sm), off.ctypes.data, idx.ctypes.data, sigs, msgs))
+                _native.check(lib, ctx, lib.gbv_sm_batch_submit(ctx, slot.sm))
+            except Exception as e:  # noqa: BLE001 -- rejects this group's promises
+                st_sm = e
+        if df:
+            try:
+                off, arr, ar, keep = self._marshal_calls([j.sets for j in df])
+                _native.check(lib, ctx, lib.gbv_vs_batch_fill(ctx, slot.vs, len(df), off.ctypes.data, arr, ar))
+                _native.check(lib, ctx, lib.gbv_vs_batch_submit(ctx, slot.vs))
+            except Exception as e:  # noqa: BLE001
+                st_df = e
+        return slot, st_sm, st_df
+
+    def _pass_wait(self, slot: _PassSlot, sm: Sequence[_Job], df: Sequence[_Job], st_sm, st_df):
+        """Worker thread: wait for both batches of a submitted pass; returns (sm result, df result):
+        the validity bytes / per-call bytes, or the group's exception."""
+        lib, ctx = self._lib, self._ctx
+        res_sm, res_df = st_sm, st_df
+        if sm and st_sm is None:
+            n = sum(len(j.sets[0]) for j in sm)
+            valid = ctypes.create_string_buffer(max(n, 1))
+            try:
+                _native.check(lib, ctx, lib.gbv_sm_batch_wait(ctx, slot.sm, valid))
+                res_sm = valid.raw[:n]
+            except Exception as e:  # noqa: BLE001
+                res_sm = e
+        if df and st_df is None:
+            out = ctypes.create_string_buffer(max(len(df), 1))
+            try:
+                _native.check(lib, ctx, lib.gbv_vs_batch_wait(ctx, slot.vs, out))
+                res_df = out.raw[:len(df)]
+            except Exception as e:  # noqa: BLE001
+                res_df = e
+        return res_sm, res_df
+
+    def _retry_default_jobs(self, df: Sequence[_Job]):
+        """Worker thread: after an argument error of a whole default group, each job alone (a bad
+        job rejects, the others resolve)."""
+        out = []
+        for j in df:
+            try:
+                out.append(self.verify_signature_sets_multi_sync([j.sets])[0])
+            except Exception as e:  # noqa: BLE001
+                out.append(e)
+        return out
+
+    async def _run_pass(self, jobs: List[_Job]):
+        m = self.pool_metrics
+        t0 = time.monotonic()
+        sm = [j for j in jobs if j.kind == "same_message"]
+        df = [j for j in jobs if j.kind == "default"]
+        m.total_jobs_groups_started.inc()
+        for kind, group in (("sameMessage", sm), ("default", df)):
+            if group:
+                m.total_jobs_started.labels(kind).inc(len(group))
+                m.total_sig_sets_started.labels(kind).inc(sum(j.n_sets() for j in group))
+        for j in jobs:
+            m.job_wait_time.observe(t0 - j.added)
+        slot = self._slots.pop() if self._slots else None
         try:
-            sm = [j for j in jobs if j.kind == "same_message"]
-            df = [j for j in jobs if j.kind == "default"]
-            if sm:
-                try:
-                    res = await asyncio.to_thread(self.verify_same_message_multi_sync, [(j.sets, j.message) for j in sm])
-                    for j, r in zip(sm, res):
-                        if not j.future.done():
-                            j.future.set_result(r)
-                except Exception as e:  # device failure rejects the whole group (index.ts:498-507)
-                    for j in sm:
-                        if not j.future.done():
-                            j.future.set_exception(e)
-            if df:
-                # every queued default job in ONE device pass; each keeps its own result (a job
-                # with an invalid set fails alone, worker.ts:73-95 / multithread.test.ts:109-129)
-                try:
-                    res = await asyncio.to_thread(self.verify_signature_sets_multi_sync, [j.sets for j in df])
-                    for j, r in zip(df, res):
-                        if j.future.done():
-                            continue
-                        if isinstance(r, Exception):
-                            j.future.set_exception(r)
-                        else:
-                            j.future.set_result(r)
-                except Exception as e:  # device failure rejects the whole group (index.ts:498-507)
-                    for j in df:
-                        if not j.future.done():
-                            j.future.set_exception(e)
+            slot, st_sm, st_df = await asyncio.to_thread(self._pass_submit, slot, sm, df)
+            res_sm, res_df = await asyncio.to_thread(self._pass_wait, slot, sm, df, st_sm, st_df)
+            if isinstance(res_df, GbvError) and res_df.code == _native.GBV_E_ARG and len(df) > 1:
+                m.batch_retries.inc()
+                res_df = await asyncio.to_thread(self._retry_default_jobs, df)
+            self.device_passes += 1
+            m.gpu_device_passes.inc()
+            m.gpu_pass_sets.observe(sum(j.n_sets() for j in jobs))
+            self._resolve_same_message(sm, res_sm)
+            self._resolve_default(df, res_df)
+        except Exception as e:  # noqa: BLE001 -- e.g. no slot could be created: reject the pass (index.ts:498-507)
+            for j in jobs:
+                if not j.future.done():
+                    j.future.set_exception(e)
         finally:
+            dt = time.monotonic() - t0
+            m.gpu_pass_time.observe(dt)
+            m.jobs_worker_time.labels(str(self._device)).inc(dt)
+            if slot is not None:
+                self._slots.append(slot)
             self._busy -= 1
+            m.workers_busy.set(self._busy)
             if self._busy == 0 and self._idle is not None:
                 self._idle.set()
-        if self._jobs and not self._closed:
-            self._schedule()
+            if self._jobs and not self._closed:
+                self._schedule()
+
+    def _resolve_same_message(self, sm: Sequence[_Job], res):
+        m = self.pool_metrics
+        if isinstance(res, Exception):  # device failure rejects the whole group (index.ts:498-507)
+            m.error_jobs_signature_sets_count.inc(sum(j.n_sets() for j in sm))
+            for j in sm:
+                if not j.future.done():
+                    j.future.set_exception(res)
+            return
+        pos = 0
+        for j in sm:
+            n = len(j.sets[0])
+            v = _np.frombuffer(res, dtype=_np.uint8, count=n, offset=pos) == 1 if n else _np.zeros(0, dtype=bool)
+            pos += n
+            ok = int(v.sum())
+            m.success_jobs_signature_sets_count.inc(n)
+            if ok == n:
+                m.batch_sigs_success.inc(n)
+            else:  # the chunk's aggregate check failed: its sets were verified one by one
+                m.same_message_retry_jobs.inc()
+                m.same_message_retry_sets.inc(n)
+            if not j.future.done():
+                j.future.set_result(v if j.packed else v.tolist())
+
+    def _resolve_default(self, df: Sequence[_Job], res):
+        m = self.pool_metrics
+        for k, j in enumerate(df):
+            if j.future.done():
+                continue
+            r = res if isinstance(res, Exception) else res[k]
+            if isinstance(r, Exception):
+                m.error_jobs_signature_sets_count.inc(len(j.sets))
+                j.future.set_exception(r)
+            elif r == _native.GBV_CALL_REJECTED:  # aggregatePublicKeys([]) threw (index.ts:398-412)
+                m.error_aggregate_signature_sets_count.labels("default").inc()
+                j.future.set_exception(EmptyAggregateError(_native.GBV_E_EMPTY_AGGREGATE, "EMPTY_AGGREGATE_ARRAY"))
+            else:
+                m.success_jobs_signature_sets_count.inc(len(j.sets))
+                if r == 1:
+                    m.batch_sigs_success.inc(len(j.sets))
+                j.future.set_result(r is True or r == 1)
 
     # ---- signing roots (SSZ hashing on the device, SURVEY 8(f) rank 3) ------------------------
     @staticmethod
@@ -681,7 +929,7 @@ class StagedSignatureSets:
         v = self._v
         out = ctypes.create_string_buffer(max(self.n_calls, 1))
         _native.check(v._lib, v._ctx, v._lib.gbv_vs_batch_wait(v._ctx, self._h, out))
-        v.metrics["device_passes"] += 1
+        v.device_passes += 1
         return list(out.raw[:self.n_calls])
 
     def verify(self) -> List[int]:
@@ -689,9 +937,10 @@ class StagedSignatureSets:
         return self.wait()
 
     def close(self):
-        if self._h:
+        # the verifier destroys live handles before its context; after that there is nothing to free
+        if self._h and self._v._ctx is not None:
             self._v._lib.gbv_vs_batch_destroy(self._v._ctx, self._h)
-            self._h = None
+        self._h = None
 
     def __del__(self):
         try:
@@ -713,7 +962,7 @@ class StagedSameMessage:
         out = ctypes.create_string_buffer(max(self.n, 1)) if want_results else None
         rc = v._lib.gbv_sm_batch_verify(v._ctx, self._h, out)
         _native.check(v._lib, v._ctx, rc)
-        v.metrics["device_passes"] += 1
+        v.device_passes += 1
         return out.raw[:self.n] if want_results else None
 
     def submit(self):
@@ -726,13 +975,13 @@ class StagedSameMessage:
         v = self._v
         out = ctypes.create_string_buffer(max(self.n, 1)) if want_results else None
         _native.check(v._lib, v._ctx, v._lib.gbv_sm_batch_wait(v._ctx, self._h, out))
-        v.metrics["device_passes"] += 1
+        v.device_passes += 1
         return out.raw[:self.n] if want_results else None
 
     def close(self):
-        if self._h:
+        if self._h and self._v._ctx is not None:
             self._v._lib.gbv_sm_batch_destroy(self._v._ctx, self._h)
-            self._h = None
+        self._h = None
 
     def __del__(self):
         try:

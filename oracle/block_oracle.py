@@ -12,7 +12,9 @@ Restates, over plain JSON-shaped dicts (the fixture format of tests/golden/c4_bl
     blsToExecutionChange.ts:19-44, block/processSyncCommittee.ts:59-111;
   * getDomain / getDomainAtFork / getDomainForVoluntaryExit, config/src/genesisConfig/index.ts:27-87,
     and computeDomain / computeForkDataRoot (:125-139);
-  * getAttestingIndices pre-electra, state-transition/src/cache/epochCache.ts:938-960.
+  * getAttestingIndices, state-transition/src/cache/epochCache.ts:953-973: pre-electra the committee of
+    (slot, index); electra the committees of committeeBits concatenated (getBeaconCommittees,
+    :813-849); either intersected with the aggregation bits (BitArray.intersectValues).
 Hashing through oracle/ssz_oracle.py (pinned by K1).  The builders under test are
 lodestar_amd/signature_sets.py; this file shares no code with them.
 """
@@ -106,9 +108,14 @@ def block_signature_sets(fix, block=None, committees=None):
             dom = get_domain(cfg, st, "attester", ia["data"]["target_epoch"] * SLOTS_PER_EPOCH)
             out.append(("aggregate", list(ia["attesting_indices"]),
                         S.compute_signing_root(S.attestation_data_root(att_data_bytes(ia["data"])), dom), sig(ia["signature"])))
+    electra = "electra" in [f[0] for f in cfg["forks"][:_fork_at(cfg, b["slot"]) + 1]]
     for att in b["attestations"]:
         d = att["data"]
-        committee = com["%d,%d" % (d["slot"], d["index"])]
+        if electra:
+            committee = [v for ci, bit in enumerate(att["committee_bits"]) if bit for v in com["%d,%d" % (d["slot"], ci)]]
+        else:
+            committee = com["%d,%d" % (d["slot"], d["index"])]
+        assert len(committee) == len(att["bits"]), "intersectValues: length mismatch"
         indices = sorted(v for v, bit in zip(committee, att["bits"]) if bit)
         dom = get_domain(cfg, st, "attester", d["target_epoch"] * SLOTS_PER_EPOCH)
         out.append(("aggregate", indices, S.compute_signing_root(S.attestation_data_root(att_data_bytes(d)), dom), sig(att["signature"])))

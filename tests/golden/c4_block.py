@@ -11,12 +11,14 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 FIX_PATH = os.path.join(HERE, "c4_block.json")
+# electra-era block: 8 attestations whose aggregation bits span up to 64 committees (committee_bits)
+FIX_PATH_ELECTRA = os.path.join(HERE, "c4_block_electra.json")
 N_VALIDATORS = 1 << 20
 N_KEYS = 1024
 
 
-def load():
-    with open(FIX_PATH) as f:
+def load(electra=False):
+    with open(FIX_PATH_ELECTRA if electra else FIX_PATH) as f:
         return json.load(f)
 
 
@@ -46,7 +48,7 @@ def to_objects(fix, block=None, committees=None):
                             for ps in b["proposer_slashings"]],
         attester_slashings=[B.AttesterSlashing(*[B.IndexedAttestation(ia["attesting_indices"], data(ia["data"]), _b(ia["signature"]))
                                                  for ia in a_s]) for a_s in b["attester_slashings"]],
-        attestations=[B.Attestation(a["bits"], data(a["data"]), _b(a["signature"])) for a in b["attestations"]],
+        attestations=[B.Attestation(a["bits"], data(a["data"]), _b(a["signature"]), a.get("committee_bits")) for a in b["attestations"]],
         voluntary_exits=[B.SignedVoluntaryExit(B.VoluntaryExit(e["message"]["epoch"], e["message"]["validator_index"]), _b(e["signature"]))
                          for e in b["voluntary_exits"]],
         sync_aggregate=B.SyncAggregate(b["sync_aggregate"]["bits"], _b(b["sync_aggregate"]["signature"])),
@@ -78,8 +80,10 @@ def corrupt(fix, kind):
     if kind == "attestation_member":
         # one committee member replaced by a validator outside the committee: the aggregate pubkey
         # no longer matches the signature
-        a = b["attestations"][7]["data"]
-        key = "%d,%d" % (a["slot"], a["index"])
+        att = b["attestations"][7]
+        a = att["data"]
+        ci = att["committee_bits"].index(True) if "committee_bits" in att else a["index"]
+        key = "%d,%d" % (a["slot"], ci)
         com = dict(com)
         members = list(com[key])
         v = (members[5] + 1) % N_VALIDATORS
@@ -115,7 +119,19 @@ def corrupt(fix, kind):
         ia = b["attester_slashings"][0][0]
         ia["attesting_indices"] = ia["attesting_indices"][:-1]
         return b, com, off["attester_slashing"]
+    if kind == "attestation_agg_bit":
+        # electra: one participant of a multi-committee aggregate dropped (its signature still counts it)
+        bits = b["attestations"][3]["bits"]
+        bits[bits.index(True)] = False
+        return b, com, off["attestation"] + 3
+    if kind == "attestation_committee_swap":
+        # electra: committee_bits name another committee of the same size than the one that signed
+        cb = b["attestations"][6]["committee_bits"]
+        i, j = cb.index(True), cb.index(False)
+        cb[i], cb[j] = False, True
+        return b, com, off["attestation"] + 6
     raise KeyError(kind)
 
 
 CORRUPTIONS = ["attestation_member", "sync_bit", "randao", "proposer", "exit", "bls_change", "proposer_slashing", "attester_slashing"]
+CORRUPTIONS_ELECTRA = CORRUPTIONS + ["attestation_agg_bit", "attestation_committee_swap"]

@@ -10,7 +10,11 @@ Expected values, all from the oracle (oracle/block_oracle.py, oracle/bls_oracle.
   * the whole block verified by the oracle's restatement of BlsMultiThreadWorkerPool
     (pool_verify_signature_sets: chunks of <=128, randomised batch, AND) -> true;
   * for every corruption kind of tests/golden/c4_block.py, the corrupted set alone -> false.
-Runtime: a few minutes on 8 cores (pure-Python pairings).  Run: python tests/golden/make_c4_fixture.py
+With --electra: tests/golden/c4_block_electra.json, an electra-era block (fork schedule up to electra)
+whose 8 attestations (MAX_ATTESTATIONS_ELECTRA) each span committees named by committee_bits --
+six over all 64 committees of their slot, one over 32, one over 17 -- so the attestation aggregates
+hold ~4 k validators each (getAttestingIndices, epochCache.ts:953-973).
+Runtime: a few minutes on 8 cores (pure-Python pairings).  Run: python tests/golden/make_c4_fixture.py [--electra]
 """
 import json
 import os
@@ -42,6 +46,16 @@ def _sign(args):
     return O.g2_compress(O.sign(sk, root)).hex()
 
 
+_PK_CACHE = {}
+
+
+def _dec(pkb):
+    p = _PK_CACHE.get(pkb)
+    if p is None:
+        p = _PK_CACHE[pkb] = O.g1_decompress(pkb)
+    return p
+
+
 def _valid_one(args):
     pkb_list, raw, root, sig = args
     if raw is not None:
@@ -50,35 +64,60 @@ def _valid_one(args):
         except O.DecodeError:
             return False
     else:
-        pk = O.aggregate_pubkeys([O.g1_decompress(p) for p in pkb_list])
+        pk = O.aggregate_pubkeys([_dec(p) for p in pkb_list])
     return O.set_is_valid(pk, root, sig)
 
 
-def main():
-    rng = np.random.Generator(np.random.PCG64(0xC4))
+def main(electra=False):
+    rng = np.random.Generator(np.random.PCG64(0xC4E if electra else 0xC4))
     rb = lambda n=32: rng.integers(0, 256, size=n, dtype=np.uint8).tobytes().hex()
     with Pool(8) as pool:
         pks = pool.map(_pk, range(K))
     sks = [O.interop_secret_key(k) for k in range(K)]
     epoch = 50
     slot = epoch * SLOTS + 5
-    cfg = {"forks": [["phase0", 0, "00000000"], ["altair", 10, "01000000"], ["bellatrix", 20, "02000000"],
-                     ["capella", 30, "03000000"], ["deneb", 40, "04000000"]],
-           "gvr": rb(), "deneb_epoch": 40}
+    forks = [["phase0", 0, "00000000"], ["altair", 10, "01000000"], ["bellatrix", 20, "02000000"],
+             ["capella", 30, "03000000"], ["deneb", 40, "04000000"]]
+    if electra:
+        forks.append(["electra", 45, "05000000"])
+    cfg = {"forks": forks, "gvr": rb(), "deneb_epoch": 40}
     committees = {}
     atts = []
-    for j in range(128):
-        a_slot = slot - 1 - (j % 8)
-        a_idx = j // 8
-        members = rng.choice(N, size=128, replace=False).astype(int).tolist()
-        committees["%d,%d" % (a_slot, a_idx)] = members
-        bits = [True] * 128
-        if j % 10 == 3:
-            for q in (1, 50, 99):
-                bits[q] = False
-        ep = a_slot // SLOTS
-        atts.append({"bits": bits, "data": {"slot": a_slot, "index": a_idx, "beacon_block_root": rb(), "source_epoch": ep - 1,
-                                            "source_root": rb(), "target_epoch": ep, "target_root": rb()}, "signature": ""})
+    if not electra:
+        for j in range(128):
+            a_slot = slot - 1 - (j % 8)
+            a_idx = j // 8
+            members = rng.choice(N, size=128, replace=False).astype(int).tolist()
+            committees["%d,%d" % (a_slot, a_idx)] = members
+            bits = [True] * 128
+            if j % 10 == 3:
+                for q in (1, 50, 99):
+                    bits[q] = False
+            ep = a_slot // SLOTS
+            atts.append({"bits": bits, "data": {"slot": a_slot, "index": a_idx, "beacon_block_root": rb(), "source_epoch": ep - 1,
+                                                "source_root": rb(), "target_epoch": ep, "target_root": rb()}, "signature": ""})
+    else:
+        # one aggregate per slot over that slot's committees (64 committees of 64 members each)
+        for j in range(8):
+            a_slot = slot - 1 - j
+            for ci in range(64):
+                committees["%d,%d" % (a_slot, ci)] = rng.choice(N, size=64, replace=False).astype(int).tolist()
+            if j < 6:
+                cbits = [True] * 64
+            elif j == 6:
+                cbits = [ci % 2 == 0 for ci in range(64)]
+            else:
+                pick = set(rng.choice(64, size=17, replace=False).tolist())
+                cbits = [ci in pick for ci in range(64)]
+            n_bits = 64 * sum(cbits)
+            bits = [True] * n_bits
+            if j % 3 == 1:
+                for q in rng.choice(n_bits, size=5, replace=False).tolist():
+                    bits[q] = False
+            ep = a_slot // SLOTS
+            atts.append({"bits": bits, "committee_bits": cbits,
+                         "data": {"slot": a_slot, "index": 0, "beacon_block_root": rb(), "source_epoch": ep - 1,
+                                  "source_root": rb(), "target_epoch": ep, "target_root": rb()}, "signature": ""})
     sync_committee = rng.choice(N, size=512, replace=False).astype(int).tolist()
     sbits = [True] * 512
     for q in rng.choice(512, size=17, replace=False).tolist():
@@ -110,11 +149,11 @@ def main():
     slots = [("randao_reveal",)]
     slots += [("proposer_slashings", 0, i, "signature") for i in range(2)]
     slots += [("attester_slashings", 0, i, "signature") for i in range(2)]
-    slots += [("attestations", j, "signature") for j in range(128)]
+    slots += [("attestations", j, "signature") for j in range(len(atts))]
     slots += [("voluntary_exits", q, "signature") for q in range(2)]
     slots += [("signature",), ("sync_aggregate", "signature"), ("bls_changes", 0, "signature")]
     sets = BO.block_signature_sets(fix)
-    assert len(sets) == len(slots) == 138
+    assert len(sets) == len(slots) == (18 if electra else 138)
     jobs = []
     for kind, key, root, _ in sets:
         if kind == "raw":
@@ -140,16 +179,17 @@ def main():
             if kind == "raw":
                 pk = {"pubkey": O.pubkey_from_bytes(key, validate=True)}
             elif kind == "single":
-                pk = {"pubkey": O.g1_decompress(bytes.fromhex(pks[key % K]))}
+                pk = {"pubkey": _dec(bytes.fromhex(pks[key % K]))}
             else:
-                pk = {"pubkeys": [O.g1_decompress(bytes.fromhex(pks[v % K])) for v in key]}
+                pk = {"pubkeys": [_dec(bytes.fromhex(pks[v % K])) for v in key]}
             out.append(dict(pk, msg=root, sig=sig))
         return out
     fix["expected_valid"] = O.pool_verify_signature_sets(pool_dicts(sets))
     assert fix["expected_valid"] is True
     corr = {}
     args = []
-    for kind in C.CORRUPTIONS:
+    kinds = C.CORRUPTIONS_ELECTRA if electra else C.CORRUPTIONS
+    for kind in kinds:
         b2, com2, k = C.corrupt(fix, kind)
         s2 = BO.block_signature_sets(fix, b2, com2)
         kind_k, key, root, sig = s2[k]
@@ -159,7 +199,7 @@ def main():
         corr[kind] = {"set": k}
     with Pool(8) as pool:
         res = pool.map(_valid_one, args)
-    for kind, r in zip(C.CORRUPTIONS, res):
+    for kind, r in zip(kinds, res):
         assert r is False, kind
         corr[kind]["valid"] = r
     fix["corruptions"] = corr
@@ -168,10 +208,11 @@ def main():
     agg = O.aggregate_pubkeys([O.g1_decompress(bytes.fromhex(pks[v % K])) for v in sync_committee])
     fix["sync_committee_aggregate"] = O.g1_compress(agg).hex()
     fix["pubkeys"] = pks
-    with open(C.FIX_PATH, "w") as f:
+    path = C.FIX_PATH_ELECTRA if electra else C.FIX_PATH
+    with open(path, "w") as f:
         json.dump(fix, f, separators=(",", ":"))
-    print("wrote %s: %d sets, %d bytes" % (C.FIX_PATH, len(sets), os.path.getsize(C.FIX_PATH)))
+    print("wrote %s: %d sets, %d bytes" % (path, len(sets), os.path.getsize(path)))
 
 
 if __name__ == "__main__":
-    main()
+    main(electra="--electra" in sys.argv)

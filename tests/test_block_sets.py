@@ -20,6 +20,7 @@ sys.path.insert(0, os.path.join(HERE, "golden"))
 import c4_block as C  # noqa: E402
 
 FIX = C.load()
+FIXE = C.load(electra=True)  # electra: 8 attestations over up to 64 committees each (committee_bits)
 R_ORDER = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
 
 
@@ -65,6 +66,46 @@ def test_builders_match_oracle_restatement():
     # signatures travel unchanged, in reference order
     assert bytes(sets[0].signature).hex() == FIX["block"]["randao_reveal"]
     assert bytes(sets[-3].signature).hex() == FIX["block"]["signature"]
+
+
+def test_electra_builders_match_oracle_restatement():
+    """getAttestingIndices from electra on (epochCache.ts:953-973): the committees of committee_bits
+    concatenated and intersected with the aggregation bits -- aggregates of ~1-4 k validators."""
+    from lodestar_amd.signature_sets import get_block_signature_sets
+    state, block = C.to_objects(FIXE)
+    h = HostHasher()
+    sets = get_block_signature_sets(state, block, h)
+    assert _as_expected(sets) == FIXE["expected_sets"]
+    assert dict(h.calls)["att"] == 8 + 2
+    sizes = [len(s.indices) for s in sets[5:13]]
+    assert min(sizes) >= 1000 and max(sizes) == 64 * 64, sizes
+    # the same block read with the pre-electra rule fails (aggregation bits span many committees)
+    from lodestar_amd import signature_sets as B
+    with pytest.raises(ValueError):
+        state.attesting_indices(block.message.body.attestations[0], B.FORK_ORDER.index("deneb"))
+
+
+def test_electra_attestation_without_committee_bits_is_rejected():
+    from lodestar_amd import signature_sets as B
+    state, block = C.to_objects(FIXE)
+    att = block.message.body.attestations[0]
+    electra = B.FORK_ORDER.index("electra")
+    with pytest.raises(ValueError):
+        state.attesting_indices(B.Attestation(att.aggregation_bits, att.data, att.signature, None), electra)
+    with pytest.raises(ValueError):  # getBeaconCommittees([]) throws
+        state.attesting_indices(B.Attestation([], att.data, att.signature, [False] * 64), electra)
+
+
+@pytest.mark.parametrize("kind", C.CORRUPTIONS_ELECTRA)
+def test_electra_builders_track_corruptions(kind):
+    from lodestar_amd.signature_sets import get_block_signature_sets
+    from oracle import block_oracle as BO
+    b2, com2, k = C.corrupt(FIXE, kind)
+    state, block = C.to_objects(FIXE, b2, com2)
+    got = _as_expected(get_block_signature_sets(state, block, HostHasher()))
+    want = [{"kind": kd, "key": key.hex() if kd == "raw" else key, "root": root.hex()} for kd, key, root, _ in BO.block_signature_sets(FIXE, b2, com2)]
+    assert got == want
+    assert FIXE["corruptions"][kind] == {"set": k, "valid": False}
 
 
 @pytest.mark.parametrize("kind", C.CORRUPTIONS)
@@ -168,6 +209,53 @@ def test_gpu_range_sync_segment_staged(gpu):
             assert st.verify() == [1 if i % 2 == 0 else 0 for i in range(16)]
     finally:
         st.close()
+
+
+@pytest.mark.gpu
+def test_gpu_electra_block_and_corruptions_one_pass(gpu):
+    """The electra block (aggregates of ~1-4 k validators: k_vs_agg_big slices) and each of its
+    corruptions as calls of one device pass: only the clean block is true (oracle-made fixture)."""
+    from lodestar_amd.signature_sets import get_block_signature_sets
+    calls = []
+    for kind in [None] + C.CORRUPTIONS_ELECTRA:
+        b2, com2 = (None, None) if kind is None else C.corrupt(FIXE, kind)[:2]
+        state, block = C.to_objects(FIXE, b2, com2)
+        calls.append(get_block_signature_sets(state, block, gpu))
+    assert _as_expected(calls[0]) == FIXE["expected_sets"]
+    res = gpu.verify_signature_sets_multi_sync(calls)
+    assert res == [FIXE["expected_valid"]] + [FIXE["corruptions"][k]["valid"] for k in C.CORRUPTIONS_ELECTRA]
+    assert res == [True] + [False] * len(C.CORRUPTIONS_ELECTRA)
+    # the electra block alone (latency form: one call) and its aggregate pubkeys byte-exact
+    assert gpu.verify_signature_sets_sync(calls[0]) is True
+    agg = calls[0][5]
+    from oracle import bls_oracle as O
+    want = O.g1_compress(O.aggregate_pubkeys([O.g1_decompress(bytes.fromhex(FIXE["pubkeys"][v % C.N_KEYS])) for v in agg.indices]))
+    assert gpu.aggregate_pubkeys(agg.indices) == want
+
+
+@pytest.mark.gpu
+def test_gpu_mixed_aggregate_sizes(gpu):
+    """Sets of 1, 2, 127, 512, 1023 (small kernel) and 1024, 2048, 2049, 5000 (sliced kernel)
+    members in one pass, each signed by the sum of its members' keys; then one member swapped."""
+    from lodestar_amd import AggregatedSignatureSet, SingleSignatureSet
+    import numpy as np
+    rng = np.random.Generator(np.random.PCG64(0xA66))
+    sizes = [1, 2, 127, 512, 1023, 1024, 2048, 2049, 5000]
+    sks = [int.from_bytes(_sk(i), "big") for i in range(C.N_KEYS)]
+    msgs = [hashlib.sha256(b"agg-size" + bytes([k])).digest() for k in range(len(sizes))]
+    members = [rng.choice(C.N_VALIDATORS, size=n, replace=False).tolist() for n in sizes]
+    agg_sk = [(sum(sks[v % C.N_KEYS] for v in m) % R_ORDER).to_bytes(32, "big") for m in members]
+    sigs = gpu.util_sign(agg_sk, list(range(len(sizes))), msgs)
+    sets = [SingleSignatureSet(m[0], msgs[k], sigs[k]) if len(m) == 1 else AggregatedSignatureSet(m, msgs[k], sigs[k])
+            for k, m in enumerate(members)]
+    calls = [[s] for s in sets] + [sets]
+    bad = []
+    for k in range(1, len(sizes)):
+        m = list(members[k])
+        m[-1] = (m[-1] + 1) % C.N_VALIDATORS  # another validator (another key: 1024 keys, consecutive indices)
+        bad.append([AggregatedSignatureSet(m, msgs[k], sigs[k])])
+    res = gpu.verify_signature_sets_multi_sync(calls + bad)
+    assert res == [True] * (len(sizes) + 1) + [False] * (len(sizes) - 1)
 
 
 @pytest.mark.gpu

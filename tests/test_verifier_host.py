@@ -8,24 +8,24 @@ import asyncio
 
 import pytest
 
+import numpy as np
+
 from lodestar_amd import QueueAbortedError, SingleSignatureSet, VerifySignatureOpts
-from lodestar_amd.verifier import GpuBlsVerifier, MAX_BUFFERED_SIGS, chunkify_maximize_chunk_size
+from lodestar_amd._native import EmptyAggregateError, GbvError
+from lodestar_amd.verifier import (AggregatedSignatureSet, GpuBlsVerifier, MAX_BUFFERED_SIGS, MAX_PASSES_IN_FLIGHT,
+                                   PackedSameMessageSets, StagedSameMessage, chunkify_maximize_chunk_size)
 
 
 class Recorder(GpuBlsVerifier):
     """GpuBlsVerifier with the device passes replaced: a set is "valid" iff its signature starts
     with 0x01; every device pass is logged."""
 
+    pubkey_count = 1 << 20  # table slots (no device to ask)
+
     def __init__(self):  # no gbv_init: nothing touches a GPU
-        self._closed = False
-        self._jobs = []
-        self._buffered = None
-        self._busy = 0
-        self._idle = None
-        self._run_scheduled = False
+        self._device = 0
+        self._init_host_state()
         self.destroyed_after = None
-        self.metrics = {"total_sig_sets": 0, "batchable_sig_sets": 0, "same_message_sets": 0,
-                        "device_passes": 0, "same_message_retry_sets": 0}
         self.passes = []
 
         rec = self
@@ -36,13 +36,33 @@ class Recorder(GpuBlsVerifier):
         self._lib = _Lib()
         self._ctx = None
 
+    # one device pass = fill + submit (recorded here) and wait (returns what submit computed)
+    def _pass_submit(self, slot, sm, df):
+        r_sm = r_df = None
+        if sm:
+            calls = [(list(zip(j.sets[0].tolist(), [j.sets[1][96 * i:96 * i + 96] for i in range(len(j.sets[0]))])), j.message)
+                     for j in sm]
+            r_sm = bytes(int(b) for r in self.verify_same_message_multi_sync(calls) for b in r)
+        if df:
+            r_df = self.verify_signature_sets_multi_sync([j.sets for j in df])
+        return object(), r_sm, r_df
+
+    def _pass_wait(self, slot, sm, df, st_sm, st_df):
+        return st_sm, st_df
+
     def verify_signature_sets_sync(self, sets):
         self.passes.append(("sets", len(sets)))
         return len(sets) > 0 and all(bytes(s.signature)[:1] == b"\x01" for s in sets)
 
     def verify_signature_sets_multi_sync(self, calls):
         self.passes.append(("multi", [len(c) for c in calls]))
-        return [len(c) > 0 and all(bytes(s.signature)[:1] == b"\x01" for s in c) for c in calls]
+        out = []
+        for c in calls:
+            if any(isinstance(s, AggregatedSignatureSet) and not s.indices for s in c):
+                out.append(EmptyAggregateError(-3, "EMPTY_AGGREGATE_ARRAY"))
+            else:
+                out.append(len(c) > 0 and all(bytes(s.signature)[:1] == b"\x01" for s in c))
+        return out
 
     def verify_same_message_multi_sync(self, calls):
         self.passes.append(("sm", [len(c[0]) for c in calls]))
@@ -139,7 +159,7 @@ def test_same_message_jobs_share_one_device_pass():
 def test_priority_jobs_go_first():
     async def go():
         v = Recorder()
-        v._busy = 1  # hold the queue as if a device pass were in flight
+        v._busy = MAX_PASSES_IN_FLIGHT  # hold the queue as if every pass slot were on the device
         f1 = asyncio.ensure_future(v.verify_signature_sets([_set()] * 2))
         f2 = asyncio.ensure_future(v.verify_signature_sets([_set()] * 5, VerifySignatureOpts(priority=True)))
         await asyncio.sleep(0)
@@ -175,36 +195,164 @@ def test_verify_on_main_thread_is_synchronous():
     assert r is True and v.passes == [("sets", 1)] and v._jobs == []
 
 
-def test_close_waits_for_the_running_device_pass():
-    """close() while a device pass runs on the worker thread: the pass finishes (its job resolves)
-    before gbv_destroy frees the context; queued jobs reject with QUEUE_ABORTED."""
-    import threading
+class Slow(Recorder):
+    """Device passes block until released (they run on worker threads, several at once)."""
 
-    class Slow(Recorder):
-        def __init__(self):
-            super().__init__()
-            self.started = threading.Event()
-            self.release = threading.Event()
+    def __init__(self):
+        super().__init__()
+        import threading
+        self.started = threading.Semaphore(0)
+        self.release = threading.Event()
 
-        def verify_signature_sets_multi_sync(self, calls):
-            self.started.set()
-            assert self.release.wait(5)
-            return super().verify_signature_sets_multi_sync(calls)
+    def verify_signature_sets_multi_sync(self, calls):
+        self.started.release()
+        assert self.release.wait(5)
+        return super().verify_signature_sets_multi_sync(calls)
 
+
+async def _wait_started(v, k):
+    for _ in range(k):
+        while not v.started.acquire(blocking=False):
+            await asyncio.sleep(0.001)
+
+
+def test_close_waits_for_the_running_device_passes():
+    """close() while device passes run on worker threads: they finish (their jobs resolve) before
+    gbv_destroy frees the context; jobs still queued reject with QUEUE_ABORTED."""
     async def go():
         v = Slow()
-        running = asyncio.ensure_future(v.verify_signature_sets([_set()]))
-        while not v.started.is_set():
-            await asyncio.sleep(0.001)
+        running = []
+        for k in range(MAX_PASSES_IN_FLIGHT):  # every pass slot busy
+            running.append(asyncio.ensure_future(v.verify_signature_sets([_set()])))
+            while v._busy < k + 1:
+                await asyncio.sleep(0)
+        await _wait_started(v, MAX_PASSES_IN_FLIGHT)
+        assert v._busy == MAX_PASSES_IN_FLIGHT and not v.can_accept_work()
         queued = asyncio.ensure_future(v.verify_signature_sets([_set()]))
         await asyncio.sleep(0)
+        assert len(v._jobs) == 1  # waits for a free pass slot
         closing = asyncio.ensure_future(v.close())
         await asyncio.sleep(0.02)
-        assert v.destroyed_after is None  # still waiting for the pass in flight
+        assert v.destroyed_after is None  # still waiting for the passes in flight
         v.release.set()
         await closing
-        assert v.destroyed_after == [("multi", [1])]
-        assert await running is True
+        assert v.destroyed_after == [("multi", [1])] * MAX_PASSES_IN_FLIGHT
+        assert [await r for r in running] == [True] * MAX_PASSES_IN_FLIGHT
         with pytest.raises(QueueAbortedError):
             await queued
     run(go())
+
+
+def test_passes_overlap_and_the_next_takes_every_queued_job():
+    """Up to MAX_PASSES_IN_FLIGHT passes run at once (index.ts:357-534 keeps every worker busy);
+    jobs queued meanwhile go into ONE pass when a slot frees up."""
+    async def go():
+        v = Slow()
+        first = []
+        for k in range(MAX_PASSES_IN_FLIGHT):  # one pass each: the next call arrives once a pass started
+            first.append(asyncio.ensure_future(v.verify_signature_sets([_set()] * (k + 1))))
+            while v._busy < k + 1:
+                await asyncio.sleep(0)
+        await _wait_started(v, MAX_PASSES_IN_FLIGHT)
+        later = [asyncio.ensure_future(v.verify_signature_sets([_set(k != 1)])) for k in range(4)]
+        await asyncio.sleep(0.01)
+        assert len(v._jobs) == 4 and not v.can_accept_work()
+        v.release.set()
+        res = await asyncio.gather(*first, *later)
+        return v, res
+    v, res = run(go())
+    assert res == [True] * MAX_PASSES_IN_FLIGHT + [True, False, True, True]
+    assert sorted(v.passes[:MAX_PASSES_IN_FLIGHT]) == [("multi", [k + 1]) for k in range(MAX_PASSES_IN_FLIGHT)]
+    assert v.passes[MAX_PASSES_IN_FLIGHT:] == [("multi", [1, 1, 1, 1])]
+    assert v.device_passes == MAX_PASSES_IN_FLIGHT + 1
+
+
+def test_invalid_call_rejects_alone_before_queueing():
+    """an out-of-range index or a malformed root rejects its own call, not the others
+    that would share its device pass."""
+    async def go():
+        v = Recorder()
+        opts = VerifySignatureOpts(batchable=True)
+        good = asyncio.ensure_future(v.verify_signature_sets([_set()], opts))
+        with pytest.raises(GbvError):
+            await v.verify_signature_sets([SingleSignatureSet(1 << 20, bytes(32), b"\x01" + bytes(95))], opts)
+        with pytest.raises(ValueError):
+            await v.verify_signature_sets([SingleSignatureSet(0, bytes(31), b"\x01" + bytes(95))], opts)
+        with pytest.raises(GbvError):
+            await v.verify_signature_sets_same_message([(1 << 20, b"\x01" + bytes(95))], bytes(32))
+        empty = asyncio.ensure_future(v.verify_signature_sets([AggregatedSignatureSet([], bytes(32), b"\x01" + bytes(95))], opts))
+        r = await good
+        with pytest.raises(EmptyAggregateError):
+            await empty
+        return v, r
+    v, r = run(go())
+    assert r is True and v.passes == [("multi", [1, 1])]
+
+
+def test_packed_same_message_sets():
+    async def go():
+        v = Recorder()
+        sigs = b"".join((b"\x01" if i % 3 else b"\x00") + bytes(95) for i in range(200))
+        r = await v.verify_signature_sets_same_message(PackedSameMessageSets(np.arange(200), sigs), bytes(32))
+        return v, r
+    v, r = run(go())
+    assert isinstance(r, np.ndarray) and r.tolist() == [i % 3 != 0 for i in range(200)]
+    assert v.passes == [("sm", [200])]  # 200 < 256: one chunk (chunkifyMaximizeChunkSize)
+
+
+def test_close_sync_rejects_buffered_jobs():
+    async def go():
+        v = Recorder()
+        fut = asyncio.ensure_future(v.verify_signature_sets([_set()], VerifySignatureOpts(batchable=True)))
+        await asyncio.sleep(0)
+        v.close_sync()
+        with pytest.raises(QueueAbortedError):
+            await fut
+        return v
+    v = run(go())
+    assert v.passes == [] and v.destroyed_after == []
+
+
+def test_staged_batches_are_released_before_the_context():
+    """staged handles still alive at close are destroyed before gbv_destroy; closing
+    them afterwards is a no-op."""
+    v = Recorder()
+    log = []
+
+    class _Lib:
+        def gbv_sm_batch_destroy(self, ctx, h):
+            log.append(("sm", ctx))
+
+        def gbv_destroy(self, ctx):
+            log.append(("ctx", ctx))
+    v._lib = _Lib()
+    v._ctx = "ctx"
+    st = StagedSameMessage(v, "h", 1)
+    v._staged.add(st)
+    v.close_sync()
+    assert log == [("sm", "ctx"), ("ctx", "ctx")]
+    st.close()
+    del st
+    assert log == [("sm", "ctx"), ("ctx", "ctx")]
+
+
+def test_metric_families_match_the_reference_names():
+    async def go():
+        v = Recorder()
+        await v.verify_signature_sets([_set(), _set(False)], VerifySignatureOpts(batchable=True, priority=True))
+        await v.verify_signature_sets_same_message([(0, b"\x01" + bytes(95)), (1, b"\x00" + bytes(95))], bytes(32))
+        return v
+    v = run(go())
+    m = v.pool_metrics
+    text = m.exposition().decode()
+    for name in ("lodestar_bls_thread_pool_sig_sets_total", "lodestar_bls_thread_pool_jobs_started_total",
+                 "lodestar_bls_thread_pool_queue_job_wait_time_seconds", "lodestar_bls_thread_pool_workers_busy",
+                 "lodestar_bls_thread_pool_same_message_sets_retries_total", "lodestar_bls_worker_thread_time_per_sigset_seconds",
+                 "lodestar_bls_thread_pool_gpu_device_passes_total"):
+        assert name in text, name
+    assert m.value("lodestar_bls_thread_pool_sig_sets_total") == 4
+    assert m.value("lodestar_bls_thread_pool_batchable_sig_sets_total") == 2
+    assert m.value("lodestar_bls_thread_pool_prioritized_sig_sets_total") == 2
+    assert m.value("lodestar_bls_thread_pool_jobs_started_total", {"type": "sameMessage"}) == 1
+    assert m.value("lodestar_bls_thread_pool_same_message_sets_retries_total") == 2
+    assert m.value("lodestar_bls_thread_pool_gpu_device_passes_total") == 2
