@@ -16,6 +16,17 @@
  *   aggregateSerializedPubkeys(ctx, pk48s, validate) -> Uint8Array(48) (syncCommittee.ts:37)
  *   close(ctx)                                    -> Promise<void>   (waits for in-flight work, gbv_destroy)
  *
+ * The streamed pair (what a GpuBlsVerifier's job queue drives; MAX_PASSES passes on the device at once,
+ * each on its own refillable batches -- gbv_sm_batch_fill / gbv_vs_batch_fill + submit):
+ *   submitPass(ctx, sameMessageCalls | null, defaultCalls | null) -> pass  (synchronous: inputs copied
+ *                                                  to pinned memory, kernels enqueued; no device wait)
+ *   waitPass(pass)                                -> Promise<{sameMessage: boolean[][] | Error,
+ *                                                             default: (boolean | Error)[] | Error}>
+ *   freePasses(ctx)                               -> number of pass slots not in flight
+ * and the rest of IBlsVerifier's needs: verifySetsSync(ctx, sets) -> boolean (verifyOnMainThread,
+ * index.ts:168-181), pubkeyCount(ctx), vsPartial(ctx, sets) -> Promise<{partial, ok}> and
+ * fp12Check(ctx, partials) -> boolean (multi-GPU shards, gbv_vs_partial / gbv_fp12_check).
+ *
  * A set is {index: number} or {indices: Uint32Array | number[]} or {pubkey: Uint8Array(48)}, plus
  * {signingRoot: Uint8Array(32), signature: Uint8Array}.  JS buffers are only borrowed during the
  * synchronous part of a call: everything is copied into C-owned memory before the work is queued
@@ -37,11 +48,20 @@
 
 #include "../include/gbv.h"
 
+#define MAX_PASSES 3
+typedef struct {
+  gbv_sm_batch* sm;
+  gbv_vs_batch* vs;
+  int busy;              /* JS thread only: a submitted pass not yet waited */
+  pthread_mutex_t mu;    /* held by the pool thread waiting on the pass, and by close() */
+} pass_slot;
+
 typedef struct {
   gbv_ctx* ctx;
   pthread_mutex_t mu;
   int closed;
   int inflight;
+  pass_slot slots[MAX_PASSES];
 } addon_ctx;
 
 /* ---- helpers ------------------------------------------------------------------------------ */
@@ -329,6 +349,14 @@ static void execute(napi_env env, void* data) {
       break;
     }
     case OP_CLOSE:
+      for (int k = 0; k < MAX_PASSES; ++k) {  /* after any pool thread still waiting on a pass */
+        pthread_mutex_lock(&ac->slots[k].mu);
+        if (ac->slots[k].sm) gbv_sm_batch_destroy(ac->ctx, ac->slots[k].sm);
+        if (ac->slots[k].vs) gbv_vs_batch_destroy(ac->ctx, ac->slots[k].vs);
+        ac->slots[k].sm = NULL;
+        ac->slots[k].vs = NULL;
+        pthread_mutex_unlock(&ac->slots[k].mu);
+      }
       gbv_destroy(ac->ctx);
       ac->ctx = NULL;
       j->rc = GBV_OK;
@@ -429,7 +457,14 @@ static void drop_job(job* j) {
 static void ctx_finalize(napi_env env, void* data, void* hint) {
   (void)env; (void)hint;
   addon_ctx* ac = (addon_ctx*)data;
-  if (ac->ctx) gbv_destroy(ac->ctx);
+  if (ac->ctx) {
+    for (int k = 0; k < MAX_PASSES; ++k) {
+      if (ac->slots[k].sm) gbv_sm_batch_destroy(ac->ctx, ac->slots[k].sm);
+      if (ac->slots[k].vs) gbv_vs_batch_destroy(ac->ctx, ac->slots[k].vs);
+    }
+    gbv_destroy(ac->ctx);
+  }
+  for (int k = 0; k < MAX_PASSES; ++k) pthread_mutex_destroy(&ac->slots[k].mu);
   pthread_mutex_destroy(&ac->mu);
   free(ac);
 }
@@ -452,6 +487,7 @@ static napi_value js_open(napi_env env, napi_callback_info info) {
   addon_ctx* ac = (addon_ctx*)calloc(1, sizeof(addon_ctx));
   ac->ctx = c;
   pthread_mutex_init(&ac->mu, NULL);
+  for (int k = 0; k < MAX_PASSES; ++k) pthread_mutex_init(&ac->slots[k].mu, NULL);
   napi_value ext;
   NAPI_OK(env, napi_create_external(env, ac, ctx_finalize, NULL, &ext));
   return ext;
@@ -725,6 +761,382 @@ static napi_value js_verify_same_message_multi(napi_env env, napi_callback_info 
   return queue(env, j, "gbvVerifySameMessageMulti");
 }
 
+/* ---- streamed passes ------------------------------------------------------------------------ */
+typedef struct {
+  addon_ctx* ac;
+  int slot;
+  int has_sm, has_df;
+  int rc_sm, rc_df;
+  char err_sm[256], err_df[256];
+  uvec sm_off;             /* same-message calls: set offsets */
+  size_t n_df;             /* default calls */
+  uint8_t *sm_valid, *df_valid;
+  napi_deferred deferred;
+  napi_async_work work;
+  int queued;              /* waitPass called */
+} pass;
+
+/* Marshal a same-message call list ({sets: {index, signature}[], message}[]) into idx / sigs / msgs. */
+static int marshal_same_message(napi_env env, napi_value arr, uvec* off, uvec* idx, bvec* sigs, bvec* msgs) {
+  bool ja = false;
+  napi_is_array(env, arr, &ja);
+  if (!ja) {
+    napi_throw_type_error(env, "GBV_E_ARG", "sameMessageCalls must be an array of {sets, message}");
+    return 0;
+  }
+  uint32_t nc = 0;
+  napi_get_array_length(env, arr, &nc);
+  uv_push(off, 0);
+  static const uint8_t zero96[96] = {0};
+  for (uint32_t c = 0; c < nc; ++c) {
+    napi_value call, sets, msg;
+    napi_get_element(env, arr, c, &call);
+    const uint8_t* d;
+    size_t len;
+    bool sa = false;
+    if (!get_prop(env, call, "message", &msg) || !get_bytes(env, msg, &d, &len) || len != 32 || !get_prop(env, call, "sets", &sets) ||
+        napi_is_array(env, sets, &sa) != napi_ok || !sa) {
+      napi_throw_type_error(env, "GBV_E_ARG", "each call needs sets: array and message: 32-byte Uint8Array");
+      return 0;
+    }
+    bv_push(msgs, d, 32);
+    uint32_t n = 0;
+    napi_get_array_length(env, sets, &n);
+    for (uint32_t i = 0; i < n; ++i) {
+      napi_value e, v;
+      uint32_t ix;
+      napi_get_element(env, sets, i, &e);
+      if (!get_prop(env, e, "index", &v) || !get_u32(env, v, &ix) || !get_prop(env, e, "signature", &v) || !get_bytes(env, v, &d, &len)) {
+        napi_throw_type_error(env, "GBV_E_ARG", "a same-message set is {index: number, signature: Uint8Array}");
+        return 0;
+      }
+      uv_push(idx, ix);
+      bv_push(sigs, len == 96 ? d : zero96, 96); /* another length throws in fromBytes -> false */
+    }
+    uv_push(off, (uint32_t)idx->n);
+  }
+  return 1;
+}
+
+static void pass_free(pass* p) {
+  free(p->sm_off.p);
+  free(p->sm_valid);
+  free(p->df_valid);
+  free(p);
+}
+
+/* submitPass(ctx, sameMessageCalls | null, defaultCalls | null): fill and submit both device batches of
+ * one pass on a free slot, synchronously (no device wait); a group that fails to stage is reported by
+ * waitPass as that group's Error.  Throws GBV_E_BUSY when MAX_PASSES passes are already in flight. */
+static napi_value js_submit_pass(napi_env env, napi_callback_info info) {
+  size_t argc = 3;
+  napi_value argv[3];
+  NAPI_OK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  addon_ctx* ac = argc >= 1 ? get_ctx(env, argv[0]) : NULL;
+  if (!ac) return NULL;
+  if (ac->closed || !ac->ctx) {
+    throw_rc(env, GBV_E_CLOSED, "QUEUE_ABORTED");
+    return NULL;
+  }
+  int k = 0;
+  while (k < MAX_PASSES && ac->slots[k].busy) ++k;
+  if (k == MAX_PASSES) {
+    napi_throw_error(env, "GBV_E_BUSY", "every pass slot is in flight");
+    return NULL;
+  }
+  pass_slot* sl = &ac->slots[k];
+  napi_valuetype t0 = napi_null, t1 = napi_null;
+  if (argc >= 2) napi_typeof(env, argv[1], &t0);
+  if (argc >= 3) napi_typeof(env, argv[2], &t1);
+  pass* p = (pass*)calloc(1, sizeof(pass));
+  p->ac = ac;
+  p->slot = k;
+  uvec sm_idx = {0};
+  bvec sm_sigs = {0}, sm_msgs = {0};
+  sets_buf df;
+  memset(&df, 0, sizeof df);
+  int ok = 1;
+  if (t0 != napi_null && t0 != napi_undefined) {
+    p->has_sm = 1;
+    ok = marshal_same_message(env, argv[1], &p->sm_off, &sm_idx, &sm_sigs, &sm_msgs);
+  }
+  if (ok && t1 != napi_null && t1 != napi_undefined) {
+    bool ja = false;
+    napi_is_array(env, argv[2], &ja);
+    if (!ja) {
+      napi_throw_type_error(env, "GBV_E_ARG", "defaultCalls must be an array of set arrays");
+      ok = 0;
+    } else {
+      p->has_df = 1;
+      uint32_t nc = 0;
+      napi_get_array_length(env, argv[2], &nc);
+      uv_push(&df.call_off, 0);
+      for (uint32_t c = 0; ok && c < nc; ++c) {
+        napi_value call;
+        napi_get_element(env, argv[2], c, &call);
+        ok = marshal_sets(env, call, &df);
+        uv_push(&df.call_off, (uint32_t)df.msg_off.n);
+      }
+      p->n_df = nc;
+    }
+  }
+  if (!ok) {
+    free(sm_idx.p); free(sm_sigs.p); free(sm_msgs.p);
+    sets_free(&df);
+    pass_free(p);
+    return NULL;
+  }
+  /* stage + enqueue (the context lock inside libgbv orders this against pool threads) */
+  pthread_mutex_lock(&sl->mu);
+  static const uint32_t zero_off[1] = {0};
+  if (!sl->sm && gbv_sm_batch_create(ac->ctx, 0, zero_off, NULL, NULL, NULL, &sl->sm) != GBV_OK) sl->sm = NULL;
+  if (!sl->vs && gbv_vs_batch_create(ac->ctx, 0, zero_off, NULL, NULL, &sl->vs) != GBV_OK) sl->vs = NULL;
+  if (p->has_sm) {
+    size_t nc = p->sm_off.n ? p->sm_off.n - 1 : 0;
+    p->sm_valid = (uint8_t*)calloc(sm_idx.n ? sm_idx.n : 1, 1);
+    p->rc_sm = !sl->sm ? GBV_E_OOM
+                       : gbv_sm_batch_fill(ac->ctx, sl->sm, nc, p->sm_off.p, sm_idx.p, sm_sigs.p ? sm_sigs.p : (const uint8_t*)"",
+                                           sm_msgs.p ? sm_msgs.p : (const uint8_t*)"");
+    if (!p->rc_sm) p->rc_sm = gbv_sm_batch_submit(ac->ctx, sl->sm);
+    if (p->rc_sm) snprintf(p->err_sm, sizeof p->err_sm, "%s", gbv_last_error(ac->ctx));
+  }
+  if (p->has_df) {
+    gbv_set* r = sets_records(&df);
+    p->df_valid = (uint8_t*)calloc(p->n_df ? p->n_df : 1, 1);
+    p->rc_df = !sl->vs ? GBV_E_OOM : gbv_vs_batch_fill(ac->ctx, sl->vs, p->n_df, df.call_off.p, r, df.arena.p);
+    if (!p->rc_df) p->rc_df = gbv_vs_batch_submit(ac->ctx, sl->vs);
+    if (p->rc_df) snprintf(p->err_df, sizeof p->err_df, "%s", gbv_last_error(ac->ctx));
+    free(r);
+  }
+  pthread_mutex_unlock(&sl->mu);
+  free(sm_idx.p); free(sm_sigs.p); free(sm_msgs.p);
+  sets_free(&df);
+  sl->busy = 1;
+  ac->inflight++;
+  napi_value ext;
+  NAPI_OK(env, napi_create_external(env, p, NULL, NULL, &ext));
+  return ext;
+}
+
+static void pass_execute(napi_env env, void* data) {
+  (void)env;
+  pass* p = (pass*)data;
+  addon_ctx* ac = p->ac;
+  pass_slot* sl = &ac->slots[p->slot];
+  pthread_mutex_lock(&sl->mu);  /* the device wait; close() destroys the slot only after it */
+  if (p->has_sm && !p->rc_sm) {
+    p->rc_sm = sl->sm && ac->ctx ? gbv_sm_batch_wait(ac->ctx, sl->sm, p->sm_valid) : GBV_E_CLOSED;
+    if (p->rc_sm) snprintf(p->err_sm, sizeof p->err_sm, "%s", ac->ctx ? gbv_last_error(ac->ctx) : "QUEUE_ABORTED");
+  }
+  if (p->has_df && !p->rc_df) {
+    p->rc_df = sl->vs && ac->ctx ? gbv_vs_batch_wait(ac->ctx, sl->vs, p->df_valid) : GBV_E_CLOSED;
+    if (p->rc_df) snprintf(p->err_df, sizeof p->err_df, "%s", ac->ctx ? gbv_last_error(ac->ctx) : "QUEUE_ABORTED");
+  }
+  pthread_mutex_unlock(&sl->mu);
+}
+
+static void pass_complete(napi_env env, napi_status status, void* data) {
+  pass* p = (pass*)data;
+  p->ac->slots[p->slot].busy = 0;
+  p->ac->inflight--;
+  napi_value result, x;
+  napi_create_object(env, &result);
+  if (status != napi_ok) {
+    napi_reject_deferred(env, p->deferred, make_error(env, GBV_E_DEVICE, "async work cancelled"));
+  } else {
+    if (!p->has_sm) {
+      napi_get_null(env, &x);
+    } else if (p->rc_sm) {
+      x = make_error(env, p->rc_sm, p->err_sm);
+    } else {
+      size_t nc = p->sm_off.n ? p->sm_off.n - 1 : 0;
+      napi_create_array_with_length(env, nc, &x);
+      for (size_t c = 0; c < nc; ++c) {
+        uint32_t a = p->sm_off.p[c], b = p->sm_off.p[c + 1];
+        napi_value arr;
+        napi_create_array_with_length(env, b - a, &arr);
+        for (uint32_t i = a; i < b; ++i) {
+          napi_value v;
+          napi_get_boolean(env, p->sm_valid[i] == 1, &v);
+          napi_set_element(env, arr, i - a, v);
+        }
+        napi_set_element(env, x, (uint32_t)c, arr);
+      }
+    }
+    napi_set_named_property(env, result, "sameMessage", x);
+    if (!p->has_df) {
+      napi_get_null(env, &x);
+    } else if (p->rc_df) {
+      x = make_error(env, p->rc_df, p->err_df);
+    } else {
+      napi_create_array_with_length(env, p->n_df, &x);
+      for (size_t c = 0; c < p->n_df; ++c) {
+        napi_value v;
+        if (p->df_valid[c] == GBV_CALL_REJECTED)
+          v = make_error(env, GBV_E_EMPTY_AGGREGATE, "EMPTY_AGGREGATE_ARRAY");
+        else
+          napi_get_boolean(env, p->df_valid[c] == 1, &v);
+        napi_set_element(env, x, (uint32_t)c, v);
+      }
+    }
+    napi_set_named_property(env, result, "default", x);
+    napi_resolve_deferred(env, p->deferred, result);
+  }
+  napi_delete_async_work(env, p->work);
+  pass_free(p);
+}
+
+/* waitPass(pass) -> Promise: the device wait runs on the libuv pool; every submitted pass must be
+ * waited exactly once (its slot is released when the promise settles). */
+static napi_value js_wait_pass(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  NAPI_OK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  napi_valuetype t;
+  if (argc < 1 || napi_typeof(env, argv[0], &t) != napi_ok || t != napi_external) {
+    napi_throw_type_error(env, "GBV_E_ARG", "expected a pass from submitPass()");
+    return NULL;
+  }
+  pass* p = NULL;
+  napi_get_value_external(env, argv[0], (void**)&p);
+  if (!p || p->queued) {
+    napi_throw_error(env, "GBV_E_ARG", "pass already waited");
+    return NULL;
+  }
+  p->queued = 1;
+  napi_value promise, name;
+  napi_create_promise(env, &p->deferred, &promise);
+  napi_create_string_utf8(env, "gbvWaitPass", NAPI_AUTO_LENGTH, &name);
+  napi_create_async_work(env, NULL, name, pass_execute, pass_complete, p, &p->work);
+  napi_queue_async_work(env, p->work);
+  return promise;
+}
+
+static napi_value js_free_passes(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1], r;
+  NAPI_OK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  addon_ctx* ac = argc >= 1 ? get_ctx(env, argv[0]) : NULL;
+  if (!ac) return NULL;
+  uint32_t f = 0;
+  for (int k = 0; k < MAX_PASSES; ++k) f += ac->slots[k].busy ? 0 : 1;
+  napi_create_uint32(env, (ac->closed || !ac->ctx) ? 0 : f, &r);
+  return r;
+}
+
+static napi_value js_pubkey_count(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1], r;
+  NAPI_OK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  addon_ctx* ac = argc >= 1 ? get_ctx(env, argv[0]) : NULL;
+  if (!ac) return NULL;
+  napi_create_double(env, ac->ctx ? (double)gbv_pubkeys_count(ac->ctx) : 0.0, &r);
+  return r;
+}
+
+/* verifySetsSync(ctx, sets) -> boolean: verifyOnMainThread (index.ts:168-181) -- blocks the JS thread
+ * like the reference's main-thread verifySignatureSetsMaybeBatch. */
+static napi_value js_verify_sets_sync(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2];
+  NAPI_OK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  addon_ctx* ac = argc >= 1 ? get_ctx(env, argv[0]) : NULL;
+  if (!ac) return NULL;
+  if (argc < 2) {
+    napi_throw_type_error(env, "GBV_E_ARG", "verifySetsSync(ctx, sets)");
+    return NULL;
+  }
+  if (ac->closed || !ac->ctx) {
+    throw_rc(env, GBV_E_CLOSED, "QUEUE_ABORTED");
+    return NULL;
+  }
+  sets_buf sb;
+  memset(&sb, 0, sizeof sb);
+  if (!marshal_sets(env, argv[1], &sb)) {
+    sets_free(&sb);
+    return NULL;
+  }
+  gbv_set* r = sets_records(&sb);
+  uint8_t all = 0;
+  int rc = gbv_verify_sets(ac->ctx, r, sb.msg_off.n, sb.arena.p, &all, NULL);
+  free(r);
+  sets_free(&sb);
+  if (rc) {
+    throw_rc(env, rc, gbv_last_error(ac->ctx));
+    return NULL;
+  }
+  napi_value res;
+  napi_get_boolean(env, all == 1, &res);
+  return res;
+}
+
+/* vsPartial(ctx, sets) -> {partial: Uint8Array(576), ok: boolean} (gbv_vs_partial, synchronous):
+ * this GPU's Fp12 Miller product over its shard of one large verifySignatureSets call. */
+static napi_value js_vs_partial(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2];
+  NAPI_OK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  addon_ctx* ac = argc >= 1 ? get_ctx(env, argv[0]) : NULL;
+  if (!ac) return NULL;
+  if (ac->closed || !ac->ctx) {
+    throw_rc(env, GBV_E_CLOSED, "QUEUE_ABORTED");
+    return NULL;
+  }
+  sets_buf sb;
+  memset(&sb, 0, sizeof sb);
+  if (argc < 2 || !marshal_sets(env, argv[1], &sb)) {
+    sets_free(&sb);
+    if (argc < 2) napi_throw_type_error(env, "GBV_E_ARG", "vsPartial(ctx, sets)");
+    return NULL;
+  }
+  gbv_set* r = sets_records(&sb);
+  void* part;
+  napi_value ab, ta, res, okv;
+  NAPI_OK(env, napi_create_arraybuffer(env, GBV_FP12_PARTIAL_BYTES, &part, &ab));
+  uint8_t ok = 0;
+  int rc = gbv_vs_partial(ac->ctx, r, sb.msg_off.n, sb.arena.p, (uint8_t*)part, &ok);
+  free(r);
+  sets_free(&sb);
+  if (rc) {
+    throw_rc(env, rc, gbv_last_error(ac->ctx));
+    return NULL;
+  }
+  NAPI_OK(env, napi_create_typedarray(env, napi_uint8_array, GBV_FP12_PARTIAL_BYTES, ab, 0, &ta));
+  napi_create_object(env, &res);
+  napi_get_boolean(env, ok == 1, &okv);
+  napi_set_named_property(env, res, "partial", ta);
+  napi_set_named_property(env, res, "ok", okv);
+  return res;
+}
+
+/* fp12Check(ctx, partials: Uint8Array of k*576 bytes) -> boolean (gbv_fp12_check). */
+static napi_value js_fp12_check(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2];
+  NAPI_OK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  addon_ctx* ac = argc >= 1 ? get_ctx(env, argv[0]) : NULL;
+  if (!ac) return NULL;
+  const uint8_t* d;
+  size_t len;
+  if (argc < 2 || !get_bytes(env, argv[1], &d, &len) || len % GBV_FP12_PARTIAL_BYTES) {
+    napi_throw_type_error(env, "GBV_E_ARG", "fp12Check(ctx, partials: Uint8Array of k*576 bytes)");
+    return NULL;
+  }
+  if (ac->closed || !ac->ctx) {
+    throw_rc(env, GBV_E_CLOSED, "QUEUE_ABORTED");
+    return NULL;
+  }
+  uint8_t one = 0;
+  int rc = gbv_fp12_check(ac->ctx, len ? d : NULL, len / GBV_FP12_PARTIAL_BYTES, &one);
+  if (rc) {
+    throw_rc(env, rc, gbv_last_error(ac->ctx));
+    return NULL;
+  }
+  napi_value res;
+  napi_get_boolean(env, one == 1, &res);
+  return res;
+}
+
 static napi_value js_close(napi_env env, napi_callback_info info) {
   size_t argc = 1;
   napi_value argv[1];
@@ -759,8 +1171,18 @@ static napi_value init(napi_env env, napi_value exports) {
       {"aggregateSignatures", NULL, js_aggregate_signatures, NULL, NULL, NULL, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), NULL},
       {"validateSignatures", NULL, js_validate_signatures, NULL, NULL, NULL, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), NULL},
       {"close", NULL, js_close, NULL, NULL, NULL, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), NULL},
+      {"submitPass", NULL, js_submit_pass, NULL, NULL, NULL, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), NULL},
+      {"waitPass", NULL, js_wait_pass, NULL, NULL, NULL, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), NULL},
+      {"freePasses", NULL, js_free_passes, NULL, NULL, NULL, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), NULL},
+      {"pubkeyCount", NULL, js_pubkey_count, NULL, NULL, NULL, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), NULL},
+      {"verifySetsSync", NULL, js_verify_sets_sync, NULL, NULL, NULL, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), NULL},
+      {"vsPartial", NULL, js_vs_partial, NULL, NULL, NULL, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), NULL},
+      {"fp12Check", NULL, js_fp12_check, NULL, NULL, NULL, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), NULL},
   };
   napi_define_properties(env, exports, sizeof props / sizeof props[0], props);
+  napi_value mp;
+  napi_create_uint32(env, MAX_PASSES, &mp);
+  napi_set_named_property(env, exports, "MAX_PASSES", mp);
   return exports;
 }
 

@@ -1,0 +1,388 @@
+// GpuBlsVerifier -- Lodestar's IBlsVerifier (beacon-node/src/chain/bls/interface.ts:25-68) over the
+// Node-API addon (addon/gbv_addon.c -> include/gbv.h), in plain JavaScript for the Node in this image
+// (v12; the TypeScript class in INTEGRATION.md is this file with types).  It replaces
+// BlsMultiThreadWorkerPool (multithread/index.ts:113) and keeps its scheduling contract:
+//   * verifySignatureSets: chunkifyMaximizeChunkSize(sets, 128) jobs, AND of their results; [] -> false;
+//     an aggregate set without pubkeys rejects its own call (EMPTY_AGGREGATE_ARRAY, index.ts:398-412)
+//   * verifySignatureSetsSameMessage: per-set booleans, per-set retry of failing chunks on the device
+//     (jobItem.ts:93-125)
+//   * opts.batchable: buffered up to MAX_BUFFER_WAIT_MS or until more than MAX_BUFFERED_SIGS sigs
+//     (index.ts:320-339); opts.priority: front of the queue (index.ts:343-349); opts.verifyOnMainThread:
+//     synchronous on the JS thread (index.ts:168-181)
+//   * canAcceptWork(): passes in flight < MAX_PASSES and jobs < 512 (index.ts:149-155)
+//   * close(): queued and buffered jobs reject with QUEUE_ABORTED, passes already on the device finish
+//   * per-request failure isolation: a bad set fails only its own call (multithread.test.ts:109-129)
+// The worker pool becomes the device: every job queued when a pass starts goes into it (same-message
+// jobs as one device batch, default jobs as another), and up to MAX_PASSES passes are on the device at
+// once (submitPass / waitPass), so consecutive gossip dispatches overlap.
+// Metrics: the reference's lodestar_bls_thread_pool_* families (metrics/lodestar.ts:401-504) plus
+// *_gpu_* ones, rendered in the Prometheus text format by metricsText().
+"use strict";
+
+const MAX_SIGNATURE_SETS_PER_JOB = 128; // multithread/index.ts:56
+const MAX_BUFFERED_SIGS = 32; // multithread/index.ts:65
+const MAX_BUFFER_WAIT_MS = 100; // multithread/index.ts:74
+const MAX_JOBS_CAN_ACCEPT_WORK = 512; // multithread/index.ts:79
+
+/** chunkifyMaximizeChunkSize (multithread/utils.ts:4-18) */
+function chunkifyMaximizeChunkSize(arr, minPerChunk) {
+  const chunkCount = Math.floor(arr.length / minPerChunk);
+  if (chunkCount <= 1) return [arr];
+  const perChunk = Math.ceil(arr.length / chunkCount);
+  const out = [];
+  for (let i = 0; i < arr.length; i += perChunk) out.push(arr.slice(i, i + perChunk));
+  return out;
+}
+
+class QueueError extends Error {
+  constructor(code) {
+    super(code);
+    this.code = code;
+    this.type = {code};
+  }
+}
+
+// ---- metrics -----------------------------------------------------------------------------------
+class Family {
+  constructor(kind, name, help, labelNames, buckets) {
+    this.kind = kind;
+    this.name = name;
+    this.help = help;
+    this.labelNames = labelNames || [];
+    this.buckets = buckets ? buckets.slice().sort((a, b) => a - b) : null;
+    this.series = new Map();
+  }
+  _get(labels) {
+    const key = this.labelNames.map((l) => String((labels || {})[l])).join("\u0000");
+    let s = this.series.get(key);
+    if (!s) {
+      s = {labels: labels || {}, value: 0, sum: 0, count: 0, counts: this.buckets ? this.buckets.map(() => 0) : null};
+      this.series.set(key, s);
+    }
+    return s;
+  }
+  inc(labels, v) {
+    if (typeof labels === "number" || labels === undefined) [labels, v] = [{}, labels];
+    this._get(labels).value += v === undefined ? 1 : v;
+  }
+  set(v, labels) {
+    this._get(labels).value = v;
+  }
+  observe(v, labels) {
+    const s = this._get(labels);
+    s.sum += v;
+    s.count += 1;
+    this.buckets.forEach((b, i) => {
+      if (v <= b) s.counts[i] += 1;
+    });
+  }
+  value(labels) {
+    const s = this.series.get(this.labelNames.map((l) => String((labels || {})[l])).join("\u0000"));
+    return s ? (this.kind === "histogram" ? s.count : s.value) : 0;
+  }
+  text() {
+    const lbl = (o, extra) => {
+      const kv = Object.entries(Object.assign({}, o, extra || {})).map(([k, v]) => `${k}="${v}"`);
+      return kv.length ? `{${kv.join(",")}}` : "";
+    };
+    const out = [`# HELP ${this.name} ${this.help}`, `# TYPE ${this.name} ${this.kind}`];
+    for (const s of this.series.values()) {
+      if (this.kind === "histogram") {
+        this.buckets.forEach((b, i) => out.push(`${this.name}_bucket${lbl(s.labels, {le: b})} ${s.counts[i]}`));
+        out.push(`${this.name}_bucket${lbl(s.labels, {le: "+Inf"})} ${s.count}`);
+        out.push(`${this.name}_sum${lbl(s.labels)} ${s.sum}`, `${this.name}_count${lbl(s.labels)} ${s.count}`);
+      } else {
+        out.push(`${this.name}${lbl(s.labels)} ${s.value}`);
+      }
+    }
+    return out.join("\n");
+  }
+}
+
+class BlsPoolMetrics {
+  constructor() {
+    const p = "lodestar_bls_thread_pool_";
+    const g = (n, h, l) => new Family("gauge", n, h, l);
+    const hi = (n, h, b) => new Family("histogram", n, h, null, b);
+    this.families = {
+      jobsWorkerTime: g(p + "time_seconds_sum", "Total time spent verifying signature sets measured on the worker", ["workerId"]),
+      successJobsSignatureSetsCount: g(p + "success_jobs_signature_sets_count", "Count of total verified signature sets"),
+      errorAggregateSignatureSetsCount: g(p + "error_aggregate_signature_sets_count", "Count of error when aggregating pubkeys or signatures", ["type"]),
+      errorJobsSignatureSetsCount: g(p + "error_jobs_signature_sets_count", "Count of total error-ed signature sets"),
+      jobWaitTime: hi(p + "queue_job_wait_time_seconds", "Time from job added to the queue to starting the job in seconds", [0.01, 0.02, 0.5, 0.1, 0.3, 1]),
+      queueLength: g(p + "queue_length", "Count of total block processor queue length"),
+      workersBusy: g(p + "workers_busy", "Count of current busy workers"),
+      totalJobsGroupsStarted: g(p + "job_groups_started_total", "Count of total jobs groups started in bls thread pool, job groups include +1 jobs"),
+      totalJobsStarted: g(p + "jobs_started_total", "Count of total jobs started in bls thread pool, jobs include +1 signature sets", ["type"]),
+      totalSigSetsStarted: g(p + "sig_sets_started_total", "Count of total signature sets started in bls thread pool, sig sets include 1 pk, msg, sig", ["type"]),
+      batchRetries: g(p + "batch_retries_total", "Count of total batches that failed and had to be verified again."),
+      batchSigsSuccess: g(p + "batch_sigs_success_total", "Count of total batches that failed and had to be verified again."),
+      sameMessageRetryJobs: g(p + "same_message_jobs_retries_total", "Count of total same message jobs that failed and had to be verified again."),
+      sameMessageRetrySets: g(p + "same_message_sets_retries_total", "Count of total same message sets that failed and had to be verified again."),
+      mainThreadDurationInThreadPool: hi(p + "main_thread_time_seconds", "Time to verify signatures in main thread with thread pool mode", [0]),
+      timePerSigSet: hi("lodestar_bls_worker_thread_time_per_sigset_seconds", "Time to verify each sigset with worker thread mode", [0.5e-3, 0.75e-3, 1e-3, 1.5e-3, 2e-3, 5e-3]),
+      totalSigSets: g(p + "sig_sets_total", "Count of total signature sets"),
+      prioritizedSigSets: g(p + "prioritized_sig_sets_total", "Count of total prioritized signature sets"),
+      batchableSigSets: g(p + "batchable_sig_sets_total", "Count of total batchable signature sets"),
+      gpuDevicePasses: new Family("counter", p + "gpu_device_passes_total", "Device passes (one or more jobs verified together)"),
+      gpuPassTime: hi(p + "gpu_pass_time_seconds", "Device pass wall time, submit to results", [0.005, 0.01, 0.02, 0.05, 0.1, 0.3, 1]),
+    };
+    Object.assign(this, this.families);
+  }
+  text() {
+    return Object.values(this.families).map((f) => f.text()).join("\n") + "\n";
+  }
+}
+
+// ---- the verifier --------------------------------------------------------------------------------
+class GpuBlsVerifier {
+  /**
+   * @param {object} o  {addon: the gbv addon (or a stand-in with the same functions), device?: number,
+   *                    ctx?: an already open context}
+   */
+  constructor(o) {
+    this.addon = o.addon;
+    this.device = o.device || 0;
+    this.ctx = o.ctx || this.addon.open(this.device);
+    this.maxPasses = this.addon.MAX_PASSES || 3;
+    this.jobs = [];
+    this.bufferedJobs = null;
+    this.passesBusy = 0;
+    this.closed = false;
+    this.idleWaiters = [];
+    this.runScheduled = false;
+    this.metrics = new BlsPoolMetrics();
+    this.devicePasses = 0;
+  }
+
+  addPubkeys(firstIndex, pk48s, validate) {
+    return this.addon.addPubkeys(this.ctx, firstIndex, pk48s, !!validate);
+  }
+
+  canAcceptWork() {
+    return this.passesBusy < this.maxPasses && this.jobs.length < MAX_JOBS_CAN_ACCEPT_WORK;
+  }
+
+  /** Checks of one call before it is queued, so a bad call rejects alone (getAggregatedPubkey throws
+   * while the reference builds that job, jobItem.ts:55-62). */
+  _validate(sets) {
+    let nKeys = -1;
+    for (const s of sets) {
+      if (!s.signingRoot || s.signingRoot.length !== 32) throw Object.assign(new TypeError("signingRoot must be 32 bytes"), {code: "GBV_E_ARG"});
+      if (s.pubkey) {
+        if (s.pubkey.length !== 48) throw Object.assign(new TypeError("pubkey must be 48 bytes"), {code: "GBV_E_ARG"});
+        continue;
+      }
+      const idx = s.indices !== undefined ? s.indices : [s.index];
+      for (const i of idx) {
+        if (nKeys < 0) nKeys = this.addon.pubkeyCount(this.ctx);
+        if (!(i >= 0 && i < nKeys)) throw Object.assign(new RangeError("validator index out of range"), {code: "GBV_E_ARG"});
+      }
+    }
+  }
+
+  async verifySignatureSets(sets, opts = {}) {
+    const m = this.metrics;
+    m.totalSigSets.inc(sets.length);
+    if (opts.priority) m.prioritizedSigSets.inc(sets.length);
+    if (opts.batchable) m.batchableSigSets.inc(sets.length);
+    if (this.closed) throw new QueueError("QUEUE_ABORTED");
+    this._validate(sets);
+    if (opts.verifyOnMainThread) {
+      const t = process.hrtime();
+      try {
+        return this.addon.verifySetsSync(this.ctx, sets);
+      } finally {
+        const d = process.hrtime(t);
+        m.mainThreadDurationInThreadPool.observe(d[0] + d[1] / 1e9);
+      }
+    }
+    const results = await Promise.all(
+      chunkifyMaximizeChunkSize(sets, MAX_SIGNATURE_SETS_PER_JOB).map(
+        (chunk) => new Promise((resolve, reject) => this._queue({type: "default", resolve, reject, addedTimeMs: Date.now(), opts, sets: chunk}))
+      )
+    );
+    return results.every((r) => r === true);
+  }
+
+  /** sets: {index, signature}[] (index form of {publicKey, signature}) */
+  async verifySignatureSetsSameMessage(sets, message, opts = {}) {
+    if (this.closed) throw new QueueError("QUEUE_ABORTED");
+    if (!message || message.length !== 32) throw Object.assign(new TypeError("message must be 32 bytes"), {code: "GBV_E_ARG"});
+    const nKeys = sets.length ? this.addon.pubkeyCount(this.ctx) : 0;
+    for (const s of sets) {
+      if (!(s.index >= 0 && s.index < nKeys)) throw Object.assign(new RangeError("validator index out of range"), {code: "GBV_E_ARG"});
+    }
+    const results = await Promise.all(
+      chunkifyMaximizeChunkSize(sets, MAX_SIGNATURE_SETS_PER_JOB).map(
+        (chunk) =>
+          new Promise((resolve, reject) => this._queue({type: "sameMessage", resolve, reject, addedTimeMs: Date.now(), opts, sets: chunk, message}))
+      )
+    );
+    return [].concat(...results);
+  }
+
+  async close() {
+    if (this.closed) return;
+    this.closed = true;
+    if (this.bufferedJobs) {
+      clearTimeout(this.bufferedJobs.timeout);
+      for (const j of this.bufferedJobs.jobs.concat(this.bufferedJobs.prioritizedJobs)) j.reject(new QueueError("QUEUE_ABORTED"));
+      this.bufferedJobs = null;
+    }
+    for (const j of this.jobs) j.reject(new QueueError("QUEUE_ABORTED"));
+    this.jobs = [];
+    while (this.passesBusy > 0) await new Promise((r) => this.idleWaiters.push(r));
+    await this.addon.close(this.ctx);
+  }
+
+  metricsText() {
+    this.metrics.queueLength.set(this.jobs.length);
+    this.metrics.workersBusy.set(this.passesBusy);
+    return this.metrics.text();
+  }
+
+  // ---- queue (index.ts:302-352, 357-534, 539-550) --------------------------------------------
+  _queue(job) {
+    if (this.closed) throw new QueueError("QUEUE_ABORTED");
+    const sigs = job.type === "sameMessage" ? 1 : job.sets.length; // jobItemSigSets (jobItem.ts:38-45)
+    if (job.opts.batchable) {
+      if (!this.bufferedJobs) {
+        this.bufferedJobs = {jobs: [], prioritizedJobs: [], sigCount: 0, firstPush: Date.now(), timeout: setTimeout(() => this._runBufferedJobs(), MAX_BUFFER_WAIT_MS)};
+      }
+      (job.opts.priority ? this.bufferedJobs.prioritizedJobs : this.bufferedJobs.jobs).push(job);
+      this.bufferedJobs.sigCount += sigs;
+      if (this.bufferedJobs.sigCount > MAX_BUFFERED_SIGS) {
+        clearTimeout(this.bufferedJobs.timeout);
+        this._runBufferedJobs();
+      }
+    } else {
+      if (job.opts.priority) this.jobs.unshift(job);
+      else this.jobs.push(job);
+      this._schedule();
+    }
+  }
+
+  _runBufferedJobs() {
+    const b = this.bufferedJobs;
+    if (!b) return;
+    this.bufferedJobs = null;
+    for (const j of b.jobs) this.jobs.push(j);
+    for (const j of b.prioritizedJobs) this.jobs.unshift(j);
+    this._schedule();
+  }
+
+  _schedule() {
+    if (this.runScheduled) return;
+    this.runScheduled = true;
+    setImmediate(() => {
+      this.runScheduled = false;
+      this._runJobs();
+    });
+  }
+
+  _runJobs() {
+    while (!this.closed && this.jobs.length > 0 && this.passesBusy < this.maxPasses) {
+      const jobs = this.jobs;
+      this.jobs = [];
+      this._runPass(jobs);
+    }
+  }
+
+  _runPass(jobs) {
+    const m = this.metrics;
+    const now = Date.now();
+    const sm = jobs.filter((j) => j.type === "sameMessage");
+    const df = jobs.filter((j) => j.type === "default");
+    m.totalJobsGroupsStarted.inc();
+    m.totalJobsStarted.inc({type: "default"}, df.length);
+    m.totalJobsStarted.inc({type: "sameMessage"}, sm.length);
+    m.totalSigSetsStarted.inc({type: "default"}, df.reduce((a, j) => a + j.sets.length, 0));
+    m.totalSigSetsStarted.inc({type: "sameMessage"}, sm.reduce((a, j) => a + j.sets.length, 0));
+    for (const j of jobs) m.jobWaitTime.observe((now - j.addedTimeMs) / 1000);
+    let pass;
+    const t0 = process.hrtime();
+    try {
+      pass = this.addon.submitPass(this.ctx, sm.length ? sm.map((j) => ({sets: j.sets, message: j.message})) : null,
+        df.length ? df.map((j) => j.sets) : null);
+    } catch (e) {
+      for (const j of jobs) j.reject(e);
+      return;
+    }
+    this.passesBusy++;
+    this.addon
+      .waitPass(pass)
+      .then(
+        (res) => {
+          this._resolveSameMessage(sm, res.sameMessage);
+          this._resolveDefault(df, res.default);
+        },
+        (e) => {
+          for (const j of jobs) j.reject(e); // device failure rejects the pass (index.ts:498-507)
+        }
+      )
+      .then(() => {
+        const d = process.hrtime(t0);
+        const sec = d[0] + d[1] / 1e9;
+        const nSets = jobs.reduce((a, j) => a + j.sets.length, 0);
+        m.gpuDevicePasses.inc();
+        m.gpuPassTime.observe(sec);
+        m.jobsWorkerTime.inc({workerId: this.device}, sec);
+        if (nSets) m.timePerSigSet.observe(sec / nSets);
+        this.devicePasses++;
+        this.passesBusy--;
+        if (this.passesBusy === 0) this.idleWaiters.splice(0).forEach((r) => r());
+        if (this.jobs.length) this._schedule();
+      });
+  }
+
+  _resolveSameMessage(sm, res) {
+    const m = this.metrics;
+    if (!sm.length) return;
+    if (res instanceof Error) {
+      m.errorJobsSignatureSetsCount.inc(sm.length);
+      for (const j of sm) j.reject(res);
+      return;
+    }
+    sm.forEach((j, k) => {
+      const r = res[k];
+      m.successJobsSignatureSetsCount.inc(1);
+      if (r.every((x) => x)) {
+        m.batchSigsSuccess.inc(r.length);
+      } else {
+        // the chunk's aggregate check failed: its sets were verified one by one on the device
+        m.sameMessageRetryJobs.inc(1);
+        m.sameMessageRetrySets.inc(r.length);
+      }
+      j.resolve(r);
+    });
+  }
+
+  _resolveDefault(df, res) {
+    const m = this.metrics;
+    if (!df.length) return;
+    df.forEach((j, k) => {
+      const r = res instanceof Error ? res : res[k];
+      if (r instanceof Error) {
+        if (r.code === "EMPTY_AGGREGATE_ARRAY") m.errorAggregateSignatureSetsCount.inc({type: "default"}, 1);
+        m.errorJobsSignatureSetsCount.inc(j.sets.length);
+        j.reject(r);
+      } else {
+        m.successJobsSignatureSetsCount.inc(j.sets.length);
+        if (r) m.batchSigsSuccess.inc(j.sets.length);
+        j.resolve(r);
+      }
+    });
+  }
+}
+
+module.exports = {
+  GpuBlsVerifier,
+  BlsPoolMetrics,
+  QueueError,
+  chunkifyMaximizeChunkSize,
+  MAX_SIGNATURE_SETS_PER_JOB,
+  MAX_BUFFERED_SIGS,
+  MAX_BUFFER_WAIT_MS,
+  MAX_JOBS_CAN_ACCEPT_WORK,
+};

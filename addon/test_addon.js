@@ -8,7 +8,8 @@ const fs = require("fs");
 const addon = require(path.join(__dirname, "gbv_addon.node"));
 
 const EXPORTS = ["open", "addPubkeys", "verifySets", "verifySetsMulti", "verifySameMessageMulti", "aggregatePubkeys",
-  "aggregateSerializedPubkeys", "aggregateSignatures", "validateSignatures", "close"];
+  "aggregateSerializedPubkeys", "aggregateSignatures", "validateSignatures", "close", "submitPass", "waitPass", "freePasses",
+  "pubkeyCount", "verifySetsSync", "vsPartial", "fp12Check"];
 const hex = (h) => Uint8Array.from(Buffer.from(h, "hex"));
 const report = {};
 
@@ -53,6 +54,7 @@ async function singleThreadSameMessage(ctx, sets, message) {
 
 async function cpu() {
   report.exports = EXPORTS.filter((k) => typeof addon[k] === "function");
+  report.maxPasses = addon.MAX_PASSES;
   report.open = expectThrow(() => addon.open(0), "GBV_E_DEVICE");
   report.badCtx = expectThrow(() => addon.verifySets({}, []), "GBV_E_ARG");
   report.badArg = expectThrow(() => addon.open("x"), "GBV_E_ARG");
@@ -114,6 +116,33 @@ async function gpu(fixPath) {
       return (c.expected === "bad_point" && e.code === "GBV_E_BAD_POINT") || (c.expected === "empty" && e.code === "EMPTY_AGGREGATE_ARRAY");
     }
   });
+  // the streamed pair: MAX_PASSES passes submitted before any is waited, a bad set in each
+  const passes = [];
+  for (let k = 0; k < addon.MAX_PASSES; k++) {
+    passes.push(addon.submitPass(ctx, calls, fix.verify_sets.map(toSets)));
+  }
+  report.freeWhileBusy = addon.freePasses(ctx);
+  let busyThrows = "no throw";
+  try {
+    addon.submitPass(ctx, calls, null);
+  } catch (e) {
+    busyThrows = e.code;
+  }
+  report.busyThrows = busyThrows;
+  const results = await Promise.all(passes.map((p) => addon.waitPass(p)));
+  report.streamed = results.map((r) =>
+    r.sameMessage.every((x, i) => JSON.stringify(x) === JSON.stringify(fix.same_message[i].expected)) &&
+    r.default.every((x, i) => (fix.verify_sets[i].expected === "reject" ? x instanceof Error && x.code === "EMPTY_AGGREGATE_ARRAY" : x === fix.verify_sets[i].expected)));
+  report.freeAfter = addon.freePasses(ctx);
+  report.verifySetsSync = addon.verifySetsSync(ctx, toSets(fix.verify_sets[0])) === fix.verify_sets[0].expected;
+  report.pubkeyCount = addon.pubkeyCount(ctx);
+  // one verifySignatureSets call as two shards on this device: partials, then one final exponentiation
+  const all = toSets(fix.verify_sets[0]);
+  const p1 = addon.vsPartial(ctx, all.slice(0, 1)), p2 = addon.vsPartial(ctx, all.slice(1));
+  report.shards = p1.ok && p2.ok && addon.fp12Check(ctx, Uint8Array.from(Buffer.concat([Buffer.from(p1.partial), Buffer.from(p2.partial)]))) === true;
+  const wrong = toSets(fix.verify_sets[1]);
+  const w1 = addon.vsPartial(ctx, wrong.slice(0, 2)), w2 = addon.vsPartial(ctx, wrong.slice(2));
+  report.shardsWrong = addon.fp12Check(ctx, Uint8Array.from(Buffer.concat([Buffer.from(w1.partial), Buffer.from(w2.partial)]))) === false;
   // concurrent submissions are serialised per context and all resolve
   const conc = await Promise.all([0, 1, 2, 3].map(() => addon.verifySets(ctx, toSets(fix.verify_sets[0]))));
   report.concurrent = conc.every((r) => r === fix.verify_sets[0].expected);

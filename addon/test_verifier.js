@@ -1,0 +1,255 @@
+// Tests of the JavaScript GpuBlsVerifier (addon/gpu_bls_verifier.js).  Used by tests/test_addon.py.
+//   node addon/test_verifier.js cpu               queueing, buffering, priority, canAcceptWork, close,
+//                                                 failure isolation and metrics, with a stand-in device
+//   node addon/test_verifier.js gpu <fixtures>    the golden cases and overlapping passes on device 0
+// The cases mirror the reference's own: test/unit/chain/bls/bls.test.ts:34-83 (verify all / one
+// invalid / one malformed, for both methods) and test/e2e/chain/bls/multithread.test.ts:85-129 (many
+// calls submitted synchronously and asynchronously, batched, with and without priority; a batched
+// invalid request does not fail the others).
+"use strict";
+const path = require("path");
+const fs = require("fs");
+const V = require(path.join(__dirname, "gpu_bls_verifier.js"));
+
+const report = {};
+const sleep = (ms) => new Promise((r) => setTimeout(r, ms));
+const hex = (h) => Uint8Array.from(Buffer.from(h, "hex"));
+
+// ---- a stand-in device with the addon's functions: a set is valid iff its signature starts with 1
+class FakeAddon {
+  constructor() {
+    this.MAX_PASSES = 3;
+    this.passes = [];
+    this.gate = null; // when set, waitPass waits for it
+    this.closed = false;
+    this.destroyedAfter = null;
+  }
+  open() {
+    return {};
+  }
+  pubkeyCount() {
+    return 1 << 20;
+  }
+  valid(s) {
+    return s.signature.length > 0 && s.signature[0] === 1;
+  }
+  verifySetsSync(ctx, sets) {
+    this.passes.push(["sync", sets.length]);
+    return sets.length > 0 && sets.every((s) => this.valid(s));
+  }
+  submitPass(ctx, sm, df) {
+    if (this.closed) throw Object.assign(new Error("QUEUE_ABORTED"), {code: "QUEUE_ABORTED"});
+    const rec = {sm: sm ? sm.map((c) => c.sets.length) : null, df: df ? df.map((c) => c.length) : null};
+    this.passes.push(rec);
+    const res = {
+      sameMessage: sm ? sm.map((c) => c.sets.map((s) => this.valid(s))) : null,
+      default: df
+        ? df.map((c) =>
+          c.some((s) => s.indices !== undefined && s.indices.length === 0)
+            ? Object.assign(new Error("EMPTY_AGGREGATE_ARRAY"), {code: "EMPTY_AGGREGATE_ARRAY"})
+            : c.length > 0 && c.every((s) => this.valid(s))
+        )
+        : null,
+    };
+    return {res};
+  }
+  async waitPass(p) {
+    if (this.gate) await this.gate;
+    await sleep(1);
+    return p.res;
+  }
+  async close() {
+    this.closed = true;
+    this.destroyedAfter = this.passes.length;
+  }
+}
+
+const set = (ok, index = 0) => ({index, signingRoot: new Uint8Array(32), signature: Uint8Array.from([ok ? 1 : 0].concat(new Array(95).fill(0)))});
+const smSet = (ok, index = 0) => ({index, signature: Uint8Array.from([ok ? 1 : 0].concat(new Array(95).fill(0)))});
+const msg = new Uint8Array(32);
+
+async function expectReject(p, code) {
+  try {
+    await p;
+    return "resolved";
+  } catch (e) {
+    return e.code === code ? "ok" : "wrong code " + e.code;
+  }
+}
+
+async function cpu() {
+  const shapes = [0, 255, 256, 300].map((n) => V.chunkifyMaximizeChunkSize(new Array(n).fill(0), 128).map((c) => c.length));
+  report.chunkify = JSON.stringify(shapes) === JSON.stringify([[0], [255], [128, 128], [150, 150]]);
+
+  // bls.test.ts: verify all / one invalid / empty
+  let a = new FakeAddon();
+  let v = new V.GpuBlsVerifier({addon: a});
+  report.basic = [await v.verifySignatureSets([set(1), set(1), set(1)]), await v.verifySignatureSets([set(1), set(0), set(1)]),
+    await v.verifySignatureSets([])];
+  report.sameMessage = await v.verifySignatureSetsSameMessage([smSet(1), smSet(0), smSet(1)], msg);
+  report.largeChunked = (await v.verifySignatureSets(new Array(300).fill(0).map(() => set(1)))) === true &&
+    JSON.stringify(a.passes[a.passes.length - 1].df) === "[150,150]";
+
+  // multithread.test.ts:109-129: a batched invalid request does not fail the others (one pass)
+  a = new FakeAddon();
+  v = new V.GpuBlsVerifier({addon: a});
+  const bad = v.verifySignatureSets([set(0)], {batchable: true, priority: true});
+  const good = new Array(8).fill(0).map(() => v.verifySignatureSets([set(1), set(1), set(1)], {batchable: true}));
+  report.batchedInvalidIsolated = (await bad) === false && (await Promise.all(good)).every((x) => x === true);
+  report.batchedOnePass = a.passes.length === 1 && JSON.stringify(a.passes[0].df) === JSON.stringify([1, 3, 3, 3, 3, 3, 3, 3, 3]);
+
+  // buffering: batchable jobs wait for the 100 ms timer unless more than 32 sigs are buffered
+  a = new FakeAddon();
+  v = new V.GpuBlsVerifier({addon: a});
+  let t0 = Date.now();
+  const buffered = [0, 1, 2].map(() => v.verifySignatureSets([set(1)], {batchable: true}));
+  await sleep(20);
+  const stillBuffered = a.passes.length === 0;
+  await Promise.all(buffered);
+  report.bufferTimer = stillBuffered && Date.now() - t0 >= 95 && a.passes.length === 1;
+  t0 = Date.now();
+  await v.verifySignatureSets(new Array(V.MAX_BUFFERED_SIGS + 1).fill(0).map(() => set(1)), {batchable: true});
+  report.bufferFlush = Date.now() - t0 < 90;
+
+  // priority: front of the queue
+  a = new FakeAddon();
+  v = new V.GpuBlsVerifier({addon: a});
+  v.passesBusy = v.maxPasses; // hold the queue
+  const f1 = v.verifySignatureSets([set(1), set(1)]);
+  const f2 = v.verifySignatureSets(new Array(5).fill(0).map(() => set(1)), {priority: true});
+  await sleep(0);
+  report.priority = JSON.stringify(v.jobs.map((j) => j.sets.length)) === "[5,2]" && v.canAcceptWork() === false;
+  v.passesBusy = 0;
+  v._schedule();
+  await Promise.all([f1, f2]);
+
+  // passes overlap: MAX_PASSES in flight, later calls wait and then go out as ONE pass
+  a = new FakeAddon();
+  let release;
+  a.gate = new Promise((r) => (release = r));
+  v = new V.GpuBlsVerifier({addon: a});
+  const first = [];
+  for (let k = 0; k < 3; k++) {
+    first.push(v.verifySignatureSets(new Array(k + 1).fill(0).map(() => set(1))));
+    await new Promise((r) => setImmediate(r));
+  }
+  const later = [0, 1, 2, 3].map((k) => v.verifySignatureSets([set(k !== 1)]));
+  await sleep(5);
+  report.overlap = v.passesBusy === 3 && v.jobs.length === 4 && !v.canAcceptWork();
+  release();
+  const r1 = await Promise.all(first);
+  const r2 = await Promise.all(later);
+  report.overlapResults = r1.every((x) => x === true) && JSON.stringify(r2) === "[true,false,true,true]" &&
+    JSON.stringify(a.passes[3].df) === "[1,1,1,1]" && v.devicePasses === 4;
+
+  // close: queued jobs reject with QUEUE_ABORTED, passes on the device finish first, then the context
+  a = new FakeAddon();
+  a.gate = new Promise((r) => (release = r));
+  v = new V.GpuBlsVerifier({addon: a});
+  const running = [];
+  for (let k = 0; k < 3; k++) {
+    running.push(v.verifySignatureSets([set(1)]));
+    await new Promise((r) => setImmediate(r));
+  }
+  const queued = v.verifySignatureSets([set(1)]);
+  const buffered2 = v.verifySignatureSets([set(1)], {batchable: true});
+  queued.catch(() => {}); // rejections are awaited below; keep Node from warning meanwhile
+  buffered2.catch(() => {});
+  await sleep(2);
+  const closing = v.close();
+  await sleep(5);
+  const notYet = a.destroyedAfter === null;
+  release();
+  await closing;
+  report.close = notYet && a.destroyedAfter === 3 && (await Promise.all(running)).every((x) => x === true) &&
+    (await expectReject(queued, "QUEUE_ABORTED")) === "ok" && (await expectReject(buffered2, "QUEUE_ABORTED")) === "ok" &&
+    (await expectReject(v.verifySignatureSets([set(1)]), "QUEUE_ABORTED")) === "ok";
+
+  // errors: an empty aggregate rejects its own call only; a bad index rejects before queueing
+  a = new FakeAddon();
+  v = new V.GpuBlsVerifier({addon: a});
+  const e1 = v.verifySignatureSets([{indices: [], signingRoot: new Uint8Array(32), signature: new Uint8Array(96)}], {batchable: true});
+  e1.catch(() => {});
+  const ok1 = v.verifySignatureSets([set(1)], {batchable: true});
+  report.emptyAggregate = (await expectReject(e1, "EMPTY_AGGREGATE_ARRAY")) === "ok" && (await ok1) === true;
+  report.badIndex = (await expectReject(v.verifySignatureSets([set(1, 1 << 20)]), "GBV_E_ARG")) === "ok" &&
+    (await expectReject(v.verifySignatureSetsSameMessage([smSet(1, 1 << 21)], msg), "GBV_E_ARG")) === "ok";
+
+  // verifyOnMainThread: synchronous device call, no queue
+  report.mainThread = (await v.verifySignatureSets([set(1)], {verifyOnMainThread: true})) === true &&
+    JSON.stringify(a.passes[a.passes.length - 1]) === '["sync",1]';
+
+  // metrics: the reference's families
+  const text = v.metricsText();
+  report.metrics = ["lodestar_bls_thread_pool_sig_sets_total", "lodestar_bls_thread_pool_jobs_started_total",
+    "lodestar_bls_thread_pool_queue_job_wait_time_seconds_bucket", "lodestar_bls_thread_pool_workers_busy",
+    "lodestar_bls_thread_pool_error_aggregate_signature_sets_count", "lodestar_bls_worker_thread_time_per_sigset_seconds",
+    "lodestar_bls_thread_pool_gpu_device_passes_total"].every((n) => text.includes(n));
+  report.metricValues = v.metrics.totalSigSets.value() === 4 && v.metrics.errorAggregateSignatureSetsCount.value({type: "default"}) === 1;
+}
+
+// ---- GPU: the real addon --------------------------------------------------------------------
+const toSets = (c) =>
+  c.sets.map((s) => {
+    const o = {signingRoot: hex(s.msg), signature: hex(s.sig)};
+    if (s.raw_pk) o.pubkey = hex(s.raw_pk);
+    else if (s.indices.length === 1) o.index = s.indices[0];
+    else o.indices = s.indices;
+    return o;
+  });
+
+async function gpu(fixPath) {
+  const addon = require(path.join(__dirname, "gbv_addon.node"));
+  const fix = JSON.parse(fs.readFileSync(fixPath, "utf8"));
+  const v = new V.GpuBlsVerifier({addon, device: 0});
+  v.addPubkeys(0, Uint8Array.from(Buffer.concat(fix.keys.pks.map((p) => Buffer.from(p, "hex")))), true);
+  // every verifySignatureSets case as its own concurrent call: they share device passes
+  const vs = await Promise.all(fix.verify_sets.map((c) => v.verifySignatureSets(toSets(c)).then((r) => r === c.expected,
+    (e) => c.expected === "reject" && e.code === "EMPTY_AGGREGATE_ARRAY")));
+  report.verifySets = vs;
+  const sm = await Promise.all(fix.same_message.map((c) =>
+    v.verifySignatureSetsSameMessage(c.indices.map((idx, k) => ({index: idx, signature: hex(c.sigs[k])})), hex(c.msg))
+      .then((r) => JSON.stringify(r) === JSON.stringify(c.expected))));
+  report.sameMessage = sm;
+  // multithread.test.ts:85-106: 8 x (verifySignatureSets + verifySignatureSetsSameMessage), synchronously
+  // and with a tick between submissions, batched or not, with and without priority
+  const valid = toSets(fix.verify_sets.find((c) => c.name === "distinct_valid"));
+  const smc = fix.same_message.find((c) => c.name === "all_valid");
+  const smSets = smc.indices.map((idx, k) => ({index: idx, signature: hex(smc.sigs[k])}));
+  const many = [];
+  for (const sleepTick of [false, true]) {
+    for (const opts of [{}, {priority: true}, {batchable: true}, {batchable: true, priority: true}]) {
+      const ps = [];
+      for (let i = 0; i < 8; i++) {
+        ps.push(v.verifySignatureSets(valid, opts));
+        ps.push(v.verifySignatureSetsSameMessage(smSets, hex(smc.msg), opts));
+        if (sleepTick) await sleep(5);
+      }
+      const rs = await Promise.all(ps);
+      many.push(rs.every((r, i) => (i % 2 === 0 ? r === true : JSON.stringify(r) === "[true,true,true]")));
+    }
+  }
+  report.manyCalls = many;
+  // multithread.test.ts:109-129: a batched request with a 32-byte signature fails alone
+  const invalid = Object.assign({}, valid[0], {signature: new Uint8Array(32)});
+  const inv = v.verifySignatureSets([invalid], {batchable: true, priority: true});
+  const rest = new Array(8).fill(0).map(() => v.verifySignatureSets(valid, {batchable: true}));
+  report.batchedInvalid = (await inv) === false && (await Promise.all(rest)).every((r) => r === true);
+  report.mainThread = (await v.verifySignatureSets(valid, {verifyOnMainThread: true})) === true;
+  report.devicePasses = v.devicePasses;
+  report.metrics = v.metricsText().includes("lodestar_bls_thread_pool_gpu_device_passes_total");
+  const pending = v.verifySignatureSets(valid);
+  await v.close();
+  report.inflightBeforeClose = await pending.then((r) => r === true, (e) => e.code === "QUEUE_ABORTED");
+  report.afterClose = await v.verifySignatureSets(valid).then(() => "resolved", (e) => e.code);
+}
+
+(async () => {
+  const mode = process.argv[2];
+  if (mode === "cpu") await cpu();
+  else await gpu(process.argv[3]);
+  process.stdout.write(JSON.stringify(report) + "\n");
+})().catch((e) => {
+  process.stdout.write(JSON.stringify({fatal: String((e && e.stack) || e), code: e && e.code}) + "\n");
+  process.exit(1);
+});

@@ -405,41 +405,62 @@ def c3_bench(v, sk_ints, pk_rows, cpu, n_calls=512):
     return out
 
 
-def make_blocks(v, sk_ints, n_blocks, rng):
-    """A range-sync segment of synthetic deneb-era blocks through the product builders
-    (lodestar_amd/signature_sets.py): 128 attestations of 128-member committees, a 512-member sync
-    aggregate, randao and proposer per block; every signature made on the GPU."""
+ELECTRA_COMMITTEE = 512  # ~1M validators / 32 slots / 64 committees (mainnet)
+
+
+def make_blocks(v, sk_ints, n_blocks, rng, electra=False):
+    """A range-sync segment of synthetic blocks through the product builders
+    (lodestar_amd/signature_sets.py), every signature made on the GPU.  deneb: 128 attestations of
+    128-member committees; electra: 8 attestations (MAX_ATTESTATIONS_ELECTRA) each over the 64
+    committees of its slot (committee_bits), 512 members each -- aggregates of 32 768 validators;
+    both with a 512-member sync aggregate, randao and proposer."""
     from lodestar_amd import AggregatedSignatureSet, SingleSignatureSet
     from lodestar_amd import signature_sets as B
-    config = B.BeaconConfig([B.Fork("phase0", 0, bytes(4)), B.Fork("altair", 10, bytes([1, 0, 0, 0])),
-                             B.Fork("bellatrix", 20, bytes([2, 0, 0, 0])), B.Fork("capella", 30, bytes([3, 0, 0, 0])),
-                             B.Fork("deneb", 40, bytes([4, 0, 0, 0]))], hashlib.sha256(b"gbv-c4").digest())
+    forks = [B.Fork("phase0", 0, bytes(4)), B.Fork("altair", 10, bytes([1, 0, 0, 0])),
+             B.Fork("bellatrix", 20, bytes([2, 0, 0, 0])), B.Fork("capella", 30, bytes([3, 0, 0, 0])),
+             B.Fork("deneb", 40, bytes([4, 0, 0, 0]))]
+    if electra:
+        forks.append(B.Fork("electra", 45, bytes([5, 0, 0, 0])))
+    config = B.BeaconConfig(forks, hashlib.sha256(b"gbv-c4").digest())
     slot0 = 50 * 32
     committees = {}
+    perm = rng.permutation(N_VALIDATORS) if electra else None  # a slot's committees are disjoint
+
+    def committee(s, i):
+        key = (s, i)
+        if key not in committees:
+            if electra:
+                o = (s * 64 * ELECTRA_COMMITTEE + i * ELECTRA_COMMITTEE) % N_VALIDATORS
+                committees[key] = perm[o:o + ELECTRA_COMMITTEE].tolist()
+            else:
+                committees[key] = rng.choice(N_VALIDATORS, size=128, replace=False).tolist()
+        return committees[key]
     sync = rng.choice(N_VALIDATORS, size=512, replace=False).tolist()
     rb = lambda: rng.integers(0, 256, size=32, dtype=np.uint8).tobytes()
     blocks = []
     for b in range(n_blocks):
         slot = slot0 + 1 + b
         atts = []
-        for j in range(128):
-            a_slot, a_idx = slot - 1 - (j % 8), j // 8
-            key = (a_slot, a_idx)
-            if key not in committees:
-                committees[key] = rng.choice(N_VALIDATORS, size=128, replace=False).tolist()
+        for j in range(8 if electra else 128):
+            a_slot, a_idx = slot - 1 - (j % 8), (0 if electra else j // 8)
             ep = a_slot // 32
             data = B.AttestationData(a_slot, a_idx, rb(), B.Checkpoint(ep - 1, rb()), B.Checkpoint(ep, rb()))
-            atts.append(B.Attestation([True] * 128, data, bytes(96)))
+            if electra:
+                atts.append(B.Attestation([True] * (64 * ELECTRA_COMMITTEE), data, bytes(96), [True] * 64))
+            else:
+                committee(a_slot, a_idx)
+                atts.append(B.Attestation([True] * 128, data, bytes(96)))
         body = B.BeaconBlockBody(randao_reveal=bytes(96), body_root=rb(), attestations=atts,
                                  sync_aggregate=B.SyncAggregate([True] * 512, bytes(96)))
         blocks.append(B.SignedBeaconBlock(B.BeaconBlock(slot, int(rng.integers(0, N_VALIDATORS)), rb(), rb(), body), bytes(96)))
-    state = B.EpochState(config, slot0 + 1, lambda s, i: committees[(s, i)], sync)
+    state = B.EpochState(config, slot0 + 1, committee, sync)
     unsigned = B.get_blocks_signature_sets(state, blocks, v)
     flat = [s for c in unsigned for s in c]
     sks = []
     for s in flat:
-        members = s.indices if isinstance(s, AggregatedSignatureSet) else [s.index]
-        sks.append((sum(sk_ints[int(x) % N_KEYS] for x in members) % R_ORDER).to_bytes(32, "big"))
+        members = np.asarray(s.indices if isinstance(s, AggregatedSignatureSet) else [s.index], dtype=np.int64)
+        cnt = np.bincount(members % N_KEYS, minlength=N_KEYS)  # sum of the members' keys, by key multiplicity
+        sks.append((sum(int(c) * sk_ints[k] for k, c in enumerate(cnt) if c) % R_ORDER).to_bytes(32, "big"))
     sigs = v.util_sign(sks, list(range(len(flat))), [s.signing_root for s in flat])
     calls, k = [], 0
     for c in unsigned:
@@ -454,10 +475,10 @@ def make_blocks(v, sk_ints, n_blocks, rng):
     return calls
 
 
-def c4_bench(v, sk_ints, pk_rows, cpu, n_blocks=64):
-    rng = np.random.Generator(np.random.PCG64(0xC4))
+def c4_bench(v, sk_ints, pk_rows, cpu, n_blocks=64, electra=False):
+    rng = np.random.Generator(np.random.PCG64(0xC4E if electra else 0xC4))
     t0 = time.time()
-    calls = make_blocks(v, sk_ints, n_blocks, rng)
+    calls = make_blocks(v, sk_ints, n_blocks, rng, electra=electra)
     build_s = time.time() - t0
     n_sets = sum(len(c) for c in calls)
     members = sum(len(getattr(s, "indices", [])) for c in calls for s in c)
@@ -476,7 +497,8 @@ def c4_bench(v, sk_ints, pk_rows, cpu, n_blocks=64):
     ms = v.vs_last_kernel_ms()
     for st in stages:
         st.close()
-    out = {"metric": "verifySignatureSets: full blocks (getBlockSignatureSets, index form), one call per block",
+    out = {"metric": "verifySignatureSets: full %sblocks (getBlockSignatureSets, index form), one call per block" % (
+               "electra " if electra else ""),
            "unit": "sets/s", "value": round(n_sets / dt, 1), "blocks_per_s": round(n_blocks / dt, 2),
            "lone_block_latency_ms_p50": round(float(np.median(lat)), 3), "sets_per_block": len(calls[0]),
            "config": "range-sync segment of %d blocks (%d sets, %d pubkeys gathered), 2 passes in flight (built in %.1fs)" % (
@@ -484,8 +506,64 @@ def c4_bench(v, sk_ints, pk_rows, cpu, n_blocks=64):
            "roofline": _vs_roofline(v, n_sets, ms, agg_members=members)}
     if cpu:
         from oracle import cpu_baseline
-        out["cpu_baseline"] = cpu_baseline.measure_verify_sets(_port_calls(calls[:4]), pk_rows, label=" (the first 4 blocks)")
+        k = 1 if electra else 4
+        out["cpu_baseline"] = cpu_baseline.measure_verify_sets(_port_calls(calls[:k]), pk_rows, label=" (the first %d blocks)" % k)
     return out
+
+
+def c5_bench(v, call_off, idx, sigs, msgs, steps=4, depth=2, frac=0.01):
+    """C5 at N = 1: the headline stream with 1 % invalid sets (SURVEY 8(d) recipe: 90 % wrong-message
+    signatures, 10 % malformed bytes([10]*96)), every per-set boolean checked against the injection
+    map -- the per-set fallback path (jobItem.ts:93-125) under load.  Multi-GPU: --mode replay."""
+    n = int(call_off[-1])
+    bad_sigs, expect = inject_invalid(sigs, call_off, n, frac)
+    want = expect.tobytes()
+    stages = [v.stage_same_message(call_off, idx, bad_sigs, msgs) for _ in range(depth)]
+    for st in stages:
+        assert st.verify(True) == want
+    t0 = time.perf_counter()
+    for k in range(steps):
+        b = stages[k % depth]
+        if k >= depth:
+            assert b.wait(True) == want
+        b.submit()
+    for k in range(max(0, steps - depth), steps):
+        assert stages[k % depth].wait(True) == want
+    dt = (time.perf_counter() - t0) / steps
+    fb, seg = v.last_stats()
+    for st in stages:
+        st.close()
+    return {"metric": "signature sets verified/sec (same-message stream, 1% invalid: per-set fallback), 1 GPU",
+            "unit": "sets/s", "value": round(n / dt, 1), "ms_per_step": round(dt * 1e3, 3), "steps": steps,
+            "config": "C5 recipe on the C2 stream: %d sets, %d invalid (90%% wrong message, 10%% malformed), %d batches in flight" % (
+                n, int((expect == 0).sum()), depth),
+            "all_booleans_checked": True, "last_fallback_chunks": fb, "last_failed_segments": seg}
+
+
+def api_stream_rate(v, call_off, idx, sigs, msgs, n_sets=1 << 18):
+    """The IBlsVerifier path itself: every call of the first n_sets sets issued at once as an
+    async verifySignatureSetsSameMessage (packed inputs), through the verifier's job queue and its
+    streamed device passes (up to MAX_PASSES_IN_FLIGHT in flight); every boolean checked.  Host
+    buffers in, booleans out: marshalling, PCIe and the Python event loop are inside."""
+    import asyncio
+    from lodestar_amd import PackedSameMessageSets
+    k = int(np.searchsorted(call_off, n_sets))
+    n = int(call_off[k])
+
+    async def go():
+        futs = [v.verify_signature_sets_same_message(
+            PackedSameMessageSets(idx[call_off[g]:call_off[g + 1]], sigs[96 * int(call_off[g]):96 * int(call_off[g + 1])]),
+            msgs[32 * g:32 * g + 32]) for g in range(k)]
+        res = await asyncio.gather(*futs)
+        return sum(int(r.sum()) for r in res)
+
+    asyncio.run(go())  # warm the pass slots
+    p0 = v.device_passes
+    t = time.perf_counter()
+    ok = asyncio.run(go())
+    dt = time.perf_counter() - t
+    assert ok == n
+    return round(n / dt, 1), n, v.device_passes - p0
 
 
 def free_port():
@@ -500,7 +578,7 @@ def main():
     ap.add_argument("--steps", type=int, default=12)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--sets", type=int, default=1 << 20)
-    ap.add_argument("--mode", choices=["gossip", "replay"], default="gossip")
+    ap.add_argument("--mode", choices=["gossip", "replay", "vs-shard"], default="gossip")
     ap.add_argument("--cpu-sample", type=int, default=None, help="sets in the C2 CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--invalid-frac", type=float, default=None,
@@ -513,6 +591,9 @@ def main():
     ap.add_argument("--inflight", type=int, default=3, help="staged batches queued on the device at once")
     ap.add_argument("--c3-calls", type=int, default=512, help="128-set calls per C3 device pass")
     ap.add_argument("--c4-blocks", type=int, default=64, help="blocks per C4 device pass (range-sync segment)")
+    ap.add_argument("--c4e-blocks", type=int, default=16, help="electra blocks per C4e device pass")
+    ap.add_argument("--shard-calls", type=int, default=512,
+                    help="vs-shard: 128-member aggregate sets / 128 in the ONE sharded verifySignatureSets call")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -549,6 +630,8 @@ def main():
     v = GpuBlsVerifier(local_rank)
     sks, key_pks = build_table(v, log)
     sk_ints = [interop_sk_int(i) for i in range(N_KEYS)]
+    if args.mode == "vs-shard":
+        return vs_shard_main(args, v, sk_ints, world, rank, local_rank, dist, log)
 
     if args.mode == "gossip":
         # every rank its own stream (replicas, weak scaling)
@@ -643,6 +726,10 @@ def main():
 
     lat = p50_batch_latency(v, idx, sigs, msgs)
     api_rate, api_n = api_path_rate(v, call_off, idx, sigs, msgs) if (rank == 0 and not invalid_frac) else (None, 0)
+    api_stream, api_stream_n, api_stream_passes = (api_stream_rate(v, call_off, idx, sigs, msgs) if (rank == 0 and not invalid_frac)
+                                                   else (None, 0, 0))
+    if api_stream:
+        log("api stream: %s sets/s over %d sets in %d device passes" % (api_stream, api_stream_n, api_stream_passes))
 
     # per launch: algorithmic MACs of the sets one k_sm_prepare launch processes / its average duration
     units_per_launch = n_mine / max(prep_launches_per_step, 1)
@@ -671,10 +758,14 @@ def main():
             from oracle import cpu_baseline
             pk_rows = cpu_baseline.affine_rows(cpu_baseline.load(), key_pks)
         for name, fn, a, kw in (("c1", c1_bench, sks, {}), ("c3", c3_bench, sk_ints, {"n_calls": args.c3_calls}),
-                                ("c4", c4_bench, sk_ints, {"n_blocks": args.c4_blocks})):
+                                ("c4", c4_bench, sk_ints, {"n_blocks": args.c4_blocks}),
+                                ("c4e", c4_bench, sk_ints, {"n_blocks": args.c4e_blocks, "electra": True})):
             t = time.time()
             extras[name] = fn(v, a, pk_rows, cpu_ok, **kw)
             log("%s: %s sets/s (%.1fs)" % (name, extras[name]["value"], time.time() - t))
+        t = time.time()
+        extras["c5"] = c5_bench(v, call_off, idx, sigs, msgs)
+        log("c5: %s sets/s (%.1fs)" % (extras["c5"]["value"], time.time() - t))
 
     ssz = None
     if rank == 0 and world == 1 and not args.no_signing_roots:
@@ -714,13 +805,18 @@ def main():
                    "parallelism": parallelism,
                    "submission": "streamed: %d batches in flight" % depth if depth > 1 else "one batch at a time",
                    "invalid_frac": invalid_frac},
-        "api_path_sets_per_s": api_rate,
-        "api_path_sample_sets": api_n,
+        "api_path_sets_per_s": api_stream,
+        "api_path": {"how": "asyncio: every call of the sample issued at once through GpuBlsVerifier.verify_signature_sets_same_message "
+                            "(packed inputs), job queue + up to 3 streamed device passes, booleans checked",
+                     "sample_sets": api_stream_n, "device_passes": api_stream_passes,
+                     "oneshot_sets_per_s": api_rate, "oneshot_how": "one gbv_verify_same_message_multi call from host buffers"},
         "roofline": roofline,
         "cpu_baseline": cpu,
         "c1": extras.get("c1"),
         "c3": extras.get("c3"),
         "c4": extras.get("c4"),
+        "c4e": extras.get("c4e"),
+        "c5": extras.get("c5"),
         "signing_roots": ssz,
     }
     if rank == 0:
@@ -730,6 +826,69 @@ def main():
     if dist is not None:
         barrier()
         dist.destroy_process_group()
+
+
+def vs_shard_main(args, v, sk_ints, world, rank, local_rank, dist, log):
+    """--mode vs-shard: ONE verifySignatureSets call (args.shard_calls x 128 sets of 128-member
+    aggregates, a C3-sized range-sync / replay call) sharded over the ranks by cost-balanced
+    contiguous ranges (lodestar_amd/sharded.py).  Each rank stages its shard in HBM; a step is
+    gbv_vs_batch_partial (the shard's Fp12 Miller product) -> 577-byte RCCL all-gather -> one final
+    exponentiation over all partials (gbv_fp12_check) on every rank.  Before timing: the sharded
+    answer equals the single-GPU gbv_verify_sets answer, and a call with one wrong signature in
+    another shard is false."""
+    import torch
+    import torch.distributed as tdist
+    from lodestar_amd.sharded import ShardedVerifier
+    from lodestar_amd import AggregatedSignatureSet
+    if dist is None:  # one rank: still a real process group on RCCL, so the same collective runs
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(free_port()))
+        torch.cuda.set_device(local_rank)
+        tdist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", local_rank))
+    backend = tdist.get_backend()
+    sv = ShardedVerifier(v)
+    rng = np.random.Generator(np.random.PCG64(0x5A))
+    sets = _agg_sets(v, sk_ints, 128 * args.shard_calls, b"gbv-shard", rng)
+    lo, hi = sv.shard_of(sets)
+    staged = v.stage_signature_sets([sets[lo:hi]])
+    log("vs-shard: %d sets, rank 0 shard [%d, %d), backend %s" % (len(sets), lo, hi, backend))
+    assert sv.verify_staged_shard(staged) is True
+    single = v.verify_signature_sets_sync(sets) if rank == 0 else None  # the same call on one GPU
+    bad = list(sets)
+    j = len(sets) - 1 - 7  # the last shard
+    bad[j] = AggregatedSignatureSet(sets[j].indices, sets[j].signing_root, sets[0].signature)
+    bad_small = bad[-256:]  # one-shot marshalling kept small: the wrong set sits in the last rank's share
+    wrong = sv.verify_signature_sets(bad_small)
+    ok_small = sv.verify_signature_sets(sets[-256:])
+    for _ in range(args.warmup):
+        assert sv.verify_staged_shard(staged) is True
+    tdist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        assert sv.verify_staged_shard(staged) is True
+    torch.cuda.synchronize()
+    tdist.barrier()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    staged.close()
+    if rank == 0:
+        line = {"metric": "signature sets verified/sec (one verifySignatureSets call sharded over GPUs: Fp12 partials + RCCL all-gather)",
+                "value": round(len(sets) * args.steps / elapsed, 1), "unit": "sets/s", "n_gpus": world, "steps": args.steps,
+                "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+                "scaling": "strong", "vs_baseline": None, "dtype": "u32 (381-bit Montgomery, integer VALU)",
+                "data": "synthetic (interop keys, 128-member committee aggregates, GPU-signed)",
+                "config": {"workload": "C3-shaped call of %d aggregate sets as ONE verifySignatureSets call" % len(sets),
+                           "parallelism": "cost-balanced shards%d + RCCL all-gather of 577-byte Fp12 partials" % world},
+                "world_size": world, "backend": backend, "gathered_from_ranks": list(range(world)),
+                "partial_bytes_per_gpu": 577, "rank0_shard": [lo, hi],
+                "parity": {"sharded_equals_single_gpu": single is True, "wrong_signature_call_false": wrong is False,
+                           "clean_small_call_true": ok_small is True}}
+        print(json.dumps(line), flush=True)
+    tdist.barrier()
+    tdist.destroy_process_group()
 
 
 if __name__ == "__main__":

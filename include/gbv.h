@@ -194,6 +194,9 @@ void gbv_sm_batch_destroy(gbv_ctx* ctx, gbv_sm_batch* b);
 #define GBV_FP12_PARTIAL_BYTES 576
 int gbv_vs_partial(gbv_ctx* ctx, const gbv_set* sets, size_t n, const uint32_t* index_arena,
                    uint8_t out576[GBV_FP12_PARTIAL_BYTES], uint8_t* shard_ok);
+/* The same partial over every set of a staged batch (gbv_vs_batch_create / fill: all its calls as
+ * one shard), device-resident inputs: the multi-GPU range-sync / replay form. */
+int gbv_vs_batch_partial(gbv_ctx* ctx, gbv_vs_batch* b, uint8_t out576[GBV_FP12_PARTIAL_BYTES], uint8_t* shard_ok);
 int gbv_fp12_check(gbv_ctx* ctx, const uint8_t* partials576, size_t k, uint8_t* is_one);
 
 /* Device time (ms, summed over launches) and launch count of each kernel of the last

@@ -478,6 +478,8 @@ int gbv_verify_sets(gbv_ctx* c, const gbv_set* sets, size_t n, const uint32_t* a
 
 // One shard of a verifySignatureSets call spread over several GPUs: the shard's sets
 // reduce to ONE Fp12 Miller product (its pairs and its own (-g1, sum r_i sig_i) pair).
+static int vs_partial_run(gbv_ctx* c, gbv_vs_batch* b, uint8_t out576[GBV_FP12_PARTIAL_BYTES], uint8_t* shard_ok);
+
 int gbv_vs_partial(gbv_ctx* c, const gbv_set* sets, size_t n, const uint32_t* arena, uint8_t out576[GBV_FP12_PARTIAL_BYTES],
                    uint8_t* shard_ok) {
   if (!c || !out576 || !shard_ok) return GBV_E_ARG;
@@ -489,6 +491,23 @@ int gbv_vs_partial(gbv_ctx* c, const gbv_set* sets, size_t n, const uint32_t* ar
   int rc = vs_fill(c, b, 1, off, sets, arena);
   if (rc) return rc;
   if (b->call_reject[0]) return gbv_fail(c, GBV_E_EMPTY_AGGREGATE, "EMPTY_AGGREGATE_ARRAY");
+  return vs_partial_run(c, b, out576, shard_ok);
+}
+
+int gbv_vs_batch_partial(gbv_ctx* c, gbv_vs_batch* b, uint8_t out576[GBV_FP12_PARTIAL_BYTES], uint8_t* shard_ok) {
+  if (!c || !b || !out576 || !shard_ok) return GBV_E_ARG;
+  GBV_LOCK(c);
+  if (c->closed) return GBV_E_CLOSED;
+  if (b->in_flight) return gbv_fail(c, GBV_E_ARG, "batch in flight");
+  *shard_ok = 1;
+  for (uint8_t r : b->call_reject)
+    if (r) return gbv_fail(c, GBV_E_EMPTY_AGGREGATE, "EMPTY_AGGREGATE_ARRAY");
+  return vs_partial_run(c, b, out576, shard_ok);
+}
+
+static int vs_partial_run(gbv_ctx* c, gbv_vs_batch* b, uint8_t out576[GBV_FP12_PARTIAL_BYTES], uint8_t* shard_ok) {
+  const size_t n = b->n;
+  int rc;
   if (n == 0) {
     fp12_pack(out576, fp12_one_host());
     return GBV_OK;

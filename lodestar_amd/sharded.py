@@ -104,6 +104,23 @@ class ShardedVerifier:
             return False  # a malformed set somewhere: its job is false, so is the call
         return self.device.fp12_check([b[:PARTIAL_BYTES] for b in blobs])
 
+    def verify_staged_shard(self, staged) -> bool:
+        """The same exchange for a call whose shard this rank has staged in HBM beforehand
+        (StagedSignatureSets over shard_of(call)): gbv_vs_batch_partial -> 577-byte all-gather ->
+        one final exponentiation (gbv_fp12_check) on every rank.  Every rank must call it together."""
+        from ._native import GbvError
+        status, part = 2, bytes(PARTIAL_BYTES)
+        try:
+            part, ok = staged.partial()
+            status = 1 if ok else 0
+        finally:
+            blobs = self._all_gather_bytes(bytes(part) + bytes([status]), PARTIAL_BYTES + 1)
+        if any(b[PARTIAL_BYTES] == 2 for b in blobs):
+            raise GbvError(-2, "device error on a peer rank")
+        if not all(b[PARTIAL_BYTES] == 1 for b in blobs):
+            return False
+        return self.device.fp12_check([b[:PARTIAL_BYTES] for b in blobs])
+
     # ---- many same-message calls (gossip stream / epoch replay) ----------------------------------
     def calls_of(self, n_calls: int) -> Tuple[int, int]:
         per = (n_calls + self.world - 1) // self.world

@@ -936,6 +936,16 @@ class StagedSignatureSets:
         self.submit()
         return self.wait()
 
+    def partial(self) -> Tuple[bytes, bool]:
+        """This device's Fp12 Miller product over every staged set (gbv_vs_batch_partial): the
+        multi-GPU shard form of a staged call, (576-byte blob, shard_ok)."""
+        v = self._v
+        out = ctypes.create_string_buffer(576)
+        ok = ctypes.c_uint8(0)
+        _native.check(v._lib, v._ctx, v._lib.gbv_vs_batch_partial(v._ctx, self._h, out, ctypes.byref(ok)))
+        v.device_passes += 1
+        return out.raw, bool(ok.value)
+
     def close(self):
         # the verifier destroys live handles before its context; after that there is nothing to free
         if self._h and self._v._ctx is not None:

@@ -35,11 +35,37 @@ def _build():
     return out
 
 
-def _run(*args, timeout=120):
+def _run(*args, timeout=120, script="test_addon.js"):
     _build()
-    p = subprocess.run([NODE, os.path.join(ADDON, "test_addon.js")] + list(args), capture_output=True, text=True, timeout=timeout)
+    p = subprocess.run([NODE, os.path.join(ADDON, script)] + list(args), capture_output=True, text=True, timeout=timeout)
     assert p.stdout.strip(), p.stderr
     return json.loads(p.stdout.strip().splitlines()[-1])
+
+
+def test_js_verifier_queue_semantics_without_gpu():
+    """addon/gpu_bls_verifier.js -- the JavaScript GpuBlsVerifier a Lodestar node would construct --
+    over a stand-in device: chunking, batchable buffering (100 ms / > 32 sigs), priority,
+    canAcceptWork with passes in flight, overlapping passes, close() -> QUEUE_ABORTED, per-request
+    failure isolation (multithread.test.ts:109-129), verifyOnMainThread, the metric families."""
+    r = _run("cpu", script="test_verifier.js")
+    assert "fatal" not in r, r
+    assert all(v is True or v == [True, False, False] or v == [True, False, True] for v in r.values()), r
+    assert r["basic"] == [True, False, False] and r["sameMessage"] == [True, False, True]
+
+
+@pytest.mark.gpu
+def test_js_verifier_golden_cases_on_gpu():
+    """The JavaScript GpuBlsVerifier over the real addon: every golden case (bls.test.ts:34-83 shapes),
+    the multithread.test.ts:85-129 submissions (sync / async / batched / priority), a batched invalid
+    request failing alone, main-thread verification and close()."""
+    r = _run("gpu", os.path.join(HERE, "golden", "fixtures.json"), timeout=300, script="test_verifier.js")
+    assert "fatal" not in r, r
+    assert all(r["verifySets"]) and len(r["verifySets"]) == 16
+    assert all(r["sameMessage"]) and len(r["sameMessage"]) == 8
+    assert r["manyCalls"] == [True] * 8
+    assert r["batchedInvalid"] is True and r["mainThread"] is True and r["metrics"] is True
+    assert r["devicePasses"] >= 4
+    assert r["inflightBeforeClose"] is True and r["afterClose"] == "QUEUE_ABORTED"
 
 
 def test_addon_builds_and_maps_errors_without_gpu():
@@ -48,7 +74,9 @@ def test_addon_builds_and_maps_errors_without_gpu():
         pytest.skip("this case checks the no-device error path")
     r = _run("cpu")
     assert r["exports"] == ["open", "addPubkeys", "verifySets", "verifySetsMulti", "verifySameMessageMulti", "aggregatePubkeys",
-                            "aggregateSerializedPubkeys", "aggregateSignatures", "validateSignatures", "close"]
+                            "aggregateSerializedPubkeys", "aggregateSignatures", "validateSignatures", "close", "submitPass",
+                            "waitPass", "freePasses", "pubkeyCount", "verifySetsSync", "vsPartial", "fp12Check"]
+    assert r["maxPasses"] == 3
     assert r["open"] == "ok"      # gbv_init without a device -> Error code GBV_E_DEVICE
     assert r["badCtx"] == "ok"    # not a context -> TypeError code GBV_E_ARG
     assert r["badArg"] == "ok"
@@ -67,5 +95,10 @@ def test_addon_golden_cases_on_gpu():
     assert all(r["singleThread"]) and len(r["singleThread"]) == 11   # singleThread.ts semantics, incl. swapped_keys
     assert all(r["aggregateSignatures"]) and len(r["aggregateSignatures"]) == 7
     assert r["concurrent"] is True
+    # the streamed pair: MAX_PASSES passes in flight at once, every result right
+    assert r["freeWhileBusy"] == 0 and r["busyThrows"] == "GBV_E_BUSY" and r["freeAfter"] == 3
+    assert r["streamed"] == [True, True, True]
+    assert r["verifySetsSync"] is True and r["pubkeyCount"] >= 1
+    assert r["shards"] is True and r["shardsWrong"] is True
     assert r["inflightBeforeClose"] is True
     assert r["afterClose"] == "QUEUE_ABORTED"
