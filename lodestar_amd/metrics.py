@@ -11,13 +11,22 @@ renders it in the Prometheus text format.
 """
 from __future__ import annotations
 
+from collections import defaultdict
+from typing import Callable, Optional
+
 from prometheus_client import CollectorRegistry, Counter, Gauge, Histogram, generate_latest
 
 JOB_TYPES = ("default", "sameMessage")  # JobQueueItemType (multithread/jobItem.ts:9)
 
 
 class BlsPoolMetrics:
+    """Hot-path counts go through ``add`` (a plain dict, ~0.1 us) and reach the prometheus families
+    when they are read (``exposition`` / ``value``), the way the reference refreshes queueLength and
+    workersBusy on collect (multithread/index.ts:140-145); ``on_collect`` runs first."""
+
     def __init__(self):
+        self._pending = defaultdict(float)
+        self.on_collect: Optional[Callable[[], None]] = None
         r = self.registry = CollectorRegistry(auto_describe=True)
         p = "lodestar_bls_thread_pool_"
         # lodestar.ts:402-405 (workerId label: the device ordinal)
@@ -74,9 +83,22 @@ class BlsPoolMetrics:
         self.gpu_pass_time = Histogram(p + "gpu_pass_time_seconds", "Device pass wall time, submit to results",
                                        buckets=[0.005, 0.01, 0.02, 0.05, 0.1, 0.3, 1], registry=r)
 
+    def add(self, family: str, v: float = 1.0, label: Optional[str] = None):
+        self._pending[(family, label)] += v
+
+    def flush(self):
+        if self.on_collect is not None:
+            self.on_collect()
+        pend, self._pending = self._pending, defaultdict(float)
+        for (family, label), v in pend.items():
+            f = getattr(self, family)
+            (f.labels(label) if label is not None else f).inc(v)
+
     def exposition(self) -> bytes:
+        self.flush()
         return generate_latest(self.registry)
 
     def value(self, name: str, labels: dict | None = None) -> float:
+        self.flush()
         v = self.registry.get_sample_value(name, labels or {})
         return 0.0 if v is None else float(v)

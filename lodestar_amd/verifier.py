@@ -157,7 +157,12 @@ class GpuBlsVerifier:
         self._all_slots: List[_PassSlot] = []
         self._staged = weakref.WeakSet()  # live StagedSignatureSets / StagedSameMessage handles
         self.pool_metrics = BlsPoolMetrics()
+        self.pool_metrics.on_collect = self._collect_gauges
         self.device_passes = 0
+
+    def _collect_gauges(self):
+        self.pool_metrics.queue_length.set(len(self._jobs))
+        self.pool_metrics.workers_busy.set(self._busy)
 
     # ---- index2pubkey table ------------------------------------------------------------------
     def add_pubkeys(self, first_index: int, pubkeys: Union[bytes, Sequence[bytes]], validate: bool = False) -> bytes:
@@ -480,11 +485,11 @@ class GpuBlsVerifier:
         opts = opts or VerifySignatureOpts()
         self._check_open()
         m = self.pool_metrics
-        m.total_sig_sets.inc(len(sets))
+        m.add("total_sig_sets", len(sets))
         if opts.priority:
-            m.prioritized_sig_sets.inc(len(sets))
+            m.add("prioritized_sig_sets", len(sets))
         if opts.batchable:
-            m.batchable_sig_sets.inc(len(sets))
+            m.add("batchable_sig_sets", len(sets))
         self._validate_sets(sets)
         if opts.verify_on_main_thread:
             t = time.monotonic()
@@ -524,12 +529,17 @@ class GpuBlsVerifier:
         if n and int(idx.max()) >= self.pubkey_count:
             raise GbvError(_native.GBV_E_ARG, "validator index out of range")
         m = self.pool_metrics
-        m.total_sig_sets.inc(n)
+        m.add("total_sig_sets", n)
         if opts.priority:
-            m.prioritized_sig_sets.inc(n)
+            m.add("prioritized_sig_sets", n)
         if opts.batchable:
-            m.batchable_sig_sets.inc(n)
+            m.add("batchable_sig_sets", n)
         loop = asyncio.get_running_loop()
+        if n < 2 * MAX_SIGNATURE_SETS_PER_JOB:  # one chunk (every gossip call): no gather
+            fut = loop.create_future()
+            self._queue(_Job("same_message", opts, fut, (idx, sigs), bytes(message), packed))
+            r = await fut
+            return r
         futs = []
         # chunkify here too so a job carries at most one reference chunk (index.ts:218-219); the
         # device re-applies the same chunk rule to the job it receives, which is then a no-op.
@@ -624,7 +634,6 @@ class GpuBlsVerifier:
             else:
                 self._jobs.append(job)
             self._schedule()
-        self.pool_metrics.queue_length.set(len(self._jobs))
 
     def _run_buffered(self):
         b = self._buffered
@@ -648,8 +657,6 @@ class GpuBlsVerifier:
         while self._jobs and not self._closed and self._busy < MAX_PASSES_IN_FLIGHT:
             jobs, self._jobs = self._jobs, []
             self._busy += 1
-            self.pool_metrics.workers_busy.set(self._busy)
-            self.pool_metrics.queue_length.set(0)
             asyncio.ensure_future(self._run_pass(jobs))
 
     def _new_slot(self) -> _PassSlot:
@@ -734,8 +741,8 @@ class GpuBlsVerifier:
         m.total_jobs_groups_started.inc()
         for kind, group in (("sameMessage", sm), ("default", df)):
             if group:
-                m.total_jobs_started.labels(kind).inc(len(group))
-                m.total_sig_sets_started.labels(kind).inc(sum(j.n_sets() for j in group))
+                m.add("total_jobs_started", len(group), kind)
+                m.add("total_sig_sets_started", sum(j.n_sets() for j in group), kind)
         for j in jobs:
             m.job_wait_time.observe(t0 - j.added)
         slot = self._slots.pop() if self._slots else None
@@ -761,7 +768,6 @@ class GpuBlsVerifier:
             if slot is not None:
                 self._slots.append(slot)
             self._busy -= 1
-            m.workers_busy.set(self._busy)
             if self._busy == 0 and self._idle is not None:
                 self._idle.set()
             if self._jobs and not self._closed:
@@ -769,26 +775,31 @@ class GpuBlsVerifier:
 
     def _resolve_same_message(self, sm: Sequence[_Job], res):
         m = self.pool_metrics
+        if not sm:
+            return
         if isinstance(res, Exception):  # device failure rejects the whole group (index.ts:498-507)
             m.error_jobs_signature_sets_count.inc(sum(j.n_sets() for j in sm))
             for j in sm:
                 if not j.future.done():
                     j.future.set_exception(res)
             return
-        pos = 0
+        pos, ok_sets, retry_jobs, retry_sets = 0, 0, 0, 0
+        allv = _np.frombuffer(res, dtype=_np.uint8) == 1 if len(res) else _np.zeros(0, dtype=bool)
         for j in sm:
             n = len(j.sets[0])
-            v = _np.frombuffer(res, dtype=_np.uint8, count=n, offset=pos) == 1 if n else _np.zeros(0, dtype=bool)
-            pos += n
-            ok = int(v.sum())
-            m.success_jobs_signature_sets_count.inc(n)
-            if ok == n:
-                m.batch_sigs_success.inc(n)
+            v = allv[pos:pos + n]
+            if res.count(1, pos, pos + n) == n:
+                ok_sets += n
             else:  # the chunk's aggregate check failed: its sets were verified one by one
-                m.same_message_retry_jobs.inc()
-                m.same_message_retry_sets.inc(n)
+                retry_jobs += 1
+                retry_sets += n
+            pos += n
             if not j.future.done():
                 j.future.set_result(v if j.packed else v.tolist())
+        m.add("success_jobs_signature_sets_count", pos)
+        m.add("batch_sigs_success", ok_sets)
+        m.add("same_message_retry_jobs", retry_jobs)
+        m.add("same_message_retry_sets", retry_sets)
 
     def _resolve_default(self, df: Sequence[_Job], res):
         m = self.pool_metrics
@@ -803,9 +814,9 @@ class GpuBlsVerifier:
                 m.error_aggregate_signature_sets_count.labels("default").inc()
                 j.future.set_exception(EmptyAggregateError(_native.GBV_E_EMPTY_AGGREGATE, "EMPTY_AGGREGATE_ARRAY"))
             else:
-                m.success_jobs_signature_sets_count.inc(len(j.sets))
+                m.add("success_jobs_signature_sets_count", len(j.sets))
                 if r == 1:
-                    m.batch_sigs_success.inc(len(j.sets))
+                    m.add("batch_sigs_success", len(j.sets))
                 j.future.set_result(r is True or r == 1)
 
     # ---- signing roots (SSZ hashing on the device) ------------------------

@@ -90,7 +90,19 @@ def _sets(sks, bad=None):
         sets[4] = SingleSignatureSet(5, msgs[4], O.g2_compress(O.sign(sks[5], msgs[0])))
     elif bad == "malformed":
         sets[1] = SingleSignatureSet(1, msgs[1], bytes([10]) * 96)
+    elif bad == "malformed_last":  # in the last rank's shard
+        sets[4] = SingleSignatureSet(5, msgs[4], bytes([10]) * 96)
     return sets
+
+
+class OracleStaged:
+    """Stand-in for a StagedSignatureSets holding this rank's shard (ShardedVerifier.verify_staged_shard)."""
+
+    def __init__(self, device, sets):
+        self.device, self.sets = device, sets
+
+    def partial(self):
+        return self.device.vs_partial(self.sets)
 
 
 def _worker(rank, world, port, q):
@@ -107,6 +119,12 @@ def _worker(rank, world, port, q):
         res["valid"] = sv.verify_signature_sets(_sets(sks))
         res["wrong_msg"] = sv.verify_signature_sets(_sets(sks, "wrong_msg"))
         res["malformed"] = sv.verify_signature_sets(_sets(sks, "malformed"))
+        res["malformed_last"] = sv.verify_signature_sets(_sets(sks, "malformed_last"))
+        # the staged form: each rank stages its own shard, then partial -> all-gather -> one check
+        for name, bad in (("staged", None), ("staged_wrong", "wrong_msg"), ("staged_malformed", "malformed_last")):
+            call = _sets(sks, bad)
+            lo, hi = sv.shard_of(call)
+            res[name] = sv.verify_staged_shard(OracleStaged(sv.device, call[lo:hi]))
         res["empty"] = sv.verify_signature_sets([])
         try:
             sv.verify_signature_sets(_sets(sks) + [AggregatedSignatureSet([], bytes(32), bytes(96))])
@@ -167,6 +185,8 @@ def test_sharded_world2_gloo():
     for rank in (0, 1):
         r = out[rank]
         assert r["valid"] is True and r["wrong_msg"] is False and r["malformed"] is False
+        assert r["malformed_last"] is False
+        assert r["staged"] is True and r["staged_wrong"] is False and r["staged_malformed"] is False
         assert r["empty"] is False and r["empty_agg"] == "rejected"
         assert r["sm"] == [[True, True], [True, False], [False]]
         assert r["sm_err"] == "raised"
