@@ -610,18 +610,25 @@ def main():
     invalid_frac = args.invalid_frac if args.invalid_frac is not None else (0.01 if args.mode == "replay" else 0.0)
     dist = None
     torch = None
-    if world > 1:
+    if world > 1 or args.mode == "vs-shard":
+        # torch (and RCCL) initialise the GPU before libgbv does; --mode vs-shard joins a real RCCL
+        # process group even at one rank, so the same collective runs at every N
         import torch
         import torch.distributed as dist
         torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))  # RCCL over xGMI
+        if world == 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", str(free_port()))
+            dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", local_rank))
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))  # RCCL over xGMI
 
     def log(msg):
         if rank == 0:
             print("[bench] " + msg, file=sys.stderr, flush=True)
 
     def barrier():
-        if dist is not None:
+        if dist is not None and world > 1:
             dist.barrier(device_ids=[local_rank])
 
     from lodestar_amd import GpuBlsVerifier
@@ -840,11 +847,6 @@ def vs_shard_main(args, v, sk_ints, world, rank, local_rank, dist, log):
     import torch.distributed as tdist
     from lodestar_amd.sharded import ShardedVerifier
     from lodestar_amd import AggregatedSignatureSet
-    if dist is None:  # one rank: still a real process group on RCCL, so the same collective runs
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        os.environ.setdefault("MASTER_PORT", str(free_port()))
-        torch.cuda.set_device(local_rank)
-        tdist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", local_rank))
     backend = tdist.get_backend()
     sv = ShardedVerifier(v)
     rng = np.random.Generator(np.random.PCG64(0x5A))

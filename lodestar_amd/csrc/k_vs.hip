@@ -1,4 +1,6 @@
 // Distinct-message path kernels (verifySignatureSets, maybeBatch.ts:15-45), batched over many calls.
+#include <cstring>
+
 #include "launch.h"
 #include "kernel_common.h"
 #include "pair.h"
@@ -229,8 +231,8 @@ __global__ void GBV_MILLER_ATTR k_vs_miller(uint32_t n, const uint8_t* __restric
 // The same Miller values on lane pairs (pair.h): set i on lanes 2(i mod 32), 2(i mod 32) + 1 of block
 // i / 32; lane 0 of the pair writes c0 of the conjugated value, lane 1 c1.  Every lane runs the loop
 // (the pair exchanges need both lanes); pairs past n or whose set did not decode write nothing.
-__global__ void GBV_MILLER_ATTR k_vs_miller_pair(uint32_t n, const uint8_t* __restrict__ status, const G1J* __restrict__ rP,
-                                                 const G2A* __restrict__ H, Fp12* __restrict__ F) {
+__device__ __forceinline__ void vs_miller_pair_body(uint32_t n, const uint8_t* __restrict__ status, const G1J* __restrict__ rP,
+                                                     const G2A* __restrict__ H, Fp12* __restrict__ F) {
   const bool h = (threadIdx.x & 1) != 0;
   const uint32_t i = blockIdx.x * 32 + (threadIdx.x >> 1);
   const bool act = i < n && status[i] == SET_OK;
@@ -253,6 +255,16 @@ __global__ void GBV_MILLER_ATTR k_vs_miller_pair(uint32_t n, const uint8_t* __re
     }
   }
   if (act) ((Fp6*)&F[i])[h ? 1 : 0] = h ? fp6_neg(M) : M;
+}
+// one wave per SIMD (no spills) and two waves per SIMD (the 256-register budget: some spills, but
+// twice the waves to hide the product chains' latency); GBV_VS_MILLER selects (A/B)
+__global__ void GBV_MILLER_ATTR k_vs_miller_pair(uint32_t n, const uint8_t* __restrict__ status, const G1J* __restrict__ rP,
+                                                 const G2A* __restrict__ H, Fp12* __restrict__ F) {
+  vs_miller_pair_body(n, status, rP, H, F);
+}
+__global__ void GBV_KERNEL_ATTR k_vs_miller_pair2(uint32_t n, const uint8_t* __restrict__ status, const G1J* __restrict__ rP,
+                                                  const G2A* __restrict__ H, Fp12* __restrict__ F) {
+  vs_miller_pair_body(n, status, rP, H, F);
 }
 
 // Signature.fromBytes(sig, true) (maybeBatch.ts:23; the "BLS deserializing signatures" perf id,
@@ -353,11 +365,17 @@ void launch_vs_hash_sig(hipStream_t s, uint32_t n, const uint8_t* msgs32, const 
 
 void launch_vs_miller(LaunchCfg c, uint32_t n, const uint8_t* status, const G1J* rP, const G2A* H, Fp12* F) {
   if (n == 0) return;
-  // lane pairs by default; GBV_VS_MILLER=thread selects one thread per set (A/B)
-  static const bool thread = getenv("GBV_VS_MILLER") && getenv("GBV_VS_MILLER")[0] == 't';
+  // lane pairs by default; GBV_VS_MILLER=thread selects one thread per set, =pair2 the lane pairs
+  // at two waves per SIMD (A/B)
+  static const char* sel = getenv("GBV_VS_MILLER");
+  static const bool thread = sel && sel[0] == 't';
+  static const bool pair2 = sel && !strcmp(sel, "pair2");
   if (thread) {
     hipLaunchKernelGGL(k_vs_miller, dim3((n + 63) / 64), dim3(64), 0, c.stream, n, status, rP, H, F);
     debug_sync(c.stream, "k_vs_miller");
+  } else if (pair2) {
+    hipLaunchKernelGGL(k_vs_miller_pair2, dim3((n + 31) / 32), dim3(64), 0, c.stream, n, status, rP, H, F);
+    debug_sync(c.stream, "k_vs_miller_pair2");
   } else {
     hipLaunchKernelGGL(k_vs_miller_pair, dim3((n + 31) / 32), dim3(64), 0, c.stream, n, status, rP, H, F);
     debug_sync(c.stream, "k_vs_miller_pair");

@@ -10,7 +10,7 @@ export TMPDIR=/tmp
 BENCH="bench.py --steps 1 --warmup 0 --sets 262144 --no-cpu-baseline --no-stream"
 run_pass() {
   local name=$1; shift
-  timeout -s KILL 180 rocprofv3 --pmc "$@" --output-format csv -d "$OUT/$name" -o run -- python3 -u $BENCH \
+  timeout -s KILL 400 rocprofv3 --pmc "$@" --output-format csv -d "$OUT/$name" -o run -- python3 -u $BENCH \
     > "$OUT/$name.log" 2>&1 || { echo "pmc pass $name failed"; tail -20 "$OUT/$name.log"; exit 1; }
 }
 run_pass fetch FETCH_SIZE
