@@ -1,4 +1,9 @@
-// hash_to_G2 kernels.
+// hash_to_G2 kernels.  The few-message forms are latency-bound (lane pairs, one wave per message):
+// GBV_HASH_CHAINS accumulator chains per product column (fp.h GBV_MUL28_CHAINS) for A/B builds.
+#ifndef GBV_HASH_CHAINS
+#define GBV_HASH_CHAINS 1
+#endif
+#define GBV_MUL28_CHAINS GBV_HASH_CHAINS
 #include "launch.h"
 #include "kernel_common.h"
 

@@ -1,6 +1,12 @@
 // Same-message path kernels built on the wave-cooperative pairing arithmetic (coop.h): one
 // workgroup = one wave = one pairing job.  Kept in their own translation unit so their small
 // register budget (one Fp product per lane) is not merged with the thread-per-set kernels'.
+// The cooperative kernels run one wave per pairing (latency): GBV_COOP_CHAINS accumulator chains per
+// product column (fp.h GBV_MUL28_CHAINS) for A/B builds.
+#ifndef GBV_COOP_CHAINS
+#define GBV_COOP_CHAINS 1
+#endif
+#define GBV_MUL28_CHAINS GBV_COOP_CHAINS
 #include <cstdlib>
 
 #include "launch.h"

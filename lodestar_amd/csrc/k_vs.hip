@@ -3,7 +3,6 @@
 
 #include "launch.h"
 #include "kernel_common.h"
-#include "pair.h"
 
 namespace gbv {
 
@@ -215,58 +214,6 @@ __global__ void GBV_KERNEL_ATTR k_vs_hash_sig(uint32_t n, uint32_t nb, uint32_t 
   rS_out[i] = rs;
 }
 
-// Miller value f_{|x|, H(m_i)}(r_i pk_i) of every set that decoded (P Jacobian: the lines carry a
-// Z^3 factor that the final exponentiation removes).
-// One wave per SIMD (512 registers, VGPRs + AGPRs): a C3 pass of 65 536 sets is 1024 waves, one per
-// SIMD anyway, and the 576-byte accumulator, T, the line and the operands then stay in registers
-// (at two waves per SIMD the accumulator lived in scratch: 775 KB of HBM traffic per set).
-#define GBV_MILLER_ATTR __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1)))
-__global__ void GBV_MILLER_ATTR k_vs_miller(uint32_t n, const uint8_t* __restrict__ status, const G1J* __restrict__ rP,
-                                            const G2A* __restrict__ H, Fp12* __restrict__ F) {
-  uint32_t i = blockIdx.x * 64 + threadIdx.x;
-  if (i >= n || status[i] != SET_OK) return;
-  F[i] = miller_loop_1j(rP[i], H[i]);
-}
-
-// The same Miller values on lane pairs (pair.h): set i on lanes 2(i mod 32), 2(i mod 32) + 1 of block
-// i / 32; lane 0 of the pair writes c0 of the conjugated value, lane 1 c1.  Every lane runs the loop
-// (the pair exchanges need both lanes); pairs past n or whose set did not decode write nothing.
-__device__ __forceinline__ void vs_miller_pair_body(uint32_t n, const uint8_t* __restrict__ status, const G1J* __restrict__ rP,
-                                                     const G2A* __restrict__ H, Fp12* __restrict__ F) {
-  const bool h = (threadIdx.x & 1) != 0;
-  const uint32_t i = blockIdx.x * 32 + (threadIdx.x >> 1);
-  const bool act = i < n && status[i] == SET_OK;
-  const uint32_t j = i < n ? i : n - 1;
-  const G1J p = rP[j];
-  PairP P;
-  P.z3 = fp_mul(fp_sqr(p.z), p.z);
-  P.nxz = fp_neg(fp_mul(p.x, p.z));
-  P.y = p.y;
-  const G2A Q = H[j];
-  PairT T{Q.x, Q.y, fp2_one()};
-  Fp6 M = fp6_sel(h, fp6_zero(), fp6_one());
-  for (int b = 62; b >= 0; --b) {
-    if (b != 62) pair_sqr(M, h);
-    Line l = pair_dbl(T, P, h);
-    pair_mul_line(M, l, h);
-    if ((X_ABS >> b) & 1ull) {
-      l = pair_add(T, Q, P, h);
-      pair_mul_line(M, l, h);
-    }
-  }
-  if (act) ((Fp6*)&F[i])[h ? 1 : 0] = h ? fp6_neg(M) : M;
-}
-// one wave per SIMD (no spills) and two waves per SIMD (the 256-register budget: some spills, but
-// twice the waves to hide the product chains' latency); GBV_VS_MILLER selects (A/B)
-__global__ void GBV_MILLER_ATTR k_vs_miller_pair(uint32_t n, const uint8_t* __restrict__ status, const G1J* __restrict__ rP,
-                                                 const G2A* __restrict__ H, Fp12* __restrict__ F) {
-  vs_miller_pair_body(n, status, rP, H, F);
-}
-__global__ void GBV_KERNEL_ATTR k_vs_miller_pair2(uint32_t n, const uint8_t* __restrict__ status, const G1J* __restrict__ rP,
-                                                  const G2A* __restrict__ H, Fp12* __restrict__ F) {
-  vs_miller_pair_body(n, status, rP, H, F);
-}
-
 // Signature.fromBytes(sig, true) (maybeBatch.ts:23; the "BLS deserializing signatures" perf id,
 // test/perf/bls/bls.test.ts:89-100): decode + subgroup check, and the recompressed encoding of
 // every accepted point (byte-identical to the input for canonical compressed signatures).
@@ -361,25 +308,6 @@ void launch_vs_hash_sig(hipStream_t s, uint32_t n, const uint8_t* msgs32, const 
   hipLaunchKernelGGL(k_vs_hash_sig, dim3(nb + (split ? 2 : 1) * nsig), dim3(64), 0, s, n, nb, pair, split ? 1u : 0u, msgs32, set_off,
                      arena, raw_flag, raw_pk48, sig, sig_stride, sig_len, table, table_ok, pk_agg, pk_st, seed, nonce, H, rP, rS, status);
   debug_sync(s, "k_vs_hash_sig");
-}
-
-void launch_vs_miller(LaunchCfg c, uint32_t n, const uint8_t* status, const G1J* rP, const G2A* H, Fp12* F) {
-  if (n == 0) return;
-  // lane pairs by default; GBV_VS_MILLER=thread selects one thread per set, =pair2 the lane pairs
-  // at two waves per SIMD (A/B)
-  static const char* sel = getenv("GBV_VS_MILLER");
-  static const bool thread = sel && sel[0] == 't';
-  static const bool pair2 = sel && !strcmp(sel, "pair2");
-  if (thread) {
-    hipLaunchKernelGGL(k_vs_miller, dim3((n + 63) / 64), dim3(64), 0, c.stream, n, status, rP, H, F);
-    debug_sync(c.stream, "k_vs_miller");
-  } else if (pair2) {
-    hipLaunchKernelGGL(k_vs_miller_pair2, dim3((n + 31) / 32), dim3(64), 0, c.stream, n, status, rP, H, F);
-    debug_sync(c.stream, "k_vs_miller_pair2");
-  } else {
-    hipLaunchKernelGGL(k_vs_miller_pair, dim3((n + 31) / 32), dim3(64), 0, c.stream, n, status, rP, H, F);
-    debug_sync(c.stream, "k_vs_miller_pair");
-  }
 }
 
 void launch_sig_validate(LaunchCfg c, uint32_t n, const uint8_t* sig, uint32_t sig_len, uint8_t* status, uint8_t* out96) {

@@ -25,6 +25,7 @@ index2pubkey table (state-transition/src/cache/epochCache.ts:126-133) fed by add
 """
 from __future__ import annotations
 
+import array
 import asyncio
 import ctypes
 import time
@@ -206,7 +207,7 @@ class GpuBlsVerifier:
         count, so 10^5-set calls marshal in well under a second."""
         import numpy as np
         n = len(sets)
-        arena: List[int] = []
+        arena = array.array("I")  # u32: an index outside [0, 2^32) raises OverflowError here
         roots, sigs, raws = [], [], []
         sig_off = np.zeros(n, dtype=np.uint64)
         sig_len = np.zeros(n, dtype=np.uint32)
@@ -226,7 +227,10 @@ class GpuBlsVerifier:
             pos += len(sig)
             if isinstance(s, AggregatedSignatureSet):
                 idx_off[i], idx_len[i] = len(arena), len(s.indices)
-                arena.extend(int(x) for x in s.indices)
+                if isinstance(s.indices, np.ndarray):
+                    arena.frombytes(np.ascontiguousarray(s.indices, dtype=np.uint32).tobytes())
+                else:
+                    arena.extend(s.indices)
             elif s.pubkey is not None:
                 pk = bytes(s.pubkey)
                 if len(pk) != 48:
@@ -248,8 +252,10 @@ class GpuBlsVerifier:
             rec["sig"][:n] = np.where(sig_len > 0, ctypes.addressof(sbuf) + sig_off, 0)
             rec["sig_len"][:n] = sig_len
             rec["raw"][:n] = np.where(raw_off >= 0, ctypes.addressof(pbuf) + np.maximum(raw_off, 0).astype(np.uint64), 0)
-        ar = np.ascontiguousarray(np.asarray(arena if arena else [0], dtype=np.uint32))
-        keep = [rbuf, sbuf, pbuf, rec, ar]
+        if not arena:
+            arena.append(0)
+        ar = np.frombuffer(arena, dtype=np.uint32)
+        keep = [rbuf, sbuf, pbuf, rec, ar, arena]
         return ctypes.cast(rec.ctypes.data, ctypes.POINTER(GbvSet)), ar.ctypes.data, keep
 
     def verify_signature_sets_sync(self, sets: Sequence[ISignatureSet]) -> bool:

@@ -45,4 +45,14 @@ for rep in range(8):
     t1 = time.perf_counter()
     print("c1 call %.2f ms  kernels %s  ok %s" % ((t1 - t0) * 1e3, dict(zip(bench.VS_KERNELS, [round(float(x), 2) for x in v.vs_last_kernel_ms()])), ok),
           flush=True)
+# C4: one deneb block and one electra block (8 aggregates of 32 768 validators) as lone calls
+sk_ints = [bench.interop_sk_int(i) for i in range(bench.N_KEYS)]
+for name, electra in (("c4 block", False), ("c4e block", True)):
+    calls = bench.make_blocks(v, sk_ints, 1, np.random.Generator(np.random.PCG64(0xB10C)), electra=electra)
+    for rep in range(6):
+        t0 = time.perf_counter()
+        ok = v.verify_signature_sets_sync(calls[0])
+        t1 = time.perf_counter()
+        print("%s %.2f ms  kernels %s  ok %s" % (name, (t1 - t0) * 1e3, dict(zip(bench.VS_KERNELS, [round(float(x), 2) for x in v.vs_last_kernel_ms()])),
+                                              ok), flush=True)
 v.close_sync()
