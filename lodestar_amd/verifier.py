@@ -35,7 +35,7 @@ from typing import List, Optional, Sequence, Tuple, Union
 
 from . import _native
 from ._native import EmptyAggregateError, GbvError, GbvSet, QueueAbortedError  # noqa: F401
-from .metrics import BlsPoolMetrics
+from .metrics import BlsPoolMetrics, observe_many
 
 MAX_SIGNATURE_SETS_PER_JOB = 128   # multithread/index.ts:56
 MAX_BUFFERED_SIGS = 32             # multithread/index.ts:65
@@ -44,6 +44,10 @@ MAX_JOBS_CAN_ACCEPT_WORK = 512     # multithread/index.ts:79
 # Device passes in flight at once (the GPU analogue of the pool's worker count, index.ts:46): with
 # three, pass k+1's per-set kernels run beside pass k's chunk tail and pass k+2 is staged.
 MAX_PASSES_IN_FLIGHT = 3
+# A pass takes queued jobs up to about this many signature sets, so that a deep queue (a burst of
+# gossip calls) becomes several passes that overlap on the device instead of one long serial one;
+# 2^18 sets still fill the chip and take the same-message path's bucket-MSM segment form.
+MAX_PASS_SETS = 1 << 18
 
 # struct gbv_set as a numpy record (include/gbv.h; 40 bytes on LP64, checked against ctypes below)
 import numpy as _np  # noqa: E402
@@ -108,7 +112,10 @@ def chunkify_maximize_chunk_size(arr, min_per_chunk):
     return [list(arr[i:i + per_chunk]) for i in range(0, len(arr), per_chunk)]
 
 
-@dataclass
+_DEFAULT_OPTS = VerifySignatureOpts()
+
+
+@dataclass(slots=True)
 class _Job:
     kind: str  # "default" | "same_message"
     opts: VerifySignatureOpts
@@ -513,7 +520,7 @@ class GpuBlsVerifier:
 
     def _pack_same_message(self, sets) -> Tuple[_np.ndarray, bytes, bool]:
         if isinstance(sets, PackedSameMessageSets):
-            return sets.indices, bytes(sets.signatures), True
+            return sets.indices, sets.signatures, True
         idx = _np.fromiter((int(i) for i, _ in sets), dtype=_np.int64, count=len(sets))
         if len(idx) and (idx.min() < 0 or idx.max() > 0xFFFFFFFF):
             raise GbvError(_native.GBV_E_ARG, "validator index out of range")
@@ -522,30 +529,41 @@ class GpuBlsVerifier:
         sigs = b"".join(bytes(sig) if len(sig) == 96 else bytes(96) for _, sig in sets)
         return idx.astype(_np.uint32), sigs, False
 
-    async def verify_signature_sets_same_message(self, sets, message: bytes,
-                                                 opts: Optional[VerifySignatureOpts] = None):
+    def verify_signature_sets_same_message(self, sets, message: bytes, opts: Optional[VerifySignatureOpts] = None):
         """verifySignatureSetsSameMessage (interface.ts:55-59): ``sets`` is a list of
-        (validator index, signature bytes) or a PackedSameMessageSets."""
-        opts = opts or VerifySignatureOpts()
-        self._check_open()
-        if len(message) != 32:
-            raise ValueError("message must be 32 bytes")
-        idx, sigs, packed = self._pack_same_message(sets)
+        (validator index, signature bytes) or a PackedSameMessageSets.  Returns an awaitable (the
+        reference's Promise<boolean[]>): argument errors reject it, they are not raised at the call.
+
+        A gossip call is one job and its future is returned directly -- no coroutine, no task -- so
+        the per-call host cost stays a few microseconds (the validator-index range check of the
+        call runs vectorised over the whole device pass, _take_sm_jobs)."""
+        loop = asyncio.get_running_loop()
+        try:
+            self._check_open()
+            if len(message) != 32:
+                raise ValueError("message must be 32 bytes")
+            idx, sigs, packed = self._pack_same_message(sets)
+        except Exception as e:  # noqa: BLE001 -- rejects this call's promise only
+            fut = loop.create_future()
+            fut.set_exception(e)
+            return fut
+        opts = opts or _DEFAULT_OPTS
         n = len(idx)
-        if n and int(idx.max()) >= self.pubkey_count:
-            raise GbvError(_native.GBV_E_ARG, "validator index out of range")
         m = self.pool_metrics
         m.add("total_sig_sets", n)
         if opts.priority:
             m.add("prioritized_sig_sets", n)
         if opts.batchable:
             m.add("batchable_sig_sets", n)
-        loop = asyncio.get_running_loop()
-        if n < 2 * MAX_SIGNATURE_SETS_PER_JOB:  # one chunk (every gossip call): no gather
+        if n < 2 * MAX_SIGNATURE_SETS_PER_JOB:  # one chunk (every gossip call): the job's own future
             fut = loop.create_future()
             self._queue(_Job("same_message", opts, fut, (idx, sigs), bytes(message), packed))
-            r = await fut
-            return r
+            return fut
+        return asyncio.ensure_future(self._same_message_chunked(idx, sigs, bytes(message), packed, opts))
+
+    async def _same_message_chunked(self, idx, sigs, message: bytes, packed: bool, opts: VerifySignatureOpts):
+        loop = asyncio.get_running_loop()
+        n = len(idx)
         futs = []
         # chunkify here too so a job carries at most one reference chunk (index.ts:218-219); the
         # device re-applies the same chunk rule to the job it receives, which is then a no-op.
@@ -661,7 +679,12 @@ class GpuBlsVerifier:
         takes every job queued at that moment."""
         self._run_scheduled = False
         while self._jobs and not self._closed and self._busy < MAX_PASSES_IN_FLIGHT:
-            jobs, self._jobs = self._jobs, []
+            q = self._jobs
+            k, tot = 0, 0
+            while k < len(q) and (k == 0 or tot < MAX_PASS_SETS):
+                tot += q[k].n_sets()
+                k += 1
+            jobs, self._jobs = (q, []) if k == len(q) else (q[:k], q[k:])
             self._busy += 1
             asyncio.ensure_future(self._run_pass(jobs))
 
@@ -674,6 +697,26 @@ class GpuBlsVerifier:
             self._lib.gbv_sm_batch_destroy(self._ctx, sm)
             _native.check(self._lib, self._ctx, rc)
         return _PassSlot(sm, vs)
+
+    def _check_sm_indices(self, sm: List[_Job]) -> List[_Job]:
+        """Validator-index range check of a pass's same-message jobs, vectorised over the pass (one
+        max over the concatenated indices when every slot exists): a job naming a slot past the
+        table rejects alone with GBV_E_ARG -- the reference fails such a call while building its job
+        (index2pubkey[i], jobItem.ts:55-62) -- and the rest of the pass goes on."""
+        if not sm:
+            return sm
+        parts = [j.sets[0] for j in sm]
+        cat = _np.concatenate(parts) if len(parts) > 1 else parts[0]
+        n_keys = self.pubkey_count
+        if not len(cat) or int(cat.max()) < n_keys:
+            return sm
+        keep = []
+        for j, a in zip(sm, parts):
+            if len(a) and int(a.max()) >= n_keys:
+                j.future.set_exception(GbvError(_native.GBV_E_ARG, "validator index out of range"))
+            else:
+                keep.append(j)
+        return keep
 
     @staticmethod
     def _sm_group(jobs: Sequence[_Job]):
@@ -749,8 +792,8 @@ class GpuBlsVerifier:
             if group:
                 m.add("total_jobs_started", len(group), kind)
                 m.add("total_sig_sets_started", sum(j.n_sets() for j in group), kind)
-        for j in jobs:
-            m.job_wait_time.observe(t0 - j.added)
+        observe_many(m.job_wait_time, t0 - _np.fromiter((j.added for j in jobs), dtype=_np.float64, count=len(jobs)))
+        sm = self._check_sm_indices(sm)
         slot = self._slots.pop() if self._slots else None
         try:
             slot, st_sm, st_df = await asyncio.to_thread(self._pass_submit, slot, sm, df)
@@ -789,23 +832,25 @@ class GpuBlsVerifier:
                 if not j.future.done():
                     j.future.set_exception(res)
             return
-        pos, ok_sets, retry_jobs, retry_sets = 0, 0, 0, 0
-        allv = _np.frombuffer(res, dtype=_np.uint8) == 1 if len(res) else _np.zeros(0, dtype=bool)
-        for j in sm:
-            n = len(j.sets[0])
-            v = allv[pos:pos + n]
-            if res.count(1, pos, pos + n) == n:
-                ok_sets += n
-            else:  # the chunk's aggregate check failed: its sets were verified one by one
-                retry_jobs += 1
-                retry_sets += n
-            pos += n
+        lens = _np.fromiter((len(j.sets[0]) for j in sm), dtype=_np.int64, count=len(sm))
+        ends = _np.cumsum(lens)
+        allv = _np.frombuffer(res, dtype=_np.uint8)[:int(ends[-1])] == 1
+        # per job: all sets true (its chunk's aggregate check passed) -- else the sets were verified
+        # one by one (the pool's same-message retry); one vectorised pass, then one view per job
+        cs = _np.zeros(len(allv) + 1, dtype=_np.int64)
+        _np.cumsum(allv, out=cs[1:])
+        n_true = cs[ends] - cs[ends - lens]
+        retried = (n_true != lens) & (lens > 0)
+        a = 0
+        for j, e in zip(sm, ends.tolist()):
             if not j.future.done():
+                v = allv[a:e]
                 j.future.set_result(v if j.packed else v.tolist())
-        m.add("success_jobs_signature_sets_count", pos)
-        m.add("batch_sigs_success", ok_sets)
-        m.add("same_message_retry_jobs", retry_jobs)
-        m.add("same_message_retry_sets", retry_sets)
+            a = e
+        m.add("success_jobs_signature_sets_count", int(ends[-1]))
+        m.add("batch_sigs_success", int(lens[~retried].sum()))
+        m.add("same_message_retry_jobs", int(retried.sum()))
+        m.add("same_message_retry_sets", int(lens[retried].sum()))
 
     def _resolve_default(self, df: Sequence[_Job], res):
         m = self.pool_metrics

@@ -356,3 +356,40 @@ def test_metric_families_match_the_reference_names():
     assert m.value("lodestar_bls_thread_pool_jobs_started_total", {"type": "sameMessage"}) == 1
     assert m.value("lodestar_bls_thread_pool_same_message_sets_retries_total") == 2
     assert m.value("lodestar_bls_thread_pool_gpu_device_passes_total") == 2
+
+
+def test_deep_queue_is_cut_into_overlapping_passes(monkeypatch):
+    # a burst of gossip calls deeper than MAX_PASS_SETS becomes several passes (each <= the cap plus
+    # its last job), so they overlap on the device; every call still resolves with its own booleans
+    import lodestar_amd.verifier as V
+    monkeypatch.setattr(V, "MAX_PASS_SETS", 100)
+
+    async def go():
+        v = Recorder()
+        sig = lambda ok: (b"\x01" if ok else b"\x00") + bytes(95)  # noqa: E731
+        calls = [[(i, sig((i + g) % 7 != 0)) for i in range(40)] for g in range(10)]
+        res = await asyncio.gather(*[v.verify_signature_sets_same_message(c, bytes([g]) * 32) for g, c in enumerate(calls)])
+        return v, calls, res
+    v, calls, res = run(go())
+    sm_passes = [p[1] for p in v.passes if p[0] == "sm"]
+    assert sum(len(p) for p in sm_passes) == 10 and len(sm_passes) >= 3
+    assert all(sum(p) - p[-1] < 100 for p in sm_passes)
+    assert res == [[(i + g) % 7 != 0 for i in range(40)] for g in range(10)]
+
+
+def test_out_of_range_index_rejects_its_call_inside_a_shared_pass():
+    # the index range check runs over the whole pass; only the call naming a missing slot rejects
+    async def go():
+        v = Recorder()
+        ok = b"\x01" + bytes(95)
+        good1 = v.verify_signature_sets_same_message(PackedSameMessageSets(np.array([1, 2], dtype=np.uint32), ok * 2), bytes(32))
+        bad = v.verify_signature_sets_same_message(PackedSameMessageSets(np.array([3, 1 << 20], dtype=np.uint32), ok * 2), bytes(32))
+        good2 = v.verify_signature_sets_same_message([(5, ok)], bytes(32))
+        r1 = await good1
+        with pytest.raises(GbvError):
+            await bad
+        r2 = await good2
+        return v, r1, r2
+    v, r1, r2 = run(go())
+    assert r1.tolist() == [True, True] and r2 == [True]
+    assert [p for p in v.passes if p[0] == "sm"] == [("sm", [2, 1])]
