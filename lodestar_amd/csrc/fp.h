@@ -210,9 +210,28 @@ inline unsigned long long g_fme_count = 0;
 #ifndef GBV_MUL28_CHAINS
 #define GBV_MUL28_CHAINS 1
 #endif
+// GBV_MUL28_ASM (per translation unit, default 0): 2, 3 or 4 -- the device product and squaring
+// from mul28_asm.h (tools/gen_mul28_asm.py), each column's limb products one inline-asm block over
+// that many independent accumulator chains.  In C, LLVM reassociates a column's adds back into ONE
+// dependent v_mad_u64_u32 chain whatever GBV_MUL28_CHAINS says; only the asm keeps them apart.
+#ifndef GBV_MUL28_ASM
+#define GBV_MUL28_ASM 0
+#endif
+}  // namespace gbv
+#include "mul28_asm.h"
+namespace gbv {
+#if defined(__HIP_DEVICE_COMPILE__) && GBV_MUL28_ASM >= 2
+#define GBV_M28_CAT2(a, b) a##b
+#define GBV_M28_CAT(a, b) GBV_M28_CAT2(a, b)
+#define GBV_MUL28_DEV GBV_M28_CAT(mul28_asm, GBV_MUL28_ASM)
+#define GBV_SQR28_DEV GBV_M28_CAT(sqr28_asm, GBV_MUL28_ASM)
+#endif
 GBV_HD F28 mul28_inl(const F28& a, const F28& b) {
 #if defined(GBV_HOST_TEST)
   ++g_fme_count;
+#endif
+#if defined(GBV_MUL28_DEV)
+  return GBV_MUL28_DEV(a, b);
 #endif
   constexpr int C = GBV_MUL28_CHAINS;
   uint32_t m[14], r[14];
@@ -259,6 +278,9 @@ GBV_HD F28 mul28_inl(const F28& a, const F28& b) {
 GBV_HD F28 sqr28_inl(const F28& a) {
 #if defined(GBV_HOST_TEST)
   ++g_fme_count;
+#endif
+#if defined(GBV_SQR28_DEV)
+  return GBV_SQR28_DEV(a);
 #endif
   constexpr int C = GBV_MUL28_CHAINS;
   uint32_t d[14], m[14], r[14];

@@ -4,6 +4,10 @@
 #include "launch.h"
 #include "kernel_common.h"
 
+#ifndef GBV_DEC_SPLIT_DEFAULT
+#define GBV_DEC_SPLIT_DEFAULT 1
+#endif
+
 namespace gbv {
 
 // ---- wave-level helpers ---------------------------------------------------------------------
@@ -32,7 +36,10 @@ constexpr unsigned SCAN_W = 8;  // lanes per scan group (power of two, <= 64)
 // then sums its terms per chunk with a segmented suffix scan (log2(SCAN_W) levels of point
 // additions) and the first lane of every chunk segment in the group writes the segment's sum at
 // its own set index; k_sm_chunk_finish adds the <= ceil(len/SCAN_W)+1 segment sums of a chunk.
-template <bool WITH_G2>
+//
+// PRE: the signatures were decoded by k_sig_decode (k_dec.hip): status[i] holds the decode code and
+// S_out[i] the point, so this kernel starts at the subgroup check.
+template <bool WITH_G2, bool PRE>
 __global__ void GBV_KERNEL_ATTR k_sm_prepare(uint32_t base, uint32_t n, const uint32_t* __restrict__ idx, const uint8_t* __restrict__ sig96,
                                              const uint32_t* __restrict__ set_grp, const G1A* __restrict__ table,
                                              const uint8_t* __restrict__ table_ok, uint32_t table_n, const uint4* __restrict__ comb,
@@ -50,11 +57,17 @@ __global__ void GBV_KERNEL_ATTR k_sm_prepare(uint32_t base, uint32_t n, const ui
     uint8_t st = SET_OK;
     if (k >= table_n || !table_ok[k]) st = SET_BAD_PK;
     G2A s;
-    uint8_t ds = g2_decode(s, sig96 + 96ull * i, 96);
+    uint8_t ds;
+    if (PRE) {
+      ds = status[i];
+      if (ds == PT_OK) s = S_out[i];
+    } else {
+      ds = g2_decode(s, sig96 + 96ull * i, 96);
+    }
     if (ds != PT_OK || !g2_in_subgroup(s)) st = SET_BAD_SIG;
     status[i] = st;
     if (st == SET_OK) {
-      S_out[i] = s;
+      if (!PRE) S_out[i] = s;
       uint64_t r = prf_scalar(seed, i, nonce);
       if (comb && comb_ok[k]) {  // r pk from the validator's comb table (curve.h comb_mul)
         rp = comb_mul(comb + (size_t)k * (COMB_ENTRIES * COMB_U4), (uint32_t)r, (uint32_t)(r >> 32));
@@ -498,15 +511,28 @@ void launch_sm_prepare(LaunchCfg c, uint32_t base, uint32_t n, const uint32_t* i
   // Sh == nullptr: G1 terms only (the segment's G2 sum comes from the bucket MSM); comb == nullptr:
   // no comb tables (GBV_COMB=0 or not built), the ladder forms r pk
   static const uint32_t split_max = getenv("GBV_PREPARE_SPLIT_MAX") ? (uint32_t)atoi(getenv("GBV_PREPARE_SPLIT_MAX")) : 2048;
-  if (Sh && n <= split_max)  // latency: two waves per 64 sets
+  // throughput forms: decompression first as its own kernel at a higher occupancy (k_dec.hip),
+  // unless GBV_DEC_SPLIT=0 (A/B)
+  static const bool dec_split = getenv("GBV_DEC_SPLIT") ? atoi(getenv("GBV_DEC_SPLIT")) != 0 : GBV_DEC_SPLIT_DEFAULT != 0;
+  const dim3 grid((n + 63) / 64);
+  if (Sh && n <= split_max) {  // latency: two waves per 64 sets
     hipLaunchKernelGGL(k_sm_prepare_split, dim3((n + 63) / 64), dim3(128), 0, c.stream, base, n, idx, sig96, set_grp, table, table_ok, table_n,
                        comb, comb_ok, seed, nonce, S_out, Sh, Ph, status);
-  else if (Sh)
-    hipLaunchKernelGGL(k_sm_prepare<true>, dim3((n + 63) / 64), dim3(64), 0, c.stream, base, n, idx, sig96, set_grp, table, table_ok, table_n,
+  } else if (dec_split) {
+    launch_sig_decode(c.stream, base, n, sig96, S_out, status);
+    if (Sh)
+      hipLaunchKernelGGL((k_sm_prepare<true, true>), grid, dim3(64), 0, c.stream, base, n, idx, sig96, set_grp, table, table_ok, table_n,
+                         comb, comb_ok, seed, nonce, S_out, Sh, Ph, status);
+    else
+      hipLaunchKernelGGL((k_sm_prepare<false, true>), grid, dim3(64), 0, c.stream, base, n, idx, sig96, set_grp, table, table_ok, table_n,
+                         comb, comb_ok, seed, nonce, S_out, Sh, Ph, status);
+  } else if (Sh) {
+    hipLaunchKernelGGL((k_sm_prepare<true, false>), grid, dim3(64), 0, c.stream, base, n, idx, sig96, set_grp, table, table_ok, table_n,
                        comb, comb_ok, seed, nonce, S_out, Sh, Ph, status);
-  else
-    hipLaunchKernelGGL(k_sm_prepare<false>, dim3((n + 63) / 64), dim3(64), 0, c.stream, base, n, idx, sig96, set_grp, table, table_ok,
+  } else {
+    hipLaunchKernelGGL((k_sm_prepare<false, false>), grid, dim3(64), 0, c.stream, base, n, idx, sig96, set_grp, table, table_ok,
                        table_n, comb, comb_ok, seed, nonce, S_out, Sh, Ph, status);
+  }
   debug_sync(c.stream, "k_sm_prepare");
 }
 void launch_sm_redo_g2(LaunchCfg c, uint32_t base, uint32_t n, const uint32_t* set_grp, const uint8_t* status, const G2A* S, const Seed& seed,

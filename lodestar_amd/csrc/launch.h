@@ -14,6 +14,8 @@ void launch_hash_msgs(LaunchCfg c, const uint8_t* msgs32, uint32_t n, G2A* H, G2
 void launch_hash_clear_coop(hipStream_t s, uint32_t n, const G2J* Qpre, G2A* H);
 void launch_util_g2_out(LaunchCfg c, uint32_t n, const G2A* H, uint8_t* out192);
 
+// Signature.fromBytes decoding of sets [base, base + n): S[i] = the point, status[i] = GBV_PT_* (k_dec.hip)
+void launch_sig_decode(hipStream_t s, uint32_t base, uint32_t n, const uint8_t* sig96, G2A* S, uint8_t* status);
 void launch_sm_prepare(LaunchCfg c, uint32_t base, uint32_t n, const uint32_t* idx, const uint8_t* sig96, const uint32_t* set_grp,
                        const G1A* table, const uint8_t* table_ok, uint32_t table_n, const uint4* comb, const uint8_t* comb_ok,
                        const Seed& seed, uint32_t nonce, G2A* S_out, G2J* Sh, G1J* Ph, uint8_t* status);

@@ -6,11 +6,8 @@ set -e
 NAME=$1; shift
 OUT=lodestar_amd/variants
 mkdir -p $OUT/obj_$NAME
-for f in lodestar_amd/csrc/*.hip; do
-  b=$(basename $f .hip)
-  hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 "$@" -c $f -o $OUT/obj_$NAME/$b.o &
-done
-wait
+export FLAGS="$*" OBJ=$OUT/obj_$NAME
+ls lodestar_amd/csrc/*.hip | xargs -P 6 -I{} sh -c 'hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 $FLAGS -c {} -o $OBJ/$(basename {} .hip).o 2>/dev/null || { echo "FAILED {}"; exit 1; }'
 hipcc --offload-arch=gfx950 -shared -fPIC -o $OUT/libgbv_$NAME.so $OUT/obj_$NAME/*.o
 rm -rf $OUT/obj_$NAME
 echo built $OUT/libgbv_$NAME.so
