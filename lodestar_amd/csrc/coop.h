@@ -164,16 +164,29 @@ __device__ inline void ws_put(const Ws& w, uint32_t src, uint32_t idx, const Fp&
 // maximum length (lanes with fewer terms are masked off for the tail) -- then the nsc scaled terms
 // (|c| > 1: doubling / cyclotomic coefficients), read from the record in memory (rg) by a rolled
 // double-and-add loop.  No calls: the interpreter keeps its registers across the whole program.
-template <int N> GBV_HD Fp lin_eval(const Ws& w, const uint32_t* r, uint32_t npos, uint32_t nneg, uint32_t nsc, const uint32_t* rg) {
+//
+// The unit terms are summed WITHOUT modular reduction (every slot holds a canonical value, so a raw
+// 384-bit sum of up to 8 of them stays below 8p < 2^384): one 12-limb carry chain per term instead of
+// the add + conditional subtraction of fp_add, one 3-step reduction (fp_reduce8) after the 8th term and
+// where a canonical value is needed -- before the scaled terms, and for CANON results (sums that are
+// stored back into the workspace).  A product operand may stay below 8p: fp_mul_inl takes it (64 p^2 <
+// 2^392 p keeps the Montgomery output below 2p, reduced once).
+#ifndef GBV_COOP_LAZY
+#define GBV_COOP_LAZY 1  // 0: modular adds throughout (A/B)
+#endif
+template <int N, bool CANON>
+GBV_HD Fp lin_eval(const Ws& w, const uint32_t* r, uint32_t npos, uint32_t nneg, uint32_t nsc, const uint32_t* rg) {
   const uint32_t nu = npos + nneg;
   Fp acc = fp_zero();
 #pragma unroll
   for (int i = 0; i < N; ++i) {
     if ((uint32_t)i < nu) {
       Fp v = term_load(w, r[i], (uint32_t)i >= npos ? 1u : 0u);
-      acc = i == 0 ? v : fp_add(acc, v);
+      acc = i == 0 ? v : GBV_COOP_LAZY ? fp_add_lazy(acc, v) : fp_add(acc, v);
     }
+    if (GBV_COOP_LAZY && i == 7 && N > 8 && nu > 8) acc = fp_reduce8(acc);
   }
+  if (GBV_COOP_LAZY && nu > 1 && (CANON || nsc)) acc = fp_reduce8(acc);
   for (uint32_t j = 0; j < nsc; ++j) {
     const uint32_t t = rg[nu + j], m = t >> 16;
     const Fp v = term_load(w, t, (t >> 4) & 1);
@@ -204,13 +217,13 @@ template <int N> GBV_HD void load_words(uint32_t (&r)[N], const uint32_t* t) {
 // product k: Z[k] = A * B (rg: the record in memory, for the scaled terms)
 GBV_HD void prod_lane(const uint32_t (&r)[PROD_WORDS], const uint32_t* rg, int k, const Ws& w) {
   const uint32_t h = r[0], hs = r[1 + 2 * OPW];
-  Fp x = lin_eval<OPW>(w, r + 1, h & 0xFF, (h >> 8) & 0xFF, hs & 0xFF, rg + 1);
-  Fp y = lin_eval<OPW>(w, r + 1 + OPW, (h >> 16) & 0xFF, h >> 24, (hs >> 8) & 0xFF, rg + 1 + OPW);
+  Fp x = lin_eval<OPW, false>(w, r + 1, h & 0xFF, (h >> 8) & 0xFF, hs & 0xFF, rg + 1);
+  Fp y = lin_eval<OPW, false>(w, r + 1 + OPW, (h >> 16) & 0xFF, h >> 24, (hs >> 8) & 0xFF, rg + 1 + OPW);
   ws_put(w, SRC_Z, (uint32_t)k, fp_mul_inl(x, y));
 }
 
 GBV_HD Fp sum_lane(const uint32_t (&r)[SUM_WORDS], const uint32_t* rg, const Ws& w) {
-  return lin_eval<SUM_TERMS>(w, r + 1, r[0] & 0xFF, (r[0] >> 8) & 0xFF, (r[0] >> 16) & 0xFF, rg + 1);
+  return lin_eval<SUM_TERMS, true>(w, r + 1, r[0] & 0xFF, (r[0] >> 8) & 0xFF, (r[0] >> 16) & 0xFF, rg + 1);
 }
 
 #if defined(GBV_HOST_TEST)

@@ -128,11 +128,22 @@ GBV_HD Fp fp_dbl(const Fp& a) { return fp_add(a, a); }
 // the conditional subtraction of a modular add/sub is skipped.  fp_sub_lazy4: a + 4p - b for b < 4p.
 static constexpr Fp P4_RAW = {{0xfffeaaacu, 0xe7fbffffu, 0xc54ffffeu, 0x7aaffffau, 0xdac3d890u, 0x9cc34a83u, 0xce144afdu,
                                0x91dd2e13u, 0x0d2eb35du, 0x2c6e9ed9u, 0xe5ff9a69u, 0x680447a8u}};  // 4 p < 2^383
+static constexpr Fp P2_RAW = {{0xffff5556u, 0x73fdffffu, 0x62a7ffffu, 0x3d57fffdu, 0xed61ec48u, 0xce61a541u, 0xe70a257eu,
+                               0xc8ee9709u, 0x869759aeu, 0x96374f6cu, 0x72ffcd34u, 0x340223d4u}};  // 2 p
 #if defined(__HIP_DEVICE_COMPILE__)
 GBV_HD Fp fp_add_lazy(const Fp& a, const Fp& b) {
   Fp s;
   GBV_ASM_ADD_RAW(s, a, b);
   return s;
+}
+// x in [0, 8p) (a raw sum of up to 8 canonical values) -> [0, p): conditional subtractions of 4p, 2p, p
+GBV_HD Fp fp_reduce8(const Fp& x) {
+  Fp a, b, c;
+  const Fp k4 = P4_RAW, k2 = P2_RAW, k1 = P_RAW;
+  GBV_ASM_REDUCE_ONCE(a, x, k4);
+  GBV_ASM_REDUCE_ONCE(b, a, k2);
+  GBV_ASM_REDUCE_ONCE(c, b, k1);
+  return c;
 }
 GBV_HD Fp fp_sub_lazy4(const Fp& a, const Fp& b) {
   Fp t, d;
@@ -145,6 +156,13 @@ GBV_HD Fp fp_add_lazy(const Fp& a, const Fp& b) {
   Fp s;
   raw_add(s, a, b);
   return s;
+}
+GBV_HD Fp fp_reduce8(const Fp& x) {
+  Fp t, y = x;
+  if (!raw_sub(t, y, P4_RAW)) y = t;
+  if (!raw_sub(t, y, P2_RAW)) y = t;
+  if (!raw_sub(t, y, P_RAW)) y = t;
+  return y;
 }
 GBV_HD Fp fp_sub_lazy4(const Fp& a, const Fp& b) {
   Fp t, d;

@@ -6,8 +6,9 @@ TAG=$1; shift
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-LODESTAR_AMD_LIB=lodestar_amd/variants/libgbv_$1.so timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_parity.py tests/test_gpu_c3.py tests/test_gpu_c5.py > "$OUT/test_$1.log" 2>&1 || { echo "tests failed"; tail -30 "$OUT/test_$1.log"; exit 1; }
-tail -n 1 "$OUT/test_$1.log"
+# full GPU parity suite on the in-tree library (the candidate default)
+timeout -k 10 420 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > "$OUT/test_base.log" 2>&1 || { echo "tests failed"; tail -30 "$OUT/test_base.log"; exit 1; }
+tail -n 1 "$OUT/test_base.log"
 for v in base "$@"; do
   if [ "$v" = base ]; then lib=""; else lib=lodestar_amd/variants/libgbv_$v.so; fi
   LODESTAR_AMD_LIB=$lib timeout -k 10 200 python3 -u tools/latency_probe.py > "$OUT/lat_$v.log" 2>&1 || { echo "probe $v failed"; tail -20 "$OUT/lat_$v.log"; exit 1; }
