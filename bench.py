@@ -777,6 +777,14 @@ def main():
         extras["c5"] = c5_bench(v, call_off, idx, sigs, msgs)
         log("c5: %s sets/s (%.1fs)" % (extras["c5"]["value"], time.time() - t))
 
+    vs_shard = None
+    if world > 1 and args.mode == "gossip" and not args.no_extras:
+        # the north_star multi-GPU path beside the gossip replicas: ONE verifySignatureSets call sharded
+        # over every rank, Fp12 Miller partials all-gathered over RCCL, one final exponentiation each
+        vs_shard = vs_shard_measure(args, v, sk_ints, world, rank, log)
+        if rank == 0:
+            log("vs-shard: %s sets/s over %d ranks" % (vs_shard["value"], world))
+
     ssz = None
     if rank == 0 and world == 1 and not args.no_signing_roots:
         ssz = signing_roots_bench(v, cpu_sample=0 if args.no_cpu_baseline else 20000)
@@ -828,6 +836,7 @@ def main():
         "c4e": extras.get("c4e"),
         "c5": extras.get("c5"),
         "signing_roots": ssz,
+        "vs_shard": vs_shard,
     }
     if rank == 0:
         print(json.dumps(line), flush=True)
@@ -839,8 +848,17 @@ def main():
 
 
 def vs_shard_main(args, v, sk_ints, world, rank, local_rank, dist, log):
-    """--mode vs-shard: ONE verifySignatureSets call (args.shard_calls x 128 sets of 128-member
-    aggregates, a C3-sized range-sync / replay call) sharded over the ranks by cost-balanced
+    line = vs_shard_measure(args, v, sk_ints, world, rank, log)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    import torch.distributed as tdist
+    tdist.barrier()
+    tdist.destroy_process_group()
+
+
+def vs_shard_measure(args, v, sk_ints, world, rank, log):
+    """--mode vs-shard (and the `vs_shard` object of a multi-GPU gossip line): ONE verifySignatureSets
+    call (args.shard_calls x 128 sets of 128-member aggregates, a C3-sized range-sync / replay call) sharded over the ranks by cost-balanced
     contiguous ranges (lodestar_amd/sharded.py).  Each rank stages its shard in HBM; a step is
     gbv_vs_batch_partial (the shard's Fp12 Miller product) -> 577-byte RCCL all-gather -> one final
     exponentiation over all partials (gbv_fp12_check) on every rank.  Before timing: the sharded
@@ -879,6 +897,7 @@ def vs_shard_main(args, v, sk_ints, world, rank, local_rank, dist, log):
     tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
     elapsed = float(t.item())
     staged.close()
+    line = None
     if rank == 0:
         line = {"metric": "signature sets verified/sec (one verifySignatureSets call sharded over GPUs: Fp12 partials + RCCL all-gather)",
                 "value": round(len(sets) * args.steps / elapsed, 1), "unit": "sets/s", "n_gpus": world, "steps": args.steps,
@@ -891,9 +910,7 @@ def vs_shard_main(args, v, sk_ints, world, rank, local_rank, dist, log):
                 "partial_bytes_per_gpu": 577, "rank0_shard": [lo, hi],
                 "parity": {"sharded_equals_single_gpu": single is True, "wrong_signature_call_false": wrong is False,
                            "clean_small_call_true": ok_small is True}}
-        print(json.dumps(line), flush=True)
-    tdist.barrier()
-    tdist.destroy_process_group()
+    return line
 
 
 if __name__ == "__main__":

@@ -34,6 +34,8 @@ namespace coop {
 struct Prog {
   uint8_t n_rounds, n_part, n_out;
   uint16_t round_end[6];
+  uint8_t amax[6], bmax[6];  // per round: the largest unit-term count of the A / B operands
+  uint8_t pmax, omax;        // the same for the partial sums and the outputs
   const uint32_t* prods;
   const uint32_t* parts;
   const uint32_t* outs;
@@ -141,10 +143,14 @@ __device__ inline Ws make_ws(Slot* mem, uint16_t z, uint16_t o0, uint16_t o1 = 0
   auto u = [m](uint16_t o) { return m + 2u * o; };
   return Ws{{u(o0) | u(o1) << 16, u(o2) | u(o3) << 16, u(o4) | u(o5) << 16, u(z) | lds_unit(GBV_CONSTS_LDS) << 16}};
 }
+// branch-free: a term's source differs per lane, and a select chain written as ?: compiled to
+// exec-mask branches around every term
 __device__ inline uint32_t ws_unit(const Ws& w, uint32_t src, uint32_t idx) {
-  const uint32_t pr = src >> 1;
-  const uint32_t word = pr == 0 ? w.b[0] : pr == 1 ? w.b[1] : pr == 2 ? w.b[2] : w.b[3];
-  return ((src & 1) ? word >> 16 : word & 0xFFFFu) + 2u * idx;
+  const uint32_t m1 = 0u - ((src >> 1) & 1u), m2 = 0u - ((src >> 2) & 1u);
+  const uint32_t w01 = w.b[0] ^ ((w.b[0] ^ w.b[1]) & m1);
+  const uint32_t w23 = w.b[2] ^ ((w.b[2] ^ w.b[3]) & m1);
+  const uint32_t word = w01 ^ ((w01 ^ w23) & m2);
+  return ((word >> ((src & 1u) << 4)) & 0xFFFFu) + 2u * idx;
 }
 __device__ inline Fp term_load(const Ws& w, uint32_t t, uint32_t neg) {
   const LFp* q = (const LFp*)(size_t)((ws_unit(w, t & 7, (t >> 8) & 0xFF) + neg) << 6);
@@ -159,41 +165,55 @@ __device__ inline void ws_put(const Ws& w, uint32_t src, uint32_t idx, const Fp&
 }
 #endif
 
-// Signed sum of a record's terms: the npos (+1) and nneg (-1) unit terms of r[0 .. N) -- each one
-// slot load of the value or its stored negation, then one modular add, unrolled over the record's
-// maximum length (lanes with fewer terms are masked off for the tail) -- then the nsc scaled terms
-// (|c| > 1: doubling / cyclotomic coefficients), read from the record in memory (rg) by a rolled
-// double-and-add loop.  No calls: the interpreter keeps its registers across the whole program.
+// Signed sum of a record's terms: the nu unit terms (+1, or -1 with the neg bit of the term word)
+// of r[0 .. N) -- each one slot load of the value or its stored negation -- then the nsc scaled terms
+// (|c| > 1: doubling / cyclotomic coefficients) that follow them, read from the record in memory (rg)
+// by a rolled double-and-add loop.  No calls: the interpreter keeps its registers across the whole
+// program.
 //
-// The unit terms are summed WITHOUT modular reduction (every slot holds a canonical value, so a raw
-// 384-bit sum of up to 8 of them stays below 8p < 2^384): one 12-limb carry chain per term instead of
-// the add + conditional subtraction of fp_add, one 3-step reduction (fp_reduce8) after the 8th term and
-// where a canonical value is needed -- before the scaled terms, and for CANON results (sums that are
-// stored back into the workspace).  A product operand may stay below 8p: fp_mul_inl takes it (64 p^2 <
-// 2^392 p keeps the Montgomery output below 2p, reduced once).
+// The unit-term loop runs `umax` times on every lane -- the phase's largest unit count, from the
+// program (wave-uniform: scalar branches only) -- and a lane's words past its own nu are masked to the
+// zero constant (ZERO_TERM) by one select each.  So all the loads of an operand issue back to back
+// and their latencies overlap, and the adds follow without per-term branches.  The adds are raw
+// 384-bit sums (every slot holds a canonical value; a sum of up to 8 stays below 8p < 2^384): one
+// 12-limb carry chain per term, reduced (fp_reduce8) after the 8th term and where a canonical value is
+// needed -- before the scaled terms, and for CANON results (sums stored back into the workspace).  A
+// product operand may stay below 8p: fp_mul_inl takes it (64 p^2 < 2^392 p keeps the Montgomery
+// output below 2p, reduced once).
 #ifndef GBV_COOP_LAZY
 #define GBV_COOP_LAZY 1  // 0: modular adds throughout (A/B)
 #endif
 template <int N, bool CANON>
-GBV_HD Fp lin_eval(const Ws& w, const uint32_t* r, uint32_t npos, uint32_t nneg, uint32_t nsc, const uint32_t* rg) {
-  const uint32_t nu = npos + nneg;
+GBV_HD Fp lin_eval(const Ws& w, const uint32_t* r, uint32_t umax, uint32_t nu, uint32_t nsc, const uint32_t* rg) {
+  // groups of G terms: the G loads issue together, then their adds (G x 12 VGPRs in flight)
+  constexpr int G = 4;
   Fp acc = fp_zero();
 #pragma unroll
-  for (int i = 0; i < N; ++i) {
-    if ((uint32_t)i < nu) {
-      Fp v = term_load(w, r[i], (uint32_t)i >= npos ? 1u : 0u);
-      acc = i == 0 ? v : GBV_COOP_LAZY ? fp_add_lazy(acc, v) : fp_add(acc, v);
+  for (int g = 0; g < N; g += G) {
+    Fp v[G];
+#pragma unroll
+    for (int q = 0; q < G; ++q) {
+      const int i = g + q;
+      if (i < N && (uint32_t)i < umax) {
+        const uint32_t t = (uint32_t)i < nu ? r[i] : ZERO_TERM;
+        v[q] = term_load(w, t, (t >> 4) & 1);
+      }
     }
-    if (GBV_COOP_LAZY && i == 7 && N > 8 && nu > 8) acc = fp_reduce8(acc);
+#pragma unroll
+    for (int q = 0; q < G; ++q) {
+      const int i = g + q;
+      if (i < N && (uint32_t)i < umax) acc = i == 0 ? v[q] : GBV_COOP_LAZY ? fp_add_lazy(acc, v[q]) : fp_add(acc, v[q]);
+      if (GBV_COOP_LAZY && i == 7 && N > 8 && umax > 8) acc = fp_reduce8(acc);
+    }
   }
-  if (GBV_COOP_LAZY && nu > 1 && (CANON || nsc)) acc = fp_reduce8(acc);
+  if (GBV_COOP_LAZY && umax > 1 && (CANON || nsc)) acc = fp_reduce8(acc);
   for (uint32_t j = 0; j < nsc; ++j) {
     const uint32_t t = rg[nu + j], m = t >> 16;
-    const Fp v = term_load(w, t, (t >> 4) & 1);
-    Fp s = v;
+    const Fp vs = term_load(w, t, (t >> 4) & 1);
+    Fp s = vs;
     for (int bit = 30 - __builtin_clz(m); bit >= 0; --bit) {  // m >= 2: below the top bit
       s = fp_dbl(s);
-      if ((m >> bit) & 1) s = fp_add(s, v);
+      if ((m >> bit) & 1) s = fp_add(s, vs);
     }
     acc = (nu == 0 && j == 0) ? s : fp_add(acc, s);
   }
@@ -214,16 +234,17 @@ template <int N> GBV_HD void load_words(uint32_t (&r)[N], const uint32_t* t) {
   }
 }
 
-// product k: Z[k] = A * B (rg: the record in memory, for the scaled terms)
-GBV_HD void prod_lane(const uint32_t (&r)[PROD_WORDS], const uint32_t* rg, int k, const Ws& w) {
+// product k: Z[k] = A * B (rg: the record in memory, for the scaled terms; amax / bmax: the round's
+// unit-term trip counts)
+GBV_HD void prod_lane(const uint32_t (&r)[PROD_WORDS], const uint32_t* rg, int k, const Ws& w, uint32_t amax, uint32_t bmax) {
   const uint32_t h = r[0], hs = r[1 + 2 * OPW];
-  Fp x = lin_eval<OPW, false>(w, r + 1, h & 0xFF, (h >> 8) & 0xFF, hs & 0xFF, rg + 1);
-  Fp y = lin_eval<OPW, false>(w, r + 1 + OPW, (h >> 16) & 0xFF, h >> 24, (hs >> 8) & 0xFF, rg + 1 + OPW);
+  Fp x = lin_eval<OPW, false>(w, r + 1, amax, (h & 0xFF) + ((h >> 8) & 0xFF), hs & 0xFF, rg + 1);
+  Fp y = lin_eval<OPW, false>(w, r + 1 + OPW, bmax, ((h >> 16) & 0xFF) + (h >> 24), (hs >> 8) & 0xFF, rg + 1 + OPW);
   ws_put(w, SRC_Z, (uint32_t)k, fp_mul_inl(x, y));
 }
 
-GBV_HD Fp sum_lane(const uint32_t (&r)[SUM_WORDS], const uint32_t* rg, const Ws& w) {
-  return lin_eval<SUM_TERMS, true>(w, r + 1, r[0] & 0xFF, (r[0] >> 8) & 0xFF, (r[0] >> 16) & 0xFF, rg + 1);
+GBV_HD Fp sum_lane(const uint32_t (&r)[SUM_WORDS], const uint32_t* rg, const Ws& w, uint32_t umax) {
+  return lin_eval<SUM_TERMS, true>(w, r + 1, umax, (r[0] & 0xFF) + ((r[0] >> 8) & 0xFF), (r[0] >> 16) & 0xFF, rg + 1);
 }
 
 #if defined(GBV_HOST_TEST)
@@ -240,18 +261,18 @@ inline void run(const Prog& P, const Ws& w) {
   for (int r = 0; r < P.n_rounds; ++r) {
     for (int k = p0; k < P.round_end[r]; ++k) {
       load_words(rec, P.prods + PROD_WORDS * k);
-      prod_lane(rec, P.prods + PROD_WORDS * k, k, w);
+      prod_lane(rec, P.prods + PROD_WORDS * k, k, w, P.amax[r], P.bmax[r]);
     }
     p0 = P.round_end[r];
   }
   for (int j = 0; j < P.n_part; ++j) {
     load_words(r8, P.parts + SUM_WORDS * j);
-    ws_put(w, SRC_Z, P.round_end[P.n_rounds - 1] + j, sum_lane(r8, P.parts + SUM_WORDS * j, w));
+    ws_put(w, SRC_Z, P.round_end[P.n_rounds - 1] + j, sum_lane(r8, P.parts + SUM_WORDS * j, w, P.pmax));
   }
   Fp o[LANES];
   for (int k = 0; k < P.n_out; ++k) {
     load_words(r8, P.outs + SUM_WORDS * k);
-    o[k] = sum_lane(r8, P.outs + SUM_WORDS * k, w);
+    o[k] = sum_lane(r8, P.outs + SUM_WORDS * k, w, P.omax);
   }
   for (int k = 0; k < P.n_out; ++k) ws_put(w, P.out_dst[k], P.out_idx[k], o[k]);
 }
@@ -282,15 +303,19 @@ __device__ __noinline__ void run_ni(const Prog* PP, uint32_t b0, uint32_t b1, ui
   if (have_out) load_words(rout, gout);
   for (int r = 0; r < P.n_rounds; ++r) {
     int p1 = P.round_end[r];
-    if (p0 + lane < p1) prod_lane(rec, P.prods + PROD_WORDS * (p0 + lane), p0 + lane, w);  // every round has <= 64 products
+    // the round's unit-term trip counts, wave-uniform (scalar registers: the term loops branch on them
+    // without exec-mask juggling)
+    const uint32_t am = __builtin_amdgcn_readfirstlane(P.amax[r]), bm = __builtin_amdgcn_readfirstlane(P.bmax[r]);
+    if (p0 + lane < p1) prod_lane(rec, P.prods + PROD_WORDS * (p0 + lane), p0 + lane, w, am, bm);  // every round has <= 64 products
     if (r + 1 < P.n_rounds && p1 + lane < P.round_end[r + 1]) load_words(rec, P.prods + PROD_WORDS * (p1 + lane));
     p0 = p1;
     __syncthreads();
   }
-  if (have_part) ws_put(w, SRC_Z, P.round_end[P.n_rounds - 1] + lane, sum_lane(rpart, gpart, w));
+  const uint32_t pm = __builtin_amdgcn_readfirstlane(P.pmax), om = __builtin_amdgcn_readfirstlane(P.omax);
+  if (have_part) ws_put(w, SRC_Z, P.round_end[P.n_rounds - 1] + lane, sum_lane(rpart, gpart, w, pm));
   if (P.n_part) __syncthreads();
   Fp o;
-  if (have_out) o = sum_lane(rout, gout, w);
+  if (have_out) o = sum_lane(rout, gout, w, om);
   __syncthreads();
   if (have_out) ws_put(w, P.out_dst[lane], P.out_idx[lane], o);
   __syncthreads();

@@ -83,6 +83,8 @@ class Const:
 
 
 CONSTS = Const()
+CONSTS.get(0)
+ZERO_IDX = CONSTS.index[0]  # the constant 0 (registered first): padding of the records
 
 
 class Builder:
@@ -459,17 +461,26 @@ def term_word(t, neg=False):
     return src | (int(neg) << 4) | (idx << 8) | (abs(c) << 16)
 
 
+ZERO_TERM = SRC_C | (ZERO_IDX << 8) | (1 << 16)
+
+
 def signed_record(T, t0, tn, width):
-    """(npos, nneg, nsc, words): the terms of T[t0:t0+tn] -- coefficient +1 terms, then -1 terms,
-    then scaled terms (|c| > 1, sign bit 4) -- each a u32 (src | neg << 4 | idx << 8 | |c| << 16),
-    padded to `width` words."""
+    """(npos, nneg, nsc, words): the terms of T[t0:t0+tn] as `width` u32 words (src | neg << 4 |
+    idx << 8 | |c| << 16): the unit terms (+1, then -1 with the neg bit) from word 0, then the scaled
+    terms (|c| > 1), then the zero constant (ZERO_TERM) as padding."""
     ts = list(T[t0:t0 + tn])
     pos = [t for t in ts if t[2] == 1]
     neg = [t for t in ts if t[2] == -1]
     sc = [t for t in ts if abs(t[2]) > 1]
     assert len(pos) + len(neg) + len(sc) == len(ts) and len(ts) <= width
-    words = [term_word(t) for t in pos + neg] + [term_word(t, t[2] < 0) for t in sc]
-    return len(pos), len(neg), len(sc), words + [0] * (width - len(words))
+    words = [term_word(t) for t in pos] + [term_word(t, True) for t in neg] + [term_word(t, t[2] < 0) for t in sc]
+    return len(pos), len(neg), len(sc), words + [ZERO_TERM] * (width - len(words))
+
+
+def phase_umax(T, recs):
+    """The wave-uniform trip count of a phase's unit-term loop (its lanes' records recs = [(t0, tn)]):
+    the largest unit count.  A lane masks the words past its own count to the zero constant."""
+    return max([sum(1 for t in T[t0:t0 + tn] if abs(t[2]) == 1) for t0, tn in recs] or [0])
 
 
 def emit(progs, path):
@@ -478,6 +489,7 @@ def emit(progs, path):
          "#pragma once", '#include "fp_types.h"', "", "namespace gbv {", "namespace coop {", ""]
     assert len(CONSTS.vals) <= 16
     L.append("constexpr int N_CONSTS = %d;" % len(CONSTS.vals))
+    L.append("constexpr uint32_t ZERO_TERM = 0x%xu;  // the constant 0: record padding, masked-off terms" % ZERO_TERM)
     L.append("GBV_COOP_TABLE Fp CONSTS[%d] = {" % max(1, len(CONSTS.vals)))
     for v in CONSTS.vals or [0]:
         L.append("    {{%s}}," % ", ".join(limbs(mont(v))))
@@ -515,8 +527,18 @@ def emit(progs, path):
         L.append("GBV_COOP_TABLE uint8_t %s_OUT_IDX[%d] = {%s};" % (n, len(p["outs"]), ", ".join(str(o[3]) for o in p["outs"])))
         re = p["round_end"] + [0] * (6 - len(p["round_end"]))
         assert len(p["round_end"]) <= 6
-        L.append("GBV_COOP_TABLE Prog %s = {%d, %d, %d, {%s}, &%s_PRODS[0][0], &%s_PARTS[0][0], &%s_OUTS[0][0], %s_OUT_DST, %s_OUT_IDX};" % (
-            n, len(p["round_end"]), len(p["parts"]), len(p["outs"]), ", ".join(map(str, re)), n, n, n, n, n))
+        amax, bmax, r0 = [], [], 0
+        for r1 in p["round_end"]:
+            amax.append(phase_umax(T, [(a0, an) for (a0, an, _, _) in p["prods"][r0:r1]]))
+            bmax.append(phase_umax(T, [(b0, bn) for (_, _, b0, bn) in p["prods"][r0:r1]]))
+            r0 = r1
+        amax += [0] * (6 - len(amax))
+        bmax += [0] * (6 - len(bmax))
+        pmax = phase_umax(T, [(t0, tn) for (t0, tn, _) in p["parts"]])
+        omax = phase_umax(T, [(t0, tn) for (t0, tn, _, _) in p["outs"]])
+        L.append("GBV_COOP_TABLE Prog %s = {%d, %d, %d, {%s}, {%s}, {%s}, %d, %d, &%s_PRODS[0][0], &%s_PARTS[0][0], &%s_OUTS[0][0], %s_OUT_DST, %s_OUT_IDX};" % (
+            n, len(p["round_end"]), len(p["parts"]), len(p["outs"]), ", ".join(map(str, re)), ", ".join(map(str, amax)),
+            ", ".join(map(str, bmax)), pmax, omax, n, n, n, n, n))
     L += ["", "}  // namespace coop", "}  // namespace gbv", ""]
     open(path, "w").write("\n".join(L))
 
