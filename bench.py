@@ -116,6 +116,29 @@ def pmc_evidence(units_per_launch, kernel="k_sm_prepare<false>", alg_bytes=ALG_B
     return per_set * units_per_launch, ev
 
 
+def pmc_stage_evidence(units_per_launch, kernels, alg_bytes):
+    """pmc_evidence for a stage of several kernels run back to back on one stream (the same-message
+    prepare stage: k_sig_decode then k_sm_prepare<false, true>): HBM bytes and VALU instructions per
+    set summed over the kernels, issue utilisation over their summed durations.  Falls back to the
+    single-kernel form (older summaries: one k_sm_prepare<false>)."""
+    try:
+        summary = json.load(open(PMC_SUMMARY))
+    except (OSError, ValueError):
+        return None, None
+    ds = [summary.get(k) for k in kernels]
+    if not all(d and "FETCH_SIZE" in d and "WRITE_SIZE" in d for d in ds):
+        return pmc_evidence(units_per_launch, "k_sm_prepare<false>", alg_bytes)
+    per_set = sum((2 * d["FETCH_SIZE"] + d["WRITE_SIZE"]) * 1024.0 / d["grid_size"] for d in ds)
+    have_sq = all("SQ_INSTS_VALU" in d and "SQ_WAVES" in d for d in ds)
+    dur = sum(d["duration_ms"] for d in ds)
+    ev = {"source": os.path.relpath(PMC_SUMMARY, ROOT), "kernel": " + ".join(kernels), "pmc_grid_sets": int(ds[0]["grid_size"]),
+          "hbm_bytes_per_set": round(per_set, 1), "algorithmic_bytes_per_set": alg_bytes,
+          "valu_wave_instr_per_set": round(sum(d["SQ_INSTS_VALU"] / d["SQ_WAVES"] for d in ds)) if have_sq else None,
+          "valu_issue_utilisation": round(sum(d["SQ_INSTS_VALU"] for d in ds) / (dur * 1e-3 * PEAK_VALU_WAVE_INSTR_PER_S), 4) if have_sq else None,
+          "per_kernel_ms_at_pmc_grid": {k: round(d["duration_ms"], 3) for k, d in zip(kernels, ds)}}
+    return per_set * units_per_launch, ev
+
+
 # device kernels of one same-message verify, in gbv_last_kernel_ms order
 KERNELS = ["hash", "prepare", "chunk_finish", "miller", "seg_check", "group_pairing", "fallback", "msm"]
 VS_KERNELS = ["agg", "hash_sig", "miller", "chunk_check"]
@@ -549,7 +572,7 @@ def api_stream_rate(v, call_off, idx, sigs, msgs, n_sets=1 << 20):
     objects (the caller's deserialized gossip data) are built before it."""
     import asyncio
     from lodestar_amd import PackedSameMessageSets
-    k = int(np.searchsorted(call_off, n_sets))
+    k = min(int(np.searchsorted(call_off, n_sets)), len(call_off) - 1)
     n = int(call_off[k])
     sig_mv = memoryview(sigs)
     reqs = [(PackedSameMessageSets(idx[call_off[g]:call_off[g + 1]], sig_mv[96 * int(call_off[g]):96 * int(call_off[g + 1])]),
@@ -589,6 +612,8 @@ def main():
                          "default 0 for gossip, 0.01 for replay (C5)")
     ap.add_argument("--no-signing-roots", action="store_true", help="skip the signing-root secondary line")
     ap.add_argument("--no-extras", action="store_true", help="skip the c1/c3/c4 secondary lines")
+    ap.add_argument("--no-api", action="store_true",
+                    help="skip the API-path rates (their 2^18-set passes would mix launch sizes into a rocprof summary)")
     ap.add_argument("--no-stream", dest="stream", action="store_false",
                     help="one batch at a time (no overlap of consecutive verifications)")
     ap.add_argument("--inflight", type=int, default=3, help="staged batches queued on the device at once")
@@ -735,9 +760,9 @@ def main():
         assert all(g == gather[2] for g in gathered), (gathered[:3], gather[2])
 
     lat = p50_batch_latency(v, idx, sigs, msgs)
-    api_rate, api_n = api_path_rate(v, call_off, idx, sigs, msgs) if (rank == 0 and not invalid_frac) else (None, 0)
-    api_stream, api_stream_n, api_stream_passes = (api_stream_rate(v, call_off, idx, sigs, msgs) if (rank == 0 and not invalid_frac)
-                                                   else (None, 0, 0))
+    do_api = rank == 0 and not invalid_frac and not args.no_api
+    api_rate, api_n = api_path_rate(v, call_off, idx, sigs, msgs) if do_api else (None, 0)
+    api_stream, api_stream_n, api_stream_passes = api_stream_rate(v, call_off, idx, sigs, msgs) if do_api else (None, 0, 0)
     if api_stream:
         log("api stream: %s sets/s over %d sets in %d device passes" % (api_stream, api_stream_n, api_stream_passes))
 
@@ -748,9 +773,11 @@ def main():
     w_fme = (W_PREPARE_FME_MSM_COMB if comb else W_PREPARE_FME_MSM) if kcnt[7] > 0 else W_PREPARE_FME
     achieved = units_per_launch * w_fme * MAC_PER_FME / t_launch / 1e12 if t_launch > 0 else 0.0
     peak = PEAK_MAC_PER_S / 1e12
-    traffic, pmc = pmc_evidence(units_per_launch, "k_sm_prepare<false>" if kcnt[7] > 0 else "k_sm_prepare<true>",
-                                ALG_BYTES_PER_SET_COMB if comb else ALG_BYTES_PER_SET)
-    roofline = {"bound": "valu-int", "kernel": "k_sm_prepare", "achieved": round(achieved, 4), "peak": peak,
+    traffic, pmc = (pmc_stage_evidence(units_per_launch, ["k_sig_decode", "k_sm_prepare<false, true>"],
+                                       ALG_BYTES_PER_SET_COMB if comb else ALG_BYTES_PER_SET) if kcnt[7] > 0
+                    else pmc_evidence(units_per_launch, "k_sm_prepare<true, true>", ALG_BYTES_PER_SET))
+    roofline = {"bound": "valu-int", "kernel": "k_sm_prepare (k_sig_decode + k_sm_prepare<false, true>, one stream)",
+                "achieved": round(achieved, 4), "peak": peak,
                 "unit": "T u32-MAC/s", "frac": round(achieved / peak, 5),
                 "traffic": round(traffic) if traffic is not None else None, "pmc": pmc,
                 "work_per_unit_fme": w_fme, "work_per_unit_fme_survey": W_SURVEY_SAME_MESSAGE, "comb_tables": comb,
@@ -824,8 +851,9 @@ def main():
                    "submission": "streamed: %d batches in flight" % depth if depth > 1 else "one batch at a time",
                    "invalid_frac": invalid_frac},
         "api_path_sets_per_s": api_stream,
-        "api_path": {"how": "asyncio: every call of the sample issued at once through GpuBlsVerifier.verify_signature_sets_same_message "
-                            "(packed inputs), job queue + up to 3 streamed device passes, booleans checked",
+        "api_path": {"how": "asyncio: every gossip call of the workload issued through GpuBlsVerifier.verify_signature_sets_same_message "
+                            "(packed inputs, prebuilt requests); the job queue cuts passes of <= 2^18 sets, up to 3 on the device "
+                            "at once; every boolean checked",
                      "sample_sets": api_stream_n, "device_passes": api_stream_passes,
                      "oneshot_sets_per_s": api_rate, "oneshot_how": "one gbv_verify_same_message_multi call from host buffers"},
         "roofline": roofline,

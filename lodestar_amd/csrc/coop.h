@@ -280,11 +280,20 @@ inline void run(const Prog& P, const Ws& w) {
 #define COOP_LANE0 if (true)
 #else
 __device__ inline unsigned lane_id() { return threadIdx.x; }
-__device__ inline void barrier() { __syncthreads(); }
+// A coop job is ONE wave: its phases synchronise at wavefront scope -- the workgroup-scope fences
+// of __syncthreads (prior LDS writes complete and visible, later reads not hoisted) around a wave
+// barrier instead of s_barrier.  For the one-wave workgroups this is what __syncthreads compiles to
+// anyway; it also lets a workgroup hold a second wave doing other work (k_hash_clear_coop), which
+// meets the coop wave only at explicit __syncthreads.
+__device__ inline void barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
 // Every kernel that runs programs calls this first (lane-parallel copy of the constant pool).
 __device__ inline void load_consts() {
   if (threadIdx.x < N_CONSTS) put(GBV_CONSTS_LDS + threadIdx.x, CONSTS[threadIdx.x]);
-  __syncthreads();
+  barrier();
 }
 
 // All of a lane's records for this program are fetched up front (one memory latency), the next
@@ -309,16 +318,16 @@ __device__ __noinline__ void run_ni(const Prog* PP, uint32_t b0, uint32_t b1, ui
     if (p0 + lane < p1) prod_lane(rec, P.prods + PROD_WORDS * (p0 + lane), p0 + lane, w, am, bm);  // every round has <= 64 products
     if (r + 1 < P.n_rounds && p1 + lane < P.round_end[r + 1]) load_words(rec, P.prods + PROD_WORDS * (p1 + lane));
     p0 = p1;
-    __syncthreads();
+    barrier();
   }
   const uint32_t pm = __builtin_amdgcn_readfirstlane(P.pmax), om = __builtin_amdgcn_readfirstlane(P.omax);
   if (have_part) ws_put(w, SRC_Z, P.round_end[P.n_rounds - 1] + lane, sum_lane(rpart, gpart, w, pm));
-  if (P.n_part) __syncthreads();
+  if (P.n_part) barrier();
   Fp o;
   if (have_out) o = sum_lane(rout, gout, w, om);
-  __syncthreads();
+  barrier();
   if (have_out) ws_put(w, P.out_dst[lane], P.out_idx[lane], o);
-  __syncthreads();
+  barrier();
 }
 // One out-of-line copy of the interpreter serves every call site (the drivers make hundreds).
 __device__ inline void run(const Prog& P, const Ws& w) { run_ni(&P, w.b[0], w.b[1], w.b[2], w.b[3]); }

@@ -11,6 +11,7 @@
 #include "fp_types.h"
 #include "bls_constants.h"
 #include "fp_asm.h"
+#include "inv_sg.h"
 
 namespace gbv {
 
@@ -424,7 +425,10 @@ GBV_HD Fp fp_half(const Fp& x) {
 // until u == 0, when v = 1 and x2 = A^-1; the result is A^-1 R^3 R^-1 = a^-1 R.  Every lane runs
 // the same straight-line step (~190 VALU ops), checked for completion every 32 steps: about
 // 2.5x cheaper than the 381-bit exponentiation (608 Fp products) it replaces.
-GBV_NI Fp fp_inv(Fp a) {
+#ifndef GBV_INV_SAFEGCD
+#define GBV_INV_SAFEGCD 1  // 0: the binary extended GCD below (A/B)
+#endif
+GBV_NI Fp fp_inv_bgcd(Fp a) {
   Fp u = a, v = P_RAW, x1 = FP_ONE_RAW_, x2 = fp_zero();
   for (int outer = 0; outer < 48; ++outer) {  // <= 2 * 381 steps are needed; 48 * 32 = 1536
     for (int k = 0; k < 32; ++k) {
@@ -451,6 +455,15 @@ GBV_NI Fp fp_inv(Fp a) {
 #endif
   }
   return fp_mul(x2, R3_RAW);
+}
+
+// Inverse by safegcd divsteps (inv_sg.h): (a R)^-1 R^3 R^-1 = a^-1 R.  0 -> 0.
+GBV_NI Fp fp_inv(Fp a) {
+#if GBV_INV_SAFEGCD
+  return fp_mul(sg::inv_raw(a), R3_RAW);
+#else
+  return fp_inv_bgcd(a);
+#endif
 }
 
 // Canonical (non-Montgomery) value comparisons used by sign rules ----------------------------

@@ -7,6 +7,9 @@
 #ifndef GBV_DEC_SPLIT_DEFAULT
 #define GBV_DEC_SPLIT_DEFAULT 1
 #endif
+#ifndef GBV_SUB_SPLIT_DEFAULT
+#define GBV_SUB_SPLIT_DEFAULT 0
+#endif
 
 namespace gbv {
 
@@ -104,6 +107,55 @@ __global__ void GBV_KERNEL_ATTR k_sm_prepare(uint32_t base, uint32_t n, const ui
     if (WITH_G2) Sh_out[i] = rs;
     Ph_out[i] = rp;
   }
+}
+
+// The G1-only throughput form (bucket-MSM segments) in two more kernels after k_sig_decode, each
+// with the registers of its own phase: the G2 subgroup check (the long chain: 63 Jacobian doublings
+// over Fp2, two waves per SIMD) only writes the status byte; r_i pk_i from the comb table and the
+// 8-lane chunk scan (G1 points: a small live state) run after it at a higher occupancy.  Same r_i,
+// statuses, scan and outputs as k_sm_prepare<false, true>.
+__global__ void GBV_KERNEL_ATTR k_sm_subgroup(uint32_t base, uint32_t n, const uint32_t* __restrict__ idx, const uint8_t* __restrict__ table_ok,
+                                              uint32_t table_n, const G2A* __restrict__ S, uint8_t* __restrict__ status) {
+  const uint32_t t = blockIdx.x * 64 + threadIdx.x;
+  if (t >= n) return;
+  const uint32_t i = base + t;
+  const uint32_t k = idx[i];
+  uint8_t st = (k >= table_n || !table_ok[k]) ? SET_BAD_PK : SET_OK;
+  const uint8_t ds = status[i];
+  if (ds != PT_OK || !g2_in_subgroup(S[i])) st = SET_BAD_SIG;
+  status[i] = st;
+}
+
+#ifndef GBV_RPK_WAVES
+#define GBV_RPK_WAVES 2
+#endif
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GBV_RPK_WAVES)))
+k_sm_rpk(uint32_t base, uint32_t n, const uint32_t* __restrict__ idx, const uint32_t* __restrict__ set_grp, const G1A* __restrict__ table,
+         const uint4* __restrict__ comb, const uint8_t* __restrict__ comb_ok, Seed seed, uint32_t nonce, G1J* __restrict__ Ph_out,
+         const uint8_t* __restrict__ status) {
+  const unsigned lane = threadIdx.x;
+  const uint32_t t = blockIdx.x * 64 + lane;
+  const bool act = t < n;
+  const uint32_t i = base + t;
+  const uint32_t key = act ? set_grp[i] : 0xffffffffu;
+  G1J rp = jac_infinity<Fp>();
+  if (act && status[i] == SET_OK) {
+    const uint32_t k = idx[i];
+    const uint64_t r = prf_scalar(seed, i, nonce);
+    if (comb && comb_ok[k]) {
+      rp = comb_mul(comb + (size_t)k * (COMB_ENTRIES * COMB_U4), (uint32_t)r, (uint32_t)(r >> 32));
+    } else {
+      const G1A pk = table[k];
+      if (!randomize_g1(pk, r, &rp)) rp = g1_mul_u64(pk, r);
+    }
+  }
+  for (unsigned d = 1; d < SCAN_W; d <<= 1) {
+    const G1J po = shfl_down_jac(rp, d);
+    const uint32_t ko = __shfl_down(key, d, 64);
+    if ((lane & (SCAN_W - 1)) + d < SCAN_W && ko == key) rp = jac_add(rp, po);
+  }
+  const uint32_t kprev = __shfl_up(key, 1, 64);
+  if (act && ((lane & (SCAN_W - 1)) == 0 || kprev != key)) Ph_out[i] = rp;
 }
 
 // Latency form of k_sm_prepare<true> for segments of few sets (a lone gossip call): TWO waves per 64
@@ -514,10 +566,17 @@ void launch_sm_prepare(LaunchCfg c, uint32_t base, uint32_t n, const uint32_t* i
   // throughput forms: decompression first as its own kernel at a higher occupancy (k_dec.hip),
   // unless GBV_DEC_SPLIT=0 (A/B)
   static const bool dec_split = getenv("GBV_DEC_SPLIT") ? atoi(getenv("GBV_DEC_SPLIT")) != 0 : GBV_DEC_SPLIT_DEFAULT != 0;
+  // and, for the G1-only form, the subgroup check apart from r pk (GBV_SUB_SPLIT=0: one kernel, A/B)
+  static const bool sub_split = getenv("GBV_SUB_SPLIT") ? atoi(getenv("GBV_SUB_SPLIT")) != 0 : GBV_SUB_SPLIT_DEFAULT != 0;
   const dim3 grid((n + 63) / 64);
   if (Sh && n <= split_max) {  // latency: two waves per 64 sets
     hipLaunchKernelGGL(k_sm_prepare_split, dim3((n + 63) / 64), dim3(128), 0, c.stream, base, n, idx, sig96, set_grp, table, table_ok, table_n,
                        comb, comb_ok, seed, nonce, S_out, Sh, Ph, status);
+  } else if (dec_split && !Sh && sub_split) {  // decode, subgroup check, r pk + scan
+    launch_sig_decode(c.stream, base, n, sig96, S_out, status);
+    hipLaunchKernelGGL(k_sm_subgroup, grid, dim3(64), 0, c.stream, base, n, idx, table_ok, table_n, S_out, status);
+    debug_sync(c.stream, "k_sm_subgroup");
+    hipLaunchKernelGGL(k_sm_rpk, grid, dim3(64), 0, c.stream, base, n, idx, set_grp, table, comb, comb_ok, seed, nonce, Ph, status);
   } else if (dec_split) {
     launch_sig_decode(c.stream, base, n, sig96, S_out, status);
     if (Sh)

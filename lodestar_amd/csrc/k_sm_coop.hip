@@ -253,68 +253,74 @@ k_sm_group_fe(uint32_t g0, const uint8_t* __restrict__ seg_ok, const Fp12* __res
   }
 }
 
-// hash_to_G2's cofactor clearing for few messages, one wave per message (latency: a lone gossip
-// call hashes one message).  clear_cofactor_g2 (RFC 9380 G.3) with its two [|x|] scalar
-// multiplications run by the Miller loop's cooperative point steps (coop::mul_xabs_point: each
-// doubling two rounds of independent products instead of 16 dependent ones); lane 0 does the
-// psi maps, the five additions and the affine conversions.  Qpre = Q0 + Q1 (k_hash_msgs_pre).
-// A base at infinity (never, for a hash) takes the thread-serial clear_cofactor_g2 on lane 0.
+// hash_to_G2's cofactor clearing for few messages (latency: a lone gossip call hashes one message),
+// TWO waves per message.  clear_cofactor_g2 (RFC 9380 G.3):
+//   h(P) = [x]([x]P + psi(P)) + psi^2(2P) - psi(P) - [x]P - P.
+// Wave 0 runs the two [|x|] scalar multiplications by the Miller loop's cooperative point steps
+// (coop::mul_xabs_point: each doubling two rounds of independent products instead of 16 dependent
+// ones) and, on its lane 0, the affine conversions they need; wave 1's lane 0 meanwhile forms the
+// rest -- psi(P) and u = psi^2(2P) - psi(P) - P during the first multiplication, u - [x]P during the
+// second -- so only two point additions and three inversions stay on the chain.  The coop wave
+// synchronises its phases at wavefront scope (coop::barrier) and meets wave 1 at the three
+// __syncthreads below, which every thread of the block reaches.  Qpre = Q0 + Q1 (k_hash_msgs_pre).
+// A base at infinity (never, for a hash) takes the thread-serial clear_cofactor_g2.
 __device__ inline G2A g2_aff_out(const G2J& q) {
   G2A out;
   jac_to_aff(out, q);
   return out;
 }
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
+__global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2)))
 k_hash_clear_coop(const G2J* __restrict__ Qpre, G2A* __restrict__ H) {
   __shared__ coop::Slot ws[coop::MILLER_WS];
   __shared__ Fp st[4];
-  __shared__ int ok;
+  __shared__ G2J sh_psi, sh_t1, sh_u;
+  __shared__ int ok_p, ok_t2;
   const uint32_t m = blockIdx.x;
-  const unsigned lane = threadIdx.x;
-  coop::load_consts();
-  G2J p, t1, t3;  // lane 0's
-  if (lane == 0) {
-    p = Qpre[m];
-    G2A a;
-    ok = jac_to_aff(a, p) ? 1 : 0;
-    if (!ok) H[m] = g2_aff_out(clear_cofactor_g2(p));
-    st[0] = a.x.c0;
-    st[1] = a.x.c1;
-    st[2] = a.y.c0;
-    st[3] = a.y.c1;
-  }
-  coop::barrier();
-  if (!ok) return;
-  coop::mul_xabs_point(ws, G2A{Fp2{st[0], st[1]}, Fp2{st[2], st[3]}});
-  if (lane == 0) {
-    t1 = jac_neg(coop::point_jac(ws));             // [x] P
-    G2J t2 = g2_psi_jac(p);                        // psi(P)
-    t3 = g2_psi_jac(g2_psi_jac(jac_dbl(p)));       // psi^2(2P)
-    t3 = g2_add(t3, jac_neg(t2));
-    t2 = g2_add(t1, t2);
-    G2A a;
-    ok = jac_to_aff(a, t2) ? 1 : 0;
-    if (!ok) {  // t2 at infinity: [x] t2 is infinity too
-      t3 = g2_add(t3, jac_neg(t1));
-      H[m] = g2_aff_out(g2_add(t3, jac_neg(p)));
+  const unsigned lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  const G2J p = Qpre[m];
+  if (wv == 0) {
+    coop::load_consts();
+    if (lane == 0) {
+      G2A a;
+      ok_p = jac_to_aff(a, p) ? 1 : 0;
+      st[0] = a.x.c0;
+      st[1] = a.x.c1;
+      st[2] = a.y.c0;
+      st[3] = a.y.c1;
+      if (!ok_p) H[m] = g2_aff_out(clear_cofactor_g2(p));
     }
-    st[0] = a.x.c0;
-    st[1] = a.x.c1;
-    st[2] = a.y.c0;
-    st[3] = a.y.c1;
+    coop::barrier();
+    if (ok_p) coop::mul_xabs_point(ws, G2A{Fp2{st[0], st[1]}, Fp2{st[2], st[3]}});
+  } else if (lane == 0) {
+    const G2J psi = g2_psi_jac(p);
+    sh_psi = psi;
+    sh_u = g2_add(g2_add(g2_psi_jac(g2_psi_jac(jac_dbl(p))), jac_neg(psi)), jac_neg(p));
   }
-  coop::barrier();
-  if (!ok) return;
-  coop::mul_xabs_point(ws, G2A{Fp2{st[0], st[1]}, Fp2{st[2], st[3]}});
-  if (lane == 0) {
-    const G2J t2 = jac_neg(coop::point_jac(ws));  // [x] t2
-    t3 = g2_add(t3, t2);
-    t3 = g2_add(t3, jac_neg(t1));
-    H[m] = g2_aff_out(g2_add(t3, jac_neg(p)));
+  __syncthreads();  // S1: [|x|] P in ws, psi(P) and u in LDS
+  if (wv == 0 && lane == 0 && ok_p) sh_t1 = jac_neg(coop::point_jac(ws));  // [x] P
+  __syncthreads();  // S2: t1 in LDS (wave 0 may now reuse ws)
+  if (wv == 0) {
+    if (lane == 0 && ok_p) {
+      G2A a;
+      ok_t2 = jac_to_aff(a, g2_add(sh_t1, sh_psi)) ? 1 : 0;  // t2 = [x] P + psi(P)
+      st[0] = a.x.c0;
+      st[1] = a.x.c1;
+      st[2] = a.y.c0;
+      st[3] = a.y.c1;
+    }
+    coop::barrier();
+    if (ok_p && ok_t2) coop::mul_xabs_point(ws, G2A{Fp2{st[0], st[1]}, Fp2{st[2], st[3]}});
+  } else if (lane == 0 && ok_p) {
+    sh_u = g2_add(sh_u, jac_neg(sh_t1));  // u - [x] P
+  }
+  __syncthreads();  // S3: [|x|] t2 in ws, u - [x] P in LDS
+  if (wv == 0 && lane == 0 && ok_p) {
+    // t2 at infinity: [x] t2 is infinity too
+    H[m] = g2_aff_out(ok_t2 ? g2_add(jac_neg(coop::point_jac(ws)), sh_u) : sh_u);
   }
 }
 void launch_hash_clear_coop(hipStream_t s, uint32_t n, const G2J* Qpre, G2A* H) {
-  hipLaunchKernelGGL(k_hash_clear_coop, dim3(n), dim3(64), 0, s, Qpre, H);
+  hipLaunchKernelGGL(k_hash_clear_coop, dim3(n), dim3(128), 0, s, Qpre, H);
   debug_sync(s, "k_hash_clear_coop");
 }
 

@@ -7,7 +7,7 @@ TAG=${1:-r01}
 OUT=gpurun_out/pmc_$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-BENCH="bench.py --steps 1 --warmup 0 --sets 262144 --no-cpu-baseline --no-stream"
+BENCH="bench.py --steps 1 --warmup 0 --sets 262144 --no-cpu-baseline --no-stream --no-api"
 run_pass() {
   local name=$1; shift
   timeout -s KILL 400 rocprofv3 --pmc "$@" --output-format csv -d "$OUT/$name" -o run -- python3 -u $BENCH \
