@@ -418,10 +418,12 @@ GBV_HD void miller_load_pair(Slot* mem, int j, const G1A& P, const G2A& Q) {
 GBV_HD void miller_loop(Slot* mem, int npairs) {
   set_one12(mem + M_F);
   for (int i = 62; i >= 0; --i) {
-    if (i != 62) run(FP12_SQR, ws2(mem, M_Z, M_F, M_F));
     for (int j = 0; j < npairs; ++j) {
       uint16_t t = M_PAIR + 12 * j;
-      run(G2_DBL_STEP, make_ws(mem, M_Z, t, (uint16_t)(t + 10), t, M_L));
+      if (j == 0 && i != 62)  // f^2 and pair 0's doubling step are independent: one program
+        run(MILLER_SQR_DBL, make_ws(mem, M_Z, M_F, t, (uint16_t)(t + 10), M_F, t, M_L));
+      else
+        run(G2_DBL_STEP, make_ws(mem, M_Z, t, (uint16_t)(t + 10), t, M_L));
       run(FP12_MUL_LINE, ws3(mem, M_Z, M_F, M_L, M_F));
     }
     if ((X_ABS >> i) & 1ull) {
@@ -444,7 +446,7 @@ GBV_HD void mul_xabs_point(Slot* mem, const G2A& Q) {
   miller_load_pair(mem, 0, G1A{fp_zero(), fp_zero()}, Q);
   const uint16_t t = M_PAIR;
   for (int i = 62; i >= 0; --i) {
-    run(G2_DBL_STEP, make_ws(mem, M_Z, t, (uint16_t)(t + 10), t, M_L));
+    run(G2_DBL_PT, make_ws(mem, M_Z, t, t));  // the doubling without its line: 19 products, 6 outputs
     if ((X_ABS >> i) & 1ull) run(G2_ADD_STEP, make_ws(mem, M_Z, t, (uint16_t)(t + 6), (uint16_t)(t + 10), t, M_L));
   }
 }

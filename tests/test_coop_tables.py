@@ -130,6 +130,13 @@ def test_dbl_and_add_steps():
     ops = run("G2_DBL_STEP", T, Pp, None, None)
     assert proj_to_aff(ops[2]) == O.g2_add(Q, Q)
     T2 = ops[2]
+    # the line-free doubling (cofactor clearing's [|x|] chains) gives the same projective point
+    assert run("G2_DBL_PT", T, None)[1] == T2
+    # the fused Miller-bit program: the Fp12 square and the same doubling step and line
+    f = flat12(O.f12_mul(O.F12_ONE, unflat12([(7 * k + 3) % P for k in range(12)])))
+    fused = run("MILLER_SQR_DBL", f, T, Pp, None, None, None)
+    assert fused[3] == flat12(O.f12_mul(unflat12(f), unflat12(f)))
+    assert fused[4] == T2 and fused[5] == run("G2_DBL_STEP", T, Pp, None, None)[3]
     ops = run("G2_ADD_STEP", T2, [Q[0][0], Q[0][1], Q[1][0], Q[1][1]], Pp, None, None)
     assert proj_to_aff(ops[3]) == O.g2_mul(Q, 3)
 
@@ -145,15 +152,17 @@ def miller_loop(pairs):
     bits = bin(O.X_ABS)[3:]
     first = True
     for bit in bits:
-        if not first:
-            F = run("FP12_SQR", F, None)[1]
-        first = False
         nst = []
-        for T, Q, Pp in st:
-            ops = run("G2_DBL_STEP", T, Pp, None, None)
-            T, L = ops[2], ops[3]
+        for j, (T, Q, Pp) in enumerate(st):
+            if j == 0 and not first:  # the square of f fused with pair 0's doubling step
+                ops = run("MILLER_SQR_DBL", F, T, Pp, None, None, None)
+                F, T, L = ops[3], ops[4], ops[5]
+            else:
+                ops = run("G2_DBL_STEP", T, Pp, None, None)
+                T, L = ops[2], ops[3]
             F = run("FP12_MUL_LINE", F, L, None)[2]
             nst.append([T, Q, Pp])
+        first = False
         st = nst
         if bit == "1":
             for s in st:

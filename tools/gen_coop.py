@@ -293,11 +293,11 @@ def prog_frob(n):
     return b
 
 
-def prog_dbl_step():
-    # T (6: x, y, z in Fp2), P (2: -xP, yP)  ->  T' = 4 * [2]T (homogeneous), line (6: c0, c2, c3)
-    b = Builder("G2_DBL_STEP", [("t", 6, "in"), ("p", 2, "in"), ("t_out", 6, "out"), ("l", 6, "out")])
-    X, Y, Z = fp2_in(0, 0), fp2_in(0, 1), fp2_in(0, 2)
-    nxp, yp = inp(1, 0), inp(1, 1)
+def dbl_step_into(b, t_op, p_op, t_out, l_out):
+    """The doubling step T -> 4 [2]T (homogeneous) with its line through P = (-xP, yP), emitted into
+    builder b with the given operand indices."""
+    X, Y, Z = fp2_in(t_op, 0), fp2_in(t_op, 1), fp2_in(t_op, 2)
+    nxp, yp = inp(p_op, 0), inp(p_op, 1)
     A = b.f2mul(X, Y)           # XY (the 1/2 of the unscaled formula is folded into the x4 scaling)
     B = b.f2sqr(Y)
     C = b.f2sqr(Z)
@@ -312,8 +312,45 @@ def prog_dbl_step():
     l0 = f2sub(B, E)
     l2 = b.f2mulfp(f2scale(X2, 3), nxp)
     l3 = b.f2mulfp(H, yp)
-    b.out_vec(2, [X3[0], X3[1], Y3[0], Y3[1], Z3[0], Z3[1]])
-    b.out_vec(3, [l0[0], l0[1], l2[0], l2[1], l3[0], l3[1]])
+    b.out_vec(t_out, [X3[0], X3[1], Y3[0], Y3[1], Z3[0], Z3[1]])
+    b.out_vec(l_out, [l0[0], l0[1], l2[0], l2[1], l3[0], l3[1]])
+
+
+def prog_dbl_step():
+    # T (6: x, y, z in Fp2), P (2: -xP, yP)  ->  T' = 4 * [2]T (homogeneous), line (6: c0, c2, c3)
+    b = Builder("G2_DBL_STEP", [("t", 6, "in"), ("p", 2, "in"), ("t_out", 6, "out"), ("l", 6, "out")])
+    dbl_step_into(b, 0, 1, 2, 3)
+    return b
+
+
+def prog_sqr_dbl():
+    # One Miller-loop bit's independent halves in ONE program: f^2 (the 36 products of the Fp12
+    # square) and the doubling step of T with its line (11 + 14 products), so the square's products
+    # and the doubling's first round share a round (47 lanes) -- one program, its phases and barriers,
+    # per bit fewer.  f (12), T (6), P (2) -> f^2 (12), T' (6), line (6); f^2 may overwrite f.
+    b = Builder("MILLER_SQR_DBL", [("f", 12, "in"), ("t", 6, "in"), ("p", 2, "in"), ("f_out", 12, "out"),
+                                   ("t_out", 6, "out"), ("l", 6, "out")])
+    b.out_vec(3, fp12_flat(b.f12sqr(fp12_in(0))))
+    dbl_step_into(b, 1, 2, 4, 5)
+    return b
+
+
+def prog_dbl_pt():
+    # T (6) -> T' = 4 * [2]T (homogeneous): the doubling step without its line (cofactor clearing and
+    # other plain [|x|] multiplications): 19 products in two rounds, 6 outputs
+    b = Builder("G2_DBL_PT", [("t", 6, "in"), ("t_out", 6, "out")])
+    X, Y, Z = fp2_in(0, 0), fp2_in(0, 1), fp2_in(0, 2)
+    A = b.f2mul(X, Y)
+    B = b.f2sqr(Y)
+    C = b.f2sqr(Z)
+    YZ2 = b.f2sqr(f2add(Y, Z))
+    E = f2scale(f2xi(C), 12)
+    F = f2scale(E, 3)
+    H = f2sub(YZ2, f2add(B, C))
+    X3 = f2scale(b.f2mul(A, f2sub(B, F)), 2)
+    Y3 = f2sub(b.f2sqr(f2add(B, F)), f2scale(b.f2sqr(E), 12))
+    Z3 = f2scale(b.f2mul(B, H), 4)
+    b.out_vec(1, [X3[0], X3[1], Y3[0], Y3[1], Z3[0], Z3[1]])
     return b
 
 
@@ -343,7 +380,7 @@ def prog_add_step():
 
 
 PROGRAMS = [prog_fp12_mul, prog_fp12_sqr, prog_cyc_sqr, prog_mul_line, lambda: prog_frob(1), lambda: prog_frob(2),
-            prog_dbl_step, prog_add_step]
+            prog_dbl_step, prog_add_step, prog_dbl_pt, prog_sqr_dbl]
 
 
 # ---- scheduling and encoding -------------------------------------------------------------------
