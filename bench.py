@@ -498,6 +498,22 @@ def make_blocks(v, sk_ints, n_blocks, rng, electra=False):
     return calls
 
 
+def _pmc_gather(kernel, members):
+    """HBM read rate of the pubkey gather kernel from the committed PMC summary (FETCH_SIZE doubled per
+    the gfx950 calibration, over that launch's own duration) -- measured, not by formula -- and the
+    bytes fetched per gathered member (the PMC run uses the same default C4 / C4e pass)."""
+    try:
+        d = json.load(open(PMC_SUMMARY)).get(kernel)
+    except (OSError, ValueError):
+        return None
+    if not d or "FETCH_SIZE" not in d:
+        return None
+    fetched = 2 * d["FETCH_SIZE"] * 1024.0
+    return {"source": os.path.relpath(PMC_SUMMARY, ROOT), "kernel": kernel, "hbm_read_GBps": round(fetched / (d["duration_ms"] * 1e-3) / 1e9, 1),
+            "fetched_bytes_per_member": round(fetched / max(members, 1), 1), "launch_ms_at_pmc": round(d["duration_ms"], 3),
+            "hbm_peak_GBps": 8000.0}
+
+
 def c4_bench(v, sk_ints, pk_rows, cpu, n_blocks=64, electra=False):
     rng = np.random.Generator(np.random.PCG64(0xC4E if electra else 0xC4))
     t0 = time.time()
@@ -527,6 +543,9 @@ def c4_bench(v, sk_ints, pk_rows, cpu, n_blocks=64, electra=False):
            "config": "range-sync segment of %d blocks (%d sets, %d pubkeys gathered), 2 passes in flight (built in %.1fs)" % (
                n_blocks, n_sets, members, build_s),
            "roofline": _vs_roofline(v, n_sets, ms, agg_members=members)}
+    g = _pmc_gather("k_vs_agg_big", members) if electra else None  # (k_vs_agg's largest PMC launch is C3's)
+    if g:
+        out["roofline"]["agg_gather_pmc"] = g
     if cpu:
         from oracle import cpu_baseline
         k = 1 if electra else 4
