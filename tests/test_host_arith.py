@@ -81,13 +81,31 @@ def test_fp_lazy_product_inputs(lib):
 
 
 def test_fp_inv_edges(lib):
-    """Binary-GCD inversion (fp.h fp_inv) at edge values; 0 maps to 0 like the exponentiation."""
+    """Inversion (fp.h fp_inv: safegcd divsteps, inv_sg.h) at edge values; 0 maps to 0 like the
+    exponentiation."""
     out = buf(48)
     for a in (1, 2, 3, o.P - 1, o.P - 2, (o.P - 1) // 2, 1 << 380, (1 << 381) % o.P, 0x1234567):
         lib.ht_fp_inv(out, be(a))
         assert int.from_bytes(out.raw, "big") * a % o.P == 1, hex(a)
     lib.ht_fp_inv(out, be(0))
     assert out.raw == bytes(48)
+
+
+def test_fp_inv_safegcd_bulk(lib):
+    """safegcd's variable-time batches on many shapes of input: uniform values, small values, powers
+    of two and their neighbours (long runs of zero bits: the divsteps skip them in one shift), values
+    just below p, and inputs whose Montgomery form is small."""
+    rng = random.Random(11)
+    vals = [rng.randrange(1, o.P) for _ in range(600)]
+    vals += list(range(1, 40)) + [1 << k for k in range(0, 381, 7)] + [(1 << k) - 1 for k in range(2, 381, 11)]
+    vals += [o.P - k for k in range(1, 40)] + [(o.P >> k) | 1 for k in range(1, 380, 13)]
+    out = buf(48)
+    for a in vals:
+        a %= o.P
+        if a == 0:
+            continue
+        lib.ht_fp_inv(out, be(a))
+        assert int.from_bytes(out.raw, "big") * a % o.P == 1, hex(a)
 
 
 def test_fp2_mul_sqrt(lib):
