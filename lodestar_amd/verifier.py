@@ -123,7 +123,7 @@ class _Job:
     sets: list  # default: ISignatureSet list; same_message: (u32 index array, 96-byte signature blob)
     message: bytes = b""
     packed: bool = False  # same_message: resolve with a numpy bool array
-    added: float = field(default_factory=time.monotonic)
+    added: float = field(default_factory=time.monotonic)  # the gossip fast path passes it explicitly
 
     def n_sets(self):
         return len(self.sets) if self.kind == "default" else len(self.sets[0])
@@ -547,10 +547,20 @@ class GpuBlsVerifier:
             fut = loop.create_future()
             fut.set_exception(e)
             return fut
-        opts = opts or _DEFAULT_OPTS
         n = len(idx)
         m = self.pool_metrics
         m.add("total_sig_sets", n)
+        if opts is None and n < 2 * MAX_SIGNATURE_SETS_PER_JOB:
+            # the gossip call (default opts, one chunk): straight onto the queue, what _queue does
+            # for a non-batchable, non-priority job
+            fut = loop.create_future()
+            self._jobs.append(_Job("same_message", _DEFAULT_OPTS, fut, (idx, sigs), message if type(message) is bytes else bytes(message),
+                                   packed, time.monotonic()))
+            if not self._run_scheduled:
+                self._run_scheduled = True
+                loop.call_soon(self._run_jobs)
+            return fut
+        opts = opts or _DEFAULT_OPTS
         if opts.priority:
             m.add("prioritized_sig_sets", n)
         if opts.batchable:
