@@ -168,7 +168,7 @@ __device__ inline void ws_put(const Ws& w, uint32_t src, uint32_t idx, const Fp&
 // Signed sum of a record's terms: the nu unit terms (+1, or -1 with the neg bit of the term word)
 // of r[0 .. N) -- each one slot load of the value or its stored negation -- then the nsc scaled terms
 // (|c| > 1: doubling / cyclotomic coefficients) that follow them, read from the record in memory (rg)
-// by a rolled double-and-add loop.  No calls: the interpreter keeps its registers across the whole
+// and multiplied in by fp_mul_small.  No calls: the interpreter keeps its registers across the whole
 // program.
 //
 // The unit-term loop runs `umax` times on every lane -- the phase's largest unit count, from the
@@ -202,19 +202,21 @@ GBV_HD Fp lin_eval(const Ws& w, const uint32_t* r, uint32_t umax, uint32_t nu, u
 #pragma unroll
     for (int q = 0; q < G; ++q) {
       const int i = g + q;
-      if (i < N && (uint32_t)i < umax) acc = i == 0 ? v[q] : GBV_COOP_LAZY ? fp_add_lazy(acc, v[q]) : fp_add(acc, v[q]);
-      if (GBV_COOP_LAZY && i == 7 && N > 8 && umax > 8) acc = fp_reduce8(acc);
+      if (i < N && (uint32_t)i < umax) {
+        if (i == 0)
+          acc = v[q];
+        else if (GBV_COOP_LAZY)
+          fp_acc_lazy(acc, v[q]);
+        else
+          acc = fp_add(acc, v[q]);
+      }
+      if (GBV_COOP_LAZY && i == 7 && N > 8 && umax > 8) fp_reduce8_ip(acc);
     }
   }
-  if (GBV_COOP_LAZY && umax > 1 && (CANON || nsc)) acc = fp_reduce8(acc);
+  if (GBV_COOP_LAZY && umax > 1 && (CANON || nsc)) fp_reduce8_ip(acc);
   for (uint32_t j = 0; j < nsc; ++j) {
     const uint32_t t = rg[nu + j], m = t >> 16;
-    const Fp vs = term_load(w, t, (t >> 4) & 1);
-    Fp s = vs;
-    for (int bit = 30 - __builtin_clz(m); bit >= 0; --bit) {  // m >= 2: below the top bit
-      s = fp_dbl(s);
-      if ((m >> bit) & 1) s = fp_add(s, vs);
-    }
+    const Fp s = fp_mul_small(term_load(w, t, (t >> 4) & 1), m);
     acc = (nu == 0 && j == 0) ? s : fp_add(acc, s);
   }
   return acc;

@@ -124,6 +124,35 @@ GBV_HD Fp fp_neg(const Fp& a) {
 
 GBV_HD Fp fp_dbl(const Fp& a) { return fp_add(a, a); }
 
+// m x mod p for canonical x and 2 <= m < 2^16 (the scaled terms of the cooperative programs: 3b
+// multiples up to 144): r = m x as 13 limbs (one multiply-add chain), q = floor(r_top / (p_11 + 1))
+// from r's top 45 bits in double precision -- exact for these magnitudes and at most one below
+// floor(r / p) -- then r - q p < 2p and one conditional subtraction.  ~60 VALU ops against ~300 for
+// a double-and-add chain of modular doublings.
+GBV_HD Fp fp_mul_small(const Fp& x, uint32_t m) {
+  uint32_t r[13];
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    c += (uint64_t)x.v[i] * m;
+    r[i] = (uint32_t)c;
+    c >>= 32;
+  }
+  r[12] = (uint32_t)c;
+  const double top = (double)r[12] * 4294967296.0 + (double)r[11];
+  const uint32_t q = (uint32_t)(top * (1.0 / 436277739.0));  // p_11 + 1 = 0x1a0111eb
+  Fp d;
+  uint64_t s = 0;
+  uint32_t br = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    s += (uint64_t)P_RAW.v[i] * q;
+    d.v[i] = __builtin_subc(r[i], (uint32_t)s, br, &br);
+    s >>= 32;
+  }
+  return fp_reduce_once(d);
+}
+
 // Lazy forms for values that only feed a product: the product takes any input below 2^384 (fp_to28)
 // and its Montgomery output stays below 1.02 p for inputs below 7 p (7p x 7p / 2^392 < 0.02 p), so
 // the conditional subtraction of a modular add/sub is skipped.  fp_sub_lazy4: a + 4p - b for b < 4p.
@@ -152,6 +181,15 @@ GBV_HD Fp fp_sub_lazy4(const Fp& a, const Fp& b) {
   GBV_ASM_SUB_RAW_K(t, d, a, b, k);
   return d;
 }
+// In-place forms for accumulators (the asm output is the input's registers: no copies at joins)
+GBV_HD void fp_acc_lazy(Fp& acc, const Fp& b) { GBV_ASM_ACC_RAW(acc, b); }
+GBV_HD void fp_reduce8_ip(Fp& x) {
+  Fp t;
+  const Fp k4 = P4_RAW, k2 = P2_RAW, k1 = P_RAW;
+  GBV_ASM_REDUCE_IP(x, t, k4);
+  GBV_ASM_REDUCE_IP(x, t, k2);
+  GBV_ASM_REDUCE_IP(x, t, k1);
+}
 #else
 GBV_HD Fp fp_add_lazy(const Fp& a, const Fp& b) {
   Fp s;
@@ -171,6 +209,8 @@ GBV_HD Fp fp_sub_lazy4(const Fp& a, const Fp& b) {
   raw_sub(d, t, b);
   return d;
 }
+GBV_HD void fp_acc_lazy(Fp& acc, const Fp& b) { raw_add(acc, acc, b); }
+GBV_HD void fp_reduce8_ip(Fp& x) { x = fp_reduce8(x); }
 #endif
 
 // ---- the product: 14 x 28-bit limbs, Montgomery radix R = 2^392 ---------------------------------

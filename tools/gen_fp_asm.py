@@ -81,11 +81,31 @@ def sub_raw_k():
                  "d = a + k - b, no reduction (b <= k, a + k < 2^384; t is scratch).  24 VALU ops.")
 
 
+def acc_raw():
+    s = regs(0)
+    b = regs(12)
+    body = ["v_add_co_u32 %s, vcc, %s, %s" % (s[0], s[0], b[0])]
+    body += ["v_addc_co_u32 %s, vcc, %s, %s, vcc" % (s[i], s[i], b[i]) for i in range(1, N)]
+    return block("GBV_ASM_ACC_RAW", body, [("s", "+v")], [("b", "v")],
+                 "s += b in place, no reduction (the accumulator of a lazy sum: no copy out of the asm's\n"
+                 "// registers at every term).  12 VALU ops.")
+
+
+def reduce_ip():
+    x, t = regs(0), regs(12)
+    p = regs(24)
+    body = ["v_sub_co_u32 %s, vcc, %s, %s" % (t[0], x[0], p[0])]
+    body += ["v_subb_co_u32 %s, vcc, %s, %s, vcc" % (t[i], x[i], p[i]) for i in range(1, N)]
+    body += ["v_cndmask_b32 %s, %s, %s, vcc" % (x[i], t[i], x[i]) for i in range(N)]
+    return block("GBV_ASM_REDUCE_IP", body, [("x", "+v"), ("t", "=&v")], [("p", "v")],
+                 "x = x < p ? x : x - p in place for x < 2p (t is scratch).  24 VALU ops.")
+
+
 def main():
     out = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "lodestar_amd", "csrc", "fp_asm.h")
     src = ["// GENERATED by tools/gen_fp_asm.py -- do not edit.",
            "// 384-bit modular add/sub carry chains as single gfx950 inline-asm blocks (device only).",
-           "#pragma once", "", add_reduce(), sub_mod(), reduce_once(), add_raw(), sub_raw_k()]
+           "#pragma once", "", add_reduce(), sub_mod(), reduce_once(), add_raw(), sub_raw_k(), acc_raw(), reduce_ip()]
     open(out, "w").write("\n".join(src))
     print("wrote", os.path.normpath(out))
 
