@@ -611,6 +611,23 @@ def api_stream_rate(v, call_off, idx, sigs, msgs, n_sets=1 << 20):
     return round(n / dt, 1), n, v.device_passes - p0
 
 
+_JSON_OUT = None
+
+
+def claim_stdout():
+    """The bench line must be alone on stdout, but native libraries print there too (RCCL's version
+    banner at process-group init): fd 1 is pointed at stderr for the rest of the process and the
+    line goes out through a private copy of the original stdout."""
+    global _JSON_OUT
+    sys.stdout.flush()
+    _JSON_OUT = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
+
+
+def emit_json(line):
+    print(json.dumps(line), file=_JSON_OUT or sys.stdout, flush=True)
+
+
 def free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
@@ -649,6 +666,7 @@ def main():
                "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.abspath(__file__)] + sys.argv[1:]
         sys.exit(subprocess.call(cmd))
 
+    claim_stdout()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -886,7 +904,7 @@ def main():
         "vs_shard": vs_shard,
     }
     if rank == 0:
-        print(json.dumps(line), flush=True)
+        emit_json(line)
     for st in stages:
         st.close()
     if dist is not None:
@@ -897,7 +915,7 @@ def main():
 def vs_shard_main(args, v, sk_ints, world, rank, local_rank, dist, log):
     line = vs_shard_measure(args, v, sk_ints, world, rank, log)
     if rank == 0:
-        print(json.dumps(line), flush=True)
+        emit_json(line)
     import torch.distributed as tdist
     tdist.barrier()
     tdist.destroy_process_group()
