@@ -281,7 +281,7 @@ inline void run(const Prog& P, const Ws& w) {
 #define COOP_LANES(l) for (unsigned l = 0; l < (unsigned)LANES; ++l)
 #define COOP_LANE0 if (true)
 #else
-__device__ inline unsigned lane_id() { return threadIdx.x; }
+__device__ inline unsigned lane_id() { return threadIdx.x & 63u; }  // a job is one wave; a block may hold several
 // A coop job is ONE wave: its phases synchronise at wavefront scope -- the workgroup-scope fences
 // of __syncthreads (prior LDS writes complete and visible, later reads not hoisted) around a wave
 // barrier instead of s_barrier.  For the one-wave workgroups this is what __syncthreads compiles to
@@ -303,7 +303,7 @@ __device__ inline void load_consts() {
 __device__ __noinline__ void run_ni(const Prog* PP, uint32_t b0, uint32_t b1, uint32_t b2, uint32_t b3) {
   const Prog& P = *PP;
   const Ws w{{b0, b1, b2, b3}};
-  const int lane = (int)threadIdx.x;
+  const int lane = (int)(threadIdx.x & 63u);
   uint32_t rec[PROD_WORDS], rpart[SUM_WORDS], rout[SUM_WORDS];
   const bool have_part = lane < P.n_part, have_out = lane < P.n_out;
   const uint32_t* gpart = P.parts + SUM_WORDS * lane;
@@ -333,8 +333,8 @@ __device__ __noinline__ void run_ni(const Prog* PP, uint32_t b0, uint32_t b1, ui
 }
 // One out-of-line copy of the interpreter serves every call site (the drivers make hundreds).
 __device__ inline void run(const Prog& P, const Ws& w) { run_ni(&P, w.b[0], w.b[1], w.b[2], w.b[3]); }
-#define COOP_LANES(l) for (unsigned l = threadIdx.x; l == threadIdx.x; l = ~0u)
-#define COOP_LANE0 if (threadIdx.x == 0)
+#define COOP_LANES(l) for (unsigned l = threadIdx.x & 63u; l == (threadIdx.x & 63u); l = ~0u)
+#define COOP_LANE0 if ((threadIdx.x & 63u) == 0)
 #endif
 
 // ---- operand helpers (lane-parallel, end with a barrier) ------------------------------------

@@ -114,7 +114,10 @@ __global__ void GBV_KERNEL_ATTR k_sm_prepare(uint32_t base, uint32_t n, const ui
 // over Fp2, two waves per SIMD) only writes the status byte; r_i pk_i from the comb table and the
 // 8-lane chunk scan (G1 points: a small live state) run after it at a higher occupancy.  Same r_i,
 // statuses, scan and outputs as k_sm_prepare<false, true>.
-__global__ void GBV_KERNEL_ATTR k_sm_subgroup(uint32_t base, uint32_t n, const uint32_t* __restrict__ idx, const uint8_t* __restrict__ table_ok,
+#ifndef GBV_SUB_WAVES
+#define GBV_SUB_WAVES GBV_WAVES_PER_EU
+#endif
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GBV_SUB_WAVES))) k_sm_subgroup(uint32_t base, uint32_t n, const uint32_t* __restrict__ idx, const uint8_t* __restrict__ table_ok,
                                               uint32_t table_n, const G2A* __restrict__ S, uint8_t* __restrict__ status) {
   const uint32_t t = blockIdx.x * 64 + threadIdx.x;
   if (t >= n) return;
