@@ -94,6 +94,7 @@ class Builder:
         self.prods = []  # (Lin, Lin)
         self.outs = []   # (dst operand, coord, Lin)
         self.xparts = []  # explicit partial sums (Lin over products / inputs / constants)
+        self.out_max = OUT_MAX  # outputs longer than this are split into partial sums
 
     def part(self, lin):
         """An explicit partial sum: one lane of the partial-sum phase computes it into Z, so an
@@ -191,6 +192,42 @@ class Builder:
         n5 = f2add(f2scale(t3, 3), f2scale(z5, 2))
         return ((n0, n4, n3), (n2, n1, n5))
 
+    def f12cyc_sqr3(self, a):
+        """The same squaring with no partial-sum phase: the 3 of every 3 t +- 2 z is carried by one
+        operand of each base product (unit copies: the round has lanes to spare), so each output is
+        a signed sum of <= 9 product terms and two copies of z -- one output phase of <= 11 terms."""
+        z0, z4, z3 = a[0]
+        z2, z1, z5 = a[1]
+
+        def weight(lin):
+            return sum(abs(c) for c in lin.d.values())
+
+        def mul3(p, q):
+            return self.mul(p.scale(3), q) if weight(p) <= weight(q) else self.mul(p, q.scale(3))
+
+        def f2mul3(x, y):  # 3 x y
+            t0 = mul3(x[0], y[0])
+            t1 = mul3(x[1], y[1])
+            t2 = mul3(x[0] + x[1], y[0] + y[1])
+            return (t0 - t1, t2 - t0 - t1)
+
+        def fp4_sqr3(x, y):  # 3 (t0, t1) of fp4_sqr
+            tmp = f2mul3(x, y)
+            t0 = f2sub(f2sub(f2mul3(f2add(x, y), f2add(f2xi(y), x)), tmp), f2xi(tmp))
+            return t0, f2add(tmp, tmp)
+
+        t0, t1 = fp4_sqr3(z0, z1)
+        t2, t3 = fp4_sqr3(z2, z3)
+        t4, t5 = fp4_sqr3(z4, z5)
+        t5x = f2xi(t5)
+        n0 = f2sub(t0, f2scale(z0, 2))
+        n1 = f2add(t1, f2scale(z1, 2))
+        n2 = f2add(t5x, f2scale(z2, 2))
+        n3 = f2sub(t4, f2scale(z3, 2))
+        n4 = f2sub(t2, f2scale(z4, 2))
+        n5 = f2add(t3, f2scale(z5, 2))
+        return ((n0, n4, n3), (n2, n1, n5))
+
     def out_vec(self, op, lins):
         for i, l in enumerate(lins):
             self.outs.append((op, i, l))
@@ -263,9 +300,16 @@ def prog_fp12_sqr():
     return b
 
 
+CYC_DIRECT = int(os.environ.get("GBV_GEN_CYC_DIRECT", "0"))  # 1: no partial-sum phase (measured: no faster)
+
+
 def prog_cyc_sqr():
     b = Builder("FP12_CYC_SQR", [("a", 12, "in"), ("c", 12, "out")])
-    b.out_vec(1, fp12_flat(b.f12cyc_sqr(fp12_in(0))))
+    if CYC_DIRECT:
+        b.out_max = SUM_TERMS
+        b.out_vec(1, fp12_flat(b.f12cyc_sqr3(fp12_in(0))))
+    else:
+        b.out_vec(1, fp12_flat(b.f12cyc_sqr(fp12_in(0))))
     return b
 
 
@@ -460,10 +504,10 @@ def encode(b):
         nz += 1
     outs = []
     for op, i, lin in b.outs:
-        tl = expand(lin, OUT_MAX)
-        if len(tl) > OUT_MAX:  # split: expand freely inside the pieces
+        tl = expand(lin, b.out_max)
+        if len(tl) > b.out_max:  # split: expand freely inside the pieces
             tl = expand(lin, 4 * SUM_TERMS * SUM_TERMS)
-        if len(tl) > OUT_MAX:
+        if len(tl) > b.out_max:
             refs = []
             for j in range(0, len(tl), PART_TERMS):
                 t0, tn = put(tl[j:j + PART_TERMS])
