@@ -95,6 +95,7 @@ struct gbv_ctx {
   // latency-bound work) and the hash stream 4 at the highest.  Three streams = three hardware
   // queues (GPU_MAX_HW_QUEUES=4 leaves one for the runtime): no two streams share a queue.
   hipStream_t stream = nullptr, stream2 = nullptr, stream4 = nullptr;
+  hipStream_t stream5 = nullptr;  // small verifySignatureSets passes: the signature half beside the aggregation
   gbv::G1A* table = nullptr;
   uint8_t* table_ok = nullptr;
   size_t table_cap = 0;

@@ -38,7 +38,7 @@ int gbv_fail(gbv_ctx* c, int code, const std::string& msg) {
 }
 
 void ctx_drain(gbv_ctx* c) {
-  for (hipStream_t s : {c->stream, c->stream2, c->stream4})
+  for (hipStream_t s : {c->stream, c->stream2, c->stream4, c->stream5})
     if (s) (void)hipStreamSynchronize(s);
   (void)hipGetLastError();
 }
@@ -227,9 +227,10 @@ int gbv_init(int device, gbv_ctx** out) {
   bool ok = hipSetDevice(device) == hipSuccess && hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) == hipSuccess &&
             hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, prio_lo) == hipSuccess &&
             hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, prio_hi) == hipSuccess &&
-            hipStreamCreateWithPriority(&c->stream4, hipStreamNonBlocking, prio_hi) == hipSuccess;
+            hipStreamCreateWithPriority(&c->stream4, hipStreamNonBlocking, prio_hi) == hipSuccess &&
+            hipStreamCreateWithPriority(&c->stream5, hipStreamNonBlocking, prio_hi) == hipSuccess;
   if (!ok) {
-    for (hipStream_t s : {c->stream, c->stream2, c->stream4})
+    for (hipStream_t s : {c->stream, c->stream2, c->stream4, c->stream5})
       if (s) hipStreamDestroy(s);
     delete c;
     return GBV_E_DEVICE;
@@ -248,7 +249,7 @@ void gbv_destroy(gbv_ctx* c) {
   hipSetDevice(c->device);
   c->closed = true;
   // every stream drains before anything it may still read or write is freed
-  for (hipStream_t s : {c->stream, c->stream2, c->stream4})
+  for (hipStream_t s : {c->stream, c->stream2, c->stream4, c->stream5})
     if (s) hipStreamSynchronize(s);
   sm_destroy(c->sm_scratch);
   vs_batch_free(c->vs_scratch);
@@ -261,7 +262,7 @@ void gbv_destroy(gbv_ctx* c) {
   for (auto* p : c->ssz_buf) hipFree(p);
   for (auto e : c->ssz_ev)
     if (e) hipEventDestroy(e);
-  for (hipStream_t s : {c->stream, c->stream2, c->stream4})
+  for (hipStream_t s : {c->stream, c->stream2, c->stream4, c->stream5})
     if (s) hipStreamDestroy(s);
   delete c;
 }

@@ -64,6 +64,7 @@ struct gbv_vs_batch {
   hipEvent_t ev[7] = {};
   hipEvent_t done = nullptr;
   hipEvent_t copied = nullptr;  // the last fill's input copy (stream A); see gbv_sm_batch::copied
+  hipEvent_t pre = nullptr;     // "pre" mode: k_vs_sig_pre done (stream 5)
   bool in_flight = false;
   int tail = 0;
 };
@@ -92,6 +93,7 @@ void vs_batch_free(gbv_vs_batch* b) {
   for (auto e : b->ev)
     if (e) hipEventDestroy(e);
   if (b->done) hipEventDestroy(b->done);
+  if (b->pre) hipEventDestroy(b->pre);
   delete b;
 }
 
@@ -111,6 +113,7 @@ static int vs_reserve(gbv_ctx* c, gbv_vs_batch* b, size_t n, size_t C) {
   for (auto& ev : b->ev)
     if (!ev) chk(hipEventCreate(&ev));
   if (!b->done) chk(hipEventCreateWithFlags(&b->done, hipEventDisableTiming));
+  if (!b->pre) chk(hipEventCreateWithFlags(&b->pre, hipEventDisableTiming));
   if (e != hipSuccess) {
     vs_free_work(b);
     return gbv_fail(c, GBV_E_OOM, std::string("hipMalloc: ") + hipGetErrorString(e));
@@ -286,6 +289,13 @@ static bool vs_split_on() {  // GBV_VS_SPLIT=0: hash and signature roles in one 
   return on;
 }
 
+// "pre" mode for passes of at most GBV_VS_PRE_MAX sets (0: off): k_vs_sig_pre + k_vs_pk_rand in place
+// of k_vs_hash_sig's signature roles
+static bool vs_pre_on(const gbv_vs_batch* b) {
+  static const size_t maxn = getenv("GBV_VS_PRE_MAX") ? (size_t)atol(getenv("GBV_VS_PRE_MAX")) : 2048;
+  return b->n <= maxn;
+}
+
 static bool vs_fs_small(const gbv_vs_batch* b) {
   static const size_t maxc = getenv("GBV_VS_FS_MAXC") ? (size_t)atol(getenv("GBV_VS_FS_MAXC")) : 256;
   return vs_fs_on() && (b->n <= VS_COOP_MILLER_MAX || b->C <= maxc);
@@ -300,6 +310,13 @@ static int vs_enqueue_sets(gbv_ctx* c, gbv_vs_batch* b, hipStream_t m, bool with
   hipStream_t s = c->stream;
   Seed seed = fresh_seed();
   uint32_t nonce = c->nonce++;
+  // small passes (latency): the signature half first, on stream 5, beside the aggregation below
+  const bool pre = with_fs && m != s && vs_fs_small(b) && vs_split_on() && vs_pre_on(b);
+  if (pre) {
+    HIP_CHECK(c, hipStreamWaitEvent(c->stream5, b->copied, 0));
+    launch_vs_sig_pre(c->stream5, (uint32_t)b->n, b->sig, b->sig_stride, b->siglen, seed, nonce, b->rS, b->status);
+    HIP_CHECK(c, hipEventRecord(b->pre, c->stream5));
+  }
   HIP_CHECK(c, hipEventRecord(b->ev[0], s));
   if (b->n_agg) launch_vs_agg(LaunchCfg{(unsigned)b->n_agg, 64, s}, b->agg_list, b->set_off, b->arena, c->table, c->table_ok, b->pk, b->pk_st);
   launch_vs_agg_big(s, (uint32_t)b->n_slices, b->slices, (uint32_t)b->n_big, b->big, b->arena, c->table, c->table_ok, b->agg_part,
@@ -310,8 +327,14 @@ static int vs_enqueue_sets(gbv_ctx* c, gbv_vs_batch* b, hipStream_t m, bool with
   const bool split = with_fs && m != s && vs_fs_small(b) && vs_split_on();
   if (split) HIP_CHECK(c, hipStreamWaitEvent(m, b->copied, 0));
   if (split) launch_hash_msgs(LaunchCfg{blocks_for(b->n), TPB, m}, b->msgs, (uint32_t)b->n, b->H, b->Hpre);
-  launch_vs_hash_sig(s, (uint32_t)b->n, b->msgs, b->set_off, b->arena, b->raw_flag, b->raw_pk, b->sig, b->sig_stride, b->siglen, c->table,
-                     c->table_ok, b->pk, b->pk_st, seed, nonce, b->H, b->rP, b->rS, b->status, split);
+  if (pre) {
+    HIP_CHECK(c, hipStreamWaitEvent(s, b->pre, 0));
+    launch_vs_pk_rand(s, (uint32_t)b->n, b->set_off, b->arena, b->raw_flag, b->raw_pk, c->table, c->table_ok, b->pk, b->pk_st, seed, nonce,
+                      b->rP, b->status);
+  } else {
+    launch_vs_hash_sig(s, (uint32_t)b->n, b->msgs, b->set_off, b->arena, b->raw_flag, b->raw_pk, b->sig, b->sig_stride, b->siglen, c->table,
+                       c->table_ok, b->pk, b->pk_st, seed, nonce, b->H, b->rP, b->rS, b->status, split);
+  }
   HIP_CHECK(c, hipEventRecord(b->ev[2], s));
   if (m != s) HIP_CHECK(c, hipStreamWaitEvent(m, b->ev[2], 0));
   HIP_CHECK(c, hipEventRecord(b->ev[3], m));

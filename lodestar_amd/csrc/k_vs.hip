@@ -214,6 +214,73 @@ __global__ void GBV_KERNEL_ATTR k_vs_hash_sig(uint32_t n, uint32_t nb, uint32_t 
   rS_out[i] = rs;
 }
 
+// Small passes, latency form ("pre" mode, gbv_vs.hip): the signature work that needs no pubkey runs
+// on its own stream beside the pubkey aggregation -- blocks [0, nsig) decode and group-check each
+// signature (status = its verdict), blocks [nsig, 2 nsig) decode it again and form r_i sig_i
+// (randomize_g2: the same r_i = a - b x^2 split as randomize_pair_jac) -- and k_vs_pk_rand, after the
+// aggregation and these, takes the pubkey, merges its verdict and forms r_i pk_i.  The aggregation
+// (an Electra block's committee sums: ~3.7 ms) then no longer sits in front of the signature chain.
+__global__ void GBV_KERNEL_ATTR k_vs_sig_pre(uint32_t n, const uint8_t* __restrict__ sig, uint32_t sig_stride, const uint32_t* __restrict__ sig_len,
+                                             Seed seed, uint32_t nonce, G2J* __restrict__ rS_out, uint8_t* __restrict__ status) {
+  const uint32_t nsig = (n + 63) / 64;
+  uint32_t blk = blockIdx.x;
+  const bool rand = blk >= nsig;
+  if (rand) blk -= nsig;
+  const uint32_t i = blk * 64 + threadIdx.x;
+  if (i >= n) return;
+  G2A s;
+  const uint8_t ds = g2_decode(s, sig + (size_t)sig_stride * i, sig_len[i]);
+  if (!rand) {
+    status[i] = (ds != PT_OK || !g2_in_subgroup(s)) ? SET_BAD_SIG : SET_OK;
+    return;
+  }
+  if (ds != PT_OK) return;
+  const uint64_t r = prf_scalar(seed, i, nonce);
+  G2J rs;
+  if (!randomize_g2(s, r, &rs)) rs = g2_mul_u64(s, r);  // unreachable for subgroup points
+  rS_out[i] = rs;
+}
+
+// The pubkey half (stream A, after the aggregation and k_vs_sig_pre): a rejected signature's verdict
+// stands (it wins over a bad pubkey, as in k_vs_hash_sig); otherwise the pubkey's verdict is merged
+// and r_i pk_i formed.  Raw pubkeys (PublicKey.fromBytes(pk, true)) are decoded and group-checked here.
+__global__ void GBV_KERNEL_ATTR k_vs_pk_rand(uint32_t n, const uint32_t* __restrict__ set_off, const uint32_t* __restrict__ arena,
+                                             const uint8_t* __restrict__ raw_flag, const uint8_t* __restrict__ raw_pk48,
+                                             const G1A* __restrict__ table, const uint8_t* __restrict__ table_ok,
+                                             const G1J* __restrict__ pk_agg, const uint8_t* __restrict__ pk_st, Seed seed, uint32_t nonce,
+                                             G1J* __restrict__ rP_out, uint8_t* __restrict__ status) {
+  const uint32_t i = blockIdx.x * 64 + threadIdx.x;
+  if (i >= n || status[i] != SET_OK) return;
+  bool ok = true, jac = false;
+  G1A pa{fp_zero(), fp_zero()};
+  G1J pj;
+  if (raw_flag[i]) {
+    ok = g1_decompress(pa, raw_pk48 + 48ull * i) == PT_OK && g1_in_subgroup(pa);
+  } else {
+    const uint32_t b = set_off[i], e = set_off[i + 1];
+    if (e - b == 1) {
+      const uint32_t k = arena[b];
+      pa = table[k];
+      ok = table_ok[k] != 0;
+    } else if (e == b) {
+      ok = false;  // empty aggregate: its call is rejected on the host, never verified
+    } else {
+      pj = pk_agg[i];
+      jac = true;
+      ok = pk_st[i] == SET_OK;
+    }
+  }
+  if (ok && jac) ok = jac_to_aff(pa, pj);  // an OK aggregate is never infinity (k_vs_agg)
+  if (!ok) {
+    status[i] = SET_BAD_PK;
+    return;
+  }
+  const uint64_t r = prf_scalar(seed, i, nonce);
+  G1J rp;
+  if (!randomize_g1(pa, r, &rp)) rp = g1_mul_u64(pa, r);
+  rP_out[i] = rp;
+}
+
 // Signature.fromBytes(sig, true) (maybeBatch.ts:23; the "BLS deserializing signatures" perf id,
 // test/perf/bls/bls.test.ts:89-100): decode + subgroup check, and the recompressed encoding of
 // every accepted point (byte-identical to the input for canonical compressed signatures).
@@ -308,6 +375,20 @@ void launch_vs_hash_sig(hipStream_t s, uint32_t n, const uint8_t* msgs32, const 
   hipLaunchKernelGGL(k_vs_hash_sig, dim3(nb + (split ? 2 : 1) * nsig), dim3(64), 0, s, n, nb, pair, split ? 1u : 0u, msgs32, set_off,
                      arena, raw_flag, raw_pk48, sig, sig_stride, sig_len, table, table_ok, pk_agg, pk_st, seed, nonce, H, rP, rS, status);
   debug_sync(s, "k_vs_hash_sig");
+}
+
+void launch_vs_sig_pre(hipStream_t s, uint32_t n, const uint8_t* sig, uint32_t sig_stride, const uint32_t* sig_len, const Seed& seed,
+                       uint32_t nonce, G2J* rS, uint8_t* status) {
+  const uint32_t nsig = (n + 63) / 64;
+  hipLaunchKernelGGL(k_vs_sig_pre, dim3(2 * nsig), dim3(64), 0, s, n, sig, sig_stride, sig_len, seed, nonce, rS, status);
+  debug_sync(s, "k_vs_sig_pre");
+}
+void launch_vs_pk_rand(hipStream_t s, uint32_t n, const uint32_t* set_off, const uint32_t* arena, const uint8_t* raw_flag,
+                       const uint8_t* raw_pk48, const G1A* table, const uint8_t* table_ok, const G1J* pk_agg, const uint8_t* pk_st,
+                       const Seed& seed, uint32_t nonce, G1J* rP, uint8_t* status) {
+  hipLaunchKernelGGL(k_vs_pk_rand, dim3((n + 63) / 64), dim3(64), 0, s, n, set_off, arena, raw_flag, raw_pk48, table, table_ok, pk_agg, pk_st,
+                     seed, nonce, rP, status);
+  debug_sync(s, "k_vs_pk_rand");
 }
 
 void launch_sig_validate(LaunchCfg c, uint32_t n, const uint8_t* sig, uint32_t sig_len, uint8_t* status, uint8_t* out96) {
