@@ -50,6 +50,7 @@ struct gbv_vs_batch {
   G1J* rP = nullptr;
   G2J* rS = nullptr;
   uint8_t* status = nullptr;
+  uint8_t* sig_st = nullptr;  // "pre" mode: the signature verdicts alone (k_vs_sig_pre), read by k_vs_chunk_s_miller
   Fp12* F = nullptr;
   G2J* Hpre = nullptr;        // per set: Q0 + Q1 before the cofactor clearing (small passes)
   Fp12* Fs = nullptr;         // per chunk: Miller value of (-g1, sum r_i sig_i) (small passes, k_vs_miller_coop)
@@ -72,8 +73,8 @@ struct gbv_vs_batch {
 static void vs_free_work(gbv_vs_batch* b) {
   // teardown: a failing free has nothing left to report to
   (void)hipFree(b->pk); (void)hipFree(b->pk_st); (void)hipFree(b->H); (void)hipFree(b->rP); (void)hipFree(b->rS);
-  (void)hipFree(b->status); (void)hipFree(b->F); (void)hipFree(b->Fs); (void)hipFree(b->Hpre); (void)hipFree(b->fs_flag); (void)hipFree(b->chunk_valid); (void)hipHostFree(b->chunk_valid_host);
-  b->pk = nullptr; b->pk_st = nullptr; b->H = nullptr; b->rP = nullptr; b->rS = nullptr; b->status = nullptr; b->F = nullptr; b->Fs = nullptr; b->fs_flag = nullptr; b->Hpre = nullptr;
+  (void)hipFree(b->status); (void)hipFree(b->sig_st); (void)hipFree(b->F); (void)hipFree(b->Fs); (void)hipFree(b->Hpre); (void)hipFree(b->fs_flag); (void)hipFree(b->chunk_valid); (void)hipHostFree(b->chunk_valid_host);
+  b->pk = nullptr; b->pk_st = nullptr; b->H = nullptr; b->rP = nullptr; b->rS = nullptr; b->status = nullptr; b->sig_st = nullptr; b->F = nullptr; b->Fs = nullptr; b->fs_flag = nullptr; b->Hpre = nullptr;
   b->chunk_valid = nullptr; b->chunk_valid_host = nullptr;
   b->allocated = false;
 }
@@ -107,7 +108,7 @@ static int vs_reserve(gbv_ctx* c, gbv_vs_batch* b, size_t n, size_t C) {
   hipError_t e = hipSuccess;
   auto chk = [&](hipError_t x) { if (x != hipSuccess && e == hipSuccess) e = x; };
   chk(dalloc(&b->pk, n)); chk(dalloc(&b->pk_st, n)); chk(dalloc(&b->H, n)); chk(dalloc(&b->rP, n)); chk(dalloc(&b->rS, n));
-  chk(dalloc(&b->status, n)); chk(dalloc(&b->F, n)); chk(dalloc(&b->chunk_valid, C));
+  chk(dalloc(&b->status, n)); chk(dalloc(&b->sig_st, n)); chk(dalloc(&b->F, n)); chk(dalloc(&b->chunk_valid, C));
   chk(dalloc(&b->Fs, C)); chk(dalloc(&b->fs_flag, C)); chk(dalloc(&b->Hpre, n));
   chk(hipHostMalloc((void**)&b->chunk_valid_host, std::max<size_t>(C, 1), hipHostMallocDefault));
   for (auto& ev : b->ev)
@@ -314,8 +315,12 @@ static int vs_enqueue_sets(gbv_ctx* c, gbv_vs_batch* b, hipStream_t m, bool with
   const bool pre = with_fs && m != s && vs_fs_small(b) && vs_split_on() && vs_pre_on(b);
   if (pre) {
     HIP_CHECK(c, hipStreamWaitEvent(c->stream5, b->copied, 0));
-    launch_vs_sig_pre(c->stream5, (uint32_t)b->n, b->sig, b->sig_stride, b->siglen, seed, nonce, b->rS, b->status);
+    launch_vs_sig_pre(c->stream5, (uint32_t)b->n, b->sig, b->sig_stride, b->siglen, seed, nonce, b->rS, b->status, b->sig_st);
     HIP_CHECK(c, hipEventRecord(b->pre, c->stream5));
+    // each chunk's sum r_i sig_i and its (-g1, sum) Miller value need no pubkey either: they follow
+    // on stream 5 (a chunk with a rejected pubkey is caught by the chunk check's own status scan)
+    launch_vs_chunk_s_miller(c->stream5, (uint32_t)b->C, b->sig_st, b->chunk_off, b->rS, b->Fs, b->fs_flag);
+    HIP_CHECK(c, hipEventRecord(b->ev[6], c->stream5));
   }
   HIP_CHECK(c, hipEventRecord(b->ev[0], s));
   if (b->n_agg) launch_vs_agg(LaunchCfg{(unsigned)b->n_agg, 64, s}, b->agg_list, b->set_off, b->arena, c->table, c->table_ok, b->pk, b->pk_st);
@@ -343,7 +348,9 @@ static int vs_enqueue_sets(gbv_ctx* c, gbv_vs_batch* b, hipStream_t m, bool with
   else
     launch_vs_miller(LaunchCfg{blocks_for(b->n), TPB, m}, (uint32_t)b->n, b->status, b->rP, b->H, b->F);
   HIP_CHECK(c, hipEventRecord(b->ev[4], m));
-  if (with_fs && vs_fs_small(b)) {  // beside the per-set Miller values, on stream A (free after hash_sig)
+  if (pre) {
+    HIP_CHECK(c, hipStreamWaitEvent(m, b->ev[6], 0));
+  } else if (with_fs && vs_fs_small(b)) {  // beside the per-set Miller values, on stream A (free after hash_sig)
     launch_vs_chunk_s_miller(s, (uint32_t)b->C, b->status, b->chunk_off, b->rS, b->Fs, b->fs_flag);
     HIP_CHECK(c, hipEventRecord(b->ev[6], s));
     if (m != s) HIP_CHECK(c, hipStreamWaitEvent(m, b->ev[6], 0));

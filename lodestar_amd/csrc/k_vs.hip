@@ -221,7 +221,8 @@ __global__ void GBV_KERNEL_ATTR k_vs_hash_sig(uint32_t n, uint32_t nb, uint32_t 
 // aggregation and these, takes the pubkey, merges its verdict and forms r_i pk_i.  The aggregation
 // (an Electra block's committee sums: ~3.7 ms) then no longer sits in front of the signature chain.
 __global__ void GBV_KERNEL_ATTR k_vs_sig_pre(uint32_t n, const uint8_t* __restrict__ sig, uint32_t sig_stride, const uint32_t* __restrict__ sig_len,
-                                             Seed seed, uint32_t nonce, G2J* __restrict__ rS_out, uint8_t* __restrict__ status) {
+                                             Seed seed, uint32_t nonce, G2J* __restrict__ rS_out, uint8_t* __restrict__ status,
+                                             uint8_t* __restrict__ sig_st) {
   const uint32_t nsig = (n + 63) / 64;
   uint32_t blk = blockIdx.x;
   const bool rand = blk >= nsig;
@@ -231,7 +232,9 @@ __global__ void GBV_KERNEL_ATTR k_vs_sig_pre(uint32_t n, const uint8_t* __restri
   G2A s;
   const uint8_t ds = g2_decode(s, sig + (size_t)sig_stride * i, sig_len[i]);
   if (!rand) {
-    status[i] = (ds != PT_OK || !g2_in_subgroup(s)) ? SET_BAD_SIG : SET_OK;
+    const uint8_t st = (ds != PT_OK || !g2_in_subgroup(s)) ? SET_BAD_SIG : SET_OK;
+    status[i] = st;
+    sig_st[i] = st;  // a copy k_vs_pk_rand does not touch (k_vs_chunk_s_miller reads it meanwhile)
     return;
   }
   if (ds != PT_OK) return;
@@ -378,9 +381,9 @@ void launch_vs_hash_sig(hipStream_t s, uint32_t n, const uint8_t* msgs32, const 
 }
 
 void launch_vs_sig_pre(hipStream_t s, uint32_t n, const uint8_t* sig, uint32_t sig_stride, const uint32_t* sig_len, const Seed& seed,
-                       uint32_t nonce, G2J* rS, uint8_t* status) {
+                       uint32_t nonce, G2J* rS, uint8_t* status, uint8_t* sig_st) {
   const uint32_t nsig = (n + 63) / 64;
-  hipLaunchKernelGGL(k_vs_sig_pre, dim3(2 * nsig), dim3(64), 0, s, n, sig, sig_stride, sig_len, seed, nonce, rS, status);
+  hipLaunchKernelGGL(k_vs_sig_pre, dim3(2 * nsig), dim3(64), 0, s, n, sig, sig_stride, sig_len, seed, nonce, rS, status, sig_st);
   debug_sync(s, "k_vs_sig_pre");
 }
 void launch_vs_pk_rand(hipStream_t s, uint32_t n, const uint32_t* set_off, const uint32_t* arena, const uint8_t* raw_flag,
