@@ -293,7 +293,7 @@ static bool vs_split_on() {  // GBV_VS_SPLIT=0: hash and signature roles in one 
 // "pre" mode for passes of at most GBV_VS_PRE_MAX sets (0: off): k_vs_sig_pre + k_vs_pk_rand in place
 // of k_vs_hash_sig's signature roles
 static bool vs_pre_on(const gbv_vs_batch* b) {
-  static const size_t maxn = getenv("GBV_VS_PRE_MAX") ? (size_t)atol(getenv("GBV_VS_PRE_MAX")) : 2048;
+  static const size_t maxn = getenv("GBV_VS_PRE_MAX") ? (size_t)atol(getenv("GBV_VS_PRE_MAX")) : 16384;
   return b->n <= maxn;
 }
 

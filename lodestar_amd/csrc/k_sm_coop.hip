@@ -343,13 +343,26 @@ __device__ inline bool coop_pair_check(coop::Slot* ws, const G1A& P, const G2A& 
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
 k_sm_fb_blocks_coop(const uint4* __restrict__ runs, const uint32_t* __restrict__ n_runs, uint32_t cap, const uint8_t* __restrict__ status,
                     const uint32_t* __restrict__ grp_msg, const G2J* __restrict__ Sh, const G1J* __restrict__ Ph, const G2A* __restrict__ H,
-                    uint8_t* __restrict__ valid, uint32_t* __restrict__ set_list, uint32_t* __restrict__ n_list) {
+                    uint8_t* __restrict__ valid, uint32_t* __restrict__ set_list, uint32_t* __restrict__ n_list, int direct_ok) {
   __shared__ coop::Slot ws[SEG_WS];
   __shared__ Fp st[6];
   __shared__ int flags[3];
   uint32_t cnt = min(*n_runs, cap);
   if (cnt > FB_COOP_MAX) return;
   unsigned lane = threadIdx.x;
+  if (direct_ok && cnt * FB_RUN_MAX <= FB_COOP_MAX) {  // few sets in all: straight to the per-set checks
+    for (uint32_t k = blockIdx.x; k < cnt; k += gridDim.x) {
+      const uint4 r = runs[k];
+      if (lane == 0)
+        for (uint32_t i = r.x; i < r.y; ++i) {
+          if (status[i] != SET_OK)
+            valid[i] = 0;
+          else
+            set_list[atomicAdd(n_list, 1u)] = i;
+        }
+    }
+    return;
+  }
   if (blockIdx.x < cnt) coop::load_consts();
   for (uint32_t k = blockIdx.x; k < cnt; k += gridDim.x) {
     uint4 r = runs[k];
@@ -450,8 +463,9 @@ k_sm_fb_sets_fe(const uint32_t* __restrict__ set_list, const uint32_t* __restric
 void launch_sm_fb_blocks_coop(LaunchCfg c, const uint4* runs, const uint32_t* n_runs, uint32_t cap, const uint8_t* status,
                               const uint32_t* grp_msg, const G2J* Sh, const G1J* Ph, const G2A* H, uint8_t* valid, uint32_t* set_list,
                               uint32_t* n_list) {
+  static const int direct = !(getenv("GBV_FB_DIRECT") && atoi(getenv("GBV_FB_DIRECT")) == 0);
   hipLaunchKernelGGL(k_sm_fb_blocks_coop, dim3(FB_COOP_MAX), dim3(64), 0, c.stream, runs, n_runs, cap, status, grp_msg, Sh, Ph, H, valid,
-                     set_list, n_list);
+                     set_list, n_list, direct);
   debug_sync(c.stream, "k_sm_fb_blocks_coop");
 }
 void launch_sm_fb_sets_coop(LaunchCfg c, const uint32_t* set_list, const uint32_t* n_list, const uint32_t* set_grp, const uint32_t* grp_msg,

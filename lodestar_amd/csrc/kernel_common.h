@@ -52,6 +52,10 @@ enum : uint8_t { GRP_PENDING = 0, GRP_FALLBACK = 1, GRP_OK = 2 };
 // Failure-path item counts up to which one wave per item (k_sm_fb_*_coop, latency) beats one
 // thread per item (k_sm_fb_blocks / k_sm_fb_sets, throughput).
 constexpr uint32_t FB_COOP_MAX = 256;
+// Sets per failure-path run (the 8-set scan windows of k_sm_prepare).  When the failing runs hold at
+// most FB_COOP_MAX sets in all, k_sm_fb_blocks_coop skips the run checks and hands every set to the
+// per-set stage: one pairing stage of latency instead of two (GBV_FB_DIRECT=0: always two).
+constexpr uint32_t FB_RUN_MAX = 8;
 // Message counts up to which hash_to_G2 runs on lane pairs (latency) instead of one lane each.
 constexpr uint32_t HASH_PAIR_MAX = 4096;
 // HASH_PAIR_MAX, overridable for A/B runs (GBV_HASH_PAIR_MAX); host side only
