@@ -311,25 +311,28 @@ static int vs_enqueue_sets(gbv_ctx* c, gbv_vs_batch* b, hipStream_t m, bool with
   hipStream_t s = c->stream;
   Seed seed = fresh_seed();
   uint32_t nonce = c->nonce++;
-  // small passes (latency): the signature half first, on stream 5, beside the aggregation below
-  const bool pre = with_fs && m != s && vs_fs_small(b) && vs_split_on() && vs_pre_on(b);
+  // passes up to GBV_VS_PRE_MAX sets: the signature half first, on stream 5, beside the aggregation below
+  const bool small = with_fs && vs_fs_small(b);
+  const bool pre = with_fs && m != s && vs_split_on() && vs_pre_on(b);
   if (pre) {
     HIP_CHECK(c, hipStreamWaitEvent(c->stream5, b->copied, 0));
     launch_vs_sig_pre(c->stream5, (uint32_t)b->n, b->sig, b->sig_stride, b->siglen, seed, nonce, b->rS, b->status, b->sig_st);
     HIP_CHECK(c, hipEventRecord(b->pre, c->stream5));
-    // each chunk's sum r_i sig_i and its (-g1, sum) Miller value need no pubkey either: they follow
-    // on stream 5 (a chunk with a rejected pubkey is caught by the chunk check's own status scan)
-    launch_vs_chunk_s_miller(c->stream5, (uint32_t)b->C, b->sig_st, b->chunk_off, b->rS, b->Fs, b->fs_flag);
-    HIP_CHECK(c, hipEventRecord(b->ev[6], c->stream5));
+    if (small) {
+      // each chunk's sum r_i sig_i and its (-g1, sum) Miller value need no pubkey either: they follow
+      // on stream 5 (a chunk with a rejected pubkey is caught by the chunk check's own status scan)
+      launch_vs_chunk_s_miller(c->stream5, (uint32_t)b->C, b->sig_st, b->chunk_off, b->rS, b->Fs, b->fs_flag);
+      HIP_CHECK(c, hipEventRecord(b->ev[6], c->stream5));
+    }
   }
   HIP_CHECK(c, hipEventRecord(b->ev[0], s));
   if (b->n_agg) launch_vs_agg(LaunchCfg{(unsigned)b->n_agg, 64, s}, b->agg_list, b->set_off, b->arena, c->table, c->table_ok, b->pk, b->pk_st);
   launch_vs_agg_big(s, (uint32_t)b->n_slices, b->slices, (uint32_t)b->n_big, b->big, b->arena, c->table, c->table_ok, b->agg_part,
                     b->agg_part_bad, b->pk, b->pk_st);
   HIP_CHECK(c, hipEventRecord(b->ev[1], s));
-  // small passes (latency): the hash on stream m (lane-pair maps, cooperative cofactor clearing)
-  // beside the signature checks and the randomisation, which run as two block roles on stream A
-  const bool split = with_fs && m != s && vs_fs_small(b) && vs_split_on();
+  // small passes and pre mode: the hash on stream m (for few messages lane-pair maps and the
+  // cooperative cofactor clearing) beside the signature work
+  const bool split = with_fs && m != s && (small || pre) && vs_split_on();
   if (split) HIP_CHECK(c, hipStreamWaitEvent(m, b->copied, 0));
   if (split) launch_hash_msgs(LaunchCfg{blocks_for(b->n), TPB, m}, b->msgs, (uint32_t)b->n, b->H, b->Hpre);
   if (pre) {
@@ -348,9 +351,9 @@ static int vs_enqueue_sets(gbv_ctx* c, gbv_vs_batch* b, hipStream_t m, bool with
   else
     launch_vs_miller(LaunchCfg{blocks_for(b->n), TPB, m}, (uint32_t)b->n, b->status, b->rP, b->H, b->F);
   HIP_CHECK(c, hipEventRecord(b->ev[4], m));
-  if (pre) {
+  if (pre && small) {
     HIP_CHECK(c, hipStreamWaitEvent(m, b->ev[6], 0));
-  } else if (with_fs && vs_fs_small(b)) {  // beside the per-set Miller values, on stream A (free after hash_sig)
+  } else if (small) {  // beside the per-set Miller values, on stream A (free after hash_sig)
     launch_vs_chunk_s_miller(s, (uint32_t)b->C, b->status, b->chunk_off, b->rS, b->Fs, b->fs_flag);
     HIP_CHECK(c, hipEventRecord(b->ev[6], s));
     if (m != s) HIP_CHECK(c, hipStreamWaitEvent(m, b->ev[6], 0));
