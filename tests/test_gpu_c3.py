@@ -88,3 +88,22 @@ def test_c3_oracle_spot_check(c3):
         assert O.set_is_valid(agg, s.signing_root, s.signature)
         # and the device's aggregatePublicKeys of the same committee is byte-identical
         assert v.aggregate_pubkeys(list(s.indices)) == O.g1_compress(agg)
+
+
+def test_c3_large_pass_thread_forms(c3):
+    """A pass of 40 960 sets (the fixture's 80 calls four times over): above the 16 384-set bound of
+    the split signature/pubkey form and the 32 768-set bound of the lane-pair Miller values, so the
+    throughput kernels run -- k_vs_hash_sig with both roles, k_vs_miller one thread per set, the chunk
+    checks without precomputed (-g1, sum) values -- with a bad pubkey and a bad signature placed in
+    the last copy."""
+    from lodestar_amd import AggregatedSignatureSet
+    v, sets, _ = c3
+    calls = [list(sets[i:i + PER_CALL]) for i in range(0, N_SETS, PER_CALL)] * 4
+    assert sum(len(c) for c in calls) == 4 * N_SETS
+    assert v.verify_signature_sets_multi_sync(calls) == [True] * 320
+    bad = [list(c) for c in calls]
+    s = bad[250][9]  # committee one member short
+    bad[250][9] = AggregatedSignatureSet(list(s.indices)[:-1], s.signing_root, s.signature)
+    s = bad[319][127]  # malformed signature bytes
+    bad[319][127] = AggregatedSignatureSet(s.indices, s.signing_root, bytes([10]) * 96)
+    assert v.verify_signature_sets_multi_sync(bad) == [c not in (250, 319) for c in range(320)]
