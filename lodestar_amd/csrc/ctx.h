@@ -96,6 +96,7 @@ struct gbv_ctx {
   // queues (GPU_MAX_HW_QUEUES=4 leaves one for the runtime): no two streams share a queue.
   hipStream_t stream = nullptr, stream2 = nullptr, stream4 = nullptr;
   hipStream_t stream5 = nullptr;  // small verifySignatureSets passes: the signature half beside the aggregation
+  hipStream_t stream6 = nullptr;  // GBV_MSM_CUS > 0: the same-message chunk sums + bucket MSM on their own CUs
   gbv::G1A* table = nullptr;
   uint8_t* table_ok = nullptr;
   size_t table_cap = 0;

@@ -38,7 +38,7 @@ int gbv_fail(gbv_ctx* c, int code, const std::string& msg) {
 }
 
 void ctx_drain(gbv_ctx* c) {
-  for (hipStream_t s : {c->stream, c->stream2, c->stream4, c->stream5})
+  for (hipStream_t s : {c->stream, c->stream2, c->stream4, c->stream5, c->stream6})
     if (s) (void)hipStreamSynchronize(s);
   (void)hipGetLastError();
 }
@@ -213,6 +213,10 @@ static void sm_destroy(gbv_sm_batch* b) {
 
 extern "C" {
 
+#ifndef GBV_MSM_CUS_DEFAULT
+#define GBV_MSM_CUS_DEFAULT 0
+#endif
+
 int gbv_init(int device, gbv_ctx** out) {
   if (!out) return GBV_E_ARG;
   *out = nullptr;
@@ -230,10 +234,35 @@ int gbv_init(int device, gbv_ctx** out) {
             hipStreamCreateWithPriority(&c->stream4, hipStreamNonBlocking, prio_hi) == hipSuccess &&
             hipStreamCreateWithPriority(&c->stream5, hipStreamNonBlocking, prio_hi) == hipSuccess;
   if (!ok) {
-    for (hipStream_t s : {c->stream, c->stream2, c->stream4, c->stream5})
+    for (hipStream_t s : {c->stream, c->stream2, c->stream4, c->stream5, c->stream6})
       if (s) hipStreamDestroy(s);
     delete c;
     return GBV_E_DEVICE;
+  }
+  // GBV_MSM_CUS = k > 0: stream A loses k CUs (every (n/k)-th, spread over the XCDs) to a stream of
+  // their own for the same-message chunk sums and bucket MSM, which then run beside the next batch's
+  // k_sm_prepare instead of after it (on shared CUs the prepare waves starve them)
+  const int msm_cus = getenv("GBV_MSM_CUS") ? atoi(getenv("GBV_MSM_CUS")) : GBV_MSM_CUS_DEFAULT;
+  hipDeviceProp_t prop;
+  if (msm_cus > 0 && hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 2 * msm_cus) {
+    const int ncu = prop.multiProcessorCount, step = ncu / msm_cus;
+    std::vector<uint32_t> ma((ncu + 31) / 32, 0u), mm((ncu + 31) / 32, 0u);
+    int taken = 0;
+    for (int cu = 0; cu < ncu; ++cu) {
+      const bool m = cu % step == step - 1 && taken < msm_cus;
+      taken += m ? 1 : 0;
+      (m ? mm : ma)[cu / 32] |= 1u << (cu % 32);
+    }
+    hipStream_t a2 = nullptr, m2 = nullptr;
+    if (hipExtStreamCreateWithCUMask(&a2, (uint32_t)ma.size(), ma.data()) == hipSuccess &&
+        hipExtStreamCreateWithCUMask(&m2, (uint32_t)mm.size(), mm.data()) == hipSuccess) {
+      hipStreamDestroy(c->stream);
+      c->stream = a2;
+      c->stream6 = m2;
+    } else {
+      if (a2) hipStreamDestroy(a2);
+      if (m2) hipStreamDestroy(m2);
+    }
   }
   const char* comb_env = getenv("GBV_COMB");
   c->comb_on = !(comb_env && comb_env[0] == '0');
@@ -249,7 +278,7 @@ void gbv_destroy(gbv_ctx* c) {
   hipSetDevice(c->device);
   c->closed = true;
   // every stream drains before anything it may still read or write is freed
-  for (hipStream_t s : {c->stream, c->stream2, c->stream4, c->stream5})
+  for (hipStream_t s : {c->stream, c->stream2, c->stream4, c->stream5, c->stream6})
     if (s) hipStreamSynchronize(s);
   sm_destroy(c->sm_scratch);
   vs_batch_free(c->vs_scratch);
@@ -262,7 +291,7 @@ void gbv_destroy(gbv_ctx* c) {
   for (auto* p : c->ssz_buf) hipFree(p);
   for (auto e : c->ssz_ev)
     if (e) hipEventDestroy(e);
-  for (hipStream_t s : {c->stream, c->stream2, c->stream4, c->stream5})
+  for (hipStream_t s : {c->stream, c->stream2, c->stream4, c->stream5, c->stream6})
     if (s) hipStreamDestroy(s);
   delete c;
 }
@@ -758,8 +787,9 @@ static int sm_submit_enqueue(gbv_ctx* c, gbv_sm_batch* b) {
     // k_sm_prepare (the MSM's bucket pass then has the whole device instead of fighting the next
     // k_sm_prepare for CUs); the tail stream waits for them.  Other segments sum their chunks on
     // the tail stream.
-    hipStream_t scf = msm ? sa : sb;
-    if (!msm) HIP_CHECK(c, hipStreamWaitEvent(sb, e[1], 0));
+    hipStream_t sm6 = c->stream6;  // GBV_MSM_CUS: chunk sums + bucket MSM on their own CUs
+    hipStream_t scf = msm ? (sm6 ? sm6 : sa) : sb;
+    if (scf != sa) HIP_CHECK(c, hipStreamWaitEvent(scf, e[1], 0));
     HIP_CHECK(c, hipStreamWaitEvent(scf, ev[1], 0));
     HIP_CHECK(c, hipEventRecord(e[2], scf));
     launch_sm_chunk_finish(LaunchCfg{0, 64, scf}, g0, G, s0, b->grp_off, b->status, Sh, b->rP, b->PgJ, b->SgJ, b->grp_state,
@@ -768,8 +798,8 @@ static int sm_submit_enqueue(gbv_ctx* c, gbv_sm_batch* b) {
     // the bucket pass runs on stream A (default) or, with GBV_MSM_STREAM=h, on the hash stream beside
     // the tail's Miller values
     static const bool msm_on_hash = getenv("GBV_MSM_STREAM") && getenv("GBV_MSM_STREAM")[0] == 'h';
-    hipStream_t smsm = msm ? (msm_on_hash ? sh : sa) : scf;
-    if (msm && msm_on_hash) HIP_CHECK(c, hipStreamWaitEvent(sh, e[3], 0));
+    hipStream_t smsm = msm ? (sm6 ? sm6 : msm_on_hash ? sh : sa) : scf;
+    if (msm && !sm6 && msm_on_hash) HIP_CHECK(c, hipStreamWaitEvent(sh, e[3], 0));
     HIP_CHECK(c, hipEventRecord(e[10], smsm));
     // segment s-2 shares this segment's bucket buffers: its reduction (tail stream) must be done
     if (msm && s >= 2 && b->seg_msm[s - 2]) HIP_CHECK(c, hipStreamWaitEvent(smsm, ev[2 + EPS * (s - 2) + 12], 0));
