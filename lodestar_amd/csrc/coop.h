@@ -300,7 +300,7 @@ __device__ inline void load_consts() {
 
 // All of a lane's records for this program are fetched up front (one memory latency), the next
 // round's while the current round computes.
-__device__ __noinline__ void run_ni(const Prog* PP, uint32_t b0, uint32_t b1, uint32_t b2, uint32_t b3) {
+__device__ __forceinline__ void run_body(const Prog* PP, uint32_t b0, uint32_t b1, uint32_t b2, uint32_t b3) {
   const Prog& P = *PP;
   const Ws w{{b0, b1, b2, b3}};
   const int lane = (int)(threadIdx.x & 63u);
@@ -332,7 +332,11 @@ __device__ __noinline__ void run_ni(const Prog* PP, uint32_t b0, uint32_t b1, ui
   barrier();
 }
 // One out-of-line copy of the interpreter serves every call site (the drivers make hundreds).
+__device__ __noinline__ void run_ni(const Prog* PP, uint32_t b0, uint32_t b1, uint32_t b2, uint32_t b3) { run_body(PP, b0, b1, b2, b3); }
 __device__ inline void run(const Prog& P, const Ws& w) { run_ni(&P, w.b[0], w.b[1], w.b[2], w.b[3]); }
+// The interpreter inlined at one call site and specialised for its program (the program's counts
+// fold into the code; no call, no callee-saved spills): for the program a hot loop runs tens of times.
+__device__ __forceinline__ void run_inl(const Prog& P, const Ws& w) { run_body(&P, w.b[0], w.b[1], w.b[2], w.b[3]); }
 #define COOP_LANES(l) for (unsigned l = threadIdx.x & 63u; l == (threadIdx.x & 63u); l = ~0u)
 #define COOP_LANE0 if ((threadIdx.x & 63u) == 0)
 #endif
@@ -381,7 +385,19 @@ GBV_HD Ws ws2(Slot* mem, uint16_t z, uint16_t a, uint16_t b) { return make_ws(me
 GBV_HD Ws ws3(Slot* mem, uint16_t z, uint16_t a, uint16_t b, uint16_t c) { return make_ws(mem, z, a, b, c); }
 
 GBV_HD void mul12(Slot* mem, uint16_t z, uint16_t a, uint16_t b, uint16_t c) { run(FP12_MUL, ws3(mem, z, a, b, c)); }
+#ifndef GBV_COOP_INLINE_CYC
+#define GBV_COOP_INLINE_CYC 1  // the final exponentiation's ~320 cyclotomic squarings through run_inl
+#endif
+#if defined(GBV_HOST_TEST)
 GBV_HD void cyc_sqr12(Slot* mem, uint16_t z, uint16_t a, uint16_t c) { run(FP12_CYC_SQR, ws2(mem, z, a, c)); }
+#else
+GBV_HD void cyc_sqr12(Slot* mem, uint16_t z, uint16_t a, uint16_t c) {
+  if (GBV_COOP_INLINE_CYC)
+    run_inl(FP12_CYC_SQR, ws2(mem, z, a, c));
+  else
+    run(FP12_CYC_SQR, ws2(mem, z, a, c));
+}
+#endif
 GBV_HD void frob12(Slot* mem, uint16_t z, int n, uint16_t a, uint16_t c) { run(n == 1 ? FP12_FROB1 : FP12_FROB2, ws2(mem, z, a, c)); }
 
 // ---- Miller loop over up to 2 pairs ---------------------------------------------------------
