@@ -388,6 +388,20 @@ GBV_HD void mul12(Slot* mem, uint16_t z, uint16_t a, uint16_t b, uint16_t c) { r
 #ifndef GBV_COOP_INLINE_CYC
 #define GBV_COOP_INLINE_CYC 1  // the final exponentiation's ~320 cyclotomic squarings through run_inl
 #endif
+#ifndef GBV_COOP_INLINE_LOOPS
+#define GBV_COOP_INLINE_LOOPS 1  // the Miller loop's per-bit programs and the [|x|] doublings too
+#endif
+// a program called from a 63-step loop: inlined (GBV_COOP_INLINE_LOOPS) or the shared interpreter
+#if defined(GBV_HOST_TEST)
+#define run_hot run
+#else
+GBV_HD void run_hot(const Prog& P, const Ws& w) {
+  if (GBV_COOP_INLINE_LOOPS)
+    run_inl(P, w);
+  else
+    run(P, w);
+}
+#endif
 #if defined(GBV_HOST_TEST)
 GBV_HD void cyc_sqr12(Slot* mem, uint16_t z, uint16_t a, uint16_t c) { run(FP12_CYC_SQR, ws2(mem, z, a, c)); }
 #else
@@ -439,10 +453,10 @@ GBV_HD void miller_loop(Slot* mem, int npairs) {
     for (int j = 0; j < npairs; ++j) {
       uint16_t t = M_PAIR + 12 * j;
       if (j == 0 && i != 62)  // f^2 and pair 0's doubling step are independent: one program
-        run(MILLER_SQR_DBL, make_ws(mem, M_Z, M_F, t, (uint16_t)(t + 10), M_F, t, M_L));
+        run_hot(MILLER_SQR_DBL, make_ws(mem, M_Z, M_F, t, (uint16_t)(t + 10), M_F, t, M_L));
       else
         run(G2_DBL_STEP, make_ws(mem, M_Z, t, (uint16_t)(t + 10), t, M_L));
-      run(FP12_MUL_LINE, ws3(mem, M_Z, M_F, M_L, M_F));
+      run_hot(FP12_MUL_LINE, ws3(mem, M_Z, M_F, M_L, M_F));
     }
     if ((X_ABS >> i) & 1ull) {
       for (int j = 0; j < npairs; ++j) {
@@ -464,7 +478,7 @@ GBV_HD void mul_xabs_point(Slot* mem, const G2A& Q) {
   miller_load_pair(mem, 0, G1A{fp_zero(), fp_zero()}, Q);
   const uint16_t t = M_PAIR;
   for (int i = 62; i >= 0; --i) {
-    run(G2_DBL_PT, make_ws(mem, M_Z, t, t));  // the doubling without its line: 19 products, 6 outputs
+    run_hot(G2_DBL_PT, make_ws(mem, M_Z, t, t));  // the doubling without its line: 19 products, 6 outputs
     if ((X_ABS >> i) & 1ull) run(G2_ADD_STEP, make_ws(mem, M_Z, t, (uint16_t)(t + 6), (uint16_t)(t + 10), t, M_L));
   }
 }
