@@ -779,7 +779,7 @@ static int sm_submit_enqueue(gbv_ctx* c, gbv_sm_batch* b) {
     HIP_CHECK(c, hipEventRecord(e[0], sa));
     launch_sm_prepare(LaunchCfg{0, 64, sa}, s0, s1 - s0, b->idx, b->sig, b->set_grp, c->table, c->table_ok, (uint32_t)c->table_n,
                       c->comb_on ? c->comb : nullptr, c->comb_ok, seed,
-                      nonce, b->S, Sh, b->rP, b->status);
+                      nonce, b->S, Sh, b->rP, b->status, b->valid);  // valid: free until the tail's fallback writes it
     HIP_CHECK(c, hipEventRecord(e[1], sa));
     // A segment of a few chunks (a lone gossip call) skips the combined check (seg_direct): each
     // chunk goes straight to its own one-wave check, which is the shorter dependency chain.

@@ -233,6 +233,47 @@ k_sm_prepare_split(uint32_t base, uint32_t n, const uint32_t* __restrict__ idx, 
   }
 }
 
+// After k_sm_prep_roles (k_sm_coop.hip): per set the verdict -- pubkey slot, decode code, the
+// cooperative subgroup check (sub_ok) -- merged as k_sm_prepare merges it (a bad signature outranks a
+// bad key), the set's r pk / r sig (Ph / Sh at its own index) kept only when it is valid, then the
+// 8-set segmented scan with the sums written at the run heads (in place: every lane reads its own
+// terms before the scan).
+__global__ void GBV_KERNEL_ATTR k_sm_prep_scan(uint32_t base, uint32_t n, const uint32_t* __restrict__ idx,
+                                               const uint32_t* __restrict__ set_grp, const uint8_t* __restrict__ table_ok,
+                                               uint32_t table_n, const uint8_t* __restrict__ sub_ok, uint8_t* __restrict__ status,
+                                               G2J* __restrict__ Sh, G1J* __restrict__ Ph) {
+  const unsigned lane = threadIdx.x;
+  const uint32_t t = blockIdx.x * 64 + lane;
+  const bool act = t < n;
+  const uint32_t i = base + t;
+  const uint32_t key = act ? set_grp[i] : 0xffffffffu;
+  G2J rs = jac_infinity<Fp2>();
+  G1J rp = jac_infinity<Fp>();
+  if (act) {
+    const uint32_t k = idx[i];
+    uint8_t st = (k >= table_n || !table_ok[k]) ? SET_BAD_PK : SET_OK;
+    if (status[i] != PT_OK || !sub_ok[i]) st = SET_BAD_SIG;
+    status[i] = st;
+    if (st == SET_OK) {
+      rs = Sh[i];
+      rp = Ph[i];
+    }
+  }
+  for (unsigned d = 1; d < SCAN_W; d <<= 1) {
+    G1J po = shfl_down_jac(rp, d);
+    uint32_t ko = __shfl_down(key, d, 64);
+    bool take = (lane & (SCAN_W - 1)) + d < SCAN_W && ko == key;
+    G2J so = shfl_down_jac(rs, d);
+    if (take) rs = g2_add(rs, so);
+    if (take) rp = jac_add(rp, po);
+  }
+  uint32_t kprev = __shfl_up(key, 1, 64);
+  if (act && ((lane & (SCAN_W - 1)) == 0 || kprev != key)) {
+    Sh[i] = rs;
+    Ph[i] = rp;
+  }
+}
+
 // The G2 half of k_sm_prepare for a segment whose fast check used the bucket MSM (k_msm.hip) and
 // FAILED (or holds a chunk bound for the per-set path): the failure path needs the per-set
 // r_i sig_i group sums (Sh) and the chunk sums S_g after all.  Same r_i (prf_scalar of the same seed/nonce/index), same 8-lane scan, so Sh/S_g are
@@ -562,7 +603,7 @@ void launch_sm_fb_sets(LaunchCfg c, const uint32_t* set_list, const uint32_t* n_
 
 void launch_sm_prepare(LaunchCfg c, uint32_t base, uint32_t n, const uint32_t* idx, const uint8_t* sig96, const uint32_t* set_grp,
                        const G1A* table, const uint8_t* table_ok, uint32_t table_n, const uint4* comb, const uint8_t* comb_ok,
-                       const Seed& seed, uint32_t nonce, G2A* S_out, G2J* Sh, G1J* Ph, uint8_t* status) {
+                       const Seed& seed, uint32_t nonce, G2A* S_out, G2J* Sh, G1J* Ph, uint8_t* status, uint8_t* scratch8) {
   // Sh == nullptr: G1 terms only (the segment's G2 sum comes from the bucket MSM); comb == nullptr:
   // no comb tables (GBV_COMB=0 or not built), the ladder forms r pk
   static const uint32_t split_max = getenv("GBV_PREPARE_SPLIT_MAX") ? (uint32_t)atoi(getenv("GBV_PREPARE_SPLIT_MAX")) : 2048;
@@ -572,7 +613,15 @@ void launch_sm_prepare(LaunchCfg c, uint32_t base, uint32_t n, const uint32_t* i
   // and, for the G1-only form, the subgroup check apart from r pk (GBV_SUB_SPLIT=0: one kernel, A/B)
   static const bool sub_split = getenv("GBV_SUB_SPLIT") ? atoi(getenv("GBV_SUB_SPLIT")) != 0 : GBV_SUB_SPLIT_DEFAULT != 0;
   const dim3 grid((n + 63) / 64);
-  if (Sh && n <= split_max) {  // latency: two waves per 64 sets
+  // latency, few sets: decode, then the subgroup checks one wave per set beside the randomisation,
+  // then the verdicts and the scan (GBV_PREP_COOP=0: k_sm_prepare_split's two waves per 64 sets)
+  static const bool prep_coop = !(getenv("GBV_PREP_COOP") && atoi(getenv("GBV_PREP_COOP")) == 0);
+  if (Sh && n <= split_max && prep_coop && scratch8) {
+    launch_sig_decode(c.stream, base, n, sig96, S_out, status);
+    launch_sm_prep_roles(c.stream, base, n, idx, table, table_ok, table_n, comb, comb_ok, seed, nonce, S_out, status, scratch8, Sh, Ph);
+    hipLaunchKernelGGL(k_sm_prep_scan, grid, dim3(64), 0, c.stream, base, n, idx, set_grp, table_ok, table_n, scratch8, status, Sh, Ph);
+    debug_sync(c.stream, "k_sm_prep_scan");
+  } else if (Sh && n <= split_max) {  // latency: two waves per 64 sets
     hipLaunchKernelGGL(k_sm_prepare_split, dim3((n + 63) / 64), dim3(128), 0, c.stream, base, n, idx, sig96, set_grp, table, table_ok, table_n,
                        comb, comb_ok, seed, nonce, S_out, Sh, Ph, status);
   } else if (dec_split && !Sh && sub_split) {  // decode, subgroup check, r pk + scan

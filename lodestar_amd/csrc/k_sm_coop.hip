@@ -324,6 +324,67 @@ void launch_hash_clear_coop(hipStream_t s, uint32_t n, const G2J* Qpre, G2A* H) 
   debug_sync(s, "k_hash_clear_coop");
 }
 
+// Latency form of the same-message prepare stage for few sets, after k_sig_decode (S, status = the
+// decode code): two block roles in one launch.  Blocks [0, n): ONE WAVE PER SET runs the G2
+// subgroup check psi(Q) == [x] Q on the cooperative point doublings (coop::mul_xabs_point, ~0.7 ms
+// against ~1.6 ms of dependent products on one lane) and writes the verdict to sub_ok.  Blocks
+// [n, n + ceil(n / 64)): one lane per set forms r pk and r sig (as k_sm_prepare_split's wave 1) into
+// Ph / Sh at the set's own index.  k_sm_prep_scan then merges the verdicts and runs the chunk scan.
+// The cooperative doublings are exact for points of the order-r subgroup; for a point with a
+// small-order component they either stay exact (and the psi test rejects it) or degenerate to
+// Z = 0, which the comparison also rejects -- a rejected point is the right answer either way.
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
+k_sm_prep_roles(uint32_t base, uint32_t n, const uint32_t* __restrict__ idx, const G1A* __restrict__ table,
+                const uint8_t* __restrict__ table_ok, uint32_t table_n, const uint4* __restrict__ comb, const uint8_t* __restrict__ comb_ok,
+                Seed seed, uint32_t nonce, const G2A* __restrict__ S, const uint8_t* __restrict__ status, uint8_t* __restrict__ sub_ok,
+                G2J* __restrict__ Sh, G1J* __restrict__ Ph) {
+  __shared__ coop::Slot ws[coop::MILLER_WS];
+  const unsigned lane = threadIdx.x;
+  if (blockIdx.x < n) {
+    const uint32_t i = base + blockIdx.x;
+    if (status[i] != PT_OK) {  // uniform per block
+      if (lane == 0) sub_ok[i] = 0;
+      return;
+    }
+    const G2A q = S[i];
+    coop::load_consts();
+    coop::mul_xabs_point(ws, q);  // [|x|] q at M_PAIR
+    if (lane == 0) sub_ok[i] = jac_eq_aff(jac_neg(coop::point_jac(ws)), g2_psi(q)) ? 1 : 0;
+    return;
+  }
+  const uint32_t t = (blockIdx.x - n) * 64 + lane;
+  if (t >= n) return;
+  const uint32_t i = base + t, k = idx[i];
+  G2J rs = jac_infinity<Fp2>();
+  G1J rp = jac_infinity<Fp>();
+  if (status[i] == PT_OK && k < table_n && table_ok[k]) {  // (discarded by k_sm_prep_scan when the subgroup check fails)
+    const G2A s = S[i];
+    const uint64_t r = prf_scalar(seed, i, nonce);
+    if (comb && comb_ok[k]) {
+      rp = comb_mul(comb + (size_t)k * (COMB_ENTRIES * COMB_U4), (uint32_t)r, (uint32_t)(r >> 32));
+      if (!randomize_g2(s, r, &rs)) {
+        rs = g2_mul_u64(s, r);
+        rp = g1_mul_u64(table[k], r);
+      }
+    } else {
+      const G1A pk = table[k];
+      if (!randomize_pair(pk, s, r, &rp, &rs)) {
+        rs = g2_mul_u64(s, r);
+        rp = g1_mul_u64(pk, r);
+      }
+    }
+  }
+  Sh[i] = rs;
+  Ph[i] = rp;
+}
+void launch_sm_prep_roles(hipStream_t s, uint32_t base, uint32_t n, const uint32_t* idx, const G1A* table, const uint8_t* table_ok,
+                          uint32_t table_n, const uint4* comb, const uint8_t* comb_ok, const Seed& seed, uint32_t nonce, const G2A* S,
+                          const uint8_t* status, uint8_t* sub_ok, G2J* Sh, G1J* Ph) {
+  hipLaunchKernelGGL(k_sm_prep_roles, dim3(n + (n + 63) / 64), dim3(64), 0, s, base, n, idx, table, table_ok, table_n, comb, comb_ok, seed,
+                     nonce, S, status, sub_ok, Sh, Ph);
+  debug_sync(s, "k_sm_prep_roles");
+}
+
 // e(P, Q) * e(-g1, S) == 1 by one wave (S = infinity drops the second pair).  Arguments must be
 // wave-uniform (the callers stage them in LDS).
 __device__ inline bool coop_pair_check(coop::Slot* ws, const G1A& P, const G2A& Q, bool s_inf, const G2A& S) {
