@@ -183,8 +183,18 @@ __device__ inline void ws_put(const Ws& w, uint32_t src, uint32_t idx, const Fp&
 #ifndef GBV_COOP_LAZY
 #define GBV_COOP_LAZY 1  // 0: modular adds throughout (A/B)
 #endif
-template <int N, bool CANON>
-GBV_HD Fp lin_eval(const Ws& w, const uint32_t* r, uint32_t umax, uint32_t nu, uint32_t nsc, const uint32_t* rg) {
+// unit term i of a record held in registers: resolved from the term word and the bindings
+struct RecLoad {
+  const Ws& w;
+  const uint32_t* r;
+  uint32_t nu;
+  GBV_HD Fp operator()(int i) const {
+    const uint32_t t = (uint32_t)i < nu ? r[i] : ZERO_TERM;
+    return term_load(w, t, (t >> 4) & 1);
+  }
+};
+template <int N, bool CANON, class Load>
+GBV_HD Fp lin_sum(const Load& load, const Ws& w, uint32_t umax, uint32_t nu, uint32_t nsc, const uint32_t* rg) {
   // groups of G terms: the G loads issue together, then their adds (G x 12 VGPRs in flight)
   constexpr int G = 4;
   Fp acc = fp_zero();
@@ -194,10 +204,7 @@ GBV_HD Fp lin_eval(const Ws& w, const uint32_t* r, uint32_t umax, uint32_t nu, u
 #pragma unroll
     for (int q = 0; q < G; ++q) {
       const int i = g + q;
-      if (i < N && (uint32_t)i < umax) {
-        const uint32_t t = (uint32_t)i < nu ? r[i] : ZERO_TERM;
-        v[q] = term_load(w, t, (t >> 4) & 1);
-      }
+      if (i < N && (uint32_t)i < umax) v[q] = load(i);
     }
 #pragma unroll
     for (int q = 0; q < G; ++q) {
@@ -220,6 +227,10 @@ GBV_HD Fp lin_eval(const Ws& w, const uint32_t* r, uint32_t umax, uint32_t nu, u
     acc = (nu == 0 && j == 0) ? s : fp_add(acc, s);
   }
   return acc;
+}
+template <int N, bool CANON>
+GBV_HD Fp lin_eval(const Ws& w, const uint32_t* r, uint32_t umax, uint32_t nu, uint32_t nsc, const uint32_t* rg) {
+  return lin_sum<N, CANON>(RecLoad{w, r, nu}, w, umax, nu, nsc, rg);
 }
 
 // Copy n (multiple of 4) words into registers with 16-byte loads: one memory latency per record.
@@ -337,6 +348,96 @@ __device__ inline void run(const Prog& P, const Ws& w) { run_ni(&P, w.b[0], w.b[
 // The interpreter inlined at one call site and specialised for its program (the program's counts
 // fold into the code; no call, no callee-saved spills): for the program a hot loop runs tens of times.
 __device__ __forceinline__ void run_inl(const Prog& P, const Ws& w) { run_body(&P, w.b[0], w.b[1], w.b[2], w.b[3]); }
+
+// A one-round program that a loop runs tens of times on the same operands (the exponentiation's
+// cyclotomic squarings): run_body resolves every unit term's source on every call (the binding
+// selects, a shift, an add: ~15 VALU per term).  pre_resolve does that once -- a lane's term
+// addresses (bytes in LDS, the sign folded in, terms past the lane's own count pointing at the zero
+// constant) and its destinations -- and run_pre loads the values straight from them.
+template <int NR> struct Pre {
+  uint32_t a[NR][OPW], b[NR][OPW], part[SUM_TERMS], out[SUM_TERMS];
+  uint32_t h[NR], hs[NR], hp, ho;  // record headers (term counts)
+  uint32_t dz[NR], dp, dout;       // destinations: products, partial sum, output
+};
+struct AddrLoad {
+  const uint32_t* a;
+  __device__ Fp operator()(int i) const {
+    Fp r;
+    r.v = ((const LFp*)(size_t)a[i])->v;
+    return r;
+  }
+};
+__device__ inline uint32_t term_addr(const Ws& w, uint32_t t) { return (ws_unit(w, t & 7, (t >> 8) & 0xFF) + ((t >> 4) & 1)) << 6; }
+template <int N> __device__ __forceinline__ void resolve_terms(uint32_t (&d)[N], const uint32_t* r, uint32_t umax, uint32_t nu, const Ws& w) {
+#pragma unroll
+  for (int i = 0; i < N; ++i)
+    if ((uint32_t)i < umax) d[i] = term_addr(w, (uint32_t)i < nu ? r[i] : ZERO_TERM);
+}
+__device__ inline void put_at(uint32_t addr, const Fp& a) {
+  LFp* q = (LFp*)(size_t)addr;
+  q[0].v = a.v;
+  q[1].v = fp_neg(a).v;
+}
+__device__ inline uint32_t nu_lo(uint32_t h) { return (h & 0xFF) + ((h >> 8) & 0xFF); }
+__device__ inline uint32_t nu_hi(uint32_t h) { return ((h >> 16) & 0xFF) + (h >> 24); }
+// NR = P.n_rounds (checked by the caller's program choice; the tables are fixed at build time)
+template <int NR> __device__ __forceinline__ Pre<NR> pre_resolve(const Prog& P, const Ws& w) {
+  Pre<NR> x;
+  const uint32_t lane = threadIdx.x & 63u;
+  uint32_t rec[PROD_WORDS], rs[SUM_WORDS];
+  const uint32_t pm = __builtin_amdgcn_readfirstlane(P.pmax), om = __builtin_amdgcn_readfirstlane(P.omax);
+#pragma unroll
+  for (int r = 0; r < NR; ++r) {
+    const uint32_t p0 = r ? P.round_end[r - 1] : 0u, k = p0 + lane;
+    const uint32_t am = __builtin_amdgcn_readfirstlane(P.amax[r]), bm = __builtin_amdgcn_readfirstlane(P.bmax[r]);
+    if (k < P.round_end[r]) {
+      load_words(rec, P.prods + PROD_WORDS * k);
+      x.h[r] = rec[0];
+      x.hs[r] = rec[1 + 2 * OPW];
+      resolve_terms(x.a[r], rec + 1, am, nu_lo(x.h[r]), w);
+      resolve_terms(x.b[r], rec + 1 + OPW, bm, nu_hi(x.h[r]), w);
+      x.dz[r] = ws_unit(w, SRC_Z, k) << 6;
+    }
+  }
+  if (lane < P.n_part) {
+    load_words(rs, P.parts + SUM_WORDS * lane);
+    x.hp = rs[0];
+    resolve_terms(x.part, rs + 1, pm, nu_lo(x.hp), w);
+    x.dp = ws_unit(w, SRC_Z, P.round_end[NR - 1] + lane) << 6;
+  }
+  if (lane < P.n_out) {
+    load_words(rs, P.outs + SUM_WORDS * lane);
+    x.ho = rs[0];
+    resolve_terms(x.out, rs + 1, om, nu_lo(x.ho), w);
+    x.dout = ws_unit(w, P.out_dst[lane], P.out_idx[lane]) << 6;
+  }
+  return x;
+}
+// the same phases as run_body (scaled terms still read from the record)
+template <int NR> __device__ __forceinline__ void run_pre(const Prog& P, const Ws& w, const Pre<NR>& x) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t pm = __builtin_amdgcn_readfirstlane(P.pmax), om = __builtin_amdgcn_readfirstlane(P.omax);
+#pragma unroll
+  for (int r = 0; r < NR; ++r) {
+    const uint32_t p0 = r ? P.round_end[r - 1] : 0u, k = p0 + lane;
+    const uint32_t am = __builtin_amdgcn_readfirstlane(P.amax[r]), bm = __builtin_amdgcn_readfirstlane(P.bmax[r]);
+    if (k < P.round_end[r]) {
+      const uint32_t* rg = P.prods + PROD_WORDS * k;
+      const Fp a = lin_sum<OPW, false>(AddrLoad{x.a[r]}, w, am, nu_lo(x.h[r]), x.hs[r] & 0xFF, rg + 1);
+      const Fp b = lin_sum<OPW, false>(AddrLoad{x.b[r]}, w, bm, nu_hi(x.h[r]), (x.hs[r] >> 8) & 0xFF, rg + 1 + OPW);
+      put_at(x.dz[r], fp_mul_inl(a, b));
+    }
+    barrier();
+  }
+  if (lane < P.n_part)
+    put_at(x.dp, lin_sum<SUM_TERMS, true>(AddrLoad{x.part}, w, pm, nu_lo(x.hp), (x.hp >> 16) & 0xFF, P.parts + SUM_WORDS * lane + 1));
+  if (P.n_part) barrier();
+  Fp o;
+  if (lane < P.n_out) o = lin_sum<SUM_TERMS, true>(AddrLoad{x.out}, w, om, nu_lo(x.ho), (x.ho >> 16) & 0xFF, P.outs + SUM_WORDS * lane + 1);
+  barrier();
+  if (lane < P.n_out) put_at(x.dout, o);
+  barrier();
+}
 #define COOP_LANES(l) for (unsigned l = threadIdx.x & 63u; l == (threadIdx.x & 63u); l = ~0u)
 #define COOP_LANE0 if ((threadIdx.x & 63u) == 0)
 #endif
@@ -447,8 +548,19 @@ GBV_HD void miller_load_pair(Slot* mem, int j, const G1A& P, const G2A& Q) {
 }
 
 // F = prod_j f_{|x|, Q_j}(P_j), conjugated (x < 0).  Pairs must be loaded first.
+#ifndef GBV_COOP_PRE_LINE
+#define GBV_COOP_PRE_LINE 0  // the Miller loop's line multiplications through run_pre as well (A/B: no gain)
+#endif
+#ifndef GBV_COOP_PRE_PT
+#define GBV_COOP_PRE_PT 0  // and the [|x|] doublings, subgroup checks and cofactor clearing (A/B: no gain)
+#endif
 GBV_HD void miller_loop(Slot* mem, int npairs) {
   set_one12(mem + M_F);
+#if !defined(GBV_HOST_TEST)
+  const Ws wl = ws3(mem, M_Z, M_F, M_L, M_F);
+  Pre<1> xl;
+  if (GBV_COOP_PRE_LINE) xl = pre_resolve<1>(FP12_MUL_LINE, wl);
+#endif
   for (int i = 62; i >= 0; --i) {
     for (int j = 0; j < npairs; ++j) {
       uint16_t t = M_PAIR + 12 * j;
@@ -456,6 +568,12 @@ GBV_HD void miller_loop(Slot* mem, int npairs) {
         run_hot(MILLER_SQR_DBL, make_ws(mem, M_Z, M_F, t, (uint16_t)(t + 10), M_F, t, M_L));
       else
         run(G2_DBL_STEP, make_ws(mem, M_Z, t, (uint16_t)(t + 10), t, M_L));
+#if !defined(GBV_HOST_TEST)
+      if (GBV_COOP_PRE_LINE) {
+        run_pre(FP12_MUL_LINE, wl, xl);
+        continue;
+      }
+#endif
       run_hot(FP12_MUL_LINE, ws3(mem, M_Z, M_F, M_L, M_F));
     }
     if ((X_ABS >> i) & 1ull) {
@@ -477,6 +595,17 @@ GBV_HD void miller_loop(Slot* mem, int npairs) {
 GBV_HD void mul_xabs_point(Slot* mem, const G2A& Q) {
   miller_load_pair(mem, 0, G1A{fp_zero(), fp_zero()}, Q);
   const uint16_t t = M_PAIR;
+#if !defined(GBV_HOST_TEST)
+  if (GBV_COOP_PRE_PT) {
+    const Ws w = make_ws(mem, M_Z, t, t);
+    const Pre<2> x = pre_resolve<2>(G2_DBL_PT, w);
+    for (int i = 62; i >= 0; --i) {
+      run_pre(G2_DBL_PT, w, x);
+      if ((X_ABS >> i) & 1ull) run(G2_ADD_STEP, make_ws(mem, M_Z, t, (uint16_t)(t + 6), (uint16_t)(t + 10), t, M_L));
+    }
+    return;
+  }
+#endif
   for (int i = 62; i >= 0; --i) {
     run_hot(G2_DBL_PT, make_ws(mem, M_Z, t, t));  // the doubling without its line: 19 products, 6 outputs
     if ((X_ABS >> i) & 1ull) run(G2_ADD_STEP, make_ws(mem, M_Z, t, (uint16_t)(t + 6), (uint16_t)(t + 10), t, M_L));
@@ -496,8 +625,23 @@ constexpr uint16_t E_F = 0, E_INV = 12, E_T = 24, E_A = 36, E_B = 48, E_C = 60, 
 constexpr int FINAL_EXP_WS = E_Z + ZSLOTS;
 
 // r = a^x (a in the cyclotomic subgroup)
+#ifndef GBV_COOP_PRE
+#define GBV_COOP_PRE 1  // the 63 squarings of an exponentiation with their term addresses resolved once
+#endif
 GBV_HD void exp_x(Slot* mem, uint16_t a, uint16_t r) {
   copy(mem + r, mem + a, 12);
+#if !defined(GBV_HOST_TEST)
+  if (GBV_COOP_PRE) {
+    const Ws w = ws2(mem, E_Z, r, r);
+    const Pre<1> x = pre_resolve<1>(FP12_CYC_SQR, w);
+    for (int i = 62; i >= 0; --i) {
+      run_pre(FP12_CYC_SQR, w, x);
+      if ((X_ABS >> i) & 1ull) mul12(mem, E_Z, r, a, r);
+    }
+    conj12(mem + r);
+    return;
+  }
+#endif
   for (int i = 62; i >= 0; --i) {
     cyc_sqr12(mem, E_Z, r, r);
     if ((X_ABS >> i) & 1ull) mul12(mem, E_Z, r, a, r);
