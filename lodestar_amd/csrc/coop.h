@@ -611,6 +611,46 @@ GBV_HD void mul_xabs_point(Slot* mem, const G2A& Q) {
     if ((X_ABS >> i) & 1ull) run(G2_ADD_STEP, make_ws(mem, M_Z, t, (uint16_t)(t + 6), (uint16_t)(t + 10), t, M_L));
   }
 }
+// [a - b x^2] Q for the batch digits (sa, sb) -- the scalar of curve.h's jac_mul_2d_signed, by its
+// signed joint ladder R = sum_i 2^i (+-Q +-E), E = -psi^2(Q) = [-x^2] Q -- on the cooperative point
+// steps, with the two digits of a step added one after the other (+-Q, then +-E: affine points
+// as they are, so no ladder table and no inversion): 31 doublings, 63 mixed additions.  T ends at
+// mem + M_PAIR like mul_xabs_point's.  For Q in the order-r subgroup no addition meets T = +-(its
+// operand): before a Q digit T = [2a + 2b lambda] Q with (a, b) != 0 -- never [+-1] Q -- and before an
+// E digit T = [odd + even lambda] Q, never +-E (|a|, |b| < 2^33 and the lattice of (u, v) with
+// u = v lambda mod r has no vector that short).  A point outside the subgroup gets a wrong multiple,
+// and the subgroup check beside it rejects that set.  Workspace: Q at M_PAIR + 6, -Q, E, -E at
+// M_PAIR + 12 / 16 / 20 (pair 1's slots).
+GBV_HD void mul_2d_point(Slot* mem, const G2A& Q, const G2A& E, uint32_t sa, uint32_t sb) {
+  const uint16_t t = M_PAIR, QP = t + 6, QN = t + 12, EP = t + 16, EN = t + 20;
+  LSlot* b = GBV_LDS(mem + M_PAIR);
+  COOP_LANES(l) {
+    if (l < 24) {
+      const G2A& p = (l >= 16) ? E : Q;
+      Fp v;
+      if (l == 4)
+        v = FP_ONE;
+      else if (l == 5 || l == 10 || l == 11)
+        v = fp_zero();
+      else {
+        const uint32_t c = l < 4 ? l : l < 10 ? l - 6 : (l & 3);  // x.c0 x.c1 y.c0 y.c1
+        v = c == 0 ? p.x.c0 : c == 1 ? p.x.c1 : c == 2 ? p.y.c0 : p.y.c1;
+        const bool neg = c >= 2 && ((l < 4 && !((sa >> 31) & 1u)) || (l >= 12 && l < 16) || l >= 20);
+        if (neg) v = fp_neg(v);
+      }
+      put(b + l, v);
+    }
+  }
+  barrier();
+  // T = +-Q (digit 31 of sa) is loaded; its E digit, then the 31 lower steps
+  run(G2_ADD_STEP, make_ws(mem, M_Z, t, ((sb >> 31) & 1u) ? EP : EN, (uint16_t)(t + 10), t, M_L));
+  for (int i = 30; i >= 0; --i) {
+    run_hot(G2_DBL_PT, make_ws(mem, M_Z, t, t));
+    run(G2_ADD_STEP, make_ws(mem, M_Z, t, ((sa >> i) & 1u) ? QP : QN, (uint16_t)(t + 10), t, M_L));
+    run(G2_ADD_STEP, make_ws(mem, M_Z, t, ((sb >> i) & 1u) ? EP : EN, (uint16_t)(t + 10), t, M_L));
+  }
+}
+
 // the point left by mul_xabs_point as a Jacobian point (X Z, Y Z^2, Z); one lane
 GBV_HD G2J point_jac(const Slot* mem) {
   const LSlot* b = GBV_LDS(mem + M_PAIR);

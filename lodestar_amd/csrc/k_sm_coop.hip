@@ -333,13 +333,31 @@ void launch_hash_clear_coop(hipStream_t s, uint32_t n, const G2J* Qpre, G2A* H) 
 // The cooperative doublings are exact for points of the order-r subgroup; for a point with a
 // small-order component they either stay exact (and the psi test rejects it) or degenerate to
 // Z = 0, which the comparison also rejects -- a rejected point is the right answer either way.
+// With coop_rand (n <= GBV_PREP_COOP_RAND, default 512 sets), blocks [n, 2n) form r sig the same
+// way (coop::mul_2d_point, one wave per set: ~1.5 ms against ~2.6 ms for the lane's ladder, which
+// was this launch's longest role) and the lanes of the last role form r pk alone (comb or 2-D
+// ladder: the same scalar a - b x^2).
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
 k_sm_prep_roles(uint32_t base, uint32_t n, const uint32_t* __restrict__ idx, const G1A* __restrict__ table,
                 const uint8_t* __restrict__ table_ok, uint32_t table_n, const uint4* __restrict__ comb, const uint8_t* __restrict__ comb_ok,
                 Seed seed, uint32_t nonce, const G2A* __restrict__ S, const uint8_t* __restrict__ status, uint8_t* __restrict__ sub_ok,
-                G2J* __restrict__ Sh, G1J* __restrict__ Ph) {
+                G2J* __restrict__ Sh, G1J* __restrict__ Ph, int coop_rand) {
   __shared__ coop::Slot ws[coop::MILLER_WS];
   const unsigned lane = threadIdx.x;
+  const uint32_t nr = coop_rand ? n : 0u;
+  if (blockIdx.x >= n && blockIdx.x < n + nr) {  // r sig, one wave per set
+    const uint32_t i = base + blockIdx.x - n, k = idx[i];
+    if (!(status[i] == PT_OK && k < table_n && table_ok[k])) {  // uniform per block
+      if (lane == 0) Sh[i] = jac_infinity<Fp2>();
+      return;
+    }
+    const G2A q = S[i];
+    const uint64_t r = prf_scalar(seed, i, nonce);
+    coop::load_consts();
+    coop::mul_2d_point(ws, q, g2_neg_psi2(q), (uint32_t)r, (uint32_t)(r >> 32));
+    if (lane == 0) Sh[i] = coop::point_jac(ws);
+    return;
+  }
   if (blockIdx.x < n) {
     const uint32_t i = base + blockIdx.x;
     if (status[i] != PT_OK) {  // uniform per block
@@ -352,11 +370,23 @@ k_sm_prep_roles(uint32_t base, uint32_t n, const uint32_t* __restrict__ idx, con
     if (lane == 0) sub_ok[i] = jac_eq_aff(jac_neg(coop::point_jac(ws)), g2_psi(q)) ? 1 : 0;
     return;
   }
-  const uint32_t t = (blockIdx.x - n) * 64 + lane;
+  const uint32_t t = (blockIdx.x - n - nr) * 64 + lane;
   if (t >= n) return;
   const uint32_t i = base + t, k = idx[i];
   G2J rs = jac_infinity<Fp2>();
   G1J rp = jac_infinity<Fp>();
+  if (coop_rand) {
+    if (status[i] == PT_OK && k < table_n && table_ok[k]) {
+      const uint64_t r = prf_scalar(seed, i, nonce);
+      // a table key is in the subgroup, so the 2-D ladder cannot fail for it
+      if (comb && comb_ok[k])
+        rp = comb_mul(comb + (size_t)k * (COMB_ENTRIES * COMB_U4), (uint32_t)r, (uint32_t)(r >> 32));
+      else if (!randomize_g1(table[k], r, &rp))
+        rp = jac_infinity<Fp>();
+    }
+    Ph[i] = rp;
+    return;
+  }
   if (status[i] == PT_OK && k < table_n && table_ok[k]) {  // (discarded by k_sm_prep_scan when the subgroup check fails)
     const G2A s = S[i];
     const uint64_t r = prf_scalar(seed, i, nonce);
@@ -380,8 +410,11 @@ k_sm_prep_roles(uint32_t base, uint32_t n, const uint32_t* __restrict__ idx, con
 void launch_sm_prep_roles(hipStream_t s, uint32_t base, uint32_t n, const uint32_t* idx, const G1A* table, const uint8_t* table_ok,
                           uint32_t table_n, const uint4* comb, const uint8_t* comb_ok, const Seed& seed, uint32_t nonce, const G2A* S,
                           const uint8_t* status, uint8_t* sub_ok, G2J* Sh, G1J* Ph) {
-  hipLaunchKernelGGL(k_sm_prep_roles, dim3(n + (n + 63) / 64), dim3(64), 0, s, base, n, idx, table, table_ok, table_n, comb, comb_ok, seed,
-                     nonce, S, status, sub_ok, Sh, Ph);
+  // a wave per set costs ~25x the CU time of a lane per set: worth it while the waves fit the chip at once
+  static const uint32_t coop_rand_max = getenv("GBV_PREP_COOP_RAND") ? (uint32_t)atoi(getenv("GBV_PREP_COOP_RAND")) : 512;
+  const int coop_rand = n <= coop_rand_max;
+  hipLaunchKernelGGL(k_sm_prep_roles, dim3(n + (coop_rand ? n : 0) + (n + 63) / 64), dim3(64), 0, s, base, n, idx, table, table_ok, table_n,
+                     comb, comb_ok, seed, nonce, S, status, sub_ok, Sh, Ph, coop_rand);
   debug_sync(s, "k_sm_prep_roles");
 }
 

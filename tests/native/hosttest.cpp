@@ -158,6 +158,18 @@ void ht_coop_clear_cofactor(uint8_t* out, const uint8_t* xy) {
   store_fp2(out, o.x);
   store_fp2(out + 96, o.y);
 }
+// [r] Q for the same batch scalar by the cooperative ladder (coop::mul_2d_point, as
+// k_sm_prep_roles runs it); out: affine
+void ht_coop_mul_2d(uint8_t* out, const uint8_t* q192, uint64_t r64) {
+  coop::load_consts();
+  std::vector<coop::Slot> mem(coop::MILLER_WS);
+  const G2A Q{load_fp2(q192), load_fp2(q192 + 96)};
+  coop::mul_2d_point(mem.data(), Q, g2_neg_psi2(Q), (uint32_t)r64, (uint32_t)(r64 >> 32));
+  G2A o;
+  jac_to_aff(o, coop::point_jac(mem.data()));
+  store_fp2(out, o.x);
+  store_fp2(out + 96, o.y);
+}
 // [r] P, [r] Q for the batch scalar r = a - b x^2 of the 64-bit digit word r64 (curve.h)
 int ht_randomize(uint8_t* outp, uint8_t* outq, const uint8_t* p96, const uint8_t* q192, uint64_t r64) {
   G1A P{load_mont(p96), load_mont(p96 + 48)};

@@ -259,6 +259,17 @@ def test_randomize_pair(lib, r64):
 
 
 
+@pytest.mark.parametrize("r64", [0, 0xFFFFFFFFFFFFFFFF, 0x0123456789ABCDEF, 0x8000000000000001, 0x7FFFFFFF80000000])
+def test_coop_mul_2d(lib, r64):
+    """The cooperative signed ladder (coop.h mul_2d_point: +-Q then +-E per step, the lone-call
+    prepare's r sig) gives [a - b x^2] Q, the scalar of randomize_pair."""
+    Q = o.g2_mul(o.G2_GEN, 0x5678)
+    lib.ht_coop_mul_2d.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint64]
+    out = buf(192)
+    lib.ht_coop_mul_2d(out, fp2b(Q[0]) + fp2b(Q[1]), r64)
+    assert (b2fp2(out.raw[:96]), b2fp2(out.raw[96:])) == o.g2_mul(Q, _digits_scalar(r64))
+
+
 @pytest.mark.parametrize("r64", [0, 0xFFFFFFFFFFFFFFFF, 0x0123456789ABCDEF, 0xDEADBEEF00C0FFEE, 0x8000000000000001])
 def test_comb_mul(lib, r64):
     """Per-validator comb table (curve.h comb_bases / comb_entry_jac / comb_mul): [a - b x^2] P
