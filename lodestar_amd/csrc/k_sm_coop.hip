@@ -418,6 +418,45 @@ void launch_sm_prep_roles(hipStream_t s, uint32_t base, uint32_t n, const uint32
   debug_sync(s, "k_sm_prep_roles");
 }
 
+// k_vs_sig_pre (k_vs.hip) for few sets: the same two roles with a wave per set and role -- blocks
+// [0, n) decode signature i and run the subgroup check on the cooperative point doublings (as
+// k_sm_prep_roles), blocks [n, 2n) decode it and form r_i sig_i by coop::mul_2d_point (the same
+// scalar as randomize_g2).  Every lane decodes (the same bytes: a uniform verdict), so the whole
+// wave takes the same branches.
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
+k_vs_sig_pre_coop(uint32_t n, const uint8_t* __restrict__ sig, uint32_t sig_stride, const uint32_t* __restrict__ sig_len, Seed seed,
+                  uint32_t nonce, G2J* __restrict__ rS_out, uint8_t* __restrict__ status, uint8_t* __restrict__ sig_st) {
+  __shared__ coop::Slot ws[coop::MILLER_WS];
+  const bool rand = blockIdx.x >= n;
+  const uint32_t i = rand ? blockIdx.x - n : blockIdx.x;
+  G2A s;
+  const bool ok = g2_decode(s, sig + (size_t)sig_stride * i, sig_len[i]) == PT_OK;
+  if (!rand) {
+    bool in = false;
+    if (ok) {
+      coop::load_consts();
+      coop::mul_xabs_point(ws, s);
+      in = jac_eq_aff(jac_neg(coop::point_jac(ws)), g2_psi(s));
+    }
+    if (threadIdx.x == 0) {
+      const uint8_t st = in ? SET_OK : SET_BAD_SIG;
+      status[i] = st;
+      sig_st[i] = st;
+    }
+    return;
+  }
+  if (!ok) return;
+  const uint64_t r = prf_scalar(seed, i, nonce);
+  coop::load_consts();
+  coop::mul_2d_point(ws, s, g2_neg_psi2(s), (uint32_t)r, (uint32_t)(r >> 32));
+  if (threadIdx.x == 0) rS_out[i] = coop::point_jac(ws);
+}
+void launch_vs_sig_pre_coop(hipStream_t s, uint32_t n, const uint8_t* sig, uint32_t sig_stride, const uint32_t* sig_len, const Seed& seed,
+                            uint32_t nonce, G2J* rS, uint8_t* status, uint8_t* sig_st) {
+  hipLaunchKernelGGL(k_vs_sig_pre_coop, dim3(2 * n), dim3(64), 0, s, n, sig, sig_stride, sig_len, seed, nonce, rS, status, sig_st);
+  debug_sync(s, "k_vs_sig_pre_coop");
+}
+
 // e(P, Q) * e(-g1, S) == 1 by one wave (S = infinity drops the second pair).  Arguments must be
 // wave-uniform (the callers stage them in LDS).
 __device__ inline bool coop_pair_check(coop::Slot* ws, const G1A& P, const G2A& Q, bool s_inf, const G2A& S) {
