@@ -182,6 +182,25 @@ def test_same_message_one_percent_invalid(world, monkeypatch, mode):
     assert res == expected
 
 
+@pytest.mark.parametrize("n_sets", [300, 700])
+def test_same_message_small_pass_roles(world, n_sets):
+    """One small pass (one segment) through the latency prepare (k_sm_prep_roles): r sig on the
+    cooperative ladder (<= 512 sets) or on the lanes (700) -- or per segment by the MSM while an
+    earlier test's failure keeps its cooldown on.  All-valid must pass the segment check outright
+    (the G1 and G2 scalars agree), and injected invalid sets come back exactly."""
+    v, sks, _ = world
+    off, idx, grp, sigs, msgs = _workload(v, sks, n_sets, 15 + n_sets)
+    assert all(_run_staged(v, off, idx, sigs, msgs))
+    assert v.last_stats() == (0, 0)
+    n = len(sigs)
+    bad = {3: sigs[(3 + 200) % n], n - 2: bytes([0xC0]) + bytes(95)}  # another call's signature; infinity
+    assert grp[3] != grp[(3 + 200) % n]
+    sigs = list(sigs)
+    for i, s in bad.items():
+        sigs[i] = s
+    assert _run_staged(v, off, idx, sigs, msgs) == [i not in bad for i in range(n)]
+
+
 def test_same_message_spot_check_oracle(world):
     """A few GPU-signed sets re-verified by the CPU oracle (pins util_sign beyond K1)."""
     from oracle import bls_oracle as O
