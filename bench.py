@@ -64,9 +64,6 @@ W_PREPARE_FME_MSM_COMB = FME_SIG_VALIDATE + FME_COMB_G1 + FME_G1_SCAN
 W_PREPARE_FME = FME_SIG_VALIDATE + FME_RANDOMIZE_PAIR + 177
 # k_vs_hash_sig: both block roles per set
 W_VS_HASH_SIG = FME_HASH_TO_G2 + FME_SIG_VALIDATE + FME_RANDOMIZE_PAIR_JAC
-# SURVEY.md 8(d)'s algorithm-independent counts for the same-message per-set work (decompress 1.8k +
-# subgroup 1.25k + r*pk 0.8k), reported beside ours
-W_SURVEY_SAME_MESSAGE = 1800 + 1250 + 800
 # Integer VALU peak: v_mad_u64_u32 measured at 37.0 T lane-ops/s on MI355X
 # (tools/ubench_int.hip, profiles/r01_ubench_int.txt); theoretical 256 CU x 4 SIMD x 16 lanes x 2.4 GHz = 39.3 T.
 PEAK_MAC_PER_S = 37.0e12
@@ -596,7 +593,7 @@ def api_stream_rate(v, call_off, idx, sigs, msgs, n_sets=1 << 20):
     sig_mv = memoryview(sigs)
     reqs = [(PackedSameMessageSets(idx[call_off[g]:call_off[g + 1]], sig_mv[96 * int(call_off[g]):96 * int(call_off[g + 1])]),
              msgs[32 * g:32 * g + 32]) for g in range(k)]
-    call = v.verify_signature_sets_same_message
+    call = v.submit_signature_sets_same_message  # the IBlsVerifier method minus its coroutine frame
 
     async def go():
         res = await asyncio.gather(*[call(s, m) for s, m in reqs])
@@ -817,8 +814,7 @@ def main():
                 "achieved": round(achieved, 4), "peak": peak,
                 "unit": "T u32-MAC/s", "frac": round(achieved / peak, 5),
                 "traffic": round(traffic) if traffic is not None else None, "pmc": pmc,
-                "work_per_unit_fme": w_fme, "work_per_unit_fme_survey": W_SURVEY_SAME_MESSAGE, "comb_tables": comb,
-                "frac_at_survey_work": round(achieved / peak * W_SURVEY_SAME_MESSAGE / w_fme, 5),
+                "work_per_unit_fme": w_fme, "comb_tables": comb,
                 "units_per_launch": round(units_per_launch, 1),
                 "avg_launch_ms": round(float(avg_launch_ms[1]), 3),
                 "kernel_ms_per_step": {k: round(float(x), 3) for k, x in zip(KERNELS, kms)},

@@ -89,6 +89,13 @@ size_t gbv_pubkeys_count(gbv_ctx* ctx);
  * GBV_COMB=0 in the environment at gbv_init, or a failed allocation, selects the ladder; results are
  * identical either way).  No reference counterpart: an accelerator of index2pubkey. */
 int gbv_comb_enabled(gbv_ctx* ctx);
+/* Change one of the context's pipeline settings, which gbv_init reads once from the environment
+ * (GBV_MSM_MIN, GBV_MSM_COOLDOWN, GBV_SEGMENTS): "msm_min" (segments of at least this many sets
+ * form their G2 sum with the bucket MSM; 0 = never), "msm_cooldown" (submits without the MSM after
+ * a failing MSM segment), "segments" (pipeline segments per same-message batch).  Results are
+ * identical for every value; tests use it to reach each pipeline form on small batches.  No
+ * reference counterpart.  GBV_E_ARG for an unknown name. */
+int gbv_tune(gbv_ctx* ctx, const char* name, uint32_t value);
 
 /* IBlsVerifier.verifySignatureSets (interface.ts:47; multithread/index.ts:157-207).
  * The sets are split with chunkifyMaximizeChunkSize(sets, 128) (multithread/utils.ts:4-18) and

@@ -548,19 +548,8 @@ GBV_HD void miller_load_pair(Slot* mem, int j, const G1A& P, const G2A& Q) {
 }
 
 // F = prod_j f_{|x|, Q_j}(P_j), conjugated (x < 0).  Pairs must be loaded first.
-#ifndef GBV_COOP_PRE_LINE
-#define GBV_COOP_PRE_LINE 0  // the Miller loop's line multiplications through run_pre as well (A/B: no gain)
-#endif
-#ifndef GBV_COOP_PRE_PT
-#define GBV_COOP_PRE_PT 0  // and the [|x|] doublings, subgroup checks and cofactor clearing (A/B: no gain)
-#endif
 GBV_HD void miller_loop(Slot* mem, int npairs) {
   set_one12(mem + M_F);
-#if !defined(GBV_HOST_TEST)
-  const Ws wl = ws3(mem, M_Z, M_F, M_L, M_F);
-  Pre<1> xl;
-  if (GBV_COOP_PRE_LINE) xl = pre_resolve<1>(FP12_MUL_LINE, wl);
-#endif
   for (int i = 62; i >= 0; --i) {
     for (int j = 0; j < npairs; ++j) {
       uint16_t t = M_PAIR + 12 * j;
@@ -568,12 +557,6 @@ GBV_HD void miller_loop(Slot* mem, int npairs) {
         run_hot(MILLER_SQR_DBL, make_ws(mem, M_Z, M_F, t, (uint16_t)(t + 10), M_F, t, M_L));
       else
         run(G2_DBL_STEP, make_ws(mem, M_Z, t, (uint16_t)(t + 10), t, M_L));
-#if !defined(GBV_HOST_TEST)
-      if (GBV_COOP_PRE_LINE) {
-        run_pre(FP12_MUL_LINE, wl, xl);
-        continue;
-      }
-#endif
       run_hot(FP12_MUL_LINE, ws3(mem, M_Z, M_F, M_L, M_F));
     }
     if ((X_ABS >> i) & 1ull) {
@@ -595,17 +578,6 @@ GBV_HD void miller_loop(Slot* mem, int npairs) {
 GBV_HD void mul_xabs_point(Slot* mem, const G2A& Q) {
   miller_load_pair(mem, 0, G1A{fp_zero(), fp_zero()}, Q);
   const uint16_t t = M_PAIR;
-#if !defined(GBV_HOST_TEST)
-  if (GBV_COOP_PRE_PT) {
-    const Ws w = make_ws(mem, M_Z, t, t);
-    const Pre<2> x = pre_resolve<2>(G2_DBL_PT, w);
-    for (int i = 62; i >= 0; --i) {
-      run_pre(G2_DBL_PT, w, x);
-      if ((X_ABS >> i) & 1ull) run(G2_ADD_STEP, make_ws(mem, M_Z, t, (uint16_t)(t + 6), (uint16_t)(t + 10), t, M_L));
-    }
-    return;
-  }
-#endif
   for (int i = 62; i >= 0; --i) {
     run_hot(G2_DBL_PT, make_ws(mem, M_Z, t, t));  // the doubling without its line: 19 products, 6 outputs
     if ((X_ABS >> i) & 1ull) run(G2_ADD_STEP, make_ws(mem, M_Z, t, (uint16_t)(t + 6), (uint16_t)(t + 10), t, M_L));

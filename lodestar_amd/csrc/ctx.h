@@ -9,6 +9,7 @@
 #include <sys/random.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -96,11 +97,10 @@ struct gbv_ctx {
   // queues (GPU_MAX_HW_QUEUES=4 leaves one for the runtime): no two streams share a queue.
   hipStream_t stream = nullptr, stream2 = nullptr, stream4 = nullptr;
   hipStream_t stream5 = nullptr;  // small verifySignatureSets passes: the signature half beside the aggregation
-  hipStream_t stream6 = nullptr;  // GBV_MSM_CUS > 0: the same-message chunk sums + bucket MSM on their own CUs
   gbv::G1A* table = nullptr;
   uint8_t* table_ok = nullptr;
   size_t table_cap = 0;
-  size_t table_n = 0;
+  std::atomic<size_t> table_n{0};  // read without the lock (gbv_pubkeys_count), written under it
   // per-slot comb tables for r pk (curve.h comb_mul; 128 affine entries = 12 KB per slot), built on
   // append / replicate; comb_on = false (GBV_COMB=0, or an allocation that failed) -> the ladder
   uint4* comb = nullptr;
@@ -113,6 +113,11 @@ struct gbv_ctx {
   // A failing MSM segment pays the per-set G2 terms after all (k_sm_redo_g2) on top of the MSM, so
   // after one the next MSM_COOLDOWN submits use the per-set ladders (invalid-dense streams, C5)
   uint32_t msm_cooldown = 0;
+  // Settings read once at gbv_init (GBV_MSM_MIN, GBV_MSM_COOLDOWN, GBV_SEGMENTS), changed only by
+  // gbv_tune: segments of at least msm_min sets form their G2 sum with the bucket MSM (k_msm.hip;
+  // 0 = never); a failing MSM segment starts a cooldown of msm_cooldown_len submits; a batch is cut
+  // into at most `segments` pipeline segments (tests use several on small batches)
+  uint32_t msm_min = 131072, msm_cooldown_len = 16, segments = 1;
   static constexpr int NK = 8;  // hash, prepare, chunk_reduce, miller, seg_check, group_pairing, fallback, msm
   float last_ms[NK] = {};
   int last_launches[NK] = {};
@@ -133,11 +138,15 @@ struct gbv_ctx {
   hipEvent_t ssz_ev[2] = {};
   float last_ssz_ms = 0.f;
   float last_vs_ms[4] = {};  // agg, hash+sig, miller, chunk check of the last vs batch
-  // Every entry point holds this while it touches the context (its scratch batches, streams, table,
-  // counters), so host threads may share a context: the Python verifier's worker threads and its
-  // event-loop thread, the addon's libuv pool.  Recursive: one-shot calls nest submit + wait.  The
-  // batch waits release it while they block on the device.
+  // Every entry point holds this while it touches the context (its streams, table, counters), so
+  // host threads may share a context: the Python verifier's worker threads and its event-loop
+  // thread, the addon's libuv pool.  Recursive: a fill nests inside a one-shot call.  No entry point
+  // holds it while it blocks on the device: the batch waits and the one-shot calls (which hold
+  // their scratch batch's own mutex instead) wait on an event without it.
   std::recursive_mutex mu;
+  // The one-shot calls' scratch batches, each owned by one call at a time.  Lock order: a scratch
+  // mutex first, then mu.
+  std::mutex sm_scratch_mu, vs_scratch_mu;
 };
 
 #define GBV_LOCK(c) std::lock_guard<std::recursive_mutex> gbv_lock_((c)->mu)

@@ -3,14 +3,6 @@
 // Scott's endomorphism subgroup tests, and 64-bit scalar multiplication.
 #pragma once
 #include "fp2.h"
-#include "f28_lazy.h"
-
-#ifndef GBV_LAZY_UNIFORM
-#define GBV_LAZY_UNIFORM 1
-#endif
-#ifndef GBV_LAZY_G2
-#define GBV_LAZY_G2 0  // 1: subgroup-check chain in lazy 28-bit limbs (f28_lazy.h; measured)
-#endif
 
 namespace gbv {
 
@@ -218,60 +210,6 @@ GBV_NI G1J g1_mul_u64(G1A q, uint64_t k) { G1J r = jac_mul_u64(q, k); return ret
 GBV_NI G2J g2_mul_u64(G2A q, uint64_t k) { G2J r = jac_mul_u64(q, k); return ret_copy(r); }
 GBV_NI G2J g2_mul_xabs(G2A q) { G2J r = jac_mul_xabs(q); return ret_copy(r); }
 
-// [|x|] q with the 63 doublings in lazy 28-bit limbs (f28_lazy.h); the 5 additions of q leave
-// for the canonical Fp2 form (jac_add_aff handles the exceptional cases) and come back.
-GBV_HD L2J l2j_from(const G2J& a) { return L2J{l2_from(a.x), l2_from(a.y), l2_from(a.z)}; }
-GBV_HD G2J l2j_to(const L2J& a) { return G2J{l2_to(a.x), l2_to(a.y), l2_to(a.z)}; }
-// madd-2007-bl as jac_add_aff, without a divergent branch: the exceptional case (same x) is a
-// wave-uniform branch taken only when some lane needs it, then resolved per lane by selects.
-template <class F> GBV_HD Jac<F> jac_add_aff_uniform(const Jac<F>& p, const Aff<F>& q) {
-  F Z1Z1 = f_sqr(p.z);
-  F U2 = f_mul(q.x, Z1Z1);
-  F S2 = f_mul(q.y, f_mul(p.z, Z1Z1));
-  F H = f_sub(U2, p.x);
-  F rr = f_dbl(f_sub(S2, p.y));
-  const bool p_inf = f_is_zero(p.z);
-  const bool same_x = f_is_zero(H) && !p_inf;
-  F HH = f_sqr(H);
-  F I = f_dbl(f_dbl(HH));
-  F J = f_mul(H, I);
-  F V = f_mul(p.x, I);
-  Jac<F> r;
-  r.x = f_sub(f_sub(f_sqr(rr), J), f_dbl(V));
-  r.y = f_sub(f_mul(rr, f_sub(V, r.x)), f_dbl(f_mul(p.y, J)));
-  r.z = f_sub(f_sub(f_sqr(f_add(p.z, H)), Z1Z1), HH);
-#if defined(__HIP_DEVICE_COMPILE__)
-  if (__any(same_x)) {
-#else
-  if (same_x) {
-#endif
-    const Jac<F> e = jac_sel(f_is_zero(rr), jac_dbl(p), jac_infinity<F>());
-    r = jac_sel(same_x, e, r);
-  }
-  return jac_sel(p_inf, jac_from_aff(q), r);
-}
-
-GBV_NI G2J g2_mul_xabs_lazy(G2A q) {
-  L2J r = l2j_from(jac_from_aff(q));
-  for (int i = 62; i >= 0; --i) {
-    r = l2j_dbl(r);
-#if GBV_LAZY_UNIFORM
-    if ((X_ABS >> i) & 1ull) r = l2j_from(jac_add_aff_uniform(l2j_to(r), q));
-#else
-    if ((X_ABS >> i) & 1ull) r = l2j_from(jac_add_aff(l2j_to(r), q));
-#endif
-  }
-  G2J out = l2j_to(r);
-  return ret_copy(out);
-}
-// Keep g2_mul_xabs_lazy on the standard calling convention (callee-saved SGPRs saved by the
-// callee): taking its address rules out the backend's interprocedural "no callee-saved registers"
-// form.  In that form (ROCm 7.2, IPRA on) the ~60 SGPR constants of the lazy chain left
-// k_vs_hash_sig with a corrupted pointer after the call (illegal address on the GPU, reproduced
-// and gone with -mllvm -enable-ipra=false).
-#if GBV_LAZY_G2
-__device__ __attribute__((used)) static void* const g_keep_lazy_xabs_cc = (void*)&g2_mul_xabs_lazy;
-#endif
 GBV_NI G2J g2_mul_xabs_jac(G2J q) { G2J r = jac_mul_xabs_jac(q); return ret_copy(r); }
 GBV_NI G1J g1_mul_u256(G1A q, const uint32_t* k) { G1J r = jac_mul_u256(q, k); return ret_copy(r); }
 GBV_NI G2J g2_mul_u256(G2A q, const uint32_t* k) { G2J r = jac_mul_u256(q, k); return ret_copy(r); }
@@ -397,11 +335,7 @@ GBV_HD G2J g2_psi_jac(const G2J& a) {
 
 // G2 membership (Scott 2021): psi(Q) == [x] Q = -[|x|] Q.  Q affine, not infinity.
 GBV_NI bool g2_in_subgroup(G2A q) {
-#if GBV_LAZY_G2
-  G2J xq = jac_neg(g2_mul_xabs_lazy(q));
-#else
   G2J xq = jac_neg(g2_mul_xabs(q));
-#endif
   return jac_eq_aff(xq, g2_psi(q));
 }
 

@@ -258,73 +258,37 @@ inline unsigned long long g_fme_count = 0;
 #endif
 
 // a b 2^-392 mod p (< 2p) by product scanning: column k of a*b and of m*p in one 64-bit
-// accumulator, m_k from the column's low 28 bits for k < 14, output limb k-14 for k >= 14.
-//
-// GBV_MUL28_CHAINS (per translation unit, default 1): the terms of a column go round-robin into
-// that many independent 64-bit accumulators, summed once per column.  One chain is the fewest
-// instructions and suits kernels with two waves per SIMD to hide the v_mad_u64_u32 latency; the
-// latency-bound kernels (one wave per SIMD: the verifySignatureSets Miller loops, the cooperative
-// pairing engine) can issue independent chains back to back instead.  Every column sum stays below
-// 2^61 either way (the bound above), so the result is identical.
-#ifndef GBV_MUL28_CHAINS
-#define GBV_MUL28_CHAINS 1
-#endif
-// GBV_MUL28_ASM (per translation unit, default 0): 2, 3 or 4 -- the device product and squaring
-// from mul28_asm.h (tools/gen_mul28_asm.py), each column's limb products one inline-asm block over
-// that many independent accumulator chains.  In C, LLVM reassociates a column's adds back into ONE
-// dependent v_mad_u64_u32 chain whatever GBV_MUL28_CHAINS says; only the asm keeps them apart.
-#ifndef GBV_MUL28_ASM
-#define GBV_MUL28_ASM 0
-#endif
-}  // namespace gbv
-#include "mul28_asm.h"
-namespace gbv {
-#if defined(__HIP_DEVICE_COMPILE__) && GBV_MUL28_ASM >= 2
-#define GBV_M28_CAT2(a, b) a##b
-#define GBV_M28_CAT(a, b) GBV_M28_CAT2(a, b)
-#define GBV_MUL28_DEV GBV_M28_CAT(mul28_asm, GBV_MUL28_ASM)
-#define GBV_SQR28_DEV GBV_M28_CAT(sqr28_asm, GBV_MUL28_ASM)
-#endif
+// accumulator, m_k from the column's low 28 bits for k < 14, output limb k-14 for k >= 14.  (Two or
+// four independent accumulators per column were measured, in C and as generated asm: LLVM
+// reassociates the C form back into one chain, and the asm form issued no faster)
 GBV_HD F28 mul28_inl(const F28& a, const F28& b) {
 #if defined(GBV_HOST_TEST)
   ++g_fme_count;
 #endif
-#if defined(GBV_MUL28_DEV)
-  return GBV_MUL28_DEV(a, b);
-#endif
-  constexpr int C = GBV_MUL28_CHAINS;
   uint32_t m[14], r[14];
-  uint64_t acc[C];
-#pragma unroll
-  for (int c = 0; c < C; ++c) acc[c] = 0;
+  uint64_t acc = 0;
 #pragma unroll
   for (int k = 0; k < 27; ++k) {
-    int t = 0;
 #pragma unroll
     for (int i = 0; i < 14; ++i) {
       const int j = k - i;
-      if (j >= 0 && j < 14) acc[(t++) % C] += (uint64_t)a.v[i] * b.v[j];
+      if (j >= 0 && j < 14) acc += (uint64_t)a.v[i] * b.v[j];
     }
 #pragma unroll
     for (int i = 0; i < 14; ++i) {
       const int j = k - i;
-      if (i < k && j >= 0 && j < 14) acc[(t++) % C] += (uint64_t)m[i] * P28[j];
+      if (i < k && j >= 0 && j < 14) acc += (uint64_t)m[i] * P28[j];
     }
-    uint64_t s = acc[0];
-#pragma unroll
-    for (int c = 1; c < C; ++c) {
-      s += acc[c];
-      acc[c] = 0;
-    }
+    uint64_t s = acc;
     if (k < 14) {
       m[k] = ((uint32_t)s * NP28) & M28;
       s += (uint64_t)m[k] * P28[0];
     } else {
       r[k - 14] = (uint32_t)s & M28;
     }
-    acc[0] = s >> 28;
+    acc = s >> 28;
   }
-  r[13] = (uint32_t)acc[0];
+  r[13] = (uint32_t)acc;
   F28 o;
 #pragma unroll
   for (int i = 0; i < 14; ++i) o.v[i] = r[i];
@@ -338,45 +302,33 @@ GBV_HD F28 sqr28_inl(const F28& a) {
 #if defined(GBV_HOST_TEST)
   ++g_fme_count;
 #endif
-#if defined(GBV_SQR28_DEV)
-  return GBV_SQR28_DEV(a);
-#endif
-  constexpr int C = GBV_MUL28_CHAINS;
   uint32_t d[14], m[14], r[14];
 #pragma unroll
   for (int i = 0; i < 14; ++i) d[i] = a.v[i] << 1;
-  uint64_t acc[C];
-#pragma unroll
-  for (int c = 0; c < C; ++c) acc[c] = 0;
+  uint64_t acc = 0;
 #pragma unroll
   for (int k = 0; k < 27; ++k) {
-    int t = 0;
 #pragma unroll
     for (int i = 0; i < 14; ++i) {
       const int j = k - i;
-      if (i < j && j < 14) acc[(t++) % C] += (uint64_t)a.v[i] * d[j];
+      if (i < j && j < 14) acc += (uint64_t)a.v[i] * d[j];
     }
-    if ((k & 1) == 0 && (k >> 1) < 14) acc[(t++) % C] += (uint64_t)a.v[k >> 1] * a.v[k >> 1];
+    if ((k & 1) == 0 && (k >> 1) < 14) acc += (uint64_t)a.v[k >> 1] * a.v[k >> 1];
 #pragma unroll
     for (int i = 0; i < 14; ++i) {
       const int j = k - i;
-      if (i < k && j >= 0 && j < 14) acc[(t++) % C] += (uint64_t)m[i] * P28[j];
+      if (i < k && j >= 0 && j < 14) acc += (uint64_t)m[i] * P28[j];
     }
-    uint64_t s = acc[0];
-#pragma unroll
-    for (int c = 1; c < C; ++c) {
-      s += acc[c];
-      acc[c] = 0;
-    }
+    uint64_t s = acc;
     if (k < 14) {
       m[k] = ((uint32_t)s * NP28) & M28;
       s += (uint64_t)m[k] * P28[0];
     } else {
       r[k - 14] = (uint32_t)s & M28;
     }
-    acc[0] = s >> 28;
+    acc = s >> 28;
   }
-  r[13] = (uint32_t)acc[0];
+  r[13] = (uint32_t)acc;
   F28 o;
 #pragma unroll
   for (int i = 0; i < 14; ++i) o.v[i] = r[i];

@@ -87,24 +87,6 @@ GBV_NI void fp12_mul_line_to(Fp12* f, const Line* l) {
   f->c0 = fp6_add(a, fp6_mul_v(b));
 }
 
-// f = f^2 * line in one out-of-line call (the Miller loop's doubling bit): the squared value stays in
-// registers for the line product instead of a store and reload through the frame
-// (GBV_MILLER_FUSED, k_vs_miller).
-GBV_NI void fp12_sqr_mul_line_to(Fp12* f, const Line* l) {
-  Fp6 c0, c1;
-  {
-    const Fp6 a0 = f->c0, a1 = f->c1;
-    const Fp6 t = fp6_mul(a0, a1);
-    c0 = fp6_sub(fp6_sub(fp6_mul(fp6_add(a0, a1), fp6_add(a0, fp6_mul_v(a1))), t), fp6_mul_v(t));
-    c1 = fp6_add(t, t);
-  }
-  const Fp6 a = fp6_mul_by_01(c0, l->c0, l->c2);
-  const Fp6 b = fp6_mul_by_1(c1, l->c3);
-  const Fp6 e = fp6_mul_by_01(fp6_add(c0, c1), l->c0, fp2_add(l->c2, l->c3));
-  f->c1 = fp6_sub(fp6_sub(e, a), b);
-  f->c0 = fp6_add(a, fp6_mul_v(b));
-}
-
 GBV_NI void fp12_inv_to(Fp12* r, const Fp12* a) {
   Fp6 d = fp6_sub(fp6_mul(a->c0, a->c0), fp6_mul_v(fp6_mul(a->c1, a->c1)));
   Fp6 di = fp6_inv(d);

@@ -13,15 +13,9 @@ constexpr unsigned FB_GRID = 2048;  // persistent failure-path grids: 2 waves pe
 constexpr uint32_t GROUP_CHECK_THREAD_MIN = 512;
 // segments of at most this many chunks skip the combined segment check (latency of small calls)
 constexpr uint32_t DIRECT_CHUNK_MAX = 32;
-// segments of at least this many sets form their G2 sum sum r_i sig_i with the bucket MSM
-// (k_msm.hip) instead of per-set ladders; GBV_MSM_MIN overrides (0 = never)
-constexpr uint32_t MSM_MIN_SETS = 131072;
-constexpr uint32_t MSM_COOLDOWN = 16;
 // events per segment: [0,1] prepare, [2,3] chunk finish, [4,5] miller, [6,7] seg check,
 // [8,9] group checks, [10,11] msm buckets, [12] msm reduce done
 constexpr size_t EPS = 13;
-
-size_t msm_min_sets() { return getenv("GBV_MSM_MIN") ? (size_t)atol(getenv("GBV_MSM_MIN")) : MSM_MIN_SETS; }
 
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
@@ -38,7 +32,7 @@ int gbv_fail(gbv_ctx* c, int code, const std::string& msg) {
 }
 
 void ctx_drain(gbv_ctx* c) {
-  for (hipStream_t s : {c->stream, c->stream2, c->stream4, c->stream5, c->stream6})
+  for (hipStream_t s : {c->stream, c->stream2, c->stream4, c->stream5})
     if (s) (void)hipStreamSynchronize(s);
   (void)hipGetLastError();
 }
@@ -213,13 +207,10 @@ static void sm_destroy(gbv_sm_batch* b) {
 
 extern "C" {
 
-#ifndef GBV_MSM_CUS_DEFAULT
-#define GBV_MSM_CUS_DEFAULT 0
-#endif
-
 int gbv_init(int device, gbv_ctx** out) {
   if (!out) return GBV_E_ARG;
   *out = nullptr;
+  tuning_load();
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return GBV_E_DEVICE;
   if (device < 0 || device >= ndev) return GBV_E_ARG;
@@ -234,38 +225,21 @@ int gbv_init(int device, gbv_ctx** out) {
             hipStreamCreateWithPriority(&c->stream4, hipStreamNonBlocking, prio_hi) == hipSuccess &&
             hipStreamCreateWithPriority(&c->stream5, hipStreamNonBlocking, prio_hi) == hipSuccess;
   if (!ok) {
-    for (hipStream_t s : {c->stream, c->stream2, c->stream4, c->stream5, c->stream6})
+    for (hipStream_t s : {c->stream, c->stream2, c->stream4, c->stream5})
       if (s) hipStreamDestroy(s);
     delete c;
     return GBV_E_DEVICE;
   }
-  // GBV_MSM_CUS = k > 0: stream A loses k CUs (every (n/k)-th, spread over the XCDs) to a stream of
-  // their own for the same-message chunk sums and bucket MSM, which then run beside the next batch's
-  // k_sm_prepare instead of after it (on shared CUs the prepare waves starve them)
-  const int msm_cus = getenv("GBV_MSM_CUS") ? atoi(getenv("GBV_MSM_CUS")) : GBV_MSM_CUS_DEFAULT;
-  hipDeviceProp_t prop;
-  if (msm_cus > 0 && hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 2 * msm_cus) {
-    const int ncu = prop.multiProcessorCount, step = ncu / msm_cus;
-    std::vector<uint32_t> ma((ncu + 31) / 32, 0u), mm((ncu + 31) / 32, 0u);
-    int taken = 0;
-    for (int cu = 0; cu < ncu; ++cu) {
-      const bool m = cu % step == step - 1 && taken < msm_cus;
-      taken += m ? 1 : 0;
-      (m ? mm : ma)[cu / 32] |= 1u << (cu % 32);
-    }
-    hipStream_t a2 = nullptr, m2 = nullptr;
-    if (hipExtStreamCreateWithCUMask(&a2, (uint32_t)ma.size(), ma.data()) == hipSuccess &&
-        hipExtStreamCreateWithCUMask(&m2, (uint32_t)mm.size(), mm.data()) == hipSuccess) {
-      hipStreamDestroy(c->stream);
-      c->stream = a2;
-      c->stream6 = m2;
-    } else {
-      if (a2) hipStreamDestroy(a2);
-      if (m2) hipStreamDestroy(m2);
-    }
-  }
-  const char* comb_env = getenv("GBV_COMB");
-  c->comb_on = !(comb_env && comb_env[0] == '0');
+  // the context's own settings, read once here (gbv_tune changes them for tests)
+  auto rd = [](const char* name, uint32_t& v) {
+    if (const char* e = getenv(name)) v = (uint32_t)strtoul(e, nullptr, 10);
+  };
+  rd("GBV_MSM_MIN", c->msm_min);
+  rd("GBV_MSM_COOLDOWN", c->msm_cooldown_len);
+  rd("GBV_SEGMENTS", c->segments);
+  uint32_t comb = 1;
+  rd("GBV_COMB", comb);
+  c->comb_on = comb != 0;
   *out = c;
   return GBV_OK;
 }
@@ -273,12 +247,15 @@ int gbv_init(int device, gbv_ctx** out) {
 void gbv_destroy(gbv_ctx* c) {
   if (!c) return;
   {
-    GBV_LOCK(c);  // a call still running on another thread finishes first
+    // a call still running on another thread finishes first (one-shot calls hold a scratch mutex
+    // while they wait on the device)
+    std::lock_guard<std::mutex> g1(c->sm_scratch_mu), g2(c->vs_scratch_mu);
+    GBV_LOCK(c);
   }
   hipSetDevice(c->device);
   c->closed = true;
   // every stream drains before anything it may still read or write is freed
-  for (hipStream_t s : {c->stream, c->stream2, c->stream4, c->stream5, c->stream6})
+  for (hipStream_t s : {c->stream, c->stream2, c->stream4, c->stream5})
     if (s) hipStreamSynchronize(s);
   sm_destroy(c->sm_scratch);
   vs_batch_free(c->vs_scratch);
@@ -291,17 +268,26 @@ void gbv_destroy(gbv_ctx* c) {
   for (auto* p : c->ssz_buf) hipFree(p);
   for (auto e : c->ssz_ev)
     if (e) hipEventDestroy(e);
-  for (hipStream_t s : {c->stream, c->stream2, c->stream4, c->stream5, c->stream6})
+  for (hipStream_t s : {c->stream, c->stream2, c->stream4, c->stream5})
     if (s) hipStreamDestroy(s);
   delete c;
+}
+
+int gbv_tune(gbv_ctx* c, const char* name, uint32_t value) {
+  if (!c || !name) return GBV_E_ARG;
+  GBV_LOCK(c);
+  if (!strcmp(name, "msm_min")) c->msm_min = value;
+  else if (!strcmp(name, "msm_cooldown")) c->msm_cooldown_len = value;
+  else if (!strcmp(name, "segments")) c->segments = std::max<uint32_t>(value, 1);
+  else return gbv_fail(c, GBV_E_ARG, std::string("unknown setting: ") + name);
+  return GBV_OK;
 }
 
 const char* gbv_last_error(gbv_ctx* c) { return c ? t_err.c_str() : "null context"; }
 
 size_t gbv_pubkeys_count(gbv_ctx* c) {
   if (!c) return 0;
-  GBV_LOCK(c);
-  return c->table_n;
+  return c->table_n.load(std::memory_order_acquire);  // no lock: the event loop never waits on a device pass
 }
 int gbv_comb_enabled(gbv_ctx* c) {
   if (!c) return 0;
@@ -426,7 +412,7 @@ int gbv_pubkeys_append(gbv_ctx* c, uint32_t first, const uint8_t* pk48, size_t n
   HIP_CHECK(c, hipStreamSynchronize(c->stream));
   if (status) memcpy(status, h, n);
   const size_t keep = c->table_n;
-  c->table_n = std::max(c->table_n, (size_t)first + n);
+  c->table_n.store(std::max(keep, (size_t)first + n), std::memory_order_release);
   return comb_build(c, first, n, keep);
 }
 
@@ -442,7 +428,7 @@ int gbv_pubkeys_replicate(gbv_ctx* c, uint32_t src_first, uint32_t src_n, uint32
   HIP_CHECK(c, hipGetLastError());
   HIP_CHECK(c, hipStreamSynchronize(c->stream));
   const size_t keep = c->table_n;
-  c->table_n = std::max(c->table_n, (size_t)dst_first + n);
+  c->table_n.store(std::max(keep, (size_t)dst_first + n), std::memory_order_release);
   if (c->comb_on && (rc = comb_reserve(c, (size_t)dst_first + n, keep)) != GBV_OK) return rc;
   if (c->comb_on) {  // the source slots' tables are built: copy them like the table entries
     launch_comb_replicate(c->stream, c->comb, c->comb_ok, src_first, src_n, dst_first, (uint32_t)n);
@@ -606,7 +592,7 @@ static int sm_fill(gbv_ctx* c, gbv_sm_batch* b, size_t n_calls, const uint32_t* 
   grp_off.push_back((uint32_t)n);
   size_t G = grp_msg.size();
   HIP_CHECK(c, hipSetDevice(c->device));
-  bool want_msm = msm_min_sets() && n >= msm_min_sets();
+  bool want_msm = c->msm_min && n >= c->msm_min;
   int rc = sm_reserve(c, b, n, G, n_calls, want_msm);
   if (rc) return rc;
   // input blob: idx 4n | sig 96n | set_grp 4n | grp_off 4(G+1) | grp_msg 4G | msgs 32 calls
@@ -704,26 +690,20 @@ int gbv_sm_batch_submit(gbv_ctx* c, gbv_sm_batch* b) {
 static int sm_submit_enqueue(gbv_ctx* c, gbv_sm_batch* b) {
   Seed seed = fresh_seed();
   uint32_t nonce = c->nonce++;
-  // Same-message batches: hash on stream 4, tail on stream 2, every batch.  Alternating the tails
-  // of consecutive batches over two streams (GBV_ALT_TAIL=1, diagnosis) used to stall the device
-  // for 0.1-8 s at a time while the failure-path kernels needed 27-28 KB of scratch per lane and
-  // were dispatched from two hardware queues; with the pointer-based Fp12 layer (<= 8.7 KB) it runs
-  // clean, but buys nothing while the tail is shorter than k_sm_prepare.
-  static const bool alt_tail = getenv("GBV_ALT_TAIL") != nullptr;  // diagnosis only
-  const bool flip = alt_tail && (c->sm_submits++ & 1) != 0;
-  // Invalid-dense regime (a segment failed within the last MSM_COOLDOWN submits, e.g. C5's 1 %
+  // Same-message batches: hash on stream 4, tail on stream 2, every batch (alternating the tails of
+  // consecutive batches over two streams buys nothing while the tail is shorter than k_sm_prepare).
+  // Invalid-dense regime (a segment failed within the last msm_cooldown_len submits, e.g. C5's 1 %
   // invalid stream): the failure path -- latency-bound run and per-set checks, ~170 ms per 1M
   // sets at 1 % -- goes to stream 4 and the hash to stream A, so batch k's failure path runs
   // beside batch k+1's chunk tail instead of in front of it (three streams either way).
-  // GBV_FB_STREAM=0 keeps the failure path on the tail stream.
-  static const bool fb_stream_env = !(getenv("GBV_FB_STREAM") && getenv("GBV_FB_STREAM")[0] == '0');
-  const bool dense = fb_stream_env && !alt_tail && c->msm_cooldown != 0;
+  ++c->sm_submits;
+  const bool dense = c->msm_cooldown != 0;
   hipStream_t sa = c->stream;
-  hipStream_t tail = flip ? c->stream4 : c->stream2, sh = alt_tail ? tail : (dense ? sa : c->stream4);
+  hipStream_t tail = c->stream2, sh = dense ? sa : c->stream4;
   hipStream_t sbs[2] = {tail, tail};
   hipStream_t sf = dense ? c->stream4 : tail;  // failure path + copy-out
   const size_t max_seg = b->seg_cap;
-  const size_t n_seg = getenv("GBV_SEGMENTS") ? (size_t)std::max(1, atoi(getenv("GBV_SEGMENTS"))) : 1;
+  const size_t n_seg = c->segments;
   size_t sub_sets = std::max<size_t>((b->n + n_seg - 1) / n_seg, 16384);
   std::vector<uint32_t> gcut{0};
   {
@@ -737,7 +717,7 @@ static int sm_submit_enqueue(gbv_ctx* c, gbv_sm_batch* b) {
   gcut.push_back((uint32_t)b->G);
   size_t S = gcut.size() - 1;
   b->n_seg = S;
-  const size_t msm_min = c->msm_cooldown ? 0 : msm_min_sets();
+  const size_t msm_min = c->msm_cooldown ? 0 : c->msm_min;
   if (c->msm_cooldown) --c->msm_cooldown;
   bool any_msm = false;
   for (size_t s = 0; s < S; ++s) {
@@ -754,7 +734,7 @@ static int sm_submit_enqueue(gbv_ctx* c, gbv_sm_batch* b) {
   }
   // events: [0,1] hash; EPS per segment; then [tail] 2 fallback
   size_t need = 2 + EPS * S + 2;
-  b->cur = flip ? 1 : 0;
+  b->cur = 0;
   std::vector<hipEvent_t>& evv = b->evs[b->cur];
   if (evv.size() < need) {
     size_t old = evv.size();
@@ -787,19 +767,14 @@ static int sm_submit_enqueue(gbv_ctx* c, gbv_sm_batch* b) {
     // k_sm_prepare (the MSM's bucket pass then has the whole device instead of fighting the next
     // k_sm_prepare for CUs); the tail stream waits for them.  Other segments sum their chunks on
     // the tail stream.
-    hipStream_t sm6 = c->stream6;  // GBV_MSM_CUS: chunk sums + bucket MSM on their own CUs
-    hipStream_t scf = msm ? (sm6 ? sm6 : sa) : sb;
+    hipStream_t scf = msm ? sa : sb;
     if (scf != sa) HIP_CHECK(c, hipStreamWaitEvent(scf, e[1], 0));
     HIP_CHECK(c, hipStreamWaitEvent(scf, ev[1], 0));
     HIP_CHECK(c, hipEventRecord(e[2], scf));
     launch_sm_chunk_finish(LaunchCfg{0, 64, scf}, g0, G, s0, b->grp_off, b->status, Sh, b->rP, b->PgJ, b->SgJ, b->grp_state,
                            b->n_fallback);
     HIP_CHECK(c, hipEventRecord(e[3], scf));
-    // the bucket pass runs on stream A (default) or, with GBV_MSM_STREAM=h, on the hash stream beside
-    // the tail's Miller values
-    static const bool msm_on_hash = getenv("GBV_MSM_STREAM") && getenv("GBV_MSM_STREAM")[0] == 'h';
-    hipStream_t smsm = msm ? (sm6 ? sm6 : msm_on_hash ? sh : sa) : scf;
-    if (msm && !sm6 && msm_on_hash) HIP_CHECK(c, hipStreamWaitEvent(sh, e[3], 0));
+    hipStream_t smsm = scf;  // the bucket pass: stream A for an MSM segment
     HIP_CHECK(c, hipEventRecord(e[10], smsm));
     // segment s-2 shares this segment's bucket buffers: its reduction (tail stream) must be done
     if (msm && s >= 2 && b->seg_msm[s - 2]) HIP_CHECK(c, hipStreamWaitEvent(smsm, ev[2 + EPS * (s - 2) + 12], 0));
@@ -893,7 +868,7 @@ int gbv_sm_batch_wait(gbv_ctx* c, gbv_sm_batch* b, uint8_t* valid) {
     bool failed = !(b->seg_ok_host[s] || b->seg_direct[s]);
     c->last_failed_segments += failed ? 1 : 0;
     if (failed && b->seg_msm[s])
-      c->msm_cooldown = getenv("GBV_MSM_COOLDOWN") ? (uint32_t)atoi(getenv("GBV_MSM_COOLDOWN")) : MSM_COOLDOWN;
+      c->msm_cooldown = c->msm_cooldown_len;
   }
   for (auto& x : c->last_ms) x = 0.f;
   for (auto& x : c->last_launches) x = 0;
@@ -918,8 +893,7 @@ int gbv_sm_batch_wait(gbv_ctx* c, gbv_sm_batch* b, uint8_t* valid) {
 
 int gbv_sm_batch_verify(gbv_ctx* c, gbv_sm_batch* b, uint8_t* valid) {
   if (!c) return GBV_E_ARG;
-  GBV_LOCK(c);
-  int rc = gbv_sm_batch_submit(c, b);
+  int rc = gbv_sm_batch_submit(c, b);  // the batch belongs to the caller: the wait needs no lock held
   if (rc) return rc;
   return gbv_sm_batch_wait(c, b, valid);
 }
@@ -948,12 +922,18 @@ int gbv_last_kernel_ms(gbv_ctx* c, float* out, int* launches, int max) {
 int gbv_verify_same_message_multi(gbv_ctx* c, size_t n_calls, const uint32_t* call_off, const uint32_t* idx, const uint8_t* sigs96,
                                   const uint8_t* msgs32, uint8_t* valid) {
   if (!c) return GBV_E_ARG;
-  GBV_LOCK(c);  // the scratch batch is shared by every one-shot call on this context
-  if (c->closed) return GBV_E_CLOSED;
-  if (!c->sm_scratch) c->sm_scratch = new gbv_sm_batch();
-  int rc = sm_fill(c, c->sm_scratch, n_calls, call_off, idx, sigs96, msgs32);
-  if (rc) return rc;
-  return gbv_sm_batch_verify(c, c->sm_scratch, valid);
+  std::lock_guard<std::mutex> sg(c->sm_scratch_mu);  // the scratch batch: one one-shot call at a time
+  gbv_sm_batch* b = nullptr;
+  {
+    GBV_LOCK(c);
+    if (c->closed) return GBV_E_CLOSED;
+    if (!c->sm_scratch) c->sm_scratch = new gbv_sm_batch();
+    b = c->sm_scratch;
+    int rc = sm_fill(c, b, n_calls, call_off, idx, sigs96, msgs32);
+    if (rc) return rc;
+    if ((rc = gbv_sm_batch_submit(c, b))) return rc;
+  }
+  return gbv_sm_batch_wait(c, b, valid);  // blocks without the context lock
 }
 
 int gbv_verify_same_message(gbv_ctx* c, const uint32_t* idx, const uint8_t* sigs96, size_t n, const uint8_t* msg32, uint8_t* valid) {
@@ -1170,14 +1150,27 @@ int gbv_util_sign(gbv_ctx* c, const uint8_t* sk32, size_t n, const uint32_t* grp
 }  // extern "C"
 
 namespace gbv {
-uint32_t hash_pair_max() {
-  static const uint32_t v = getenv("GBV_HASH_PAIR_MAX") ? (uint32_t)atoi(getenv("GBV_HASH_PAIR_MAX")) : HASH_PAIR_MAX;
-  return v;
+static Tuning g_tuning;
+static std::once_flag g_tuning_once;
+const Tuning& tuning() { return g_tuning; }
+void tuning_load() {
+  std::call_once(g_tuning_once, [] {
+    auto rd = [](const char* name, uint32_t& v) {
+      if (const char* e = getenv(name)) v = (uint32_t)strtoul(e, nullptr, 10);
+    };
+    rd("GBV_HASH_PAIR_MAX", g_tuning.hash_pair_max);
+    rd("GBV_HASH_COOP_MAX", g_tuning.hash_coop_max);
+    rd("GBV_PREPARE_SPLIT_MAX", g_tuning.prepare_split_max);
+    rd("GBV_PREP_COOP_RAND", g_tuning.prep_coop_rand_max);
+    rd("GBV_CHUNK_FINISH_WAVE_MAX", g_tuning.chunk_finish_wave_max);
+    rd("GBV_VS_PRE_MAX", g_tuning.vs_pre_max);
+    rd("GBV_VS_FS_MAXC", g_tuning.vs_fs_maxc);
+    rd("GBV_SYNC_DEBUG", g_tuning.sync_debug);
+  });
 }
 
 void debug_sync(hipStream_t s, const char* kernel) {
-  static int on = getenv("GBV_SYNC_DEBUG") ? atoi(getenv("GBV_SYNC_DEBUG")) : 0;
-  if (!on) return;
+  if (!g_tuning.sync_debug) return;
   hipError_t e = hipStreamSynchronize(s);
   if (e == hipSuccess) e = hipGetLastError();
   fprintf(stderr, "[gbv] %s: %s\n", kernel, hipGetErrorString(e));

@@ -62,6 +62,9 @@ struct gbv_vs_batch {
   G2J* Spart = nullptr;
   uint8_t *has = nullptr, *flag = nullptr;
   size_t part_cap = 0;
+  uint8_t* part_host = nullptr;  // pinned: the shard's Fp12 then its n status bytes
+  size_t part_host_cap = 0;
+  bool part_empty = false;
   hipEvent_t ev[7] = {};
   hipEvent_t done = nullptr;
   hipEvent_t copied = nullptr;  // the last fill's input copy (stream A); see gbv_sm_batch::copied
@@ -90,6 +93,7 @@ void vs_batch_free(gbv_vs_batch* b) {
   hipFree(b->in_dev);
   hipHostFree(b->in_host);
   hipFree(b->Fpart); hipFree(b->Spart); hipFree(b->has); hipFree(b->f_out); hipFree(b->flag);
+  hipHostFree(b->part_host);
   hipFree(b->agg_part); hipFree(b->agg_part_bad);
   for (auto e : b->ev)
     if (e) hipEventDestroy(e);
@@ -180,12 +184,14 @@ static int vs_fill(gbv_ctx* c, gbv_vs_batch* b, size_t n_calls, const uint32_t* 
   int rc = vs_reserve(c, b, n, C);
   if (rc) return rc;
   if (b->agg_part_cap < n_slices) {
+    // grow geometrically (each larger Electra aggregate would otherwise free + allocate, and a
+    // hipFree synchronises the device under the passes in flight)
+    const size_t cap = std::max(n_slices, 2 * b->agg_part_cap);
     hipFree(b->agg_part);
     hipFree(b->agg_part_bad);
     b->agg_part = nullptr;
     b->agg_part_bad = nullptr;
     b->agg_part_cap = 0;
-    size_t cap = std::max(n_slices, 2 * b->agg_part_cap);
     HIP_CHECK(c, dalloc(&b->agg_part, cap));
     HIP_CHECK(c, dalloc(&b->agg_part_bad, cap));
     b->agg_part_cap = cap;
@@ -278,29 +284,14 @@ static int vs_fill(gbv_ctx* c, gbv_vs_batch* b, size_t n_calls, const uint32_t* 
   return GBV_OK;
 }
 
-static bool vs_fs_on() {  // GBV_VS_FS=0: the chunk check forms the (-g1, sum) Miller value itself (A/B)
-  static const bool on = !(getenv("GBV_VS_FS") && atoi(getenv("GBV_VS_FS")) == 0);
-  return on;
-}
+// "pre" mode for passes of at most tuning().vs_pre_max sets: k_vs_sig_pre + k_vs_pk_rand in place of
+// k_vs_hash_sig's signature roles
+static bool vs_pre_on(const gbv_vs_batch* b) { return b->n <= tuning().vs_pre_max; }
 
 // Small passes, and passes of few chunks (a range-sync segment of blocks: 2 chunks per block), whose
-// chunk checks are latency-bound; GBV_VS_FS_MAXC sets the chunk bound (A/B).
-static bool vs_split_on() {  // GBV_VS_SPLIT=0: hash and signature roles in one k_vs_hash_sig launch (A/B)
-  static const bool on = !(getenv("GBV_VS_SPLIT") && atoi(getenv("GBV_VS_SPLIT")) == 0);
-  return on;
-}
-
-// "pre" mode for passes of at most GBV_VS_PRE_MAX sets (0: off): k_vs_sig_pre + k_vs_pk_rand in place
-// of k_vs_hash_sig's signature roles
-static bool vs_pre_on(const gbv_vs_batch* b) {
-  static const size_t maxn = getenv("GBV_VS_PRE_MAX") ? (size_t)atol(getenv("GBV_VS_PRE_MAX")) : 16384;
-  return b->n <= maxn;
-}
-
-static bool vs_fs_small(const gbv_vs_batch* b) {
-  static const size_t maxc = getenv("GBV_VS_FS_MAXC") ? (size_t)atol(getenv("GBV_VS_FS_MAXC")) : 256;
-  return vs_fs_on() && (b->n <= VS_COOP_MILLER_MAX || b->C <= maxc);
-}
+// chunk checks are latency-bound: each chunk's (-g1, sum r_i sig_i) Miller value is formed beside the
+// per-set ones instead of inside the chunk check.
+static bool vs_fs_small(const gbv_vs_batch* b) { return b->n <= VS_COOP_MILLER_MAX || b->C <= tuning().vs_fs_maxc; }
 
 // Per-set kernels: aggregate and hash + signature + randomisation on stream A, the Miller values on
 // stream m (a tail stream, so that they overlap the next batch's stream-A kernels; or stream A).
@@ -313,7 +304,7 @@ static int vs_enqueue_sets(gbv_ctx* c, gbv_vs_batch* b, hipStream_t m, bool with
   uint32_t nonce = c->nonce++;
   // passes up to GBV_VS_PRE_MAX sets: the signature half first, on stream 5, beside the aggregation below
   const bool small = with_fs && vs_fs_small(b);
-  const bool pre = with_fs && m != s && vs_split_on() && vs_pre_on(b);
+  const bool pre = with_fs && m != s && vs_pre_on(b);
   if (pre) {
     HIP_CHECK(c, hipStreamWaitEvent(c->stream5, b->copied, 0));
     launch_vs_sig_pre(c->stream5, (uint32_t)b->n, b->sig, b->sig_stride, b->siglen, seed, nonce, b->rS, b->status, b->sig_st);
@@ -332,7 +323,7 @@ static int vs_enqueue_sets(gbv_ctx* c, gbv_vs_batch* b, hipStream_t m, bool with
   HIP_CHECK(c, hipEventRecord(b->ev[1], s));
   // small passes and pre mode: the hash on stream m (for few messages lane-pair maps and the
   // cooperative cofactor clearing) beside the signature work
-  const bool split = with_fs && m != s && (small || pre) && vs_split_on();
+  const bool split = with_fs && m != s && (small || pre);
   if (split) HIP_CHECK(c, hipStreamWaitEvent(m, b->copied, 0));
   if (split) launch_hash_msgs(LaunchCfg{blocks_for(b->n), TPB, m}, b->msgs, (uint32_t)b->n, b->H, b->Hpre);
   if (pre) {
@@ -476,29 +467,38 @@ static gbv_vs_batch* scratch(gbv_ctx* c) {
 int gbv_verify_sets_multi(gbv_ctx* c, size_t n_calls, const uint32_t* call_off, const gbv_set* sets, const uint32_t* arena,
                           uint8_t* call_valid) {
   if (!c || (n_calls && !call_valid)) return GBV_E_ARG;
-  GBV_LOCK(c);  // the scratch batch is shared by every one-shot call on this context
-  if (c->closed) return GBV_E_CLOSED;
-  gbv_vs_batch* b = scratch(c);
-  int rc = vs_fill(c, b, n_calls, call_off, sets, arena);
-  if (rc) return rc;
-  if ((rc = gbv_vs_batch_submit(c, b))) return rc;
-  return gbv_vs_batch_wait(c, b, call_valid);
+  std::lock_guard<std::mutex> sg(c->vs_scratch_mu);  // the scratch batch: one one-shot call at a time
+  gbv_vs_batch* b = nullptr;
+  {
+    GBV_LOCK(c);
+    if (c->closed) return GBV_E_CLOSED;
+    b = scratch(c);
+    int rc = vs_fill(c, b, n_calls, call_off, sets, arena);
+    if (rc) return rc;
+    if ((rc = gbv_vs_batch_submit(c, b))) return rc;
+  }
+  return gbv_vs_batch_wait(c, b, call_valid);  // blocks without the context lock
 }
 
 int gbv_verify_sets(gbv_ctx* c, const gbv_set* sets, size_t n, const uint32_t* arena, uint8_t* all_valid, uint8_t* chunk_valid) {
   if (!c || !all_valid) return GBV_E_ARG;
-  GBV_LOCK(c);
-  if (c->closed) return GBV_E_CLOSED;
+  std::lock_guard<std::mutex> sg(c->vs_scratch_mu);
   *all_valid = 0;
   uint32_t off[2] = {0, (uint32_t)n};
-  gbv_vs_batch* b = scratch(c);
-  int rc = vs_fill(c, b, 1, off, sets, arena);
-  if (rc) return rc;
-  // aggregatePublicKeys([]) throws before any verification: the call rejects (index.ts:398-412)
-  if (b->call_reject[0]) return gbv_fail(c, GBV_E_EMPTY_AGGREGATE, "EMPTY_AGGREGATE_ARRAY");
-  if ((rc = gbv_vs_batch_submit(c, b))) return rc;
+  gbv_vs_batch* b = nullptr;
+  {
+    GBV_LOCK(c);
+    if (c->closed) return GBV_E_CLOSED;
+    b = scratch(c);
+    int rc = vs_fill(c, b, 1, off, sets, arena);
+    if (rc) return rc;
+    // aggregatePublicKeys([]) throws before any verification: the call rejects (index.ts:398-412)
+    if (b->call_reject[0]) return gbv_fail(c, GBV_E_EMPTY_AGGREGATE, "EMPTY_AGGREGATE_ARRAY");
+    if ((rc = gbv_vs_batch_submit(c, b))) return rc;
+  }
   uint8_t v = 0;
-  if ((rc = gbv_vs_batch_wait(c, b, &v))) return rc;
+  int rc = gbv_vs_batch_wait(c, b, &v);
+  if (rc) return rc;
   *all_valid = v;
   if (chunk_valid) {
     if (b->C)
@@ -510,41 +510,50 @@ int gbv_verify_sets(gbv_ctx* c, const gbv_set* sets, size_t n, const uint32_t* a
 }
 
 // One shard of a verifySignatureSets call spread over several GPUs: the shard's sets
-// reduce to ONE Fp12 Miller product (its pairs and its own (-g1, sum r_i sig_i) pair).
-static int vs_partial_run(gbv_ctx* c, gbv_vs_batch* b, uint8_t out576[GBV_FP12_PARTIAL_BYTES], uint8_t* shard_ok);
+// reduce to ONE Fp12 Miller product (its pairs and its own (-g1, sum r_i sig_i) pair).  Enqueued
+// under the context lock, collected without it.
+static int vs_partial_enqueue(gbv_ctx* c, gbv_vs_batch* b);
+static int vs_partial_collect(gbv_ctx* c, gbv_vs_batch* b, uint8_t out576[GBV_FP12_PARTIAL_BYTES], uint8_t* shard_ok);
 
 int gbv_vs_partial(gbv_ctx* c, const gbv_set* sets, size_t n, const uint32_t* arena, uint8_t out576[GBV_FP12_PARTIAL_BYTES],
                    uint8_t* shard_ok) {
   if (!c || !out576 || !shard_ok) return GBV_E_ARG;
-  GBV_LOCK(c);
-  if (c->closed) return GBV_E_CLOSED;
+  std::lock_guard<std::mutex> sg(c->vs_scratch_mu);
   *shard_ok = 1;
   uint32_t off[2] = {0, (uint32_t)n};
-  gbv_vs_batch* b = scratch(c);
-  int rc = vs_fill(c, b, 1, off, sets, arena);
-  if (rc) return rc;
-  if (b->call_reject[0]) return gbv_fail(c, GBV_E_EMPTY_AGGREGATE, "EMPTY_AGGREGATE_ARRAY");
-  return vs_partial_run(c, b, out576, shard_ok);
+  gbv_vs_batch* b = nullptr;
+  {
+    GBV_LOCK(c);
+    if (c->closed) return GBV_E_CLOSED;
+    b = scratch(c);
+    int rc = vs_fill(c, b, 1, off, sets, arena);
+    if (rc) return rc;
+    if (b->call_reject[0]) return gbv_fail(c, GBV_E_EMPTY_AGGREGATE, "EMPTY_AGGREGATE_ARRAY");
+    if ((rc = vs_partial_enqueue(c, b))) return rc;
+  }
+  return vs_partial_collect(c, b, out576, shard_ok);
 }
 
 int gbv_vs_batch_partial(gbv_ctx* c, gbv_vs_batch* b, uint8_t out576[GBV_FP12_PARTIAL_BYTES], uint8_t* shard_ok) {
   if (!c || !b || !out576 || !shard_ok) return GBV_E_ARG;
-  GBV_LOCK(c);
-  if (c->closed) return GBV_E_CLOSED;
-  if (b->in_flight) return gbv_fail(c, GBV_E_ARG, "batch in flight");
-  *shard_ok = 1;
-  for (uint8_t r : b->call_reject)
-    if (r) return gbv_fail(c, GBV_E_EMPTY_AGGREGATE, "EMPTY_AGGREGATE_ARRAY");
-  return vs_partial_run(c, b, out576, shard_ok);
+  {
+    GBV_LOCK(c);
+    if (c->closed) return GBV_E_CLOSED;
+    if (b->in_flight) return gbv_fail(c, GBV_E_ARG, "batch in flight");
+    *shard_ok = 1;
+    for (uint8_t r : b->call_reject)
+      if (r) return gbv_fail(c, GBV_E_EMPTY_AGGREGATE, "EMPTY_AGGREGATE_ARRAY");
+    int rc = vs_partial_enqueue(c, b);
+    if (rc) return rc;
+  }
+  return vs_partial_collect(c, b, out576, shard_ok);
 }
 
-static int vs_partial_run(gbv_ctx* c, gbv_vs_batch* b, uint8_t out576[GBV_FP12_PARTIAL_BYTES], uint8_t* shard_ok) {
+static int vs_partial_enqueue(gbv_ctx* c, gbv_vs_batch* b) {
   const size_t n = b->n;
   int rc;
-  if (n == 0) {
-    fp12_pack(out576, fp12_one_host());
-    return GBV_OK;
-  }
+  b->part_empty = n == 0;
+  if (n == 0) return GBV_OK;
   size_t np = seg_reduce_scratch(n);
   if (b->part_cap < np) {
     hipFree(b->Fpart); hipFree(b->Spart); hipFree(b->has); hipFree(b->f_out); hipFree(b->flag);
@@ -553,6 +562,14 @@ static int vs_partial_run(gbv_ctx* c, gbv_vs_batch* b, uint8_t out576[GBV_FP12_P
     HIP_CHECK(c, dalloc(&b->Fpart, np)); HIP_CHECK(c, dalloc(&b->Spart, np)); HIP_CHECK(c, dalloc(&b->has, np));
     HIP_CHECK(c, dalloc(&b->f_out, 1)); HIP_CHECK(c, dalloc(&b->flag, 1));
     b->part_cap = np;
+  }
+  if (b->part_host_cap < sizeof(Fp12) + n) {
+    hipHostFree(b->part_host);
+    b->part_host = nullptr;
+    b->part_host_cap = 0;
+    const size_t cap = std::max(sizeof(Fp12) + n, 2 * b->part_host_cap);
+    HIP_CHECK(c, hipHostMalloc((void**)&b->part_host, cap, hipHostMallocDefault));
+    b->part_host_cap = cap;
   }
   HIP_CHECK(c, hipSetDevice(c->device));
   hipStream_t s = c->stream;
@@ -564,19 +581,29 @@ static int vs_partial_run(gbv_ctx* c, gbv_vs_batch* b, uint8_t out576[GBV_FP12_P
   // the reduction is a tree over 64-set blocks (k_sm_seg_reduce, k_sm_part_reduce)
   launch_sm_seg_check(LaunchCfg{1, 64, s}, 0, (uint32_t)n, b->status, b->F, b->rS, b->Fpart, b->Spart, b->has, b->flag, b->f_out);
   HIP_CHECK_DRAIN(c, hipGetLastError());
-  uint8_t* h = nullptr;
-  if ((rc = ctx_small_host(c, sizeof(Fp12) + n, &h))) {
-    ctx_drain(c);
-    return rc;
+  HIP_CHECK_DRAIN(c, hipMemcpyAsync(b->part_host, b->f_out, sizeof(Fp12), hipMemcpyDeviceToHost, s));
+  HIP_CHECK_DRAIN(c, hipMemcpyAsync(b->part_host + sizeof(Fp12), b->status, n, hipMemcpyDeviceToHost, s));
+  HIP_CHECK_DRAIN(c, hipEventRecord(b->done, s));
+  return GBV_OK;
+}
+
+static int vs_partial_collect(gbv_ctx* c, gbv_vs_batch* b, uint8_t out576[GBV_FP12_PARTIAL_BYTES], uint8_t* shard_ok) {
+  if (b->part_empty) {
+    fp12_pack(out576, fp12_one_host());
+    return GBV_OK;
   }
-  HIP_CHECK_DRAIN(c, hipMemcpyAsync(h, b->f_out, sizeof(Fp12), hipMemcpyDeviceToHost, s));
-  HIP_CHECK_DRAIN(c, hipMemcpyAsync(h + sizeof(Fp12), b->status, n, hipMemcpyDeviceToHost, s));
-  HIP_CHECK_DRAIN(c, hipStreamSynchronize(s));
+  HIP_CHECK(c, hipSetDevice(c->device));
+  const hipError_t we = hipEventSynchronize(b->done);  // no context lock held
+  if (we != hipSuccess) {
+    GBV_LOCK(c);
+    return gbv_fail(c, GBV_E_DEVICE, std::string("hipEventSynchronize: ") + hipGetErrorString(we));
+  }
   Fp12 f;
-  memcpy((void*)&f, h, sizeof(Fp12));
+  memcpy((void*)&f, b->part_host, sizeof(Fp12));
   fp12_pack(out576, f);
-  for (size_t i = 0; i < n; ++i)
-    if (h[sizeof(Fp12) + i] != SET_OK) *shard_ok = 0;
+  const uint8_t* st = b->part_host + sizeof(Fp12);
+  for (size_t i = 0; i < b->n; ++i)
+    if (st[i] != SET_OK) *shard_ok = 0;
   return GBV_OK;
 }
 

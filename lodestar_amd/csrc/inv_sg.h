@@ -11,9 +11,31 @@
 // Montgomery-style correction per batch (the matrix divides by 2^62).
 //
 // The algorithm: D. J. Bernstein, B.-Y. Yang, "Fast constant-time gcd computation and modular
-// inversion" (2019), in its variable-time form with eta = -delta and 62-step batches as documented for
-// libsecp256k1's modinv64 (Wuille, "safegcd implementation notes").  Written for BLS12-381's p here;
-// checked against the oracle by tests/test_host_arith.py (the same code compiled for the host).
+// inversion" (2019), in its variable-time form with eta = -delta and 62-step batches.  Checked against
+// the oracle by tests/test_host_arith.py (the same code compiled for the host).
+//
+// Attribution.  divsteps_62_var, update_de_62, update_fg_62 and the limb-length reduction of
+// inv_var below follow libsecp256k1's src/modinv64_impl.h (secp256k1_modinv64_divsteps_62_var,
+// _update_de_62, _update_fg_62, _modinv64_var), re-parameterised for BLS12-381's p (7 signed
+// 62-bit limbs, p^-1 mod 2^62) and for device code.  That file is distributed under the MIT license:
+//
+//   Copyright (c) 2020 Peter Dettman
+//   Copyright (c) 2013 Pieter Wuille and the libsecp256k1 contributors
+//
+//   Permission is hereby granted, free of charge, to any person obtaining a copy of this software
+//   and associated documentation files (the "Software"), to deal in the Software without
+//   restriction, including without limitation the rights to use, copy, modify, merge, publish,
+//   distribute, sublicense, and/or sell copies of the Software, and to permit persons to whom the
+//   Software is furnished to do so, subject to the following conditions:
+//
+//   The above copyright notice and this permission notice shall be included in all copies or
+//   substantial portions of the Software.
+//
+//   THE SOFTWARE IS PROVIDED "AS IS", WITHOUT WARRANTY OF ANY KIND, EXPRESS OR IMPLIED, INCLUDING
+//   BUT NOT LIMITED TO THE WARRANTIES OF MERCHANTABILITY, FITNESS FOR A PARTICULAR PURPOSE AND
+//   NONINFRINGEMENT. IN NO EVENT SHALL THE AUTHORS OR COPYRIGHT HOLDERS BE LIABLE FOR ANY CLAIM,
+//   DAMAGES OR OTHER LIABILITY, WHETHER IN AN ACTION OF CONTRACT, TORT OR OTHERWISE, ARISING FROM,
+//   OUT OF OR IN CONNECTION WITH THE SOFTWARE OR THE USE OR OTHER DEALINGS IN THE SOFTWARE.
 #pragma once
 #include "fp_types.h"
 #include "bls_constants.h"

@@ -1,9 +1,4 @@
-// hash_to_G2 kernels.  The few-message forms are latency-bound (lane pairs, one wave per message):
-// GBV_HASH_CHAINS accumulator chains per product column (fp.h GBV_MUL28_CHAINS) for A/B builds.
-#ifndef GBV_HASH_CHAINS
-#define GBV_HASH_CHAINS 1
-#endif
-#define GBV_MUL28_CHAINS GBV_HASH_CHAINS
+// hash_to_G2 kernels.  The few-message forms are latency-bound (lane pairs, one wave per message).
 #include "launch.h"
 #include "kernel_common.h"
 
@@ -49,14 +44,13 @@ __global__ void GBV_KERNEL_ATTR k_util_g2_out(uint32_t n, const G2A* __restrict_
 
 
 void launch_hash_msgs(LaunchCfg c, const uint8_t* msgs32, uint32_t n, G2A* H, G2J* Qpre) {
-  static const uint32_t coop_max = getenv("GBV_HASH_COOP_MAX") ? (uint32_t)atoi(getenv("GBV_HASH_COOP_MAX")) : 256;
-  if (Qpre && n <= coop_max) {  // latency: lane-pair maps, then the cofactor clearing one wave per message
+  if (Qpre && n <= tuning().hash_coop_max) {  // latency: lane-pair maps, then the cofactor clearing one wave per message
     hipLaunchKernelGGL(k_hash_msgs_pre, dim3((2 * n + 63) / 64), dim3(64), 0, c.stream, msgs32, n, Qpre);
     debug_sync(c.stream, "k_hash_msgs_pre");
     launch_hash_clear_coop(c.stream, n, Qpre, H);
     return;
   }
-  if (n <= hash_pair_max())  // latency: lane pairs (grid sized here; c.blocks is for one lane per message)
+  if (n <= tuning().hash_pair_max)  // latency: lane pairs (grid sized here; c.blocks is for one lane per message)
     hipLaunchKernelGGL(k_hash_msgs_pair, dim3((2 * n + 63) / 64), dim3(64), 0, c.stream, msgs32, n, H);
   else
     hipLaunchKernelGGL(k_hash_msgs, dim3(c.blocks), dim3(c.threads), 0, c.stream, msgs32, n, H);

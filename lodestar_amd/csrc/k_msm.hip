@@ -96,17 +96,6 @@ __device__ inline G2A msm_entry_point(uint32_t v, uint32_t s0, const G2A* __rest
   return q;
 }
 
-// One thread per bucket: B_key = sum of its entries' (signed) points (GBV_MSM_RUNS=0 variant).
-__global__ void GBV_KERNEL_ATTR k_msm_buckets(uint32_t s0, const uint32_t* __restrict__ off, const uint32_t* __restrict__ end,
-                                              const uint32_t* __restrict__ ent, const G2A* __restrict__ S, G2J* __restrict__ B) {
-  uint32_t key = blockIdx.x * blockDim.x + threadIdx.x;
-  if (key >= MSM_KEYS) return;
-  G2J acc = jac_infinity<Fp2>();
-  for (uint32_t e = off[key], e1 = end[key]; e < e1; ++e)
-    acc = jac_add_aff(acc, msm_entry_point(ent[e], s0, S));  // inlined: a call would move acc through scratch
-  B[key] = acc;
-}
-
 // One thread per run of MSM_RUN consecutive sorted entries, so every lane does the same number of
 // additions whatever the bucket sizes (window-0 digits are all odd: half those buckets are empty,
 // the others hold twice the mean).  A bucket lying inside the run is written to B directly; a
@@ -228,17 +217,11 @@ void launch_msm_g2_buckets(hipStream_t s, uint32_t s0, uint32_t n, const uint32_
   debug_sync(s, "k_msm_scan");
   hipLaunchKernelGGL(k_msm_entries<true>, dim3(eb), dim3(64), 0, s, s0, n, set_grp, status, grp_state, seed, nonce, cur, ent);
   debug_sync(s, "k_msm_entries<scatter>");
-  static const bool per_bucket = getenv("GBV_MSM_RUNS") && atoi(getenv("GBV_MSM_RUNS")) == 0;
-  if (per_bucket) {
-    hipLaunchKernelGGL(k_msm_buckets, dim3(MSM_KEYS / 64), dim3(64), 0, s, s0, off, cur, ent, S, buckets);
-    debug_sync(s, "k_msm_buckets");
-  } else {
-    uint32_t runs = (uint32_t)((4ull * n + MSM_RUN - 1) / MSM_RUN);  // upper bound; runs past the end exit
-    hipLaunchKernelGGL(k_msm_runs, dim3((runs + 63) / 64), dim3(64), 0, s, s0, off, cur, ent, S, buckets, head, tail);
-    debug_sync(s, "k_msm_runs");
-    hipLaunchKernelGGL(k_msm_fixup, dim3(MSM_KEYS / 64), dim3(64), 0, s, off, cur, head, tail, buckets);
-    debug_sync(s, "k_msm_fixup");
-  }
+  const uint32_t runs = (uint32_t)((4ull * n + MSM_RUN - 1) / MSM_RUN);  // upper bound; runs past the end exit
+  hipLaunchKernelGGL(k_msm_runs, dim3((runs + 63) / 64), dim3(64), 0, s, s0, off, cur, ent, S, buckets, head, tail);
+  debug_sync(s, "k_msm_runs");
+  hipLaunchKernelGGL(k_msm_fixup, dim3(MSM_KEYS / 64), dim3(64), 0, s, off, cur, head, tail, buckets);
+  debug_sync(s, "k_msm_fixup");
 }
 
 void launch_msm_g2_reduce(hipStream_t s, const G2J* buckets, G2J* part, G2J* total) {

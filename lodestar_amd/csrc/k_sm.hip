@@ -4,12 +4,6 @@
 #include "launch.h"
 #include "kernel_common.h"
 
-#ifndef GBV_DEC_SPLIT_DEFAULT
-#define GBV_DEC_SPLIT_DEFAULT 1
-#endif
-#ifndef GBV_SUB_SPLIT_DEFAULT
-#define GBV_SUB_SPLIT_DEFAULT 0
-#endif
 
 namespace gbv {
 
@@ -40,9 +34,9 @@ constexpr unsigned SCAN_W = 8;  // lanes per scan group (power of two, <= 64)
 // additions) and the first lane of every chunk segment in the group writes the segment's sum at
 // its own set index; k_sm_chunk_finish adds the <= ceil(len/SCAN_W)+1 segment sums of a chunk.
 //
-// PRE: the signatures were decoded by k_sig_decode (k_dec.hip): status[i] holds the decode code and
-// S_out[i] the point, so this kernel starts at the subgroup check.
-template <bool WITH_G2, bool PRE>
+// The signatures were decoded by k_sig_decode (k_dec.hip, its own kernel at a higher occupancy):
+// status[i] holds the decode code and S_out[i] the point, so this kernel starts at the subgroup check.
+template <bool WITH_G2>
 __global__ void GBV_KERNEL_ATTR k_sm_prepare(uint32_t base, uint32_t n, const uint32_t* __restrict__ idx, const uint8_t* __restrict__ sig96,
                                              const uint32_t* __restrict__ set_grp, const G1A* __restrict__ table,
                                              const uint8_t* __restrict__ table_ok, uint32_t table_n, const uint4* __restrict__ comb,
@@ -60,17 +54,11 @@ __global__ void GBV_KERNEL_ATTR k_sm_prepare(uint32_t base, uint32_t n, const ui
     uint8_t st = SET_OK;
     if (k >= table_n || !table_ok[k]) st = SET_BAD_PK;
     G2A s;
-    uint8_t ds;
-    if (PRE) {
-      ds = status[i];
-      if (ds == PT_OK) s = S_out[i];
-    } else {
-      ds = g2_decode(s, sig96 + 96ull * i, 96);
-    }
+    const uint8_t ds = status[i];
+    if (ds == PT_OK) s = S_out[i];
     if (ds != PT_OK || !g2_in_subgroup(s)) st = SET_BAD_SIG;
     status[i] = st;
     if (st == SET_OK) {
-      if (!PRE) S_out[i] = s;
       uint64_t r = prf_scalar(seed, i, nonce);
       if (comb && comb_ok[k]) {  // r pk from the validator's comb table (curve.h comb_mul)
         rp = comb_mul(comb + (size_t)k * (COMB_ENTRIES * COMB_U4), (uint32_t)r, (uint32_t)(r >> 32));
@@ -107,58 +95,6 @@ __global__ void GBV_KERNEL_ATTR k_sm_prepare(uint32_t base, uint32_t n, const ui
     if (WITH_G2) Sh_out[i] = rs;
     Ph_out[i] = rp;
   }
-}
-
-// The G1-only throughput form (bucket-MSM segments) in two more kernels after k_sig_decode, each
-// with the registers of its own phase: the G2 subgroup check (the long chain: 63 Jacobian doublings
-// over Fp2, two waves per SIMD) only writes the status byte; r_i pk_i from the comb table and the
-// 8-lane chunk scan (G1 points: a small live state) run after it at a higher occupancy.  Same r_i,
-// statuses, scan and outputs as k_sm_prepare<false, true>.
-#ifndef GBV_SUB_WAVES
-#define GBV_SUB_WAVES GBV_WAVES_PER_EU
-#endif
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GBV_SUB_WAVES))) k_sm_subgroup(uint32_t base, uint32_t n, const uint32_t* __restrict__ idx, const uint8_t* __restrict__ table_ok,
-                                              uint32_t table_n, const G2A* __restrict__ S, uint8_t* __restrict__ status) {
-  const uint32_t t = blockIdx.x * 64 + threadIdx.x;
-  if (t >= n) return;
-  const uint32_t i = base + t;
-  const uint32_t k = idx[i];
-  uint8_t st = (k >= table_n || !table_ok[k]) ? SET_BAD_PK : SET_OK;
-  const uint8_t ds = status[i];
-  if (ds != PT_OK || !g2_in_subgroup(S[i])) st = SET_BAD_SIG;
-  status[i] = st;
-}
-
-#ifndef GBV_RPK_WAVES
-#define GBV_RPK_WAVES 2
-#endif
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GBV_RPK_WAVES)))
-k_sm_rpk(uint32_t base, uint32_t n, const uint32_t* __restrict__ idx, const uint32_t* __restrict__ set_grp, const G1A* __restrict__ table,
-         const uint4* __restrict__ comb, const uint8_t* __restrict__ comb_ok, Seed seed, uint32_t nonce, G1J* __restrict__ Ph_out,
-         const uint8_t* __restrict__ status) {
-  const unsigned lane = threadIdx.x;
-  const uint32_t t = blockIdx.x * 64 + lane;
-  const bool act = t < n;
-  const uint32_t i = base + t;
-  const uint32_t key = act ? set_grp[i] : 0xffffffffu;
-  G1J rp = jac_infinity<Fp>();
-  if (act && status[i] == SET_OK) {
-    const uint32_t k = idx[i];
-    const uint64_t r = prf_scalar(seed, i, nonce);
-    if (comb && comb_ok[k]) {
-      rp = comb_mul(comb + (size_t)k * (COMB_ENTRIES * COMB_U4), (uint32_t)r, (uint32_t)(r >> 32));
-    } else {
-      const G1A pk = table[k];
-      if (!randomize_g1(pk, r, &rp)) rp = g1_mul_u64(pk, r);
-    }
-  }
-  for (unsigned d = 1; d < SCAN_W; d <<= 1) {
-    const G1J po = shfl_down_jac(rp, d);
-    const uint32_t ko = __shfl_down(key, d, 64);
-    if ((lane & (SCAN_W - 1)) + d < SCAN_W && ko == key) rp = jac_add(rp, po);
-  }
-  const uint32_t kprev = __shfl_up(key, 1, 64);
-  if (act && ((lane & (SCAN_W - 1)) == 0 || kprev != key)) Ph_out[i] = rp;
 }
 
 // Latency form of k_sm_prepare<true> for segments of few sets (a lone gossip call): TWO waves per 64
@@ -606,43 +542,26 @@ void launch_sm_prepare(LaunchCfg c, uint32_t base, uint32_t n, const uint32_t* i
                        const Seed& seed, uint32_t nonce, G2A* S_out, G2J* Sh, G1J* Ph, uint8_t* status, uint8_t* scratch8) {
   // Sh == nullptr: G1 terms only (the segment's G2 sum comes from the bucket MSM); comb == nullptr:
   // no comb tables (GBV_COMB=0 or not built), the ladder forms r pk
-  static const uint32_t split_max = getenv("GBV_PREPARE_SPLIT_MAX") ? (uint32_t)atoi(getenv("GBV_PREPARE_SPLIT_MAX")) : 2048;
-  // throughput forms: decompression first as its own kernel at a higher occupancy (k_dec.hip),
-  // unless GBV_DEC_SPLIT=0 (A/B)
-  static const bool dec_split = getenv("GBV_DEC_SPLIT") ? atoi(getenv("GBV_DEC_SPLIT")) != 0 : GBV_DEC_SPLIT_DEFAULT != 0;
-  // and, for the G1-only form, the subgroup check apart from r pk (GBV_SUB_SPLIT=0: one kernel, A/B)
-  static const bool sub_split = getenv("GBV_SUB_SPLIT") ? atoi(getenv("GBV_SUB_SPLIT")) != 0 : GBV_SUB_SPLIT_DEFAULT != 0;
   const dim3 grid((n + 63) / 64);
-  // latency, few sets: decode, then the subgroup checks one wave per set beside the randomisation,
-  // then the verdicts and the scan (GBV_PREP_COOP=0: k_sm_prepare_split's two waves per 64 sets)
-  static const bool prep_coop = !(getenv("GBV_PREP_COOP") && atoi(getenv("GBV_PREP_COOP")) == 0);
-  if (Sh && n <= split_max && prep_coop && scratch8) {
+  if (Sh && n <= tuning().prepare_split_max && scratch8) {
+    // latency, few sets: decode, then the subgroup checks one wave per set beside the randomisation,
+    // then the verdicts and the scan
     launch_sig_decode(c.stream, base, n, sig96, S_out, status);
     launch_sm_prep_roles(c.stream, base, n, idx, table, table_ok, table_n, comb, comb_ok, seed, nonce, S_out, status, scratch8, Sh, Ph);
     hipLaunchKernelGGL(k_sm_prep_scan, grid, dim3(64), 0, c.stream, base, n, idx, set_grp, table_ok, table_n, scratch8, status, Sh, Ph);
     debug_sync(c.stream, "k_sm_prep_scan");
-  } else if (Sh && n <= split_max) {  // latency: two waves per 64 sets
+  } else if (Sh && n <= tuning().prepare_split_max) {  // latency: two waves per 64 sets
     hipLaunchKernelGGL(k_sm_prepare_split, dim3((n + 63) / 64), dim3(128), 0, c.stream, base, n, idx, sig96, set_grp, table, table_ok, table_n,
                        comb, comb_ok, seed, nonce, S_out, Sh, Ph, status);
-  } else if (dec_split && !Sh && sub_split) {  // decode, subgroup check, r pk + scan
-    launch_sig_decode(c.stream, base, n, sig96, S_out, status);
-    hipLaunchKernelGGL(k_sm_subgroup, grid, dim3(64), 0, c.stream, base, n, idx, table_ok, table_n, S_out, status);
-    debug_sync(c.stream, "k_sm_subgroup");
-    hipLaunchKernelGGL(k_sm_rpk, grid, dim3(64), 0, c.stream, base, n, idx, set_grp, table, comb, comb_ok, seed, nonce, Ph, status);
-  } else if (dec_split) {
+  } else {
+    // throughput: decompression first as its own kernel at a higher occupancy (k_dec.hip)
     launch_sig_decode(c.stream, base, n, sig96, S_out, status);
     if (Sh)
-      hipLaunchKernelGGL((k_sm_prepare<true, true>), grid, dim3(64), 0, c.stream, base, n, idx, sig96, set_grp, table, table_ok, table_n,
-                         comb, comb_ok, seed, nonce, S_out, Sh, Ph, status);
+      hipLaunchKernelGGL((k_sm_prepare<true>), grid, dim3(64), 0, c.stream, base, n, idx, sig96, set_grp, table, table_ok, table_n, comb,
+                         comb_ok, seed, nonce, S_out, Sh, Ph, status);
     else
-      hipLaunchKernelGGL((k_sm_prepare<false, true>), grid, dim3(64), 0, c.stream, base, n, idx, sig96, set_grp, table, table_ok, table_n,
-                         comb, comb_ok, seed, nonce, S_out, Sh, Ph, status);
-  } else if (Sh) {
-    hipLaunchKernelGGL((k_sm_prepare<true, false>), grid, dim3(64), 0, c.stream, base, n, idx, sig96, set_grp, table, table_ok, table_n,
-                       comb, comb_ok, seed, nonce, S_out, Sh, Ph, status);
-  } else {
-    hipLaunchKernelGGL((k_sm_prepare<false, false>), grid, dim3(64), 0, c.stream, base, n, idx, sig96, set_grp, table, table_ok,
-                       table_n, comb, comb_ok, seed, nonce, S_out, Sh, Ph, status);
+      hipLaunchKernelGGL((k_sm_prepare<false>), grid, dim3(64), 0, c.stream, base, n, idx, sig96, set_grp, table, table_ok, table_n, comb,
+                         comb_ok, seed, nonce, S_out, Sh, Ph, status);
   }
   debug_sync(c.stream, "k_sm_prepare");
 }
@@ -659,8 +578,7 @@ void launch_sm_chunk_finish_s(LaunchCfg c, uint32_t g0, uint32_t G, uint32_t s0,
 }
 void launch_sm_chunk_finish(LaunchCfg c, uint32_t g0, uint32_t G, uint32_t s0, const uint32_t* grp_off, const uint8_t* status, const G2J* Sh,
                             const G1J* Ph, G1J* PgJ, G2J* SgJ, uint8_t* grp_state, uint32_t* n_fallback) {
-  static const uint32_t wave_max = getenv("GBV_CHUNK_FINISH_WAVE_MAX") ? (uint32_t)atoi(getenv("GBV_CHUNK_FINISH_WAVE_MAX")) : 32;
-  if (G <= wave_max)  // latency (a lone call): a wave per chunk, tree over its group sums
+  if (G <= tuning().chunk_finish_wave_max)  // latency (a lone call): a wave per chunk, tree over its group sums
     hipLaunchKernelGGL(k_sm_chunk_finish_wave, dim3(G), dim3(64), 0, c.stream, g0, s0, grp_off, status, Sh, Ph, PgJ, SgJ, grp_state,
                        n_fallback);
   else

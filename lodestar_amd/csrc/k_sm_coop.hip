@@ -1,12 +1,6 @@
 // Same-message path kernels built on the wave-cooperative pairing arithmetic (coop.h): one
 // workgroup = one wave = one pairing job.  Kept in their own translation unit so their small
 // register budget (one Fp product per lane) is not merged with the thread-per-set kernels'.
-// The cooperative kernels run one wave per pairing (latency): GBV_COOP_CHAINS accumulator chains per
-// product column (fp.h GBV_MUL28_CHAINS) for A/B builds.
-#ifndef GBV_COOP_CHAINS
-#define GBV_COOP_CHAINS 1
-#endif
-#define GBV_MUL28_CHAINS GBV_COOP_CHAINS
 #include <cstdlib>
 
 #include "launch.h"
@@ -411,50 +405,10 @@ void launch_sm_prep_roles(hipStream_t s, uint32_t base, uint32_t n, const uint32
                           uint32_t table_n, const uint4* comb, const uint8_t* comb_ok, const Seed& seed, uint32_t nonce, const G2A* S,
                           const uint8_t* status, uint8_t* sub_ok, G2J* Sh, G1J* Ph) {
   // a wave per set costs ~25x the CU time of a lane per set: worth it while the waves fit the chip at once
-  static const uint32_t coop_rand_max = getenv("GBV_PREP_COOP_RAND") ? (uint32_t)atoi(getenv("GBV_PREP_COOP_RAND")) : 512;
-  const int coop_rand = n <= coop_rand_max;
+  const int coop_rand = n <= tuning().prep_coop_rand_max;
   hipLaunchKernelGGL(k_sm_prep_roles, dim3(n + (coop_rand ? n : 0) + (n + 63) / 64), dim3(64), 0, s, base, n, idx, table, table_ok, table_n,
                      comb, comb_ok, seed, nonce, S, status, sub_ok, Sh, Ph, coop_rand);
   debug_sync(s, "k_sm_prep_roles");
-}
-
-// k_vs_sig_pre (k_vs.hip) for few sets: the same two roles with a wave per set and role -- blocks
-// [0, n) decode signature i and run the subgroup check on the cooperative point doublings (as
-// k_sm_prep_roles), blocks [n, 2n) decode it and form r_i sig_i by coop::mul_2d_point (the same
-// scalar as randomize_g2).  Every lane decodes (the same bytes: a uniform verdict), so the whole
-// wave takes the same branches.
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
-k_vs_sig_pre_coop(uint32_t n, const uint8_t* __restrict__ sig, uint32_t sig_stride, const uint32_t* __restrict__ sig_len, Seed seed,
-                  uint32_t nonce, G2J* __restrict__ rS_out, uint8_t* __restrict__ status, uint8_t* __restrict__ sig_st) {
-  __shared__ coop::Slot ws[coop::MILLER_WS];
-  const bool rand = blockIdx.x >= n;
-  const uint32_t i = rand ? blockIdx.x - n : blockIdx.x;
-  G2A s;
-  const bool ok = g2_decode(s, sig + (size_t)sig_stride * i, sig_len[i]) == PT_OK;
-  if (!rand) {
-    bool in = false;
-    if (ok) {
-      coop::load_consts();
-      coop::mul_xabs_point(ws, s);
-      in = jac_eq_aff(jac_neg(coop::point_jac(ws)), g2_psi(s));
-    }
-    if (threadIdx.x == 0) {
-      const uint8_t st = in ? SET_OK : SET_BAD_SIG;
-      status[i] = st;
-      sig_st[i] = st;
-    }
-    return;
-  }
-  if (!ok) return;
-  const uint64_t r = prf_scalar(seed, i, nonce);
-  coop::load_consts();
-  coop::mul_2d_point(ws, s, g2_neg_psi2(s), (uint32_t)r, (uint32_t)(r >> 32));
-  if (threadIdx.x == 0) rS_out[i] = coop::point_jac(ws);
-}
-void launch_vs_sig_pre_coop(hipStream_t s, uint32_t n, const uint8_t* sig, uint32_t sig_stride, const uint32_t* sig_len, const Seed& seed,
-                            uint32_t nonce, G2J* rS, uint8_t* status, uint8_t* sig_st) {
-  hipLaunchKernelGGL(k_vs_sig_pre_coop, dim3(2 * n), dim3(64), 0, s, n, sig, sig_stride, sig_len, seed, nonce, rS, status, sig_st);
-  debug_sync(s, "k_vs_sig_pre_coop");
 }
 
 // e(P, Q) * e(-g1, S) == 1 by one wave (S = infinity drops the second pair).  Arguments must be
@@ -596,15 +550,13 @@ k_sm_fb_sets_fe(const uint32_t* __restrict__ set_list, const uint32_t* __restric
 void launch_sm_fb_blocks_coop(LaunchCfg c, const uint4* runs, const uint32_t* n_runs, uint32_t cap, const uint8_t* status,
                               const uint32_t* grp_msg, const G2J* Sh, const G1J* Ph, const G2A* H, uint8_t* valid, uint32_t* set_list,
                               uint32_t* n_list) {
-  static const int direct = !(getenv("GBV_FB_DIRECT") && atoi(getenv("GBV_FB_DIRECT")) == 0);
   hipLaunchKernelGGL(k_sm_fb_blocks_coop, dim3(FB_COOP_MAX), dim3(64), 0, c.stream, runs, n_runs, cap, status, grp_msg, Sh, Ph, H, valid,
-                     set_list, n_list, direct);
+                     set_list, n_list, 1);
   debug_sync(c.stream, "k_sm_fb_blocks_coop");
 }
 void launch_sm_fb_sets_coop(LaunchCfg c, const uint32_t* set_list, const uint32_t* n_list, const uint32_t* set_grp, const uint32_t* grp_msg,
                             const uint32_t* idx, const G1A* table, const G2A* S, const G2A* H, uint8_t* valid, Fp12* Fpair) {
-  static const bool one_wave = getenv("GBV_GROUP_PAIRING_1W") && atoi(getenv("GBV_GROUP_PAIRING_1W")) != 0;
-  if (Fpair && !one_wave) {  // 2 * FB_COOP_MAX Fp12 of scratch
+  if (Fpair) {  // 2 * FB_COOP_MAX Fp12 of scratch
     hipLaunchKernelGGL(k_sm_fb_sets_miller2, dim3(FB_COOP_MAX, 2), dim3(64), 0, c.stream, set_list, n_list, set_grp, grp_msg, idx, table, S, H,
                        Fpair);
     debug_sync(c.stream, "k_sm_fb_sets_miller2");
@@ -627,8 +579,7 @@ void launch_sm_seg_check(LaunchCfg c, uint32_t g0, uint32_t G, uint8_t* grp_stat
 }
 void launch_sm_group_pairing(LaunchCfg c, uint32_t g0, uint32_t G, const uint32_t* grp_msg, const G1J* PgJ, const G2J* SgJ, const G2A* H,
                              const uint8_t* seg_ok, uint8_t* grp_state, uint32_t* n_fallback, Fp12* Fpair, uint8_t* pair_ok) {
-  static const bool one_wave = getenv("GBV_GROUP_PAIRING_1W") && atoi(getenv("GBV_GROUP_PAIRING_1W")) != 0;
-  if (one_wave || !Fpair) {
+  if (!Fpair) {
     hipLaunchKernelGGL(k_sm_group_pairing, dim3(G), dim3(64), 0, c.stream, g0, grp_msg, PgJ, SgJ, H, seg_ok, grp_state, n_fallback);
     debug_sync(c.stream, "k_sm_group_pairing");
     return;

@@ -372,7 +372,7 @@ void launch_vs_hash_sig(hipStream_t s, uint32_t n, const uint8_t* msgs32, const 
                         const uint8_t* raw_flag, const uint8_t* raw_pk48, const uint8_t* sig, uint32_t sig_stride, const uint32_t* sig_len,
                         const G1A* table, const uint8_t* table_ok, const G1J* pk_agg, const uint8_t* pk_st, const Seed& seed,
                         uint32_t nonce, G2A* H, G1J* rP, G2J* rS, uint8_t* status, bool split) {
-  const uint32_t pair = n <= hash_pair_max() ? 1u : 0u;
+  const uint32_t pair = n <= tuning().hash_pair_max ? 1u : 0u;
   const uint32_t nsig = (n + 63) / 64;
   const uint32_t nb = split ? 0u : pair ? (2 * n + 63) / 64 : (n + 63) / 64;  // split: the caller hashes
   hipLaunchKernelGGL(k_vs_hash_sig, dim3(nb + (split ? 2 : 1) * nsig), dim3(64), 0, s, n, nb, pair, split ? 1u : 0u, msgs32, set_off,
@@ -382,14 +382,6 @@ void launch_vs_hash_sig(hipStream_t s, uint32_t n, const uint8_t* msgs32, const 
 
 void launch_vs_sig_pre(hipStream_t s, uint32_t n, const uint8_t* sig, uint32_t sig_stride, const uint32_t* sig_len, const Seed& seed,
                        uint32_t nonce, G2J* rS, uint8_t* status, uint8_t* sig_st) {
-  // few sets: a wave per set and role on the cooperative point steps (k_sm_coop.hip).  Off by default:
-  // it shortens the signature chain (C1 hash_sig 4.1 -> 3.3-4.0 ms) but not the call, and an Electra
-  // block got slower (10.3 -> 12.3 ms) with its waves beside the aggregation (profiles/r03_ab/ab_vscoop)
-  static const uint32_t coop_max = getenv("GBV_VS_PRE_COOP") ? (uint32_t)atoi(getenv("GBV_VS_PRE_COOP")) : 0;
-  if (n <= coop_max) {
-    launch_vs_sig_pre_coop(s, n, sig, sig_stride, sig_len, seed, nonce, rS, status, sig_st);
-    return;
-  }
   const uint32_t nsig = (n + 63) / 64;
   hipLaunchKernelGGL(k_vs_sig_pre, dim3(2 * nsig), dim3(64), 0, s, n, sig, sig_stride, sig_len, seed, nonce, rS, status, sig_st);
   debug_sync(s, "k_vs_sig_pre");

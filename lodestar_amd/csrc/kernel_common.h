@@ -54,12 +54,26 @@ enum : uint8_t { GRP_PENDING = 0, GRP_FALLBACK = 1, GRP_OK = 2 };
 constexpr uint32_t FB_COOP_MAX = 256;
 // Sets per failure-path run (the 8-set scan windows of k_sm_prepare).  When the failing runs hold at
 // most FB_COOP_MAX sets in all, k_sm_fb_blocks_coop skips the run checks and hands every set to the
-// per-set stage: one pairing stage of latency instead of two (GBV_FB_DIRECT=0: always two).
+// per-set stage: one pairing stage of latency instead of two.
 constexpr uint32_t FB_RUN_MAX = 8;
 // Message counts up to which hash_to_G2 runs on lane pairs (latency) instead of one lane each.
 constexpr uint32_t HASH_PAIR_MAX = 4096;
-// HASH_PAIR_MAX, overridable for A/B runs (GBV_HASH_PAIR_MAX); host side only
-uint32_t hash_pair_max();
+
+// Launch-shape tunables (host side only).  Read ONCE, from GBV_* environment variables, by the first
+// gbv_init of the process (tuning_load); the launchers only read this struct, so nothing in a submit
+// path consults the environment.  Defaults are the measured choices of DESIGN.md section 7.
+struct Tuning {
+  uint32_t hash_pair_max = HASH_PAIR_MAX;  // GBV_HASH_PAIR_MAX: hash on lane pairs up to this many messages
+  uint32_t hash_coop_max = 256;            // GBV_HASH_COOP_MAX: cooperative cofactor clearing up to this many
+  uint32_t prepare_split_max = 2048;       // GBV_PREPARE_SPLIT_MAX: same-message latency prepare up to this many sets
+  uint32_t prep_coop_rand_max = 512;       // GBV_PREP_COOP_RAND: r sig one wave per set up to this many sets
+  uint32_t chunk_finish_wave_max = 32;     // GBV_CHUNK_FINISH_WAVE_MAX: chunk sums one wave per chunk up to this many
+  uint32_t vs_pre_max = 16384;             // GBV_VS_PRE_MAX: verifySignatureSets signature half beside the aggregation
+  uint32_t vs_fs_maxc = 256;               // GBV_VS_FS_MAXC: per-chunk (-g1, sum) Miller value beside the per-set ones
+  uint32_t sync_debug = 0;                 // GBV_SYNC_DEBUG: synchronise + report after every launch (debugging)
+};
+const Tuning& tuning();
+void tuning_load();
 // verifySignatureSets passes up to this many sets compute their Miller values one wave per set
 // (cooperative, ~2.9 ms) instead of one thread per set (~16 ms of latency, far less VALU in total).
 constexpr uint32_t VS_COOP_MILLER_MAX = 2048;

@@ -106,8 +106,6 @@ void launch_vs_hash_sig(hipStream_t s, uint32_t n, const uint8_t* msgs32, const 
 // aggregation, then the pubkeys (k_vs.hip)
 void launch_vs_sig_pre(hipStream_t s, uint32_t n, const uint8_t* sig, uint32_t sig_stride, const uint32_t* sig_len, const Seed& seed,
                        uint32_t nonce, G2J* rS, uint8_t* status, uint8_t* sig_st);
-void launch_vs_sig_pre_coop(hipStream_t s, uint32_t n, const uint8_t* sig, uint32_t sig_stride, const uint32_t* sig_len, const Seed& seed,
-                            uint32_t nonce, G2J* rS, uint8_t* status, uint8_t* sig_st);
 void launch_vs_pk_rand(hipStream_t s, uint32_t n, const uint32_t* set_off, const uint32_t* arena, const uint8_t* raw_flag,
                        const uint8_t* raw_pk48, const G1A* table, const uint8_t* table_ok, const G1J* pk_agg, const uint8_t* pk_st,
                        const Seed& seed, uint32_t nonce, G1J* rP, uint8_t* status);

@@ -6,10 +6,6 @@
 #include "fp12.h"
 #include "curve.h"
 
-#ifndef GBV_MILLER_FUSED
-#define GBV_MILLER_FUSED 0  // 1: square and doubling-line product in one call (miller_loop_1j_to)
-#endif
-
 namespace gbv {
 
 struct G2Proj { Fp2 x, y, z; };
@@ -118,12 +114,8 @@ GBV_NI void miller_loop_1j_to(Fp12* out, G1J P, G2A Q0) {
   for (int i = 62; i >= 0; --i) {
     l = dbl_step(T0, nxz, P.y);
     l.c0 = fp2_mul_fp(l.c0, z3);
-    if (GBV_MILLER_FUSED && i != 62) {
-      fp12_sqr_mul_line_to(&f, &l);
-    } else {
-      if (i != 62) fp12_sqr_to(&f, &f);
-      fp12_mul_line_to(&f, &l);
-    }
+    if (i != 62) fp12_sqr_to(&f, &f);
+    fp12_mul_line_to(&f, &l);
     if ((X_ABS >> i) & 1ull) {
       l = add_step(T0, Q0, nxz, P.y);
       l.c0 = fp2_mul_fp(l.c0, z3);

@@ -197,6 +197,11 @@ class GpuBlsVerifier:
         """True when r*pk comes from the per-slot comb tables (12 KB of HBM per validator)."""
         return bool(self._lib.gbv_comb_enabled(self._ctx))
 
+    def tune(self, name: str, value: int):
+        """Change a pipeline setting of this context (gbv_tune: "msm_min", "msm_cooldown",
+        "segments"); booleans are identical for every value (tests reach each pipeline form)."""
+        _native.check(self._lib, self._ctx, self._lib.gbv_tune(self._ctx, name.encode(), int(value)))
+
     def aggregate_pubkeys(self, indices: Sequence[int]) -> bytes:
         """aggregatePublicKeys(index2pubkey[indices]).toBytes() (bls/utils.ts:5-20)."""
         self._check_open()
@@ -529,10 +534,17 @@ class GpuBlsVerifier:
         sigs = b"".join(bytes(sig) if len(sig) == 96 else bytes(96) for _, sig in sets)
         return idx.astype(_np.uint32), sigs, False
 
-    def verify_signature_sets_same_message(self, sets, message: bytes, opts: Optional[VerifySignatureOpts] = None):
+    async def verify_signature_sets_same_message(self, sets, message: bytes,
+                                                 opts: Optional[VerifySignatureOpts] = None) -> List[bool]:
         """verifySignatureSetsSameMessage (interface.ts:55-59): ``sets`` is a list of
-        (validator index, signature bytes) or a PackedSameMessageSets.  Returns an awaitable (the
-        reference's Promise<boolean[]>): argument errors reject it, they are not raised at the call.
+        (validator index, signature bytes) or a PackedSameMessageSets.  A coroutine, like the
+        reference's async method: argument errors surface when it is awaited."""
+        return await self.submit_signature_sets_same_message(sets, message, opts)
+
+    def submit_signature_sets_same_message(self, sets, message: bytes, opts: Optional[VerifySignatureOpts] = None):
+        """verify_signature_sets_same_message without the coroutine frame, for callers that issue
+        many gossip calls at once: the job is queued at the call and its future returned (a running
+        event loop is required).  Argument errors reject the future, they are not raised here.
 
         A gossip call is one job and its future is returned directly -- no coroutine, no task -- so
         the per-call host cost stays a few microseconds (the validator-index range check of the

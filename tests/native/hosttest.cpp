@@ -56,22 +56,6 @@ int ht_g2_in_subgroup(const uint8_t* xy) {
   G2A a{load_fp2(xy), load_fp2(xy + 96)};
   return g2_in_subgroup(a);
 }
-// [|x|] Q by the lazy 28-bit chain and by the canonical Fp2 chain (Jacobian, canonical BE out)
-void ht_g2_xabs_both(uint8_t* out_lazy, uint8_t* out_ref, const uint8_t* xy) {
-  G2A a{load_fp2(xy), load_fp2(xy + 96)};
-  G2J l = g2_mul_xabs_lazy(a), r = g2_mul_xabs(a);
-  store_fp2(out_lazy, l.x); store_fp2(out_lazy + 96, l.y); store_fp2(out_lazy + 192, l.z);
-  store_fp2(out_ref, r.x); store_fp2(out_ref + 96, r.y); store_fp2(out_ref + 192, r.z);
-}
-// lazy Fp2 product / square on raw 28-bit limbs (u32[28] each: c0 then c1); canonical Fp2 out
-// (Montgomery values: out = a b 2^-392 mod p).  Checks the limb-bound analysis of f28_lazy.h.
-void ht_l2_mul(uint8_t* out, const uint32_t* a, const uint32_t* b, int sqr_k) {
-  L2 x, y;
-  for (int i = 0; i < 14; ++i) { x.c0.v[i] = a[i]; x.c1.v[i] = a[14 + i]; y.c0.v[i] = b[i]; y.c1.v[i] = b[14 + i]; }
-  L2 r = sqr_k == 2 ? l2_sqr(x, K2P_28) : sqr_k == 4 ? l2_sqr(x, K4P_28) : l2_mul(x, y);
-  Fp2 c = l2_to(l2_norm(r));
-  fp_store_be48(out, c.c0); fp_store_be48(out + 48, c.c1);
-}
 int ht_g1_decompress(uint8_t* out, const uint8_t* in) {
   G1A a;
   uint8_t st = g1_decompress(a, in);

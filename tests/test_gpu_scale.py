@@ -106,13 +106,27 @@ def _run_staged(v, off, idx, sigs, msgs):
         st.close()
 
 
+def _tune(v, segments, msm_min, cooldown):
+    v.tune("segments", segments)
+    v.tune("msm_min", msm_min)
+    v.tune("msm_cooldown", cooldown)
+
+
+@pytest.fixture(autouse=True)
+def _default_settings(request):
+    """Every test starts from, and leaves, the context's default pipeline settings."""
+    yield
+    if "world" in request.fixturenames:
+        _tune(request.getfixturevalue("world")[0], 1, 131072, 16)
+
+
 @pytest.fixture(params=["ladder", "msm"])
-def segments(monkeypatch, request):
-    monkeypatch.setenv("GBV_SEGMENTS", "4")  # read by gbv_sm_batch_verify on every call
-    # G2 terms per set (32-step ladders) or per segment (bucket MSM, k_msm.hip): both must give the
-    # same booleans, and an all-valid stream must pass the segment checks either way
-    monkeypatch.setenv("GBV_MSM_MIN", "0" if request.param == "ladder" else "1000")
-    monkeypatch.setenv("GBV_MSM_COOLDOWN", "0")  # keep the MSM on after a failing segment
+def segments(world, request):
+    v = world[0]
+    # four pipeline segments; G2 terms per set (32-step ladders) or per segment (bucket MSM,
+    # k_msm.hip): both must give the same booleans, and an all-valid stream must pass the segment
+    # checks either way; cooldown 0 keeps the MSM on after a failing segment
+    _tune(v, 4, 0 if request.param == "ladder" else 1000, 0)
     return request.param
 
 
@@ -153,14 +167,13 @@ def test_same_message_injected_invalid(world, segments):
 
 
 @pytest.mark.parametrize("mode", ["ladder", "msm"])
-def test_same_message_one_percent_invalid(world, monkeypatch, mode):
+def test_same_message_one_percent_invalid(world, mode):
     """C5-style density: 1 % of 60 000 sets invalid, so hundreds of chunks fail.  The
     failure path then runs its thread-per-item kernels (group checks, 8-set run checks, per-set
     checks: more than FB_COOP_MAX items each) and must still return exactly the per-set booleans.
     In MSM mode the failing segment first recomputes its per-set G2 terms (k_sm_redo_g2)."""
-    monkeypatch.setenv("GBV_MSM_MIN", "0" if mode == "ladder" else "1000")
-    monkeypatch.setenv("GBV_MSM_COOLDOWN", "0")
     v, sks, _ = world
+    _tune(v, 1, 0 if mode == "ladder" else 1000, 0)
     off, idx, grp, sigs, msgs = _workload(v, sks, 60000, 14)
     n = len(sigs)
     rng = np.random.Generator(np.random.PCG64(0xC0FFEE))
@@ -287,14 +300,12 @@ def test_sharded_verifier_single_rank(world):
         dist.destroy_process_group()
 
 
-def test_same_message_msm_single_segment(world, monkeypatch):
+def test_same_message_msm_single_segment(world):
     """One 100 000-set segment through the bucket MSM at its default size threshold (the bench's
     shape at 1/10 scale): the segment check must pass on the MSM's sum alone, and the MSM kernels
     must have run (their time is reported in slot 7 of last_kernel_ms)."""
-    monkeypatch.setenv("GBV_SEGMENTS", "1")
-    monkeypatch.setenv("GBV_MSM_MIN", "65536")
-    monkeypatch.setenv("GBV_MSM_COOLDOWN", "0")
     v, sks, _ = world
+    _tune(v, 1, 65536, 0)
     off, idx, grp, sigs, msgs = _workload(v, sks, 100000, 15)
     res = _run_staged(v, off, idx, sigs, msgs)
     assert all(res)
@@ -310,13 +321,11 @@ def test_same_message_msm_single_segment(world, monkeypatch):
     assert fb == 1 and seg == 1
 
 
-def test_msm_cooldown_after_failing_segment(world, monkeypatch):
+def test_msm_cooldown_after_failing_segment(world):
     """After an MSM segment fails, the next submits use the per-set ladders (an invalid-dense stream
     would otherwise pay the MSM and the G2 recomputation); booleans are the same either way."""
-    monkeypatch.setenv("GBV_SEGMENTS", "1")
-    monkeypatch.setenv("GBV_MSM_MIN", "1000")
-    monkeypatch.setenv("GBV_MSM_COOLDOWN", "2")
     v, sks, _ = world
+    _tune(v, 1, 1000, 2)
     off, idx, grp, sigs, msgs = _workload(v, sks, 5000, 16)
     bad = list(sigs)
     bad[123] = bytes([10]) * 96

@@ -315,28 +315,6 @@ def test_roofline_work_constants_are_counted(lib):
     assert bench.W_VS_HASH_SIG == bench.FME_HASH_TO_G2 + bench.FME_SIG_VALIDATE + bench.FME_RANDOMIZE_PAIR_JAC
 
 
-def test_g2_xabs_lazy_chain(lib):
-    """[|x|]Q in lazy 28-bit limbs (f28_lazy.h, the subgroup check's chain) equals the canonical
-    Fp2 chain as projective points, on subgroup and non-subgroup points of E2."""
-    import random
-    rnd = random.Random(5)
-    lib.ht_g2_xabs_both.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p]
-    pts = [o.sign(3 + i, bytes([i]) * 32) for i in range(3)]
-    pts += [o.iso_map_g2(o.map_to_curve_sswu_g2((rnd.randrange(o.P), rnd.randrange(o.P)))) for _ in range(6)]
-    for q in pts:
-        xy = be(q[0][0]) + be(q[0][1]) + be(q[1][0]) + be(q[1][1])
-        a, b = buf(288), buf(288)
-        lib.ht_g2_xabs_both(a, b, xy)
-        la = [int.from_bytes(a.raw[48 * i:48 * i + 48], "big") for i in range(6)]
-        lb = [int.from_bytes(b.raw[48 * i:48 * i + 48], "big") for i in range(6)]
-        X1, Y1, Z1 = (la[0], la[1]), (la[2], la[3]), (la[4], la[5])
-        X2, Y2, Z2 = (lb[0], lb[1]), (lb[2], lb[3]), (lb[4], lb[5])
-        z1s, z2s = o.f2_sqr(Z1), o.f2_sqr(Z2)
-        assert o.f2_mul(X1, z2s) == o.f2_mul(X2, z1s)
-        assert o.f2_mul(Y1, o.f2_mul(z2s, Z2)) == o.f2_mul(Y2, o.f2_mul(z1s, Z1))
-        assert Z1 != (0, 0)
-
-
 def test_coop_clear_cofactor(lib):
     """hash_to_G2's cofactor clearing with both [|x|] multiplications by the cooperative Miller-loop
     point steps (coop.h mul_xabs_point, k_hash_clear_coop) equals the oracle's clear_cofactor_g2 on
@@ -350,47 +328,3 @@ def test_coop_clear_cofactor(lib):
         got = [int.from_bytes(out.raw[48 * i:48 * i + 48], "big") for i in range(4)]
         want = o.clear_cofactor_g2(q)
         assert ((got[0], got[1]), (got[2], got[3])) == (want[0], want[1])
-
-
-def test_lazy_fp2_limb_bounds(lib):
-    """l2_mul / l2_sqr at the limb and value bounds f28_lazy.h allows: every limb 2^28 - 1 and
-    values up to 16 p (mul) / the K of the square, against exact Montgomery arithmetic."""
-    import random
-    rnd = random.Random(9)
-    R_INV = pow(2, -392, o.P)
-    M = (1 << 28) - 1
-    lib.ht_l2_mul.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
-
-    def limbs_of(v, maxed):
-        # normalized 28-bit limbs of v; "maxed": push lower limbs to 2^28 - 1 where the value allows
-        ls = [(v >> (28 * i)) & M for i in range(13)] + [v >> 364]
-        if maxed:
-            ls = [M] * 13 + [(v - sum(M << (28 * i) for i in range(13))) >> 364]
-            assert ls[13] >= 0 and sum(l << (28 * i) for i, l in enumerate(ls)) <= v
-        return ls
-
-    def run(a, b, k):
-        A = (ctypes.c_uint32 * 28)(*(a[0] + a[1]))
-        B = (ctypes.c_uint32 * 28)(*(b[0] + b[1]))
-        out = buf(96)
-        lib.ht_l2_mul(out, ctypes.cast(A, ctypes.c_void_p), ctypes.cast(B, ctypes.c_void_p), k)
-        return int.from_bytes(out.raw[:48], "big"), int.from_bytes(out.raw[48:], "big")
-
-    def val(ls):
-        return sum(l << (28 * i) for i, l in enumerate(ls))
-
-    for trial in range(40):
-        cap = 16 * o.P if trial % 2 else 2 * o.P
-        maxed = trial % 4 >= 2
-        vals = [cap - 1 - rnd.randrange(1 << 300) if maxed else rnd.randrange(cap) for _ in range(4)]
-        a = [limbs_of(vals[0], maxed), limbs_of(vals[1], maxed)]
-        b = [limbs_of(vals[2], maxed), limbs_of(vals[3], maxed)]
-        a0, a1, b0, b1 = (val(x) for x in a + b)
-        got = run(a, b, 0)
-        want = ((a0 * b0 - a1 * b1) * R_INV % o.P, (a0 * b1 + a1 * b0) * R_INV % o.P)
-        assert got == want, trial
-        if cap == 2 * o.P:
-            for k in (2, 4):
-                got = run(a, a, k)
-                want = ((a0 * a0 - a1 * a1) * R_INV % o.P, 2 * a0 * a1 * R_INV % o.P)
-                assert got == want, (trial, k)

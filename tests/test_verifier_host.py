@@ -382,9 +382,9 @@ def test_out_of_range_index_rejects_its_call_inside_a_shared_pass():
     async def go():
         v = Recorder()
         ok = b"\x01" + bytes(95)
-        good1 = v.verify_signature_sets_same_message(PackedSameMessageSets(np.array([1, 2], dtype=np.uint32), ok * 2), bytes(32))
-        bad = v.verify_signature_sets_same_message(PackedSameMessageSets(np.array([3, 1 << 20], dtype=np.uint32), ok * 2), bytes(32))
-        good2 = v.verify_signature_sets_same_message([(5, ok)], bytes(32))
+        good1 = v.submit_signature_sets_same_message(PackedSameMessageSets(np.array([1, 2], dtype=np.uint32), ok * 2), bytes(32))
+        bad = v.submit_signature_sets_same_message(PackedSameMessageSets(np.array([3, 1 << 20], dtype=np.uint32), ok * 2), bytes(32))
+        good2 = v.submit_signature_sets_same_message([(5, ok)], bytes(32))
         r1 = await good1
         with pytest.raises(GbvError):
             await bad
@@ -393,3 +393,21 @@ def test_out_of_range_index_rejects_its_call_inside_a_shared_pass():
     v, r1, r2 = run(go())
     assert r1.tolist() == [True, True] and r2 == [True]
     assert [p for p in v.passes if p[0] == "sm"] == [("sm", [2, 1])]
+
+
+def test_same_message_public_method_is_a_coroutine():
+    """The IBlsVerifier method is async (like the reference's): it composes with gather, wait_for and
+    create_task, and an argument error rejects when awaited, not at the call."""
+    async def go():
+        v = Recorder()
+        ok = b"\x01" + bytes(95)
+        coro = v.verify_signature_sets_same_message([(0, ok)], bytes(5))  # bad message length: no raise yet
+        assert asyncio.iscoroutine(coro)
+        with pytest.raises(ValueError):
+            await coro
+        t = asyncio.create_task(v.verify_signature_sets_same_message([(1, ok)], bytes(32)))
+        a, b = await asyncio.gather(v.verify_signature_sets_same_message([(2, ok), (3, ok)], bytes(32)),
+                                    asyncio.wait_for(v.verify_signature_sets_same_message([(4, ok)], bytes(32)), 10))
+        return await t, a, b
+    r, a, b = run(go())
+    assert r == [True] and a == [True, True] and b == [True]

@@ -46,7 +46,7 @@ def main():
     idx = rng.integers(0, 1 << 20, size=n).astype(np.uint32)
     mv = memoryview(bytes(96 * n))
     reqs = [(PackedSameMessageSets(idx[off[g]:off[g + 1]], mv[96 * off[g]:96 * off[g + 1]]), bytes(32)) for g in range(len(sizes))]
-    call = v.verify_signature_sets_same_message
+    call = v.submit_signature_sets_same_message
 
     async def go():
         t = time.perf_counter()
