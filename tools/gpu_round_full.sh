@@ -1,13 +1,13 @@
 #!/bin/bash
-# Round-3 GPU session: parity tests, smoke, the default bench, the multi-GPU shard mode at N=1, a rocprofv3 kernel-trace
+# GPU round session: parity tests, smoke, the default bench, the multi-GPU shard mode at N=1, a rocprofv3 kernel-trace
 # summary, PMC passes and the lone-call latency probe.  Each GPU step has its own limit; the script
 # stops at the first failure.   Usage (via gpurun): bash tools/r03_round.sh tag
 set -o pipefail
-TAG=${1:-r03}
+TAG=${1:-run}
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-echo "[r03] host: $(nproc) cpus, $(grep -m1 'model name' /proc/cpuinfo | cut -d: -f2)" | tee "$OUT/host.txt"
+echo "[gpu] host: $(nproc) cpus, $(grep -m1 'model name' /proc/cpuinfo | cut -d: -f2)" | tee "$OUT/host.txt"
 timeout -k 10 420 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1 || { echo "pytest failed"; tail -40 "$OUT/pytest_gpu.log"; exit 1; }
 tail -2 "$OUT/pytest_gpu.log"
 timeout -k 10 180 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 || { echo "smoke failed"; tail -30 "$OUT/smoke.log"; exit 1; }
@@ -33,4 +33,4 @@ for k in ("bench",):
     if d.get("c5"):
         print("  c5 %.2fM" % (d["c5"]["value"] / 1e6))
 PY
-echo "[r03] done"
+echo "[gpu] done"
