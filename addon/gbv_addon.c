@@ -307,6 +307,7 @@ typedef struct {
   size_t n_out;
   int rc;
   char err[256];
+  napi_ref ctx_ref;  /* keeps the context external (and so ac) alive until complete() */
 } job;
 
 static void lock_begin(addon_ctx* ac) {
@@ -413,14 +414,18 @@ static void complete(napi_env env, napi_status status, void* data) {
     napi_resolve_deferred(env, j->deferred, result);
   }
   napi_delete_async_work(env, j->work);
+  napi_delete_reference(env, j->ctx_ref);
   sets_free(&j->sets);
   free(j->sm_idx.p); free(j->sm_sigs.p); free(j->sm_msgs.p);
   free(j->out);
   free(j);
 }
 
-static napi_value queue(napi_env env, job* j, const char* name) {
+/* ctxv: the context external the job works on, referenced until the job completes so that a
+ * context dropped by JS while work is queued is not finalized under it. */
+static napi_value queue(napi_env env, job* j, const char* name, napi_value ctxv) {
   napi_value promise, res_name;
+  napi_create_reference(env, ctxv, 1, &j->ctx_ref);
   napi_create_promise(env, &j->deferred, &promise);
   napi_create_string_utf8(env, name, NAPI_AUTO_LENGTH, &res_name);
   napi_create_async_work(env, NULL, res_name, execute, complete, j, &j->work);
@@ -675,7 +680,7 @@ static napi_value js_verify_sets(napi_env env, napi_callback_info info) {
     drop_job(j);
     return NULL;
   }
-  return queue(env, j, "gbvVerifySets");
+  return queue(env, j, "gbvVerifySets", argv[0]);
 }
 
 static napi_value js_verify_sets_multi(napi_env env, napi_callback_info info) {
@@ -705,7 +710,7 @@ static napi_value js_verify_sets_multi(napi_env env, napi_callback_info info) {
     }
     uv_push(&j->sets.call_off, (uint32_t)j->sets.msg_off.n);
   }
-  return queue(env, j, "gbvVerifySetsMulti");
+  return queue(env, j, "gbvVerifySetsMulti", argv[0]);
 }
 
 static napi_value js_verify_same_message_multi(napi_env env, napi_callback_info info) {
@@ -758,7 +763,7 @@ static napi_value js_verify_same_message_multi(napi_env env, napi_callback_info 
     }
     uv_push(&j->sets.call_off, (uint32_t)j->sm_idx.n);
   }
-  return queue(env, j, "gbvVerifySameMessageMulti");
+  return queue(env, j, "gbvVerifySameMessageMulti", argv[0]);
 }
 
 /* ---- streamed passes ------------------------------------------------------------------------ */
@@ -773,7 +778,10 @@ typedef struct {
   uint8_t *sm_valid, *df_valid;
   napi_deferred deferred;
   napi_async_work work;
+  napi_ref ctx_ref;        /* the context external, alive while the pass is */
   int queued;              /* waitPass called */
+  int done;                /* waitPass settled */
+  int external_gone;       /* the JS pass object was finalized */
 } pass;
 
 /* Marshal a same-message call list ({sets: {index, signature}[], message}[]) into idx / sigs / msgs. */
@@ -818,11 +826,35 @@ static int marshal_same_message(napi_env env, napi_value arr, uvec* off, uvec* i
   return 1;
 }
 
-static void pass_free(pass* p) {
+static void pass_free(napi_env env, pass* p) {
+  if (p->ctx_ref) napi_delete_reference(env, p->ctx_ref);
   free(p->sm_off.p);
   free(p->sm_valid);
   free(p->df_valid);
   free(p);
+}
+
+/* The JS pass object is gone.  A pass whose waitPass is still running is freed by pass_complete; a
+ * pass never waited (a broken caller: every submitted pass must be waited once) is waited here so
+ * that its slot and batches are free again. */
+static void pass_finalize(napi_env env, void* data, void* hint) {
+  (void)hint;
+  pass* p = (pass*)data;
+  if (p->queued && !p->done) {
+    p->external_gone = 1;
+    return;
+  }
+  if (!p->queued) {
+    addon_ctx* ac = p->ac;
+    pass_slot* sl = &ac->slots[p->slot];
+    pthread_mutex_lock(&sl->mu);
+    if (ac->ctx && p->has_sm && !p->rc_sm && sl->sm) gbv_sm_batch_wait(ac->ctx, sl->sm, NULL);
+    if (ac->ctx && p->has_df && !p->rc_df && sl->vs) gbv_vs_batch_wait(ac->ctx, sl->vs, NULL);
+    pthread_mutex_unlock(&sl->mu);
+    sl->busy = 0;
+    ac->inflight--;
+  }
+  pass_free(env, p);
 }
 
 /* submitPass(ctx, sameMessageCalls | null, defaultCalls | null): fill and submit both device batches of
@@ -883,7 +915,7 @@ static napi_value js_submit_pass(napi_env env, napi_callback_info info) {
   if (!ok) {
     free(sm_idx.p); free(sm_sigs.p); free(sm_msgs.p);
     sets_free(&df);
-    pass_free(p);
+    pass_free(env, p);
     return NULL;
   }
   /* stage + enqueue (the context lock inside libgbv orders this against pool threads) */
@@ -913,8 +945,9 @@ static napi_value js_submit_pass(napi_env env, napi_callback_info info) {
   sets_free(&df);
   sl->busy = 1;
   ac->inflight++;
+  napi_create_reference(env, argv[0], 1, &p->ctx_ref);
   napi_value ext;
-  NAPI_OK(env, napi_create_external(env, p, NULL, NULL, &ext));
+  NAPI_OK(env, napi_create_external(env, p, pass_finalize, NULL, &ext));
   return ext;
 }
 
@@ -983,7 +1016,11 @@ static void pass_complete(napi_env env, napi_status status, void* data) {
     napi_resolve_deferred(env, p->deferred, result);
   }
   napi_delete_async_work(env, p->work);
-  pass_free(p);
+  p->done = 1;
+  free(p->sm_valid);
+  free(p->df_valid);
+  p->sm_valid = p->df_valid = NULL;
+  if (p->external_gone) pass_free(env, p);  /* else the external's finalizer frees it */
 }
 
 /* waitPass(pass) -> Promise: the device wait runs on the libuv pool; every submitted pass must be
@@ -1156,7 +1193,7 @@ static napi_value js_close(napi_env env, napi_callback_info info) {
   j->op = OP_CLOSE;
   j->ac = ac;
   ac->closed = 1;  // new calls reject with QUEUE_ABORTED; queued ones run before the destroy (mutex order)
-  return queue(env, j, "gbvClose");
+  return queue(env, j, "gbvClose", argv[0]);
 }
 
 static napi_value init(napi_env env, napi_value exports) {

@@ -18,9 +18,12 @@ LIB = os.path.join(HERE, "c", "libblsport.so")
 
 def load():
     src = os.path.join(HERE, "c", "blsport.c")
-    if not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(src):
-        subprocess.check_call([os.path.join(HERE, "c", "build.sh")])
-    lib = ctypes.CDLL(LIB)
+    if os.environ.get("GBV_BLSPORT_LIB"):  # a sanitizer build (tools/sanitize_host.sh)
+        lib = ctypes.CDLL(os.environ["GBV_BLSPORT_LIB"])
+    else:
+        if not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(src):
+            subprocess.check_call([os.path.join(HERE, "c", "build.sh")])
+        lib = ctypes.CDLL(LIB)
     lib.port_verify_same_message_batch.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_char_p,
                                                    ctypes.c_char_p, ctypes.c_char_p, ctypes.c_void_p, ctypes.c_uint64]
     lib.port_g1_decompress.argtypes = [ctypes.c_char_p, ctypes.c_void_p]

@@ -18,6 +18,8 @@ LIB = os.path.join(HERE, "native", "libhosttest.so")
 
 @pytest.fixture(scope="module")
 def lib():
+    if os.environ.get("GBV_HOSTTEST_LIB"):  # a sanitizer build (tools/sanitize_host.sh)
+        return ctypes.CDLL(os.environ["GBV_HOSTTEST_LIB"])
     srcs = [os.path.join(HERE, "native", "hosttest.cpp")] + [
         os.path.join(HERE, "..", "lodestar_amd", "csrc", f) for f in os.listdir(os.path.join(HERE, "..", "lodestar_amd", "csrc")) if f.endswith(".h")]
     if not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(s) for s in srcs):
