@@ -25,7 +25,9 @@
  *   freePasses(ctx)                               -> number of pass slots not in flight
  * and the rest of IBlsVerifier's needs: verifySetsSync(ctx, sets) -> boolean (verifyOnMainThread,
  * index.ts:168-181), pubkeyCount(ctx), vsPartial(ctx, sets) -> Promise<{partial, ok}> and
- * fp12Check(ctx, partials) -> boolean (multi-GPU shards, gbv_vs_partial / gbv_fp12_check).
+ * fp12Check(ctx, partials) -> boolean (multi-GPU shards, gbv_vs_partial / gbv_fp12_check), and the
+ * device hashing of the signature-set builders: merkleRoots(ctx, chunks, depth) (gbv_merkle_roots) and
+ * signingRoots(ctx, objectRoots, domains, domIdx) (gbv_signing_roots).
  *
  * A set is {index: number} or {indices: Uint32Array | number[]} or {pubkey: Uint8Array(48)}, plus
  * {signingRoot: Uint8Array(32), signature: Uint8Array}.  JS buffers are only borrowed during the
@@ -1174,6 +1176,84 @@ static napi_value js_fp12_check(napi_env env, napi_callback_info info) {
   return res;
 }
 
+/* merkleRoots(ctx, chunks: Uint8Array of n * 2^depth * 32 bytes, depth) -> Uint8Array(32 n)
+ * (gbv_merkle_roots: ContainerType.hashTreeRoot over field roots on the device). */
+static napi_value js_merkle_roots(napi_env env, napi_callback_info info) {
+  size_t argc = 3;
+  napi_value argv[3];
+  NAPI_OK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  addon_ctx* ac = argc >= 1 ? get_ctx(env, argv[0]) : NULL;
+  if (!ac) return NULL;
+  const uint8_t* d;
+  size_t len;
+  uint32_t depth = 0;
+  if (argc < 3 || !get_bytes(env, argv[1], &d, &len) || !get_u32(env, argv[2], &depth) || depth > 24 ||
+      len % ((size_t)32 << depth)) {
+    napi_throw_type_error(env, "GBV_E_ARG", "merkleRoots(ctx, chunks: Uint8Array of n*2^depth*32 bytes, depth <= 24)");
+    return NULL;
+  }
+  if (ac->closed || !ac->ctx) {
+    throw_rc(env, GBV_E_CLOSED, "QUEUE_ABORTED");
+    return NULL;
+  }
+  size_t n = len / ((size_t)32 << depth);
+  void* out = NULL;
+  napi_value ab, ta;
+  NAPI_OK(env, napi_create_arraybuffer(env, n ? 32 * n : 1, &out, &ab));
+  NAPI_OK(env, napi_create_typedarray(env, napi_uint8_array, 32 * n, ab, 0, &ta));
+  lock_begin(ac);
+  int rc = gbv_merkle_roots(ac->ctx, n ? d : (const uint8_t*)"", n, depth, (uint8_t*)out);
+  if (rc) throw_rc(env, rc, gbv_last_error(ac->ctx));
+  lock_end(ac);
+  return rc ? NULL : ta;
+}
+
+/* signingRoots(ctx, objectRoots: Uint8Array(32 n), domains: Uint8Array(32 k), domIdx: Uint32Array(n) | null)
+ * -> Uint8Array(32 n) (gbv_signing_roots: computeSigningRoot, signingRoot.ts:7-13). */
+static napi_value js_signing_roots(napi_env env, napi_callback_info info) {
+  size_t argc = 4;
+  napi_value argv[4];
+  NAPI_OK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  addon_ctx* ac = argc >= 1 ? get_ctx(env, argv[0]) : NULL;
+  if (!ac) return NULL;
+  const uint8_t *r, *dm;
+  size_t rlen, dlen;
+  if (argc < 3 || !get_bytes(env, argv[1], &r, &rlen) || rlen % 32 || !get_bytes(env, argv[2], &dm, &dlen) || dlen % 32 || dlen == 0) {
+    napi_throw_type_error(env, "GBV_E_ARG", "signingRoots(ctx, objectRoots: Uint8Array(32 n), domains: Uint8Array(32 k), domIdx)");
+    return NULL;
+  }
+  size_t n = rlen / 32;
+  const uint32_t* idx = NULL;
+  napi_valuetype t = napi_undefined;
+  if (argc >= 4) napi_typeof(env, argv[3], &t);
+  if (t != napi_undefined && t != napi_null) {
+    bool is_ta = false;
+    napi_is_typedarray(env, argv[3], &is_ta);
+    napi_typedarray_type type;
+    size_t m = 0, off;
+    void* p = NULL;
+    napi_value ab;
+    if (!is_ta || napi_get_typedarray_info(env, argv[3], &type, &m, &p, &ab, &off) != napi_ok || type != napi_uint32_array || m != n) {
+      napi_throw_type_error(env, "GBV_E_ARG", "domIdx must be a Uint32Array of one index per root");
+      return NULL;
+    }
+    idx = (const uint32_t*)p;
+  }
+  if (ac->closed || !ac->ctx) {
+    throw_rc(env, GBV_E_CLOSED, "QUEUE_ABORTED");
+    return NULL;
+  }
+  void* out = NULL;
+  napi_value ab, ta;
+  NAPI_OK(env, napi_create_arraybuffer(env, n ? 32 * n : 1, &out, &ab));
+  NAPI_OK(env, napi_create_typedarray(env, napi_uint8_array, 32 * n, ab, 0, &ta));
+  lock_begin(ac);
+  int rc = gbv_signing_roots(ac->ctx, n ? r : (const uint8_t*)"", n, dm, dlen / 32, idx, (uint8_t*)out);
+  if (rc) throw_rc(env, rc, gbv_last_error(ac->ctx));
+  lock_end(ac);
+  return rc ? NULL : ta;
+}
+
 static napi_value js_close(napi_env env, napi_callback_info info) {
   size_t argc = 1;
   napi_value argv[1];
@@ -1215,6 +1295,8 @@ static napi_value init(napi_env env, napi_value exports) {
       {"verifySetsSync", NULL, js_verify_sets_sync, NULL, NULL, NULL, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), NULL},
       {"vsPartial", NULL, js_vs_partial, NULL, NULL, NULL, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), NULL},
       {"fp12Check", NULL, js_fp12_check, NULL, NULL, NULL, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), NULL},
+      {"merkleRoots", NULL, js_merkle_roots, NULL, NULL, NULL, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), NULL},
+      {"signingRoots", NULL, js_signing_roots, NULL, NULL, NULL, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), NULL},
   };
   napi_define_properties(env, exports, sizeof props / sizeof props[0], props);
   napi_value mp;

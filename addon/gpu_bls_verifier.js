@@ -159,6 +159,16 @@ class GpuBlsVerifier {
     return this.addon.addPubkeys(this.ctx, firstIndex, pk48s, !!validate);
   }
 
+  /** Device hashing for the signature-set builders (addon/gossip_sets.js): Merkle roots of objects of
+   * 2^depth chunks (gbv_merkle_roots) and computeSigningRoot over object roots (gbv_signing_roots). */
+  merkleRoots(chunks, depth) {
+    return this.addon.merkleRoots(this.ctx, chunks, depth);
+  }
+
+  signingRoots(objectRoots, domains, domIdx) {
+    return this.addon.signingRoots(this.ctx, objectRoots, domains, domIdx || null);
+  }
+
   canAcceptWork() {
     return this.passesBusy < this.maxPasses && this.jobs.length < MAX_JOBS_CAN_ACCEPT_WORK;
   }

@@ -75,7 +75,8 @@ def test_addon_builds_and_maps_errors_without_gpu():
     r = _run("cpu")
     assert r["exports"] == ["open", "addPubkeys", "verifySets", "verifySetsMulti", "verifySameMessageMulti", "aggregatePubkeys",
                             "aggregateSerializedPubkeys", "aggregateSignatures", "validateSignatures", "close", "submitPass",
-                            "waitPass", "freePasses", "pubkeyCount", "verifySetsSync", "vsPartial", "fp12Check"]
+                            "waitPass", "freePasses", "pubkeyCount", "verifySetsSync", "vsPartial", "fp12Check", "merkleRoots",
+                            "signingRoots"]
     assert r["maxPasses"] == 3
     assert r["open"] == "ok"      # gbv_init without a device -> Error code GBV_E_DEVICE
     assert r["badCtx"] == "ok"    # not a context -> TypeError code GBV_E_ARG
@@ -102,3 +103,28 @@ def test_addon_golden_cases_on_gpu():
     assert r["shards"] is True and r["shardsWrong"] is True
     assert r["inflightBeforeClose"] is True
     assert r["afterClose"] == "QUEUE_ABORTED"
+
+
+GOSSIP = os.path.join(HERE, "golden", "gossip_sets.json")
+
+
+def test_js_gossip_builders_match_oracle_without_gpu():
+    """addon/gossip_sets.js (validateAggregateAndProof / contribution / sync-message builders in index
+    form) reproduces the oracle's sets of tests/golden/gossip_sets.json with a host SHA-256 stand-in."""
+    r = _run("cpu", GOSSIP, script="test_gossip.js")
+    assert "fatal" not in r, r
+    assert r["builders"] == [True] * 7
+
+
+@pytest.mark.gpu
+def test_js_gossip_calls_on_gpu():
+    """The JS builders with every root hashed on the device, then each call -- the three-set
+    aggregate-and-proof call (phase0 and electra), the contribution-and-proof call, sync messages --
+    and one corruption per set kind, through GpuBlsVerifier.verifySignatureSets(sets, {batchable: true,
+    priority: true}): exactly the oracle's per-call results."""
+    r = _run("gpu", GOSSIP, timeout=300, script="test_gossip.js")
+    assert "fatal" not in r, r
+    assert r["ingest"] is True
+    assert r["deviceBuilders"] == [True] * 7
+    assert r["calls"] == [True] * 7
+    assert r["devicePasses"] >= 1
