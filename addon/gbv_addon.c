@@ -165,6 +165,28 @@ static void uv_push(uvec* v, uint32_t x) {
   }
   v->p[v->n++] = x;
 }
+static void uv_push_n(uvec* v, const uint32_t* x, size_t n) {
+  if (v->n + n > v->cap) {
+    v->cap = (v->n + n) * 2 + 64;
+    v->p = (uint32_t*)realloc(v->p, v->cap * sizeof(uint32_t));
+  }
+  memcpy(v->p + v->n, x, n * sizeof(uint32_t));
+  v->n += n;
+}
+
+/* Borrow a Uint32Array's elements (only valid during the synchronous part). */
+static int get_u32_array(napi_env env, napi_value v, const uint32_t** data, size_t* n) {
+  bool is_ta = false;
+  napi_is_typedarray(env, v, &is_ta);
+  if (!is_ta) return 0;
+  napi_typedarray_type type;
+  size_t off;
+  void* d;
+  napi_value ab;
+  if (napi_get_typedarray_info(env, v, &type, n, &d, &ab, &off) != napi_ok || type != napi_uint32_array) return 0;
+  *data = (const uint32_t*)d;
+  return 1;
+}
 
 /* ---- signature-set marshalling ---------------------------------------------------------- */
 /* Copied sets: per set (arena offset/len, raw-pk offset or -1, msg offset, sig offset/len). */
@@ -715,6 +737,8 @@ static napi_value js_verify_sets_multi(napi_env env, napi_callback_info info) {
   return queue(env, j, "gbvVerifySetsMulti", argv[0]);
 }
 
+static int marshal_same_message(napi_env env, napi_value arr, uvec* off, uvec* idx, bvec* sigs, bvec* msgs, bvec* packed);
+
 static napi_value js_verify_same_message_multi(napi_env env, napi_callback_info info) {
   size_t argc = 2;
   napi_value argv[2];
@@ -730,40 +754,9 @@ static napi_value js_verify_same_message_multi(napi_env env, napi_callback_info 
   if (ac->closed) return rejected_closed(env);
   job* j = new_job(env, ac, OP_SAME_MESSAGE_MULTI);
   if (!j) return NULL;
-  uint32_t nc = 0;
-  napi_get_array_length(env, argv[1], &nc);
-  uv_push(&j->sets.call_off, 0);
-  static const uint8_t zero96[96] = {0};
-  for (uint32_t c = 0; c < nc; ++c) {
-    napi_value call, sets, msg;
-    napi_get_element(env, argv[1], c, &call);
-    const uint8_t* d;
-    size_t len;
-    bool sa = false;
-    if (!get_prop(env, call, "message", &msg) || !get_bytes(env, msg, &d, &len) || len != 32 || !get_prop(env, call, "sets", &sets) ||
-        napi_is_array(env, sets, &sa) != napi_ok || !sa) {
-      drop_job(j);
-      napi_throw_type_error(env, "GBV_E_ARG", "each call needs sets: array and message: 32-byte Uint8Array");
-      return NULL;
-    }
-    bv_push(&j->sm_msgs, d, 32);
-    uint32_t n = 0;
-    napi_get_array_length(env, sets, &n);
-    for (uint32_t i = 0; i < n; ++i) {
-      napi_value e, v;
-      uint32_t idx;
-      napi_get_element(env, sets, i, &e);
-      if (!get_prop(env, e, "index", &v) || !get_u32(env, v, &idx) || !get_prop(env, e, "signature", &v) || !get_bytes(env, v, &d, &len)) {
-        drop_job(j);
-        napi_throw_type_error(env, "GBV_E_ARG", "a same-message set is {index: number, signature: Uint8Array}");
-        return NULL;
-      }
-      uv_push(&j->sm_idx, idx);
-      /* SSZ Bytes96 on the wire; another length throws in fromBytes -> that set is false: the
-       * all-zero encoding (no compression flag) is rejected the same way */
-      bv_push(&j->sm_sigs, len == 96 ? d : zero96, 96);
-    }
-    uv_push(&j->sets.call_off, (uint32_t)j->sm_idx.n);
+  if (!marshal_same_message(env, argv[1], &j->sets.call_off, &j->sm_idx, &j->sm_sigs, &j->sm_msgs, NULL)) {
+    drop_job(j);
+    return NULL;
   }
   return queue(env, j, "gbvVerifySameMessageMulti", argv[0]);
 }
@@ -778,6 +771,7 @@ typedef struct {
   uvec sm_off;             /* same-message calls: set offsets */
   size_t n_df;             /* default calls */
   uint8_t *sm_valid, *df_valid;
+  bvec sm_packed;          /* per same-message call: 1 = packed sets (result as a Uint8Array) */
   napi_deferred deferred;
   napi_async_work work;
   napi_ref ctx_ref;        /* the context external, alive while the pass is */
@@ -786,8 +780,10 @@ typedef struct {
   int external_gone;       /* the JS pass object was finalized */
 } pass;
 
-/* Marshal a same-message call list ({sets: {index, signature}[], message}[]) into idx / sigs / msgs. */
-static int marshal_same_message(napi_env env, napi_value arr, uvec* off, uvec* idx, bvec* sigs, bvec* msgs) {
+/* Marshal a same-message call list ({sets, message}[]) into idx / sigs / msgs.  A call's sets are either
+ * {index, signature}[] or the packed form {indices: Uint32Array(n), signatures: Uint8Array(96 n)}
+ * (copied in two memcpys; packed[c] = 1 then, so waitPass answers that call with a Uint8Array). */
+static int marshal_same_message(napi_env env, napi_value arr, uvec* off, uvec* idx, bvec* sigs, bvec* msgs, bvec* packed) {
   bool ja = false;
   napi_is_array(env, arr, &ja);
   if (!ja) {
@@ -805,11 +801,29 @@ static int marshal_same_message(napi_env env, napi_value arr, uvec* off, uvec* i
     size_t len;
     bool sa = false;
     if (!get_prop(env, call, "message", &msg) || !get_bytes(env, msg, &d, &len) || len != 32 || !get_prop(env, call, "sets", &sets) ||
-        napi_is_array(env, sets, &sa) != napi_ok || !sa) {
-      napi_throw_type_error(env, "GBV_E_ARG", "each call needs sets: array and message: 32-byte Uint8Array");
+        napi_is_array(env, sets, &sa) != napi_ok) {
+      napi_throw_type_error(env, "GBV_E_ARG", "each call needs sets and message: 32-byte Uint8Array");
       return 0;
     }
     bv_push(msgs, d, 32);
+    if (!sa) {  /* packed */
+      napi_value iv, sv;
+      const uint32_t* ix;
+      size_t n = 0;
+      if (!get_prop(env, sets, "indices", &iv) || !get_u32_array(env, iv, &ix, &n) || !get_prop(env, sets, "signatures", &sv) ||
+          !get_bytes(env, sv, &d, &len) || len != 96 * n) {
+        napi_throw_type_error(env, "GBV_E_ARG", "sets: {index, signature}[] or {indices: Uint32Array(n), signatures: Uint8Array(96 n)}");
+        return 0;
+      }
+      uv_push_n(idx, ix, n);
+      bv_push(sigs, d, 96 * n);
+      uv_push(off, (uint32_t)idx->n);
+      const uint8_t one = 1;
+      if (packed) bv_push(packed, &one, 1);
+      continue;
+    }
+    const uint8_t zero = 0;
+    if (packed) bv_push(packed, &zero, 1);
     uint32_t n = 0;
     napi_get_array_length(env, sets, &n);
     for (uint32_t i = 0; i < n; ++i) {
@@ -831,6 +845,7 @@ static int marshal_same_message(napi_env env, napi_value arr, uvec* off, uvec* i
 static void pass_free(napi_env env, pass* p) {
   if (p->ctx_ref) napi_delete_reference(env, p->ctx_ref);
   free(p->sm_off.p);
+  free(p->sm_packed.p);
   free(p->sm_valid);
   free(p->df_valid);
   free(p);
@@ -892,7 +907,7 @@ static napi_value js_submit_pass(napi_env env, napi_callback_info info) {
   int ok = 1;
   if (t0 != napi_null && t0 != napi_undefined) {
     p->has_sm = 1;
-    ok = marshal_same_message(env, argv[1], &p->sm_off, &sm_idx, &sm_sigs, &sm_msgs);
+    ok = marshal_same_message(env, argv[1], &p->sm_off, &sm_idx, &sm_sigs, &sm_msgs, &p->sm_packed);
   }
   if (ok && t1 != napi_null && t1 != napi_undefined) {
     bool ja = false;
@@ -989,11 +1004,19 @@ static void pass_complete(napi_env env, napi_status status, void* data) {
       for (size_t c = 0; c < nc; ++c) {
         uint32_t a = p->sm_off.p[c], b = p->sm_off.p[c + 1];
         napi_value arr;
-        napi_create_array_with_length(env, b - a, &arr);
-        for (uint32_t i = a; i < b; ++i) {
-          napi_value v;
-          napi_get_boolean(env, p->sm_valid[i] == 1, &v);
-          napi_set_element(env, arr, i - a, v);
+        if (c < p->sm_packed.n && p->sm_packed.p[c]) {  /* packed call: one Uint8Array of 0 / 1 */
+          void* dst = NULL;
+          napi_value ab;
+          napi_create_arraybuffer(env, b > a ? b - a : 1, &dst, &ab);
+          if (b > a) memcpy(dst, p->sm_valid + a, b - a);
+          napi_create_typedarray(env, napi_uint8_array, b - a, ab, 0, &arr);
+        } else {
+          napi_create_array_with_length(env, b - a, &arr);
+          for (uint32_t i = a; i < b; ++i) {
+            napi_value v;
+            napi_get_boolean(env, p->sm_valid[i] == 1, &v);
+            napi_set_element(env, arr, i - a, v);
+          }
         }
         napi_set_element(env, x, (uint32_t)c, arr);
       }
@@ -1254,6 +1277,30 @@ static napi_value js_signing_roots(napi_env env, napi_callback_info info) {
   return rc ? NULL : ta;
 }
 
+/* replicatePubkeys(ctx, srcFirst, srcN, dstFirst, n): slot[dstFirst + i] = slot[srcFirst + i % srcN]
+ * (gbv_pubkeys_replicate: synthetic tables for benches and tests). */
+static napi_value js_replicate_pubkeys(napi_env env, napi_callback_info info) {
+  size_t argc = 5;
+  napi_value argv[5];
+  NAPI_OK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  addon_ctx* ac = argc >= 1 ? get_ctx(env, argv[0]) : NULL;
+  if (!ac) return NULL;
+  uint32_t a = 0, b = 0, d = 0, n = 0;
+  if (argc < 5 || !get_u32(env, argv[1], &a) || !get_u32(env, argv[2], &b) || !get_u32(env, argv[3], &d) || !get_u32(env, argv[4], &n)) {
+    napi_throw_type_error(env, "GBV_E_ARG", "replicatePubkeys(ctx, srcFirst, srcN, dstFirst, n)");
+    return NULL;
+  }
+  if (ac->closed || !ac->ctx) {
+    throw_rc(env, GBV_E_CLOSED, "QUEUE_ABORTED");
+    return NULL;
+  }
+  lock_begin(ac);
+  int rc = gbv_pubkeys_replicate(ac->ctx, a, b, d, n);
+  if (rc) throw_rc(env, rc, gbv_last_error(ac->ctx));
+  lock_end(ac);
+  return NULL;
+}
+
 static napi_value js_close(napi_env env, napi_callback_info info) {
   size_t argc = 1;
   napi_value argv[1];
@@ -1297,6 +1344,7 @@ static napi_value init(napi_env env, napi_value exports) {
       {"fp12Check", NULL, js_fp12_check, NULL, NULL, NULL, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), NULL},
       {"merkleRoots", NULL, js_merkle_roots, NULL, NULL, NULL, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), NULL},
       {"signingRoots", NULL, js_signing_roots, NULL, NULL, NULL, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), NULL},
+      {"replicatePubkeys", NULL, js_replicate_pubkeys, NULL, NULL, NULL, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), NULL},
   };
   napi_define_properties(env, exports, sizeof props / sizeof props[0], props);
   napi_value mp;

@@ -9,7 +9,7 @@ const addon = require(path.join(__dirname, "gbv_addon.node"));
 
 const EXPORTS = ["open", "addPubkeys", "verifySets", "verifySetsMulti", "verifySameMessageMulti", "aggregatePubkeys",
   "aggregateSerializedPubkeys", "aggregateSignatures", "validateSignatures", "close", "submitPass", "waitPass", "freePasses",
-  "pubkeyCount", "verifySetsSync", "vsPartial", "fp12Check", "merkleRoots", "signingRoots"];
+  "pubkeyCount", "verifySetsSync", "vsPartial", "fp12Check", "merkleRoots", "signingRoots", "replicatePubkeys"];
 const hex = (h) => Uint8Array.from(Buffer.from(h, "hex"));
 const report = {};
 

@@ -76,7 +76,7 @@ def test_addon_builds_and_maps_errors_without_gpu():
     assert r["exports"] == ["open", "addPubkeys", "verifySets", "verifySetsMulti", "verifySameMessageMulti", "aggregatePubkeys",
                             "aggregateSerializedPubkeys", "aggregateSignatures", "validateSignatures", "close", "submitPass",
                             "waitPass", "freePasses", "pubkeyCount", "verifySetsSync", "vsPartial", "fp12Check", "merkleRoots",
-                            "signingRoots"]
+                            "signingRoots", "replicatePubkeys"]
     assert r["maxPasses"] == 3
     assert r["open"] == "ok"      # gbv_init without a device -> Error code GBV_E_DEVICE
     assert r["badCtx"] == "ok"    # not a context -> TypeError code GBV_E_ARG
