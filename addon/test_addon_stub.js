@@ -125,6 +125,14 @@ async function verifier() {
   const smp = v.verifySignatureSetsSameMessage([{index: 0, signature: sig(1)}, {index: 1, signature: sig(0)}], root);
   report.jsBatched = (await bad) === false && (await Promise.all(good)).every((x) => x === true) &&
     JSON.stringify(await smp) === "[true,false]";
+  // packed same-message calls: one chunk, and 300 sets in two chunks (chunkifyMaximizeChunkSize)
+  const packed = (oks) => ({indices: Uint32Array.from(oks.map((_, i) => i % 4)), signatures: Uint8Array.from(Buffer.concat(oks.map((ok) => Buffer.from(sig(ok)))))});
+  const p1 = await v.verifySignatureSetsSameMessage(packed([1, 0, 1]), root);
+  const big = new Array(300).fill(1).map((_, i) => (i % 97 === 5 ? 0 : 1));
+  const p2 = await v.verifySignatureSetsSameMessage(packed(big), root);
+  report.jsPacked = p1 instanceof Uint8Array && Array.from(p1).join(",") === "1,0,1" && p2.length === 300 &&
+    Array.from(p2).every((x, i) => x === big[i]);
+  report.jsPackedBadLength = await codeOf(v.verifySignatureSetsSameMessage({indices: Uint32Array.from([0]), signatures: new Uint8Array(95)}, root));
   // close() with work on the device and queued behind it: device passes resolve, queued jobs reject
   // with QUEUE_ABORTED (multithread/index.ts:238-259), later calls too
   const calls = [v.verifySignatureSets(new Array(300).fill(0).map((_, i) => set(1, i % 4)))].concat(

@@ -282,6 +282,42 @@ def api_path_rate(v, call_off, idx, sigs, msgs, n_sets=1 << 18):
     return round(n / dt, 1), n
 
 
+def api_path_js(call_off, idx, sigs, msgs, key_pks, log, reps=3):
+    """The C2 stream through the JavaScript GpuBlsVerifier over the Node-API addon (addon/bench_api.js, a
+    Node child process with its own device context): every gossip call issued as
+    verifySignatureSetsSameMessage, packed and object-form inputs, every boolean checked.  None when Node
+    or the addon is missing."""
+    import shutil
+    import tempfile
+    node = shutil.which("node") or shutil.which("nodejs")
+    addon = os.path.join(ROOT, "addon", "gbv_addon.node")
+    if node is None or not os.path.exists(addon):
+        return None
+    d = tempfile.mkdtemp(prefix="gbv-api-js-")
+    try:
+        n_calls = len(call_off) - 1
+        with open(os.path.join(d, "meta.json"), "w") as f:
+            json.dump({"n_sets": int(call_off[-1]), "n_calls": n_calls, "n_keys": len(key_pks), "table": N_VALIDATORS}, f)
+        np.asarray(call_off, dtype=np.uint32).tofile(os.path.join(d, "call_off.u32"))
+        np.asarray(idx, dtype=np.uint32).tofile(os.path.join(d, "idx.u32"))
+        for name, blob in (("sigs.bin", sigs), ("msgs.bin", msgs), ("keys.bin", b"".join(key_pks))):
+            with open(os.path.join(d, name), "wb") as f:
+                f.write(blob)
+        p = subprocess.run([node, os.path.join(ROOT, "addon", "bench_api.js"), d, str(reps)], capture_output=True, text=True, timeout=400)
+        lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+        if p.returncode != 0 or not lines:
+            log("api path (js) failed: rc %d %s %s" % (p.returncode, p.stdout[-500:], p.stderr[-500:]))
+            return None
+        r = json.loads(lines[-1])
+        r["how"] = ("node addon/bench_api.js: every gossip call of the C2 workload through GpuBlsVerifier.verifySignatureSetsSameMessage "
+                    "(addon/gpu_bls_verifier.js) over the Node-API addon, all promises awaited, every boolean checked; "
+                    "'packed' = {indices: Uint32Array, signatures: Uint8Array} per call, 'objects' = one {index, signature} per set "
+                    "(built before the clock); best of %d; its own device context beside the bench's" % reps)
+        return r
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+
+
 # ---- verifySignatureSets configs (C1, C3, C4) ------------------------------------------------------
 # device kernel name of each verifySignatureSets stage (the larger-pass forms) and its PMC key
 VS_KERNEL_NAMES = {"agg": "k_vs_agg", "hash_sig": "k_vs_hash_sig", "miller": "k_vs_miller_pair", "chunk_check": "k_vs_chunk_coop"}
@@ -799,6 +835,10 @@ def main():
     api_stream, api_stream_n, api_stream_passes = api_stream_rate(v, call_off, idx, sigs, msgs) if do_api else (None, 0, 0)
     if api_stream:
         log("api stream: %s sets/s over %d sets in %d device passes" % (api_stream, api_stream_n, api_stream_passes))
+    api_js = api_path_js(call_off, idx, sigs, msgs, key_pks, log) if do_api and world == 1 else None
+    if api_js:
+        log("api stream (js): packed %s, objects %s sets/s, lone call %s ms" % (api_js["packed"]["sets_per_s"], api_js["objects"]["sets_per_s"],
+                                                                               api_js["lone_call_p50_ms"]))
 
     # per launch: algorithmic MACs of the sets one k_sm_prepare launch processes / its average duration
     units_per_launch = n_mine / max(prep_launches_per_step, 1)
@@ -851,11 +891,15 @@ def main():
         log("signing roots: %s roots/s" % ssz["value"])
 
     cpu = None
+    cpu_lat = None
     if cpu_ok:
         from oracle import cpu_baseline
         cpu = cpu_baseline.measure_same_message(call_off, idx, sigs, msgs, key_pks, N_KEYS,
                                                 target_sets=args.cpu_sample or 32768)
         log("cpu baseline: %s" % cpu)
+        if not invalid_frac:
+            cpu_lat = cpu_baseline.measure_lone_call_latency(idx, sigs, msgs, key_pks, N_KEYS)
+            log("cpu lone-call latency: %s ms" % cpu_lat["p50_ms"])
 
     if args.mode == "gossip":
         metric = "signature sets verified/sec (batch verify, same-message gossip stream)"
@@ -874,6 +918,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 3),
         "p50_batch_latency_ms": round(lat, 3),
+        "cpu_lone_call_latency": cpu_lat,
         "higher_is_better": True,
         "scaling": scaling,
         "vs_baseline": None,
@@ -889,6 +934,8 @@ def main():
                             "at once; every boolean checked",
                      "sample_sets": api_stream_n, "device_passes": api_stream_passes,
                      "oneshot_sets_per_s": api_rate, "oneshot_how": "one gbv_verify_same_message_multi call from host buffers"},
+        "api_path_js_sets_per_s": api_js["packed"]["sets_per_s"] if api_js else None,
+        "api_path_js": api_js,
         "roofline": roofline,
         "cpu_baseline": cpu,
         "c1": extras.get("c1"),

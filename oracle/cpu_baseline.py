@@ -121,3 +121,33 @@ def measure_verify_sets(calls, pk_rows, threads=None, label=""):
             "sample": "%d sets in %d verifySignatureSets calls%s, %.2fs wall, %d/%d calls true; oracle/c/blsport.c "
                       "(C port, not blst), %d worker threads" % (n, len(calls), label, dt, sum(res), len(calls), threads),
             "all_valid": all(res)}
+
+
+def measure_lone_call_latency(idx, sigs96, msg32, table_pk48, n_keys, n=64, reps=5):
+    """Latency of ONE verifySignatureSetsSameMessage call of n sets on the CPU port, the way the
+    reference pool runs a lone gossip call: one job, aggregateWithRandomness + one verify, no other
+    work to share the cores with -- i.e. single-threaded (multithread/index.ts:212-236, jobItem.ts:
+    69-88).  Beside bench.py's p50_batch_latency_ms (the same call on the GPU through the API).
+    Returns {"p50_ms", "reps", "threads", "kind", "sample"}."""
+    lib = load()
+    aff = {}
+    rows = []
+    for i in range(n):
+        k = int(idx[i]) % n_keys
+        if k not in aff:
+            out = ctypes.create_string_buffer(96)
+            assert lib.port_g1_decompress(bytes(table_pk48[k]), out) == 0
+            aff[k] = out.raw
+        rows.append(aff[k])
+    off = np.array([0, n], dtype=np.uint32)
+    lat, ok = [], True
+    for _ in range(reps):
+        valid = (ctypes.c_uint8 * n)()
+        t = time.perf_counter()
+        lib.port_verify_same_message_batch(1, 1, off.ctypes.data, b"".join(rows), bytes(sigs96[:96 * n]), bytes(msg32[:32]), valid,
+                                           int.from_bytes(os.urandom(8), "little"))
+        lat.append((time.perf_counter() - t) * 1e3)
+        ok = ok and sum(valid) == n
+    return {"p50_ms": round(float(np.median(lat)), 3), "reps": reps, "threads": 1, "kind": "port", "all_valid": ok,
+            "sample": "one %d-set same-message call (the first call's message), oracle/c/blsport.c (C port, not blst), "
+                      "one thread as the pool runs a lone job" % n}

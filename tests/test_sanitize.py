@@ -24,5 +24,6 @@ def test_host_code_is_sanitizer_clean(tmp_path):
     assert all(v is True for k, v in r.items() if isinstance(v, bool)), r
     assert r["streamed"] == [True, True, True] and r["busyThrows"] == "GBV_E_BUSY" and r["waitTwice"] == "GBV_E_ARG"
     assert r["afterClose"] == "QUEUE_ABORTED,QUEUE_ABORTED,QUEUE_ABORTED" and r["pendingAtClose"] == "resolved"
+    assert r["jsPacked"] is True and r["jsPackedBadLength"] == "GBV_E_ARG"
     v = json.load(open(tmp_path / "verifier_cpu.json"))
     assert "fatal" not in v and v["close"] is True and v["basic"] == [True, False, False], v
