@@ -1165,6 +1165,8 @@ void tuning_load() {
     rd("GBV_CHUNK_FINISH_WAVE_MAX", g_tuning.chunk_finish_wave_max);
     rd("GBV_VS_PRE_MAX", g_tuning.vs_pre_max);
     rd("GBV_VS_FS_MAXC", g_tuning.vs_fs_maxc);
+    rd("GBV_VS_QUAD_MAX", g_tuning.vs_quad_max);
+    rd("GBV_VS_PAIR_MAX", g_tuning.vs_pair_max);
     rd("GBV_SYNC_DEBUG", g_tuning.sync_debug);
   });
 }

@@ -1,8 +1,9 @@
-// verifySignatureSets per-set Miller values (k_vs_miller, k_vs_miller_pair) in a translation unit of
-// their own: these kernels run one wave per SIMD (512 registers, VGPRs + AGPRs).
+// verifySignatureSets per-set Miller values (k_vs_miller, k_vs_miller_pair, k_vs_miller_quad) in a
+// translation unit of their own: these kernels run one wave per SIMD (512 registers, VGPRs + AGPRs).
 #include "launch.h"
 #include "kernel_common.h"
 #include "pair.h"
+#include "quad.h"
 
 namespace gbv {
 
@@ -52,18 +53,61 @@ __global__ void GBV_MILLER_ATTR k_vs_miller_pair(uint32_t n, const uint8_t* __re
   vs_miller_pair_body(n, status, rP, H, F);
 }
 
+// The same Miller values on lane quads (quad.h): set i on lanes 4(i mod 16) .. 4(i mod 16) + 3 of
+// block i / 16; lane 2h + s writes Fp components 3s .. 3s + 2 of half h of the conjugated value.
+// Every lane runs the loop (the quad exchanges need all four); quads past n or whose set did not
+// decode write nothing.
+__global__ void GBV_MILLER_ATTR k_vs_miller_quad(uint32_t n, const uint8_t* __restrict__ status, const G1J* __restrict__ rP,
+                                                 const G2A* __restrict__ H, Fp12* __restrict__ F) {
+  quad::Lane L;
+  L.q = threadIdx.x & 3u;
+  L.h = (L.q & 2u) != 0;
+  L.s = (L.q & 1u) != 0;
+  const uint32_t i = blockIdx.x * 16 + (threadIdx.x >> 2);
+  const bool act = i < n && status[i] == SET_OK;
+  const uint32_t j = i < n ? i : n - 1;
+  const G1J p = rP[j];
+  PairP P;
+  P.z3 = fp_mul(fp_sqr(p.z), p.z);
+  P.nxz = fp_neg(fp_mul(p.x, p.z));
+  P.y = p.y;
+  const G2A Q = H[j];
+  PairT T{Q.x, Q.y, fp2_one()};
+  Fp6 M = fp6_sel(L.h, fp6_zero(), fp6_one());
+  for (int b = 62; b >= 0; --b) {
+    if (b != 62) quad::sqr(M, L);
+    Line l = quad::dbl(T, P, L.q);
+    quad::mul_line(M, l, L);
+    if ((X_ABS >> b) & 1ull) {
+      l = quad::add(T, Q, P, L.q);
+      quad::mul_line(M, l, L);
+    }
+  }
+  if (!act) return;
+  if (L.h) M = fp6_neg(M);
+  // this lane's three Fp of the half: s = 0 -> c0.c0, c0.c1, c1.c0; s = 1 -> c1.c1, c2.c0, c2.c1
+  Fp* out = (Fp*)&F[i] + 6 * (L.h ? 1 : 0) + 3 * (L.s ? 1 : 0);
+  out[0] = fp_sel(L.s, M.c1.c1, M.c0.c0);
+  out[1] = fp_sel(L.s, M.c2.c0, M.c0.c1);
+  out[2] = fp_sel(L.s, M.c2.c1, M.c1.c0);
+}
+
 void launch_vs_miller(LaunchCfg c, uint32_t n, const uint8_t* status, const G1J* rP, const G2A* H, Fp12* F) {
   if (n == 0) return;
-  // Lane pairs for passes of up to PAIR_MAX sets (range-sync segments: the pairs halve each set's
-  // latency and the pass has fewer waves than SIMDs), one thread per set above (C3-sized passes,
-  // measured equal or better: profiles/r03e).
-  constexpr uint32_t PAIR_MAX = 32768;
-  if (n > PAIR_MAX) {
+  // Lane quads for passes of up to vs_quad_max sets (range-sync segments, shards: the pass has fewer
+  // waves than SIMDs, and four lanes per set quarter each set's latency's product count), lane pairs
+  // up to vs_pair_max, one thread per set above (C3-sized passes, measured equal or better:
+  // profiles/r03e).
+  const Tuning& t = tuning();
+  if (n > t.vs_pair_max) {
     hipLaunchKernelGGL(k_vs_miller, dim3((n + 63) / 64), dim3(64), 0, c.stream, n, status, rP, H, F);
     debug_sync(c.stream, "k_vs_miller");
-  } else {
+  } else if (n > t.vs_quad_max) {
     hipLaunchKernelGGL(k_vs_miller_pair, dim3((n + 31) / 32), dim3(64), 0, c.stream, n, status, rP, H, F);
     debug_sync(c.stream, "k_vs_miller_pair");
+  } else {
+    hipLaunchKernelGGL(k_vs_miller_quad, dim3((n + 15) / 16), dim3(64), 0, c.stream, n, status, rP, H, F);
+    debug_sync(c.stream, "k_vs_miller_quad");
   }
 }
 

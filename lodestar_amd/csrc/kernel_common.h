@@ -70,6 +70,8 @@ struct Tuning {
   uint32_t chunk_finish_wave_max = 32;     // GBV_CHUNK_FINISH_WAVE_MAX: chunk sums one wave per chunk up to this many
   uint32_t vs_pre_max = 16384;             // GBV_VS_PRE_MAX: verifySignatureSets signature half beside the aggregation
   uint32_t vs_fs_maxc = 256;               // GBV_VS_FS_MAXC: per-chunk (-g1, sum) Miller value beside the per-set ones
+  uint32_t vs_quad_max = 16384;            // GBV_VS_QUAD_MAX: per-set Miller values on lane quads up to this many sets
+  uint32_t vs_pair_max = 32768;            // GBV_VS_PAIR_MAX: ... on lane pairs up to this many (one lane per set above)
   uint32_t sync_debug = 0;                 // GBV_SYNC_DEBUG: synchronise + report after every launch (debugging)
 };
 const Tuning& tuning();
