@@ -1,6 +1,7 @@
 // hash_to_G2 kernels.  The few-message forms are latency-bound (lane pairs, one wave per message).
 #include "launch.h"
 #include "kernel_common.h"
+#include "quad_g2.h"
 
 namespace gbv {
 
@@ -21,6 +22,23 @@ __global__ void GBV_KERNEL_ATTR k_hash_msgs_pair(const uint8_t* __restrict__ msg
   if (act) load_msg_words(w, msgs32 + 32ull * i);
   G2A h;
   if (hash_to_g2_lane_pair(w, act, &h)) H[i] = h;
+}
+
+// Four lanes per message (quad_g2.h): lanes q = 0, 2 map u_0 and lanes 1, 3 map u_1 (the map is two
+// Fp exponentiations in a row: nothing to split), then the quad adds Q0 + Q1, clears the cofactor and
+// makes the point affine with every product on its own lane -- about half the pair form's chain.
+__global__ void GBV_KERNEL_ATTR k_hash_msgs_quad(const uint8_t* __restrict__ msgs32, uint32_t n, G2A* __restrict__ H) {
+  const uint32_t q = threadIdx.x & 3u;
+  const uint32_t i = blockIdx.x * 16 + (threadIdx.x >> 2);
+  const bool act = i < n;
+  uint32_t w[8];
+  load_msg_words(w, msgs32 + 32ull * (act ? i : 0u));  // past n: message 0 again, nothing written
+  const G2J m = hash_map_iso(hash_to_field_fp2(w, (int)(q & 1u)));
+  G2J p = quad::g2_add(quad::dpp<0x00>(m), quad::dpp<0x55>(m), q);
+  p = quad::g2_clear_cofactor(p, q);
+  G2A a;
+  quad::g2_to_aff(a, p, q);
+  if (act) quad::store_split<4>((Fp*)&H[i], (const Fp*)&a, q);
 }
 
 __global__ void GBV_KERNEL_ATTR k_hash_msgs_pre(const uint8_t* __restrict__ msgs32, uint32_t n, G2J* __restrict__ Qpre) {
@@ -50,7 +68,9 @@ void launch_hash_msgs(LaunchCfg c, const uint8_t* msgs32, uint32_t n, G2A* H, G2
     launch_hash_clear_coop(c.stream, n, Qpre, H);
     return;
   }
-  if (n <= tuning().hash_pair_max)  // latency: lane pairs (grid sized here; c.blocks is for one lane per message)
+  if (n <= tuning().hash_quad_max)  // latency: lane quads, then lane pairs (grids sized here; c.blocks is for one lane per message)
+    hipLaunchKernelGGL(k_hash_msgs_quad, dim3((n + 15) / 16), dim3(64), 0, c.stream, msgs32, n, H);
+  else if (n <= tuning().hash_pair_max)
     hipLaunchKernelGGL(k_hash_msgs_pair, dim3((2 * n + 63) / 64), dim3(64), 0, c.stream, msgs32, n, H);
   else
     hipLaunchKernelGGL(k_hash_msgs, dim3(c.blocks), dim3(c.threads), 0, c.stream, msgs32, n, H);

@@ -3,6 +3,7 @@
 
 #include "launch.h"
 #include "kernel_common.h"
+#include "quad_g2.h"
 
 namespace gbv {
 
@@ -244,6 +245,37 @@ __global__ void GBV_KERNEL_ATTR k_vs_sig_pre(uint32_t n, const uint8_t* __restri
   rS_out[i] = rs;
 }
 
+// The same two roles on lane quads (quad_g2.h), one quad per set and role: blocks [0, nq) check,
+// blocks [nq, 2 nq) randomise, 16 sets per block.  Every lane decodes (the square root is two Fp
+// exponentiations in a row); the subgroup check's 63 doublings and r_i sig_i's 31-step ladder run
+// their products four at a time.
+__global__ void GBV_KERNEL_ATTR k_vs_sig_pre_quad(uint32_t n, const uint8_t* __restrict__ sig, uint32_t sig_stride,
+                                                  const uint32_t* __restrict__ sig_len, Seed seed, uint32_t nonce, G2J* __restrict__ rS_out,
+                                                  uint8_t* __restrict__ status, uint8_t* __restrict__ sig_st) {
+  const uint32_t nq = (n + 15) / 16;
+  uint32_t blk = blockIdx.x;
+  const bool rand = blk >= nq;
+  if (rand) blk -= nq;
+  const uint32_t q = threadIdx.x & 3u;
+  const uint32_t i = blk * 16 + (threadIdx.x >> 2);
+  if (i >= n) return;  // whole quads
+  G2A s;
+  const uint8_t ds = g2_decode(s, sig + (size_t)sig_stride * i, sig_len[i]);
+  if (!rand) {
+    const uint8_t st = (ds != PT_OK || !quad::g2_in_subgroup(s, q)) ? SET_BAD_SIG : SET_OK;
+    if (q == 0) {
+      status[i] = st;
+      sig_st[i] = st;
+    }
+    return;
+  }
+  if (ds != PT_OK) return;
+  const uint64_t r = prf_scalar(seed, i, nonce);
+  G2J rs;
+  if (!quad::g2_randomize(s, r, &rs, q)) rs = g2_mul_u64(s, r);  // unreachable for subgroup points
+  quad::store_split<6>((Fp*)&rS_out[i], (const Fp*)&rs, q);
+}
+
 // The pubkey half (stream A, after the aggregation and k_vs_sig_pre): a rejected signature's verdict
 // stands (it wins over a bad pubkey, as in k_vs_hash_sig); otherwise the pubkey's verdict is merged
 // and r_i pk_i formed.  Raw pubkeys (PublicKey.fromBytes(pk, true)) are decoded and group-checked here.
@@ -282,6 +314,46 @@ __global__ void GBV_KERNEL_ATTR k_vs_pk_rand(uint32_t n, const uint32_t* __restr
   G1J rp;
   if (!randomize_g1(pa, r, &rp)) rp = g1_mul_u64(pa, r);
   rP_out[i] = rp;
+}
+
+// k_vs_pk_rand on lane quads (small passes): the same pubkey fetch and verdict merge on every lane of
+// the quad, r_i pk_i by quad_g2.h's G1 ladder (3 + 5 product rounds a step against 18 products).
+__global__ void GBV_KERNEL_ATTR k_vs_pk_rand_quad(uint32_t n, const uint32_t* __restrict__ set_off, const uint32_t* __restrict__ arena,
+                                                  const uint8_t* __restrict__ raw_flag, const uint8_t* __restrict__ raw_pk48,
+                                                  const G1A* __restrict__ table, const uint8_t* __restrict__ table_ok,
+                                                  const G1J* __restrict__ pk_agg, const uint8_t* __restrict__ pk_st, Seed seed, uint32_t nonce,
+                                                  G1J* __restrict__ rP_out, uint8_t* __restrict__ status) {
+  const uint32_t q = threadIdx.x & 3u;
+  const uint32_t i = blockIdx.x * 16 + (threadIdx.x >> 2);
+  if (i >= n || status[i] != SET_OK) return;  // whole quads
+  bool ok = true, jac = false;
+  G1A pa{fp_zero(), fp_zero()};
+  G1J pj;
+  if (raw_flag[i]) {
+    ok = g1_decompress(pa, raw_pk48 + 48ull * i) == PT_OK && g1_in_subgroup(pa);
+  } else {
+    const uint32_t b = set_off[i], e = set_off[i + 1];
+    if (e - b == 1) {
+      const uint32_t k = arena[b];
+      pa = table[k];
+      ok = table_ok[k] != 0;
+    } else if (e == b) {
+      ok = false;
+    } else {
+      pj = pk_agg[i];
+      jac = true;
+      ok = pk_st[i] == SET_OK;
+    }
+  }
+  if (ok && jac) ok = jac_to_aff(pa, pj);
+  if (!ok) {
+    if (q == 0) status[i] = SET_BAD_PK;
+    return;
+  }
+  const uint64_t r = prf_scalar(seed, i, nonce);
+  G1J rp;
+  if (!quad::g1_randomize(pa, r, &rp, q)) rp = g1_mul_u64(pa, r);
+  quad::store_split<3>((Fp*)&rP_out[i], (const Fp*)&rp, q);
 }
 
 // Signature.fromBytes(sig, true) (maybeBatch.ts:23; the "BLS deserializing signatures" perf id,
@@ -382,6 +454,12 @@ void launch_vs_hash_sig(hipStream_t s, uint32_t n, const uint8_t* msgs32, const 
 
 void launch_vs_sig_pre(hipStream_t s, uint32_t n, const uint8_t* sig, uint32_t sig_stride, const uint32_t* sig_len, const Seed& seed,
                        uint32_t nonce, G2J* rS, uint8_t* status, uint8_t* sig_st) {
+  if (n <= tuning().vs_sig_quad_max) {
+    hipLaunchKernelGGL(k_vs_sig_pre_quad, dim3(2 * ((n + 15) / 16)), dim3(64), 0, s, n, sig, sig_stride, sig_len, seed, nonce, rS, status,
+                       sig_st);
+    debug_sync(s, "k_vs_sig_pre_quad");
+    return;
+  }
   const uint32_t nsig = (n + 63) / 64;
   hipLaunchKernelGGL(k_vs_sig_pre, dim3(2 * nsig), dim3(64), 0, s, n, sig, sig_stride, sig_len, seed, nonce, rS, status, sig_st);
   debug_sync(s, "k_vs_sig_pre");
@@ -389,6 +467,12 @@ void launch_vs_sig_pre(hipStream_t s, uint32_t n, const uint8_t* sig, uint32_t s
 void launch_vs_pk_rand(hipStream_t s, uint32_t n, const uint32_t* set_off, const uint32_t* arena, const uint8_t* raw_flag,
                        const uint8_t* raw_pk48, const G1A* table, const uint8_t* table_ok, const G1J* pk_agg, const uint8_t* pk_st,
                        const Seed& seed, uint32_t nonce, G1J* rP, uint8_t* status) {
+  if (n <= tuning().vs_sig_quad_max) {
+    hipLaunchKernelGGL(k_vs_pk_rand_quad, dim3((n + 15) / 16), dim3(64), 0, s, n, set_off, arena, raw_flag, raw_pk48, table, table_ok, pk_agg,
+                       pk_st, seed, nonce, rP, status);
+    debug_sync(s, "k_vs_pk_rand_quad");
+    return;
+  }
   hipLaunchKernelGGL(k_vs_pk_rand, dim3((n + 63) / 64), dim3(64), 0, s, n, set_off, arena, raw_flag, raw_pk48, table, table_ok, pk_agg, pk_st,
                      seed, nonce, rP, status);
   debug_sync(s, "k_vs_pk_rand");

@@ -53,11 +53,15 @@ __global__ void GBV_MILLER_ATTR k_vs_miller_pair(uint32_t n, const uint8_t* __re
   vs_miller_pair_body(n, status, rP, H, F);
 }
 
+#ifndef GBV_MILLER_QUAD_WPE
+#define GBV_MILLER_QUAD_WPE 2
+#endif
+#define GBV_MILLER_QUAD_ATTR __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GBV_MILLER_QUAD_WPE, GBV_MILLER_QUAD_WPE)))
 // The same Miller values on lane quads (quad.h): set i on lanes 4(i mod 16) .. 4(i mod 16) + 3 of
 // block i / 16; lane 2h + s writes Fp components 3s .. 3s + 2 of half h of the conjugated value.
 // Every lane runs the loop (the quad exchanges need all four); quads past n or whose set did not
 // decode write nothing.
-__global__ void GBV_MILLER_ATTR k_vs_miller_quad(uint32_t n, const uint8_t* __restrict__ status, const G1J* __restrict__ rP,
+__global__ void GBV_MILLER_QUAD_ATTR k_vs_miller_quad(uint32_t n, const uint8_t* __restrict__ status, const G1J* __restrict__ rP,
                                                  const G2A* __restrict__ H, Fp12* __restrict__ F) {
   quad::Lane L;
   L.q = threadIdx.x & 3u;

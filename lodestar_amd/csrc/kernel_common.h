@@ -64,6 +64,7 @@ constexpr uint32_t HASH_PAIR_MAX = 4096;
 // path consults the environment.  Defaults are the measured choices of DESIGN.md section 7.
 struct Tuning {
   uint32_t hash_pair_max = HASH_PAIR_MAX;  // GBV_HASH_PAIR_MAX: hash on lane pairs up to this many messages
+  uint32_t hash_quad_max = 16384;          // GBV_HASH_QUAD_MAX: hash on lane quads up to this many messages
   uint32_t hash_coop_max = 256;            // GBV_HASH_COOP_MAX: cooperative cofactor clearing up to this many
   uint32_t prepare_split_max = 2048;       // GBV_PREPARE_SPLIT_MAX: same-message latency prepare up to this many sets
   uint32_t prep_coop_rand_max = 512;       // GBV_PREP_COOP_RAND: r sig one wave per set up to this many sets
@@ -71,6 +72,7 @@ struct Tuning {
   uint32_t vs_pre_max = 16384;             // GBV_VS_PRE_MAX: verifySignatureSets signature half beside the aggregation
   uint32_t vs_fs_maxc = 256;               // GBV_VS_FS_MAXC: per-chunk (-g1, sum) Miller value beside the per-set ones
   uint32_t vs_quad_max = 16384;            // GBV_VS_QUAD_MAX: per-set Miller values on lane quads up to this many sets
+  uint32_t vs_sig_quad_max = 16384;        // GBV_VS_SIG_QUAD_MAX: "pre" signature work on lane quads up to this many sets
   uint32_t vs_pair_max = 32768;            // GBV_VS_PAIR_MAX: ... on lane pairs up to this many (one lane per set above)
   uint32_t sync_debug = 0;                 // GBV_SYNC_DEBUG: synchronise + report after every launch (debugging)
 };

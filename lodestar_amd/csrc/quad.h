@@ -43,6 +43,9 @@ template <int CTRL> __device__ __forceinline__ Fp dpp(const Fp& a) {
 }
 template <int CTRL> __device__ __forceinline__ Fp2 dpp(const Fp2& a) { return Fp2{dpp<CTRL>(a.c0), dpp<CTRL>(a.c1)}; }
 template <int CTRL> __device__ __forceinline__ Fp6 dpp(const Fp6& a) { return Fp6{dpp<CTRL>(a.c0), dpp<CTRL>(a.c1), dpp<CTRL>(a.c2)}; }
+template <int CTRL, class F> __device__ __forceinline__ Jac<F> dpp(const Jac<F>& a) {
+  return Jac<F>{dpp<CTRL>(a.x), dpp<CTRL>(a.y), dpp<CTRL>(a.z)};
+}
 
 struct Lane {
   uint32_t q;  // lane in the quad
@@ -51,6 +54,19 @@ struct Lane {
 
 __device__ __forceinline__ Fp sel4(uint32_t q, const Fp& x0, const Fp& x1, const Fp& x2, const Fp& x3) {
   return fp_sel((q & 2u) != 0, fp_sel((q & 1u) != 0, x3, x2), fp_sel((q & 1u) != 0, x1, x0));
+}
+
+// Store of a value every quad lane holds: lane j writes Fp words j, j + 4, ... (n_fp Fp in all)
+template <int NFP> __device__ __forceinline__ void store_split(Fp* out, const Fp* v, uint32_t q) {
+#pragma unroll
+  for (int k = 0; k < NFP; k += 4) {
+    if (k + 3 < NFP) {
+      out[k + q] = sel4(q, v[k], v[k + 1], v[k + 2], v[k + 3]);
+    } else {
+      const Fp a = v[k], b = k + 1 < NFP ? v[k + 1] : v[k], c = k + 2 < NFP ? v[k + 2] : v[k];
+      if (k + q < (uint32_t)NFP) out[k + q] = sel4(q, a, b, c, c);
+    }
+  }
 }
 
 // One round of four Fp products on the quad: lane j runs a_j b_j; every lane returns all four.

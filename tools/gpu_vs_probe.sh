@@ -7,8 +7,8 @@ shift
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-timeout -k 10 150 python3 -u tools/vs_probe.py --blocks 64 > "$OUT/a.txt" 2>&1 || { tail -20 "$OUT/a.txt"; exit 1; }
-tail -1 "$OUT/a.txt"
+timeout -k 10 200 python3 -u tools/vs_probe.py --blocks 64 --inflight ${INFLIGHT:-1,2,3,4} > "$OUT/a.txt" 2>&1 || { tail -20 "$OUT/a.txt"; exit 1; }
+grep -v "^\[probe\]" "$OUT/a.txt"
 if [ $# -gt 0 ]; then
   env "$@" timeout -k 10 150 python3 -u tools/vs_probe.py --blocks 64 > "$OUT/b.txt" 2>&1 || { tail -20 "$OUT/b.txt"; exit 1; }
   echo "B ($*):"; tail -1 "$OUT/b.txt"
