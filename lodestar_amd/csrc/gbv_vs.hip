@@ -297,14 +297,15 @@ static bool vs_fs_small(const gbv_vs_batch* b) { return b->n <= VS_COOP_MILLER_M
 // stream m (a tail stream, so that they overlap the next batch's stream-A kernels; or stream A).
 // Events: ev0 agg ev1 hash_sig ev2 | (m) ev3 miller ev4.
 // with_fs: the chunk checks follow (gbv_vs_batch_submit), so a small pass also forms each chunk's
-// (-g1, sum r_i sig_i) Miller value beside the per-set ones.
-static int vs_enqueue_sets(gbv_ctx* c, gbv_vs_batch* b, hipStream_t m, bool with_fs) {
+// (-g1, sum r_i sig_i) Miller value beside the per-set ones.  partial: a shard's Fp12 partial follows
+// (gbv_vs_partial); it takes the same split of the signature half (pre mode) and the hash on stream m.
+static int vs_enqueue_sets(gbv_ctx* c, gbv_vs_batch* b, hipStream_t m, bool with_fs, bool partial = false) {
   hipStream_t s = c->stream;
   Seed seed = fresh_seed();
   uint32_t nonce = c->nonce++;
   // passes up to GBV_VS_PRE_MAX sets: the signature half first, on stream 5, beside the aggregation below
   const bool small = with_fs && vs_fs_small(b);
-  const bool pre = with_fs && m != s && vs_pre_on(b);
+  const bool pre = (with_fs || partial) && m != s && vs_pre_on(b);
   if (pre) {
     HIP_CHECK(c, hipStreamWaitEvent(c->stream5, b->copied, 0));
     launch_vs_sig_pre(c->stream5, (uint32_t)b->n, b->sig, b->sig_stride, b->siglen, seed, nonce, b->rS, b->status, b->sig_st);
@@ -323,7 +324,7 @@ static int vs_enqueue_sets(gbv_ctx* c, gbv_vs_batch* b, hipStream_t m, bool with
   HIP_CHECK(c, hipEventRecord(b->ev[1], s));
   // small passes and pre mode: the hash on stream m (for few messages lane-pair maps and the
   // cooperative cofactor clearing) beside the signature work
-  const bool split = with_fs && m != s && (small || pre);
+  const bool split = (with_fs || partial) && m != s && (small || pre);
   if (split) HIP_CHECK(c, hipStreamWaitEvent(m, b->copied, 0));
   if (split) launch_hash_msgs(LaunchCfg{blocks_for(b->n), TPB, m}, b->msgs, (uint32_t)b->n, b->H, b->Hpre);
   if (pre) {
@@ -572,8 +573,10 @@ static int vs_partial_enqueue(gbv_ctx* c, gbv_vs_batch* b) {
     b->part_host_cap = cap;
   }
   HIP_CHECK(c, hipSetDevice(c->device));
-  hipStream_t s = c->stream;
-  if ((rc = vs_enqueue_sets(c, b, s, false))) {
+  // a shard of up to GBV_VS_PRE_MAX sets (a per-GPU share of one large call at N = 8): the hash on the
+  // tail stream beside the split signature / pubkey halves, the rest on the tail stream after them
+  hipStream_t s = vs_pre_on(b) ? c->stream2 : c->stream;
+  if ((rc = vs_enqueue_sets(c, b, s, false, true))) {
     ctx_drain(c);
     return rc;
   }

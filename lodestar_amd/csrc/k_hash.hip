@@ -27,7 +27,7 @@ __global__ void GBV_KERNEL_ATTR k_hash_msgs_pair(const uint8_t* __restrict__ msg
 // Four lanes per message (quad_g2.h): lanes q = 0, 2 map u_0 and lanes 1, 3 map u_1 (the map is two
 // Fp exponentiations in a row: nothing to split), then the quad adds Q0 + Q1, clears the cofactor and
 // makes the point affine with every product on its own lane -- about half the pair form's chain.
-__global__ void GBV_KERNEL_ATTR k_hash_msgs_quad(const uint8_t* __restrict__ msgs32, uint32_t n, G2A* __restrict__ H) {
+__global__ void GBV_QUAD_ATTR k_hash_msgs_quad(const uint8_t* __restrict__ msgs32, uint32_t n, G2A* __restrict__ H) {
   const uint32_t q = threadIdx.x & 3u;
   const uint32_t i = blockIdx.x * 16 + (threadIdx.x >> 2);
   const bool act = i < n;

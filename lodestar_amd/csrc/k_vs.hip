@@ -249,7 +249,7 @@ __global__ void GBV_KERNEL_ATTR k_vs_sig_pre(uint32_t n, const uint8_t* __restri
 // blocks [nq, 2 nq) randomise, 16 sets per block.  Every lane decodes (the square root is two Fp
 // exponentiations in a row); the subgroup check's 63 doublings and r_i sig_i's 31-step ladder run
 // their products four at a time.
-__global__ void GBV_KERNEL_ATTR k_vs_sig_pre_quad(uint32_t n, const uint8_t* __restrict__ sig, uint32_t sig_stride,
+__global__ void GBV_QUAD_ATTR k_vs_sig_pre_quad(uint32_t n, const uint8_t* __restrict__ sig, uint32_t sig_stride,
                                                   const uint32_t* __restrict__ sig_len, Seed seed, uint32_t nonce, G2J* __restrict__ rS_out,
                                                   uint8_t* __restrict__ status, uint8_t* __restrict__ sig_st) {
   const uint32_t nq = (n + 15) / 16;
@@ -318,7 +318,7 @@ __global__ void GBV_KERNEL_ATTR k_vs_pk_rand(uint32_t n, const uint32_t* __restr
 
 // k_vs_pk_rand on lane quads (small passes): the same pubkey fetch and verdict merge on every lane of
 // the quad, r_i pk_i by quad_g2.h's G1 ladder (3 + 5 product rounds a step against 18 products).
-__global__ void GBV_KERNEL_ATTR k_vs_pk_rand_quad(uint32_t n, const uint32_t* __restrict__ set_off, const uint32_t* __restrict__ arena,
+__global__ void GBV_QUAD_ATTR k_vs_pk_rand_quad(uint32_t n, const uint32_t* __restrict__ set_off, const uint32_t* __restrict__ arena,
                                                   const uint8_t* __restrict__ raw_flag, const uint8_t* __restrict__ raw_pk48,
                                                   const G1A* __restrict__ table, const uint8_t* __restrict__ table_ok,
                                                   const G1J* __restrict__ pk_agg, const uint8_t* __restrict__ pk_st, Seed seed, uint32_t nonce,

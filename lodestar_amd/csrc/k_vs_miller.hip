@@ -54,7 +54,7 @@ __global__ void GBV_MILLER_ATTR k_vs_miller_pair(uint32_t n, const uint8_t* __re
 }
 
 #ifndef GBV_MILLER_QUAD_WPE
-#define GBV_MILLER_QUAD_WPE 2
+#define GBV_MILLER_QUAD_WPE 1  // one wave per SIMD: 512 registers, far fewer frame spills (64-block pass Miller 6.2 -> 3.7 ms)
 #endif
 #define GBV_MILLER_QUAD_ATTR __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GBV_MILLER_QUAD_WPE, GBV_MILLER_QUAD_WPE)))
 // The same Miller values on lane quads (quad.h): set i on lanes 4(i mod 16) .. 4(i mod 16) + 3 of

@@ -31,6 +31,11 @@
 #define GBV_WAVES_PER_EU 2
 #endif
 #define GBV_KERNEL_ATTR __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GBV_WAVES_PER_EU)))
+// lane-quad point kernels of small passes (k_hash_msgs_quad, k_vs_sig_pre_quad, k_vs_pk_rand_quad)
+#ifndef GBV_QUAD_WPE
+#define GBV_QUAD_WPE 1  // 512 registers, fewer frame spills: 64-block pass 12.2 -> 11.75 ms, 2 in flight 9.3 -> 8.3-8.6 ms
+#endif
+#define GBV_QUAD_ATTR __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GBV_QUAD_WPE, GBV_QUAD_WPE)))
 
 // Tail kernels (chunk Miller values, MSM reduction, segment reduction and check) share SIMDs with
 // the next batch's k_sm_prepare; GBV_TAIL_PRIO > 0 raises their waves' issue priority (s_setprio)
@@ -65,7 +70,8 @@ constexpr uint32_t HASH_PAIR_MAX = 4096;
 struct Tuning {
   uint32_t hash_pair_max = HASH_PAIR_MAX;  // GBV_HASH_PAIR_MAX: hash on lane pairs up to this many messages
   uint32_t hash_quad_max = 16384;          // GBV_HASH_QUAD_MAX: hash on lane quads up to this many messages
-  uint32_t hash_coop_max = 256;            // GBV_HASH_COOP_MAX: cooperative cofactor clearing up to this many
+  uint32_t hash_coop_max = 0;              // GBV_HASH_COOP_MAX: cooperative cofactor clearing up to this many (0: the
+                                           // lane-quad hash is shorter for every count: lone call 7.05 -> 6.65 ms)
   uint32_t prepare_split_max = 2048;       // GBV_PREPARE_SPLIT_MAX: same-message latency prepare up to this many sets
   uint32_t prep_coop_rand_max = 512;       // GBV_PREP_COOP_RAND: r sig one wave per set up to this many sets
   uint32_t chunk_finish_wave_max = 32;     // GBV_CHUNK_FINISH_WAVE_MAX: chunk sums one wave per chunk up to this many
