@@ -53,6 +53,8 @@ struct gbv_vs_batch {
   uint8_t* sig_st = nullptr;  // "pre" mode: the signature verdicts alone (k_vs_sig_pre), read by k_vs_chunk_s_miller
   Fp12* F = nullptr;
   G2J* Hpre = nullptr;        // per set: Q0 + Q1 before the cofactor clearing (small passes)
+  G2A* Sd = nullptr;          // "pre" mode on lane quads: the decoded signatures (k_vs_sig_decode)
+  uint8_t* dec_st = nullptr;  // ... and their GBV_PT_* decode codes
   Fp12* Fs = nullptr;         // per chunk: Miller value of (-g1, sum r_i sig_i) (small passes, k_vs_miller_coop)
   uint8_t* fs_flag = nullptr;
   uint8_t* chunk_valid = nullptr;
@@ -76,8 +78,8 @@ struct gbv_vs_batch {
 static void vs_free_work(gbv_vs_batch* b) {
   // teardown: a failing free has nothing left to report to
   (void)hipFree(b->pk); (void)hipFree(b->pk_st); (void)hipFree(b->H); (void)hipFree(b->rP); (void)hipFree(b->rS);
-  (void)hipFree(b->status); (void)hipFree(b->sig_st); (void)hipFree(b->F); (void)hipFree(b->Fs); (void)hipFree(b->Hpre); (void)hipFree(b->fs_flag); (void)hipFree(b->chunk_valid); (void)hipHostFree(b->chunk_valid_host);
-  b->pk = nullptr; b->pk_st = nullptr; b->H = nullptr; b->rP = nullptr; b->rS = nullptr; b->status = nullptr; b->sig_st = nullptr; b->F = nullptr; b->Fs = nullptr; b->fs_flag = nullptr; b->Hpre = nullptr;
+  (void)hipFree(b->status); (void)hipFree(b->sig_st); (void)hipFree(b->F); (void)hipFree(b->Fs); (void)hipFree(b->Hpre); (void)hipFree(b->Sd); (void)hipFree(b->dec_st); (void)hipFree(b->fs_flag); (void)hipFree(b->chunk_valid); (void)hipHostFree(b->chunk_valid_host);
+  b->pk = nullptr; b->pk_st = nullptr; b->H = nullptr; b->rP = nullptr; b->rS = nullptr; b->status = nullptr; b->sig_st = nullptr; b->F = nullptr; b->Fs = nullptr; b->fs_flag = nullptr; b->Hpre = nullptr; b->Sd = nullptr; b->dec_st = nullptr;
   b->chunk_valid = nullptr; b->chunk_valid_host = nullptr;
   b->allocated = false;
 }
@@ -114,6 +116,7 @@ static int vs_reserve(gbv_ctx* c, gbv_vs_batch* b, size_t n, size_t C) {
   chk(dalloc(&b->pk, n)); chk(dalloc(&b->pk_st, n)); chk(dalloc(&b->H, n)); chk(dalloc(&b->rP, n)); chk(dalloc(&b->rS, n));
   chk(dalloc(&b->status, n)); chk(dalloc(&b->sig_st, n)); chk(dalloc(&b->F, n)); chk(dalloc(&b->chunk_valid, C));
   chk(dalloc(&b->Fs, C)); chk(dalloc(&b->fs_flag, C)); chk(dalloc(&b->Hpre, n));
+  chk(dalloc(&b->Sd, n)); chk(dalloc(&b->dec_st, n));
   chk(hipHostMalloc((void**)&b->chunk_valid_host, std::max<size_t>(C, 1), hipHostMallocDefault));
   for (auto& ev : b->ev)
     if (!ev) chk(hipEventCreate(&ev));
@@ -308,7 +311,8 @@ static int vs_enqueue_sets(gbv_ctx* c, gbv_vs_batch* b, hipStream_t m, bool with
   const bool pre = (with_fs || partial) && m != s && vs_pre_on(b);
   if (pre) {
     HIP_CHECK(c, hipStreamWaitEvent(c->stream5, b->copied, 0));
-    launch_vs_sig_pre(c->stream5, (uint32_t)b->n, b->sig, b->sig_stride, b->siglen, seed, nonce, b->rS, b->status, b->sig_st);
+    launch_vs_sig_pre(c->stream5, (uint32_t)b->n, b->sig, b->sig_stride, b->siglen, seed, nonce, b->rS, b->status, b->sig_st, b->Sd,
+                      b->dec_st);
     HIP_CHECK(c, hipEventRecord(b->pre, c->stream5));
     if (small) {
       // each chunk's sum r_i sig_i and its (-g1, sum) Miller value need no pubkey either: they follow

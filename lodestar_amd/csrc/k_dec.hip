@@ -29,6 +29,27 @@ k_sig_decode(uint32_t base, uint32_t n, const uint8_t* __restrict__ sig96, G2A* 
   status[i] = ds;
 }
 
+// The same for verifySignatureSets passes on lane quads (k_vs_sig_pre_quad): compressed or uncompressed
+// encodings (sig_len 96 / 192; 0 = a length the reference rejects), one thread per signature, so that
+// the quad roles do not each run the ~900-product decompression chain on all four lanes.
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GBV_DEC_WAVES)))
+k_vs_sig_decode(uint32_t n, const uint8_t* __restrict__ sig, uint32_t sig_stride, const uint32_t* __restrict__ sig_len,
+                G2A* __restrict__ S, uint8_t* __restrict__ dec_st) {
+  const uint32_t i = blockIdx.x * 64 + threadIdx.x;
+  if (i >= n) return;
+  G2A s;
+  const uint8_t ds = g2_decode(s, sig + (size_t)sig_stride * i, sig_len[i]);
+  if (ds == PT_OK) S[i] = s;
+  dec_st[i] = ds;
+}
+
+void launch_vs_sig_decode(hipStream_t s, uint32_t n, const uint8_t* sig, uint32_t sig_stride, const uint32_t* sig_len, G2A* S,
+                          uint8_t* dec_st) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_vs_sig_decode, dim3((n + 63) / 64), dim3(64), 0, s, n, sig, sig_stride, sig_len, S, dec_st);
+  debug_sync(s, "k_vs_sig_decode");
+}
+
 void launch_sig_decode(hipStream_t s, uint32_t base, uint32_t n, const uint8_t* sig96, G2A* S, uint8_t* status) {
   if (!n) return;
   hipLaunchKernelGGL(k_sig_decode, dim3((n + 63) / 64), dim3(64), 0, s, base, n, sig96, S, status);

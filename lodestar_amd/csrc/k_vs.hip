@@ -246,12 +246,12 @@ __global__ void GBV_KERNEL_ATTR k_vs_sig_pre(uint32_t n, const uint8_t* __restri
 }
 
 // The same two roles on lane quads (quad_g2.h), one quad per set and role: blocks [0, nq) check,
-// blocks [nq, 2 nq) randomise, 16 sets per block.  Every lane decodes (the square root is two Fp
-// exponentiations in a row); the subgroup check's 63 doublings and r_i sig_i's 31-step ladder run
-// their products four at a time.
-__global__ void GBV_QUAD_ATTR k_vs_sig_pre_quad(uint32_t n, const uint8_t* __restrict__ sig, uint32_t sig_stride,
-                                                  const uint32_t* __restrict__ sig_len, Seed seed, uint32_t nonce, G2J* __restrict__ rS_out,
-                                                  uint8_t* __restrict__ status, uint8_t* __restrict__ sig_st) {
+// blocks [nq, 2 nq) randomise, 16 sets per block.  The signatures were decoded by k_vs_sig_decode (one
+// thread each: the square root is two Fp exponentiations in a row, nothing for a quad to share); the
+// subgroup check's 63 doublings and r_i sig_i's 31-step ladder run their products four at a time.
+__global__ void GBV_QUAD_ATTR k_vs_sig_pre_quad(uint32_t n, const G2A* __restrict__ Sd, const uint8_t* __restrict__ dec_st, Seed seed,
+                                                  uint32_t nonce, G2J* __restrict__ rS_out, uint8_t* __restrict__ status,
+                                                  uint8_t* __restrict__ sig_st) {
   const uint32_t nq = (n + 15) / 16;
   uint32_t blk = blockIdx.x;
   const bool rand = blk >= nq;
@@ -259,8 +259,9 @@ __global__ void GBV_QUAD_ATTR k_vs_sig_pre_quad(uint32_t n, const uint8_t* __res
   const uint32_t q = threadIdx.x & 3u;
   const uint32_t i = blk * 16 + (threadIdx.x >> 2);
   if (i >= n) return;  // whole quads
-  G2A s;
-  const uint8_t ds = g2_decode(s, sig + (size_t)sig_stride * i, sig_len[i]);
+  const uint8_t ds = dec_st[i];
+  G2A s{fp2_zero(), fp2_zero()};
+  if (ds == PT_OK) s = Sd[i];
   if (!rand) {
     const uint8_t st = (ds != PT_OK || !quad::g2_in_subgroup(s, q)) ? SET_BAD_SIG : SET_OK;
     if (q == 0) {
@@ -453,10 +454,10 @@ void launch_vs_hash_sig(hipStream_t s, uint32_t n, const uint8_t* msgs32, const 
 }
 
 void launch_vs_sig_pre(hipStream_t s, uint32_t n, const uint8_t* sig, uint32_t sig_stride, const uint32_t* sig_len, const Seed& seed,
-                       uint32_t nonce, G2J* rS, uint8_t* status, uint8_t* sig_st) {
+                       uint32_t nonce, G2J* rS, uint8_t* status, uint8_t* sig_st, G2A* Sd, uint8_t* dec_st) {
   if (n <= tuning().vs_sig_quad_max) {
-    hipLaunchKernelGGL(k_vs_sig_pre_quad, dim3(2 * ((n + 15) / 16)), dim3(64), 0, s, n, sig, sig_stride, sig_len, seed, nonce, rS, status,
-                       sig_st);
+    launch_vs_sig_decode(s, n, sig, sig_stride, sig_len, Sd, dec_st);
+    hipLaunchKernelGGL(k_vs_sig_pre_quad, dim3(2 * ((n + 15) / 16)), dim3(64), 0, s, n, Sd, dec_st, seed, nonce, rS, status, sig_st);
     debug_sync(s, "k_vs_sig_pre_quad");
     return;
   }

@@ -16,6 +16,8 @@ void launch_util_g2_out(LaunchCfg c, uint32_t n, const G2A* H, uint8_t* out192);
 
 // Signature.fromBytes decoding of sets [base, base + n): S[i] = the point, status[i] = GBV_PT_* (k_dec.hip)
 void launch_sig_decode(hipStream_t s, uint32_t base, uint32_t n, const uint8_t* sig96, G2A* S, uint8_t* status);
+void launch_vs_sig_decode(hipStream_t s, uint32_t n, const uint8_t* sig, uint32_t sig_stride, const uint32_t* sig_len, G2A* S,
+                          uint8_t* dec_st);
 void launch_sm_prepare(LaunchCfg c, uint32_t base, uint32_t n, const uint32_t* idx, const uint8_t* sig96, const uint32_t* set_grp,
                        const G1A* table, const uint8_t* table_ok, uint32_t table_n, const uint4* comb, const uint8_t* comb_ok,
                        const Seed& seed, uint32_t nonce, G2A* S_out, G2J* Sh, G1J* Ph, uint8_t* status, uint8_t* scratch8 = nullptr);
@@ -105,7 +107,7 @@ void launch_vs_hash_sig(hipStream_t s, uint32_t n, const uint8_t* msgs32, const 
 // the same per-set work in two halves for small passes: signatures (no pubkey needed) beside the
 // aggregation, then the pubkeys (k_vs.hip)
 void launch_vs_sig_pre(hipStream_t s, uint32_t n, const uint8_t* sig, uint32_t sig_stride, const uint32_t* sig_len, const Seed& seed,
-                       uint32_t nonce, G2J* rS, uint8_t* status, uint8_t* sig_st);
+                       uint32_t nonce, G2J* rS, uint8_t* status, uint8_t* sig_st, G2A* Sd, uint8_t* dec_st);
 void launch_vs_pk_rand(hipStream_t s, uint32_t n, const uint32_t* set_off, const uint32_t* arena, const uint8_t* raw_flag,
                        const uint8_t* raw_pk48, const G1A* table, const uint8_t* table_ok, const G1J* pk_agg, const uint8_t* pk_st,
                        const Seed& seed, uint32_t nonce, G1J* rP, uint8_t* status);

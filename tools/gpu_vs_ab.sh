@@ -18,8 +18,7 @@ run_with() {  # run_with V cmd...
     *) LODESTAR_AMD_LIB=lodestar_amd/variants/libgbv_$v.so "$@" ;;
   esac
 }
-for v in "$@"; do
-  [ "$v" = base ] && continue
+for v in base "$@"; do
   run_with "$v" timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
     tests/test_gpu_parity.py tests/test_block_sets.py > "$OUT/test_${v//[:=\/]/_}.log" 2>&1 || { echo "tests failed ($v)"; tail -30 "$OUT/test_${v//[:=\/]/_}.log"; exit 1; }
   echo "$v: $(tail -1 "$OUT/test_${v//[:=\/]/_}.log")"
