@@ -41,6 +41,18 @@ __global__ void GBV_QUAD_ATTR k_hash_msgs_quad(const uint8_t* __restrict__ msgs3
   if (act) quad::store_split<4>((Fp*)&H[i], (const Fp*)&a, q);
 }
 
+// Cofactor clearing of k_hash_msgs_pre's Q0 + Q1 on lane quads (the maps ran on lane pairs, two lanes
+// per message instead of four doing each map twice), then the affine form.
+__global__ void GBV_QUAD_ATTR k_hash_clear_quad(uint32_t n, const G2J* __restrict__ Qpre, G2A* __restrict__ H) {
+  const uint32_t q = threadIdx.x & 3u;
+  const uint32_t i = blockIdx.x * 16 + (threadIdx.x >> 2);
+  const bool act = i < n;
+  const G2J p = quad::g2_clear_cofactor(Qpre[act ? i : 0u], q);  // past n: message 0 again, nothing written
+  G2A a;
+  quad::g2_to_aff(a, p, q);
+  if (act) quad::store_split<4>((Fp*)&H[i], (const Fp*)&a, q);
+}
+
 __global__ void GBV_KERNEL_ATTR k_hash_msgs_pre(const uint8_t* __restrict__ msgs32, uint32_t n, G2J* __restrict__ Qpre) {
   uint32_t i = (blockIdx.x * blockDim.x + threadIdx.x) >> 1;
   bool act = i < n;
@@ -68,7 +80,11 @@ void launch_hash_msgs(LaunchCfg c, const uint8_t* msgs32, uint32_t n, G2A* H, G2
     launch_hash_clear_coop(c.stream, n, Qpre, H);
     return;
   }
-  if (n <= tuning().hash_quad_max)  // latency: lane quads, then lane pairs (grids sized here; c.blocks is for one lane per message)
+  if (Qpre && n <= tuning().hash_quad_max) {  // latency: maps on lane pairs, the cofactor clearing on lane quads
+    hipLaunchKernelGGL(k_hash_msgs_pre, dim3((2 * n + 63) / 64), dim3(64), 0, c.stream, msgs32, n, Qpre);
+    debug_sync(c.stream, "k_hash_msgs_pre");
+    hipLaunchKernelGGL(k_hash_clear_quad, dim3((n + 15) / 16), dim3(64), 0, c.stream, n, Qpre, H);
+  } else if (n <= tuning().hash_quad_max)  // lane quads, then lane pairs (grids sized here; c.blocks is for one lane per message)
     hipLaunchKernelGGL(k_hash_msgs_quad, dim3((n + 15) / 16), dim3(64), 0, c.stream, msgs32, n, H);
   else if (n <= tuning().hash_pair_max)
     hipLaunchKernelGGL(k_hash_msgs_pair, dim3((2 * n + 63) / 64), dim3(64), 0, c.stream, msgs32, n, H);
