@@ -586,7 +586,7 @@ def c4_bench(v, sk_ints, pk_rows, cpu, n_blocks=64, electra=False):
     return out
 
 
-def c5_bench(v, call_off, idx, sigs, msgs, steps=4, depth=2, frac=0.01):
+def c5_bench(v, call_off, idx, sigs, msgs, steps=6, depth=3, frac=0.01):
     """C5 at N = 1: the headline stream with 1 % invalid sets (SURVEY 8(d) recipe: 90 % wrong-message
     signatures, 10 % malformed bytes([10]*96)), every per-set boolean checked against the injection
     map -- the per-set fallback path (jobItem.ts:93-125) under load.  Multi-GPU: --mode replay."""
