@@ -6,6 +6,7 @@
 #include "launch.h"
 #include "kernel_common.h"
 #include "coop.h"
+#include "quad.h"
 
 namespace gbv {
 
@@ -623,6 +624,64 @@ k_vs_chunk_coop(const uint32_t* __restrict__ chunk_be, const uint8_t* __restrict
   uint32_t b = chunk_be[2 * c], e = chunk_be[2 * c + 1];
   int bad = b == e;
   int any = 0;
+  if (FS) {
+    for (uint32_t i = b + lane; i < e; i += 64) bad |= status[i] != SET_OK;
+    if (__any(bad)) {
+      if (lane == 0) chunk_valid[c] = 0;
+      return;
+    }
+    // product of the chunk's Miller values on lane quads (quad::mul12): quad j multiplies values
+    // j, j + 16, ... in a row, then a 4-level tree over the quads (15 product latencies a level
+    // where one lane's fp12_mul costs 54); the quad-0 lanes of each half stage the result
+    quad::Lane L;
+    L.q = lane & 3u;
+    L.h = (L.q & 2u) != 0;
+    L.s = (L.q & 1u) != 0;
+    const uint32_t j = lane >> 2;
+    const uint32_t hf = L.h ? 1u : 0u;
+    Fp6 M = fp6_zero();
+    int has = 0;
+    for (uint32_t i = b + j; i < e; i += 16) {  // quad-uniform trip count
+      const Fp6 G = ((const Fp6*)&f[i])[hf];
+      if (has) {
+        quad::mul12(M, G, L);
+      } else {
+        M = G;
+        has = 1;
+      }
+    }
+    for (unsigned d = 8; d >= 1; d >>= 1) {
+      Fp6 O;
+      Fp* od = (Fp*)&O;
+      const Fp* md = (const Fp*)&M;
+      for (int k = 0; k < 6; ++k) od[k] = shfl_down_fp_c(md[k], 4 * d);
+      const int ho = __shfl_down(has, 4 * d, 64);
+      if (j < d && ho) {  // quad-uniform
+        if (has) {
+          quad::mul12(M, O, L);
+        } else {
+          M = O;
+          has = 1;
+        }
+      }
+    }
+    coop::load_consts();
+    if (lane == 0)
+      for (int k = 0; k < 6; ++k) stage[k] = ((const Fp*)&M)[k];  // lane 0: c0 (Fp 0..5), then lane 2: c1 (Fp 6..11)
+    __syncthreads();
+    if (lane < 6) coop::put(ws + coop::E_F + lane, stage[lane]);
+    __syncthreads();
+    if (lane == 2)
+      for (int k = 0; k < 6; ++k) stage[k] = ((const Fp*)&M)[k];
+    __syncthreads();
+    if (lane < 6) coop::put(ws + coop::E_F + 6 + lane, stage[lane]);
+    if (fs_flag[c] == 1 && lane < 12) coop::put(ws + coop::E_TMP + lane, ((const Fp*)&Fs[c])[lane]);
+    coop::barrier();
+    if (fs_flag[c] == 1) coop::mul12(ws, coop::E_Z, coop::E_F, coop::E_TMP, coop::E_F);
+    bool ok = fs_flag[c] != 0 && coop::final_exp_is_one(ws);
+    if (lane == 0) chunk_valid[c] = ok ? 1 : 0;
+    return;
+  }
   Fp12 acc = fp12_one();
   G2J s = jac_infinity<Fp2>();
   for (uint32_t i = b + lane; i < e; i += 64) {
@@ -631,22 +690,11 @@ k_vs_chunk_coop(const uint32_t* __restrict__ chunk_be, const uint8_t* __restrict
       continue;
     }
     acc = any ? fp12_mul(acc, f[i]) : f[i];
-    if (!FS) s = any ? g2_add(s, rS[i]) : rS[i];
+    s = any ? g2_add(s, rS[i]) : rS[i];
     any = 1;
   }
   if (__any(bad)) {
     if (lane == 0) chunk_valid[c] = 0;
-    return;
-  }
-  if (FS) {
-    wave_reduce_f_coop(acc, any);
-    coop::load_consts();
-    if (lane == 0) coop::store12(ws + coop::E_F, acc);
-    if (fs_flag[c] == 1 && lane < 12) coop::put(ws + coop::E_TMP + lane, ((const Fp*)&Fs[c])[lane]);
-    coop::barrier();
-    if (fs_flag[c] == 1) coop::mul12(ws, coop::E_Z, coop::E_F, coop::E_TMP, coop::E_F);
-    bool ok = fs_flag[c] != 0 && coop::final_exp_is_one(ws);
-    if (lane == 0) chunk_valid[c] = ok ? 1 : 0;
     return;
   }
   wave_reduce_fs_coop(acc, s, any);
