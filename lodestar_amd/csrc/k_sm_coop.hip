@@ -7,10 +7,12 @@
 #include "kernel_common.h"
 #include "coop.h"
 #include "quad.h"
+#include "quad_g2.h"
 
 namespace gbv {
 
 GBV_NI G2J g2_add_j(G2J a, G2J b) { return jac_add(a, b); }
+__device__ __forceinline__ G2J quad_g2_add(const G2J& a, const G2J& b, uint32_t q) { return quad::g2_add(a, b, q); }
 #define g2_add g2_add_j
 
 __device__ inline Fp shfl_down_fp_c(const Fp& a, unsigned d) {
@@ -18,57 +20,6 @@ __device__ inline Fp shfl_down_fp_c(const Fp& a, unsigned d) {
 #pragma unroll
   for (int i = 0; i < 12; ++i) r.v[i] = __shfl_down((unsigned)a.v[i], d, 64);
   return r;
-}
-
-// cross-lane tree: lane 0 ends with the product of the lanes' f and the sum of their s
-__device__ inline void wave_reduce_fs_coop(Fp12& f, G2J& s, int& any) {
-  unsigned lane = threadIdx.x;
-  for (unsigned d = 32; d >= 1; d >>= 1) {
-    Fp12 fo;
-    G2J so;
-    Fp* fd = (Fp*)&fo;
-    const Fp* fsrc = (const Fp*)&f;
-    for (int i = 0; i < 12; ++i) fd[i] = shfl_down_fp_c(fsrc[i], d);
-    Fp* sd = (Fp*)&so;
-    const Fp* ssrc = (const Fp*)&s;
-    for (int i = 0; i < 6; ++i) sd[i] = shfl_down_fp_c(ssrc[i], d);
-    int ao = __shfl_down(any, d, 64);
-    if (lane < d && ao) {
-      f = any ? fp12_mul(f, fo) : fo;
-      s = any ? g2_add(s, so) : so;
-      any = 1;
-    }
-  }
-}
-
-// cross-lane trees over one of the two: lane 0 ends with the product of the f / the sum of the s
-__device__ inline void wave_reduce_f_coop(Fp12& f, int& any) {
-  unsigned lane = threadIdx.x;
-  for (unsigned d = 32; d >= 1; d >>= 1) {
-    Fp12 fo;
-    Fp* fd = (Fp*)&fo;
-    const Fp* fsrc = (const Fp*)&f;
-    for (int i = 0; i < 12; ++i) fd[i] = shfl_down_fp_c(fsrc[i], d);
-    int ao = __shfl_down(any, d, 64);
-    if (lane < d && ao) {
-      f = any ? fp12_mul(f, fo) : fo;
-      any = 1;
-    }
-  }
-}
-__device__ inline void wave_reduce_s_coop(G2J& s, int& any) {
-  unsigned lane = threadIdx.x;
-  for (unsigned d = 32; d >= 1; d >>= 1) {
-    G2J so;
-    Fp* sd = (Fp*)&so;
-    const Fp* ssrc = (const Fp*)&s;
-    for (int i = 0; i < 6; ++i) sd[i] = shfl_down_fp_c(ssrc[i], d);
-    int ao = __shfl_down(any, d, 64);
-    if (lane < d && ao) {
-      s = any ? g2_add(s, so) : so;
-      any = 1;
-    }
-  }
 }
 
 // One wave per segment: the randomised chunk equations of the whole segment are folded into one
@@ -606,11 +557,93 @@ k_fp12_check(uint32_t k, const Fp12* __restrict__ parts, uint8_t* __restrict__ o
   if (lane == 0) out[0] = ok ? 1 : 0;
 }
 
+// Lane-quad reductions over a chunk's sets b .. e - 1 (all with status OK), one wave: quad j takes
+// sets b + j, b + j + 16, ... in a row, then a 4-level tree over the 16 quads.
+//   quad_chunk_f12: the product of the sets' Miller values (quad::mul12: 15 product latencies a
+//     level where one lane's fp12_mul costs 54), staged into the workspace slot ws + slot;
+//   quad_chunk_g2sum: the sum of their r_i sig_i (quad::g2_add, 11 product rounds where one lane's
+//     addition has 43 products), returned on every lane of quad 0.
+__device__ inline void quad_chunk_f12(const Fp12* __restrict__ f, uint32_t b, uint32_t e, coop::Slot* ws, int slot, Fp* stage) {
+  const unsigned lane = threadIdx.x;
+  quad::Lane L;
+  L.q = lane & 3u;
+  L.h = (L.q & 2u) != 0;
+  L.s = (L.q & 1u) != 0;
+  const uint32_t j = lane >> 2, hf = L.h ? 1u : 0u;
+  Fp6 M = fp6_zero();
+  int has = 0;
+  for (uint32_t i = b + j; i < e; i += 16) {  // quad-uniform trip count
+    const Fp6 G = ((const Fp6*)&f[i])[hf];
+    if (has) {
+      quad::mul12(M, G, L);
+    } else {
+      M = G;
+      has = 1;
+    }
+  }
+  for (unsigned d = 8; d >= 1; d >>= 1) {
+    Fp6 O;
+    Fp* od = (Fp*)&O;
+    const Fp* md = (const Fp*)&M;
+    for (int k = 0; k < 6; ++k) od[k] = shfl_down_fp_c(md[k], 4 * d);
+    const int ho = __shfl_down(has, 4 * d, 64);
+    if (j < d && ho) {  // quad-uniform
+      if (has) {
+        quad::mul12(M, O, L);
+      } else {
+        M = O;
+        has = 1;
+      }
+    }
+  }
+  for (int half = 0; half < 2; ++half) {  // lane 0 holds c0 (Fp 0..5), lane 2 c1 (Fp 6..11)
+    if (lane == 2u * half)
+      for (int k = 0; k < 6; ++k) stage[k] = ((const Fp*)&M)[k];
+    __syncthreads();
+    if (lane < 6) coop::put(ws + slot + 6 * half + lane, stage[lane]);
+    __syncthreads();
+  }
+}
+
+__device__ inline G2J quad_chunk_g2sum(const G2J* __restrict__ rS, uint32_t b, uint32_t e) {
+  const unsigned lane = threadIdx.x;
+  const uint32_t q = lane & 3u, j = lane >> 2;
+  G2J S = jac_infinity<Fp2>();
+  int has = 0;
+  for (uint32_t i = b + j; i < e; i += 16) {
+    const G2J P = rS[i];
+    if (has) {
+      S = quad_g2_add(S, P, q);
+    } else {
+      S = P;
+      has = 1;
+    }
+  }
+  for (unsigned d = 8; d >= 1; d >>= 1) {
+    G2J O;
+    Fp* od = (Fp*)&O;
+    const Fp* sd = (const Fp*)&S;
+    for (int k = 0; k < 6; ++k) od[k] = shfl_down_fp_c(sd[k], 4 * d);
+    const int ho = __shfl_down(has, 4 * d, 64);
+    if (j < d && ho) {
+      if (has) {
+        S = quad_g2_add(S, O, q);
+      } else {
+        S = O;
+        has = 1;
+      }
+    }
+  }
+  return S;
+}
+
 // verifySignatureSets chunks (<= 255 sets each, chunkifyMaximizeChunkSize; (begin, end) pairs): one wave per chunk
-// multiplies its sets' Miller values and sums r_i sig_i (cross-lane tree), then runs the
+// multiplies its sets' Miller values and sums r_i sig_i (lane-quad trees), then runs the
 // (-g1, sum) pair and the final exponentiation cooperatively (maybeBatch.ts:17-26).
 // With Fs (small passes): the (-g1, sum) Miller value was formed beside the per-set ones by
-// k_vs_miller_coop (fs_flag 1; 2: the sum is infinity, no pair), so this kernel only multiplies.
+// k_vs_chunk_s_miller (fs_flag 1; 2: the sum is infinity, no pair), so this kernel only multiplies.
+constexpr int CHUNK_PROD_SLOT = coop::MILLER_WS;  // 12 slots the Miller loop does not touch
+static_assert(CHUNK_PROD_SLOT + 12 <= SEG_WS, "chunk product slot inside the workspace");
 template <bool FS>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
 k_vs_chunk_coop(const uint32_t* __restrict__ chunk_be, const uint8_t* __restrict__ status, const Fp12* __restrict__ f,
@@ -623,58 +656,14 @@ k_vs_chunk_coop(const uint32_t* __restrict__ chunk_be, const uint8_t* __restrict
   uint32_t c = blockIdx.x;
   uint32_t b = chunk_be[2 * c], e = chunk_be[2 * c + 1];
   int bad = b == e;
-  int any = 0;
+  for (uint32_t i = b + lane; i < e; i += 64) bad |= status[i] != SET_OK;
+  if (__any(bad)) {
+    if (lane == 0) chunk_valid[c] = 0;
+    return;
+  }
+  coop::load_consts();
   if (FS) {
-    for (uint32_t i = b + lane; i < e; i += 64) bad |= status[i] != SET_OK;
-    if (__any(bad)) {
-      if (lane == 0) chunk_valid[c] = 0;
-      return;
-    }
-    // product of the chunk's Miller values on lane quads (quad::mul12): quad j multiplies values
-    // j, j + 16, ... in a row, then a 4-level tree over the quads (15 product latencies a level
-    // where one lane's fp12_mul costs 54); the quad-0 lanes of each half stage the result
-    quad::Lane L;
-    L.q = lane & 3u;
-    L.h = (L.q & 2u) != 0;
-    L.s = (L.q & 1u) != 0;
-    const uint32_t j = lane >> 2;
-    const uint32_t hf = L.h ? 1u : 0u;
-    Fp6 M = fp6_zero();
-    int has = 0;
-    for (uint32_t i = b + j; i < e; i += 16) {  // quad-uniform trip count
-      const Fp6 G = ((const Fp6*)&f[i])[hf];
-      if (has) {
-        quad::mul12(M, G, L);
-      } else {
-        M = G;
-        has = 1;
-      }
-    }
-    for (unsigned d = 8; d >= 1; d >>= 1) {
-      Fp6 O;
-      Fp* od = (Fp*)&O;
-      const Fp* md = (const Fp*)&M;
-      for (int k = 0; k < 6; ++k) od[k] = shfl_down_fp_c(md[k], 4 * d);
-      const int ho = __shfl_down(has, 4 * d, 64);
-      if (j < d && ho) {  // quad-uniform
-        if (has) {
-          quad::mul12(M, O, L);
-        } else {
-          M = O;
-          has = 1;
-        }
-      }
-    }
-    coop::load_consts();
-    if (lane == 0)
-      for (int k = 0; k < 6; ++k) stage[k] = ((const Fp*)&M)[k];  // lane 0: c0 (Fp 0..5), then lane 2: c1 (Fp 6..11)
-    __syncthreads();
-    if (lane < 6) coop::put(ws + coop::E_F + lane, stage[lane]);
-    __syncthreads();
-    if (lane == 2)
-      for (int k = 0; k < 6; ++k) stage[k] = ((const Fp*)&M)[k];
-    __syncthreads();
-    if (lane < 6) coop::put(ws + coop::E_F + 6 + lane, stage[lane]);
+    quad_chunk_f12(f, b, e, ws, coop::E_F, stage);
     if (fs_flag[c] == 1 && lane < 12) coop::put(ws + coop::E_TMP + lane, ((const Fp*)&Fs[c])[lane]);
     coop::barrier();
     if (fs_flag[c] == 1) coop::mul12(ws, coop::E_Z, coop::E_F, coop::E_TMP, coop::E_F);
@@ -682,23 +671,7 @@ k_vs_chunk_coop(const uint32_t* __restrict__ chunk_be, const uint8_t* __restrict
     if (lane == 0) chunk_valid[c] = ok ? 1 : 0;
     return;
   }
-  Fp12 acc = fp12_one();
-  G2J s = jac_infinity<Fp2>();
-  for (uint32_t i = b + lane; i < e; i += 64) {
-    if (status[i] != SET_OK) {
-      bad = 1;
-      continue;
-    }
-    acc = any ? fp12_mul(acc, f[i]) : f[i];
-    s = any ? g2_add(s, rS[i]) : rS[i];
-    any = 1;
-  }
-  if (__any(bad)) {
-    if (lane == 0) chunk_valid[c] = 0;
-    return;
-  }
-  wave_reduce_fs_coop(acc, s, any);
-  coop::load_consts();
+  const G2J s = quad_chunk_g2sum(rS, b, e);
   if (lane == 0) {
     G2A sa;
     flags[0] = jac_to_aff(sa, s) ? 1 : 0;
@@ -711,17 +684,26 @@ k_vs_chunk_coop(const uint32_t* __restrict__ chunk_be, const uint8_t* __restrict
     stage[5] = sa.y.c1;
   }
   coop::barrier();
-  if (flags[0]) {  // F = f_(-g1, sum r_i sig_i) * prod f_i (shared Miller / final-exp workspace)
-    const Fp* st = stage;
-    coop::miller_load_pair(ws, 0, G1A{st[0], st[1]}, G2A{Fp2{st[2], st[3]}, Fp2{st[4], st[5]}});
+  const bool pair = flags[0] != 0;
+  G1A ng;
+  G2A sa;
+  if (pair) {
+    ng = G1A{stage[0], stage[1]};
+    sa = G2A{Fp2{stage[2], stage[3]}, Fp2{stage[4], stage[5]}};
+  }
+  __syncthreads();
+  // the product first, parked above the Miller workspace (stage is reused), then the (-g1, S) Miller
+  // value into E_F (shared Miller / final-exp workspace) and F = f_(-g1, S) * prod f_i
+  quad_chunk_f12(f, b, e, ws, pair ? CHUNK_PROD_SLOT : coop::E_F, stage);
+  if (pair) {
+    coop::miller_load_pair(ws, 0, ng, sa);
     coop::miller_loop(ws, 1);
-    if (lane == 0) coop::store12(ws + coop::E_TMP, acc);
+    coop::barrier();
+    if (lane < 12) coop::put(ws + coop::E_TMP + lane, coop::get(ws + CHUNK_PROD_SLOT + lane));
     coop::barrier();
     coop::mul12(ws, coop::E_Z, coop::E_F, coop::E_TMP, coop::E_F);
-  } else {
-    if (lane == 0) coop::store12(ws + coop::E_F, acc);
-    coop::barrier();
   }
+  coop::barrier();
   bool ok = coop::final_exp_is_one(ws);
   if (lane == 0) chunk_valid[c] = ok ? 1 : 0;
 }
@@ -739,21 +721,13 @@ k_vs_chunk_s_miller(const uint8_t* __restrict__ status, const uint32_t* __restri
   const unsigned lane = threadIdx.x;
   const uint32_t c = blockIdx.x;
   const uint32_t b = chunk_be[2 * c], e = chunk_be[2 * c + 1];
-  int bad = b == e, any = 0;
-  G2J s = jac_infinity<Fp2>();
-  for (uint32_t i = b + lane; i < e; i += 64) {
-    if (status[i] != SET_OK) {
-      bad = 1;
-      continue;
-    }
-    s = any ? g2_add(s, rS[i]) : rS[i];
-    any = 1;
-  }
+  int bad = b == e;
+  for (uint32_t i = b + lane; i < e; i += 64) bad |= status[i] != SET_OK;
   if (__any(bad)) {
     if (lane == 0) fs_flag[c] = 0;
     return;
   }
-  wave_reduce_s_coop(s, any);
+  const G2J s = quad_chunk_g2sum(rS, b, e);
   coop::load_consts();
   if (lane == 0) {
     G2A sa;
