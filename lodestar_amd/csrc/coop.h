@@ -296,7 +296,7 @@ __device__ inline unsigned lane_id() { return threadIdx.x & 63u; }  // a job is 
 // A coop job is ONE wave: its phases synchronise at wavefront scope -- the workgroup-scope fences
 // of __syncthreads (prior LDS writes complete and visible, later reads not hoisted) around a wave
 // barrier instead of s_barrier.  For the one-wave workgroups this is what __syncthreads compiles to
-// anyway; it also lets a workgroup hold a second wave doing other work (k_hash_clear_coop), which
+// anyway; it also lets a workgroup hold a second wave doing other work, which
 // meets the coop wave only at explicit __syncthreads.
 __device__ inline void barrier() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");

@@ -1162,11 +1162,9 @@ void tuning_load() {
       if (const char* e = getenv(name)) v = (uint32_t)strtoul(e, nullptr, 10);
     };
     rd("GBV_HASH_PAIR_MAX", g_tuning.hash_pair_max);
-    rd("GBV_HASH_COOP_MAX", g_tuning.hash_coop_max);
     rd("GBV_HASH_QUAD_MAX", g_tuning.hash_quad_max);
     rd("GBV_VS_SIG_QUAD_MAX", g_tuning.vs_sig_quad_max);
     rd("GBV_PREPARE_SPLIT_MAX", g_tuning.prepare_split_max);
-    rd("GBV_PREP_COOP_RAND", g_tuning.prep_coop_rand_max);
     rd("GBV_CHUNK_FINISH_WAVE_MAX", g_tuning.chunk_finish_wave_max);
     rd("GBV_VS_PRE_MAX", g_tuning.vs_pre_max);
     rd("GBV_VS_FS_MAXC", g_tuning.vs_fs_maxc);

@@ -169,7 +169,7 @@ k_sm_prepare_split(uint32_t base, uint32_t n, const uint32_t* __restrict__ idx, 
   }
 }
 
-// After k_sm_prep_roles (k_sm_coop.hip): per set the verdict -- pubkey slot, decode code, the
+// After k_sm_prep_roles_quad (k_vs.hip): per set the verdict -- pubkey slot, decode code, the
 // cooperative subgroup check (sub_ok) -- merged as k_sm_prepare merges it (a bad signature outranks a
 // bad key), the set's r pk / r sig (Ph / Sh at its own index) kept only when it is valid, then the
 // 8-set segmented scan with the sums written at the run heads (in place: every lane reads its own
@@ -547,7 +547,7 @@ void launch_sm_prepare(LaunchCfg c, uint32_t base, uint32_t n, const uint32_t* i
     // latency, few sets: decode, then the subgroup checks one wave per set beside the randomisation,
     // then the verdicts and the scan
     launch_sig_decode(c.stream, base, n, sig96, S_out, status);
-    launch_sm_prep_roles(c.stream, base, n, idx, table, table_ok, table_n, comb, comb_ok, seed, nonce, S_out, status, scratch8, Sh, Ph);
+    launch_sm_prep_roles_quad(c.stream, base, n, idx, table, table_ok, table_n, comb, comb_ok, seed, nonce, S_out, status, scratch8, Sh, Ph);
     hipLaunchKernelGGL(k_sm_prep_scan, grid, dim3(64), 0, c.stream, base, n, idx, set_grp, table_ok, table_n, scratch8, status, Sh, Ph);
     debug_sync(c.stream, "k_sm_prep_scan");
   } else if (Sh && n <= tuning().prepare_split_max) {  // latency: two waves per 64 sets

@@ -199,169 +199,7 @@ k_sm_group_fe(uint32_t g0, const uint8_t* __restrict__ seg_ok, const Fp12* __res
   }
 }
 
-// hash_to_G2's cofactor clearing for few messages (latency: a lone gossip call hashes one message),
-// TWO waves per message.  clear_cofactor_g2 (RFC 9380 G.3):
-//   h(P) = [x]([x]P + psi(P)) + psi^2(2P) - psi(P) - [x]P - P.
-// Wave 0 runs the two [|x|] scalar multiplications by the Miller loop's cooperative point steps
-// (coop::mul_xabs_point: each doubling two rounds of independent products instead of 16 dependent
-// ones) and, on its lane 0, the affine conversions they need; wave 1's lane 0 meanwhile forms the
-// rest -- psi(P) and u = psi^2(2P) - psi(P) - P during the first multiplication, u - [x]P during the
-// second -- so only two point additions and three inversions stay on the chain.  The coop wave
-// synchronises its phases at wavefront scope (coop::barrier) and meets wave 1 at the three
-// __syncthreads below, which every thread of the block reaches.  Qpre = Q0 + Q1 (k_hash_msgs_pre).
-// A base at infinity (never, for a hash) takes the thread-serial clear_cofactor_g2.
-__device__ inline G2A g2_aff_out(const G2J& q) {
-  G2A out;
-  jac_to_aff(out, q);
-  return out;
-}
-__global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2)))
-k_hash_clear_coop(const G2J* __restrict__ Qpre, G2A* __restrict__ H) {
-  __shared__ coop::Slot ws[coop::MILLER_WS];
-  __shared__ Fp st[4];
-  __shared__ G2J sh_psi, sh_t1, sh_u;
-  __shared__ int ok_p, ok_t2;
-  const uint32_t m = blockIdx.x;
-  const unsigned lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-  const G2J p = Qpre[m];
-  if (wv == 0) {
-    coop::load_consts();
-    if (lane == 0) {
-      G2A a;
-      ok_p = jac_to_aff(a, p) ? 1 : 0;
-      st[0] = a.x.c0;
-      st[1] = a.x.c1;
-      st[2] = a.y.c0;
-      st[3] = a.y.c1;
-      if (!ok_p) H[m] = g2_aff_out(clear_cofactor_g2(p));
-    }
-    coop::barrier();
-    if (ok_p) coop::mul_xabs_point(ws, G2A{Fp2{st[0], st[1]}, Fp2{st[2], st[3]}});
-  } else if (lane == 0) {
-    const G2J psi = g2_psi_jac(p);
-    sh_psi = psi;
-    sh_u = g2_add(g2_add(g2_psi_jac(g2_psi_jac(jac_dbl(p))), jac_neg(psi)), jac_neg(p));
-  }
-  __syncthreads();  // S1: [|x|] P in ws, psi(P) and u in LDS
-  if (wv == 0 && lane == 0 && ok_p) sh_t1 = jac_neg(coop::point_jac(ws));  // [x] P
-  __syncthreads();  // S2: t1 in LDS (wave 0 may now reuse ws)
-  if (wv == 0) {
-    if (lane == 0 && ok_p) {
-      G2A a;
-      ok_t2 = jac_to_aff(a, g2_add(sh_t1, sh_psi)) ? 1 : 0;  // t2 = [x] P + psi(P)
-      st[0] = a.x.c0;
-      st[1] = a.x.c1;
-      st[2] = a.y.c0;
-      st[3] = a.y.c1;
-    }
-    coop::barrier();
-    if (ok_p && ok_t2) coop::mul_xabs_point(ws, G2A{Fp2{st[0], st[1]}, Fp2{st[2], st[3]}});
-  } else if (lane == 0 && ok_p) {
-    sh_u = g2_add(sh_u, jac_neg(sh_t1));  // u - [x] P
-  }
-  __syncthreads();  // S3: [|x|] t2 in ws, u - [x] P in LDS
-  if (wv == 0 && lane == 0 && ok_p) {
-    // t2 at infinity: [x] t2 is infinity too
-    H[m] = g2_aff_out(ok_t2 ? g2_add(jac_neg(coop::point_jac(ws)), sh_u) : sh_u);
-  }
-}
-void launch_hash_clear_coop(hipStream_t s, uint32_t n, const G2J* Qpre, G2A* H) {
-  hipLaunchKernelGGL(k_hash_clear_coop, dim3(n), dim3(128), 0, s, Qpre, H);
-  debug_sync(s, "k_hash_clear_coop");
-}
 
-// Latency form of the same-message prepare stage for few sets, after k_sig_decode (S, status = the
-// decode code): two block roles in one launch.  Blocks [0, n): ONE WAVE PER SET runs the G2
-// subgroup check psi(Q) == [x] Q on the cooperative point doublings (coop::mul_xabs_point, ~0.7 ms
-// against ~1.6 ms of dependent products on one lane) and writes the verdict to sub_ok.  Blocks
-// [n, n + ceil(n / 64)): one lane per set forms r pk and r sig (as k_sm_prepare_split's wave 1) into
-// Ph / Sh at the set's own index.  k_sm_prep_scan then merges the verdicts and runs the chunk scan.
-// The cooperative doublings are exact for points of the order-r subgroup; for a point with a
-// small-order component they either stay exact (and the psi test rejects it) or degenerate to
-// Z = 0, which the comparison also rejects -- a rejected point is the right answer either way.
-// With coop_rand (n <= GBV_PREP_COOP_RAND, default 512 sets), blocks [n, 2n) form r sig the same
-// way (coop::mul_2d_point, one wave per set: ~1.5 ms against ~2.6 ms for the lane's ladder, which
-// was this launch's longest role) and the lanes of the last role form r pk alone (comb or 2-D
-// ladder: the same scalar a - b x^2).
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
-k_sm_prep_roles(uint32_t base, uint32_t n, const uint32_t* __restrict__ idx, const G1A* __restrict__ table,
-                const uint8_t* __restrict__ table_ok, uint32_t table_n, const uint4* __restrict__ comb, const uint8_t* __restrict__ comb_ok,
-                Seed seed, uint32_t nonce, const G2A* __restrict__ S, const uint8_t* __restrict__ status, uint8_t* __restrict__ sub_ok,
-                G2J* __restrict__ Sh, G1J* __restrict__ Ph, int coop_rand) {
-  __shared__ coop::Slot ws[coop::MILLER_WS];
-  const unsigned lane = threadIdx.x;
-  const uint32_t nr = coop_rand ? n : 0u;
-  if (blockIdx.x >= n && blockIdx.x < n + nr) {  // r sig, one wave per set
-    const uint32_t i = base + blockIdx.x - n, k = idx[i];
-    if (!(status[i] == PT_OK && k < table_n && table_ok[k])) {  // uniform per block
-      if (lane == 0) Sh[i] = jac_infinity<Fp2>();
-      return;
-    }
-    const G2A q = S[i];
-    const uint64_t r = prf_scalar(seed, i, nonce);
-    coop::load_consts();
-    coop::mul_2d_point(ws, q, g2_neg_psi2(q), (uint32_t)r, (uint32_t)(r >> 32));
-    if (lane == 0) Sh[i] = coop::point_jac(ws);
-    return;
-  }
-  if (blockIdx.x < n) {
-    const uint32_t i = base + blockIdx.x;
-    if (status[i] != PT_OK) {  // uniform per block
-      if (lane == 0) sub_ok[i] = 0;
-      return;
-    }
-    const G2A q = S[i];
-    coop::load_consts();
-    coop::mul_xabs_point(ws, q);  // [|x|] q at M_PAIR
-    if (lane == 0) sub_ok[i] = jac_eq_aff(jac_neg(coop::point_jac(ws)), g2_psi(q)) ? 1 : 0;
-    return;
-  }
-  const uint32_t t = (blockIdx.x - n - nr) * 64 + lane;
-  if (t >= n) return;
-  const uint32_t i = base + t, k = idx[i];
-  G2J rs = jac_infinity<Fp2>();
-  G1J rp = jac_infinity<Fp>();
-  if (coop_rand) {
-    if (status[i] == PT_OK && k < table_n && table_ok[k]) {
-      const uint64_t r = prf_scalar(seed, i, nonce);
-      // a table key is in the subgroup, so the 2-D ladder cannot fail for it
-      if (comb && comb_ok[k])
-        rp = comb_mul(comb + (size_t)k * (COMB_ENTRIES * COMB_U4), (uint32_t)r, (uint32_t)(r >> 32));
-      else if (!randomize_g1(table[k], r, &rp))
-        rp = jac_infinity<Fp>();
-    }
-    Ph[i] = rp;
-    return;
-  }
-  if (status[i] == PT_OK && k < table_n && table_ok[k]) {  // (discarded by k_sm_prep_scan when the subgroup check fails)
-    const G2A s = S[i];
-    const uint64_t r = prf_scalar(seed, i, nonce);
-    if (comb && comb_ok[k]) {
-      rp = comb_mul(comb + (size_t)k * (COMB_ENTRIES * COMB_U4), (uint32_t)r, (uint32_t)(r >> 32));
-      if (!randomize_g2(s, r, &rs)) {
-        rs = g2_mul_u64(s, r);
-        rp = g1_mul_u64(table[k], r);
-      }
-    } else {
-      const G1A pk = table[k];
-      if (!randomize_pair(pk, s, r, &rp, &rs)) {
-        rs = g2_mul_u64(s, r);
-        rp = g1_mul_u64(pk, r);
-      }
-    }
-  }
-  Sh[i] = rs;
-  Ph[i] = rp;
-}
-void launch_sm_prep_roles(hipStream_t s, uint32_t base, uint32_t n, const uint32_t* idx, const G1A* table, const uint8_t* table_ok,
-                          uint32_t table_n, const uint4* comb, const uint8_t* comb_ok, const Seed& seed, uint32_t nonce, const G2A* S,
-                          const uint8_t* status, uint8_t* sub_ok, G2J* Sh, G1J* Ph) {
-  // a wave per set costs ~25x the CU time of a lane per set: worth it while the waves fit the chip at once
-  const int coop_rand = n <= tuning().prep_coop_rand_max;
-  hipLaunchKernelGGL(k_sm_prep_roles, dim3(n + (coop_rand ? n : 0) + (n + 63) / 64), dim3(64), 0, s, base, n, idx, table, table_ok, table_n,
-                     comb, comb_ok, seed, nonce, S, status, sub_ok, Sh, Ph, coop_rand);
-  debug_sync(s, "k_sm_prep_roles");
-}
 
 // e(P, Q) * e(-g1, S) == 1 by one wave (S = infinity drops the second pair).  Arguments must be
 // wave-uniform (the callers stage them in LDS).

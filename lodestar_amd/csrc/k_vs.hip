@@ -277,6 +277,60 @@ __global__ void GBV_QUAD_ATTR k_vs_sig_pre_quad(uint32_t n, const G2A* __restric
   quad::store_split<6>((Fp*)&rS_out[i], (const Fp*)&rs, q);
 }
 
+// Same-message latency prepare (segments <= prepare_split_max sets, after k_sig_decode) on lane quads:
+// blocks [0, nq) run the G2 subgroup checks (sub_ok[i]), blocks [nq, 2 nq) the randomisation
+// (Sh[i] = r_i sig_i by quad_g2.h's ladder, Ph[i] = r_i pk_i from the comb table or the G1 ladder),
+// one quad per set and role, 16 sets per block: the point chains four lanes wide (round 3 ran them on
+// the cooperative interpreter, one wave per set: prepare 2.8-3.0 -> 2.35 ms).  k_sm_prep_scan merges the
+// verdicts.
+__global__ void GBV_QUAD_ATTR k_sm_prep_roles_quad(uint32_t base, uint32_t n, const uint32_t* __restrict__ idx, const G1A* __restrict__ table,
+                                                   const uint8_t* __restrict__ table_ok, uint32_t table_n, const uint4* __restrict__ comb,
+                                                   const uint8_t* __restrict__ comb_ok, Seed seed, uint32_t nonce, const G2A* __restrict__ S,
+                                                   const uint8_t* __restrict__ status, uint8_t* __restrict__ sub_ok, G2J* __restrict__ Sh,
+                                                   G1J* __restrict__ Ph) {
+  const uint32_t nq = (n + 15) / 16;
+  uint32_t blk = blockIdx.x;
+  const bool rand = blk >= nq;
+  if (rand) blk -= nq;
+  const uint32_t q = threadIdx.x & 3u;
+  const uint32_t t = blk * 16 + (threadIdx.x >> 2);
+  if (t >= n) return;  // whole quads
+  const uint32_t i = base + t;
+  if (!rand) {
+    const bool ok = status[i] == PT_OK && quad::g2_in_subgroup(S[i], q);
+    if (q == 0) sub_ok[i] = ok ? 1 : 0;
+    return;
+  }
+  const uint32_t k = idx[i];
+  if (!(status[i] == PT_OK && k < table_n && table_ok[k])) {  // discarded by k_sm_prep_scan
+    if (q == 0) {
+      Sh[i] = jac_infinity<Fp2>();
+      Ph[i] = jac_infinity<Fp>();
+    }
+    return;
+  }
+  const uint64_t r = prf_scalar(seed, i, nonce);
+  G2J rs;
+  if (!quad::g2_randomize(S[i], r, &rs, q)) rs = g2_mul_u64(S[i], r);  // unreachable for subgroup points (the check role decides)
+  quad::store_split<6>((Fp*)&Sh[i], (const Fp*)&rs, q);
+  if (q == 0) {
+    G1J rp;
+    if (comb && comb_ok[k])
+      rp = comb_mul(comb + (size_t)k * (COMB_ENTRIES * COMB_U4), (uint32_t)r, (uint32_t)(r >> 32));
+    else if (!randomize_g1(table[k], r, &rp))  // a table key is in the subgroup: the 2-D ladder cannot fail
+      rp = jac_infinity<Fp>();
+    Ph[i] = rp;
+  }
+}
+
+void launch_sm_prep_roles_quad(hipStream_t s, uint32_t base, uint32_t n, const uint32_t* idx, const G1A* table, const uint8_t* table_ok,
+                               uint32_t table_n, const uint4* comb, const uint8_t* comb_ok, const Seed& seed, uint32_t nonce, const G2A* S,
+                               const uint8_t* status, uint8_t* sub_ok, G2J* Sh, G1J* Ph) {
+  hipLaunchKernelGGL(k_sm_prep_roles_quad, dim3(2 * ((n + 15) / 16)), dim3(64), 0, s, base, n, idx, table, table_ok, table_n, comb, comb_ok, seed,
+                     nonce, S, status, sub_ok, Sh, Ph);
+  debug_sync(s, "k_sm_prep_roles_quad");
+}
+
 // The pubkey half (stream A, after the aggregation and k_vs_sig_pre): a rejected signature's verdict
 // stands (it wins over a bad pubkey, as in k_vs_hash_sig); otherwise the pubkey's verdict is merged
 // and r_i pk_i formed.  Raw pubkeys (PublicKey.fromBytes(pk, true)) are decoded and group-checked here.

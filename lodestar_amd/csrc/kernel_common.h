@@ -70,10 +70,7 @@ constexpr uint32_t HASH_PAIR_MAX = 4096;
 struct Tuning {
   uint32_t hash_pair_max = HASH_PAIR_MAX;  // GBV_HASH_PAIR_MAX: hash on lane pairs up to this many messages
   uint32_t hash_quad_max = 16384;          // GBV_HASH_QUAD_MAX: hash on lane quads up to this many messages
-  uint32_t hash_coop_max = 0;              // GBV_HASH_COOP_MAX: cooperative cofactor clearing up to this many (0: the
-                                           // lane-quad hash is shorter for every count: lone call 7.05 -> 6.65 ms)
   uint32_t prepare_split_max = 2048;       // GBV_PREPARE_SPLIT_MAX: same-message latency prepare up to this many sets
-  uint32_t prep_coop_rand_max = 512;       // GBV_PREP_COOP_RAND: r sig one wave per set up to this many sets
   uint32_t chunk_finish_wave_max = 32;     // GBV_CHUNK_FINISH_WAVE_MAX: chunk sums one wave per chunk up to this many
   uint32_t vs_pre_max = 16384;             // GBV_VS_PRE_MAX: verifySignatureSets signature half beside the aggregation
   uint32_t vs_fs_maxc = 256;               // GBV_VS_FS_MAXC: per-chunk (-g1, sum) Miller value beside the per-set ones
@@ -129,7 +126,7 @@ __device__ inline bool hash_to_g2_lane_pair(const uint32_t w[8], bool active, G2
 }
 
 // The same lane pairs, stopping before the cofactor clearing: Q0 + Q1 (Jacobian) on the even lane
-// (k_hash_clear_coop then clears the cofactor with one wave per message).
+// (k_hash_clear_quad then clears the cofactor on a lane quad per message).
 __device__ inline bool hash_to_g2_lane_pair_pre(const uint32_t w[8], bool active, G2J* out) {
   const int lane = (int)threadIdx.x, half = lane & 1;
   G2J q = jac_infinity<Fp2>();

@@ -9,9 +9,8 @@ namespace gbv {
 struct Seed;
 struct LaunchCfg { unsigned blocks; unsigned threads; hipStream_t stream; };
 
-// Qpre (optional, n entries): scratch of the latency form for few messages (k_hash_clear_coop)
+// Qpre (optional, n entries): Q0 + Q1 of the lane-pair maps ahead of the lane-quad cofactor clearing (k_hash_clear_quad)
 void launch_hash_msgs(LaunchCfg c, const uint8_t* msgs32, uint32_t n, G2A* H, G2J* Qpre = nullptr);
-void launch_hash_clear_coop(hipStream_t s, uint32_t n, const G2J* Qpre, G2A* H);
 void launch_util_g2_out(LaunchCfg c, uint32_t n, const G2A* H, uint8_t* out192);
 
 // Signature.fromBytes decoding of sets [base, base + n): S[i] = the point, status[i] = GBV_PT_* (k_dec.hip)
@@ -23,9 +22,9 @@ void launch_sm_prepare(LaunchCfg c, uint32_t base, uint32_t n, const uint32_t* i
                        const Seed& seed, uint32_t nonce, G2A* S_out, G2J* Sh, G1J* Ph, uint8_t* status, uint8_t* scratch8 = nullptr);
 // few sets (k_sm_coop.hip): cooperative subgroup checks (one wave per set, verdict in sub_ok) beside
 // the per-set randomisation (r sig / r pk into Sh / Ph at the set's index), after k_sig_decode
-void launch_sm_prep_roles(hipStream_t s, uint32_t base, uint32_t n, const uint32_t* idx, const G1A* table, const uint8_t* table_ok,
-                          uint32_t table_n, const uint4* comb, const uint8_t* comb_ok, const Seed& seed, uint32_t nonce, const G2A* S,
-                          const uint8_t* status, uint8_t* sub_ok, G2J* Sh, G1J* Ph);
+void launch_sm_prep_roles_quad(hipStream_t s, uint32_t base, uint32_t n, const uint32_t* idx, const G1A* table, const uint8_t* table_ok,
+                               uint32_t table_n, const uint4* comb, const uint8_t* comb_ok, const Seed& seed, uint32_t nonce, const G2A* S,
+                               const uint8_t* status, uint8_t* sub_ok, G2J* Sh, G1J* Ph);
 void launch_sm_chunk_finish(LaunchCfg c, uint32_t g0, uint32_t G, uint32_t s0, const uint32_t* grp_off, const uint8_t* status, const G2J* Sh,
                             const G1J* Ph, G1J* PgJ, G2J* SgJ, uint8_t* grp_state, uint32_t* n_fallback);
 void launch_sm_miller(LaunchCfg c, uint32_t g0, uint32_t G, const uint32_t* grp_msg, const uint8_t* grp_state, const G1J* PgJ, const G2A* H,

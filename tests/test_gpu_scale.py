@@ -197,10 +197,10 @@ def test_same_message_one_percent_invalid(world, mode):
 
 @pytest.mark.parametrize("n_sets", [300, 700])
 def test_same_message_small_pass_roles(world, n_sets):
-    """One small pass (one segment) through the latency prepare (k_sm_prep_roles): r sig on the
-    cooperative ladder (<= 512 sets) or on the lanes (700) -- or per segment by the MSM while an
-    earlier test's failure keeps its cooldown on.  All-valid must pass the segment check outright
-    (the G1 and G2 scalars agree), and injected invalid sets come back exactly."""
+    """One small pass (one segment) through the latency prepare (k_sm_prep_roles_quad: subgroup
+    checks and r sig / r pk on lane quads) -- or per segment by the MSM while an earlier test's
+    failure keeps its cooldown on.  All-valid must pass the segment check outright (the G1 and G2
+    scalars agree), and injected invalid sets come back exactly."""
     v, sks, _ = world
     off, idx, grp, sigs, msgs = _workload(v, sks, n_sets, 15 + n_sets)
     assert all(_run_staged(v, off, idx, sigs, msgs))

@@ -10,7 +10,7 @@ run_with() {
   local v=$1; shift
   case "$v" in
     base) "$@" ;;
-    E:*) env "${v#E:}" "$@" ;;
+    E:*) env $(echo "${v#E:}" | tr , " ") "$@" ;;
     *) LODESTAR_AMD_LIB=lodestar_amd/variants/libgbv_$v.so "$@" ;;
   esac
 }
