@@ -39,7 +39,7 @@ inline std::vector<uint32_t> chunk_offsets(uint32_t len, uint32_t min_per_chunk)
 
 inline unsigned blocks_for(size_t n, int tpb = TPB) { return (unsigned)((n + tpb - 1) / tpb); }
 
-// Entries written by launch_sm_seg_reduce / k_sm_part_reduce for n items: every level of 64-way
+// Entries written by launch_seg_reduce_quad for n items: every level of 64-way
 // reductions is stored until 4 or fewer partials remain (ceil(n/64) + ceil(ceil(n/64)/64) + ...).
 inline size_t seg_reduce_scratch(size_t n) {
   size_t total = 0, m = (n + 63) / 64;

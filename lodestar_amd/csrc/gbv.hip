@@ -682,7 +682,7 @@ int gbv_sm_batch_submit(gbv_ctx* c, gbv_sm_batch* b) {
 //   stream H      : k_hash_msgs
 //   stream A      : k_sm_prepare(segment s)  -- throughput-bound, also forms per-wave chunk sums
 //   streams B0/B1 : (segment s alternates) wait(prepare s, hash) k_sm_chunk_finish, k_sm_miller,
-//                   k_sm_seg_reduce + k_sm_seg_check, k_sm_group_pairing (exits at once unless
+//                   k_seg_reduce_quad + k_sm_seg_check, k_sm_group_pairing (exits at once unless
 //                   the segment check failed)
 //   stream B0     : wait(all) k_sm_fallback (per-set retry of failed chunks only), copy-out
 // Each segment ends in ONE randomised multi-pairing check over all its chunks; only a failing

@@ -585,7 +585,7 @@ static int vs_partial_enqueue(gbv_ctx* c, gbv_vs_batch* b) {
     return rc;
   }
   // status doubles as the per-"chunk" state: SET_OK == GRP_PENDING (every valid set takes part);
-  // the reduction is a tree over 64-set blocks (k_sm_seg_reduce, k_sm_part_reduce)
+  // the reduction is a tree over 64-set blocks (k_seg_reduce_quad)
   launch_sm_seg_check(LaunchCfg{1, 64, s}, 0, (uint32_t)n, b->status, b->F, b->rS, b->Fpart, b->Spart, b->has, b->flag, b->f_out);
   HIP_CHECK_DRAIN(c, hipGetLastError());
   HIP_CHECK_DRAIN(c, hipMemcpyAsync(b->part_host, b->f_out, sizeof(Fp12), hipMemcpyDeviceToHost, s));

@@ -18,10 +18,6 @@ __device__ inline Fp2 shfl_down_fp(const Fp2& a, unsigned d) { return Fp2{shfl_d
 template <class F> __device__ inline Jac<F> shfl_down_jac(const Jac<F>& a, unsigned d) {
   return Jac<F>{shfl_down_fp(a.x, d), shfl_down_fp(a.y, d), shfl_down_fp(a.z, d)};
 }
-__device__ inline Fp6 shfl_down_fp6(const Fp6& a, unsigned d) {
-  return Fp6{shfl_down_fp(a.c0, d), shfl_down_fp(a.c1, d), shfl_down_fp(a.c2, d)};
-}
-__device__ inline Fp12 shfl_down_fp12(const Fp12& a, unsigned d) { return Fp12{shfl_down_fp6(a.c0, d), shfl_down_fp6(a.c1, d)}; }
 
 GBV_NI G1J g1_add(G1J a, G1J b) { return jac_add(a, b); }
 GBV_NI G2J g2_add(G2J a, G2J b) { return jac_add(a, b); }
@@ -344,60 +340,6 @@ __global__ void GBV_KERNEL_ATTR k_sm_miller(uint32_t g0, uint32_t G, const uint3
 }
 
 
-// Cross-lane tree: lane 0 ends with the product of the lanes' f and the sum of their s (lanes
-// with any == 0 hold nothing).
-__device__ inline void wave_reduce_fs(Fp12& f, G2J& s, int& any) {
-  unsigned lane = threadIdx.x;
-  for (unsigned d = 32; d >= 1; d >>= 1) {
-    Fp12 fo = shfl_down_fp12(f, d);
-    G2J so = shfl_down_jac(s, d);
-    int ao = __shfl_down(any, d, 64);
-    if (lane < d && ao) {
-      f = any ? fp12_mul(f, fo) : fo;
-      s = any ? g2_add(s, so) : so;
-      any = 1;
-    }
-  }
-}
-
-// Per block of 64 chunks of a segment: product of the pending chunks' Miller values and sum of
-// their S_g.  has[blk] = 0 when the block holds no pending chunk.
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
-k_sm_seg_reduce(uint32_t g0, uint32_t G, const uint8_t* __restrict__ grp_state, const Fp12* __restrict__ F, const G2J* __restrict__ SgJ,
-                Fp12* __restrict__ Fpart, G2J* __restrict__ Spart, uint8_t* __restrict__ has) {
-  GBV_TAIL_WAVE_PRIO();
-  uint32_t g = g0 + blockIdx.x * 64 + threadIdx.x;
-  int any = g < g0 + G && grp_state[g] == GRP_PENDING;
-  Fp12 f = any ? F[g] : fp12_one();
-  G2J s = any ? SgJ[g] : jac_infinity<Fp2>();
-  wave_reduce_fs(f, s, any);
-  if (threadIdx.x == 0) {
-    has[blockIdx.x] = (uint8_t)any;
-    if (any) {
-      Fpart[blockIdx.x] = f;
-      Spart[blockIdx.x] = s;
-    }
-  }
-}
-
-// Next level of the same reduction: 64 partials per block -> one.
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
-k_sm_part_reduce(uint32_t n, const uint8_t* __restrict__ has_in, const Fp12* __restrict__ Fin, const G2J* __restrict__ Sin,
-                 Fp12* __restrict__ Fout, G2J* __restrict__ Sout, uint8_t* __restrict__ has_out) {
-  GBV_TAIL_WAVE_PRIO();
-  uint32_t k = blockIdx.x * 64 + threadIdx.x;
-  int any = k < n && has_in[k];
-  Fp12 f = any ? Fin[k] : fp12_one();
-  G2J s = any ? Sin[k] : jac_infinity<Fp2>();
-  wave_reduce_fs(f, s, any);
-  if (threadIdx.x == 0) {
-    has_out[blockIdx.x] = (uint8_t)any;
-    if (any) {
-      Fout[blockIdx.x] = f;
-      Sout[blockIdx.x] = s;
-    }
-  }
-}
 
 // valid[i] for every set; sets of failed chunks are verified one by one (2-pair check each).
 __global__ void GBV_KERNEL_ATTR k_sm_fallback(uint32_t n, const uint32_t* __restrict__ set_grp, const uint32_t* __restrict__ grp_msg,
@@ -590,25 +532,6 @@ void launch_sm_miller(LaunchCfg c, uint32_t g0, uint32_t G, const uint32_t* grp_
                       Fp12* F) {
   hipLaunchKernelGGL(k_sm_miller, dim3((G + 63) / 64), dim3(64), 0, c.stream, g0, G, grp_msg, grp_state, PgJ, H, F);
   debug_sync(c.stream, "k_sm_miller");
-}
-// Reduces the segment's pending chunks to <= 4 partials (levels of 64); returns the offset of
-// the final level inside Fpart / Spart / has and its length in *n_out.
-uint32_t launch_sm_seg_reduce(LaunchCfg c, uint32_t g0, uint32_t G, const uint8_t* grp_state, const Fp12* F, const G2J* SgJ, Fp12* Fpart,
-                              G2J* Spart, uint8_t* has, uint32_t* n_out) {
-  uint32_t n = (G + 63) / 64;
-  hipLaunchKernelGGL(k_sm_seg_reduce, dim3(n), dim3(64), 0, c.stream, g0, G, grp_state, F, SgJ, Fpart, Spart, has);
-  debug_sync(c.stream, "k_sm_seg_reduce");
-  uint32_t off = 0;
-  while (n > 4) {
-    uint32_t m = (n + 63) / 64;
-    hipLaunchKernelGGL(k_sm_part_reduce, dim3(m), dim3(64), 0, c.stream, n, has + off, Fpart + off, Spart + off, Fpart + off + n,
-                       Spart + off + n, has + off + n);
-    debug_sync(c.stream, "k_sm_part_reduce");
-    off += n;
-    n = m;
-  }
-  *n_out = n;
-  return off;
 }
 void launch_sm_fallback(LaunchCfg c, uint32_t n, const uint32_t* set_grp, const uint32_t* grp_msg, const uint8_t* grp_state,
                         const uint8_t* status, const uint32_t* idx, const G1A* table, const G2A* S, const G2A* H, uint8_t* valid,

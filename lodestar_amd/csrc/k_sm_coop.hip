@@ -359,10 +359,87 @@ void launch_sm_fb_sets_coop(LaunchCfg c, const uint32_t* set_list, const uint32_
   debug_sync(c.stream, "k_sm_fb_sets_coop");
 }
 
+// One level of a segment's reduction on lane quads: block b combines items k = 64 b + j + 16 m
+// (quad j, m < 4) that are active (k < n, act[k] == act_val) into the product of their Fp12 values and
+// the sum of their G2 points -- per quad three quad::mul12 / quad::g2_add at most, then a 4-level
+// tree -- where the thread form ran a 6-level tree of one-lane fp12_mul + G2 additions (~580
+// product latencies against ~180).  has_out[b] = 0 when the block holds no active item.
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
+k_seg_reduce_quad(uint32_t n, const uint8_t* __restrict__ act, uint8_t act_val, const Fp12* __restrict__ Fin, const G2J* __restrict__ Sin,
+                  Fp12* __restrict__ Fout, G2J* __restrict__ Sout, uint8_t* __restrict__ has_out) {
+  GBV_TAIL_WAVE_PRIO();
+  const unsigned lane = threadIdx.x;
+  quad::Lane L;
+  L.q = lane & 3u;
+  L.h = (L.q & 2u) != 0;
+  L.s = (L.q & 1u) != 0;
+  const uint32_t j = lane >> 2, hf = L.h ? 1u : 0u;
+  Fp6 M = fp6_zero();
+  G2J S = jac_infinity<Fp2>();
+  int has = 0;
+  for (uint32_t m = 0; m < 4; ++m) {  // quad-uniform
+    const uint32_t k = blockIdx.x * 64 + j + 16 * m;
+    if (k >= n || act[k] != act_val) continue;
+    const Fp6 G = ((const Fp6*)&Fin[k])[hf];
+    const G2J P = Sin[k];
+    if (has) {
+      quad::mul12(M, G, L);
+      S = quad_g2_add(S, P, L.q);
+    } else {
+      M = G;
+      S = P;
+      has = 1;
+    }
+  }
+  for (unsigned d = 8; d >= 1; d >>= 1) {
+    Fp6 O;
+    G2J T;
+    Fp* od = (Fp*)&O;
+    const Fp* md = (const Fp*)&M;
+    for (int k = 0; k < 6; ++k) od[k] = shfl_down_fp_c(md[k], 4 * d);
+    Fp* td = (Fp*)&T;
+    const Fp* sd = (const Fp*)&S;
+    for (int k = 0; k < 6; ++k) td[k] = shfl_down_fp_c(sd[k], 4 * d);
+    const int ho = __shfl_down(has, 4 * d, 64);
+    if (j < d && ho) {
+      if (has) {
+        quad::mul12(M, O, L);
+        S = quad_g2_add(S, T, L.q);
+      } else {
+        M = O;
+        S = T;
+        has = 1;
+      }
+    }
+  }
+  if (lane == 0) has_out[blockIdx.x] = (uint8_t)has;
+  if (!has || j != 0) return;
+  if (!L.s) ((Fp6*)&Fout[blockIdx.x])[hf] = M;  // lane 0: c0, lane 2: c1
+  if (L.q == 0) Sout[blockIdx.x] = S;
+}
+
+uint32_t launch_seg_reduce_quad(hipStream_t s, uint32_t g0, uint32_t G, const uint8_t* grp_state, const Fp12* F, const G2J* SgJ, Fp12* Fpart,
+                                G2J* Spart, uint8_t* has, uint32_t* n_out) {
+  uint32_t n = (G + 63) / 64;
+  hipLaunchKernelGGL(k_seg_reduce_quad, dim3(n), dim3(64), 0, s, G, grp_state + g0, (uint8_t)GRP_PENDING, F + g0, SgJ + g0, Fpart, Spart, has);
+  debug_sync(s, "k_seg_reduce_quad");
+  uint32_t off = 0;
+  while (n > 4) {
+    const uint32_t m = (n + 63) / 64;
+    hipLaunchKernelGGL(k_seg_reduce_quad, dim3(m), dim3(64), 0, s, n, has + off, (uint8_t)1, Fpart + off, Spart + off, Fpart + off + n,
+                       Spart + off + n, has + off + n);
+    debug_sync(s, "k_seg_reduce_quad");
+    off += n;
+    n = m;
+  }
+  *n_out = n;
+  return off;
+}
+
 void launch_sm_seg_check(LaunchCfg c, uint32_t g0, uint32_t G, uint8_t* grp_state, const Fp12* F, const G2J* SgJ, Fp12* Fpart, G2J* Spart,
                          uint8_t* has, uint8_t* seg_ok, Fp12* miller_out, const G2J* S_extra) {
   uint32_t nb = 0;
-  uint32_t off = launch_sm_seg_reduce(c, g0, G, grp_state, F, SgJ, Fpart, Spart, has, &nb);
+  const uint32_t off = launch_seg_reduce_quad(c.stream, g0, G, grp_state, F, SgJ, Fpart, Spart, has, &nb);
   hipLaunchKernelGGL(k_sm_seg_check, dim3(1), dim3(64), 0, c.stream, g0, G, nb, Fpart + off, Spart + off, has + off, grp_state, seg_ok,
                      miller_out, S_extra);
   debug_sync(c.stream, "k_sm_seg_check");

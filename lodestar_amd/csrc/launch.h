@@ -29,8 +29,8 @@ void launch_sm_chunk_finish(LaunchCfg c, uint32_t g0, uint32_t G, uint32_t s0, c
                             const G1J* Ph, G1J* PgJ, G2J* SgJ, uint8_t* grp_state, uint32_t* n_fallback);
 void launch_sm_miller(LaunchCfg c, uint32_t g0, uint32_t G, const uint32_t* grp_msg, const uint8_t* grp_state, const G1J* PgJ, const G2A* H,
                       Fp12* F);
-uint32_t launch_sm_seg_reduce(LaunchCfg c, uint32_t g0, uint32_t G, const uint8_t* grp_state, const Fp12* F, const G2J* SgJ, Fp12* Fpart,
-                              G2J* Spart, uint8_t* has, uint32_t* n_out);
+uint32_t launch_seg_reduce_quad(hipStream_t s, uint32_t g0, uint32_t G, const uint8_t* grp_state, const Fp12* F, const G2J* SgJ, Fp12* Fpart,
+                                G2J* Spart, uint8_t* has, uint32_t* n_out);
 void launch_sm_seg_check(LaunchCfg c, uint32_t g0, uint32_t G, uint8_t* grp_state, const Fp12* F, const G2J* SgJ, Fp12* Fpart, G2J* Spart,
                          uint8_t* has, uint8_t* seg_ok, Fp12* miller_out = nullptr, const G2J* S_extra = nullptr);
 // runs when the segment check failed or any chunk went to the per-set path (n_fallback > 0)
