@@ -93,10 +93,12 @@ struct gbv_sm_batch;
 struct gbv_ctx {
   int device = 0;
   // stream A (per-set throughput kernels) at the lowest priority; the tail stream 2 (chunk-level
-  // latency-bound work) and the hash stream 4 at the highest.  Three streams = three hardware
-  // queues (GPU_MAX_HW_QUEUES=4 leaves one for the runtime): no two streams share a queue.
+  // latency-bound work), the hash stream 4 and stream 5 at the highest.  Stream 5 carries the
+  // signature half of small verifySignatureSets passes and, in the invalid-dense same-message regime,
+  // every other batch's failure path (the hash then runs on stream A): at most four streams are live
+  // at once, one per hardware queue (GPU_MAX_HW_QUEUES=4).
   hipStream_t stream = nullptr, stream2 = nullptr, stream4 = nullptr;
-  hipStream_t stream5 = nullptr;  // small verifySignatureSets passes: the signature half beside the aggregation
+  hipStream_t stream5 = nullptr;
   gbv::G1A* table = nullptr;
   uint8_t* table_ok = nullptr;
   size_t table_cap = 0;

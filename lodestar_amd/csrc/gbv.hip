@@ -694,8 +694,8 @@ static int sm_submit_enqueue(gbv_ctx* c, gbv_sm_batch* b) {
   // consecutive batches over two streams buys nothing while the tail is shorter than k_sm_prepare).
   // Invalid-dense regime (a segment failed within the last msm_cooldown_len submits, e.g. C5's 1 %
   // invalid stream): the failure path -- latency-bound run and per-set checks, ~170 ms per 1M
-  // sets at 1 % -- goes to stream 4 and the hash to stream A, so batch k's failure path runs
-  // beside batch k+1's chunk tail instead of in front of it (three streams either way).
+  // sets at 1 % -- goes to streams 4 and 5 (alternating per batch) and the hash to stream A, so batch
+  // k's failure path runs beside batch k+1's chunk tail and batch k+1's own failure path.
   ++c->sm_submits;
   const bool dense = c->msm_cooldown != 0;
   hipStream_t sa = c->stream;

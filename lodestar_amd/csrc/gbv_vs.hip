@@ -410,8 +410,8 @@ static int vs_submit_enqueue(gbv_ctx* c, gbv_vs_batch* b) {
 // Enqueue the whole verification without a host round trip: the per-set kernels on stream A, the
 // Miller values and chunk checks on a tail stream, alternating per submit between stream 2 and the
 // hash stream (idle in this path), so that consecutive batches' tails overlap each other and the
-// next batch's per-set kernels -- still three streams in all (gbv_sm_batch_submit: a fourth live
-// stream oversubscribes GPU_MAX_HW_QUEUES=4).
+// next batch's per-set kernels; small passes add stream 5 for the signature half (four live streams,
+// one per hardware queue: GPU_MAX_HW_QUEUES=4).
 int gbv_vs_batch_submit(gbv_ctx* c, gbv_vs_batch* b) {
   if (!c || !b) return GBV_E_ARG;
   GBV_LOCK(c);
