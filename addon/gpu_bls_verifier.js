@@ -23,6 +23,10 @@ const MAX_SIGNATURE_SETS_PER_JOB = 128; // multithread/index.ts:56
 const MAX_BUFFERED_SIGS = 32; // multithread/index.ts:65
 const MAX_BUFFER_WAIT_MS = 100; // multithread/index.ts:74
 const MAX_JOBS_CAN_ACCEPT_WORK = 512; // multithread/index.ts:79
+// A device pass takes queued jobs up to this many sets (the Python verifier's MAX_PASS_SETS): a burst
+// of gossip calls then becomes several passes, so the addon's marshalling of pass k + 1 and the
+// resolution of pass k - 1 run while pass k is on the device.
+const MAX_PASS_SETS = 1 << 18;
 
 /** chunkifyMaximizeChunkSize (multithread/utils.ts:4-18) */
 function chunkifyMaximizeChunkSize(arr, minPerChunk) {
@@ -327,8 +331,10 @@ class GpuBlsVerifier {
 
   _runJobs() {
     while (!this.closed && this.jobs.length > 0 && this.passesBusy < this.maxPasses) {
-      const jobs = this.jobs;
-      this.jobs = [];
+      let k = 0;
+      for (let sets = 0; k < this.jobs.length && (k === 0 || sets < MAX_PASS_SETS); ++k) sets += this.jobs[k].sets.length;
+      const jobs = k === this.jobs.length ? this.jobs : this.jobs.slice(0, k);
+      this.jobs = k === this.jobs.length ? [] : this.jobs.slice(k);
       this._runPass(jobs);
     }
   }
@@ -391,7 +397,7 @@ class GpuBlsVerifier {
     sm.forEach((j, k) => {
       const r = res[k];
       m.successJobsSignatureSetsCount.inc(1);
-      if (r.every((x) => x)) {
+      if (ArrayBuffer.isView(r) ? r.indexOf(0) < 0 : r.every(Boolean)) {
         m.batchSigsSuccess.inc(r.length);
       } else {
         // the chunk's aggregate check failed: its sets were verified one by one on the device
@@ -429,4 +435,5 @@ module.exports = {
   MAX_BUFFERED_SIGS,
   MAX_BUFFER_WAIT_MS,
   MAX_JOBS_CAN_ACCEPT_WORK,
+  MAX_PASS_SETS,
 };
