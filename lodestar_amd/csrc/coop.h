@@ -10,7 +10,8 @@
 //   outputs        : lane o computes output coordinate o, then every lane stores after a barrier
 // with term lists of their true length (records carry the counts; positive terms first), so an
 // Fp12 multiplication costs about one Fp product plus a few dozen adds of latency instead of 54
-// products.  The same drivers compile for the host (GBV_HOST_TEST: the 64 lanes run one after
+// products.  The final exponentiation's cyclotomic squarings are written out instead (cyc_sqr: two
+// phases, no records).  The same drivers compile for the host (GBV_HOST_TEST: the 64 lanes run one after
 // another) and are checked against the oracle in tests/test_host_arith.py;
 // tests/test_coop_tables.py checks the programs themselves.
 #pragma once
@@ -349,95 +350,6 @@ __device__ inline void run(const Prog& P, const Ws& w) { run_ni(&P, w.b[0], w.b[
 // fold into the code; no call, no callee-saved spills): for the program a hot loop runs tens of times.
 __device__ __forceinline__ void run_inl(const Prog& P, const Ws& w) { run_body(&P, w.b[0], w.b[1], w.b[2], w.b[3]); }
 
-// A one-round program that a loop runs tens of times on the same operands (the exponentiation's
-// cyclotomic squarings): run_body resolves every unit term's source on every call (the binding
-// selects, a shift, an add: ~15 VALU per term).  pre_resolve does that once -- a lane's term
-// addresses (bytes in LDS, the sign folded in, terms past the lane's own count pointing at the zero
-// constant) and its destinations -- and run_pre loads the values straight from them.
-template <int NR> struct Pre {
-  uint32_t a[NR][OPW], b[NR][OPW], part[SUM_TERMS], out[SUM_TERMS];
-  uint32_t h[NR], hs[NR], hp, ho;  // record headers (term counts)
-  uint32_t dz[NR], dp, dout;       // destinations: products, partial sum, output
-};
-struct AddrLoad {
-  const uint32_t* a;
-  __device__ Fp operator()(int i) const {
-    Fp r;
-    r.v = ((const LFp*)(size_t)a[i])->v;
-    return r;
-  }
-};
-__device__ inline uint32_t term_addr(const Ws& w, uint32_t t) { return (ws_unit(w, t & 7, (t >> 8) & 0xFF) + ((t >> 4) & 1)) << 6; }
-template <int N> __device__ __forceinline__ void resolve_terms(uint32_t (&d)[N], const uint32_t* r, uint32_t umax, uint32_t nu, const Ws& w) {
-#pragma unroll
-  for (int i = 0; i < N; ++i)
-    if ((uint32_t)i < umax) d[i] = term_addr(w, (uint32_t)i < nu ? r[i] : ZERO_TERM);
-}
-__device__ inline void put_at(uint32_t addr, const Fp& a) {
-  LFp* q = (LFp*)(size_t)addr;
-  q[0].v = a.v;
-  q[1].v = fp_neg(a).v;
-}
-__device__ inline uint32_t nu_lo(uint32_t h) { return (h & 0xFF) + ((h >> 8) & 0xFF); }
-__device__ inline uint32_t nu_hi(uint32_t h) { return ((h >> 16) & 0xFF) + (h >> 24); }
-// NR = P.n_rounds (checked by the caller's program choice; the tables are fixed at build time)
-template <int NR> __device__ __forceinline__ Pre<NR> pre_resolve(const Prog& P, const Ws& w) {
-  Pre<NR> x;
-  const uint32_t lane = threadIdx.x & 63u;
-  uint32_t rec[PROD_WORDS], rs[SUM_WORDS];
-  const uint32_t pm = __builtin_amdgcn_readfirstlane(P.pmax), om = __builtin_amdgcn_readfirstlane(P.omax);
-#pragma unroll
-  for (int r = 0; r < NR; ++r) {
-    const uint32_t p0 = r ? P.round_end[r - 1] : 0u, k = p0 + lane;
-    const uint32_t am = __builtin_amdgcn_readfirstlane(P.amax[r]), bm = __builtin_amdgcn_readfirstlane(P.bmax[r]);
-    if (k < P.round_end[r]) {
-      load_words(rec, P.prods + PROD_WORDS * k);
-      x.h[r] = rec[0];
-      x.hs[r] = rec[1 + 2 * OPW];
-      resolve_terms(x.a[r], rec + 1, am, nu_lo(x.h[r]), w);
-      resolve_terms(x.b[r], rec + 1 + OPW, bm, nu_hi(x.h[r]), w);
-      x.dz[r] = ws_unit(w, SRC_Z, k) << 6;
-    }
-  }
-  if (lane < P.n_part) {
-    load_words(rs, P.parts + SUM_WORDS * lane);
-    x.hp = rs[0];
-    resolve_terms(x.part, rs + 1, pm, nu_lo(x.hp), w);
-    x.dp = ws_unit(w, SRC_Z, P.round_end[NR - 1] + lane) << 6;
-  }
-  if (lane < P.n_out) {
-    load_words(rs, P.outs + SUM_WORDS * lane);
-    x.ho = rs[0];
-    resolve_terms(x.out, rs + 1, om, nu_lo(x.ho), w);
-    x.dout = ws_unit(w, P.out_dst[lane], P.out_idx[lane]) << 6;
-  }
-  return x;
-}
-// the same phases as run_body (scaled terms still read from the record)
-template <int NR> __device__ __forceinline__ void run_pre(const Prog& P, const Ws& w, const Pre<NR>& x) {
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t pm = __builtin_amdgcn_readfirstlane(P.pmax), om = __builtin_amdgcn_readfirstlane(P.omax);
-#pragma unroll
-  for (int r = 0; r < NR; ++r) {
-    const uint32_t p0 = r ? P.round_end[r - 1] : 0u, k = p0 + lane;
-    const uint32_t am = __builtin_amdgcn_readfirstlane(P.amax[r]), bm = __builtin_amdgcn_readfirstlane(P.bmax[r]);
-    if (k < P.round_end[r]) {
-      const uint32_t* rg = P.prods + PROD_WORDS * k;
-      const Fp a = lin_sum<OPW, false>(AddrLoad{x.a[r]}, w, am, nu_lo(x.h[r]), x.hs[r] & 0xFF, rg + 1);
-      const Fp b = lin_sum<OPW, false>(AddrLoad{x.b[r]}, w, bm, nu_hi(x.h[r]), (x.hs[r] >> 8) & 0xFF, rg + 1 + OPW);
-      put_at(x.dz[r], fp_mul_inl(a, b));
-    }
-    barrier();
-  }
-  if (lane < P.n_part)
-    put_at(x.dp, lin_sum<SUM_TERMS, true>(AddrLoad{x.part}, w, pm, nu_lo(x.hp), (x.hp >> 16) & 0xFF, P.parts + SUM_WORDS * lane + 1));
-  if (P.n_part) barrier();
-  Fp o;
-  if (lane < P.n_out) o = lin_sum<SUM_TERMS, true>(AddrLoad{x.out}, w, om, nu_lo(x.ho), (x.ho >> 16) & 0xFF, P.outs + SUM_WORDS * lane + 1);
-  barrier();
-  if (lane < P.n_out) put_at(x.dout, o);
-  barrier();
-}
 #define COOP_LANES(l) for (unsigned l = threadIdx.x & 63u; l == (threadIdx.x & 63u); l = ~0u)
 #define COOP_LANE0 if ((threadIdx.x & 63u) == 0)
 #endif
@@ -486,9 +398,6 @@ GBV_HD Ws ws2(Slot* mem, uint16_t z, uint16_t a, uint16_t b) { return make_ws(me
 GBV_HD Ws ws3(Slot* mem, uint16_t z, uint16_t a, uint16_t b, uint16_t c) { return make_ws(mem, z, a, b, c); }
 
 GBV_HD void mul12(Slot* mem, uint16_t z, uint16_t a, uint16_t b, uint16_t c) { run(FP12_MUL, ws3(mem, z, a, b, c)); }
-#ifndef GBV_COOP_INLINE_CYC
-#define GBV_COOP_INLINE_CYC 1  // the final exponentiation's ~320 cyclotomic squarings through run_inl
-#endif
 #ifndef GBV_COOP_INLINE_LOOPS
 #define GBV_COOP_INLINE_LOOPS 1  // the Miller loop's per-bit programs and the [|x|] doublings too
 #endif
@@ -501,16 +410,6 @@ GBV_HD void run_hot(const Prog& P, const Ws& w) {
     run_inl(P, w);
   else
     run(P, w);
-}
-#endif
-#if defined(GBV_HOST_TEST)
-GBV_HD void cyc_sqr12(Slot* mem, uint16_t z, uint16_t a, uint16_t c) { run(FP12_CYC_SQR, ws2(mem, z, a, c)); }
-#else
-GBV_HD void cyc_sqr12(Slot* mem, uint16_t z, uint16_t a, uint16_t c) {
-  if (GBV_COOP_INLINE_CYC)
-    run_inl(FP12_CYC_SQR, ws2(mem, z, a, c));
-  else
-    run(FP12_CYC_SQR, ws2(mem, z, a, c));
 }
 #endif
 GBV_HD void frob12(Slot* mem, uint16_t z, int n, uint16_t a, uint16_t c) { run(n == 1 ? FP12_FROB1 : FP12_FROB2, ws2(mem, z, a, c)); }
@@ -636,28 +535,139 @@ GBV_HD G2J point_jac(const Slot* mem) {
 constexpr uint16_t E_F = 0, E_INV = 12, E_T = 24, E_A = 36, E_B = 48, E_C = 60, E_TMP = 72, E_TMP2 = 84, E_Z = 96;
 constexpr int FINAL_EXP_WS = E_Z + ZSLOTS;
 
-// r = a^x (a in the cyclotomic subgroup)
-#ifndef GBV_COOP_PRE
-#define GBV_COOP_PRE 1  // the 63 squarings of an exponentiation with their term addresses resolved once
+// ---- cyclotomic squaring written out (the exponentiations' ~315 squarings) --------------------
+// Granger-Scott: f in the cyclotomic subgroup as three Fp4 pairs (z0, z1), (z2, z3), (z4, z5) --
+// slots (0 1 | 8 9), (6 7 | 4 5), (2 3 | 10 11) -- each pair's t0 = a^2 + xi b^2,
+// t1 = (a + b)^2 - a^2 - b^2, and
+//   z0' = 3 t0(z0,z1) - 2 z0   z1' = 3 t1(z0,z1) + 2 z1   z4' = 3 t0(z2,z3) - 2 z4
+//   z5' = 3 t1(z2,z3) + 2 z5   z2' = 3 xi t1(z4,z5) + 2 z2   z3' = 3 t0(z4,z5) - 2 z3.
+// An Fp2 square x^2 is two Fp products, P = (x0 + x1)(x0 - x1) and Q = x0 (2 x1): 18 products, one
+// per lane, then 12 output lanes, each 3 (<= 6 signed products) +- 2 z_o.  Against the interpreted
+// FP12_CYC_SQR (18 products, 12 partial sums with scaled terms read from the record, 12 outputs): no
+// partial-sum phase, no scaled terms, no record reads, and a lane's term addresses resolved once
+// per exponentiation.  The output lane of slot o reads input slot o only, so c may be a.
+#if defined(GBV_HOST_TEST)
+typedef const Fp* CAddr;
+inline CAddr caddr(const LSlot* s, uint32_t neg) { return neg ? &s->n : &s->v; }
+inline Fp cload(CAddr a) { return *a; }
+#else
+typedef uint32_t CAddr;  // LDS byte address of a value or its stored negation
+__device__ inline CAddr caddr(const LSlot* s, uint32_t neg) { return (uint32_t)(size_t)s + (neg << 6); }
+__device__ inline Fp cload(CAddr a) {
+  Fp r;
+  r.v = ((const LFp*)(size_t)a)->v;
+  return r;
+}
 #endif
+struct CycLane {
+  CAddr a[4], b[4];  // product lane (l < 18): the terms of its two operands
+  CAddr o[6], z;     // output lane (l < 12): its signed product terms, +-z_o
+  LSlot *dz, *dout;
+};
+GBV_HD CycLane cyc_lane(Slot* memg, uint16_t zo, uint16_t ao, uint16_t co, uint32_t l) {
+  LSlot* mem = GBV_LDS(memg);
+  const LSlot* in = mem + ao;
+  const LSlot* zs = mem + zo;
+  const CAddr zero = caddr(GBV_CONSTS_LDS, 0);
+  CycLane x;
+  for (int i = 0; i < 4; ++i) x.a[i] = x.b[i] = zero;
+  for (int i = 0; i < 6; ++i) x.o[i] = zero;
+  x.z = zero;
+  x.dz = mem + zo + (l < 18 ? l : 0);
+  x.dout = mem + co + (l < 12 ? l : 0);
+  if (l < 18) {
+    const uint32_t k = l / 6, j = l - 6 * k;
+    const uint32_t A = k == 0 ? 0 : k == 1 ? 6 : 2, B = k == 0 ? 8 : k == 1 ? 4 : 10;
+    const CAddr x0 = caddr(in + A, 0), x1 = caddr(in + A + 1, 0), x2 = caddr(in + B, 0), x3 = caddr(in + B + 1, 0);
+    const CAddr n1 = caddr(in + A + 1, 1), n3 = caddr(in + B + 1, 1);
+    switch (j) {
+      case 0: x.a[0] = x0, x.a[1] = x1, x.b[0] = x0, x.b[1] = n1; break;  // P(a)
+      case 1: x.a[0] = x0, x.b[0] = x1, x.b[1] = x1; break;                // Q(a)
+      case 2: x.a[0] = x2, x.a[1] = x3, x.b[0] = x2, x.b[1] = n3; break;  // P(b)
+      case 3: x.a[0] = x2, x.b[0] = x3, x.b[1] = x3; break;                // Q(b)
+      case 4:                                                              // P(a + b)
+        x.a[0] = x0, x.a[1] = x2, x.a[2] = x1, x.a[3] = x3;
+        x.b[0] = x0, x.b[1] = x2, x.b[2] = n1, x.b[3] = n3;
+        break;
+      default: x.a[0] = x0, x.a[1] = x2, x.b[0] = x1, x.b[1] = x3, x.b[2] = x1, x.b[3] = x3; break;  // Q(a + b)
+    }
+  }
+  if (l < 12) {
+    // slot pair s: z0 z4 z3 | z2 | z1 z5 -> t0 of pair s (minus 2z) | xi t1 of pair 2 | t1 of pair s - 4
+    const uint32_t s = l >> 1, c = l & 1;
+    const uint32_t k = s < 3 ? s : s == 3 ? 2 : s - 4;
+    const LSlot* p = zs + 6 * k;  // P(a) Q(a) P(b) Q(b) P(a+b) Q(a+b)
+    auto t = [&](int m, uint32_t neg) { return caddr(p + m, neg); };
+    if (s < 3) {
+      x.o[0] = c ? t(1, 0) : t(0, 0), x.o[1] = t(2, 0), x.o[2] = t(3, c ? 0 : 1);  // t0
+    } else if (s == 3) {
+      x.o[0] = t(4, 0), x.o[1] = t(0, 1), x.o[2] = t(2, 1);  // xi t1 = (t1.0 - t1.1, t1.0 + t1.1)
+      x.o[3] = t(5, c ? 0 : 1), x.o[4] = t(1, c ? 1 : 0), x.o[5] = t(3, c ? 1 : 0);
+    } else {
+      x.o[0] = t(c ? 5 : 4, 0), x.o[1] = t(c ? 1 : 0, 1), x.o[2] = t(c ? 3 : 2, 1);  // t1
+    }
+    x.z = caddr(in + l, s < 3 ? 1 : 0);
+  }
+  return x;
+}
+GBV_HD void cyc_prod(const CycLane& x) {
+  Fp a = cload(x.a[0]), b = cload(x.b[0]);
+  const Fp a1 = cload(x.a[1]), a2 = cload(x.a[2]), a3 = cload(x.a[3]);
+  const Fp b1 = cload(x.b[1]), b2 = cload(x.b[2]), b3 = cload(x.b[3]);
+  fp_acc_lazy(a, a1);  // operands below 4p: the product takes them
+  fp_acc_lazy(a, a2);
+  fp_acc_lazy(a, a3);
+  fp_acc_lazy(b, b1);
+  fp_acc_lazy(b, b2);
+  fp_acc_lazy(b, b3);
+  put(x.dz, fp_mul_inl(a, b));
+}
+GBV_HD void cyc_out(const CycLane& x) {
+  Fp u = cload(x.o[0]);
+  Fp v[5];
+  for (int i = 0; i < 5; ++i) v[i] = cload(x.o[1 + i]);
+  const Fp z = cload(x.z);
+  for (int i = 0; i < 5; ++i) fp_acc_lazy(u, v[i]);
+  fp_reduce8_ip(u);  // < 6p -> canonical
+  Fp r = u;
+  fp_acc_lazy(r, u);
+  fp_acc_lazy(r, u);
+  fp_acc_lazy(r, z);
+  fp_acc_lazy(r, z);
+  fp_reduce8_ip(r);  // 3u +- 2z < 5p
+  put(x.dout, r);
+}
+#if defined(GBV_HOST_TEST)
+inline void cyc_sqr(Slot* mem, uint16_t zo, uint16_t ao, uint16_t co) {
+  for (uint32_t l = 0; l < 18; ++l) cyc_prod(cyc_lane(mem, zo, ao, co, l));
+  for (uint32_t l = 0; l < 12; ++l) cyc_out(cyc_lane(mem, zo, ao, co, l));
+}
+#else
+__device__ __forceinline__ void cyc_sqr_lane(const CycLane& x) {
+  const uint32_t l = lane_id();
+  if (l < 18) cyc_prod(x);
+  barrier();
+  if (l < 12) cyc_out(x);
+  barrier();
+}
+__device__ inline void cyc_sqr(Slot* mem, uint16_t zo, uint16_t ao, uint16_t co) { cyc_sqr_lane(cyc_lane(mem, zo, ao, co, lane_id())); }
+#endif
+
+// r = a^x (a in the cyclotomic subgroup)
 GBV_HD void exp_x(Slot* mem, uint16_t a, uint16_t r) {
   copy(mem + r, mem + a, 12);
-#if !defined(GBV_HOST_TEST)
-  if (GBV_COOP_PRE) {
-    const Ws w = ws2(mem, E_Z, r, r);
-    const Pre<1> x = pre_resolve<1>(FP12_CYC_SQR, w);
-    for (int i = 62; i >= 0; --i) {
-      run_pre(FP12_CYC_SQR, w, x);
-      if ((X_ABS >> i) & 1ull) mul12(mem, E_Z, r, a, r);
-    }
-    conj12(mem + r);
-    return;
-  }
-#endif
+#if defined(GBV_HOST_TEST)
   for (int i = 62; i >= 0; --i) {
-    cyc_sqr12(mem, E_Z, r, r);
+    cyc_sqr(mem, E_Z, r, r);
     if ((X_ABS >> i) & 1ull) mul12(mem, E_Z, r, a, r);
   }
+#else
+  const CycLane x = cyc_lane(mem, E_Z, r, r, lane_id());
+  for (int i = 62; i >= 0; --i) {
+    cyc_sqr_lane(x);
+    if ((X_ABS >> i) & 1ull) mul12(mem, E_Z, r, a, r);
+  }
+#endif
   conj12(mem + r);
 }
 
@@ -685,7 +695,7 @@ GBV_HD bool final_exp_is_one(Slot* mem) {
   mul12(mem, E_Z, E_C, E_TMP, E_C);
   conj12(mem + E_B);
   mul12(mem, E_Z, E_C, E_B, E_C);         // c = b^(x^2 + p^2 - 1)
-  cyc_sqr12(mem, E_Z, E_T, E_TMP);
+  cyc_sqr(mem, E_Z, E_T, E_TMP);
   mul12(mem, E_Z, E_TMP, E_T, E_TMP);     // t^3
   mul12(mem, E_Z, E_C, E_TMP, E_C);
   return is_one12(mem + E_C);

@@ -28,8 +28,33 @@ __global__ void __launch_bounds__(64) k_coop_cyc(Fp* out, int iters) {
   coop::load_consts();
   if (threadIdx.x < 24) coop::put(ws + threadIdx.x, seed_fp(threadIdx.x));
   __syncthreads();
-  for (int i = 0; i < iters; ++i) coop::cyc_sqr12(ws, 36, 0, 0);
+  for (int i = 0; i < iters; ++i) coop::run(coop::FP12_CYC_SQR, coop::ws2(ws, 36, 0, 0));  // the interpreted program
   if (threadIdx.x < 12) out[blockIdx.x * 12 + threadIdx.x] = coop::get(ws + threadIdx.x);
+}
+
+// the squarings as exp_x runs them (coop::cyc_sqr_lane: written out, lane terms resolved once)
+__global__ void __launch_bounds__(64) k_coop_cyc_hand(Fp* out, int iters) {
+  __shared__ coop::Slot ws[36 + coop::ZSLOTS];
+  coop::load_consts();
+  if (threadIdx.x < 24) coop::put(ws + threadIdx.x, seed_fp(threadIdx.x));
+  __syncthreads();
+  const coop::CycLane x = coop::cyc_lane(ws, 36, 0, 0, threadIdx.x);
+  for (int i = 0; i < iters; ++i) coop::cyc_sqr_lane(x);
+  if (threadIdx.x < 12) out[blockIdx.x * 12 + threadIdx.x] = coop::get(ws + threadIdx.x);
+}
+
+// one wave: the final exponentiation alone
+__global__ void __launch_bounds__(64) k_coop_fe(Fp* out, int iters) {
+  __shared__ coop::Slot ws[coop::FINAL_EXP_WS];
+  coop::load_consts();
+  bool ok = false;
+  for (int i = 0; i < iters; ++i) {
+    if (threadIdx.x < 12) coop::put(ws + coop::E_F + threadIdx.x, seed_fp(threadIdx.x + i));
+    __syncthreads();
+    ok ^= coop::final_exp_is_one(ws);
+  }
+  if (threadIdx.x < 12) out[blockIdx.x * 12 + threadIdx.x] = coop::get(ws + coop::E_C + threadIdx.x);
+  if (threadIdx.x == 0) out[0].v[0] += ok;
 }
 
 // one wave, one lane: dependent Fp products (latency of the thread-level primitive)
@@ -128,6 +153,8 @@ int main() {
   run("fp12_mul lat", k_fp12_mul_lat, out, 1, 100, 54);
   run("coop mul12", k_coop_mul, out, 1, 200, 54);
   run("coop cyc_sqr", k_coop_cyc, out, 1, 200, 18);
+  run("coop cyc hand", k_coop_cyc_hand, out, 1, 200, 18);
+  run("coop FE", k_coop_fe, out, 1, 3, 8400);
   run("coop miller1", k_coop_miller, out, 1, 5, 6200);
   run("coop ML1+FE", k_coop_pairing, out, 1, 3, 14600);
   run("fp12_inv lane", k_lane0_fp12_inv, out, 1, 5, 500);
