@@ -10,8 +10,8 @@
 //   outputs        : lane o computes output coordinate o, then every lane stores after a barrier
 // with term lists of their true length (records carry the counts; positive terms first), so an
 // Fp12 multiplication costs about one Fp product plus a few dozen adds of latency instead of 54
-// products.  The final exponentiation's cyclotomic squarings are written out instead (cyc_sqr: two
-// phases, no records).  The same drivers compile for the host (GBV_HOST_TEST: the 64 lanes run one after
+// products.  The Miller loop's line products and the final exponentiation's cyclotomic squarings
+// are written out instead (mul_line, cyc_sqr: two phases, no records).  The same drivers compile for the host (GBV_HOST_TEST: the 64 lanes run one after
 // another) and are checked against the oracle in tests/test_host_arith.py;
 // tests/test_coop_tables.py checks the programs themselves.
 #pragma once
@@ -414,138 +414,10 @@ GBV_HD void run_hot(const Prog& P, const Ws& w) {
 #endif
 GBV_HD void frob12(Slot* mem, uint16_t z, int n, uint16_t a, uint16_t c) { run(n == 1 ? FP12_FROB1 : FP12_FROB2, ws2(mem, z, a, c)); }
 
-// ---- Miller loop over up to 2 pairs ---------------------------------------------------------
-// Workspace layout (slot offsets), MILLER_WS slots in total:
-//   F 0..11 | L 12..17 | per pair j: T 18+12j (6), Q 24+12j (4), P 28+12j (2: -xP, yP) | Z 42..169
-constexpr uint16_t M_F = 0, M_L = 12, M_PAIR = 18, M_Z = 42;
-constexpr int MILLER_WS = M_Z + ZSLOTS;
-
-// Load pair j: P affine G1, Q affine G2 (neither infinity).  Lane-parallel, ends with a barrier.
-GBV_HD void miller_load_pair(Slot* mem, int j, const G1A& P, const G2A& Q) {
-  LSlot* b = GBV_LDS(mem + M_PAIR + 12 * j);
-  COOP_LANES(l) {
-    if (l < 12) {
-      Fp v;
-      switch (l) {
-        case 0: v = Q.x.c0; break;
-        case 1: v = Q.x.c1; break;
-        case 2: v = Q.y.c0; break;
-        case 3: v = Q.y.c1; break;
-        case 4: v = FP_ONE; break;
-        case 5: v = fp_zero(); break;
-        case 6: v = Q.x.c0; break;
-        case 7: v = Q.x.c1; break;
-        case 8: v = Q.y.c0; break;
-        case 9: v = Q.y.c1; break;
-        case 10: v = fp_neg(P.x); break;
-        default: v = P.y; break;
-      }
-      put(b + l, v);
-    }
-  }
-  barrier();
-}
-
-// F = prod_j f_{|x|, Q_j}(P_j), conjugated (x < 0).  Pairs must be loaded first.
-GBV_HD void miller_loop(Slot* mem, int npairs) {
-  set_one12(mem + M_F);
-  for (int i = 62; i >= 0; --i) {
-    for (int j = 0; j < npairs; ++j) {
-      uint16_t t = M_PAIR + 12 * j;
-      if (j == 0 && i != 62)  // f^2 and pair 0's doubling step are independent: one program
-        run_hot(MILLER_SQR_DBL, make_ws(mem, M_Z, M_F, t, (uint16_t)(t + 10), M_F, t, M_L));
-      else
-        run(G2_DBL_STEP, make_ws(mem, M_Z, t, (uint16_t)(t + 10), t, M_L));
-      run_hot(FP12_MUL_LINE, ws3(mem, M_Z, M_F, M_L, M_F));
-    }
-    if ((X_ABS >> i) & 1ull) {
-      for (int j = 0; j < npairs; ++j) {
-        uint16_t t = M_PAIR + 12 * j;
-        run(G2_ADD_STEP, make_ws(mem, M_Z, t, (uint16_t)(t + 6), (uint16_t)(t + 10), t, M_L));
-        run(FP12_MUL_LINE, ws3(mem, M_Z, M_F, M_L, M_F));
-      }
-    }
-  }
-  conj12(mem + M_F);
-}
-
-// [|x|] Q (Q affine, not infinity) by the Miller loop's point steps alone (the lines they also
-// write to M_L are ignored): T ends at mem + M_PAIR in homogeneous projective coordinates
-// (x = X/Z, y = Y/Z).  The mixed addition is incomplete only for T = +-Q, i.e. for Q of order
-// dividing k -+ 1 with k < 2^64: a point of a small-order subgroup of E'(Fp2), never a hash output
-// or a curve point that has a component in the order-r subgroup.
-GBV_HD void mul_xabs_point(Slot* mem, const G2A& Q) {
-  miller_load_pair(mem, 0, G1A{fp_zero(), fp_zero()}, Q);
-  const uint16_t t = M_PAIR;
-  for (int i = 62; i >= 0; --i) {
-    run_hot(G2_DBL_PT, make_ws(mem, M_Z, t, t));  // the doubling without its line: 19 products, 6 outputs
-    if ((X_ABS >> i) & 1ull) run(G2_ADD_STEP, make_ws(mem, M_Z, t, (uint16_t)(t + 6), (uint16_t)(t + 10), t, M_L));
-  }
-}
-// [a - b x^2] Q for the batch digits (sa, sb) -- the scalar of curve.h's jac_mul_2d_signed, by its
-// signed joint ladder R = sum_i 2^i (+-Q +-E), E = -psi^2(Q) = [-x^2] Q -- on the cooperative point
-// steps, with the two digits of a step added one after the other (+-Q, then +-E: affine points
-// as they are, so no ladder table and no inversion): 31 doublings, 63 mixed additions.  T ends at
-// mem + M_PAIR like mul_xabs_point's.  For Q in the order-r subgroup no addition meets T = +-(its
-// operand): before a Q digit T = [2a + 2b lambda] Q with (a, b) != 0 -- never [+-1] Q -- and before an
-// E digit T = [odd + even lambda] Q, never +-E (|a|, |b| < 2^33 and the lattice of (u, v) with
-// u = v lambda mod r has no vector that short).  A point outside the subgroup gets a wrong multiple,
-// and the subgroup check beside it rejects that set.  Workspace: Q at M_PAIR + 6, -Q, E, -E at
-// M_PAIR + 12 / 16 / 20 (pair 1's slots).
-GBV_HD void mul_2d_point(Slot* mem, const G2A& Q, const G2A& E, uint32_t sa, uint32_t sb) {
-  const uint16_t t = M_PAIR, QP = t + 6, QN = t + 12, EP = t + 16, EN = t + 20;
-  LSlot* b = GBV_LDS(mem + M_PAIR);
-  COOP_LANES(l) {
-    if (l < 24) {
-      const G2A& p = (l >= 16) ? E : Q;
-      Fp v;
-      if (l == 4)
-        v = FP_ONE;
-      else if (l == 5 || l == 10 || l == 11)
-        v = fp_zero();
-      else {
-        const uint32_t c = l < 4 ? l : l < 10 ? l - 6 : (l & 3);  // x.c0 x.c1 y.c0 y.c1
-        v = c == 0 ? p.x.c0 : c == 1 ? p.x.c1 : c == 2 ? p.y.c0 : p.y.c1;
-        const bool neg = c >= 2 && ((l < 4 && !((sa >> 31) & 1u)) || (l >= 12 && l < 16) || l >= 20);
-        if (neg) v = fp_neg(v);
-      }
-      put(b + l, v);
-    }
-  }
-  barrier();
-  // T = +-Q (digit 31 of sa) is loaded; its E digit, then the 31 lower steps
-  run(G2_ADD_STEP, make_ws(mem, M_Z, t, ((sb >> 31) & 1u) ? EP : EN, (uint16_t)(t + 10), t, M_L));
-  for (int i = 30; i >= 0; --i) {
-    run_hot(G2_DBL_PT, make_ws(mem, M_Z, t, t));
-    run(G2_ADD_STEP, make_ws(mem, M_Z, t, ((sa >> i) & 1u) ? QP : QN, (uint16_t)(t + 10), t, M_L));
-    run(G2_ADD_STEP, make_ws(mem, M_Z, t, ((sb >> i) & 1u) ? EP : EN, (uint16_t)(t + 10), t, M_L));
-  }
-}
-
-// the point left by mul_xabs_point as a Jacobian point (X Z, Y Z^2, Z); one lane
-GBV_HD G2J point_jac(const Slot* mem) {
-  const LSlot* b = GBV_LDS(mem + M_PAIR);
-  const Fp2 X{get(b + 0), get(b + 1)}, Y{get(b + 2), get(b + 3)}, Z{get(b + 4), get(b + 5)};
-  return G2J{fp2_mul(X, Z), fp2_mul(Y, fp2_sqr(Z)), Z};
-}
-
-// ---- final exponentiation: f^(3 (p^12 - 1)/r) == 1 ? -----------------------------------------
-// Workspace (slot offsets): F 0..11 (input, clobbered) | INV 12 | T 24 | A 36 | B 48 | C 60 |
-// TMP 72 | TMP2 84 | Z 96..223
-constexpr uint16_t E_F = 0, E_INV = 12, E_T = 24, E_A = 36, E_B = 48, E_C = 60, E_TMP = 72, E_TMP2 = 84, E_Z = 96;
-constexpr int FINAL_EXP_WS = E_Z + ZSLOTS;
-
-// ---- cyclotomic squaring written out (the exponentiations' ~315 squarings) --------------------
-// Granger-Scott: f in the cyclotomic subgroup as three Fp4 pairs (z0, z1), (z2, z3), (z4, z5) --
-// slots (0 1 | 8 9), (6 7 | 4 5), (2 3 | 10 11) -- each pair's t0 = a^2 + xi b^2,
-// t1 = (a + b)^2 - a^2 - b^2, and
-//   z0' = 3 t0(z0,z1) - 2 z0   z1' = 3 t1(z0,z1) + 2 z1   z4' = 3 t0(z2,z3) - 2 z4
-//   z5' = 3 t1(z2,z3) + 2 z5   z2' = 3 xi t1(z4,z5) + 2 z2   z3' = 3 t0(z4,z5) - 2 z3.
-// An Fp2 square x^2 is two Fp products, P = (x0 + x1)(x0 - x1) and Q = x0 (2 x1): 18 products, one
-// per lane, then 12 output lanes, each 3 (<= 6 signed products) +- 2 z_o.  Against the interpreted
-// FP12_CYC_SQR (18 products, 12 partial sums with scaled terms read from the record, 12 outputs): no
-// partial-sum phase, no scaled terms, no record reads, and a lane's term addresses resolved once
-// per exponentiation.  The output lane of slot o reads input slot o only, so c may be a.
+// ---- written-out programs: lane descriptors resolved once, no records -------------------------
+// The hottest programs (the Miller loop's line products, the exponentiations' cyclotomic squarings)
+// as fixed two-phase code: product lanes, a barrier, output lanes.  A lane's term addresses (value or
+// stored negation, the zero constant for padding) are resolved once per loop into registers.
 #if defined(GBV_HOST_TEST)
 typedef const Fp* CAddr;
 inline CAddr caddr(const LSlot* s, uint32_t neg) { return neg ? &s->n : &s->v; }
@@ -559,6 +431,100 @@ __device__ inline Fp cload(CAddr a) {
   return r;
 }
 #endif
+
+// Sparse line product c = f l, l = c0 + c2 w^2 + c3 w^3 (slots l: c0 0 1 | c2 2 3 | c3 4 5; the lines
+// of G2_DBL_STEP / G2_ADD_STEP / MILLER_SQR_DBL).  Over Fp2[w]/(w^6 - xi) -- f_k at slot 2k for even
+// k, 2k + 5 for odd -- the w^m coefficient of f l is f_m c0 + [xi] f_(m-2) c2 + [xi] f_(m-3) c3 (xi
+// where the index wraps): 18 Fp2 products, each Karatsuba (P0 = f0 c0, P1 = f1 c1, P2 = (f0 + f1)
+// (c0 + c1)), one Fp product per lane on 54 lanes; then 12 output lanes of <= 9 unit terms --
+// (P0 - P1, P2 - P0 - P1), or (2 P0 - P2, P2 - 2 P1) for a xi-twisted product.  Against the
+// interpreted FP12_MUL_LINE (39 products, 24 partial sums, 318 terms): one phase fewer and ~220 terms.
+struct LineLane {
+  CAddr a[2], b[2];  // product lane (l < 54)
+  CAddr o[9];        // output lane (l < 12)
+  LSlot *dz, *dout;
+};
+GBV_HD LineLane line_lane(Slot* memg, uint16_t zo, uint16_t fo, uint16_t lo, uint16_t co, uint32_t l) {
+  LSlot* mem = GBV_LDS(memg);
+  const LSlot *f = mem + fo, *ln = mem + lo, *zs = mem + zo;
+  const CAddr zero = caddr(GBV_CONSTS_LDS, 0);
+  LineLane x;
+  x.a[0] = x.a[1] = x.b[0] = x.b[1] = zero;
+  for (int i = 0; i < 9; ++i) x.o[i] = zero;
+  x.dz = mem + zo + (l < 54 ? l : 0);
+  x.dout = mem + co + (l < 12 ? l : 0);
+  if (l < 54) {
+    const uint32_t t = l / 3, r = l - 3 * t, m = t / 3, s = t - 3 * m;
+    const uint32_t sh = s == 0 ? 0 : s + 1;  // w-degree of the line coefficient: 0, 2, 3
+    const uint32_t k = (m + 6 - sh) % 6;
+    const LSlot* fk = f + (k & 1 ? k + 5 : k);
+    const LSlot* lc = ln + 2 * s;
+    if (r < 2) {
+      x.a[0] = caddr(fk + r, 0), x.b[0] = caddr(lc + r, 0);
+    } else {
+      x.a[0] = caddr(fk, 0), x.a[1] = caddr(fk + 1, 0), x.b[0] = caddr(lc, 0), x.b[1] = caddr(lc + 1, 0);
+    }
+  }
+  if (l < 12) {
+    const uint32_t sp = l >> 1, c = l & 1, m = sp < 3 ? 2 * sp : 2 * (sp - 3) + 1;
+    int n = 0;
+    for (uint32_t s = 0; s < 3; ++s) {
+      const LSlot* P = zs + 3 * (3 * m + s);  // P0 P1 P2 of the product
+      const bool tw = m < (s == 0 ? 0u : s + 1);
+      if (!tw) {
+        if (!c) x.o[n++] = caddr(P, 0), x.o[n++] = caddr(P + 1, 1);
+        else x.o[n++] = caddr(P + 2, 0), x.o[n++] = caddr(P, 1), x.o[n++] = caddr(P + 1, 1);
+      } else {
+        if (!c) x.o[n++] = caddr(P, 0), x.o[n++] = caddr(P, 0), x.o[n++] = caddr(P + 2, 1);
+        else x.o[n++] = caddr(P + 2, 0), x.o[n++] = caddr(P + 1, 1), x.o[n++] = caddr(P + 1, 1);
+      }
+    }
+  }
+  return x;
+}
+GBV_HD void line_prod(const LineLane& x) {
+  Fp a = cload(x.a[0]), b = cload(x.b[0]);
+  const Fp a1 = cload(x.a[1]), b1 = cload(x.b[1]);
+  fp_acc_lazy(a, a1);
+  fp_acc_lazy(b, b1);
+  put(x.dz, fp_mul_inl(a, b));
+}
+GBV_HD void line_out(const LineLane& x) {
+  Fp v[9];
+  for (int i = 0; i < 9; ++i) v[i] = cload(x.o[i]);
+  Fp u = v[0];
+  for (int i = 1; i < 6; ++i) fp_acc_lazy(u, v[i]);
+  fp_reduce8_ip(u);  // < 6p
+  for (int i = 6; i < 9; ++i) fp_acc_lazy(u, v[i]);
+  fp_reduce8_ip(u);  // < 4p
+  put(x.dout, u);
+}
+#if defined(GBV_HOST_TEST)
+inline void mul_line(Slot* mem, uint16_t zo, uint16_t fo, uint16_t lo, uint16_t co) {
+  for (uint32_t l = 0; l < 54; ++l) line_prod(line_lane(mem, zo, fo, lo, co, l));
+  for (uint32_t l = 0; l < 12; ++l) line_out(line_lane(mem, zo, fo, lo, co, l));
+}
+#else
+__device__ __forceinline__ void mul_line_lane(const LineLane& x) {
+  const uint32_t l = lane_id();
+  if (l < 54) line_prod(x);
+  barrier();
+  if (l < 12) line_out(x);
+  barrier();
+}
+#endif
+
+// ---- cyclotomic squaring written out (the exponentiations' ~315 squarings) --------------------
+// Granger-Scott: f in the cyclotomic subgroup as three Fp4 pairs (z0, z1), (z2, z3), (z4, z5) --
+// slots (0 1 | 8 9), (6 7 | 4 5), (2 3 | 10 11) -- each pair's t0 = a^2 + xi b^2,
+// t1 = (a + b)^2 - a^2 - b^2, and
+//   z0' = 3 t0(z0,z1) - 2 z0   z1' = 3 t1(z0,z1) + 2 z1   z4' = 3 t0(z2,z3) - 2 z4
+//   z5' = 3 t1(z2,z3) + 2 z5   z2' = 3 xi t1(z4,z5) + 2 z2   z3' = 3 t0(z4,z5) - 2 z3.
+// An Fp2 square x^2 is two Fp products, P = (x0 + x1)(x0 - x1) and Q = x0 (2 x1): 18 products, one
+// per lane, then 12 output lanes, each 3 (<= 6 signed products) +- 2 z_o.  Against the interpreted
+// FP12_CYC_SQR (18 products, 12 partial sums with scaled terms read from the record, 12 outputs): no
+// partial-sum phase, no scaled terms, no record reads, and a lane's term addresses resolved once
+// per exponentiation.  The output lane of slot o reads input slot o only, so c may be a.
 struct CycLane {
   CAddr a[4], b[4];  // product lane (l < 18): the terms of its two operands
   CAddr o[6], z;     // output lane (l < 12): its signed product terms, +-z_o
@@ -653,6 +619,133 @@ __device__ __forceinline__ void cyc_sqr_lane(const CycLane& x) {
 __device__ inline void cyc_sqr(Slot* mem, uint16_t zo, uint16_t ao, uint16_t co) { cyc_sqr_lane(cyc_lane(mem, zo, ao, co, lane_id())); }
 #endif
 
+// ---- Miller loop over up to 2 pairs ---------------------------------------------------------
+// Workspace layout (slot offsets), MILLER_WS slots in total:
+//   F 0..11 | L 12..17 | per pair j: T 18+12j (6), Q 24+12j (4), P 28+12j (2: -xP, yP) | Z 42..169
+constexpr uint16_t M_F = 0, M_L = 12, M_PAIR = 18, M_Z = 42;
+constexpr int MILLER_WS = M_Z + ZSLOTS;
+
+// Load pair j: P affine G1, Q affine G2 (neither infinity).  Lane-parallel, ends with a barrier.
+GBV_HD void miller_load_pair(Slot* mem, int j, const G1A& P, const G2A& Q) {
+  LSlot* b = GBV_LDS(mem + M_PAIR + 12 * j);
+  COOP_LANES(l) {
+    if (l < 12) {
+      Fp v;
+      switch (l) {
+        case 0: v = Q.x.c0; break;
+        case 1: v = Q.x.c1; break;
+        case 2: v = Q.y.c0; break;
+        case 3: v = Q.y.c1; break;
+        case 4: v = FP_ONE; break;
+        case 5: v = fp_zero(); break;
+        case 6: v = Q.x.c0; break;
+        case 7: v = Q.x.c1; break;
+        case 8: v = Q.y.c0; break;
+        case 9: v = Q.y.c1; break;
+        case 10: v = fp_neg(P.x); break;
+        default: v = P.y; break;
+      }
+      put(b + l, v);
+    }
+  }
+  barrier();
+}
+
+// F = prod_j f_{|x|, Q_j}(P_j), conjugated (x < 0).  Pairs must be loaded first.
+GBV_HD void miller_loop(Slot* mem, int npairs) {
+#if defined(GBV_HOST_TEST)
+  auto mline = [&]() { mul_line(mem, M_Z, M_F, M_L, M_F); };
+#else
+  const LineLane lx = line_lane(mem, M_Z, M_F, M_L, M_F, lane_id());  // f = f l, resolved once
+  auto mline = [&]() { mul_line_lane(lx); };
+#endif
+  set_one12(mem + M_F);
+  for (int i = 62; i >= 0; --i) {
+    for (int j = 0; j < npairs; ++j) {
+      uint16_t t = M_PAIR + 12 * j;
+      if (j == 0 && i != 62)  // f^2 and pair 0's doubling step are independent: one program
+        run_hot(MILLER_SQR_DBL, make_ws(mem, M_Z, M_F, t, (uint16_t)(t + 10), M_F, t, M_L));
+      else
+        run(G2_DBL_STEP, make_ws(mem, M_Z, t, (uint16_t)(t + 10), t, M_L));
+      mline();
+    }
+    if ((X_ABS >> i) & 1ull) {
+      for (int j = 0; j < npairs; ++j) {
+        uint16_t t = M_PAIR + 12 * j;
+        run(G2_ADD_STEP, make_ws(mem, M_Z, t, (uint16_t)(t + 6), (uint16_t)(t + 10), t, M_L));
+        mline();
+      }
+    }
+  }
+  conj12(mem + M_F);
+}
+
+// [|x|] Q (Q affine, not infinity) by the Miller loop's point steps alone (the lines they also
+// write to M_L are ignored): T ends at mem + M_PAIR in homogeneous projective coordinates
+// (x = X/Z, y = Y/Z).  The mixed addition is incomplete only for T = +-Q, i.e. for Q of order
+// dividing k -+ 1 with k < 2^64: a point of a small-order subgroup of E'(Fp2), never a hash output
+// or a curve point that has a component in the order-r subgroup.
+GBV_HD void mul_xabs_point(Slot* mem, const G2A& Q) {
+  miller_load_pair(mem, 0, G1A{fp_zero(), fp_zero()}, Q);
+  const uint16_t t = M_PAIR;
+  for (int i = 62; i >= 0; --i) {
+    run_hot(G2_DBL_PT, make_ws(mem, M_Z, t, t));  // the doubling without its line: 19 products, 6 outputs
+    if ((X_ABS >> i) & 1ull) run(G2_ADD_STEP, make_ws(mem, M_Z, t, (uint16_t)(t + 6), (uint16_t)(t + 10), t, M_L));
+  }
+}
+// [a - b x^2] Q for the batch digits (sa, sb) -- the scalar of curve.h's jac_mul_2d_signed, by its
+// signed joint ladder R = sum_i 2^i (+-Q +-E), E = -psi^2(Q) = [-x^2] Q -- on the cooperative point
+// steps, with the two digits of a step added one after the other (+-Q, then +-E: affine points
+// as they are, so no ladder table and no inversion): 31 doublings, 63 mixed additions.  T ends at
+// mem + M_PAIR like mul_xabs_point's.  For Q in the order-r subgroup no addition meets T = +-(its
+// operand): before a Q digit T = [2a + 2b lambda] Q with (a, b) != 0 -- never [+-1] Q -- and before an
+// E digit T = [odd + even lambda] Q, never +-E (|a|, |b| < 2^33 and the lattice of (u, v) with
+// u = v lambda mod r has no vector that short).  A point outside the subgroup gets a wrong multiple,
+// and the subgroup check beside it rejects that set.  Workspace: Q at M_PAIR + 6, -Q, E, -E at
+// M_PAIR + 12 / 16 / 20 (pair 1's slots).
+GBV_HD void mul_2d_point(Slot* mem, const G2A& Q, const G2A& E, uint32_t sa, uint32_t sb) {
+  const uint16_t t = M_PAIR, QP = t + 6, QN = t + 12, EP = t + 16, EN = t + 20;
+  LSlot* b = GBV_LDS(mem + M_PAIR);
+  COOP_LANES(l) {
+    if (l < 24) {
+      const G2A& p = (l >= 16) ? E : Q;
+      Fp v;
+      if (l == 4)
+        v = FP_ONE;
+      else if (l == 5 || l == 10 || l == 11)
+        v = fp_zero();
+      else {
+        const uint32_t c = l < 4 ? l : l < 10 ? l - 6 : (l & 3);  // x.c0 x.c1 y.c0 y.c1
+        v = c == 0 ? p.x.c0 : c == 1 ? p.x.c1 : c == 2 ? p.y.c0 : p.y.c1;
+        const bool neg = c >= 2 && ((l < 4 && !((sa >> 31) & 1u)) || (l >= 12 && l < 16) || l >= 20);
+        if (neg) v = fp_neg(v);
+      }
+      put(b + l, v);
+    }
+  }
+  barrier();
+  // T = +-Q (digit 31 of sa) is loaded; its E digit, then the 31 lower steps
+  run(G2_ADD_STEP, make_ws(mem, M_Z, t, ((sb >> 31) & 1u) ? EP : EN, (uint16_t)(t + 10), t, M_L));
+  for (int i = 30; i >= 0; --i) {
+    run_hot(G2_DBL_PT, make_ws(mem, M_Z, t, t));
+    run(G2_ADD_STEP, make_ws(mem, M_Z, t, ((sa >> i) & 1u) ? QP : QN, (uint16_t)(t + 10), t, M_L));
+    run(G2_ADD_STEP, make_ws(mem, M_Z, t, ((sb >> i) & 1u) ? EP : EN, (uint16_t)(t + 10), t, M_L));
+  }
+}
+
+// the point left by mul_xabs_point as a Jacobian point (X Z, Y Z^2, Z); one lane
+GBV_HD G2J point_jac(const Slot* mem) {
+  const LSlot* b = GBV_LDS(mem + M_PAIR);
+  const Fp2 X{get(b + 0), get(b + 1)}, Y{get(b + 2), get(b + 3)}, Z{get(b + 4), get(b + 5)};
+  return G2J{fp2_mul(X, Z), fp2_mul(Y, fp2_sqr(Z)), Z};
+}
+
+// ---- final exponentiation: f^(3 (p^12 - 1)/r) == 1 ? -----------------------------------------
+// Workspace (slot offsets): F 0..11 (input, clobbered) | INV 12 | T 24 | A 36 | B 48 | C 60 |
+// TMP 72 | TMP2 84 | Z 96..223
+constexpr uint16_t E_F = 0, E_INV = 12, E_T = 24, E_A = 36, E_B = 48, E_C = 60, E_TMP = 72, E_TMP2 = 84, E_Z = 96;
+constexpr int FINAL_EXP_WS = E_Z + ZSLOTS;
+
 // r = a^x (a in the cyclotomic subgroup)
 GBV_HD void exp_x(Slot* mem, uint16_t a, uint16_t r) {
   copy(mem + r, mem + a, 12);
@@ -671,10 +764,31 @@ GBV_HD void exp_x(Slot* mem, uint16_t a, uint16_t r) {
   conj12(mem + r);
 }
 
+// f^-1 (E_F -> E_INV; E_T .. E_TMP are scratch) by norms down to Fp2, the products cooperative and
+// one Fp2 inversion on lane 0: t = f conj(f) in Fp6, s = t^(p^2 + p^4) (two Frobenius maps), N = t s
+// in Fp2, f^-1 = conj(f) s N^-1.  Against fp12_inv on one lane (~250 us: ~100 dependent thread-level
+// Fp products around the Fp inversion) four cooperative products and the Fp2 inversion alone.
+GBV_HD void inv12(Slot* mem) {
+  copy(mem + E_TMP, mem + E_F, 12);
+  conj12(mem + E_TMP);
+  mul12(mem, E_Z, E_F, E_TMP, E_T);  // t
+  frob12(mem, E_Z, 2, E_T, E_A);
+  frob12(mem, E_Z, 2, E_A, E_B);
+  mul12(mem, E_Z, E_A, E_B, E_C);    // s
+  mul12(mem, E_Z, E_T, E_C, E_A);    // N (coordinates 0, 1; the rest 0)
+  mul12(mem, E_Z, E_TMP, E_C, E_B);  // conj(f) s
+  COOP_LANE0 {
+    const Fp2 ni = fp2_inv(Fp2{get(GBV_LDS(mem + E_A)), get(GBV_LDS(mem + E_A + 1))});
+    put(GBV_LDS(mem + E_A), ni.c0);
+    put(GBV_LDS(mem + E_A + 1), ni.c1);
+  }
+  barrier();
+  mul12(mem, E_Z, E_B, E_A, E_INV);
+}
+
 // f (at mem + E_F) -> returns f^(3 (p^12-1)/r) == 1 (same value on every lane)
 GBV_HD bool final_exp_is_one(Slot* mem) {
-  COOP_LANE0 store12(mem + E_INV, fp12_inv(load12(mem + E_F)));  // one scalar inversion
-  barrier();
+  inv12(mem);
   conj12(mem + E_F);
   mul12(mem, E_Z, E_F, E_INV, E_T);       // t = f^(p^6 - 1)
   frob12(mem, E_Z, 2, E_T, E_TMP);
