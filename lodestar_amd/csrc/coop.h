@@ -439,6 +439,19 @@ __device__ inline Fp cload(CAddr a) {
 // (c0 + c1)), one Fp product per lane on 54 lanes; then 12 output lanes of <= 9 unit terms --
 // (P0 - P1, P2 - P0 - P1), or (2 P0 - P2, P2 - 2 P1) for a xi-twisted product.  Against the
 // interpreted FP12_MUL_LINE (39 products, 24 partial sums, 318 terms): one phase fewer and ~220 terms.
+// The unit terms of component c of a Karatsuba Fp2 product (P0 = a0 b0, P1 = a1 b1, P2 = (a0 + a1)
+// (b0 + b1) at P): (P0 - P1, P2 - P0 - P1), or times xi (2 P0 - P2, P2 - 2 P1); a plain real part has
+// two terms, the third the zero constant.
+struct Terms3 {
+  CAddr t[3];
+};
+GBV_HD Terms3 kara_terms(const LSlot* P, uint32_t c, bool tw, CAddr zero) {
+  Terms3 r;
+  r.t[0] = c ? caddr(P + 2, 0) : caddr(P, 0);
+  r.t[1] = c ? caddr(P + 1, 1) : tw ? caddr(P, 0) : caddr(P + 1, 1);
+  r.t[2] = c ? (tw ? caddr(P + 1, 1) : caddr(P, 1)) : tw ? caddr(P + 2, 1) : zero;
+  return r;
+}
 struct LineLane {
   CAddr a[2], b[2];  // product lane (l < 54)
   CAddr o[9];        // output lane (l < 12)
@@ -467,17 +480,10 @@ GBV_HD LineLane line_lane(Slot* memg, uint16_t zo, uint16_t fo, uint16_t lo, uin
   }
   if (l < 12) {
     const uint32_t sp = l >> 1, c = l & 1, m = sp < 3 ? 2 * sp : 2 * (sp - 3) + 1;
-    int n = 0;
-    for (uint32_t s = 0; s < 3; ++s) {
-      const LSlot* P = zs + 3 * (3 * m + s);  // P0 P1 P2 of the product
-      const bool tw = m < (s == 0 ? 0u : s + 1);
-      if (!tw) {
-        if (!c) x.o[n++] = caddr(P, 0), x.o[n++] = caddr(P + 1, 1);
-        else x.o[n++] = caddr(P + 2, 0), x.o[n++] = caddr(P, 1), x.o[n++] = caddr(P + 1, 1);
-      } else {
-        if (!c) x.o[n++] = caddr(P, 0), x.o[n++] = caddr(P, 0), x.o[n++] = caddr(P + 2, 1);
-        else x.o[n++] = caddr(P + 2, 0), x.o[n++] = caddr(P + 1, 1), x.o[n++] = caddr(P + 1, 1);
-      }
+#pragma unroll
+    for (uint32_t s = 0; s < 3; ++s) {  // fixed register positions: no dynamically indexed arrays
+      const Terms3 t = kara_terms(zs + 3 * (3 * m + s), c, m < (s == 0 ? 0u : s + 1), zero);
+      x.o[3 * s] = t.t[0], x.o[3 * s + 1] = t.t[1], x.o[3 * s + 2] = t.t[2];
     }
   }
   return x;
@@ -510,6 +516,216 @@ __device__ __forceinline__ void mul_line_lane(const LineLane& x) {
   if (l < 54) line_prod(x);
   barrier();
   if (l < 12) line_out(x);
+  barrier();
+}
+#endif
+
+// One Miller-loop bit written out: f^2 (optional) and the doubling step of T with its line, the
+// same maps as MILLER_SQR_DBL / G2_DBL_STEP (tools/gen_coop.py dbl_step_into: T' = 4 [2]T
+// homogeneous; line (B - E, 3 X^2 (-xP), H yP)).  Round 1: the doubling's 11 products d0..d10 (XY
+// Karatsuba, Y^2, Z^2, (Y + Z)^2, X^2) on lanes 0..10 and f^2's first 53 products on lanes 11..63;
+// round 2: the doubling's 14 products r0..r13, whose operands are small multiples of round-1 products
+// (3b' = 12 xi, so 36, 72, 3456 ...: unit terms plus k times a sum, fp_mul_small), and f^2's last 4;
+// then 24 output lanes: f^2 (<= 9 unit terms), T', the line.  f^2 over Fp2[w]/(w^6 - xi): the
+// w^m coefficient sums f_i f_j over i + j = m mod 6 (xi where it wraps): 15 cross products
+// (2 f_i) f_j (Karatsuba, 3 products) and 6 squares (2 products), 57 in all.  Z: d at 0..10, the
+// square's products at 11..67, r at 68..81.
+struct SqrDblLane {
+  CAddr a[4], b[4];                    // round 1
+  CAddr a2[4], av[3], b2[4], bv[3];    // round 2: operand = unit terms + k (sum of v terms)
+  uint32_t ak, bk;
+  CAddr o[12], ov[2];                  // output: unit terms + k (sum of v terms)
+  uint32_t ok;
+  LSlot *dz1, *dz2, *dout;
+};
+constexpr uint32_t SD_F2 = 11, SD_R2 = 68;
+// the operands of the square's product k (< 57): unit terms only
+GBV_HD void sqr_prod_terms(CAddr (&a)[4], CAddr (&b)[4], const LSlot* f, uint32_t k, CAddr zero) {
+  const bool cross = k < 45;
+  const uint32_t c = k / 3, rc = k - 3 * c, sq = (k - 45) >> 1, rs = (k - 45) & 1;
+  uint32_t ci = 0, cj = 0, n = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < 6; ++i)
+#pragma unroll
+    for (uint32_t j = i + 1; j < 6; ++j, ++n)
+      if (n == c) ci = i, cj = j;
+  const uint32_t i = cross ? ci : sq;
+  const LSlot* A = f + (i & 1 ? i + 5 : i);
+  const LSlot* B = f + (cj & 1 ? cj + 5 : cj);
+  const CAddr a0 = caddr(A, 0), a1 = caddr(A + 1, 0), b0 = caddr(B, 0), b1 = caddr(B + 1, 0);
+  for (int q = 0; q < 4; ++q) a[q] = b[q] = zero;
+  if (cross) {  // (2 f_i) f_j
+    a[0] = a[1] = rc == 1 ? a1 : a0;
+    a[2] = a[3] = rc == 2 ? a1 : zero;
+    b[0] = rc == 1 ? b1 : b0;
+    b[1] = rc == 2 ? b1 : zero;
+  } else {  // f_i^2 = ((a0 + a1)(a0 - a1), a0 (2 a1))
+    a[0] = a0;
+    a[1] = rs ? zero : a1;
+    b[0] = rs ? a1 : a0;
+    b[1] = rs ? a1 : caddr(A + 1, 1);
+  }
+}
+GBV_HD SqrDblLane sqr_dbl_lane(Slot* memg, uint16_t zo, uint16_t fo, uint16_t to, uint16_t po, uint16_t lo, uint32_t l) {
+  LSlot* mem = GBV_LDS(memg);
+  const LSlot *f = mem + fo, *T = mem + to, *P = mem + po, *zs = mem + zo;
+  const CAddr zero = caddr(GBV_CONSTS_LDS, 0);
+  SqrDblLane x;
+  for (int q = 0; q < 4; ++q) x.a[q] = x.b[q] = x.a2[q] = x.b2[q] = zero;
+  for (int q = 0; q < 3; ++q) x.av[q] = x.bv[q] = zero;
+  for (int q = 0; q < 12; ++q) x.o[q] = zero;
+  x.ov[0] = x.ov[1] = zero;
+  x.ak = x.bk = x.ok = 1;
+  x.dz1 = mem + zo + (l < 64 ? l : 0);
+  x.dz2 = mem + zo + (l < 14 ? SD_R2 + l : l < 18 ? l + SD_F2 + 39 : 0);
+  x.dout = l < 12 ? mem + fo + l : l < 18 ? mem + to + (l - 12) : l < 24 ? mem + lo + (l - 18) : mem + zo;
+  auto t = [&](uint32_t i, uint32_t neg) { return caddr(T + i, neg); };  // x0 x1 y0 y1 z0 z1
+  auto d = [&](uint32_t i, uint32_t neg) { return caddr(zs + i, neg); };
+  // round 1
+  if (l < 11) {
+    switch (l) {
+      case 0: x.a[0] = t(0, 0), x.b[0] = t(2, 0); break;
+      case 1: x.a[0] = t(1, 0), x.b[0] = t(3, 0); break;
+      case 2: x.a[0] = t(0, 0), x.a[1] = t(1, 0), x.b[0] = t(2, 0), x.b[1] = t(3, 0); break;
+      case 3: x.a[0] = t(2, 0), x.a[1] = t(3, 0), x.b[0] = t(2, 0), x.b[1] = t(3, 1); break;
+      case 4: x.a[0] = t(2, 0), x.b[0] = x.b[1] = t(3, 0); break;
+      case 5: x.a[0] = t(4, 0), x.a[1] = t(5, 0), x.b[0] = t(4, 0), x.b[1] = t(5, 1); break;
+      case 6: x.a[0] = t(4, 0), x.b[0] = x.b[1] = t(5, 0); break;
+      case 7:
+        x.a[0] = t(2, 0), x.a[1] = t(4, 0), x.a[2] = t(3, 0), x.a[3] = t(5, 0);
+        x.b[0] = t(2, 0), x.b[1] = t(4, 0), x.b[2] = t(3, 1), x.b[3] = t(5, 1);
+        break;
+      case 8:
+        x.a[0] = t(2, 0), x.a[1] = t(4, 0);
+        x.b[0] = x.b[2] = t(3, 0), x.b[1] = x.b[3] = t(5, 0);
+        break;
+      case 9: x.a[0] = t(0, 0), x.a[1] = t(1, 0), x.b[0] = t(0, 0), x.b[1] = t(1, 1); break;
+      default: x.a[0] = t(0, 0), x.b[0] = x.b[1] = t(1, 0); break;
+    }
+  } else if (l < 64) {
+    sqr_prod_terms(x.a, x.b, f, l - SD_F2, zero);
+  }
+  // round 2
+  if (l < 14) {
+    switch (l) {
+      case 0: x.a2[0] = x.a2[1] = d(0, 0), x.a2[2] = x.a2[3] = d(1, 1), x.b2[0] = d(3, 0), x.bv[0] = d(6, 0), x.bv[1] = d(5, 1), x.bk = 36; break;
+      case 1: x.av[0] = d(2, 0), x.av[1] = d(0, 1), x.av[2] = d(1, 1), x.ak = 2, x.b2[0] = d(4, 0), x.bv[0] = d(5, 1), x.bv[1] = d(6, 1), x.bk = 36; break;
+      case 2: x.av[0] = d(2, 0), x.av[1] = x.av[2] = d(1, 1), x.ak = 2, x.b2[0] = d(3, 0), x.b2[1] = d(4, 0), x.bv[0] = d(5, 1), x.bk = 72; break;
+      case 3: x.a2[0] = d(3, 0), x.a2[1] = d(4, 0), x.av[0] = d(5, 0), x.ak = 72, x.b2[0] = d(3, 0), x.b2[1] = d(4, 1), x.bv[0] = d(6, 1), x.bk = 72; break;
+      case 4: x.a2[0] = d(3, 0), x.av[0] = d(5, 0), x.av[1] = d(6, 1), x.ak = 36, x.b2[0] = x.b2[1] = d(4, 0), x.bv[0] = d(5, 0), x.bv[1] = d(6, 0), x.bk = 72; break;
+      case 5: x.av[0] = d(5, 0), x.ak = 3456, x.b2[0] = x.b2[1] = d(6, 1); break;
+      case 6: x.av[0] = d(5, 0), x.av[1] = d(6, 1), x.ak = 3456, x.b2[0] = d(5, 0), x.b2[1] = d(6, 0); break;
+      case 7: x.a2[0] = x.a2[1] = x.a2[2] = x.a2[3] = d(3, 0), x.b2[0] = d(7, 0), x.b2[1] = d(3, 1), x.b2[2] = d(5, 1); break;
+      case 8: x.a2[0] = x.a2[1] = x.a2[2] = x.a2[3] = d(4, 0), x.b2[0] = d(8, 0), x.b2[1] = d(4, 1), x.b2[2] = d(6, 1); break;
+      case 9:
+        x.av[0] = d(3, 0), x.av[1] = d(4, 0), x.ak = 4;
+        x.b2[0] = d(7, 0), x.b2[1] = d(8, 0), x.b2[2] = d(3, 1), x.b2[3] = d(4, 1), x.bv[0] = d(5, 1), x.bv[1] = d(6, 1);
+        break;
+      case 10: x.a2[0] = x.a2[1] = x.a2[2] = d(9, 0), x.b2[0] = caddr(P, 0); break;
+      case 11: x.a2[0] = x.a2[1] = x.a2[2] = d(10, 0), x.b2[0] = caddr(P, 0); break;
+      case 12: x.a2[0] = d(7, 0), x.a2[1] = d(3, 1), x.a2[2] = d(5, 1), x.b2[0] = caddr(P + 1, 0); break;
+      default: x.a2[0] = d(8, 0), x.a2[1] = d(4, 1), x.a2[2] = d(6, 1), x.b2[0] = caddr(P + 1, 0); break;
+    }
+  } else if (l < 18) {
+    sqr_prod_terms(x.a2, x.b2, f, l + 39, zero);
+  }
+  // outputs
+  if (l < 12) {
+    const uint32_t sp = l >> 1, c = l & 1, m = sp < 3 ? 2 * sp : 2 * (sp - 3) + 1;
+    uint32_t q = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < 6; ++i) {
+      const uint32_t j = (m + 6 - i) % 6;
+      const bool use = i <= j, tw = i + j >= 6;
+      Terms3 tt;
+      if (i < j) {
+        const uint32_t cp = i * (11 - i) / 2 + (j - i - 1);  // cross pair index
+        tt = kara_terms(zs + SD_F2 + 3 * cp, c, tw, zero);
+      } else {  // f_i^2 = (S0, S1), times xi: (S0 - S1, S0 + S1)
+        const LSlot* S = zs + SD_F2 + 45 + 2 * i;
+        tt.t[0] = c ? caddr(S + 1, 0) : caddr(S, 0);
+        tt.t[1] = tw ? (c ? caddr(S, 0) : caddr(S + 1, 1)) : zero;
+        tt.t[2] = zero;
+      }
+#pragma unroll
+      for (uint32_t qq = 0; qq < 4; ++qq)
+        if (use && q == qq) x.o[3 * qq] = tt.t[0], x.o[3 * qq + 1] = tt.t[1], x.o[3 * qq + 2] = tt.t[2];
+      q += use ? 1 : 0;
+    }
+  } else if (l < 24) {
+    const LSlot* R = zs + SD_R2;
+    auto r = [&](uint32_t i, uint32_t neg) { return caddr(R + i, neg); };
+    switch (l - 12) {
+      case 0: x.o[0] = r(0, 0), x.o[1] = r(1, 1); break;                   // X' = 2A (B - F)
+      case 1: x.o[0] = r(2, 0), x.o[1] = r(0, 1), x.o[2] = r(1, 1); break;
+      case 2: x.o[0] = r(3, 0), x.o[1] = r(5, 1); break;                   // Y' = (B + F)^2 - 12 E^2
+      case 3: x.o[0] = r(4, 0), x.o[1] = r(6, 1); break;
+      case 4: x.o[0] = r(7, 0), x.o[1] = r(8, 1); break;                   // Z' = 4 B H
+      case 5: x.o[0] = r(9, 0), x.o[1] = r(7, 1), x.o[2] = r(8, 1); break;
+      case 6: x.o[0] = d(3, 0), x.ov[0] = d(6, 0), x.ov[1] = d(5, 1), x.ok = 12; break;  // B - E
+      case 7: x.o[0] = d(4, 0), x.ov[0] = d(5, 1), x.ov[1] = d(6, 1), x.ok = 12; break;
+      case 8: x.o[0] = r(10, 0); break;                                    // 3 X^2 (-xP)
+      case 9: x.o[0] = r(11, 0); break;
+      case 10: x.o[0] = r(12, 0); break;                                   // H yP
+      default: x.o[0] = r(13, 0); break;
+    }
+  }
+  return x;
+}
+GBV_HD Fp sd_sum4(const CAddr (&u)[4]) {
+  Fp s = cload(u[0]);
+  const Fp s1 = cload(u[1]), s2 = cload(u[2]), s3 = cload(u[3]);
+  fp_acc_lazy(s, s1);
+  fp_acc_lazy(s, s2);
+  fp_acc_lazy(s, s3);
+  return s;  // < 4p
+}
+// unit terms + k (sum of v terms): < 5p, a product operand
+GBV_HD Fp sd_operand(const CAddr (&u)[4], const CAddr (&v)[3], uint32_t k) {
+  Fp w = cload(v[0]);
+  const Fp w1 = cload(v[1]), w2 = cload(v[2]);
+  Fp s = sd_sum4(u);
+  fp_acc_lazy(w, w1);
+  fp_acc_lazy(w, w2);
+  fp_reduce8_ip(w);
+  fp_acc_lazy(s, fp_mul_small(w, k));
+  return s;
+}
+GBV_HD void sd_round1(const SqrDblLane& x) { put(x.dz1, fp_mul_inl(sd_sum4(x.a), sd_sum4(x.b))); }
+GBV_HD void sd_round2(const SqrDblLane& x) { put(x.dz2, fp_mul_inl(sd_operand(x.a2, x.av, x.ak), sd_operand(x.b2, x.bv, x.bk))); }
+GBV_HD void sd_out(const SqrDblLane& x) {
+  Fp v[12];
+  for (int i = 0; i < 12; ++i) v[i] = cload(x.o[i]);
+  Fp w = cload(x.ov[0]);
+  const Fp w1 = cload(x.ov[1]);
+  Fp u = v[0];
+  for (int i = 1; i < 6; ++i) fp_acc_lazy(u, v[i]);
+  fp_reduce8_ip(u);
+  for (int i = 6; i < 12; ++i) fp_acc_lazy(u, v[i]);
+  fp_reduce8_ip(u);  // < 7p
+  fp_acc_lazy(w, w1);
+  fp_reduce8_ip(w);
+  fp_acc_lazy(u, fp_mul_small(w, x.ok));
+  fp_reduce8_ip(u);  // < 2p
+  put(x.dout, u);
+}
+#if defined(GBV_HOST_TEST)
+inline void sqr_dbl(Slot* mem, uint16_t zo, uint16_t fo, uint16_t to, uint16_t po, uint16_t lo, bool sqr) {
+  for (uint32_t l = 0; l < 64; ++l)
+    if (l < 11 || sqr) sd_round1(sqr_dbl_lane(mem, zo, fo, to, po, lo, l));
+  for (uint32_t l = 0; l < 18; ++l)
+    if (l < 14 || sqr) sd_round2(sqr_dbl_lane(mem, zo, fo, to, po, lo, l));
+  for (uint32_t l = 0; l < 24; ++l)
+    if (l >= 12 || sqr) sd_out(sqr_dbl_lane(mem, zo, fo, to, po, lo, l));
+}
+#else
+__device__ __forceinline__ void sqr_dbl_run(const SqrDblLane& x, bool sqr) {
+  const uint32_t l = lane_id();
+  if (l < 11 || sqr) sd_round1(x);
+  barrier();
+  if (l < 14 || (sqr && l < 18)) sd_round2(x);
+  barrier();
+  if ((l >= 12 && l < 24) || (sqr && l < 12)) sd_out(x);
   barrier();
 }
 #endif
@@ -655,18 +871,19 @@ GBV_HD void miller_load_pair(Slot* mem, int j, const G1A& P, const G2A& Q) {
 GBV_HD void miller_loop(Slot* mem, int npairs) {
 #if defined(GBV_HOST_TEST)
   auto mline = [&]() { mul_line(mem, M_Z, M_F, M_L, M_F); };
+  auto sqdbl = [&](int j) { sqr_dbl(mem, M_Z, M_F, M_PAIR + 12 * j, M_PAIR + 12 * j + 10, M_L, j == 0); };
 #else
-  const LineLane lx = line_lane(mem, M_Z, M_F, M_L, M_F, lane_id());  // f = f l, resolved once
+  // every lane's terms resolved once: f = f l, and per pair the bit's doubling (with f^2 for pair 0)
+  const LineLane lx = line_lane(mem, M_Z, M_F, M_L, M_F, lane_id());
+  const SqrDblLane d0 = sqr_dbl_lane(mem, M_Z, M_F, M_PAIR, M_PAIR + 10, M_L, lane_id());
+  const SqrDblLane d1 = sqr_dbl_lane(mem, M_Z, M_F, M_PAIR + 12, M_PAIR + 22, M_L, lane_id());
   auto mline = [&]() { mul_line_lane(lx); };
+  auto sqdbl = [&](int j) { sqr_dbl_run(j == 0 ? d0 : d1, j == 0); };
 #endif
   set_one12(mem + M_F);
   for (int i = 62; i >= 0; --i) {
     for (int j = 0; j < npairs; ++j) {
-      uint16_t t = M_PAIR + 12 * j;
-      if (j == 0 && i != 62)  // f^2 and pair 0's doubling step are independent: one program
-        run_hot(MILLER_SQR_DBL, make_ws(mem, M_Z, M_F, t, (uint16_t)(t + 10), M_F, t, M_L));
-      else
-        run(G2_DBL_STEP, make_ws(mem, M_Z, t, (uint16_t)(t + 10), t, M_L));
+      sqdbl(j);  // f^2 (pair 0, f = 1 on the first bit) and pair j's doubling step with its line
       mline();
     }
     if ((X_ABS >> i) & 1ull) {
