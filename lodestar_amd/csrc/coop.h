@@ -346,9 +346,6 @@ __device__ __forceinline__ void run_body(const Prog* PP, uint32_t b0, uint32_t b
 // One out-of-line copy of the interpreter serves every call site (the drivers make hundreds).
 __device__ __noinline__ void run_ni(const Prog* PP, uint32_t b0, uint32_t b1, uint32_t b2, uint32_t b3) { run_body(PP, b0, b1, b2, b3); }
 __device__ inline void run(const Prog& P, const Ws& w) { run_ni(&P, w.b[0], w.b[1], w.b[2], w.b[3]); }
-// The interpreter inlined at one call site and specialised for its program (the program's counts
-// fold into the code; no call, no callee-saved spills): for the program a hot loop runs tens of times.
-__device__ __forceinline__ void run_inl(const Prog& P, const Ws& w) { run_body(&P, w.b[0], w.b[1], w.b[2], w.b[3]); }
 
 #define COOP_LANES(l) for (unsigned l = threadIdx.x & 63u; l == (threadIdx.x & 63u); l = ~0u)
 #define COOP_LANE0 if ((threadIdx.x & 63u) == 0)
@@ -398,20 +395,6 @@ GBV_HD Ws ws2(Slot* mem, uint16_t z, uint16_t a, uint16_t b) { return make_ws(me
 GBV_HD Ws ws3(Slot* mem, uint16_t z, uint16_t a, uint16_t b, uint16_t c) { return make_ws(mem, z, a, b, c); }
 
 GBV_HD void mul12(Slot* mem, uint16_t z, uint16_t a, uint16_t b, uint16_t c) { run(FP12_MUL, ws3(mem, z, a, b, c)); }
-#ifndef GBV_COOP_INLINE_LOOPS
-#define GBV_COOP_INLINE_LOOPS 1  // the Miller loop's per-bit programs and the [|x|] doublings too
-#endif
-// a program called from a 63-step loop: inlined (GBV_COOP_INLINE_LOOPS) or the shared interpreter
-#if defined(GBV_HOST_TEST)
-#define run_hot run
-#else
-GBV_HD void run_hot(const Prog& P, const Ws& w) {
-  if (GBV_COOP_INLINE_LOOPS)
-    run_inl(P, w);
-  else
-    run(P, w);
-}
-#endif
 GBV_HD void frob12(Slot* mem, uint16_t z, int n, uint16_t a, uint16_t c) { run(n == 1 ? FP12_FROB1 : FP12_FROB2, ws2(mem, z, a, c)); }
 
 // ---- written-out programs: lane descriptors resolved once, no records -------------------------
@@ -897,6 +880,22 @@ GBV_HD void miller_loop(Slot* mem, int npairs) {
   conj12(mem + M_F);
 }
 
+// T (at M_PAIR) = 4 [2]T by the written-out doubling step (its line, through the P slots M_PAIR + 10,
+// lands in M_L and is ignored; f is not touched).  The lane terms are resolved once per ladder.
+#if defined(GBV_HOST_TEST)
+struct DblPt {
+  Slot* mem;
+  void operator()() const { sqr_dbl(mem, M_Z, M_F, M_PAIR, M_PAIR + 10, M_L, false); }
+};
+inline DblPt dbl_point(Slot* mem) { return DblPt{mem}; }
+#else
+struct DblPt {
+  SqrDblLane x;
+  __device__ void operator()() const { sqr_dbl_run(x, false); }
+};
+__device__ inline DblPt dbl_point(Slot* mem) { return DblPt{sqr_dbl_lane(mem, M_Z, M_F, M_PAIR, M_PAIR + 10, M_L, lane_id())}; }
+#endif
+
 // [|x|] Q (Q affine, not infinity) by the Miller loop's point steps alone (the lines they also
 // write to M_L are ignored): T ends at mem + M_PAIR in homogeneous projective coordinates
 // (x = X/Z, y = Y/Z).  The mixed addition is incomplete only for T = +-Q, i.e. for Q of order
@@ -905,8 +904,9 @@ GBV_HD void miller_loop(Slot* mem, int npairs) {
 GBV_HD void mul_xabs_point(Slot* mem, const G2A& Q) {
   miller_load_pair(mem, 0, G1A{fp_zero(), fp_zero()}, Q);
   const uint16_t t = M_PAIR;
+  const DblPt dbl = dbl_point(mem);
   for (int i = 62; i >= 0; --i) {
-    run_hot(G2_DBL_PT, make_ws(mem, M_Z, t, t));  // the doubling without its line: 19 products, 6 outputs
+    dbl();
     if ((X_ABS >> i) & 1ull) run(G2_ADD_STEP, make_ws(mem, M_Z, t, (uint16_t)(t + 6), (uint16_t)(t + 10), t, M_L));
   }
 }
@@ -943,8 +943,9 @@ GBV_HD void mul_2d_point(Slot* mem, const G2A& Q, const G2A& E, uint32_t sa, uin
   barrier();
   // T = +-Q (digit 31 of sa) is loaded; its E digit, then the 31 lower steps
   run(G2_ADD_STEP, make_ws(mem, M_Z, t, ((sb >> 31) & 1u) ? EP : EN, (uint16_t)(t + 10), t, M_L));
+  const DblPt dbl = dbl_point(mem);
   for (int i = 30; i >= 0; --i) {
-    run_hot(G2_DBL_PT, make_ws(mem, M_Z, t, t));
+    dbl();
     run(G2_ADD_STEP, make_ws(mem, M_Z, t, ((sa >> i) & 1u) ? QP : QN, (uint16_t)(t + 10), t, M_L));
     run(G2_ADD_STEP, make_ws(mem, M_Z, t, ((sb >> i) & 1u) ? EP : EN, (uint16_t)(t + 10), t, M_L));
   }

@@ -119,7 +119,7 @@ int ht_coop_pairing(uint8_t* out, const uint8_t* p96, const uint8_t* q192, int n
   return ok;
 }
 // clear_cofactor_g2 with both [|x|] multiplications by the cooperative point steps
-// (coop::mul_xabs_point, as k_hash_clear_coop runs it); in: affine point of E2, out: affine
+// (coop::mul_xabs_point on the written-out doubling; the device clears on lane quads, k_hash_clear_quad); in: affine point of E2, out: affine
 void ht_coop_clear_cofactor(uint8_t* out, const uint8_t* xy) {
   coop::load_consts();
   std::vector<coop::Slot> mem(coop::MILLER_WS);

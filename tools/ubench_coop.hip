@@ -57,6 +57,15 @@ __global__ void __launch_bounds__(64) k_coop_fe(Fp* out, int iters) {
   if (threadIdx.x == 0) out[0].v[0] += ok;
 }
 
+// one wave: [|x|] Q by the cooperative point steps (the cofactor clearing's chain)
+__global__ void __launch_bounds__(64) k_coop_xabs(Fp* out, int iters) {
+  __shared__ coop::Slot ws[coop::MILLER_WS];
+  coop::load_consts();
+  G2A Q{Fp2{FP_ONE, FP_ONE}, Fp2{FP_B1, FP_ONE}};
+  for (int i = 0; i < iters; ++i) coop::mul_xabs_point(ws, Q);
+  if (threadIdx.x < 12) out[blockIdx.x * 12 + threadIdx.x] = coop::get(ws + coop::M_PAIR + threadIdx.x);
+}
+
 // one wave, one lane: dependent Fp products (latency of the thread-level primitive)
 __global__ void __launch_bounds__(64) k_fp_mul_lat(Fp* out, int iters) {
   Fp a = FP_ONE, b = FP_ONE;
@@ -156,6 +165,7 @@ int main() {
   run("coop cyc hand", k_coop_cyc_hand, out, 1, 200, 18);
   run("coop FE", k_coop_fe, out, 1, 3, 8400);
   run("coop miller1", k_coop_miller, out, 1, 5, 6200);
+  run("coop xabs", k_coop_xabs, out, 1, 5, 2000);
   run("coop ML1+FE", k_coop_pairing, out, 1, 3, 14600);
   run("fp12_inv lane", k_lane0_fp12_inv, out, 1, 5, 500);
   run("fp_inv lane", k_lane0_fp_inv, out, 1, 5, 460);
