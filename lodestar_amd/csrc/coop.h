@@ -394,7 +394,6 @@ GBV_HD bool is_one12(const Slot* fg) {
 GBV_HD Ws ws2(Slot* mem, uint16_t z, uint16_t a, uint16_t b) { return make_ws(mem, z, a, b); }
 GBV_HD Ws ws3(Slot* mem, uint16_t z, uint16_t a, uint16_t b, uint16_t c) { return make_ws(mem, z, a, b, c); }
 
-GBV_HD void mul12(Slot* mem, uint16_t z, uint16_t a, uint16_t b, uint16_t c) { run(FP12_MUL, ws3(mem, z, a, b, c)); }
 GBV_HD void frob12(Slot* mem, uint16_t z, int n, uint16_t a, uint16_t c) { run(n == 1 ? FP12_FROB1 : FP12_FROB2, ws2(mem, z, a, c)); }
 
 // ---- written-out programs: lane descriptors resolved once, no records -------------------------
@@ -713,6 +712,82 @@ __device__ __forceinline__ void sqr_dbl_run(const SqrDblLane& x, bool sqr) {
 }
 #endif
 
+// General Fp12 product c = f g, schoolbook over Fp2[w]/(w^6 - xi): the w^m coefficient sums f_i
+// g_(m-i) (xi where i > m), 36 Karatsuba Fp2 products = 108 Fp products, two per lane on 54 lanes (the
+// two independent), then 12 output lanes of <= 18 unit terms.  Against the interpreted FP12_MUL
+// (Karatsuba at every level: 54 products, partial sums, long outputs) one product more per lane and no
+// partial-sum phase.  Z: product 3 (6 i + j) + r (r: P0 P1 P2 of f_i g_j) at Z + 0 .. 107.
+struct MulLane {
+  CAddr a[2][2], b[2][2];  // product lane (l < 54): two products, two terms per operand
+  CAddr o[18];             // output lane (l < 12)
+  LSlot *dz0, *dz1, *dout;
+};
+GBV_HD MulLane mul_lane(Slot* memg, uint16_t zo, uint16_t ao, uint16_t bo, uint16_t co, uint32_t l) {
+  LSlot* mem = GBV_LDS(memg);
+  const LSlot *f = mem + ao, *g = mem + bo, *zs = mem + zo;
+  const CAddr zero = caddr(GBV_CONSTS_LDS, 0);
+  MulLane x;
+#pragma unroll
+  for (uint32_t h = 0; h < 2; ++h) {
+    const uint32_t P = l + 54 * h, t = P / 3, r = P - 3 * t, i = t / 6, j = t - 6 * i;
+    const LSlot* F = f + (i & 1 ? i + 5 : i);
+    const LSlot* G = g + (j & 1 ? j + 5 : j);
+    x.a[h][0] = caddr(F + (r == 1 ? 1 : 0), 0);
+    x.a[h][1] = r == 2 ? caddr(F + 1, 0) : zero;
+    x.b[h][0] = caddr(G + (r == 1 ? 1 : 0), 0);
+    x.b[h][1] = r == 2 ? caddr(G + 1, 0) : zero;
+  }
+  x.dz0 = mem + zo + (l < 54 ? l : 0);
+  x.dz1 = mem + zo + (l < 54 ? l + 54 : 0);
+  x.dout = mem + co + (l < 12 ? l : 0);
+  const uint32_t sp = (l < 12 ? l : 0) >> 1, c = l & 1, m = sp < 3 ? 2 * sp : 2 * (sp - 3) + 1;
+#pragma unroll
+  for (uint32_t i = 0; i < 6; ++i) {
+    const uint32_t j = (m + 6 - i) % 6;
+    const Terms3 t = kara_terms(zs + 3 * (6 * i + j), c, i > m, zero);
+    x.o[3 * i] = t.t[0], x.o[3 * i + 1] = t.t[1], x.o[3 * i + 2] = t.t[2];
+  }
+  return x;
+}
+GBV_HD void mul_prod(const MulLane& x) {
+  Fp a0 = cload(x.a[0][0]), b0 = cload(x.b[0][0]), a1 = cload(x.a[1][0]), b1 = cload(x.b[1][0]);
+  const Fp a01 = cload(x.a[0][1]), b01 = cload(x.b[0][1]), a11 = cload(x.a[1][1]), b11 = cload(x.b[1][1]);
+  fp_acc_lazy(a0, a01);
+  fp_acc_lazy(b0, b01);
+  fp_acc_lazy(a1, a11);
+  fp_acc_lazy(b1, b11);
+  put(x.dz0, fp_mul_inl(a0, b0));
+  put(x.dz1, fp_mul_inl(a1, b1));
+}
+GBV_HD void mul_out(const MulLane& x) {
+  Fp v[18];
+  for (int i = 0; i < 18; ++i) v[i] = cload(x.o[i]);
+  Fp u = v[0];
+  for (int i = 1; i < 6; ++i) fp_acc_lazy(u, v[i]);
+  fp_reduce8_ip(u);
+  for (int i = 6; i < 12; ++i) fp_acc_lazy(u, v[i]);
+  fp_reduce8_ip(u);  // < 7p
+  for (int i = 12; i < 18; ++i) fp_acc_lazy(u, v[i]);
+  fp_reduce8_ip(u);
+  put(x.dout, u);
+}
+#if defined(GBV_HOST_TEST)
+inline void mul12(Slot* mem, uint16_t z, uint16_t a, uint16_t b, uint16_t c) {
+  for (uint32_t l = 0; l < 54; ++l) mul_prod(mul_lane(mem, z, a, b, c, l));
+  for (uint32_t l = 0; l < 12; ++l) mul_out(mul_lane(mem, z, a, b, c, l));
+}
+#else
+__device__ __forceinline__ void mul12_lane(const MulLane& x) {
+  const uint32_t l = lane_id();
+  if (l < 54) mul_prod(x);
+  barrier();
+  if (l < 12) mul_out(x);
+  barrier();
+}
+// c = a b (c may be a or b)
+__device__ inline void mul12(Slot* mem, uint16_t z, uint16_t a, uint16_t b, uint16_t c) { mul12_lane(mul_lane(mem, z, a, b, c, lane_id())); }
+#endif
+
 // ---- cyclotomic squaring written out (the exponentiations' ~315 squarings) --------------------
 // Granger-Scott: f in the cyclotomic subgroup as three Fp4 pairs (z0, z1), (z2, z3), (z4, z5) --
 // slots (0 1 | 8 9), (6 7 | 4 5), (2 3 | 10 11) -- each pair's t0 = a^2 + xi b^2,
@@ -974,9 +1049,10 @@ GBV_HD void exp_x(Slot* mem, uint16_t a, uint16_t r) {
   }
 #else
   const CycLane x = cyc_lane(mem, E_Z, r, r, lane_id());
+  const MulLane y = mul_lane(mem, E_Z, r, a, r, lane_id());
   for (int i = 62; i >= 0; --i) {
     cyc_sqr_lane(x);
-    if ((X_ABS >> i) & 1ull) mul12(mem, E_Z, r, a, r);
+    if ((X_ABS >> i) & 1ull) mul12_lane(y);
   }
 #endif
   conj12(mem + r);

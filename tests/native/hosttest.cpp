@@ -118,6 +118,30 @@ int ht_coop_pairing(uint8_t* out, const uint8_t* p96, const uint8_t* q192, int n
   for (int i = 0; i < 12; ++i) store_canon(out + 48 * i, coop::get(fe + coop::E_C + i));
   return ok;
 }
+// The written-out cooperative Fp12 steps (coop.h) on one workspace, lanes in sequence: out = 4 Fp12
+// (12 canonical BE Fp each, slot order): mul12(f, g), cyc_sqr(fc) (fc in the cyclotomic subgroup),
+// inv12(f), mul_line(f, l) (l: c0, c2, c3 as 6 Fp)
+void ht_coop_f12_ops(uint8_t* out, const uint8_t* f, const uint8_t* g, const uint8_t* fc, const uint8_t* l) {
+  coop::load_consts();
+  std::vector<coop::Slot> mem(coop::FINAL_EXP_WS);
+  coop::Slot* w = mem.data();
+  for (int i = 0; i < 12; ++i) {
+    coop::put(w + coop::E_F + i, load_mont(f + 48 * i));
+    coop::put(w + coop::E_TMP + i, load_mont(g + 48 * i));
+    coop::put(w + coop::E_T + i, load_mont(fc + 48 * i));
+  }
+  for (int i = 0; i < 6; ++i) coop::put(w + coop::E_A + i, load_mont(l + 48 * i));
+  coop::mul12(w, coop::E_Z, coop::E_F, coop::E_TMP, coop::E_B);
+  coop::cyc_sqr(w, coop::E_Z, coop::E_T, coop::E_C);
+  coop::mul_line(w, coop::E_Z, coop::E_F, coop::E_A, coop::E_TMP2);
+  for (int i = 0; i < 12; ++i) {
+    store_canon(out + 48 * i, coop::get(w + coop::E_B + i));
+    store_canon(out + 576 + 48 * i, coop::get(w + coop::E_C + i));
+    store_canon(out + 1728 + 48 * i, coop::get(w + coop::E_TMP2 + i));
+  }
+  coop::inv12(w);
+  for (int i = 0; i < 12; ++i) store_canon(out + 1152 + 48 * i, coop::get(w + coop::E_INV + i));
+}
 // clear_cofactor_g2 with both [|x|] multiplications by the cooperative point steps
 // (coop::mul_xabs_point on the written-out doubling; the device clears on lane quads, k_hash_clear_quad); in: affine point of E2, out: affine
 void ht_coop_clear_cofactor(uint8_t* out, const uint8_t* xy) {

@@ -223,6 +223,37 @@ def test_coop_pairing_value(lib):
     assert got == flat
 
 
+def test_coop_written_out_f12_steps(lib):
+    """coop.h's written-out steps against the oracle on random operands: mul12 (the 108-product
+    schoolbook form), cyc_sqr (Granger-Scott, on a cyclotomic element), inv12 (norms to Fp2),
+    mul_line (f times c0 + c2 w^2 + c3 w^3)."""
+    rng = random.Random(12)
+
+    def rf12():
+        return tuple(tuple((rng.randrange(o.P), rng.randrange(o.P)) for _ in range(3)) for _ in range(2))
+
+    def flat(e):
+        return b"".join(fp2b(c) for c in (e[0][0], e[0][1], e[0][2], e[1][0], e[1][1], e[1][2]))
+
+    def unflat(b):
+        c = [b2fp2(b[96 * i:96 * i + 96]) for i in range(6)]
+        return ((c[0], c[1], c[2]), (c[3], c[4], c[5]))
+
+    for _ in range(3):
+        f, g = rf12(), rf12()
+        t = o.f12_mul(o.f12_conj(f), o.f12_inv(f))
+        fc = o.f12_mul(o.f12_frob_n(t, 2), t)  # f^((p^6 - 1)(p^2 + 1)): cyclotomic
+        c0, c2, c3 = [(rng.randrange(o.P), rng.randrange(o.P)) for _ in range(3)]
+        line = ((c0, c2, o.F2_ZERO), (o.F2_ZERO, c3, o.F2_ZERO))
+        out = buf(4 * 576)
+        lib.ht_coop_f12_ops(out, flat(f), flat(g), flat(fc), fp2b(c0) + fp2b(c2) + fp2b(c3))
+        r = out.raw
+        assert unflat(r[:576]) == o.f12_mul(f, g)
+        assert unflat(r[576:1152]) == o.f12_sqr(fc)
+        assert unflat(r[1152:1728]) == o.f12_inv(f)
+        assert unflat(r[1728:]) == o.f12_mul(f, line)
+
+
 def test_coop_two_pair_check(lib):
     sk = o.interop_secret_key(5)
     msg = bytes(range(1, 33))
