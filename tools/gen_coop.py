@@ -14,6 +14,12 @@ Fp2/Fp6/Fp12, Granger-Scott cyclotomic squaring, sparse line multiplication, hom
 projective doubling/addition steps with line coefficients, Frobenius), executed symbolically.
 tests/test_coop_tables.py re-executes every program in Python against the oracle.
 
+Round 4 wrote the hottest of these out as fixed code in coop.h (cyc_sqr, mul_line, sqr_dbl, mul12:
+lane terms resolved once, no records, no partial-sum phase); FP12_CYC_SQR, FP12_MUL_LINE,
+MILLER_SQR_DBL, G2_DBL_STEP, G2_DBL_PT and FP12_MUL stay here as the specification of the same maps
+(the written-out forms follow dbl_step_into's scaling exactly).  The device still interprets the
+Frobenius maps and G2_ADD_STEP.
+
 Program encoding (all indices small; emitted as fixed-size per-lane u32 records -- a product is a
 header (term counts) + up to 10 A terms + up to 10 B terms, a partial sum / output a header + up to
 7 terms; within a linear form the coefficient +1 terms come first, then the -1 terms (the sign of a
