@@ -681,7 +681,7 @@ int gbv_sm_batch_submit(gbv_ctx* c, gbv_sm_batch* b) {
 // throughput-bound k_sm_prepare of batch k+1):
 //   stream H      : k_hash_msgs
 //   stream A      : k_sm_prepare(segment s)  -- throughput-bound, also forms per-wave chunk sums
-//   streams B0/B1 : (segment s alternates) wait(prepare s, hash) k_sm_chunk_finish, k_sm_miller,
+//   streams B0/B1 : (segment s alternates) wait(prepare s) k_sm_chunk_finish, wait(hash) k_sm_miller,
 //                   k_seg_reduce_quad + k_sm_seg_check, k_sm_group_pairing (exits at once unless
 //                   the segment check failed)
 //   stream B0     : wait(all) k_sm_fallback (per-set retry of failed chunks only), copy-out
@@ -772,7 +772,7 @@ static int sm_submit_enqueue(gbv_ctx* c, gbv_sm_batch* b) {
     // the tail stream.
     hipStream_t scf = msm ? sa : sb;
     if (scf != sa) HIP_CHECK(c, hipStreamWaitEvent(scf, e[1], 0));
-    HIP_CHECK(c, hipStreamWaitEvent(scf, ev[1], 0));
+    HIP_CHECK(c, hipStreamWaitEvent(scf, ev[0], 0));  // n_fallback zeroed (the memsets ahead of the hash)
     HIP_CHECK(c, hipEventRecord(e[2], scf));
     launch_sm_chunk_finish(LaunchCfg{0, 64, scf}, g0, G, s0, b->grp_off, b->status, Sh, b->rP, b->PgJ, b->SgJ, b->grp_state,
                            b->n_fallback);
@@ -786,6 +786,9 @@ static int sm_submit_enqueue(gbv_ctx* c, gbv_sm_batch* b) {
                             b->msm_cur[s & 1], b->msm_ent + 4ull * s0, b->msm_buckets[s & 1], b->msm_head[s & 1], b->msm_tail[s & 1]);
     HIP_CHECK(c, hipEventRecord(e[11], smsm));
     if (msm) HIP_CHECK(c, hipStreamWaitEvent(sb, e[3], 0));
+    // the hash: the chunk sums above read none of it (a lone call's sums run beside the hash), the
+    // Miller values and checks below read H
+    HIP_CHECK(c, hipStreamWaitEvent(sb, ev[1], 0));
     HIP_CHECK(c, hipEventRecord(e[4], sb));
     if (!b->seg_direct[s]) launch_sm_miller(LaunchCfg{0, 64, sb}, g0, G, b->grp_msg, b->grp_state, b->PgJ, b->H, b->F);
     HIP_CHECK(c, hipEventRecord(e[5], sb));
