@@ -1166,6 +1166,7 @@ void tuning_load() {
     };
     rd("GBV_HASH_PAIR_MAX", g_tuning.hash_pair_max);
     rd("GBV_HASH_QUAD_MAX", g_tuning.hash_quad_max);
+    rd("GBV_HASH_COOP_MAX", g_tuning.hash_coop_max);
     rd("GBV_VS_SIG_QUAD_MAX", g_tuning.vs_sig_quad_max);
     rd("GBV_PREPARE_SPLIT_MAX", g_tuning.prepare_split_max);
     rd("GBV_CHUNK_FINISH_WAVE_MAX", g_tuning.chunk_finish_wave_max);

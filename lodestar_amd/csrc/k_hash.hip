@@ -74,6 +74,12 @@ __global__ void GBV_KERNEL_ATTR k_util_g2_out(uint32_t n, const G2A* __restrict_
 
 
 void launch_hash_msgs(LaunchCfg c, const uint8_t* msgs32, uint32_t n, G2A* H, G2J* Qpre) {
+  if (Qpre && n <= tuning().hash_coop_max) {  // latency: lane-pair maps, then the cofactor clearing one workgroup per message
+    hipLaunchKernelGGL(k_hash_msgs_pre, dim3((2 * n + 63) / 64), dim3(64), 0, c.stream, msgs32, n, Qpre);
+    debug_sync(c.stream, "k_hash_msgs_pre");
+    launch_hash_clear_coop(c.stream, n, Qpre, H);
+    return;
+  }
   if (Qpre && n <= tuning().hash_quad_max) {  // latency: maps on lane pairs, the cofactor clearing on lane quads
     hipLaunchKernelGGL(k_hash_msgs_pre, dim3((2 * n + 63) / 64), dim3(64), 0, c.stream, msgs32, n, Qpre);
     debug_sync(c.stream, "k_hash_msgs_pre");

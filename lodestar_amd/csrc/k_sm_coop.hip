@@ -710,4 +710,60 @@ void launch_vs_chunk_coop(LaunchCfg c, uint32_t C, const uint32_t* chunk_be, con
     hipLaunchKernelGGL(k_vs_chunk_coop<false>, dim3(C), dim3(64), 0, c.stream, chunk_be, status, f, rS, chunk_valid, Fs, fs_flag);
   debug_sync(c.stream, "k_vs_chunk_coop");
 }
+// hash_to_G2's cofactor clearing for few messages (launch_hash_msgs' latency form, n <= GBV_HASH_COOP_MAX):
+// h_eff P = [x^2 - x - 1] P + [x - 1] psi(P) + psi^2(2P) as quad_g2.h g2_clear_cofactor, with both
+// [|x|] multiplications on wave 0's written-out cooperative point steps (coop::mul_xabs_point, ~0.42 ms a
+// chain against ~0.85 ms on a lane quad) and the rest -- affine forms, psi maps, additions -- on one lane
+// quad of each wave (wave 1's quad forms psi(P) and psi^2(2P) - psi(P) - P beside chain 1).
+__global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(1)))
+k_hash_clear_coop(const G2J* __restrict__ Qpre, G2A* __restrict__ H) {
+  __shared__ coop::Slot ws[coop::MILLER_WS];
+  __shared__ G2A sa;
+  __shared__ G2J s_t1, s_psi, s_u;
+  __shared__ int ok, ok2;
+  const uint32_t m = blockIdx.x;
+  const unsigned lane = threadIdx.x & 63u, wv = threadIdx.x >> 6, q = lane & 3u;
+  const G2J p = Qpre[m];
+  if (wv == 0) {
+    coop::load_consts();
+    if (lane < 4) {
+      G2A a;
+      const bool okp = quad::g2_to_aff(a, p, q);
+      if (q == 0) sa = a, ok = okp ? 1 : 0;
+    }
+    coop::barrier();
+    if (ok) coop::mul_xabs_point(ws, sa);
+  } else if (lane < 4) {
+    const G2J psi = quad::g2_psi(p, q);
+    G2J u = quad_g2_add(quad::g2_psi(quad::g2_psi(quad::g2_dbl(p, q), q), q), jac_neg(psi), q);
+    u = quad_g2_add(u, jac_neg(p), q);
+    if (q == 0) s_psi = psi, s_u = u;
+  }
+  __syncthreads();  // [|x|] P in ws; psi(P), u in LDS
+  if (wv == 0 && lane < 4 && ok) {
+    const G2J t1 = jac_neg(coop::point_jac(ws));  // [x] P
+    G2A a;
+    const bool o2 = quad::g2_to_aff(a, quad_g2_add(t1, s_psi, q), q);  // t2 = [x] P + psi(P)
+    if (q == 0) s_t1 = t1, sa = a, ok2 = o2 ? 1 : 0;
+  }
+  __syncthreads();
+  if (wv == 0) {
+    if (ok && ok2) coop::mul_xabs_point(ws, sa);
+  } else if (lane < 4 && ok) {
+    const G2J u = quad_g2_add(s_u, jac_neg(s_t1), q);  // u - [x] P
+    if (q == 0) s_u = u;
+  }
+  __syncthreads();  // [|x|] t2 in ws; u - [x] P in LDS
+  if (wv == 0 && lane < 4) {
+    // P at infinity clears to infinity; t2 at infinity: [x] t2 is infinity too
+    const G2J r = !ok ? quad::g2_clear_cofactor(p, q) : ok2 ? quad_g2_add(jac_neg(coop::point_jac(ws)), s_u, q) : s_u;
+    G2A a;
+    quad::g2_to_aff(a, r, q);
+    if (q == 0) H[m] = a;
+  }
+}
+void launch_hash_clear_coop(hipStream_t s, uint32_t n, const G2J* Qpre, G2A* H) {
+  hipLaunchKernelGGL(k_hash_clear_coop, dim3(n), dim3(128), 0, s, Qpre, H);
+  debug_sync(s, "k_hash_clear_coop");
+}
 }  // namespace gbv

@@ -70,6 +70,7 @@ constexpr uint32_t HASH_PAIR_MAX = 4096;
 struct Tuning {
   uint32_t hash_pair_max = HASH_PAIR_MAX;  // GBV_HASH_PAIR_MAX: hash on lane pairs up to this many messages
   uint32_t hash_quad_max = 16384;          // GBV_HASH_QUAD_MAX: hash on lane quads up to this many messages
+  uint32_t hash_coop_max = 128;            // GBV_HASH_COOP_MAX: latency form, cofactor clearing one workgroup per message (two waves each: past ~128 messages they crowd the signature work beside them)
   uint32_t prepare_split_max = 2048;       // GBV_PREPARE_SPLIT_MAX: same-message latency prepare up to this many sets
   uint32_t chunk_finish_wave_max = 32;     // GBV_CHUNK_FINISH_WAVE_MAX: chunk sums one wave per chunk up to this many
   uint32_t vs_pre_max = 16384;             // GBV_VS_PRE_MAX: verifySignatureSets signature half beside the aggregation

@@ -9,8 +9,10 @@ namespace gbv {
 struct Seed;
 struct LaunchCfg { unsigned blocks; unsigned threads; hipStream_t stream; };
 
-// Qpre (optional, n entries): Q0 + Q1 of the lane-pair maps ahead of the lane-quad cofactor clearing (k_hash_clear_quad)
+// Qpre (optional, n entries): Q0 + Q1 of the lane-pair maps ahead of the latency forms of the cofactor
+// clearing (k_hash_clear_coop: one workgroup per message, n <= GBV_HASH_COOP_MAX; k_hash_clear_quad)
 void launch_hash_msgs(LaunchCfg c, const uint8_t* msgs32, uint32_t n, G2A* H, G2J* Qpre = nullptr);
+void launch_hash_clear_coop(hipStream_t s, uint32_t n, const G2J* Qpre, G2A* H);
 void launch_util_g2_out(LaunchCfg c, uint32_t n, const G2A* H, uint8_t* out192);
 
 // Signature.fromBytes decoding of sets [base, base + n): S[i] = the point, status[i] = GBV_PT_* (k_dec.hip)
