@@ -58,6 +58,11 @@ FME_RANDOMIZE_PAIR_JAC = 2096  # the same with P Jacobian (aggregate pubkeys str
 FME_HASH_TO_G2 = 4808       # RFC 9380 hash_to_G2 (SSWU with one norm exponentiation per map + 3-isogeny + h_eff + to affine)
 FME_MILLER_1J = 7244        # Miller value of one pair, Jacobian P
 FME_G1_SCAN = 48            # 3-level 8-lane chunk scan of r_i pk_i (3 Jacobian G1 additions)
+FME_G2_DECODE = 941         # G2 decompression alone (k_sig_decode, k_vs_sig_decode)
+FME_G2_SUBGROUP = FME_SIG_VALIDATE - FME_G2_DECODE  # the psi-based G2 subgroup check (1170)
+FME_RANDOMIZE_G2 = 1491     # r_i sig_i alone (randomize_g2: endomorphism-split ladder + affine tables)
+FME_HASH_MAPS = 2097        # hash_to_G2's two SSWU maps + isogenies + Q0 + Q1 (k_hash_msgs_pre)
+FME_HASH_CLEAR = 2711       # hash_to_G2's cofactor clearing + affine form (k_hash_clear_quad / _coop)
 # k_sm_prepare<false> (bench: G2 sum by bucket MSM) and <true> (per-set G2 ladders)
 W_PREPARE_FME_MSM = FME_SIG_VALIDATE + FME_RANDOMIZE_G1 + FME_G1_SCAN
 W_PREPARE_FME_MSM_COMB = FME_SIG_VALIDATE + FME_COMB_G1 + FME_G1_SCAN
@@ -90,50 +95,48 @@ FME_FINAL_EXP = 7709
 VS_ALG_BYTES = {"hash_sig": 32 + 96 + 8 + 4 + 128 + 1 + 256 + 192 + 384 + 1, "miller": 192 + 256 + 1 + 768}
 
 
-def pmc_evidence(units_per_launch, kernel="k_sm_prepare<false>", alg_bytes=ALG_BYTES_PER_SET, threads_per_unit=1, exact=False):
-    """HBM traffic per launch and VALU issue utilisation of a kernel (default k_sm_prepare) from the
-    committed rocprofv3 --pmc summary (separate passes; FETCH_SIZE doubled per the gfx950 calibration
-    in the MI355X guide: it counts 64 B per 128-B request; rocprofv3 reports kilobytes).
-    threads_per_unit: lanes per unit of work (2 for the lane-pair Miller kernel); exact: no fallback
-    to k_sm_prepare when the summary lacks the kernel."""
+def _pmc_summary():
     try:
-        summary = json.load(open(PMC_SUMMARY))
-        d = summary.get(kernel) or (None if exact else summary["k_sm_prepare"])
-    except (OSError, KeyError, ValueError):
-        return None, None
-    if d is None or "FETCH_SIZE" not in d or "WRITE_SIZE" not in d:
-        return None, None
-    per_set = (2 * d["FETCH_SIZE"] + d["WRITE_SIZE"]) * 1024.0 * threads_per_unit / d["grid_size"]
-    valu = d["SQ_INSTS_VALU"] / (d["duration_ms"] * 1e-3 * PEAK_VALU_WAVE_INSTR_PER_S) if "SQ_INSTS_VALU" in d else None
-    ev = {"source": os.path.relpath(PMC_SUMMARY, ROOT), "kernel": kernel if kernel in summary else "k_sm_prepare",
-          "pmc_grid_sets": int(d["grid_size"] // threads_per_unit),
-          "hbm_bytes_per_set": round(per_set, 1), "algorithmic_bytes_per_set": alg_bytes, "valu_wave_instr_per_set": round(d["SQ_INSTS_VALU"] / d["SQ_WAVES"]) if "SQ_WAVES" in d else None,
-          "valu_issue_utilisation": None if valu is None else round(valu, 4),
-          "valu_lane_utilisation": round(d["SQ_THREAD_CYCLES_VALU"] / (64.0 * d["SQ_ACTIVE_INST_VALU"]), 4) if "SQ_ACTIVE_INST_VALU" in d else None}
-    return per_set * units_per_launch, ev
-
-
-def pmc_stage_evidence(units_per_launch, kernels, alg_bytes):
-    """pmc_evidence for a stage of several kernels run back to back on one stream (the same-message
-    prepare stage: k_sig_decode then k_sm_prepare<false, true>): HBM bytes and VALU instructions per
-    set summed over the kernels, issue utilisation over their summed durations.  Falls back to the
-    single-kernel form (older summaries: one k_sm_prepare<false>)."""
-    try:
-        summary = json.load(open(PMC_SUMMARY))
+        return json.load(open(PMC_SUMMARY))
     except (OSError, ValueError):
-        return None, None
-    ds = [summary.get(k) for k in kernels]
-    if not all(d and "FETCH_SIZE" in d and "WRITE_SIZE" in d for d in ds):
-        return pmc_evidence(units_per_launch, "k_sm_prepare<false>", alg_bytes)
-    per_set = sum((2 * d["FETCH_SIZE"] + d["WRITE_SIZE"]) * 1024.0 / d["grid_size"] for d in ds)
-    have_sq = all("SQ_INSTS_VALU" in d and "SQ_WAVES" in d for d in ds)
-    dur = sum(d["duration_ms"] for d in ds)
-    ev = {"source": os.path.relpath(PMC_SUMMARY, ROOT), "kernel": " + ".join(kernels), "pmc_grid_sets": int(ds[0]["grid_size"]),
-          "hbm_bytes_per_set": round(per_set, 1), "algorithmic_bytes_per_set": alg_bytes,
-          "valu_wave_instr_per_set": round(sum(d["SQ_INSTS_VALU"] / d["SQ_WAVES"] for d in ds)) if have_sq else None,
-          "valu_issue_utilisation": round(sum(d["SQ_INSTS_VALU"] for d in ds) / (dur * 1e-3 * PEAK_VALU_WAVE_INSTR_PER_S), 4) if have_sq else None,
-          "per_kernel_ms_at_pmc_grid": {k: round(d["duration_ms"], 3) for k, d in zip(kernels, ds)}}
-    return per_set * units_per_launch, ev
+        return None
+
+
+def pmc_at(kernel, grid):
+    """Counters of `kernel` at launches of exactly `grid` work-items from the committed PMC summary
+    (tools/pmc.sh -> tools/pmc_parse.py: per kernel, per grid size), or None -- counters are only
+    attached to a roofline whose launch has the same grid as the profiled one."""
+    summary = _pmc_summary()
+    if not summary:
+        return None
+    d = (summary.get("kernels") or {}).get(kernel, {}).get(str(int(grid)))
+    return d if d and "FETCH_SIZE" in d and "WRITE_SIZE" in d else None
+
+
+def pmc_evidence(kernels, units, alg_bytes_per_unit):
+    """HBM traffic and VALU issue of one launch of each of `kernels` [(name, grid work-items)] that
+    together process `units` (sets, messages, chunks), from separate rocprofv3 --pmc passes (FETCH_SIZE
+    doubled per the gfx950 calibration of the MI355X guide: it counts 64 B per 128-B request;
+    rocprofv3 reports kilobytes).  Returns (bytes per launch, evidence) or (None, reason)."""
+    ds = [(k, g, pmc_at(k, g)) for k, g in kernels]
+    missing = ["%s@%d" % (k, g) for k, g, d in ds if d is None]
+    if missing:
+        return None, {"source": os.path.relpath(PMC_SUMMARY, ROOT), "missing_at_grid": missing}
+    total = sum((2 * d["FETCH_SIZE"] + d["WRITE_SIZE"]) * 1024.0 for _, _, d in ds)
+    have_sq = all("SQ_INSTS_VALU" in d and "SQ_WAVES" in d for _, _, d in ds)
+    dur = sum(d["duration_ms"] for _, _, d in ds)
+    summary = _pmc_summary() or {}
+    ev = {"source": os.path.relpath(PMC_SUMMARY, ROOT), "collected": summary.get("collected"),
+          "kernel": " + ".join(k for k, _, _ in ds), "pmc_grid": [int(g) for _, g, _ in ds], "pmc_grid_units": int(units),
+          "hbm_bytes_per_unit": round(total / max(units, 1), 1), "algorithmic_bytes_per_unit": alg_bytes_per_unit,
+          "write_bytes_per_unit": round(sum(d["WRITE_SIZE"] for _, _, d in ds) * 1024.0 / max(units, 1), 1),
+          "valu_wave_instr_per_unit": round(sum(d["SQ_INSTS_VALU"] for _, _, d in ds) / max(units, 1), 1) if have_sq else None,
+          "valu_issue_utilisation": round(sum(d["SQ_INSTS_VALU"] for _, _, d in ds) / (dur * 1e-3 * PEAK_VALU_WAVE_INSTR_PER_S), 4) if have_sq else None,
+          "ms_at_pmc": {k: round(d["duration_ms"], 3) for k, _, d in ds}}
+    if len(ds) == 1 and "SQ_ACTIVE_INST_VALU" in ds[0][2] and "SQ_THREAD_CYCLES_VALU" in ds[0][2]:
+        d = ds[0][2]
+        ev["valu_lane_utilisation"] = round(d["SQ_THREAD_CYCLES_VALU"] / (64.0 * d["SQ_ACTIVE_INST_VALU"]), 4)
+    return total, ev
 
 
 # device kernels of one same-message verify, in gbv_last_kernel_ms order
@@ -319,45 +322,103 @@ def api_path_js(call_off, idx, sigs, msgs, key_pks, log, reps=3):
 
 
 # ---- verifySignatureSets configs (C1, C3, C4) ------------------------------------------------------
-# device kernel name of each verifySignatureSets stage (the larger-pass forms) and its PMC key
-VS_KERNEL_NAMES = {"agg": "k_vs_agg", "hash_sig": "k_vs_hash_sig", "miller": "k_vs_miller_pair", "chunk_check": "k_vs_chunk_coop"}
+# Algorithmic work (FME) and bytes of one launch of each kernel a verifySignatureSets pass can run,
+# as a function of the launch's units (gbv_last_ops: sets, messages or chunks) and the pass (n sets,
+# gathered members of aggregates below / above AGG_BIG_MIN).  Counted on the device code path by the
+# host build (tests/test_host_arith.py pins every constant).
+AGG_BIG_MIN = 1024
 
 
-def _vs_roofline(v, n_sets, ms, agg_members=0, n_chunks=0):
-    """Roofline of the LONGEST kernel of a verifySignatureSets pass (ms: gbv_vs_last_kernel_ms, HIP
-    events on the stream each kernel runs on), with its algorithmic work per pass:
-      agg          11 FME per gathered member (mixed G1 addition)
-      hash_sig     hash_to_G2 + Signature.fromBytes + randomisation per set (W_VS_HASH_SIG)
-      miller       one Miller loop per set (FME_MILLER_1J)
-      chunk_check  per set an Fp12 product and a G2 addition, per chunk a final exponentiation and the
-                   (-g1, sum r sig) Miller loop
-    `traffic` is the kernel's HBM bytes per pass from the committed PMC summary when it holds the kernel."""
-    n_chunks = n_chunks or max(1, -(-n_sets // 128))
-    work = {"agg": agg_members * FME_G1_MADD, "hash_sig": n_sets * W_VS_HASH_SIG, "miller": n_sets * FME_MILLER_1J,
-            "chunk_check": n_sets * (FME_FP12_MUL + FME_G2_ADD) + n_chunks * (FME_FINAL_EXP + FME_MILLER_1J)}
-    k = max(range(len(VS_KERNELS)), key=lambda i: float(ms[i]))
-    name = VS_KERNELS[k]
-    t = float(ms[k])
-    achieved = work[name] * MAC_PER_FME / (t * 1e-3) / 1e12 if t > 0 else 0.0
-    if name == "miller" and os.environ.get("GBV_VS_MILLER", "").startswith("t"):
-        kname = "k_vs_miller"
-    else:
-        kname = VS_KERNEL_NAMES[name]
-    traffic, ev = None, None
-    if name in VS_ALG_BYTES:
-        pair = kname.endswith("_pair")
-        traffic, ev = pmc_evidence(n_sets, kname, VS_ALG_BYTES[name], threads_per_unit=2 if pair else 1, exact=True)
-    out = {"bound": "valu-int", "kernel": kname, "achieved": round(achieved, 4), "peak": PEAK_MAC_PER_S / 1e12,
+def vs_op_work(name, units, ps):
+    n, C = ps["n_sets"], ps["n_chunks"]
+    hash_sig_chunk = n * FME_G2_ADD + C * FME_MILLER_1J  # k_vs_chunk_s_miller: sum r_i sig_i + (-g1, sum) Miller value
+    table = {
+        "k_vs_agg": (ps["members_small"] * FME_G1_MADD, ps["members_small"] * AGG_BYTES_PER_MEMBER),
+        "k_vs_agg_big": (ps["members_big"] * FME_G1_MADD, ps["members_big"] * AGG_BYTES_PER_MEMBER),
+        "k_vs_hash_sig": (units * W_VS_HASH_SIG, units * VS_ALG_BYTES["hash_sig"]),
+        "k_hash_msgs": (units * FME_HASH_TO_G2, units * (32 + 256)),
+        "k_hash_msgs_pair": (units * FME_HASH_TO_G2, units * (32 + 256)),
+        "k_hash_msgs_quad": (units * FME_HASH_TO_G2, units * (32 + 256)),
+        "k_hash_msgs_pre": (units * FME_HASH_MAPS, units * (32 + 384)),
+        "k_hash_clear_quad": (units * FME_HASH_CLEAR, units * (384 + 256)),
+        "k_hash_clear_coop": (units * FME_HASH_CLEAR, units * (384 + 256)),
+        "k_vs_sig_decode": (units * FME_G2_DECODE, units * (96 + 4 + 256 + 1)),
+        "k_vs_sig_pre_quad": (units * (FME_G2_SUBGROUP + FME_RANDOMIZE_G2), units * (256 + 1 + 384 + 2)),
+        "k_vs_pk_rand_quad": (units * FME_RANDOMIZE_G1, units * (8 + 4 + 129 + 1 + 192)),
+        "k_vs_miller": (units * FME_MILLER_1J, units * VS_ALG_BYTES["miller"]),
+        "k_vs_miller_pair": (units * FME_MILLER_1J, units * VS_ALG_BYTES["miller"]),
+        "k_vs_miller_quad": (units * FME_MILLER_1J, units * VS_ALG_BYTES["miller"]),
+        "k_vs_miller_coop": (units * FME_MILLER_1J, units * VS_ALG_BYTES["miller"]),
+        "k_vs_chunk_s_miller": (hash_sig_chunk, n * (384 + 1) + C * 768),
+        "k_vs_chunk_coop<false>": (n * (FME_FP12_MUL + FME_G2_ADD) + C * (FME_FINAL_EXP + FME_MILLER_1J), n * (768 + 384 + 1) + C),
+        "k_vs_chunk_coop<true>": (n * FME_FP12_MUL + C * (FME_FINAL_EXP + FME_FP12_MUL), n * (768 + 1) + C * 769),
+    }
+    return table.get(name, (None, None))
+
+
+def _vs_roofline(v, n_sets, ops, members_small=0, members_big=0, n_chunks=0):
+    """Roofline of a verifySignatureSets pass from its per-kernel HIP-event timings (gbv_last_ops:
+    every launched kernel, its grid and units, its device ms on its own stream).  The roofline object
+    describes the kernel that took longest among those whose algorithmic work is known (summed over
+    its launches in the pass); `kernels` lists every launch with its fraction of the VALU peak.  PMC
+    counters are attached only from a profiled launch of that kernel at the same grid."""
+    ps = {"n_sets": n_sets, "n_chunks": n_chunks or max(1, -(-n_sets // 128)), "members_small": members_small, "members_big": members_big}
+    agg = {}
+    for name, threads, units, ms in ops:
+        e = agg.setdefault(name, {"ms": 0.0, "launches": 0, "grid": threads, "units": units, "grids": []})
+        e["ms"] += max(ms, 0.0)
+        e["launches"] += 1
+        e["grids"].append(threads)
+    kernels = []
+    for name, e in agg.items():
+        w, b = vs_op_work(name, e["units"], ps)
+        frac = round(w * MAC_PER_FME / (e["ms"] * 1e-3) / PEAK_MAC_PER_S, 4) if w and e["ms"] > 0 else None
+        kernels.append({"kernel": name, "grid": e["grid"], "units": e["units"], "launches": e["launches"], "ms": round(e["ms"], 3),
+                        "work_fme": w, "frac": frac})
+    timed = [k for k in kernels if k["work_fme"] and k["ms"] > 0]
+    if not timed:
+        return {"bound": "valu-int", "kernel": None, "kernels": kernels, "note": "no per-kernel timings recorded"}
+    dom = max(timed, key=lambda k: k["ms"])
+    t = dom["ms"] / dom["launches"]
+    achieved = dom["work_fme"] / dom["launches"] * MAC_PER_FME / (t * 1e-3) / 1e12
+    w, alg_b = vs_op_work(dom["kernel"], dom["units"], ps)
+    traffic, ev = (None, None)
+    if dom["launches"] == 1:
+        traffic, ev = pmc_evidence([(dom["kernel"], dom["grid"])], dom["units"], round(alg_b / max(dom["units"], 1), 1))
+    out = {"bound": "valu-int", "kernel": dom["kernel"], "achieved": round(achieved, 4), "peak": PEAK_MAC_PER_S / 1e12,
            "unit": "T u32-MAC/s", "frac": round(achieved * 1e12 / PEAK_MAC_PER_S, 5),
            "traffic": None if traffic is None else round(traffic), "pmc": ev,
-           "work_per_pass_fme": int(work[name]), "units_per_launch": n_sets, "avg_launch_ms": round(t, 3),
-           "kernel_ms_per_pass": {kk: round(float(x), 3) for kk, x in zip(VS_KERNELS, ms)},
-           "frac_by_kernel": {kk: round(work[kk] * MAC_PER_FME / (float(x) * 1e-3) / PEAK_MAC_PER_S, 4) if float(x) > 0 else None
-                              for kk, x in zip(VS_KERNELS, ms)},
-           "miller_fme_per_set": FME_MILLER_1J}
-    if agg_members and ms[0] > 0:
-        out["agg_gather_GBps_formula"] = round(agg_members * AGG_BYTES_PER_MEMBER / (ms[0] * 1e-3) / 1e9, 1)
+           "work_per_launch_fme": int(w), "algorithmic_bytes_per_launch": alg_b, "units_per_launch": dom["units"], "grid": dom["grid"],
+           "avg_launch_ms": round(t, 3), "timing": "HIP events around each launch on its own stream (gbv_last_ops)",
+           "kernels": sorted(kernels, key=lambda k: -k["ms"]), "miller_fme_per_set": FME_MILLER_1J}
+    if members_small + members_big:
+        for name in ("k_vs_agg", "k_vs_agg_big"):
+            if name in agg and agg[name]["ms"] > 0:
+                m = members_small if name == "k_vs_agg" else members_big
+                out.setdefault("agg_gather_GBps_formula", {})[name] = round(m * AGG_BYTES_PER_MEMBER / (agg[name]["ms"] * 1e-3) / 1e9, 1)
     return out
+
+
+def _members(calls):
+    small = big = 0
+    for c in calls:
+        for s in c:
+            k = len(getattr(s, "indices", []))
+            if k >= AGG_BIG_MIN:
+                big += k
+            elif k >= 2:
+                small += k
+    return small, big
+
+
+def _timed_ops(v, stages, steps, want):
+    """_timed_staged with per-kernel timing on; returns (seconds per step, the last pass's ops)."""
+    v.tune("kprof", 1)
+    try:
+        dt = _timed_staged(stages, steps, want)
+    finally:
+        v.tune("kprof", 0)
+    return dt, v.last_ops(1)
 
 
 def _timed_staged(stages, steps, want):
@@ -415,22 +476,24 @@ def c1_bench(v, sks, pk_rows, cpu):
         lat.append((time.perf_counter() - t) * 1e3)
         assert ok
     p50 = float(np.median(lat))
-    ms_lone = v.vs_last_kernel_ms()
+    v.tune("kprof", 1)  # one more lone call, timed kernel by kernel (outside the latency samples)
+    assert v.verify_signature_sets_sync(sets) is True
+    v.tune("kprof", 0)
+    ops_lone = v.last_ops(1)
     # throughput: 512 such calls staged, 2 passes in flight
     many = _single_sets(v, sks, 512 * 128, b"gbv-c1-many", rng)
     calls = [many[i:i + 128] for i in range(0, len(many), 128)]
     stages = [v.stage_signature_sets(calls) for _ in range(2)]
     for st in stages:
         assert st.verify() == [1] * len(calls)
-    dt = _timed_staged(stages, 6, [1] * len(calls))
-    ms = v.vs_last_kernel_ms()
+    dt, ops = _timed_ops(v, stages, 6, [1] * len(calls))
     for st in stages:
         st.close()
     out = {"metric": "verifySignatureSets: 128 distinct-message single-pubkey sets per call (verifyMultipleSignatures 128)",
            "unit": "sets/s", "value": round(128 / (p50 * 1e-3), 1), "latency_ms_p50": round(p50, 3),
-           "lone_call_kernel_ms": {k: round(float(x), 3) for k, x in zip(VS_KERNELS, ms_lone)},
+           "lone_call_kernels": [{"kernel": k, "grid": g, "units": u, "ms": round(m, 3)} for k, g, u, m in ops_lone],
            "throughput_value": round(len(many) / dt, 1), "throughput_config": "512 calls x 128 sets per pass, 2 passes in flight",
-           "roofline": _vs_roofline(v, len(many), ms)}
+           "roofline": _vs_roofline(v, len(many), ops)}
     if cpu:
         from oracle import cpu_baseline
         out["cpu_baseline"] = cpu_baseline.measure_verify_sets(_port_calls([sets]), pk_rows, threads=1,
@@ -447,14 +510,14 @@ def c3_bench(v, sk_ints, pk_rows, cpu, n_calls=512):
     stages = [v.stage_signature_sets(calls) for _ in range(2)]
     for st in stages:
         assert st.verify() == [1] * n_calls
-    dt = _timed_staged(stages, 6, [1] * n_calls)
-    ms = v.vs_last_kernel_ms()
+    dt, ops = _timed_ops(v, stages, 6, [1] * n_calls)
     for st in stages:
         st.close()
+    small, big = _members(calls)
     out = {"metric": "verifySignatureSets: 128-member committee aggregates from the HBM table (1M validators)",
            "unit": "sets/s", "value": round(len(sets) / dt, 1), "ms_per_pass": round(dt * 1e3, 3),
            "config": "%d aggregate sets of 128 members in %d calls of 128, 2 passes in flight (workload built in %.1fs)" % (len(sets), n_calls, build_s),
-           "roofline": _vs_roofline(v, len(sets), ms, agg_members=128 * len(sets))}
+           "roofline": _vs_roofline(v, len(sets), ops, members_small=small, members_big=big)}
     if cpu:
         from oracle import cpu_baseline
         out["cpu_baseline"] = cpu_baseline.measure_verify_sets(_port_calls(calls[:32]), pk_rows, label=" (the first 32 calls)")
@@ -531,20 +594,19 @@ def make_blocks(v, sk_ints, n_blocks, rng, electra=False):
     return calls
 
 
-def _pmc_gather(kernel, members):
-    """HBM read rate of the pubkey gather kernel from the committed PMC summary (FETCH_SIZE doubled per
-    the gfx950 calibration, over that launch's own duration) -- measured, not by formula -- and the
-    bytes fetched per gathered member (the PMC run uses the same default C4 / C4e pass)."""
-    try:
-        d = json.load(open(PMC_SUMMARY)).get(kernel)
-    except (OSError, ValueError):
-        return None
-    if not d or "FETCH_SIZE" not in d:
+def _pmc_gather(ops, kernel, members):
+    """HBM read rate of the pubkey gather kernel from the committed PMC summary at the grid this pass
+    launched it with (FETCH_SIZE doubled per the gfx950 calibration, over that launch's own duration):
+    measured, not by formula, and the bytes fetched per gathered member."""
+    grids = [g for k, g, _, _ in ops if k == kernel]
+    d = pmc_at(kernel, grids[0]) if grids else None
+    if not d:
         return None
     fetched = 2 * d["FETCH_SIZE"] * 1024.0
-    return {"source": os.path.relpath(PMC_SUMMARY, ROOT), "kernel": kernel, "hbm_read_GBps": round(fetched / (d["duration_ms"] * 1e-3) / 1e9, 1),
-            "fetched_bytes_per_member": round(fetched / max(members, 1), 1), "launch_ms_at_pmc": round(d["duration_ms"], 3),
-            "hbm_peak_GBps": 8000.0}
+    return {"source": os.path.relpath(PMC_SUMMARY, ROOT), "kernel": kernel, "pmc_grid": grids[0],
+            "hbm_read_GBps": round(fetched / (d["duration_ms"] * 1e-3) / 1e9, 1),
+            "fetched_bytes_per_member": round(fetched / max(members, 1), 1), "algorithmic_bytes_per_member": AGG_BYTES_PER_MEMBER,
+            "launch_ms_at_pmc": round(d["duration_ms"], 3), "hbm_peak_GBps": 8000.0}
 
 
 def c4_bench(v, sk_ints, pk_rows, cpu, n_blocks=64, electra=False):
@@ -565,18 +627,19 @@ def c4_bench(v, sk_ints, pk_rows, cpu, n_blocks=64, electra=False):
     stages = [v.stage_signature_sets(calls) for _ in range(2)]
     for st in stages:
         assert st.verify() == [1] * n_blocks
-    dt = _timed_staged(stages, 6, [1] * n_blocks)
-    ms = v.vs_last_kernel_ms()
+    dt, ops = _timed_ops(v, stages, 6, [1] * n_blocks)
     for st in stages:
         st.close()
+    small, big = _members(calls)
+    n_chunks = sum(max(1, len(c) // 128) for c in calls)  # chunkifyMaximizeChunkSize(call, 128)
     out = {"metric": "verifySignatureSets: full %sblocks (getBlockSignatureSets, index form), one call per block" % (
                "electra " if electra else ""),
            "unit": "sets/s", "value": round(n_sets / dt, 1), "blocks_per_s": round(n_blocks / dt, 2),
            "lone_block_latency_ms_p50": round(float(np.median(lat)), 3), "sets_per_block": len(calls[0]),
            "config": "range-sync segment of %d blocks (%d sets, %d pubkeys gathered), 2 passes in flight (built in %.1fs)" % (
                n_blocks, n_sets, members, build_s),
-           "roofline": _vs_roofline(v, n_sets, ms, agg_members=members)}
-    g = _pmc_gather("k_vs_agg_big", members) if electra else None  # (k_vs_agg's largest PMC launch is C3's)
+           "roofline": _vs_roofline(v, n_sets, ops, members_small=small, members_big=big, n_chunks=n_chunks)}
+    g = _pmc_gather(ops, "k_vs_agg_big" if electra else "k_vs_agg", big if electra else small)
     if g:
         out["roofline"]["agg_gather_pmc"] = g
     if cpu:
@@ -809,11 +872,15 @@ def main():
         b = stages[k % depth]
         if k >= depth:
             collect(b)
+        if k == args.steps - 1:
+            v.tune("kprof", 1)  # the last batch is also timed kernel by kernel (two events per kernel)
         b.submit()
+    v.tune("kprof", 0)
     for k in range(max(0, args.steps - depth), args.steps):
         collect(stages[k % depth])
     barrier()
     elapsed = time.perf_counter() - t0
+    step_ops = v.last_ops(0)  # the last collected batch = the last submitted one
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -847,16 +914,24 @@ def main():
     w_fme = (W_PREPARE_FME_MSM_COMB if comb else W_PREPARE_FME_MSM) if kcnt[7] > 0 else W_PREPARE_FME
     achieved = units_per_launch * w_fme * MAC_PER_FME / t_launch / 1e12 if t_launch > 0 else 0.0
     peak = PEAK_MAC_PER_S / 1e12
-    traffic, pmc = (pmc_stage_evidence(units_per_launch, ["k_sig_decode", "k_sm_prepare<false, true>"],
-                                       ALG_BYTES_PER_SET_COMB if comb else ALG_BYTES_PER_SET) if kcnt[7] > 0
-                    else pmc_evidence(units_per_launch, "k_sm_prepare<true, true>", ALG_BYTES_PER_SET))
-    roofline = {"bound": "valu-int", "kernel": "k_sm_prepare (k_sig_decode + k_sm_prepare<false, true>, one stream)",
+    prep_kernel = "k_sm_prepare<false>" if kcnt[7] > 0 else "k_sm_prepare<true>"
+    # the stage's two kernels as this run launched them (grid from gbv_last_ops) -> PMC at that grid
+    stage_ops = [(k, g, u, m) for k, g, u, m in step_ops if k in ("k_sig_decode", prep_kernel)]
+    traffic, pmc = pmc_evidence([(k, g) for k, g, _, _ in stage_ops], units_per_launch,
+                                ALG_BYTES_PER_SET_COMB if comb else ALG_BYTES_PER_SET) if stage_ops else (None, None)
+    per_unit = {"k_sig_decode": FME_G2_DECODE, prep_kernel: w_fme - FME_G2_DECODE}
+    roofline = {"bound": "valu-int", "kernel": "k_sm_prepare stage (k_sig_decode + %s, one stream)" % prep_kernel,
                 "achieved": round(achieved, 4), "peak": peak,
                 "unit": "T u32-MAC/s", "frac": round(achieved / peak, 5),
                 "traffic": round(traffic) if traffic is not None else None, "pmc": pmc,
                 "work_per_unit_fme": w_fme, "comb_tables": comb,
                 "units_per_launch": round(units_per_launch, 1),
                 "avg_launch_ms": round(float(avg_launch_ms[1]), 3),
+                "timing": "HIP events on stream A around the stage, every step; per-kernel events on the last step (gbv_last_ops)",
+                "stage_kernels": [{"kernel": k, "grid": g, "units": u, "ms": round(m, 3), "work_per_unit_fme": per_unit.get(k),
+                                   "frac": round(u * per_unit[k] * MAC_PER_FME / (m * 1e-3) / PEAK_MAC_PER_S, 4) if m > 0 and k in per_unit else None}
+                                  for k, g, u, m in stage_ops],
+                "last_step_kernels": [{"kernel": k, "grid": g, "units": u, "ms": round(m, 3)} for k, g, u, m in step_ops],
                 "kernel_ms_per_step": {k: round(float(x), 3) for k, x in zip(KERNELS, kms)},
                 "slow_path_chunks_segments": slow_path}
 

@@ -92,7 +92,8 @@ int gbv_comb_enabled(gbv_ctx* ctx);
 /* Change one of the context's pipeline settings, which gbv_init reads once from the environment
  * (GBV_MSM_MIN, GBV_MSM_COOLDOWN, GBV_SEGMENTS): "msm_min" (segments of at least this many sets
  * form their G2 sum with the bucket MSM; 0 = never), "msm_cooldown" (submits without the MSM after
- * a failing MSM segment), "segments" (pipeline segments per same-message batch).  Results are
+ * a failing MSM segment), "segments" (pipeline segments per same-message batch), "kprof" (1: record
+ * per-kernel timings, gbv_last_ops).  Results are
  * identical for every value; tests use it to reach each pipeline form on small batches.  No
  * reference counterpart.  GBV_E_ARG for an unknown name. */
 int gbv_tune(gbv_ctx* ctx, const char* name, uint32_t value);
@@ -212,6 +213,13 @@ int gbv_fp12_check(gbv_ctx* ctx, const uint8_t* partials576, size_t k, uint8_t* 
  * pass of segments whose G2 sum comes from the bucket MSM); returns the number of entries written
  * (at most 8). */
 int gbv_last_kernel_ms(gbv_ctx* ctx, float* ms_out, int* launches_out, int max);
+/* Per-kernel device time of the last waited pass, one line per launch: "<kernel> <grid work-items>
+ * <units> <ms>\n" (units: the sets / messages / chunks the launch covers; ms from two HIP events on
+ * the kernel's own stream).  path 0: same-message batches, 1: verifySignatureSets passes and shard
+ * partials.  Recorded only while gbv_tune(ctx, "kprof", 1) is set (off by default: it adds two
+ * events per kernel).  Writes at most cap - 1 bytes and a NUL; returns the full length (bench.py
+ * rooflines; no reference counterpart). */
+int gbv_last_ops(gbv_ctx* ctx, int path, char* out, size_t cap);
 /* Fast-path health of the last waited same-message verification: chunks that went to the per-set
  * retry (malformed sets or failing chunk checks) and segments whose combined check failed.  Both
  * are 0 for an all-valid batch (up to the 2^-64 batch-verification error). */

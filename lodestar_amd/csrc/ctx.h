@@ -78,6 +78,32 @@ inline Fp12 fp12_unpack(const uint8_t* in576) {
   for (int i = 0; i < 12; ++i) memcpy(&f[i], in576 + 48 * i, 48);
   return r;
 }
+// "name grid_threads units ms" per kernel of a waited pass (gbv_last_ops); every event of the pass
+// has completed once its done event has
+inline std::string kprof_format(KProf& p) {
+  std::string out;
+  char line[160];
+  for (const KRec& r : p.recs) {
+    float ms = 0.f;
+    if (hipEventSynchronize(r.b) != hipSuccess || hipEventElapsedTime(&ms, r.a, r.b) != hipSuccess) {
+      (void)hipGetLastError();
+      ms = -1.f;
+    }
+    snprintf(line, sizeof line, "%s %u %u %.4f\n", r.name, r.threads, r.units, ms);
+    out += line;
+  }
+  return out;
+}
+
+// Sets t_kprof for the enqueue routine that holds it (nothing recorded when p is null).
+struct KProfScope {
+  explicit KProfScope(KProf* p) {
+    if (p) p->reset();
+    t_kprof = p;
+  }
+  ~KProfScope() { t_kprof = nullptr; }
+};
+
 inline Fp12 fp12_one_host() {
   Fp12 r;
   memset((void*)&r, 0, sizeof(r));
@@ -140,6 +166,10 @@ struct gbv_ctx {
   hipEvent_t ssz_ev[2] = {};
   float last_ssz_ms = 0.f;
   float last_vs_ms[4] = {};  // agg, hash+sig, miller, chunk check of the last vs batch
+  // per-kernel timing of every pass (gbv_tune "kprof"; off by default: two events per kernel) and the
+  // last waited pass of each path (gbv_last_ops: 0 same-message, 1 verifySignatureSets / partials)
+  bool kprof_on = false;
+  std::string last_ops[2];
   // Every entry point holds this while it touches the context (its streams, table, counters), so
   // host threads may share a context: the Python verifier's worker threads and its event-loop
   // thread, the addon's libuv pool.  Recursive: a fill nests inside a one-shot call.  No entry point

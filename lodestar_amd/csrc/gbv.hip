@@ -117,6 +117,7 @@ struct gbv_sm_batch {
   uint32_t* msm_ent = nullptr;  // 4 per set, segment s at 4 * s0
   G2J* msm_total = nullptr;     // one per segment
   std::vector<uint8_t> seg_msm = std::vector<uint8_t>(64);
+  KProf prof;  // per-kernel events of the last submit (ctx kprof_on)
 };
 
 static void sm_free_work(gbv_sm_batch* b) {
@@ -196,6 +197,7 @@ static void sm_destroy(gbv_sm_batch* b) {
     hipEventDestroy(b->copied);
   }
   sm_free_work(b);
+  b->prof.destroy();
   hipFree(b->in_dev);
   hipHostFree(b->in_host);
   for (int k = 0; k < 2; ++k) {
@@ -279,6 +281,7 @@ int gbv_tune(gbv_ctx* c, const char* name, uint32_t value) {
   if (!strcmp(name, "msm_min")) c->msm_min = value;
   else if (!strcmp(name, "msm_cooldown")) c->msm_cooldown_len = value;
   else if (!strcmp(name, "segments")) c->segments = std::max<uint32_t>(value, 1);
+  else if (!strcmp(name, "kprof")) c->kprof_on = value != 0;
   else return gbv_fail(c, GBV_E_ARG, std::string("unknown setting: ") + name);
   return GBV_OK;
 }
@@ -688,6 +691,7 @@ int gbv_sm_batch_submit(gbv_ctx* c, gbv_sm_batch* b) {
 // Each segment ends in ONE randomised multi-pairing check over all its chunks; only a failing
 // segment pays per-chunk checks and only a failing chunk pays per-set retries.
 static int sm_submit_enqueue(gbv_ctx* c, gbv_sm_batch* b) {
+  KProfScope kp(c->kprof_on ? &b->prof : nullptr);
   Seed seed = fresh_seed();
   uint32_t nonce = c->nonce++;
   // Same-message batches: hash on stream 4, tail on stream 2, every batch (alternating the tails of
@@ -868,6 +872,10 @@ int gbv_sm_batch_wait(gbv_ctx* c, gbv_sm_batch* b, uint8_t* valid) {
   b->in_flight = false;
   if (we != hipSuccess) return gbv_fail(c, GBV_E_DEVICE, std::string("hipEventSynchronize: ") + hipGetErrorString(we));
   if (valid) memcpy(valid, b->valid_host, b->n);
+  if (!b->prof.recs.empty()) {
+    c->last_ops[0] = kprof_format(b->prof);
+    b->prof.reset();
+  }
   c->last_fallback_chunks = *b->nfb_host;
   c->last_failed_segments = 0;
   for (size_t s = 0; s < b->n_seg; ++s) {
@@ -902,6 +910,18 @@ int gbv_sm_batch_verify(gbv_ctx* c, gbv_sm_batch* b, uint8_t* valid) {
   int rc = gbv_sm_batch_submit(c, b);  // the batch belongs to the caller: the wait needs no lock held
   if (rc) return rc;
   return gbv_sm_batch_wait(c, b, valid);
+}
+
+int gbv_last_ops(gbv_ctx* c, int path, char* out, size_t cap) {
+  if (!c || (path != 0 && path != 1) || (cap && !out)) return GBV_E_ARG;
+  GBV_LOCK(c);
+  const std::string& s = c->last_ops[path];
+  if (cap) {
+    const size_t k = std::min(s.size(), cap - 1);
+    memcpy(out, s.data(), k);
+    out[k] = 0;
+  }
+  return (int)s.size();
 }
 
 int gbv_last_stats(gbv_ctx* c, uint32_t* fallback_chunks, uint32_t* failed_segments) {
@@ -1176,6 +1196,32 @@ void tuning_load() {
     rd("GBV_VS_PAIR_MAX", g_tuning.vs_pair_max);
     rd("GBV_SYNC_DEBUG", g_tuning.sync_debug);
   });
+}
+
+thread_local KProf* t_kprof = nullptr;
+
+void kprof_begin(hipStream_t s, const char* name, uint32_t threads, uint32_t units) {
+  KProf* p = t_kprof;
+  if (!p) return;
+  while (p->pool.size() < p->used + 2) {
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) {  // no timing for this pass rather than a failed submit
+      (void)hipGetLastError();
+      t_kprof = nullptr;
+      return;
+    }
+    p->pool.push_back(e);
+  }
+  KRec r{name, threads, units, p->pool[p->used], p->pool[p->used + 1]};
+  p->used += 2;
+  (void)hipEventRecord(r.a, s);
+  p->recs.push_back(r);
+}
+
+void kprof_end(hipStream_t s) {
+  KProf* p = t_kprof;
+  if (!p || p->recs.empty()) return;
+  (void)hipEventRecord(p->recs.back().b, s);
 }
 
 void debug_sync(hipStream_t s, const char* kernel) {

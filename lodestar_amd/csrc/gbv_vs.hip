@@ -73,6 +73,7 @@ struct gbv_vs_batch {
   hipEvent_t pre = nullptr;     // "pre" mode: k_vs_sig_pre done (stream 5)
   bool in_flight = false;
   int tail = 0;
+  KProf prof;  // per-kernel events of the last submit / partial (ctx kprof_on)
 };
 
 static void vs_free_work(gbv_vs_batch* b) {
@@ -92,6 +93,7 @@ void vs_batch_free(gbv_vs_batch* b) {
     (void)hipEventDestroy(b->copied);
   }
   vs_free_work(b);
+  b->prof.destroy();
   hipFree(b->in_dev);
   hipHostFree(b->in_host);
   hipFree(b->Fpart); hipFree(b->Spart); hipFree(b->has); hipFree(b->f_out); hipFree(b->flag);
@@ -393,6 +395,7 @@ int gbv_vs_batch_fill(gbv_ctx* c, gbv_vs_batch* b, size_t n_calls, const uint32_
 }
 
 static int vs_submit_enqueue(gbv_ctx* c, gbv_vs_batch* b) {
+  KProfScope kp(c->kprof_on ? &b->prof : nullptr);
   b->tail = (int)(c->sm_submits++ & 1);
   hipStream_t t = b->tail ? c->stream4 : c->stream2;
   int rc = vs_enqueue_sets(c, b, t, true);
@@ -444,6 +447,10 @@ int gbv_vs_batch_wait(gbv_ctx* c, gbv_vs_batch* b, uint8_t* call_valid) {
     for (int k = 0; k < 4; ++k)
       if (hipEventElapsedTime(&ms[k], b->ev[from[k]], b->ev[from[k] + 1]) != hipSuccess) ms[k] = 0.f;
     memcpy(c->last_vs_ms, ms, sizeof ms);
+    if (!b->prof.recs.empty()) {
+      c->last_ops[1] = kprof_format(b->prof);
+      b->prof.reset();
+    }
   } else if (b->n && b->C) {
     return gbv_fail(c, GBV_E_ARG, "batch not submitted");
   }
@@ -569,14 +576,17 @@ static int vs_partial_enqueue(gbv_ctx* c, gbv_vs_batch* b) {
     b->part_cap = np;
   }
   if (b->part_host_cap < sizeof(Fp12) + n) {
+    // grow geometrically (computed before the old capacity is dropped): a hipHostFree synchronises
+    // the device under the passes in flight
+    const size_t cap = std::max(sizeof(Fp12) + n, 2 * b->part_host_cap);
     hipHostFree(b->part_host);
     b->part_host = nullptr;
     b->part_host_cap = 0;
-    const size_t cap = std::max(sizeof(Fp12) + n, 2 * b->part_host_cap);
     HIP_CHECK(c, hipHostMalloc((void**)&b->part_host, cap, hipHostMallocDefault));
     b->part_host_cap = cap;
   }
   HIP_CHECK(c, hipSetDevice(c->device));
+  KProfScope kp(c->kprof_on ? &b->prof : nullptr);
   // a shard of up to GBV_VS_PRE_MAX sets (a per-GPU share of one large call at N = 8): the hash on the
   // tail stream beside the split signature / pubkey halves, the rest on the tail stream after them
   hipStream_t s = vs_pre_on(b) ? c->stream2 : c->stream;
@@ -604,6 +614,11 @@ static int vs_partial_collect(gbv_ctx* c, gbv_vs_batch* b, uint8_t out576[GBV_FP
   if (we != hipSuccess) {
     GBV_LOCK(c);
     return gbv_fail(c, GBV_E_DEVICE, std::string("hipEventSynchronize: ") + hipGetErrorString(we));
+  }
+  if (!b->prof.recs.empty()) {
+    GBV_LOCK(c);
+    c->last_ops[1] = kprof_format(b->prof);
+    b->prof.reset();
   }
   Fp12 f;
   memcpy((void*)&f, b->part_host, sizeof(Fp12));

@@ -46,14 +46,12 @@ k_vs_sig_decode(uint32_t n, const uint8_t* __restrict__ sig, uint32_t sig_stride
 void launch_vs_sig_decode(hipStream_t s, uint32_t n, const uint8_t* sig, uint32_t sig_stride, const uint32_t* sig_len, G2A* S,
                           uint8_t* dec_st) {
   if (!n) return;
-  hipLaunchKernelGGL(k_vs_sig_decode, dim3((n + 63) / 64), dim3(64), 0, s, n, sig, sig_stride, sig_len, S, dec_st);
-  debug_sync(s, "k_vs_sig_decode");
+  GBV_LAUNCH("k_vs_sig_decode", k_vs_sig_decode, dim3((n + 63) / 64), dim3(64), s, n, n, sig, sig_stride, sig_len, S, dec_st);
 }
 
 void launch_sig_decode(hipStream_t s, uint32_t base, uint32_t n, const uint8_t* sig96, G2A* S, uint8_t* status) {
   if (!n) return;
-  hipLaunchKernelGGL(k_sig_decode, dim3((n + 63) / 64), dim3(64), 0, s, base, n, sig96, S, status);
-  debug_sync(s, "k_sig_decode");
+  GBV_LAUNCH("k_sig_decode", k_sig_decode, dim3((n + 63) / 64), dim3(64), s, n, base, n, sig96, S, status);
 }
 
 }  // namespace gbv

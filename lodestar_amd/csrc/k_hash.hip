@@ -75,22 +75,19 @@ __global__ void GBV_KERNEL_ATTR k_util_g2_out(uint32_t n, const G2A* __restrict_
 
 void launch_hash_msgs(LaunchCfg c, const uint8_t* msgs32, uint32_t n, G2A* H, G2J* Qpre) {
   if (Qpre && n <= tuning().hash_coop_max) {  // latency: lane-pair maps, then the cofactor clearing one workgroup per message
-    hipLaunchKernelGGL(k_hash_msgs_pre, dim3((2 * n + 63) / 64), dim3(64), 0, c.stream, msgs32, n, Qpre);
-    debug_sync(c.stream, "k_hash_msgs_pre");
+    GBV_LAUNCH("k_hash_msgs_pre", k_hash_msgs_pre, dim3((2 * n + 63) / 64), dim3(64), c.stream, n, msgs32, n, Qpre);
     launch_hash_clear_coop(c.stream, n, Qpre, H);
     return;
   }
   if (Qpre && n <= tuning().hash_quad_max) {  // latency: maps on lane pairs, the cofactor clearing on lane quads
-    hipLaunchKernelGGL(k_hash_msgs_pre, dim3((2 * n + 63) / 64), dim3(64), 0, c.stream, msgs32, n, Qpre);
-    debug_sync(c.stream, "k_hash_msgs_pre");
-    hipLaunchKernelGGL(k_hash_clear_quad, dim3((n + 15) / 16), dim3(64), 0, c.stream, n, Qpre, H);
+    GBV_LAUNCH("k_hash_msgs_pre", k_hash_msgs_pre, dim3((2 * n + 63) / 64), dim3(64), c.stream, n, msgs32, n, Qpre);
+    GBV_LAUNCH("k_hash_clear_quad", k_hash_clear_quad, dim3((n + 15) / 16), dim3(64), c.stream, n, n, Qpre, H);
   } else if (n <= tuning().hash_quad_max)  // lane quads, then lane pairs (grids sized here; c.blocks is for one lane per message)
-    hipLaunchKernelGGL(k_hash_msgs_quad, dim3((n + 15) / 16), dim3(64), 0, c.stream, msgs32, n, H);
+    GBV_LAUNCH("k_hash_msgs_quad", k_hash_msgs_quad, dim3((n + 15) / 16), dim3(64), c.stream, n, msgs32, n, H);
   else if (n <= tuning().hash_pair_max)
-    hipLaunchKernelGGL(k_hash_msgs_pair, dim3((2 * n + 63) / 64), dim3(64), 0, c.stream, msgs32, n, H);
+    GBV_LAUNCH("k_hash_msgs_pair", k_hash_msgs_pair, dim3((2 * n + 63) / 64), dim3(64), c.stream, n, msgs32, n, H);
   else
-    hipLaunchKernelGGL(k_hash_msgs, dim3(c.blocks), dim3(c.threads), 0, c.stream, msgs32, n, H);
-  debug_sync(c.stream, "k_hash_msgs");
+    GBV_LAUNCH("k_hash_msgs", k_hash_msgs, dim3(c.blocks), dim3(c.threads), c.stream, n, msgs32, n, H);
 }
 void launch_util_g2_out(LaunchCfg c, uint32_t n, const G2A* H, uint8_t* out192) {
   hipLaunchKernelGGL(k_util_g2_out, dim3(c.blocks), dim3(c.threads), 0, c.stream, n, H, out192);

@@ -205,28 +205,22 @@ void launch_msm_g2_buckets(hipStream_t s, uint32_t s0, uint32_t n, const uint32_
                            const G2A* S, const Seed& seed, uint32_t nonce, uint32_t* cnt, uint32_t* off, uint32_t* cur, uint32_t* ent,
                            G2J* buckets, G2J* head, G2J* tail) {
   static_assert(MSM_KEYS % 4096 == 0 && MSM_PARTS % 64 == 0, "MSM shape");
-  hipLaunchKernelGGL(k_msm_zero, dim3(MSM_KEYS / 256), dim3(256), 0, s, cnt);
+  GBV_LAUNCH("k_msm_zero", k_msm_zero, dim3(MSM_KEYS / 256), dim3(256), s, 0, cnt);
   unsigned eb = (n + 63) / 64;
-  hipLaunchKernelGGL(k_msm_entries<false>, dim3(eb), dim3(64), 0, s, s0, n, set_grp, status, grp_state, seed, nonce, cnt, ent);
-  debug_sync(s, "k_msm_entries<count>");
+  GBV_LAUNCH("k_msm_entries<false>", k_msm_entries<false>, dim3(eb), dim3(64), s, n, s0, n, set_grp, status, grp_state, seed, nonce, cnt, ent);
   // block sums live in the (not yet used) bucket area
   uint32_t* bsum = reinterpret_cast<uint32_t*>(buckets);
-  hipLaunchKernelGGL(k_msm_scan_blocks, dim3(MSM_KEYS / 64), dim3(64), 0, s, cnt, bsum);
-  hipLaunchKernelGGL(k_msm_scan_top, dim3(1), dim3(64), 0, s, MSM_KEYS / 64, bsum);
-  hipLaunchKernelGGL(k_msm_scan_apply, dim3(MSM_KEYS / 64), dim3(64), 0, s, cnt, bsum, off, cur);
-  debug_sync(s, "k_msm_scan");
-  hipLaunchKernelGGL(k_msm_entries<true>, dim3(eb), dim3(64), 0, s, s0, n, set_grp, status, grp_state, seed, nonce, cur, ent);
-  debug_sync(s, "k_msm_entries<scatter>");
+  GBV_LAUNCH("k_msm_scan_blocks", k_msm_scan_blocks, dim3(MSM_KEYS / 64), dim3(64), s, 0, cnt, bsum);
+  GBV_LAUNCH("k_msm_scan_top", k_msm_scan_top, dim3(1), dim3(64), s, 0, MSM_KEYS / 64, bsum);
+  GBV_LAUNCH("k_msm_scan_apply", k_msm_scan_apply, dim3(MSM_KEYS / 64), dim3(64), s, 0, cnt, bsum, off, cur);
+  GBV_LAUNCH("k_msm_entries<true>", k_msm_entries<true>, dim3(eb), dim3(64), s, n, s0, n, set_grp, status, grp_state, seed, nonce, cur, ent);
   const uint32_t runs = (uint32_t)((4ull * n + MSM_RUN - 1) / MSM_RUN);  // upper bound; runs past the end exit
-  hipLaunchKernelGGL(k_msm_runs, dim3((runs + 63) / 64), dim3(64), 0, s, s0, off, cur, ent, S, buckets, head, tail);
-  debug_sync(s, "k_msm_runs");
-  hipLaunchKernelGGL(k_msm_fixup, dim3(MSM_KEYS / 64), dim3(64), 0, s, off, cur, head, tail, buckets);
-  debug_sync(s, "k_msm_fixup");
+  GBV_LAUNCH("k_msm_runs", k_msm_runs, dim3((runs + 63) / 64), dim3(64), s, n, s0, off, cur, ent, S, buckets, head, tail);
+  GBV_LAUNCH("k_msm_fixup", k_msm_fixup, dim3(MSM_KEYS / 64), dim3(64), s, 0, off, cur, head, tail, buckets);
 }
 
 void launch_msm_g2_reduce(hipStream_t s, const G2J* buckets, G2J* part, G2J* total) {
-  hipLaunchKernelGGL(k_msm_slices, dim3(MSM_PARTS / 64), dim3(64), 0, s, buckets, part);
-  debug_sync(s, "k_msm_slices");
+  GBV_LAUNCH("k_msm_slices", k_msm_slices, dim3(MSM_PARTS / 64), dim3(64), s, 0, buckets, part);
   // MSM_PARTS -> MSM_PARTS/64 -> ... -> 1
   uint32_t m = MSM_PARTS;
   G2J* src = part;
@@ -234,8 +228,7 @@ void launch_msm_g2_reduce(hipStream_t s, const G2J* buckets, G2J* part, G2J* tot
   while (m > 1) {
     uint32_t nb = (m + 63) / 64;
     G2J* o = nb == 1 ? total : dst;
-    hipLaunchKernelGGL(k_msm_sum64, dim3(nb), dim3(64), 0, s, m, src, o);
-    debug_sync(s, "k_msm_sum64");
+    GBV_LAUNCH("k_msm_sum64", k_msm_sum64, dim3(nb), dim3(64), s, m, m, src, o);
     src = o;
     dst = o + nb;
     m = nb;

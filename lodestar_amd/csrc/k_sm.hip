@@ -386,8 +386,7 @@ __global__ void GBV_KERNEL_ATTR k_sm_group_check(uint32_t g0, uint32_t G, const 
 
 void launch_sm_group_check(LaunchCfg c, uint32_t g0, uint32_t G, const Fp12* F, const G2J* SgJ, const uint8_t* seg_ok, uint8_t* grp_state,
                            uint32_t* n_fallback) {
-  hipLaunchKernelGGL(k_sm_group_check, dim3((G + 63) / 64), dim3(64), 0, c.stream, g0, G, F, SgJ, seg_ok, grp_state, n_fallback);
-  debug_sync(c.stream, "k_sm_group_check");
+  GBV_LAUNCH("k_sm_group_check", k_sm_group_check, dim3((G + 63) / 64), dim3(64), c.stream, G, g0, G, F, SgJ, seg_ok, grp_state, n_fallback);
 }
 
 // ---- failure path of a chunk: 8-set block checks, then per-set checks ---------------------------
@@ -464,19 +463,15 @@ __global__ void GBV_KERNEL_ATTR k_sm_fb_sets(const uint32_t* __restrict__ set_li
 void launch_sm_fb_runs(LaunchCfg c, uint32_t s0, uint32_t n, const uint32_t* set_grp, const uint8_t* grp_state, uint4* runs, uint32_t* n_runs,
                        uint32_t cap) {
   uint32_t windows = (n + SCAN_W - 1) / SCAN_W;
-  hipLaunchKernelGGL(k_sm_fb_runs, dim3((windows + 63) / 64), dim3(64), 0, c.stream, s0, n, set_grp, grp_state, runs, n_runs, cap);
-  debug_sync(c.stream, "k_sm_fb_runs");
+  GBV_LAUNCH("k_sm_fb_runs", k_sm_fb_runs, dim3((windows + 63) / 64), dim3(64), c.stream, n, s0, n, set_grp, grp_state, runs, n_runs, cap);
 }
 void launch_sm_fb_blocks(LaunchCfg c, const uint4* runs, const uint32_t* n_runs, uint32_t cap, const uint8_t* status, const uint32_t* grp_msg,
                          const G2J* Sh, const G1J* Ph, const G2A* H, uint8_t* valid, uint32_t* set_list, uint32_t* n_list) {
-  hipLaunchKernelGGL(k_sm_fb_blocks, dim3(c.blocks), dim3(64), 0, c.stream, runs, n_runs, cap, status, grp_msg, Sh, Ph, H, valid, set_list,
-                     n_list);
-  debug_sync(c.stream, "k_sm_fb_blocks");
+  GBV_LAUNCH("k_sm_fb_blocks", k_sm_fb_blocks, dim3(c.blocks), dim3(64), c.stream, 0, runs, n_runs, cap, status, grp_msg, Sh, Ph, H, valid, set_list, n_list);
 }
 void launch_sm_fb_sets(LaunchCfg c, const uint32_t* set_list, const uint32_t* n_list, const uint32_t* set_grp, const uint32_t* grp_msg,
                        const uint32_t* idx, const G1A* table, const G2A* S, const G2A* H, uint8_t* valid) {
-  hipLaunchKernelGGL(k_sm_fb_sets, dim3(c.blocks), dim3(64), 0, c.stream, set_list, n_list, set_grp, grp_msg, idx, table, S, H, valid);
-  debug_sync(c.stream, "k_sm_fb_sets");
+  GBV_LAUNCH("k_sm_fb_sets", k_sm_fb_sets, dim3(c.blocks), dim3(64), c.stream, 0, set_list, n_list, set_grp, grp_msg, idx, table, S, H, valid);
 }
 
 void launch_sm_prepare(LaunchCfg c, uint32_t base, uint32_t n, const uint32_t* idx, const uint8_t* sig96, const uint32_t* set_grp,
@@ -490,54 +485,44 @@ void launch_sm_prepare(LaunchCfg c, uint32_t base, uint32_t n, const uint32_t* i
     // then the verdicts and the scan
     launch_sig_decode(c.stream, base, n, sig96, S_out, status);
     launch_sm_prep_roles_quad(c.stream, base, n, idx, table, table_ok, table_n, comb, comb_ok, seed, nonce, S_out, status, scratch8, Sh, Ph);
-    hipLaunchKernelGGL(k_sm_prep_scan, grid, dim3(64), 0, c.stream, base, n, idx, set_grp, table_ok, table_n, scratch8, status, Sh, Ph);
-    debug_sync(c.stream, "k_sm_prep_scan");
+    GBV_LAUNCH("k_sm_prep_scan", k_sm_prep_scan, grid, dim3(64), c.stream, n, base, n, idx, set_grp, table_ok, table_n, scratch8, status, Sh, Ph);
   } else if (Sh && n <= tuning().prepare_split_max) {  // latency: two waves per 64 sets
-    hipLaunchKernelGGL(k_sm_prepare_split, dim3((n + 63) / 64), dim3(128), 0, c.stream, base, n, idx, sig96, set_grp, table, table_ok, table_n,
-                       comb, comb_ok, seed, nonce, S_out, Sh, Ph, status);
+    GBV_LAUNCH("k_sm_prepare_split", k_sm_prepare_split, dim3((n + 63) / 64), dim3(128), c.stream, n, base, n, idx, sig96, set_grp, table, table_ok,
+               table_n, comb, comb_ok, seed, nonce, S_out, Sh, Ph, status);
   } else {
     // throughput: decompression first as its own kernel at a higher occupancy (k_dec.hip)
     launch_sig_decode(c.stream, base, n, sig96, S_out, status);
     if (Sh)
-      hipLaunchKernelGGL((k_sm_prepare<true>), grid, dim3(64), 0, c.stream, base, n, idx, sig96, set_grp, table, table_ok, table_n, comb,
-                         comb_ok, seed, nonce, S_out, Sh, Ph, status);
+      GBV_LAUNCH("k_sm_prepare<true>", k_sm_prepare<true>, grid, dim3(64), c.stream, n, base, n, idx, sig96, set_grp, table, table_ok, table_n,
+                 comb, comb_ok, seed, nonce, S_out, Sh, Ph, status);
     else
-      hipLaunchKernelGGL((k_sm_prepare<false>), grid, dim3(64), 0, c.stream, base, n, idx, sig96, set_grp, table, table_ok, table_n, comb,
-                         comb_ok, seed, nonce, S_out, Sh, Ph, status);
+      GBV_LAUNCH("k_sm_prepare<false>", k_sm_prepare<false>, grid, dim3(64), c.stream, n, base, n, idx, sig96, set_grp, table, table_ok,
+                 table_n, comb, comb_ok, seed, nonce, S_out, Sh, Ph, status);
   }
-  debug_sync(c.stream, "k_sm_prepare");
 }
 void launch_sm_redo_g2(LaunchCfg c, uint32_t base, uint32_t n, const uint32_t* set_grp, const uint8_t* status, const G2A* S, const Seed& seed,
                        uint32_t nonce, const uint8_t* seg_ok, const uint32_t* n_fallback, G2J* Sh) {
-  hipLaunchKernelGGL(k_sm_redo_g2, dim3((n + 63) / 64), dim3(64), 0, c.stream, base, n, set_grp, status, S, seed, nonce, seg_ok, n_fallback,
-                     Sh);
-  debug_sync(c.stream, "k_sm_redo_g2");
+  GBV_LAUNCH("k_sm_redo_g2", k_sm_redo_g2, dim3((n + 63) / 64), dim3(64), c.stream, n, base, n, set_grp, status, S, seed, nonce, seg_ok, n_fallback, Sh);
 }
 void launch_sm_chunk_finish_s(LaunchCfg c, uint32_t g0, uint32_t G, uint32_t s0, const uint32_t* grp_off, const uint8_t* grp_state,
                               const G2J* Sh, const uint8_t* seg_ok, G2J* SgJ) {
-  hipLaunchKernelGGL(k_sm_chunk_finish_s, dim3((G + 63) / 64), dim3(64), 0, c.stream, g0, G, s0, grp_off, grp_state, Sh, seg_ok, SgJ);
-  debug_sync(c.stream, "k_sm_chunk_finish_s");
+  GBV_LAUNCH("k_sm_chunk_finish_s", k_sm_chunk_finish_s, dim3((G + 63) / 64), dim3(64), c.stream, G, g0, G, s0, grp_off, grp_state, Sh, seg_ok, SgJ);
 }
 void launch_sm_chunk_finish(LaunchCfg c, uint32_t g0, uint32_t G, uint32_t s0, const uint32_t* grp_off, const uint8_t* status, const G2J* Sh,
                             const G1J* Ph, G1J* PgJ, G2J* SgJ, uint8_t* grp_state, uint32_t* n_fallback) {
   if (G <= tuning().chunk_finish_wave_max)  // latency (a lone call): a wave per chunk, tree over its group sums
-    hipLaunchKernelGGL(k_sm_chunk_finish_wave, dim3(G), dim3(64), 0, c.stream, g0, s0, grp_off, status, Sh, Ph, PgJ, SgJ, grp_state,
-                       n_fallback);
+    GBV_LAUNCH("k_sm_chunk_finish_wave", k_sm_chunk_finish_wave, dim3(G), dim3(64), c.stream, G, g0, s0, grp_off, status, Sh, Ph, PgJ, SgJ,
+               grp_state, n_fallback);
   else
-    hipLaunchKernelGGL(k_sm_chunk_finish, dim3((G + 63) / 64), dim3(64), 0, c.stream, g0, G, s0, grp_off, status, Sh, Ph, PgJ, SgJ,
-                       grp_state, n_fallback);
-  debug_sync(c.stream, "k_sm_chunk_finish");
+    GBV_LAUNCH("k_sm_chunk_finish", k_sm_chunk_finish, dim3((G + 63) / 64), dim3(64), c.stream, G, g0, G, s0, grp_off, status, Sh, Ph, PgJ, SgJ, grp_state, n_fallback);
 }
 void launch_sm_miller(LaunchCfg c, uint32_t g0, uint32_t G, const uint32_t* grp_msg, const uint8_t* grp_state, const G1J* PgJ, const G2A* H,
                       Fp12* F) {
-  hipLaunchKernelGGL(k_sm_miller, dim3((G + 63) / 64), dim3(64), 0, c.stream, g0, G, grp_msg, grp_state, PgJ, H, F);
-  debug_sync(c.stream, "k_sm_miller");
+  GBV_LAUNCH("k_sm_miller", k_sm_miller, dim3((G + 63) / 64), dim3(64), c.stream, G, g0, G, grp_msg, grp_state, PgJ, H, F);
 }
 void launch_sm_fallback(LaunchCfg c, uint32_t n, const uint32_t* set_grp, const uint32_t* grp_msg, const uint8_t* grp_state,
                         const uint8_t* status, const uint32_t* idx, const G1A* table, const G2A* S, const G2A* H, uint8_t* valid,
                         int do_fallback) {
-  hipLaunchKernelGGL(k_sm_fallback, dim3(c.blocks), dim3(c.threads), 0, c.stream, n, set_grp, grp_msg, grp_state, status, idx, table, S,
-                     H, valid, do_fallback);
-  debug_sync(c.stream, "k_sm_fallback");
+  GBV_LAUNCH("k_sm_fallback", k_sm_fallback, dim3(c.blocks), dim3(c.threads), c.stream, n, n, set_grp, grp_msg, grp_state, status, idx, table, S, H, valid, do_fallback);
 }
 }  // namespace gbv

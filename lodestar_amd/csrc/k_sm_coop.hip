@@ -340,23 +340,16 @@ k_sm_fb_sets_fe(const uint32_t* __restrict__ set_list, const uint32_t* __restric
 void launch_sm_fb_blocks_coop(LaunchCfg c, const uint4* runs, const uint32_t* n_runs, uint32_t cap, const uint8_t* status,
                               const uint32_t* grp_msg, const G2J* Sh, const G1J* Ph, const G2A* H, uint8_t* valid, uint32_t* set_list,
                               uint32_t* n_list) {
-  hipLaunchKernelGGL(k_sm_fb_blocks_coop, dim3(FB_COOP_MAX), dim3(64), 0, c.stream, runs, n_runs, cap, status, grp_msg, Sh, Ph, H, valid,
-                     set_list, n_list, 1);
-  debug_sync(c.stream, "k_sm_fb_blocks_coop");
+  GBV_LAUNCH("k_sm_fb_blocks_coop", k_sm_fb_blocks_coop, dim3(FB_COOP_MAX), dim3(64), c.stream, 0, runs, n_runs, cap, status, grp_msg, Sh, Ph, H, valid, set_list, n_list, 1);
 }
 void launch_sm_fb_sets_coop(LaunchCfg c, const uint32_t* set_list, const uint32_t* n_list, const uint32_t* set_grp, const uint32_t* grp_msg,
                             const uint32_t* idx, const G1A* table, const G2A* S, const G2A* H, uint8_t* valid, Fp12* Fpair) {
   if (Fpair) {  // 2 * FB_COOP_MAX Fp12 of scratch
-    hipLaunchKernelGGL(k_sm_fb_sets_miller2, dim3(FB_COOP_MAX, 2), dim3(64), 0, c.stream, set_list, n_list, set_grp, grp_msg, idx, table, S, H,
-                       Fpair);
-    debug_sync(c.stream, "k_sm_fb_sets_miller2");
-    hipLaunchKernelGGL(k_sm_fb_sets_fe, dim3(FB_COOP_MAX), dim3(64), 0, c.stream, set_list, n_list, Fpair, valid);
-    debug_sync(c.stream, "k_sm_fb_sets_fe");
+    GBV_LAUNCH("k_sm_fb_sets_miller2", k_sm_fb_sets_miller2, dim3(FB_COOP_MAX, 2), dim3(64), c.stream, 0, set_list, n_list, set_grp, grp_msg, idx, table, S, H, Fpair);
+    GBV_LAUNCH("k_sm_fb_sets_fe", k_sm_fb_sets_fe, dim3(FB_COOP_MAX), dim3(64), c.stream, 0, set_list, n_list, Fpair, valid);
     return;
   }
-  hipLaunchKernelGGL(k_sm_fb_sets_coop, dim3(FB_COOP_MAX), dim3(64), 0, c.stream, set_list, n_list, set_grp, grp_msg, idx, table, S, H,
-                     valid);
-  debug_sync(c.stream, "k_sm_fb_sets_coop");
+  GBV_LAUNCH("k_sm_fb_sets_coop", k_sm_fb_sets_coop, dim3(FB_COOP_MAX), dim3(64), c.stream, 0, set_list, n_list, set_grp, grp_msg, idx, table, S, H, valid);
 }
 
 // One level of a segment's reduction on lane quads: block b combines items k = 64 b + j + 16 m
@@ -421,14 +414,12 @@ k_seg_reduce_quad(uint32_t n, const uint8_t* __restrict__ act, uint8_t act_val, 
 uint32_t launch_seg_reduce_quad(hipStream_t s, uint32_t g0, uint32_t G, const uint8_t* grp_state, const Fp12* F, const G2J* SgJ, Fp12* Fpart,
                                 G2J* Spart, uint8_t* has, uint32_t* n_out) {
   uint32_t n = (G + 63) / 64;
-  hipLaunchKernelGGL(k_seg_reduce_quad, dim3(n), dim3(64), 0, s, G, grp_state + g0, (uint8_t)GRP_PENDING, F + g0, SgJ + g0, Fpart, Spart, has);
-  debug_sync(s, "k_seg_reduce_quad");
+  GBV_LAUNCH("k_seg_reduce_quad", k_seg_reduce_quad, dim3(n), dim3(64), s, G, G, grp_state + g0, (uint8_t)GRP_PENDING, F + g0, SgJ + g0, Fpart, Spart, has);
   uint32_t off = 0;
   while (n > 4) {
     const uint32_t m = (n + 63) / 64;
-    hipLaunchKernelGGL(k_seg_reduce_quad, dim3(m), dim3(64), 0, s, n, has + off, (uint8_t)1, Fpart + off, Spart + off, Fpart + off + n,
-                       Spart + off + n, has + off + n);
-    debug_sync(s, "k_seg_reduce_quad");
+    GBV_LAUNCH("k_seg_reduce_quad", k_seg_reduce_quad, dim3(m), dim3(64), s, n, n, has + off, (uint8_t)1, Fpart + off, Spart + off, Fpart + off + n,
+               Spart + off + n, has + off + n);
     off += n;
     n = m;
   }
@@ -440,21 +431,16 @@ void launch_sm_seg_check(LaunchCfg c, uint32_t g0, uint32_t G, uint8_t* grp_stat
                          uint8_t* has, uint8_t* seg_ok, Fp12* miller_out, const G2J* S_extra) {
   uint32_t nb = 0;
   const uint32_t off = launch_seg_reduce_quad(c.stream, g0, G, grp_state, F, SgJ, Fpart, Spart, has, &nb);
-  hipLaunchKernelGGL(k_sm_seg_check, dim3(1), dim3(64), 0, c.stream, g0, G, nb, Fpart + off, Spart + off, has + off, grp_state, seg_ok,
-                     miller_out, S_extra);
-  debug_sync(c.stream, "k_sm_seg_check");
+  GBV_LAUNCH("k_sm_seg_check", k_sm_seg_check, dim3(1), dim3(64), c.stream, G, g0, G, nb, Fpart + off, Spart + off, has + off, grp_state, seg_ok, miller_out, S_extra);
 }
 void launch_sm_group_pairing(LaunchCfg c, uint32_t g0, uint32_t G, const uint32_t* grp_msg, const G1J* PgJ, const G2J* SgJ, const G2A* H,
                              const uint8_t* seg_ok, uint8_t* grp_state, uint32_t* n_fallback, Fp12* Fpair, uint8_t* pair_ok) {
   if (!Fpair) {
-    hipLaunchKernelGGL(k_sm_group_pairing, dim3(G), dim3(64), 0, c.stream, g0, grp_msg, PgJ, SgJ, H, seg_ok, grp_state, n_fallback);
-    debug_sync(c.stream, "k_sm_group_pairing");
+    GBV_LAUNCH("k_sm_group_pairing", k_sm_group_pairing, dim3(G), dim3(64), c.stream, G, g0, grp_msg, PgJ, SgJ, H, seg_ok, grp_state, n_fallback);
     return;
   }
-  hipLaunchKernelGGL(k_sm_group_miller2, dim3(G, 2), dim3(64), 0, c.stream, g0, grp_msg, PgJ, SgJ, H, seg_ok, grp_state, Fpair, pair_ok);
-  debug_sync(c.stream, "k_sm_group_miller2");
-  hipLaunchKernelGGL(k_sm_group_fe, dim3(G), dim3(64), 0, c.stream, g0, seg_ok, Fpair, pair_ok, grp_state, n_fallback);
-  debug_sync(c.stream, "k_sm_group_fe");
+  GBV_LAUNCH("k_sm_group_miller2", k_sm_group_miller2, dim3(G, 2), dim3(64), c.stream, G, g0, grp_msg, PgJ, SgJ, H, seg_ok, grp_state, Fpair, pair_ok);
+  GBV_LAUNCH("k_sm_group_fe", k_sm_group_fe, dim3(G), dim3(64), c.stream, G, g0, seg_ok, Fpair, pair_ok, grp_state, n_fallback);
 }
 // Product of k Fp12 Miller partials (one per shard / GPU) and ONE final exponentiation == 1?
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
@@ -690,25 +676,21 @@ k_vs_miller_coop(const uint8_t* __restrict__ status, const G1J* __restrict__ rP,
 
 void launch_vs_chunk_s_miller(hipStream_t s, uint32_t C, const uint8_t* status, const uint32_t* chunk_be, const G2J* rS, Fp12* Fs,
                               uint8_t* fs_flag) {
-  hipLaunchKernelGGL(k_vs_chunk_s_miller, dim3(C), dim3(64), 0, s, status, chunk_be, rS, Fs, fs_flag);
-  debug_sync(s, "k_vs_chunk_s_miller");
+  GBV_LAUNCH("k_vs_chunk_s_miller", k_vs_chunk_s_miller, dim3(C), dim3(64), s, C, status, chunk_be, rS, Fs, fs_flag);
 }
 void launch_vs_miller_coop(hipStream_t s, uint32_t n, const uint8_t* status, const G1J* rP, const G2A* H, Fp12* F) {
-  hipLaunchKernelGGL(k_vs_miller_coop, dim3(n), dim3(64), 0, s, status, rP, H, F);
-  debug_sync(s, "k_vs_miller_coop");
+  GBV_LAUNCH("k_vs_miller_coop", k_vs_miller_coop, dim3(n), dim3(64), s, n, status, rP, H, F);
 }
 
 void launch_fp12_check(LaunchCfg c, uint32_t k, const Fp12* parts, uint8_t* out) {
-  hipLaunchKernelGGL(k_fp12_check, dim3(1), dim3(64), 0, c.stream, k, parts, out);
-  debug_sync(c.stream, "k_fp12_check");
+  GBV_LAUNCH("k_fp12_check", k_fp12_check, dim3(1), dim3(64), c.stream, k, k, parts, out);
 }
 void launch_vs_chunk_coop(LaunchCfg c, uint32_t C, const uint32_t* chunk_be, const uint8_t* status, const Fp12* f, const G2J* rS,
                           uint8_t* chunk_valid, const Fp12* Fs, const uint8_t* fs_flag) {
   if (Fs)
-    hipLaunchKernelGGL(k_vs_chunk_coop<true>, dim3(C), dim3(64), 0, c.stream, chunk_be, status, f, rS, chunk_valid, Fs, fs_flag);
+    GBV_LAUNCH("k_vs_chunk_coop<true>", k_vs_chunk_coop<true>, dim3(C), dim3(64), c.stream, C, chunk_be, status, f, rS, chunk_valid, Fs, fs_flag);
   else
-    hipLaunchKernelGGL(k_vs_chunk_coop<false>, dim3(C), dim3(64), 0, c.stream, chunk_be, status, f, rS, chunk_valid, Fs, fs_flag);
-  debug_sync(c.stream, "k_vs_chunk_coop");
+    GBV_LAUNCH("k_vs_chunk_coop<false>", k_vs_chunk_coop<false>, dim3(C), dim3(64), c.stream, C, chunk_be, status, f, rS, chunk_valid, Fs, fs_flag);
 }
 // hash_to_G2's cofactor clearing for few messages (launch_hash_msgs' latency form, n <= GBV_HASH_COOP_MAX):
 // h_eff P = [x^2 - x - 1] P + [x - 1] psi(P) + psi^2(2P) as quad_g2.h g2_clear_cofactor, with both
@@ -763,7 +745,6 @@ k_hash_clear_coop(const G2J* __restrict__ Qpre, G2A* __restrict__ H) {
   }
 }
 void launch_hash_clear_coop(hipStream_t s, uint32_t n, const G2J* Qpre, G2A* H) {
-  hipLaunchKernelGGL(k_hash_clear_coop, dim3(n), dim3(128), 0, s, Qpre, H);
-  debug_sync(s, "k_hash_clear_coop");
+  GBV_LAUNCH("k_hash_clear_coop", k_hash_clear_coop, dim3(n), dim3(128), s, n, Qpre, H);
 }
 }  // namespace gbv

@@ -326,9 +326,7 @@ __global__ void GBV_QUAD_ATTR k_sm_prep_roles_quad(uint32_t base, uint32_t n, co
 void launch_sm_prep_roles_quad(hipStream_t s, uint32_t base, uint32_t n, const uint32_t* idx, const G1A* table, const uint8_t* table_ok,
                                uint32_t table_n, const uint4* comb, const uint8_t* comb_ok, const Seed& seed, uint32_t nonce, const G2A* S,
                                const uint8_t* status, uint8_t* sub_ok, G2J* Sh, G1J* Ph) {
-  hipLaunchKernelGGL(k_sm_prep_roles_quad, dim3(2 * ((n + 15) / 16)), dim3(64), 0, s, base, n, idx, table, table_ok, table_n, comb, comb_ok, seed,
-                     nonce, S, status, sub_ok, Sh, Ph);
-  debug_sync(s, "k_sm_prep_roles_quad");
+  GBV_LAUNCH("k_sm_prep_roles_quad", k_sm_prep_roles_quad, dim3(2 * ((n + 15) / 16)), dim3(64), s, n, base, n, idx, table, table_ok, table_n, comb, comb_ok, seed, nonce, S, status, sub_ok, Sh, Ph);
 }
 
 // The pubkey half (stream A, after the aggregation and k_vs_sig_pre): a rejected signature's verdict
@@ -481,18 +479,14 @@ void launch_sig_aggregate(hipStream_t s, uint32_t n, const uint8_t* sig, uint32_
 void launch_vs_agg(LaunchCfg c, const uint32_t* agg_list, const uint32_t* set_off, const uint32_t* arena, const G1A* table,
                    const uint8_t* table_ok, G1J* pk_out, uint8_t* pk_st) {
   const uint32_t n_agg = c.blocks;  // c.blocks carries the aggregate-set count
-  hipLaunchKernelGGL(k_vs_agg, dim3((n_agg + 64 / AGG_LANES - 1) / (64 / AGG_LANES)), dim3(64), 0, c.stream, n_agg, agg_list, set_off, arena,
-                     table, table_ok, pk_out, pk_st);
-  debug_sync(c.stream, "k_vs_agg");
+  GBV_LAUNCH("k_vs_agg", k_vs_agg, dim3((n_agg + 64 / AGG_LANES - 1) / (64 / AGG_LANES)), dim3(64), c.stream, n_agg, n_agg, agg_list, set_off, arena, table, table_ok, pk_out, pk_st);
 }
 
 void launch_vs_agg_big(hipStream_t s, uint32_t n_slices, const uint4* slices, uint32_t n_big, const uint4* big, const uint32_t* arena,
                        const G1A* table, const uint8_t* table_ok, G1J* part, uint8_t* part_bad, G1J* pk_out, uint8_t* pk_st) {
   if (!n_big) return;
-  hipLaunchKernelGGL(k_vs_agg_big, dim3(n_slices), dim3(AGG_BIG_TPB), 0, s, slices, arena, table, table_ok, part, part_bad);
-  debug_sync(s, "k_vs_agg_big");
-  hipLaunchKernelGGL(k_vs_agg_big_fin, dim3(n_big), dim3(64), 0, s, n_big, big, part, part_bad, pk_out, pk_st);
-  debug_sync(s, "k_vs_agg_big_fin");
+  GBV_LAUNCH("k_vs_agg_big", k_vs_agg_big, dim3(n_slices), dim3(AGG_BIG_TPB), s, n_slices, slices, arena, table, table_ok, part, part_bad);
+  GBV_LAUNCH("k_vs_agg_big_fin", k_vs_agg_big_fin, dim3(n_big), dim3(64), s, n_big, n_big, big, part, part_bad, pk_out, pk_st);
 }
 
 void launch_vs_hash_sig(hipStream_t s, uint32_t n, const uint8_t* msgs32, const uint32_t* set_off, const uint32_t* arena,
@@ -502,35 +496,27 @@ void launch_vs_hash_sig(hipStream_t s, uint32_t n, const uint8_t* msgs32, const 
   const uint32_t pair = n <= tuning().hash_pair_max ? 1u : 0u;
   const uint32_t nsig = (n + 63) / 64;
   const uint32_t nb = split ? 0u : pair ? (2 * n + 63) / 64 : (n + 63) / 64;  // split: the caller hashes
-  hipLaunchKernelGGL(k_vs_hash_sig, dim3(nb + (split ? 2 : 1) * nsig), dim3(64), 0, s, n, nb, pair, split ? 1u : 0u, msgs32, set_off,
-                     arena, raw_flag, raw_pk48, sig, sig_stride, sig_len, table, table_ok, pk_agg, pk_st, seed, nonce, H, rP, rS, status);
-  debug_sync(s, "k_vs_hash_sig");
+  GBV_LAUNCH("k_vs_hash_sig", k_vs_hash_sig, dim3(nb + (split ? 2 : 1) * nsig), dim3(64), s, n, n, nb, pair, split ? 1u : 0u, msgs32, set_off, arena, raw_flag, raw_pk48, sig, sig_stride, sig_len, table, table_ok, pk_agg, pk_st, seed, nonce, H, rP, rS, status);
 }
 
 void launch_vs_sig_pre(hipStream_t s, uint32_t n, const uint8_t* sig, uint32_t sig_stride, const uint32_t* sig_len, const Seed& seed,
                        uint32_t nonce, G2J* rS, uint8_t* status, uint8_t* sig_st, G2A* Sd, uint8_t* dec_st) {
   if (n <= tuning().vs_sig_quad_max) {
     launch_vs_sig_decode(s, n, sig, sig_stride, sig_len, Sd, dec_st);
-    hipLaunchKernelGGL(k_vs_sig_pre_quad, dim3(2 * ((n + 15) / 16)), dim3(64), 0, s, n, Sd, dec_st, seed, nonce, rS, status, sig_st);
-    debug_sync(s, "k_vs_sig_pre_quad");
+    GBV_LAUNCH("k_vs_sig_pre_quad", k_vs_sig_pre_quad, dim3(2 * ((n + 15) / 16)), dim3(64), s, n, n, Sd, dec_st, seed, nonce, rS, status, sig_st);
     return;
   }
   const uint32_t nsig = (n + 63) / 64;
-  hipLaunchKernelGGL(k_vs_sig_pre, dim3(2 * nsig), dim3(64), 0, s, n, sig, sig_stride, sig_len, seed, nonce, rS, status, sig_st);
-  debug_sync(s, "k_vs_sig_pre");
+  GBV_LAUNCH("k_vs_sig_pre", k_vs_sig_pre, dim3(2 * nsig), dim3(64), s, n, n, sig, sig_stride, sig_len, seed, nonce, rS, status, sig_st);
 }
 void launch_vs_pk_rand(hipStream_t s, uint32_t n, const uint32_t* set_off, const uint32_t* arena, const uint8_t* raw_flag,
                        const uint8_t* raw_pk48, const G1A* table, const uint8_t* table_ok, const G1J* pk_agg, const uint8_t* pk_st,
                        const Seed& seed, uint32_t nonce, G1J* rP, uint8_t* status) {
   if (n <= tuning().vs_sig_quad_max) {
-    hipLaunchKernelGGL(k_vs_pk_rand_quad, dim3((n + 15) / 16), dim3(64), 0, s, n, set_off, arena, raw_flag, raw_pk48, table, table_ok, pk_agg,
-                       pk_st, seed, nonce, rP, status);
-    debug_sync(s, "k_vs_pk_rand_quad");
+    GBV_LAUNCH("k_vs_pk_rand_quad", k_vs_pk_rand_quad, dim3((n + 15) / 16), dim3(64), s, n, n, set_off, arena, raw_flag, raw_pk48, table, table_ok, pk_agg, pk_st, seed, nonce, rP, status);
     return;
   }
-  hipLaunchKernelGGL(k_vs_pk_rand, dim3((n + 63) / 64), dim3(64), 0, s, n, set_off, arena, raw_flag, raw_pk48, table, table_ok, pk_agg, pk_st,
-                     seed, nonce, rP, status);
-  debug_sync(s, "k_vs_pk_rand");
+  GBV_LAUNCH("k_vs_pk_rand", k_vs_pk_rand, dim3((n + 63) / 64), dim3(64), s, n, n, set_off, arena, raw_flag, raw_pk48, table, table_ok, pk_agg, pk_st, seed, nonce, rP, status);
 }
 
 void launch_sig_validate(LaunchCfg c, uint32_t n, const uint8_t* sig, uint32_t sig_len, uint8_t* status, uint8_t* out96) {

@@ -104,14 +104,11 @@ void launch_vs_miller(LaunchCfg c, uint32_t n, const uint8_t* status, const G1J*
   // profiles/r03e).
   const Tuning& t = tuning();
   if (n > t.vs_pair_max) {
-    hipLaunchKernelGGL(k_vs_miller, dim3((n + 63) / 64), dim3(64), 0, c.stream, n, status, rP, H, F);
-    debug_sync(c.stream, "k_vs_miller");
+    GBV_LAUNCH("k_vs_miller", k_vs_miller, dim3((n + 63) / 64), dim3(64), c.stream, n, n, status, rP, H, F);
   } else if (n > t.vs_quad_max) {
-    hipLaunchKernelGGL(k_vs_miller_pair, dim3((n + 31) / 32), dim3(64), 0, c.stream, n, status, rP, H, F);
-    debug_sync(c.stream, "k_vs_miller_pair");
+    GBV_LAUNCH("k_vs_miller_pair", k_vs_miller_pair, dim3((n + 31) / 32), dim3(64), c.stream, n, n, status, rP, H, F);
   } else {
-    hipLaunchKernelGGL(k_vs_miller_quad, dim3((n + 15) / 16), dim3(64), 0, c.stream, n, status, rP, H, F);
-    debug_sync(c.stream, "k_vs_miller_quad");
+    GBV_LAUNCH("k_vs_miller_quad", k_vs_miller_quad, dim3((n + 15) / 16), dim3(64), c.stream, n, n, status, rP, H, F);
   }
 }
 

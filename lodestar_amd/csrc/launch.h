@@ -2,6 +2,8 @@
 // parallelises; gbv.hip sequences them on the context stream).
 #pragma once
 #include <hip/hip_runtime.h>
+
+#include <vector>
 #include "curve.h"
 #include "fp12.h"
 
@@ -130,4 +132,43 @@ void launch_ssz_att_signing_roots(hipStream_t s, const uint8_t* data128, uint32_
 namespace gbv {
 // GBV_SYNC_DEBUG=1: synchronise after every launch and report the failing kernel by name.
 void debug_sync(hipStream_t s, const char* kernel);
+
+// Per-kernel device time of a pass (bench rooflines, gbv_last_ops): while an enqueue routine has set
+// t_kprof (the context's "kprof" setting), every GBV_LAUNCH brackets its kernel with two HIP events
+// on the kernel's own stream and records the kernel's name, its grid in work-items (rocprofv3's
+// Grid_Size, so PMC rows can be matched to it) and the units of work it covers.
+struct KRec {
+  const char* name;
+  uint32_t threads, units;
+  hipEvent_t a, b;
+};
+struct KProf {
+  std::vector<KRec> recs;
+  std::vector<hipEvent_t> pool;  // created on first use, reused pass after pass
+  size_t used = 0;
+  void reset() { recs.clear(); used = 0; }
+  void destroy() {
+    for (hipEvent_t e : pool) (void)hipEventDestroy(e);
+    pool.clear();
+    reset();
+  }
+};
+extern thread_local KProf* t_kprof;
+void kprof_begin(hipStream_t s, const char* name, uint32_t threads, uint32_t units);
+void kprof_end(hipStream_t s);
+struct KScope {
+  hipStream_t s;
+  KScope(hipStream_t s_, const char* name, uint32_t threads, uint32_t units) : s(s_) { kprof_begin(s, name, threads, units); }
+  ~KScope() { kprof_end(s); }
+};
 }  // namespace gbv
+
+// hipLaunchKernelGGL + the kprof events + debug_sync.  NAME is the kernel's name as rocprofv3 prints
+// it (template instances included), UNITS the sets / messages / chunks the launch covers.
+#define GBV_LAUNCH(NAME, KERNEL, GRID, BLOCK, STREAM, UNITS, ...)                                              \
+  do {                                                                                                       \
+    const dim3 g_ = (GRID), b_ = (BLOCK);                                                                    \
+    gbv::KScope ks_((STREAM), NAME, (uint32_t)(g_.x * g_.y * g_.z * b_.x * b_.y * b_.z), (uint32_t)(UNITS)); \
+    hipLaunchKernelGGL(KERNEL, g_, b_, 0, (STREAM), __VA_ARGS__);                                            \
+    gbv::debug_sync((STREAM), NAME);                                                                         \
+  } while (0)

@@ -313,6 +313,21 @@ class GpuBlsVerifier:
         self._staged.add(st)
         return st
 
+    def last_ops(self, path: int):
+        """Per-kernel device time of the last waited pass (gbv_last_ops; path 0 same-message, 1
+        verifySignatureSets / shard partials), recorded while tune("kprof", 1) is set: a list of
+        (kernel, grid work-items, units, ms), one per launch."""
+        n = self._lib.gbv_last_ops(self._ctx, int(path), None, 0)
+        if n < 0:
+            _native.check(self._lib, self._ctx, n)
+        buf = ctypes.create_string_buffer(n + 1)
+        self._lib.gbv_last_ops(self._ctx, int(path), buf, n + 1)
+        out = []
+        for line in buf.value.decode().splitlines():
+            name, threads, units, ms = line.split()
+            out.append((name, int(threads), int(units), float(ms)))
+        return out
+
     def vs_last_kernel_ms(self) -> List[float]:
         """Device ms of the last verifySignatureSets pass: [aggregate, hash+signature, miller, chunk checks]."""
         buf = (ctypes.c_float * 4)()

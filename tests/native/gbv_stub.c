@@ -442,6 +442,12 @@ int gbv_last_kernel_ms(gbv_ctx* c, float* out, int* launches, int max) {
   return max < 8 ? max : 8;
 }
 
+int gbv_last_ops(gbv_ctx* c, int path, char* out, size_t cap) {
+  if (!c || (path != 0 && path != 1) || (cap && !out)) return GBV_E_ARG;
+  if (cap) out[0] = 0; /* the stub runs no kernels */
+  return 0;
+}
+
 int gbv_last_stats(gbv_ctx* c, uint32_t* fb, uint32_t* seg) {
   if (!c) return GBV_E_ARG;
   if (fb) *fb = 0;

@@ -306,6 +306,29 @@ unsigned long long ht_count_sig_validate(const uint8_t* sig96) {
   if (g2_decode(s, sig96, 96) == PT_OK) (void)g2_in_subgroup(s);
   return g_fme_count;
 }
+// G2 decompression alone (k_sig_decode / k_vs_sig_decode)
+unsigned long long ht_count_g2_decode(const uint8_t* sig96) {
+  G2A s;
+  g_fme_count = 0;
+  (void)g2_decode(s, sig96, 96);
+  return g_fme_count;
+}
+// the two halves of hash_to_G2 as the small-pass kernels split them: which = 0 the two SSWU maps +
+// isogenies and Q0 + Q1 (k_hash_msgs_pre), 1 the cofactor clearing and the affine form
+// (k_hash_clear_quad / k_hash_clear_coop)
+unsigned long long ht_count_hash_part(const uint8_t* msg32, int which) {
+  uint32_t w[8];
+  for (int i = 0; i < 8; ++i) w[i] = ((uint32_t)msg32[4*i] << 24) | ((uint32_t)msg32[4*i+1] << 16) | ((uint32_t)msg32[4*i+2] << 8) | msg32[4*i+3];
+  G2J q = jac_add(hash_map_iso(hash_to_field_fp2(w, 0)), hash_map_iso(hash_to_field_fp2(w, 1)));
+  g_fme_count = 0;
+  if (which == 0) {
+    (void)jac_add(hash_map_iso(hash_to_field_fp2(w, 0)), hash_map_iso(hash_to_field_fp2(w, 1)));
+  } else {
+    G2A out;
+    (void)jac_to_aff(out, clear_cofactor_g2(q));
+  }
+  return g_fme_count;
+}
 // randomize_pair (r pk and r sig) / randomize_g1 (r pk only)
 unsigned long long ht_count_randomize(const uint8_t* p96, const uint8_t* q192, uint64_t r64, int g1_only) {
   G1A P{load_mont(p96), load_mont(p96 + 48)};
@@ -316,6 +339,7 @@ unsigned long long ht_count_randomize(const uint8_t* p96, const uint8_t* q192, u
   g_fme_count = 0;
   if (g1_only == 1) randomize_g1(P, r64, &rp);
   else if (g1_only == 2) randomize_pair_jac(PJ, Q, r64, &rp, &rq);
+  else if (g1_only == 3) randomize_g2(Q, r64, &rq);
   else randomize_pair(P, Q, r64, &rp, &rq);
   return g_fme_count;
 }

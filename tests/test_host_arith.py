@@ -326,8 +326,10 @@ def test_roofline_work_constants_are_counted(lib):
     import sys
     sys.path.insert(0, os.path.join(HERE, ".."))
     import bench
-    for f in ("ht_count_hash_to_g2", "ht_count_sig_validate", "ht_count_randomize", "ht_count_miller_1j", "ht_count_op"):
+    for f in ("ht_count_hash_to_g2", "ht_count_sig_validate", "ht_count_randomize", "ht_count_miller_1j", "ht_count_op",
+              "ht_count_g2_decode", "ht_count_hash_part"):
         getattr(lib, f).restype = ctypes.c_ulonglong
+    lib.ht_count_hash_part.argtypes = [ctypes.c_char_p, ctypes.c_int]
     rng = random.Random(5)
     for trial in range(3):
         msg = bytes(rng.randrange(256) for _ in range(32))
@@ -345,6 +347,14 @@ def test_roofline_work_constants_are_counted(lib):
         assert lib.ht_count_randomize(p96, q192, r64, 2) == bench.FME_RANDOMIZE_PAIR_JAC
         assert lib.ht_count_miller_1j(p96, q192) == bench.FME_MILLER_1J
         assert 3 * (lib.ht_count_op(1, p96, q192) - 7) == bench.FME_G1_SCAN  # full G1 addition (minus the doubling)
+        assert lib.ht_count_g2_decode(o.g2_compress(sig_pt)) == bench.FME_G2_DECODE
+        assert lib.ht_count_randomize(p96, q192, r64, 3) == bench.FME_RANDOMIZE_G2
+        assert lib.ht_count_hash_part(msg, 0) == bench.FME_HASH_MAPS
+        assert lib.ht_count_hash_part(msg, 1) == bench.FME_HASH_CLEAR
+        assert lib.ht_count_op(0, p96, q192) == bench.FME_G1_MADD
+        assert lib.ht_count_op(2, p96, q192) == bench.FME_FP12_MUL
+        assert lib.ht_count_op(3, p96, q192) == bench.FME_G2_ADD
+        assert lib.ht_count_op(4, p96, q192) == bench.FME_FINAL_EXP
     assert bench.W_VS_HASH_SIG == bench.FME_HASH_TO_G2 + bench.FME_SIG_VALIDATE + bench.FME_RANDOMIZE_PAIR_JAC
 
 
