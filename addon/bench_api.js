@@ -5,7 +5,8 @@
 //   meta.json {n_sets, n_calls, n_keys, table}, call_off.u32, idx.u32, sigs.bin (96 n), msgs.bin (32 calls),
 //   keys.bin (48 n_keys: the table is keys[i mod n_keys], built with addPubkeys + replicatePubkeys)
 //   node addon/bench_api.js <dir> [reps]
-// Prints one JSON line: packed-form and object-form sets/s (best of reps), passes, validity.
+// Prints one JSON line: packed-form, IBlsVerifier-shaped ("ibls": objects packed per call inside the
+// clock, as the Lodestar binding does) and object-form sets/s (best of reps), passes, validity.
 "use strict";
 const path = require("path");
 const fs = require("fs");
@@ -43,7 +44,7 @@ async function main() {
     const a = callOff[g], b = callOff[g + 1];
     packed.push({indices: idx.subarray(a, b), signatures: sigs.subarray(96 * a, 96 * b)});
     const sets = new Array(b - a);
-    for (let i = a; i < b; ++i) sets[i - a] = {index: idx[i], signature: sigs.subarray(96 * i, 96 * i + 96)};
+    for (let i = a; i < b; ++i) sets[i - a] = {publicKey: null, index: idx[i], signature: sigs.subarray(96 * i, 96 * i + 96)};
     objects.push(sets);
   }
   const nSets = callOff[nCalls];
@@ -51,7 +52,12 @@ async function main() {
     const calls = form === "packed" ? packed : objects;
     const p0 = v.devicePasses;
     const t0 = process.hrtime.bigint();
-    const res = await Promise.all(calls.map((s, g) => v.verifySignatureSetsSameMessage(s, message(g))));
+    // "ibls": the IBlsVerifier call shape the Lodestar binding uses (chain/bls/gpu/index.ts over
+    // verifySameMessageSets): one {publicKey, signature, index} object per set in, boolean[] out; the
+    // packing into the device form happens here, inside the clock
+    const res = form === "ibls"
+      ? await Promise.all(calls.map((s, g) => v.verifySameMessageSets(s, message(g))))
+      : await Promise.all(calls.map((s, g) => v.verifySignatureSetsSameMessage(s, message(g))));
     let ok = 0;
     for (const r of res) for (let i = 0; i < r.length; ++i) ok += r[i] ? 1 : 0;
     const sec = Number(process.hrtime.bigint() - t0) / 1e9;
@@ -60,7 +66,7 @@ async function main() {
   }
   await stream("packed"); // warm the pass slots (first-use allocation stays out of the clock)
   const out = {sets: nSets, calls: nCalls, reps};
-  for (const form of ["packed", "objects"]) {
+  for (const form of ["packed", "ibls", "objects"]) {
     let best = null;
     for (let r = 0; r < reps; ++r) {
       const x = await stream(form);

@@ -51,10 +51,12 @@
 #include "../include/gbv.h"
 
 #define MAX_PASSES 3
+struct pass_s;
 typedef struct {
   gbv_sm_batch* sm;
   gbv_vs_batch* vs;
   int busy;              /* JS thread only: a submitted pass not yet waited */
+  struct pass_s* pass;   /* JS thread only: that pass (reclaim_orphans frees one its caller dropped unwaited) */
   pthread_mutex_t mu;    /* held by the pool thread waiting on the pass, and by close() */
 } pass_slot;
 
@@ -327,6 +329,7 @@ typedef struct {
   /* same-message: per set index + 96-byte signature, per call a message */
   uvec sm_idx;
   bvec sm_sigs, sm_msgs;
+  bvec sm_packed;    /* per same-message call: 1 = packed sets (answered with a Uint8Array) */
   uint8_t* out;
   size_t n_out;
   int rc;
@@ -421,11 +424,19 @@ static void complete(napi_env env, napi_status status, void* data) {
         for (size_t c = 0; c < nc; ++c) {
           uint32_t a = j->sets.call_off.p[c], b = j->sets.call_off.p[c + 1];
           napi_value arr;
-          napi_create_array_with_length(env, b - a, &arr);
-          for (uint32_t i = a; i < b; ++i) {
-            napi_value x;
-            napi_get_boolean(env, j->out[i] == 1, &x);
-            napi_set_element(env, arr, i - a, x);
+          if (c < j->sm_packed.n && j->sm_packed.p[c]) {  /* packed call: a Uint8Array, as waitPass answers it */
+            void* dst = NULL;
+            napi_value ab;
+            napi_create_arraybuffer(env, b > a ? b - a : 1, &dst, &ab);
+            if (b > a) memcpy(dst, j->out + a, b - a);
+            napi_create_typedarray(env, napi_uint8_array, b - a, ab, 0, &arr);
+          } else {
+            napi_create_array_with_length(env, b - a, &arr);
+            for (uint32_t i = a; i < b; ++i) {
+              napi_value x;
+              napi_get_boolean(env, j->out[i] == 1, &x);
+              napi_set_element(env, arr, i - a, x);
+            }
           }
           napi_set_element(env, result, (uint32_t)c, arr);
         }
@@ -440,7 +451,7 @@ static void complete(napi_env env, napi_status status, void* data) {
   napi_delete_async_work(env, j->work);
   napi_delete_reference(env, j->ctx_ref);
   sets_free(&j->sets);
-  free(j->sm_idx.p); free(j->sm_sigs.p); free(j->sm_msgs.p);
+  free(j->sm_idx.p); free(j->sm_sigs.p); free(j->sm_msgs.p); free(j->sm_packed.p);
   free(j->out);
   free(j);
 }
@@ -478,14 +489,20 @@ static job* new_job(napi_env env, addon_ctx* ac, int op) {
 
 static void drop_job(job* j) {
   sets_free(&j->sets);
-  free(j->sm_idx.p); free(j->sm_sigs.p); free(j->sm_msgs.p);
+  free(j->sm_idx.p); free(j->sm_sigs.p); free(j->sm_msgs.p); free(j->sm_packed.p);
   free(j);
 }
 
 /* ---- exported functions ------------------------------------------------------------------- */
+static void pass_release(struct pass_s* p);
 static void ctx_finalize(napi_env env, void* data, void* hint) {
   (void)env; (void)hint;
   addon_ctx* ac = (addon_ctx*)data;
+  /* passes still referenced by a slot: one whose JS object is gone is freed here; one whose object
+   * lives on loses its context (its own finalizer frees it) -- in either order of the two finalizers
+   * (Node-API orders none of them at environment teardown) no pass reaches freed memory */
+  for (int k = 0; k < MAX_PASSES; ++k)
+    if (ac->slots[k].pass) pass_release(ac->slots[k].pass);
   if (ac->ctx) {
     for (int k = 0; k < MAX_PASSES; ++k) {
       if (ac->slots[k].sm) gbv_sm_batch_destroy(ac->ctx, ac->slots[k].sm);
@@ -754,7 +771,7 @@ static napi_value js_verify_same_message_multi(napi_env env, napi_callback_info 
   if (ac->closed) return rejected_closed(env);
   job* j = new_job(env, ac, OP_SAME_MESSAGE_MULTI);
   if (!j) return NULL;
-  if (!marshal_same_message(env, argv[1], &j->sets.call_off, &j->sm_idx, &j->sm_sigs, &j->sm_msgs, NULL)) {
+  if (!marshal_same_message(env, argv[1], &j->sets.call_off, &j->sm_idx, &j->sm_sigs, &j->sm_msgs, &j->sm_packed)) {
     drop_job(j);
     return NULL;
   }
@@ -762,7 +779,7 @@ static napi_value js_verify_same_message_multi(napi_env env, napi_callback_info 
 }
 
 /* ---- streamed passes ------------------------------------------------------------------------ */
-typedef struct {
+typedef struct pass_s {
   addon_ctx* ac;
   int slot;
   int has_sm, has_df;
@@ -851,27 +868,55 @@ static void pass_free(napi_env env, pass* p) {
   free(p);
 }
 
-/* The JS pass object is gone.  A pass whose waitPass is still running is freed by pass_complete; a
- * pass never waited (a broken caller: every submitted pass must be waited once) is waited here so
- * that its slot and batches are free again. */
+/* The context's finalizer lets go of a pass its slot still holds (see ctx_finalize). */
+static void pass_release(struct pass_s* p) {
+  if (p->queued) return;  /* its waitPass work owns it (torn down with the environment) */
+  if (p->external_gone) {
+    /* the reference to the context external is being torn down with it: only the memory is freed */
+    free(p->sm_off.p);
+    free(p->sm_packed.p);
+    free(p->sm_valid);
+    free(p->df_valid);
+    free(p);
+  } else {
+    p->ac = NULL;
+  }
+}
+
+/* The JS pass object is gone.  A finalizer touches neither the context nor the device (Node-API does
+ * not order finalizers at environment teardown, so the context may be freed already): a pass whose
+ * waitPass is still running is freed by pass_complete; a pass never waited (a broken caller: every
+ * submitted pass must be waited once) stays in its slot, marked, and the next submitPass or close()
+ * waits for it and frees it (reclaim_orphans); a pass whose context is gone is freed here. */
 static void pass_finalize(napi_env env, void* data, void* hint) {
   (void)hint;
   pass* p = (pass*)data;
-  if (p->queued && !p->done) {
+  if (!p->ac) {
+    pass_free(env, p);
+    return;
+  }
+  if (!p->done) {
     p->external_gone = 1;
     return;
   }
-  if (!p->queued) {
-    addon_ctx* ac = p->ac;
-    pass_slot* sl = &ac->slots[p->slot];
+  pass_free(env, p);
+}
+
+/* Free the slots of passes whose JS objects were dropped without waitPass (JS thread). */
+static void reclaim_orphans(napi_env env, addon_ctx* ac) {
+  for (int k = 0; k < MAX_PASSES; ++k) {
+    pass_slot* sl = &ac->slots[k];
+    pass* p = sl->pass;
+    if (!p || p->queued || !p->external_gone) continue;
     pthread_mutex_lock(&sl->mu);
     if (ac->ctx && p->has_sm && !p->rc_sm && sl->sm) gbv_sm_batch_wait(ac->ctx, sl->sm, NULL);
     if (ac->ctx && p->has_df && !p->rc_df && sl->vs) gbv_vs_batch_wait(ac->ctx, sl->vs, NULL);
     pthread_mutex_unlock(&sl->mu);
     sl->busy = 0;
+    sl->pass = NULL;
     ac->inflight--;
+    pass_free(env, p);
   }
-  pass_free(env, p);
 }
 
 /* submitPass(ctx, sameMessageCalls | null, defaultCalls | null): fill and submit both device batches of
@@ -887,6 +932,7 @@ static napi_value js_submit_pass(napi_env env, napi_callback_info info) {
     throw_rc(env, GBV_E_CLOSED, "QUEUE_ABORTED");
     return NULL;
   }
+  reclaim_orphans(env, ac);
   int k = 0;
   while (k < MAX_PASSES && ac->slots[k].busy) ++k;
   if (k == MAX_PASSES) {
@@ -961,6 +1007,7 @@ static napi_value js_submit_pass(napi_env env, napi_callback_info info) {
   free(sm_idx.p); free(sm_sigs.p); free(sm_msgs.p);
   sets_free(&df);
   sl->busy = 1;
+  sl->pass = p;
   ac->inflight++;
   napi_create_reference(env, argv[0], 1, &p->ctx_ref);
   napi_value ext;
@@ -988,6 +1035,7 @@ static void pass_execute(napi_env env, void* data) {
 static void pass_complete(napi_env env, napi_status status, void* data) {
   pass* p = (pass*)data;
   p->ac->slots[p->slot].busy = 0;
+  p->ac->slots[p->slot].pass = NULL;
   p->ac->inflight--;
   napi_value result, x;
   napi_create_object(env, &result);
@@ -1316,6 +1364,7 @@ static napi_value js_close(napi_env env, napi_callback_info info) {
     napi_resolve_deferred(env, d, u);
     return p;
   }
+  reclaim_orphans(env, ac);
   job* j = (job*)calloc(1, sizeof(job));
   j->op = OP_CLOSE;
   j->ac = ac;

@@ -16,7 +16,10 @@
 // jobs as one device batch, default jobs as another), and up to MAX_PASSES passes are on the device at
 // once (submitPass / waitPass), so consecutive gossip dispatches overlap.
 // Metrics: the reference's lodestar_bls_thread_pool_* families (metrics/lodestar.ts:401-504) plus
-// *_gpu_* ones, rendered in the Prometheus text format by metricsText().
+// *_gpu_* ones, rendered in the Prometheus text format by metricsText(), and -- when the node passes
+// its own families (o.metrics = metrics.blsThreadPool plus the two gpu families registered on
+// metrics.register, chain/bls/gpu/index.ts) -- fed into the node's registry as well, where /metrics
+// and the dashboards read them.
 "use strict";
 
 const MAX_SIGNATURE_SETS_PER_JOB = 128; // multithread/index.ts:56
@@ -113,8 +116,41 @@ class Family {
   }
 }
 
+// One family fed to the local registry and to the node's (prom-client style: inc(labels?, v?),
+// set(labels?, v) / set(v), observe(labels?, v) / observe(v)).
+class TeeFamily {
+  constructor(local, ext) {
+    this.local = local;
+    this.ext = ext;
+    this.name = local.name;
+  }
+  inc(labels, v) {
+    this.local.inc(labels, v);
+    if (typeof labels === "number" || labels === undefined) this.ext.inc(labels === undefined ? 1 : labels);
+    else this.ext.inc(labels, v === undefined ? 1 : v);
+  }
+  set(v, labels) {
+    this.local.set(v, labels);
+    if (labels) this.ext.set(labels, v);
+    else this.ext.set(v);
+  }
+  observe(v, labels) {
+    this.local.observe(v, labels);
+    if (labels) this.ext.observe(labels, v);
+    else this.ext.observe(v);
+  }
+  value(labels) {
+    return this.local.value(labels);
+  }
+  text() {
+    return this.local.text();
+  }
+}
+
 class BlsPoolMetrics {
-  constructor() {
+  /** @param {object} [external] the node's families by the reference's property names
+   * (metrics.blsThreadPool: totalSigSets, jobWaitTime, ...; plus gpuDevicePasses, gpuPassTime) */
+  constructor(external) {
     const p = "lodestar_bls_thread_pool_";
     const g = (n, h, l) => new Family("gauge", n, h, l);
     const hi = (n, h, b) => new Family("histogram", n, h, null, b);
@@ -141,6 +177,9 @@ class BlsPoolMetrics {
       gpuDevicePasses: new Family("counter", p + "gpu_device_passes_total", "Device passes (one or more jobs verified together)"),
       gpuPassTime: hi(p + "gpu_pass_time_seconds", "Device pass wall time, submit to results", [0.005, 0.01, 0.02, 0.05, 0.1, 0.3, 1]),
     };
+    if (external) {
+      for (const [k, f] of Object.entries(this.families)) if (external[k]) this.families[k] = new TeeFamily(f, external[k]);
+    }
     Object.assign(this, this.families);
   }
   text() {
@@ -148,11 +187,24 @@ class BlsPoolMetrics {
   }
 }
 
+/** The families a Lodestar node hands GpuBlsVerifier (chain/bls/gpu/index.ts): its blsThreadPool
+ * families (metrics/lodestar.ts:401-504) and the two *_gpu_* ones registered on metrics.register, the
+ * node's RegistryMetricCreator.  Null without metrics (the node runs without --metrics). */
+function nodeMetricFamilies(metrics) {
+  if (!metrics) return null;
+  const p = "lodestar_bls_thread_pool_";
+  return Object.assign({}, metrics.blsThreadPool, {
+    gpuDevicePasses: metrics.register.gauge({name: p + "gpu_device_passes_total", help: "Device passes (one or more jobs verified together)"}),
+    gpuPassTime: metrics.register.histogram({name: p + "gpu_pass_time_seconds", help: "Device pass wall time, submit to results",
+      buckets: [0.005, 0.01, 0.02, 0.05, 0.1, 0.3, 1]}),
+  });
+}
+
 // ---- the verifier --------------------------------------------------------------------------------
 class GpuBlsVerifier {
   /**
    * @param {object} o  {addon: the gbv addon (or a stand-in with the same functions), device?: number,
-   *                    ctx?: an already open context}
+   *                    ctx?: an already open context, metrics?: the node's metric families (BlsPoolMetrics)}
    */
   constructor(o) {
     this.addon = o.addon;
@@ -165,7 +217,14 @@ class GpuBlsVerifier {
     this.closed = false;
     this.idleWaiters = [];
     this.runScheduled = false;
-    this.metrics = new BlsPoolMetrics();
+    this.metrics = new BlsPoolMetrics(o.metrics || null);
+    if (o.metrics && o.metrics.queueLength && o.metrics.queueLength.addCollect) {
+      // read at scrape time, as the pool does (multithread/index.ts:141-146)
+      o.metrics.queueLength.addCollect(() => {
+        this.metrics.queueLength.set(this.jobs.length);
+        this.metrics.workersBusy.set(this.passesBusy);
+      });
+    }
     this.devicePasses = 0;
   }
 
@@ -267,6 +326,28 @@ class GpuBlsVerifier {
       out.set(r, o);
       o += r.length;
     }
+    return out;
+  }
+
+  /** The IBlsVerifier call shape (chain/bls/gpu/index.ts, validation/attestation.ts:131-137): one
+   * {index, signature} (+ publicKey, unused) per set -> boolean[], marshalled as the packed form: one
+   * Uint32Array of indices and one signature buffer per call, so the addon copies two buffers instead
+   * of reading 2n properties.  A signature of another length than 96 bytes stays zero in the buffer:
+   * a bad encoding, false for that set alone -- as Signature.fromBytes throwing inside the pool's
+   * aggregate sends the chunk to the per-set retry, where that set fails (jobItem.ts:93-125). */
+  async verifySameMessageSets(sets, message, opts = {}) {
+    const n = sets.length;
+    const indices = new Uint32Array(n);
+    const signatures = new Uint8Array(96 * n);
+    for (let i = 0; i < n; ++i) {
+      const s = sets[i];
+      if (!(s.index >= 0)) throw Object.assign(new TypeError("same-message set without a validator index"), {code: "GBV_E_ARG"});
+      indices[i] = s.index;
+      if (s.signature.length === 96) signatures.set(s.signature, 96 * i);
+    }
+    const r = await this.verifySignatureSetsSameMessage({indices, signatures}, message, opts);
+    const out = new Array(n);
+    for (let i = 0; i < n; ++i) out[i] = r[i] === 1;
     return out;
   }
 
@@ -429,6 +510,7 @@ class GpuBlsVerifier {
 module.exports = {
   GpuBlsVerifier,
   BlsPoolMetrics,
+  nodeMetricFamilies,
   QueueError,
   chunkifyMaximizeChunkSize,
   MAX_SIGNATURE_SETS_PER_JOB,

@@ -41,8 +41,11 @@ class FakeAddon {
     if (this.closed) throw Object.assign(new Error("QUEUE_ABORTED"), {code: "QUEUE_ABORTED"});
     const rec = {sm: sm ? sm.map((c) => c.sets.length) : null, df: df ? df.map((c) => c.length) : null};
     this.passes.push(rec);
+    // a packed chunk {indices, signatures, length} answers with a Uint8Array, like the addon
+    const smRes = (c) => (Array.isArray(c.sets) ? c.sets.map((s) => this.valid(s))
+      : Uint8Array.from({length: c.sets.length}, (_, i) => (c.sets.signatures[96 * i] === 1 ? 1 : 0)));
     const res = {
-      sameMessage: sm ? sm.map((c) => c.sets.map((s) => this.valid(s))) : null,
+      sameMessage: sm ? sm.map(smRes) : null,
       default: df
         ? df.map((c) =>
           c.some((s) => s.indices !== undefined && s.indices.length === 0)
@@ -188,6 +191,89 @@ async function cpu() {
   report.metricValues = v.metrics.totalSigSets.value() === 4 && v.metrics.errorAggregateSignatureSetsCount.value({type: "default"}) === 1;
 }
 
+// ---- a stand-in of the node's metrics: prom-client-shaped families on a registry, the blsThreadPool
+// object built with the reference's names (metrics/metrics/lodestar.ts:401-504)
+class PromFamily {
+  constructor(kind, cfg) {
+    this.kind = kind;
+    this.name = cfg.name;
+    this.series = new Map();
+    this.collects = [];
+  }
+  _s(labels) {
+    const k = JSON.stringify(labels || {});
+    if (!this.series.has(k)) this.series.set(k, {value: 0, count: 0});
+    return this.series.get(k);
+  }
+  inc(a, b) {
+    if (typeof a === "object") this._s(a).value += b === undefined ? 1 : b;
+    else this._s(null).value += a === undefined ? 1 : a;
+  }
+  set(a, b) {
+    if (typeof a === "object") this._s(a).value = b;
+    else this._s(null).value = a;
+  }
+  observe(a, b) {
+    const s = typeof a === "object" ? this._s(a) : this._s(null);
+    s.value += typeof a === "object" ? b : a;
+    s.count += 1;
+  }
+  addCollect(fn) {
+    this.collects.push(fn);
+  }
+  total() {
+    let t = 0;
+    for (const s of this.series.values()) t += this.kind === "histogram" ? s.count : s.value;
+    return t;
+  }
+}
+function fakeNodeMetrics() {
+  const families = new Map();
+  const mk = (kind) => (cfg) => {
+    const f = new PromFamily(kind, cfg);
+    families.set(cfg.name, f);
+    return f;
+  };
+  const register = {gauge: mk("gauge"), histogram: mk("histogram"), families};
+  const p = "lodestar_bls_thread_pool_";
+  const g = (name) => register.gauge({name});
+  const h = (name) => register.histogram({name});
+  const blsThreadPool = {
+    jobsWorkerTime: g(p + "time_seconds_sum"), successJobsSignatureSetsCount: g(p + "success_jobs_signature_sets_count"),
+    errorAggregateSignatureSetsCount: g(p + "error_aggregate_signature_sets_count"), errorJobsSignatureSetsCount: g(p + "error_jobs_signature_sets_count"),
+    jobWaitTime: h(p + "queue_job_wait_time_seconds"), queueLength: g(p + "queue_length"), workersBusy: g(p + "workers_busy"),
+    totalJobsGroupsStarted: g(p + "job_groups_started_total"), totalJobsStarted: g(p + "jobs_started_total"),
+    totalSigSetsStarted: g(p + "sig_sets_started_total"), batchRetries: g(p + "batch_retries_total"), batchSigsSuccess: g(p + "batch_sigs_success_total"),
+    sameMessageRetryJobs: g(p + "same_message_jobs_retries_total"), sameMessageRetrySets: g(p + "same_message_sets_retries_total"),
+    latencyToWorker: h(p + "latency_to_worker"), latencyFromWorker: h(p + "latency_from_worker"),
+    mainThreadDurationInThreadPool: h(p + "main_thread_time_seconds"), timePerSigSet: h("lodestar_bls_worker_thread_time_per_sigset_seconds"),
+    totalSigSets: g(p + "sig_sets_total"), prioritizedSigSets: g(p + "prioritized_sig_sets_total"), batchableSigSets: g(p + "batchable_sig_sets_total"),
+  };
+  return {blsThreadPool, register};
+}
+
+async function cpuNodeMetrics() {
+  // the binding's wiring (chain/bls/gpu/index.ts): the node's families in, fed by every call
+  const node = fakeNodeMetrics();
+  const a = new FakeAddon();
+  const v = new V.GpuBlsVerifier({addon: a, metrics: V.nodeMetricFamilies(node)});
+  await v.verifySignatureSets([set(1), set(1)], {priority: true});
+  await v.verifySignatureSets([set(1), set(0)], {batchable: true});
+  const sm = await v.verifySameMessageSets([smSet(1, 3), smSet(0, 4), smSet(1, 5)], msg);
+  const short = await v.verifySameMessageSets([{index: 1, signature: new Uint8Array(32)}], msg);
+  for (const f of node.blsThreadPool.queueLength.collects) f();  // a scrape
+  const fam = node.register.families;
+  const got = (n) => (fam.has(n) ? fam.get(n).total() : -1);
+  const p = "lodestar_bls_thread_pool_";
+  report.nodeMetricsFed = got(p + "sig_sets_total") === 4 && got(p + "prioritized_sig_sets_total") === 2 &&
+    got(p + "batchable_sig_sets_total") === 2 && got(p + "jobs_started_total") === 4 && got(p + "sig_sets_started_total") === 8 &&
+    got(p + "job_groups_started_total") >= 2 && got(p + "queue_job_wait_time_seconds") === 4 && got(p + "gpu_device_passes_total") >= 2 &&
+    got(p + "gpu_pass_time_seconds") >= 2 && got(p + "same_message_jobs_retries_total") === 2 && got(p + "time_seconds_sum") > 0;
+  report.nodeMetricsScrape = fam.get(p + "queue_length").series.size === 1 && fam.get(p + "workers_busy").series.size === 1;
+  // the IBlsVerifier-shaped same-message call: objects in, the packed device form, boolean[] out
+  report.sameMessageObjectsPacked = JSON.stringify(sm) === "[true,false,true]" && JSON.stringify(short) === "[false]";
+}
+
 // ---- GPU: the real addon --------------------------------------------------------------------
 const toSets = (c) =>
   c.sets.map((s) => {
@@ -246,7 +332,10 @@ async function gpu(fixPath) {
 
 (async () => {
   const mode = process.argv[2];
-  if (mode === "cpu") await cpu();
+  if (mode === "cpu") {
+    await cpu();
+    await cpuNodeMetrics();
+  }
   else await gpu(process.argv[3]);
   process.stdout.write(JSON.stringify(report) + "\n");
 })().catch((e) => {

@@ -315,7 +315,9 @@ def api_path_js(call_off, idx, sigs, msgs, key_pks, log, reps=3):
         r["how"] = ("node addon/bench_api.js: every gossip call of the C2 workload through GpuBlsVerifier.verifySignatureSetsSameMessage "
                     "(addon/gpu_bls_verifier.js) over the Node-API addon, all promises awaited, every boolean checked; "
                     "'packed' = {indices: Uint32Array, signatures: Uint8Array} per call, 'objects' = one {index, signature} per set "
-                    "(built before the clock); best of %d; its own device context beside the bench's" % reps)
+                    "(built before the clock); 'ibls' = the IBlsVerifier shape the Lodestar binding uses (chain/bls/gpu/index.ts): one "
+                    "{publicKey, index, signature} object per set, packed per call into the device form INSIDE the clock, boolean[] out "
+                    "(verifySameMessageSets); best of %d; its own device context beside the bench's" % reps)
         return r
     finally:
         shutil.rmtree(d, ignore_errors=True)
@@ -904,8 +906,8 @@ def main():
         log("api stream: %s sets/s over %d sets in %d device passes" % (api_stream, api_stream_n, api_stream_passes))
     api_js = api_path_js(call_off, idx, sigs, msgs, key_pks, log) if do_api and world == 1 else None
     if api_js:
-        log("api stream (js): packed %s, objects %s sets/s, lone call %s ms" % (api_js["packed"]["sets_per_s"], api_js["objects"]["sets_per_s"],
-                                                                               api_js["lone_call_p50_ms"]))
+        log("api stream (js): packed %s, IBlsVerifier-shaped %s, objects %s sets/s, lone call %s ms" % (
+            api_js["packed"]["sets_per_s"], api_js["ibls"]["sets_per_s"], api_js["objects"]["sets_per_s"], api_js["lone_call_p50_ms"]))
 
     # per launch: algorithmic MACs of the sets one k_sm_prepare launch processes / its average duration
     units_per_launch = n_mine / max(prep_launches_per_step, 1)
@@ -1010,6 +1012,7 @@ def main():
                      "sample_sets": api_stream_n, "device_passes": api_stream_passes,
                      "oneshot_sets_per_s": api_rate, "oneshot_how": "one gbv_verify_same_message_multi call from host buffers"},
         "api_path_js_sets_per_s": api_js["packed"]["sets_per_s"] if api_js else None,
+        "api_path_js_iblsverifier_shaped_sets_per_s": api_js["ibls"]["sets_per_s"] if api_js and "ibls" in api_js else None,
         "api_path_js": api_js,
         "roofline": roofline,
         "cpu_baseline": cpu,

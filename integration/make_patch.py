@@ -424,16 +424,12 @@ GPU_INDEX_TS = '''/**
  * ISignatureSet.index / .indices select keys from the GPU's copy of index2pubkey; a set without
  * indices (a key from the message itself, e.g. a BLS-to-execution change) passes its compressed key.
  */
+import {createRequire} from "node:module";
 import {PublicKey, aggregatePublicKeys} from "@chainsafe/blst";
 import {ISignatureSet, Index2PubkeyCache, SignatureSetType, index2pubkeyListeners} from "@lodestar/state-transition";
 import {Logger} from "@lodestar/utils";
 import {Metrics} from "../../../metrics/index.js";
 import {IBlsVerifier, VerifySignatureOpts} from "../interface.js";
-
-// eslint-disable-next-line @typescript-eslint/no-require-imports
-const addon = require("./gbv_addon.node");
-// eslint-disable-next-line @typescript-eslint/no-require-imports
-const {GpuBlsVerifier: QueueOverAddon} = require("./gpu_bls_verifier.js");
 
 type IndexFormSet =
   | {index: number; signingRoot: Uint8Array; signature: Uint8Array}
@@ -443,8 +439,21 @@ type IndexFormSet =
 /** keys per addPubkeys call when the whole table is loaded */
 const LOAD_BATCH = 1 << 16;
 
+/** the job queue of gpu_bls_verifier.js (its GpuBlsVerifier class) as this binding uses it */
+interface GpuQueue {
+  addPubkeys(firstIndex: number, pk48s: Uint8Array, validate: boolean): Uint8Array;
+  canAcceptWork(): boolean;
+  verifySignatureSets(sets: IndexFormSet[], opts: VerifySignatureOpts): Promise<boolean>;
+  verifySameMessageSets(
+    sets: {signature: Uint8Array; index?: number}[],
+    message: Uint8Array,
+    opts: Omit<VerifySignatureOpts, "verifyOnMainThread">
+  ): Promise<boolean[]>;
+  close(): Promise<void>;
+}
+
 export class GpuBlsVerifier implements IBlsVerifier {
-  private readonly queue;
+  private readonly queue: GpuQueue;
   private readonly logger: Logger;
   private readonly onNewPubkeys = (firstIndex: number, pubkeys: Uint8Array[]): void => {
     this.queue.addPubkeys(firstIndex, Buffer.concat(pubkeys), false);
@@ -452,7 +461,14 @@ export class GpuBlsVerifier implements IBlsVerifier {
 
   constructor(opts: {blsGpuDevice?: number}, modules: {logger: Logger; metrics: Metrics | null}) {
     this.logger = modules.logger;
-    this.queue = new QueueOverAddon({addon, device: opts.blsGpuDevice ?? 0});
+    // The native addon and its queue load here, when a node is started with --chain.blsVerifyOnGpu,
+    // never at import time: chain/bls re-exports this class, and this package is an ES module.
+    const require = createRequire(import.meta.url);
+    const addon = require("./gbv_addon.node");
+    const {GpuBlsVerifier: QueueOverAddon, nodeMetricFamilies} = require("./gpu_bls_verifier.js");
+    // the queue feeds the node's lodestar_bls_thread_pool_* families (metrics/lodestar.ts:401-504) and
+    // two *_gpu_* ones registered on metrics.register; queue length / busy passes are read at scrape time
+    this.queue = new QueueOverAddon({addon, device: opts.blsGpuDevice ?? 0, metrics: nodeMetricFamilies(modules.metrics)});
     index2pubkeyListeners.add(this.onNewPubkeys);
   }
 
@@ -474,16 +490,14 @@ export class GpuBlsVerifier implements IBlsVerifier {
     return this.queue.verifySignatureSets(sets.map(toIndexForm), opts);
   }
 
+  /** validation/attestation.ts:131-137 hands one {publicKey, signature, index} per set: the queue packs
+   * them into one Uint32Array of indices and one signature buffer per call (the addon's packed form) */
   async verifySignatureSetsSameMessage(
     sets: {publicKey: PublicKey; signature: Uint8Array; index?: number}[],
     message: Uint8Array,
     opts: Omit<VerifySignatureOpts, "verifyOnMainThread"> = {}
   ): Promise<boolean[]> {
-    const indexed = sets.map((s) => {
-      if (s.index === undefined) throw Error("GpuBlsVerifier: same-message set without a validator index");
-      return {index: s.index, signature: s.signature};
-    });
-    return this.queue.verifySignatureSetsSameMessage(indexed, message, opts);
+    return this.queue.verifySameMessageSets(sets, message, opts);
   }
 
   async close(): Promise<void> {

@@ -51,6 +51,10 @@ def test_js_verifier_queue_semantics_without_gpu():
     assert "fatal" not in r, r
     assert all(v is True or v == [True, False, False] or v == [True, False, True] for v in r.values()), r
     assert r["basic"] == [True, False, False] and r["sameMessage"] == [True, False, True]
+    # the binding's wiring: the node's own metric families (metrics.blsThreadPool + the gpu ones on
+    # metrics.register) are fed by every call and scraped through queueLength.addCollect; the
+    # IBlsVerifier-shaped same-message call packs its objects into the device form
+    assert r["nodeMetricsFed"] is True and r["nodeMetricsScrape"] is True and r["sameMessageObjectsPacked"] is True
 
 
 @pytest.mark.gpu

@@ -30,3 +30,37 @@ def test_patch_applies_to_reference(tmp_path):
     assert "class GpuBlsVerifier implements IBlsVerifier" in gpu
     chain = (tmp_path / "packages/beacon-node/src/chain/chain.ts").read_text()
     assert "opts.blsVerifyOnGpu" in chain and "loadIndex2pubkey" in chain
+
+
+def _added_file(text, rel):
+    """The lines of a file the patch adds (its hunk against /dev/null-style empty a/ side)."""
+    out, on = [], False
+    for l in text.splitlines():
+        if l.startswith("+++ b/"):
+            on = l[6:].strip() == rel
+            continue
+        if on and l.startswith("diff "):
+            break
+        if on and l.startswith("+"):
+            out.append(l[1:])
+    return "\n".join(out)
+
+
+def test_gpu_binding_loads_native_code_lazily():
+    """chain/bls/index.ts re-exports GpuBlsVerifier and packages/beacon-node is an ES module
+    ("type": "module"): the binding must not `require` at module top level (undefined in ESM, and a
+    missing .node file would break every node importing chain/bls).  The addon and the queue load in
+    the constructor through createRequire(import.meta.url); the same-message call uses the packed
+    form; the node's metric families go to the queue."""
+    gpu = _added_file(open(PATCH).read(), "packages/beacon-node/src/chain/bls/gpu/index.ts")
+    assert "class GpuBlsVerifier implements IBlsVerifier" in gpu
+    top, depth = [], 0
+    for line in gpu.splitlines():  # statements at brace depth 0 (module scope)
+        if depth == 0:
+            top.append(line)
+        depth += line.count("{") - line.count("}")
+    assert not any("require(" in l for l in top), [l for l in top if "require(" in l]
+    ctor = gpu[gpu.index("  constructor("):gpu.index("  loadIndex2pubkey(")]
+    assert "createRequire(import.meta.url)" in ctor and 'require("./gbv_addon.node")' in ctor
+    assert "nodeMetricFamilies(modules.metrics)" in ctor
+    assert "this.queue.verifySameMessageSets(sets, message, opts)" in gpu
