@@ -754,6 +754,8 @@ def main():
     ap.add_argument("--c3-calls", type=int, default=512, help="128-set calls per C3 device pass")
     ap.add_argument("--c4-blocks", type=int, default=64, help="blocks per C4 device pass (range-sync segment)")
     ap.add_argument("--c4e-blocks", type=int, default=16, help="electra blocks per C4e device pass")
+    ap.add_argument("--tune", action="append", default=[], metavar="NAME=VALUE",
+                    help="gbv_tune setting applied before anything runs (experiments; include/gbv.h lists the names)")
     ap.add_argument("--shard-calls", type=int, default=512,
                     help="vs-shard: 128-member aggregate sets / 128 in the ONE sharded verifySignatureSets call")
     args = ap.parse_args()
@@ -798,6 +800,10 @@ def main():
     from lodestar_amd.build import build
     build()
     v = GpuBlsVerifier(local_rank)
+    for kv in args.tune:
+        name, val = kv.split("=", 1)
+        v.tune(name, int(val))
+        log("tune %s = %s" % (name, val))
     sks, key_pks = build_table(v, log)
     sk_ints = [interop_sk_int(i) for i in range(N_KEYS)]
     if args.mode == "vs-shard":

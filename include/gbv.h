@@ -86,16 +86,18 @@ int gbv_pubkeys_append(gbv_ctx* ctx, uint32_t first_index, const uint8_t* pk48, 
 /* Number of table slots currently allocated (max index + 1). */
 size_t gbv_pubkeys_count(gbv_ctx* ctx);
 /* 1 when the per-slot comb tables for r*pk are built and used by the same-message path (default;
- * GBV_COMB=0 in the environment at gbv_init, or a failed allocation, selects the ladder; results are
- * identical either way).  No reference counterpart: an accelerator of index2pubkey. */
+ * gbv_tune(ctx, "comb", 0) before the first gbv_pubkeys_append, or a failed allocation, selects the
+ * ladder; results are identical either way).  No reference counterpart: an accelerator of index2pubkey. */
 int gbv_comb_enabled(gbv_ctx* ctx);
-/* Change one of the context's pipeline settings, which gbv_init reads once from the environment
- * (GBV_MSM_MIN, GBV_MSM_COOLDOWN, GBV_SEGMENTS): "msm_min" (segments of at least this many sets
- * form their G2 sum with the bucket MSM; 0 = never), "msm_cooldown" (submits without the MSM after
- * a failing MSM segment), "segments" (pipeline segments per same-message batch), "kprof" (1: record
- * per-kernel timings, gbv_last_ops).  Results are
- * identical for every value; tests use it to reach each pipeline form on small batches.  No
- * reference counterpart.  GBV_E_ARG for an unknown name. */
+/* Change a pipeline setting (no reference counterpart; results are identical for every value -- tests
+ * and experiments use it to reach each pipeline form; nothing is read from the environment except
+ * GBV_SYNC_DEBUG, a per-launch synchronisation for debugging).  Per context: "msm_min" (segments of at
+ * least this many sets form their G2 sum with the bucket MSM; 0 = never), "msm_cooldown" (submits
+ * without the MSM after a failing MSM segment), "segments" (pipeline segments per same-message
+ * batch), "kprof" (1: record per-kernel timings, gbv_last_ops), "comb" (0: r*pk by the ladder; 1 only
+ * before any key is appended).  Process-wide launch shapes: "hash_pair_max",
+ * "hash_quad_max", "hash_coop_max", "prepare_split_max", "chunk_finish_wave_max", "vs_pre_max",
+ * "vs_fs_maxc", "vs_quad_max", "vs_pair_max".  GBV_E_ARG for an unknown name. */
 int gbv_tune(gbv_ctx* ctx, const char* name, uint32_t value);
 
 /* IBlsVerifier.verifySignatureSets (interface.ts:47; multithread/index.ts:157-207).

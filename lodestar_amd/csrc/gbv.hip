@@ -232,16 +232,6 @@ int gbv_init(int device, gbv_ctx** out) {
     delete c;
     return GBV_E_DEVICE;
   }
-  // the context's own settings, read once here (gbv_tune changes them for tests)
-  auto rd = [](const char* name, uint32_t& v) {
-    if (const char* e = getenv(name)) v = (uint32_t)strtoul(e, nullptr, 10);
-  };
-  rd("GBV_MSM_MIN", c->msm_min);
-  rd("GBV_MSM_COOLDOWN", c->msm_cooldown_len);
-  rd("GBV_SEGMENTS", c->segments);
-  uint32_t comb = 1;
-  rd("GBV_COMB", comb);
-  c->comb_on = comb != 0;
   *out = c;
   return GBV_OK;
 }
@@ -282,7 +272,8 @@ int gbv_tune(gbv_ctx* c, const char* name, uint32_t value) {
   else if (!strcmp(name, "msm_cooldown")) c->msm_cooldown_len = value;
   else if (!strcmp(name, "segments")) c->segments = std::max<uint32_t>(value, 1);
   else if (!strcmp(name, "kprof")) c->kprof_on = value != 0;
-  else return gbv_fail(c, GBV_E_ARG, std::string("unknown setting: ") + name);
+  else if (!strcmp(name, "comb")) c->comb_on = value != 0 && (c->comb_on || c->table_n == 0);  // off at any time; on before ingest only
+  else if (!tuning_set(name, value)) return gbv_fail(c, GBV_E_ARG, std::string("unknown setting: ") + name);
   return GBV_OK;
 }
 
@@ -1180,22 +1171,23 @@ static Tuning g_tuning;
 static std::once_flag g_tuning_once;
 const Tuning& tuning() { return g_tuning; }
 void tuning_load() {
+  // the only setting taken from the environment: a debugging aid that changes timing, never results
   std::call_once(g_tuning_once, [] {
-    auto rd = [](const char* name, uint32_t& v) {
-      if (const char* e = getenv(name)) v = (uint32_t)strtoul(e, nullptr, 10);
-    };
-    rd("GBV_HASH_PAIR_MAX", g_tuning.hash_pair_max);
-    rd("GBV_HASH_QUAD_MAX", g_tuning.hash_quad_max);
-    rd("GBV_HASH_COOP_MAX", g_tuning.hash_coop_max);
-    rd("GBV_VS_SIG_QUAD_MAX", g_tuning.vs_sig_quad_max);
-    rd("GBV_PREPARE_SPLIT_MAX", g_tuning.prepare_split_max);
-    rd("GBV_CHUNK_FINISH_WAVE_MAX", g_tuning.chunk_finish_wave_max);
-    rd("GBV_VS_PRE_MAX", g_tuning.vs_pre_max);
-    rd("GBV_VS_FS_MAXC", g_tuning.vs_fs_maxc);
-    rd("GBV_VS_QUAD_MAX", g_tuning.vs_quad_max);
-    rd("GBV_VS_PAIR_MAX", g_tuning.vs_pair_max);
-    rd("GBV_SYNC_DEBUG", g_tuning.sync_debug);
+    if (const char* e = getenv("GBV_SYNC_DEBUG")) g_tuning.sync_debug = (uint32_t)strtoul(e, nullptr, 10);
   });
+}
+bool tuning_set(const char* name, uint32_t v) {
+  struct { const char* n; uint32_t* p; } tab[] = {
+      {"hash_pair_max", &g_tuning.hash_pair_max}, {"hash_quad_max", &g_tuning.hash_quad_max}, {"hash_coop_max", &g_tuning.hash_coop_max},
+      {"prepare_split_max", &g_tuning.prepare_split_max}, {"chunk_finish_wave_max", &g_tuning.chunk_finish_wave_max},
+      {"vs_pre_max", &g_tuning.vs_pre_max}, {"vs_fs_maxc", &g_tuning.vs_fs_maxc}, {"vs_quad_max", &g_tuning.vs_quad_max},
+      {"vs_pair_max", &g_tuning.vs_pair_max}};
+  for (auto& t : tab)
+    if (!strcmp(name, t.n)) {
+      *t.p = v;
+      return true;
+    }
+  return false;
 }
 
 thread_local KProf* t_kprof = nullptr;

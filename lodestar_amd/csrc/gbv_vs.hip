@@ -50,7 +50,7 @@ struct gbv_vs_batch {
   G1J* rP = nullptr;
   G2J* rS = nullptr;
   uint8_t* status = nullptr;
-  uint8_t* sig_st = nullptr;  // "pre" mode: the signature verdicts alone (k_vs_sig_pre), read by k_vs_chunk_s_miller
+  uint8_t* sig_st = nullptr;  // "pre" mode: the signature verdicts alone (k_vs_sig_pre_quad), read by k_vs_chunk_s_miller
   Fp12* F = nullptr;
   G2J* Hpre = nullptr;        // per set: Q0 + Q1 before the cofactor clearing (small passes)
   G2A* Sd = nullptr;          // "pre" mode on lane quads: the decoded signatures (k_vs_sig_decode)
@@ -70,7 +70,7 @@ struct gbv_vs_batch {
   hipEvent_t ev[7] = {};
   hipEvent_t done = nullptr;
   hipEvent_t copied = nullptr;  // the last fill's input copy (stream A); see gbv_sm_batch::copied
-  hipEvent_t pre = nullptr;     // "pre" mode: k_vs_sig_pre done (stream 5)
+  hipEvent_t pre = nullptr;     // "pre" mode: k_vs_sig_pre_quad done (stream 5)
   bool in_flight = false;
   int tail = 0;
   KProf prof;  // per-kernel events of the last submit / partial (ctx kprof_on)
@@ -289,7 +289,7 @@ static int vs_fill(gbv_ctx* c, gbv_vs_batch* b, size_t n_calls, const uint32_t* 
   return GBV_OK;
 }
 
-// "pre" mode for passes of at most tuning().vs_pre_max sets: k_vs_sig_pre + k_vs_pk_rand in place of
+// "pre" mode for passes of at most tuning().vs_pre_max sets: k_vs_sig_decode + k_vs_sig_pre_quad and k_vs_pk_rand_quad in place of
 // k_vs_hash_sig's signature roles
 static bool vs_pre_on(const gbv_vs_batch* b) { return b->n <= tuning().vs_pre_max; }
 

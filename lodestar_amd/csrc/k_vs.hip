@@ -216,35 +216,11 @@ __global__ void GBV_KERNEL_ATTR k_vs_hash_sig(uint32_t n, uint32_t nb, uint32_t 
 }
 
 // Small passes, latency form ("pre" mode, gbv_vs.hip): the signature work that needs no pubkey runs
-// on its own stream beside the pubkey aggregation -- blocks [0, nsig) decode and group-check each
-// signature (status = its verdict), blocks [nsig, 2 nsig) decode it again and form r_i sig_i
-// (randomize_g2: the same r_i = a - b x^2 split as randomize_pair_jac) -- and k_vs_pk_rand, after the
-// aggregation and these, takes the pubkey, merges its verdict and forms r_i pk_i.  The aggregation
-// (an Electra block's committee sums: ~3.7 ms) then no longer sits in front of the signature chain.
-__global__ void GBV_KERNEL_ATTR k_vs_sig_pre(uint32_t n, const uint8_t* __restrict__ sig, uint32_t sig_stride, const uint32_t* __restrict__ sig_len,
-                                             Seed seed, uint32_t nonce, G2J* __restrict__ rS_out, uint8_t* __restrict__ status,
-                                             uint8_t* __restrict__ sig_st) {
-  const uint32_t nsig = (n + 63) / 64;
-  uint32_t blk = blockIdx.x;
-  const bool rand = blk >= nsig;
-  if (rand) blk -= nsig;
-  const uint32_t i = blk * 64 + threadIdx.x;
-  if (i >= n) return;
-  G2A s;
-  const uint8_t ds = g2_decode(s, sig + (size_t)sig_stride * i, sig_len[i]);
-  if (!rand) {
-    const uint8_t st = (ds != PT_OK || !g2_in_subgroup(s)) ? SET_BAD_SIG : SET_OK;
-    status[i] = st;
-    sig_st[i] = st;  // a copy k_vs_pk_rand does not touch (k_vs_chunk_s_miller reads it meanwhile)
-    return;
-  }
-  if (ds != PT_OK) return;
-  const uint64_t r = prf_scalar(seed, i, nonce);
-  G2J rs;
-  if (!randomize_g2(s, r, &rs)) rs = g2_mul_u64(s, r);  // unreachable for subgroup points
-  rS_out[i] = rs;
-}
-
+// on its own stream beside the pubkey aggregation -- k_vs_sig_decode decodes each signature, then the
+// quad roles below check it and form r_i sig_i (the same r_i = a - b x^2 split as randomize_pair_jac)
+// -- and k_vs_pk_rand_quad, after the aggregation and these, takes the pubkey, merges its verdict and
+// forms r_i pk_i.  The aggregation (an Electra block's committee sums: ~3.7 ms) then no longer sits in
+// front of the signature chain.
 // The same two roles on lane quads (quad_g2.h), one quad per set and role: blocks [0, nq) check,
 // blocks [nq, 2 nq) randomise, 16 sets per block.  The signatures were decoded by k_vs_sig_decode (one
 // thread each: the square root is two Fp exponentiations in a row, nothing for a quad to share); the
@@ -329,48 +305,11 @@ void launch_sm_prep_roles_quad(hipStream_t s, uint32_t base, uint32_t n, const u
   GBV_LAUNCH("k_sm_prep_roles_quad", k_sm_prep_roles_quad, dim3(2 * ((n + 15) / 16)), dim3(64), s, n, base, n, idx, table, table_ok, table_n, comb, comb_ok, seed, nonce, S, status, sub_ok, Sh, Ph);
 }
 
-// The pubkey half (stream A, after the aggregation and k_vs_sig_pre): a rejected signature's verdict
-// stands (it wins over a bad pubkey, as in k_vs_hash_sig); otherwise the pubkey's verdict is merged
-// and r_i pk_i formed.  Raw pubkeys (PublicKey.fromBytes(pk, true)) are decoded and group-checked here.
-__global__ void GBV_KERNEL_ATTR k_vs_pk_rand(uint32_t n, const uint32_t* __restrict__ set_off, const uint32_t* __restrict__ arena,
-                                             const uint8_t* __restrict__ raw_flag, const uint8_t* __restrict__ raw_pk48,
-                                             const G1A* __restrict__ table, const uint8_t* __restrict__ table_ok,
-                                             const G1J* __restrict__ pk_agg, const uint8_t* __restrict__ pk_st, Seed seed, uint32_t nonce,
-                                             G1J* __restrict__ rP_out, uint8_t* __restrict__ status) {
-  const uint32_t i = blockIdx.x * 64 + threadIdx.x;
-  if (i >= n || status[i] != SET_OK) return;
-  bool ok = true, jac = false;
-  G1A pa{fp_zero(), fp_zero()};
-  G1J pj;
-  if (raw_flag[i]) {
-    ok = g1_decompress(pa, raw_pk48 + 48ull * i) == PT_OK && g1_in_subgroup(pa);
-  } else {
-    const uint32_t b = set_off[i], e = set_off[i + 1];
-    if (e - b == 1) {
-      const uint32_t k = arena[b];
-      pa = table[k];
-      ok = table_ok[k] != 0;
-    } else if (e == b) {
-      ok = false;  // empty aggregate: its call is rejected on the host, never verified
-    } else {
-      pj = pk_agg[i];
-      jac = true;
-      ok = pk_st[i] == SET_OK;
-    }
-  }
-  if (ok && jac) ok = jac_to_aff(pa, pj);  // an OK aggregate is never infinity (k_vs_agg)
-  if (!ok) {
-    status[i] = SET_BAD_PK;
-    return;
-  }
-  const uint64_t r = prf_scalar(seed, i, nonce);
-  G1J rp;
-  if (!randomize_g1(pa, r, &rp)) rp = g1_mul_u64(pa, r);
-  rP_out[i] = rp;
-}
-
-// k_vs_pk_rand on lane quads (small passes): the same pubkey fetch and verdict merge on every lane of
-// the quad, r_i pk_i by quad_g2.h's G1 ladder (3 + 5 product rounds a step against 18 products).
+// The pubkey half on lane quads (stream A, after the aggregation and the signature roles): a rejected
+// signature's verdict stands (it wins over a bad pubkey, as in k_vs_hash_sig); otherwise the pubkey's
+// verdict is merged and r_i pk_i formed by quad_g2.h's G1 ladder (3 + 5 product rounds a step against
+// 18 products), the same pubkey fetch on every lane of the quad.  Raw pubkeys
+// (PublicKey.fromBytes(pk, true)) are decoded and group-checked here.
 __global__ void GBV_QUAD_ATTR k_vs_pk_rand_quad(uint32_t n, const uint32_t* __restrict__ set_off, const uint32_t* __restrict__ arena,
                                                   const uint8_t* __restrict__ raw_flag, const uint8_t* __restrict__ raw_pk48,
                                                   const G1A* __restrict__ table, const uint8_t* __restrict__ table_ok,
@@ -501,22 +440,13 @@ void launch_vs_hash_sig(hipStream_t s, uint32_t n, const uint8_t* msgs32, const 
 
 void launch_vs_sig_pre(hipStream_t s, uint32_t n, const uint8_t* sig, uint32_t sig_stride, const uint32_t* sig_len, const Seed& seed,
                        uint32_t nonce, G2J* rS, uint8_t* status, uint8_t* sig_st, G2A* Sd, uint8_t* dec_st) {
-  if (n <= tuning().vs_sig_quad_max) {
-    launch_vs_sig_decode(s, n, sig, sig_stride, sig_len, Sd, dec_st);
-    GBV_LAUNCH("k_vs_sig_pre_quad", k_vs_sig_pre_quad, dim3(2 * ((n + 15) / 16)), dim3(64), s, n, n, Sd, dec_st, seed, nonce, rS, status, sig_st);
-    return;
-  }
-  const uint32_t nsig = (n + 63) / 64;
-  GBV_LAUNCH("k_vs_sig_pre", k_vs_sig_pre, dim3(2 * nsig), dim3(64), s, n, n, sig, sig_stride, sig_len, seed, nonce, rS, status, sig_st);
+  launch_vs_sig_decode(s, n, sig, sig_stride, sig_len, Sd, dec_st);
+  GBV_LAUNCH("k_vs_sig_pre_quad", k_vs_sig_pre_quad, dim3(2 * ((n + 15) / 16)), dim3(64), s, n, n, Sd, dec_st, seed, nonce, rS, status, sig_st);
 }
 void launch_vs_pk_rand(hipStream_t s, uint32_t n, const uint32_t* set_off, const uint32_t* arena, const uint8_t* raw_flag,
                        const uint8_t* raw_pk48, const G1A* table, const uint8_t* table_ok, const G1J* pk_agg, const uint8_t* pk_st,
                        const Seed& seed, uint32_t nonce, G1J* rP, uint8_t* status) {
-  if (n <= tuning().vs_sig_quad_max) {
-    GBV_LAUNCH("k_vs_pk_rand_quad", k_vs_pk_rand_quad, dim3((n + 15) / 16), dim3(64), s, n, n, set_off, arena, raw_flag, raw_pk48, table, table_ok, pk_agg, pk_st, seed, nonce, rP, status);
-    return;
-  }
-  GBV_LAUNCH("k_vs_pk_rand", k_vs_pk_rand, dim3((n + 63) / 64), dim3(64), s, n, n, set_off, arena, raw_flag, raw_pk48, table, table_ok, pk_agg, pk_st, seed, nonce, rP, status);
+  GBV_LAUNCH("k_vs_pk_rand_quad", k_vs_pk_rand_quad, dim3((n + 15) / 16), dim3(64), s, n, n, set_off, arena, raw_flag, raw_pk48, table, table_ok, pk_agg, pk_st, seed, nonce, rP, status);
 }
 
 void launch_sig_validate(LaunchCfg c, uint32_t n, const uint8_t* sig, uint32_t sig_len, uint8_t* status, uint8_t* out96) {

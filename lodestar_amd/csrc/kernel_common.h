@@ -64,24 +64,25 @@ constexpr uint32_t FB_RUN_MAX = 8;
 // Message counts up to which hash_to_G2 runs on lane pairs (latency) instead of one lane each.
 constexpr uint32_t HASH_PAIR_MAX = 4096;
 
-// Launch-shape tunables (host side only).  Read ONCE, from GBV_* environment variables, by the first
-// gbv_init of the process (tuning_load); the launchers only read this struct, so nothing in a submit
-// path consults the environment.  Defaults are the measured choices of DESIGN.md section 7.
+// Launch-shape tunables (host side only, process-wide).  Defaults are the measured choices of
+// DESIGN.md section 7; experiments change them through gbv_tune (tuning_set, by the names below), never
+// through a beacon node's environment.  Only GBV_SYNC_DEBUG is read from the environment (tuning_load,
+// first gbv_init): it synchronises after every launch, which changes timing, not results.
 struct Tuning {
-  uint32_t hash_pair_max = HASH_PAIR_MAX;  // GBV_HASH_PAIR_MAX: hash on lane pairs up to this many messages
-  uint32_t hash_quad_max = 16384;          // GBV_HASH_QUAD_MAX: hash on lane quads up to this many messages
-  uint32_t hash_coop_max = 128;            // GBV_HASH_COOP_MAX: latency form, cofactor clearing one workgroup per message (two waves each: past ~128 messages they crowd the signature work beside them)
-  uint32_t prepare_split_max = 2048;       // GBV_PREPARE_SPLIT_MAX: same-message latency prepare up to this many sets
-  uint32_t chunk_finish_wave_max = 32;     // GBV_CHUNK_FINISH_WAVE_MAX: chunk sums one wave per chunk up to this many
-  uint32_t vs_pre_max = 16384;             // GBV_VS_PRE_MAX: verifySignatureSets signature half beside the aggregation
-  uint32_t vs_fs_maxc = 256;               // GBV_VS_FS_MAXC: per-chunk (-g1, sum) Miller value beside the per-set ones
-  uint32_t vs_quad_max = 16384;            // GBV_VS_QUAD_MAX: per-set Miller values on lane quads up to this many sets
-  uint32_t vs_sig_quad_max = 16384;        // GBV_VS_SIG_QUAD_MAX: "pre" signature work on lane quads up to this many sets
-  uint32_t vs_pair_max = 32768;            // GBV_VS_PAIR_MAX: ... on lane pairs up to this many (one lane per set above)
+  uint32_t hash_pair_max = HASH_PAIR_MAX;  // hash on lane pairs up to this many messages
+  uint32_t hash_quad_max = 16384;          // hash on lane quads up to this many messages
+  uint32_t hash_coop_max = 128;            // latency form, cofactor clearing one workgroup per message (two waves each: past ~128 messages they crowd the signature work beside them)
+  uint32_t prepare_split_max = 2048;       // same-message latency prepare up to this many sets
+  uint32_t chunk_finish_wave_max = 32;     // chunk sums one wave per chunk up to this many
+  uint32_t vs_pre_max = 16384;             // verifySignatureSets signature half (lane quads) beside the aggregation
+  uint32_t vs_fs_maxc = 256;               // per-chunk (-g1, sum) Miller value beside the per-set ones
+  uint32_t vs_quad_max = 16384;            // per-set Miller values on lane quads up to this many sets
+  uint32_t vs_pair_max = 32768;            // ... on lane pairs up to this many (one lane per set above)
   uint32_t sync_debug = 0;                 // GBV_SYNC_DEBUG: synchronise + report after every launch (debugging)
 };
 const Tuning& tuning();
 void tuning_load();
+bool tuning_set(const char* name, uint32_t value);  // false for an unknown name
 // verifySignatureSets passes up to this many sets compute their Miller values one wave per set
 // (cooperative, ~2.9 ms) instead of one thread per set (~16 ms of latency, far less VALU in total).
 constexpr uint32_t VS_COOP_MILLER_MAX = 2048;

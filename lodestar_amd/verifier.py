@@ -198,8 +198,9 @@ class GpuBlsVerifier:
         return bool(self._lib.gbv_comb_enabled(self._ctx))
 
     def tune(self, name: str, value: int):
-        """Change a pipeline setting of this context (gbv_tune: "msm_min", "msm_cooldown",
-        "segments"); booleans are identical for every value (tests reach each pipeline form)."""
+        """Change a pipeline setting (gbv_tune, include/gbv.h: per context "msm_min", "msm_cooldown",
+        "segments", "kprof", "comb"; process-wide launch shapes "hash_pair_max", "vs_pre_max", ...);
+        booleans are identical for every value (tests and experiments reach each pipeline form)."""
         _native.check(self._lib, self._ctx, self._lib.gbv_tune(self._ctx, name.encode(), int(value)))
 
     def aggregate_pubkeys(self, indices: Sequence[int]) -> bytes:

@@ -17,8 +17,9 @@ tests/test_coop_tables.py re-executes every program in Python against the oracle
 Round 4 wrote the hottest of these out as fixed code in coop.h (cyc_sqr, mul_line, sqr_dbl, mul12:
 lane terms resolved once, no records, no partial-sum phase); FP12_CYC_SQR, FP12_MUL_LINE,
 MILLER_SQR_DBL, G2_DBL_STEP, G2_DBL_PT and FP12_MUL stay here as the specification of the same maps
-(the written-out forms follow dbl_step_into's scaling exactly).  The device still interprets the
-Frobenius maps and G2_ADD_STEP.
+(the written-out forms follow dbl_step_into's scaling exactly) and are not emitted.  The device
+still interprets the Frobenius maps and G2_ADD_STEP: only those go into coop_tables.h
+(DEVICE_PROGRAMS).
 
 Program encoding (all indices small; emitted as fixed-size per-lane u32 records -- a product is a
 header (term counts) + up to 10 A terms + up to 10 B terms, a partial sum / output a header + up to
@@ -635,10 +636,16 @@ def build_all():
     return progs, list(CONSTS.vals)
 
 
+# The programs the device still interprets (coop.h run()): the Frobenius maps and the mixed addition
+# step.  The others are specifications of the written-out steps (coop.h cyc_sqr, mul_line, sqr_dbl,
+# mul12, the point doublings) and are checked here and by tests/test_coop_tables.py only.
+DEVICE_PROGRAMS = ("FP12_FROB1", "FP12_FROB2", "G2_ADD_STEP")
+
+
 def main():
     progs, consts = build_all()
     out = os.path.join(ROOT, "lodestar_amd", "csrc", "coop_tables.h")
-    emit(progs, out)
+    emit([p for p in progs if p["name"] in DEVICE_PROGRAMS], out)
     for p in progs:
         print("%-16s prods=%2d rounds=%d parts=%2d outs=%2d terms=%4d" % (
             p["name"], len(p["prods"]), len(p["round_end"]), len(p["parts"]), len(p["outs"]), len(p["terms"])))
