@@ -134,10 +134,23 @@ static int get_bytes(napi_env env, napi_value v, const uint8_t** data, size_t* l
   return 0;
 }
 
-static int get_prop(napi_env env, napi_value obj, const char* name, napi_value* out) {
-  bool has = false;
-  if (napi_has_named_property(env, obj, name, &has) != napi_ok || !has) return 0;
-  if (napi_get_named_property(env, obj, name, out) != napi_ok) return 0;
+
+/* Property keys created once per marshalled argument, not once per object: napi_get_named_property
+ * builds the key string on every call (~0.5-1 us each on this Node), a per-set cost in the object
+ * forms and a per-call cost in the packed form. */
+enum { K_SIGNING_ROOT, K_SIGNATURE, K_PUBKEY, K_INDICES, K_INDEX, K_MESSAGE, K_SETS, K_SIGNATURES, K_N };
+static const char* const KEY_NAMES[K_N] = {"signingRoot", "signature", "pubkey", "indices", "index", "message", "sets", "signatures"};
+typedef struct { napi_value k[K_N]; } keyset;
+static void keys_init(napi_env env, keyset* ks) {
+  for (int i = 0; i < K_N; ++i) napi_create_string_utf8(env, KEY_NAMES[i], NAPI_AUTO_LENGTH, &ks->k[i]);
+}
+/* obj[key] when present and neither undefined nor null */
+static int get_key(napi_env env, napi_value obj, napi_value key, napi_value* out) {
+  if (napi_get_property(env, obj, key, out) != napi_ok) {
+    const napi_extended_error_info* info;
+    napi_get_last_error_info(env, &info);
+    return 0;
+  }
   napi_valuetype t;
   napi_typeof(env, *out, &t);
   return t != napi_undefined && t != napi_null;
@@ -209,6 +222,8 @@ static void sets_free(sets_buf* s) {
 
 /* Append the sets of one JS array; returns 0 (and throws) on a malformed argument. */
 static int marshal_sets(napi_env env, napi_value arr, sets_buf* s) {
+  keyset ks;
+  keys_init(env, &ks);
   bool is_arr = false;
   napi_is_array(env, arr, &is_arr);
   if (!is_arr) {
@@ -228,13 +243,13 @@ static int marshal_sets(napi_env env, napi_value arr, sets_buf* s) {
     }
     const uint8_t* d;
     size_t len;
-    if (!get_prop(env, e, "signingRoot", &v) || !get_bytes(env, v, &d, &len) || len != 32) {
+    if (!get_key(env, e, ks.k[K_SIGNING_ROOT], &v) || !get_bytes(env, v, &d, &len) || len != 32) {
       napi_throw_type_error(env, "GBV_E_ARG", "signingRoot must be a 32-byte Uint8Array");
       return 0;
     }
     uv_push(&s->msg_off, (uint32_t)s->bytes.n);
     bv_push(&s->bytes, d, 32);
-    if (!get_prop(env, e, "signature", &v) || !get_bytes(env, v, &d, &len)) {
+    if (!get_key(env, e, ks.k[K_SIGNATURE], &v) || !get_bytes(env, v, &d, &len)) {
       napi_throw_type_error(env, "GBV_E_ARG", "signature must be a Uint8Array");
       return 0;
     }
@@ -242,7 +257,7 @@ static int marshal_sets(napi_env env, napi_value arr, sets_buf* s) {
     uv_push(&s->sig_len, (uint32_t)len);
     bv_push(&s->bytes, d, len);
     uv_push(&s->idx_off, (uint32_t)s->arena.n);
-    if (get_prop(env, e, "pubkey", &v)) {
+    if (get_key(env, e, ks.k[K_PUBKEY], &v)) {
       if (!get_bytes(env, v, &d, &len) || len != 48) {
         napi_throw_type_error(env, "GBV_E_ARG", "pubkey must be a 48-byte Uint8Array");
         return 0;
@@ -250,7 +265,7 @@ static int marshal_sets(napi_env env, napi_value arr, sets_buf* s) {
       uv_push(&s->raw_off, (uint32_t)s->bytes.n);
       bv_push(&s->bytes, d, 48);
       uv_push(&s->idx_len, 0);
-    } else if (get_prop(env, e, "indices", &v)) {
+    } else if (get_key(env, e, ks.k[K_INDICES], &v)) {
       uv_push(&s->raw_off, 0xFFFFFFFFu);
       bool ta = false, ja = false;
       napi_is_typedarray(env, v, &ta);
@@ -285,7 +300,7 @@ static int marshal_sets(napi_env env, napi_value arr, sets_buf* s) {
         return 0;
       }
       uv_push(&s->idx_len, k);
-    } else if (get_prop(env, e, "index", &v)) {
+    } else if (get_key(env, e, ks.k[K_INDEX], &v)) {
       uint32_t u;
       if (!get_u32(env, v, &u)) {
         napi_throw_type_error(env, "GBV_E_ARG", "index must be a number");
@@ -801,6 +816,8 @@ typedef struct pass_s {
  * {index, signature}[] or the packed form {indices: Uint32Array(n), signatures: Uint8Array(96 n)}
  * (copied in two memcpys; packed[c] = 1 then, so waitPass answers that call with a Uint8Array). */
 static int marshal_same_message(napi_env env, napi_value arr, uvec* off, uvec* idx, bvec* sigs, bvec* msgs, bvec* packed) {
+  keyset ks;
+  keys_init(env, &ks);
   bool ja = false;
   napi_is_array(env, arr, &ja);
   if (!ja) {
@@ -817,23 +834,69 @@ static int marshal_same_message(napi_env env, napi_value arr, uvec* off, uvec* i
     const uint8_t* d;
     size_t len;
     bool sa = false;
-    if (!get_prop(env, call, "message", &msg) || !get_bytes(env, msg, &d, &len) || len != 32 || !get_prop(env, call, "sets", &sets) ||
+    if (!get_key(env, call, ks.k[K_MESSAGE], &msg) || !get_bytes(env, msg, &d, &len) || len != 32 || !get_key(env, call, ks.k[K_SETS], &sets) ||
         napi_is_array(env, sets, &sa) != napi_ok) {
       napi_throw_type_error(env, "GBV_E_ARG", "each call needs sets and message: 32-byte Uint8Array");
       return 0;
     }
     bv_push(msgs, d, 32);
-    if (!sa) {  /* packed */
+    if (!sa) {  /* packed: signatures as one Uint8Array(96 n), or as an array of n Uint8Arrays */
       napi_value iv, sv;
-      const uint32_t* ix;
+      const uint32_t* ix = NULL;
       size_t n = 0;
-      if (!get_prop(env, sets, "indices", &iv) || !get_u32_array(env, iv, &ix, &n) || !get_prop(env, sets, "signatures", &sv) ||
-          !get_bytes(env, sv, &d, &len) || len != 96 * n) {
-        napi_throw_type_error(env, "GBV_E_ARG", "sets: {index, signature}[] or {indices: Uint32Array(n), signatures: Uint8Array(96 n)}");
+      bool list = false;
+      bool ixl = false;
+      if (!get_key(env, sets, ks.k[K_INDICES], &iv) || napi_is_array(env, iv, &ixl) != napi_ok || (!ixl && !get_u32_array(env, iv, &ix, &n)) ||
+          !get_key(env, sets, ks.k[K_SIGNATURES], &sv) || napi_is_array(env, sv, &list) != napi_ok) {
+        napi_throw_type_error(env, "GBV_E_ARG", "sets: {index, signature}[] or {indices: Uint32Array(n), signatures: Uint8Array(96 n) | Uint8Array[]}");
         return 0;
       }
-      uv_push_n(idx, ix, n);
-      bv_push(sigs, d, 96 * n);
+      if (ixl) {  /* indices as a plain array of numbers (no typed array allocated per call by the caller) */
+        uint32_t m = 0;
+        napi_get_array_length(env, iv, &m);
+        n = m;
+        for (uint32_t i = 0; i < m; ++i) {
+          napi_value x;
+          uint32_t u;
+          napi_get_element(env, iv, i, &x);
+          if (!get_u32(env, x, &u)) {
+            napi_throw_type_error(env, "GBV_E_ARG", "indices must be numbers");
+            return 0;
+          }
+          uv_push(idx, u);
+        }
+      }
+      if (list) {  /* the caller's own signature objects (chain/bls/gpu/index.ts): copied here, one memcpy each */
+        uint32_t m = 0;
+        napi_get_array_length(env, sv, &m);
+        if (m != n) {
+          napi_throw_type_error(env, "GBV_E_ARG", "signatures: one Uint8Array per index");
+          return 0;
+        }
+        if (!ixl) uv_push_n(idx, ix, n);
+        if (sigs->n + 96 * n > sigs->cap) {
+          sigs->cap = (sigs->n + 96 * n) * 2 + 64;
+          sigs->p = (uint8_t*)realloc(sigs->p, sigs->cap);
+        }
+        for (uint32_t i = 0; i < m; ++i) {
+          napi_value e;
+          napi_get_element(env, sv, i, &e);
+          if (!get_bytes(env, e, &d, &len)) {
+            napi_throw_type_error(env, "GBV_E_ARG", "signatures: one Uint8Array per index");
+            return 0;
+          }
+          /* another length throws in Signature.fromBytes -> false for that set (zero bytes: BAD_ENCODING) */
+          memcpy(sigs->p + sigs->n, len == 96 ? d : zero96, 96);
+          sigs->n += 96;
+        }
+      } else {
+        if (!get_bytes(env, sv, &d, &len) || len != 96 * n) {
+          napi_throw_type_error(env, "GBV_E_ARG", "sets: {index, signature}[] or {indices: Uint32Array(n), signatures: Uint8Array(96 n) | Uint8Array[]}");
+          return 0;
+        }
+        if (!ixl) uv_push_n(idx, ix, n);
+        bv_push(sigs, d, 96 * n);
+      }
       uv_push(off, (uint32_t)idx->n);
       const uint8_t one = 1;
       if (packed) bv_push(packed, &one, 1);
@@ -847,7 +910,7 @@ static int marshal_same_message(napi_env env, napi_value arr, uvec* off, uvec* i
       napi_value e, v;
       uint32_t ix;
       napi_get_element(env, sets, i, &e);
-      if (!get_prop(env, e, "index", &v) || !get_u32(env, v, &ix) || !get_prop(env, e, "signature", &v) || !get_bytes(env, v, &d, &len)) {
+      if (!get_key(env, e, ks.k[K_INDEX], &v) || !get_u32(env, v, &ix) || !get_key(env, e, ks.k[K_SIGNATURE], &v) || !get_bytes(env, v, &d, &len)) {
         napi_throw_type_error(env, "GBV_E_ARG", "a same-message set is {index: number, signature: Uint8Array}");
         return 0;
       }

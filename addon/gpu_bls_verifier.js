@@ -295,8 +295,10 @@ class GpuBlsVerifier {
     if (this.closed) throw new QueueError("QUEUE_ABORTED");
     if (!message || message.length !== 32) throw Object.assign(new TypeError("message must be 32 bytes"), {code: "GBV_E_ARG"});
     const packed = !Array.isArray(sets);
-    if (packed && !(sets.indices instanceof Uint32Array && sets.signatures && sets.signatures.length === 96 * sets.indices.length))
-      throw Object.assign(new TypeError("packed sets: {indices: Uint32Array(n), signatures: Uint8Array(96 n)}"), {code: "GBV_E_ARG"});
+    const sigList = packed && Array.isArray(sets.signatures);
+    if (packed && !(sets.indices instanceof Uint32Array && sets.signatures &&
+        sets.signatures.length === (sigList ? 1 : 96) * sets.indices.length))
+      throw Object.assign(new TypeError("packed sets: {indices: Uint32Array(n), signatures: Uint8Array(96 n) | Uint8Array[n]}"), {code: "GBV_E_ARG"});
     const n = packed ? sets.indices.length : sets.length;
     const nKeys = n ? this.addon.pubkeyCount(this.ctx) : 0;
     if (packed) {
@@ -308,9 +310,14 @@ class GpuBlsVerifier {
         if (!(s.index >= 0 && s.index < nKeys)) throw Object.assign(new RangeError("validator index out of range"), {code: "GBV_E_ARG"});
       }
     }
+    if (n < 2 * MAX_SIGNATURE_SETS_PER_JOB) {
+      // one chunk (every gossip call): its job's promise is the call's (no Promise.all, no concat)
+      const chunk = packed ? {indices: sets.indices, signatures: sets.signatures, length: n} : sets;
+      return new Promise((resolve, reject) => this._queue({type: "sameMessage", resolve, reject, addedTimeMs: Date.now(), opts, sets: chunk, message}));
+    }
     const chunks = packed
       ? chunkRanges(n, MAX_SIGNATURE_SETS_PER_JOB).map(([a, b]) => ({indices: sets.indices.subarray(a, b),
-        signatures: sets.signatures.subarray(96 * a, 96 * b), length: b - a}))
+        signatures: sigList ? sets.signatures.slice(a, b) : sets.signatures.subarray(96 * a, 96 * b), length: b - a}))
       : chunkifyMaximizeChunkSize(sets, MAX_SIGNATURE_SETS_PER_JOB);
     const results = await Promise.all(
       chunks.map(
@@ -331,24 +338,26 @@ class GpuBlsVerifier {
 
   /** The IBlsVerifier call shape (chain/bls/gpu/index.ts, validation/attestation.ts:131-137): one
    * {index, signature} (+ publicKey, unused) per set -> boolean[], marshalled as the packed form: one
-   * Uint32Array of indices and one signature buffer per call, so the addon copies two buffers instead
-   * of reading 2n properties.  A signature of another length than 96 bytes stays zero in the buffer:
-   * a bad encoding, false for that set alone -- as Signature.fromBytes throwing inside the pool's
-   * aggregate sends the chunk to the per-set retry, where that set fails (jobItem.ts:93-125). */
-  async verifySameMessageSets(sets, message, opts = {}) {
+   * Uint32Array of indices and the list of the caller's signature arrays, which the addon copies with
+   * one memcpy each (a property walk per set costs ~4x more in Node-API, a JS-side copy ~2x).  A
+   * signature of another length than 96 bytes becomes zero bytes: a bad encoding, false for that set
+   * alone -- as Signature.fromBytes throwing inside the pool's aggregate sends the chunk to the per-set
+   * retry, where that set fails (jobItem.ts:93-125). */
+  verifySameMessageSets(sets, message, opts = {}) {
     const n = sets.length;
     const indices = new Uint32Array(n);
-    const signatures = new Uint8Array(96 * n);
+    const signatures = new Array(n);
     for (let i = 0; i < n; ++i) {
       const s = sets[i];
-      if (!(s.index >= 0)) throw Object.assign(new TypeError("same-message set without a validator index"), {code: "GBV_E_ARG"});
+      if (!(s.index >= 0)) return Promise.reject(Object.assign(new TypeError("same-message set without a validator index"), {code: "GBV_E_ARG"}));
       indices[i] = s.index;
-      if (s.signature.length === 96) signatures.set(s.signature, 96 * i);
+      signatures[i] = s.signature;
     }
-    const r = await this.verifySignatureSetsSameMessage({indices, signatures}, message, opts);
-    const out = new Array(n);
-    for (let i = 0; i < n; ++i) out[i] = r[i] === 1;
-    return out;
+    return this.verifySignatureSetsSameMessage({indices, signatures}, message, opts).then((r) => {
+      const out = new Array(n);
+      for (let i = 0; i < n; ++i) out[i] = r[i] === 1;
+      return out;
+    });
   }
 
   async close() {

@@ -43,7 +43,8 @@ class FakeAddon {
     this.passes.push(rec);
     // a packed chunk {indices, signatures, length} answers with a Uint8Array, like the addon
     const smRes = (c) => (Array.isArray(c.sets) ? c.sets.map((s) => this.valid(s))
-      : Uint8Array.from({length: c.sets.length}, (_, i) => (c.sets.signatures[96 * i] === 1 ? 1 : 0)));
+      : Uint8Array.from({length: c.sets.length}, (_, i) => (Array.isArray(c.sets.signatures)
+        ? (c.sets.signatures[i].length === 96 && c.sets.signatures[i][0] === 1 ? 1 : 0) : (c.sets.signatures[96 * i] === 1 ? 1 : 0))));
     const res = {
       sameMessage: sm ? sm.map(smRes) : null,
       default: df

@@ -666,18 +666,23 @@ def c5_bench(v, call_off, idx, sigs, msgs, steps=6, depth=3, frac=0.01):
         b = stages[k % depth]
         if k >= depth:
             assert b.wait(True) == want
+        if k == steps - 1:
+            v.tune("kprof", 1)  # the last batch also timed kernel by kernel
         b.submit()
+    v.tune("kprof", 0)
     for k in range(max(0, steps - depth), steps):
         assert stages[k % depth].wait(True) == want
     dt = (time.perf_counter() - t0) / steps
     fb, seg = v.last_stats()
+    ops = v.last_ops(0)
     for st in stages:
         st.close()
     return {"metric": "signature sets verified/sec (same-message stream, 1% invalid: per-set fallback), 1 GPU",
             "unit": "sets/s", "value": round(n / dt, 1), "ms_per_step": round(dt * 1e3, 3), "steps": steps,
             "config": "C5 recipe on the C2 stream: %d sets, %d invalid (90%% wrong message, 10%% malformed), %d batches in flight" % (
                 n, int((expect == 0).sum()), depth),
-            "all_booleans_checked": True, "last_fallback_chunks": fb, "last_failed_segments": seg}
+            "all_booleans_checked": True, "last_fallback_chunks": fb, "last_failed_segments": seg,
+            "last_step_kernels": [{"kernel": k, "grid": g, "units": u, "ms": round(m, 3)} for k, g, u, m in ops]}
 
 
 def api_stream_rate(v, call_off, idx, sigs, msgs, n_sets=1 << 20):

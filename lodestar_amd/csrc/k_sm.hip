@@ -3,6 +3,7 @@
 
 #include "launch.h"
 #include "kernel_common.h"
+#include "locate.h"
 
 
 namespace gbv {
@@ -37,7 +38,8 @@ __global__ void GBV_KERNEL_ATTR k_sm_prepare(uint32_t base, uint32_t n, const ui
                                              const uint32_t* __restrict__ set_grp, const G1A* __restrict__ table,
                                              const uint8_t* __restrict__ table_ok, uint32_t table_n, const uint4* __restrict__ comb,
                                              const uint8_t* __restrict__ comb_ok, Seed seed, uint32_t nonce, G2A* __restrict__ S_out,
-                                             G2J* __restrict__ Sh_out, G1J* __restrict__ Ph_out, uint8_t* __restrict__ status) {
+                                             G2J* __restrict__ Sh_out, G1J* __restrict__ Ph_out, uint8_t* __restrict__ status,
+                                             G1J* __restrict__ Pset, G2J* __restrict__ Sset) {
   unsigned lane = threadIdx.x;
   uint32_t t = blockIdx.x * 64 + lane;
   bool act = t < n;
@@ -73,6 +75,9 @@ __global__ void GBV_KERNEL_ATTR k_sm_prepare(uint32_t base, uint32_t n, const ui
         if (!randomize_g1(pk, r, &rp)) rp = g1_mul_u64(pk, r);
       }
     }
+    // the per-set terms (infinity for a rejected set), for locating an invalid set of a failing chunk
+    Pset[i] = rp;
+    if (WITH_G2) Sset[i] = rs;
   }
   // segmented suffix scan inside each group of SCAN_W lanes (3 levels: the whole wave pays every
   // level, so fewer levels = less work here; k_sm_chunk_finish adds the group sums of a chunk)
@@ -93,78 +98,6 @@ __global__ void GBV_KERNEL_ATTR k_sm_prepare(uint32_t base, uint32_t n, const ui
   }
 }
 
-// Latency form of k_sm_prepare<true> for segments of few sets (a lone gossip call): TWO waves per 64
-// sets (a 128-thread block).  Both decode the signatures; wave 0 runs the subgroup checks while
-// wave 1 forms r pk and r sig (the two longest chains of a set, side by side on two SIMDs instead of
-// one after the other -- two lanes of ONE wave would only take turns); wave 0's verdicts reach
-// wave 1 through LDS and decide, exactly as in k_sm_prepare, whether a set's terms count.  Same
-// r_i, statuses, 8-set segmented scan (wave 1, lane = set) and outputs as k_sm_prepare<true>.
-__global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(GBV_WAVES_PER_EU)))
-k_sm_prepare_split(uint32_t base, uint32_t n, const uint32_t* __restrict__ idx, const uint8_t* __restrict__ sig96,
-                   const uint32_t* __restrict__ set_grp, const G1A* __restrict__ table, const uint8_t* __restrict__ table_ok,
-                   uint32_t table_n, const uint4* __restrict__ comb, const uint8_t* __restrict__ comb_ok, Seed seed, uint32_t nonce,
-                   G2A* __restrict__ S_out, G2J* __restrict__ Sh_out, G1J* __restrict__ Ph_out, uint8_t* __restrict__ status) {
-  __shared__ uint8_t sub_ok[64];
-  const unsigned lane = threadIdx.x & 63u, role = threadIdx.x >> 6;
-  const uint32_t t = blockIdx.x * 64 + lane;
-  const bool act = t < n;
-  const uint32_t i = base + t;
-  const uint32_t key = act ? set_grp[i] : 0xffffffffu;
-  G2J rs = jac_infinity<Fp2>();
-  G1J rp = jac_infinity<Fp>();
-  G2A s;
-  uint8_t st = SET_OK;
-  bool dec_ok = false;
-  uint32_t k = 0;
-  if (act) {
-    k = idx[i];
-    if (k >= table_n || !table_ok[k]) st = SET_BAD_PK;
-    dec_ok = g2_decode(s, sig96 + 96ull * i, 96) == PT_OK;
-  }
-  if (role == 0) {
-    sub_ok[lane] = (uint8_t)(act && dec_ok && g2_in_subgroup(s));
-  } else if (act && dec_ok && st == SET_OK) {  // (discarded below when wave 0 rejects the point)
-    const uint64_t r = prf_scalar(seed, i, nonce);
-    if (comb && comb_ok[k]) {
-      rp = comb_mul(comb + (size_t)k * (COMB_ENTRIES * COMB_U4), (uint32_t)r, (uint32_t)(r >> 32));
-      if (!randomize_g2(s, r, &rs)) {
-        rs = g2_mul_u64(s, r);
-        rp = g1_mul_u64(table[k], r);
-      }
-    } else {
-      G1A pk = table[k];
-      if (!randomize_pair(pk, s, r, &rp, &rs)) {
-        rs = g2_mul_u64(s, r);
-        rp = g1_mul_u64(pk, r);
-      }
-    }
-  }
-  __syncthreads();
-  if (role == 0) return;
-  if (act && !sub_ok[lane]) st = SET_BAD_SIG;  // as k_sm_prepare: a bad signature outranks a bad key
-  if (st != SET_OK) {
-    rp = jac_infinity<Fp>();
-    rs = jac_infinity<Fp2>();
-  }
-  if (act) {
-    status[i] = st;
-    if (st == SET_OK) S_out[i] = s;
-  }
-  for (unsigned d = 1; d < SCAN_W; d <<= 1) {
-    G1J po = shfl_down_jac(rp, d);
-    uint32_t ko = __shfl_down(key, d, 64);
-    bool take = (lane & (SCAN_W - 1)) + d < SCAN_W && ko == key;
-    G2J so = shfl_down_jac(rs, d);
-    if (take) rs = g2_add(rs, so);
-    if (take) rp = jac_add(rp, po);
-  }
-  uint32_t kprev = __shfl_up(key, 1, 64);
-  if (act && ((lane & (SCAN_W - 1)) == 0 || kprev != key)) {
-    Sh_out[i] = rs;
-    Ph_out[i] = rp;
-  }
-}
-
 // After k_sm_prep_roles_quad (k_vs.hip): per set the verdict -- pubkey slot, decode code, the
 // cooperative subgroup check (sub_ok) -- merged as k_sm_prepare merges it (a bad signature outranks a
 // bad key), the set's r pk / r sig (Ph / Sh at its own index) kept only when it is valid, then the
@@ -173,7 +106,7 @@ k_sm_prepare_split(uint32_t base, uint32_t n, const uint32_t* __restrict__ idx, 
 __global__ void GBV_KERNEL_ATTR k_sm_prep_scan(uint32_t base, uint32_t n, const uint32_t* __restrict__ idx,
                                                const uint32_t* __restrict__ set_grp, const uint8_t* __restrict__ table_ok,
                                                uint32_t table_n, const uint8_t* __restrict__ sub_ok, uint8_t* __restrict__ status,
-                                               G2J* __restrict__ Sh, G1J* __restrict__ Ph) {
+                                               G2J* __restrict__ Sh, G1J* __restrict__ Ph, G1J* __restrict__ Pset, G2J* __restrict__ Sset) {
   const unsigned lane = threadIdx.x;
   const uint32_t t = blockIdx.x * 64 + lane;
   const bool act = t < n;
@@ -190,6 +123,8 @@ __global__ void GBV_KERNEL_ATTR k_sm_prep_scan(uint32_t base, uint32_t n, const 
       rs = Sh[i];
       rp = Ph[i];
     }
+    Pset[i] = rp;
+    Sset[i] = rs;
   }
   for (unsigned d = 1; d < SCAN_W; d <<= 1) {
     G1J po = shfl_down_jac(rp, d);
@@ -213,7 +148,7 @@ __global__ void GBV_KERNEL_ATTR k_sm_prep_scan(uint32_t base, uint32_t n, const 
 __global__ void GBV_KERNEL_ATTR k_sm_redo_g2(uint32_t base, uint32_t n, const uint32_t* __restrict__ set_grp,
                                              const uint8_t* __restrict__ status, const G2A* __restrict__ S, Seed seed, uint32_t nonce,
                                              const uint8_t* __restrict__ seg_ok, const uint32_t* __restrict__ n_fallback,
-                                             G2J* __restrict__ Sh_out) {
+                                             G2J* __restrict__ Sh_out, G2J* __restrict__ Sset) {
   // a passing segment still needs the per-set terms when one of its chunks went to the per-set
   // path (malformed / non-subgroup signature): the run checks read Sh (k_sm_fb_blocks*)
   if (*seg_ok && *n_fallback == 0) return;
@@ -228,6 +163,7 @@ __global__ void GBV_KERNEL_ATTR k_sm_redo_g2(uint32_t base, uint32_t n, const ui
     uint64_t r = prf_scalar(seed, i, nonce);
     if (!randomize_g2(s, r, &rs)) rs = g2_mul_u64(s, r);
   }
+  if (act) Sset[i] = rs;
   for (unsigned d = 1; d < SCAN_W; d <<= 1) {
     G2J so = shfl_down_jac(rs, d);
     uint32_t ko = __shfl_down(key, d, 64);
@@ -253,9 +189,11 @@ __global__ void GBV_KERNEL_ATTR k_sm_chunk_finish_s(uint32_t g0, uint32_t G, uin
 
 // Per chunk (one thread): P_g = sum r_i pk_i, S_g = sum r_i sig_i from the segment sums at the
 // chunk start and at every SCAN_W-set group boundary inside it.  P_g stays Jacobian: the Miller loop
-// takes Jacobian P (lines scaled by Z^3, which the final exponentiation removes).  A chunk holding
-// a malformed / non-subgroup signature goes straight to the per-set retry, as
-// aggregateWithRandomness throwing does (index.ts:406-409).
+// takes Jacobian P (lines scaled by Z^3, which the final exponentiation removes).  The sums hold the
+// chunk's decodable, in-group sets only (k_sm_prepare leaves a rejected set's terms at infinity): a
+// malformed / non-subgroup signature is false on its own, and the chunk's check then decides the
+// others -- the booleans of the reference's per-set retry after aggregateWithRandomness throws
+// (index.ts:406-409, jobItem.ts:93-125).  A chunk without any such set is done: all false.
 __global__ void GBV_KERNEL_ATTR k_sm_chunk_finish(uint32_t g0, uint32_t G, uint32_t s0, const uint32_t* __restrict__ grp_off,
                                                   const uint8_t* __restrict__ status, const G2J* __restrict__ Sh,
                                                   const G1J* __restrict__ Ph, G1J* __restrict__ PgJ, G2J* __restrict__ SgJ,
@@ -264,9 +202,14 @@ __global__ void GBV_KERNEL_ATTR k_sm_chunk_finish(uint32_t g0, uint32_t G, uint3
   if (g >= G) return;
   g += g0;
   uint32_t b = grp_off[g], e = grp_off[g + 1];
-  bool bad = (b == e);
-  for (uint32_t i = b; i < e; ++i) bad |= status[i] != SET_OK;
-  if (!bad) {
+  bool any = false;
+  for (uint32_t i = b; i < e; ++i) any |= status[i] == SET_OK;
+  if (!any) {  // no set to verify (every one malformed / outside the group / without a usable key): all false
+    grp_state[g] = GRP_OK;
+    return;
+  }
+  bool bad = false;
+  {
     G1J p = Ph[b];
     G2J s = Sh ? Sh[b] : jac_infinity<Fp2>();  // Sh == nullptr: the segment's G2 sum is the MSM's
     for (uint32_t q = s0 + ((b - s0) / SCAN_W + 1) * SCAN_W; q < e; q += SCAN_W) {
@@ -291,9 +234,13 @@ k_sm_chunk_finish_wave(uint32_t g0, uint32_t s0, const uint32_t* __restrict__ gr
   const uint32_t g = g0 + blockIdx.x;
   const unsigned lane = threadIdx.x;
   const uint32_t b = grp_off[g], e = grp_off[g + 1];
-  int bad = b == e;
-  for (uint32_t i = b + lane; i < e; i += 64) bad |= status[i] != SET_OK;
-  bad = __any(bad);
+  int any_ok = 0;
+  for (uint32_t i = b + lane; i < e; i += 64) any_ok |= status[i] == SET_OK;
+  if (!__any(any_ok)) {  // nothing to verify: all false (as k_sm_chunk_finish)
+    if (lane == 0) grp_state[g] = GRP_OK;
+    return;
+  }
+  int bad = 0;
   // group starts: the chunk start, then every SCAN_W-set boundary of the segment inside the chunk
   // (lane k takes groups k, k + 64, ...: any chunk length)
   int any = 0;
@@ -346,13 +293,13 @@ __global__ void GBV_KERNEL_ATTR k_sm_fallback(uint32_t n, const uint32_t* __rest
                                                     const uint8_t* __restrict__ grp_state, const uint8_t* __restrict__ status,
                                                     const uint32_t* __restrict__ idx, const G1A* __restrict__ table,
                                                     const G2A* __restrict__ S, const G2A* __restrict__ H, uint8_t* __restrict__ valid,
-                                                    int do_fallback) {
+                                                    const uint32_t* __restrict__ grp_loc, int do_fallback) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint32_t g = set_grp[i];
   uint8_t st = grp_state[g];
-  if (st == GRP_OK) {
-    valid[i] = 1;
+  if (st == GRP_OK || st == GRP_LOCATED) {  // the chunk's check held (without its located set)
+    valid[i] = (status[i] == SET_OK && !(st == GRP_LOCATED && grp_loc[g] == i)) ? 1 : 0;
     return;
   }
   if (!do_fallback) return;
@@ -366,12 +313,15 @@ __global__ void GBV_KERNEL_ATTR k_sm_fallback(uint32_t n, const uint32_t* __rest
 
 // Failure path of a segment with many chunks: one thread per pending chunk.  It reuses the chunk's
 // Miller value F[g] = f(P_g, H(m_g)) from k_sm_miller, adds the (-g1, S_g) pair and runs the final
-// exponentiation: verify(msg, aggPk, aggSig) of the chunk (maybeBatch.ts:34-38).  Thread-serial
-// checks keep the lanes busy when thousands of chunks are pending; a handful of chunks takes the
-// wave-cooperative k_sm_group_pairing instead (lower latency per chunk).
+// exponentiation: verify(msg, aggPk, aggSig) of the chunk (maybeBatch.ts:34-38); a failing chunk then
+// tries to locate its one invalid set (above: GRP_LOCATED, grp_loc[g]) before the run / per-set
+// checks (GRP_FALLBACK).  Thread-serial checks keep the lanes busy when thousands of chunks are
+// pending; a handful of chunks takes the wave-cooperative k_sm_group_pairing instead.
 __global__ void GBV_KERNEL_ATTR k_sm_group_check(uint32_t g0, uint32_t G, const Fp12* __restrict__ F, const G2J* __restrict__ SgJ,
                                                  const uint8_t* __restrict__ seg_ok, uint8_t* __restrict__ grp_state,
-                                                 uint32_t* __restrict__ n_fallback) {
+                                                 uint32_t* __restrict__ n_fallback, const uint32_t* __restrict__ grp_off,
+                                                 const uint32_t* __restrict__ grp_msg, const G2A* __restrict__ H,
+                                                 const G1J* __restrict__ Pset, const G2J* __restrict__ Sset, uint32_t* __restrict__ grp_loc) {
   uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (*seg_ok || g >= G) return;  // launched unconditionally: no host round trip
   g += g0;
@@ -379,14 +329,23 @@ __global__ void GBV_KERNEL_ATTR k_sm_group_check(uint32_t g0, uint32_t G, const 
   G2A sa;
   Fp12 f = F[g];
   if (jac_to_aff(sa, SgJ[g])) f = fp12_mul(f, miller_loop_1(g1_neg_generator(), sa));
-  bool ok = fp12_is_one(final_exponentiation(f));
-  grp_state[g] = ok ? GRP_OK : GRP_FALLBACK;
-  if (!ok) atomicAdd(n_fallback, 1u);
+  Fp12 D;
+  final_exponentiation_to(&D, &f);
+  if (fp12_is_one(D)) {
+    grp_state[g] = GRP_OK;
+    return;
+  }
+  atomicAdd(n_fallback, 1u);
+  const uint32_t w = locate_one(grp_off[g], grp_off[g + 1], &D, H[grp_msg[g]], Pset, Sset);
+  if (w != LOC_NONE) grp_loc[g] = w;
+  grp_state[g] = w != LOC_NONE ? GRP_LOCATED : GRP_FALLBACK;
 }
 
 void launch_sm_group_check(LaunchCfg c, uint32_t g0, uint32_t G, const Fp12* F, const G2J* SgJ, const uint8_t* seg_ok, uint8_t* grp_state,
-                           uint32_t* n_fallback) {
-  GBV_LAUNCH("k_sm_group_check", k_sm_group_check, dim3((G + 63) / 64), dim3(64), c.stream, G, g0, G, F, SgJ, seg_ok, grp_state, n_fallback);
+                           uint32_t* n_fallback, const uint32_t* grp_off, const uint32_t* grp_msg, const G2A* H, const G1J* Pset,
+                           const G2J* Sset, uint32_t* grp_loc) {
+  GBV_LAUNCH("k_sm_group_check", k_sm_group_check, dim3((G + 63) / 64), dim3(64), c.stream, G, g0, G, F, SgJ, seg_ok, grp_state, n_fallback,
+             grp_off, grp_msg, H, Pset, Sset, grp_loc);
 }
 
 // ---- failure path of a chunk: 8-set block checks, then per-set checks ---------------------------
@@ -416,11 +375,13 @@ __global__ void GBV_KERNEL_ATTR k_sm_fb_runs(uint32_t s0, uint32_t n, const uint
   }
 }
 
-// Persistent over the run list: one randomised check per run; failing runs append their sets.
+// Persistent over the run list: one randomised check per run; a failing run tries to locate its one
+// invalid set (locate_one over the run's sets), and otherwise appends its sets to the per-set list.
 __global__ void GBV_KERNEL_ATTR k_sm_fb_blocks(const uint4* __restrict__ runs, const uint32_t* __restrict__ n_runs, uint32_t cap,
                                                const uint8_t* __restrict__ status, const uint32_t* __restrict__ grp_msg,
                                                const G2J* __restrict__ Sh, const G1J* __restrict__ Ph, const G2A* __restrict__ H,
-                                               uint8_t* __restrict__ valid, uint32_t* __restrict__ set_list, uint32_t* __restrict__ n_list) {
+                                               uint8_t* __restrict__ valid, uint32_t* __restrict__ set_list, uint32_t* __restrict__ n_list,
+                                               const G1J* __restrict__ Pset, const G2J* __restrict__ Sset) {
   uint32_t cnt = min(*n_runs, cap);
   if (cnt <= FB_COOP_MAX) return;  // k_sm_fb_blocks_coop has them
   for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < cnt; k += gridDim.x * blockDim.x) {
@@ -428,18 +389,18 @@ __global__ void GBV_KERNEL_ATTR k_sm_fb_blocks(const uint4* __restrict__ runs, c
     bool any = false;
     for (uint32_t i = r.x; i < r.y; ++i) any |= status[i] == SET_OK;
     bool ok = true;
+    uint32_t bad = LOC_NONE;
     if (any) {
-      G1A pa;
-      G2A sa;
-      bool p_fin = jac_to_aff(pa, Ph[r.x]);
-      bool s_fin = jac_to_aff(sa, Sh[r.x]);
-      ok = p_fin && pairing_check_2(pa, false, H[grp_msg[r.z]], g1_neg_generator(), !s_fin, sa);
+      const G2A Hm = H[grp_msg[r.z]];
+      Fp12 D;
+      ok = pair_value_to(&D, Ph[r.x], Hm, Sh[r.x]) && fp12_is_one(D);
+      if (!ok && !jac_is_inf(Ph[r.x])) bad = locate_one(r.x, r.y, &D, Hm, Pset, Sset);
     }
     for (uint32_t i = r.x; i < r.y; ++i) {
       if (status[i] != SET_OK) {
         valid[i] = 0;
-      } else if (ok) {
-        valid[i] = 1;
+      } else if (ok || bad != LOC_NONE) {
+        valid[i] = i != bad ? 1 : 0;
       } else {
         set_list[atomicAdd(n_list, 1u)] = i;
       }
@@ -466,8 +427,10 @@ void launch_sm_fb_runs(LaunchCfg c, uint32_t s0, uint32_t n, const uint32_t* set
   GBV_LAUNCH("k_sm_fb_runs", k_sm_fb_runs, dim3((windows + 63) / 64), dim3(64), c.stream, n, s0, n, set_grp, grp_state, runs, n_runs, cap);
 }
 void launch_sm_fb_blocks(LaunchCfg c, const uint4* runs, const uint32_t* n_runs, uint32_t cap, const uint8_t* status, const uint32_t* grp_msg,
-                         const G2J* Sh, const G1J* Ph, const G2A* H, uint8_t* valid, uint32_t* set_list, uint32_t* n_list) {
-  GBV_LAUNCH("k_sm_fb_blocks", k_sm_fb_blocks, dim3(c.blocks), dim3(64), c.stream, 0, runs, n_runs, cap, status, grp_msg, Sh, Ph, H, valid, set_list, n_list);
+                         const G2J* Sh, const G1J* Ph, const G2A* H, uint8_t* valid, uint32_t* set_list, uint32_t* n_list, const G1J* Pset,
+                         const G2J* Sset) {
+  GBV_LAUNCH("k_sm_fb_blocks", k_sm_fb_blocks, dim3(c.blocks), dim3(64), c.stream, 0, runs, n_runs, cap, status, grp_msg, Sh, Ph, H, valid, set_list,
+             n_list, Pset, Sset);
 }
 void launch_sm_fb_sets(LaunchCfg c, const uint32_t* set_list, const uint32_t* n_list, const uint32_t* set_grp, const uint32_t* grp_msg,
                        const uint32_t* idx, const G1A* table, const G2A* S, const G2A* H, uint8_t* valid) {
@@ -476,33 +439,30 @@ void launch_sm_fb_sets(LaunchCfg c, const uint32_t* set_list, const uint32_t* n_
 
 void launch_sm_prepare(LaunchCfg c, uint32_t base, uint32_t n, const uint32_t* idx, const uint8_t* sig96, const uint32_t* set_grp,
                        const G1A* table, const uint8_t* table_ok, uint32_t table_n, const uint4* comb, const uint8_t* comb_ok,
-                       const Seed& seed, uint32_t nonce, G2A* S_out, G2J* Sh, G1J* Ph, uint8_t* status, uint8_t* scratch8) {
+                       const Seed& seed, uint32_t nonce, G2A* S_out, G2J* Sh, G1J* Ph, uint8_t* status, uint8_t* scratch8, G1J* Pset,
+                       G2J* Sset) {
   // Sh == nullptr: G1 terms only (the segment's G2 sum comes from the bucket MSM); comb == nullptr:
-  // no comb tables (GBV_COMB=0 or not built), the ladder forms r pk
+  // no comb tables (gbv_tune "comb" 0, or not built), the ladder forms r pk
   const dim3 grid((n + 63) / 64);
-  if (Sh && n <= tuning().prepare_split_max && scratch8) {
-    // latency, few sets: decode, then the subgroup checks one wave per set beside the randomisation,
-    // then the verdicts and the scan
-    launch_sig_decode(c.stream, base, n, sig96, S_out, status);
+  launch_sig_decode(c.stream, base, n, sig96, S_out, status);  // decompression first, at a higher occupancy (k_dec.hip)
+  if (Sh && n <= tuning().prepare_split_max) {
+    // latency, few sets: the subgroup checks and the randomisation on lane quads side by side, then
+    // the verdicts and the scan
     launch_sm_prep_roles_quad(c.stream, base, n, idx, table, table_ok, table_n, comb, comb_ok, seed, nonce, S_out, status, scratch8, Sh, Ph);
-    GBV_LAUNCH("k_sm_prep_scan", k_sm_prep_scan, grid, dim3(64), c.stream, n, base, n, idx, set_grp, table_ok, table_n, scratch8, status, Sh, Ph);
-  } else if (Sh && n <= tuning().prepare_split_max) {  // latency: two waves per 64 sets
-    GBV_LAUNCH("k_sm_prepare_split", k_sm_prepare_split, dim3((n + 63) / 64), dim3(128), c.stream, n, base, n, idx, sig96, set_grp, table, table_ok,
-               table_n, comb, comb_ok, seed, nonce, S_out, Sh, Ph, status);
+    GBV_LAUNCH("k_sm_prep_scan", k_sm_prep_scan, grid, dim3(64), c.stream, n, base, n, idx, set_grp, table_ok, table_n, scratch8, status, Sh, Ph,
+               Pset, Sset);
+  } else if (Sh) {
+    GBV_LAUNCH("k_sm_prepare<true>", k_sm_prepare<true>, grid, dim3(64), c.stream, n, base, n, idx, sig96, set_grp, table, table_ok, table_n,
+               comb, comb_ok, seed, nonce, S_out, Sh, Ph, status, Pset, Sset);
   } else {
-    // throughput: decompression first as its own kernel at a higher occupancy (k_dec.hip)
-    launch_sig_decode(c.stream, base, n, sig96, S_out, status);
-    if (Sh)
-      GBV_LAUNCH("k_sm_prepare<true>", k_sm_prepare<true>, grid, dim3(64), c.stream, n, base, n, idx, sig96, set_grp, table, table_ok, table_n,
-                 comb, comb_ok, seed, nonce, S_out, Sh, Ph, status);
-    else
-      GBV_LAUNCH("k_sm_prepare<false>", k_sm_prepare<false>, grid, dim3(64), c.stream, n, base, n, idx, sig96, set_grp, table, table_ok,
-                 table_n, comb, comb_ok, seed, nonce, S_out, Sh, Ph, status);
+    GBV_LAUNCH("k_sm_prepare<false>", k_sm_prepare<false>, grid, dim3(64), c.stream, n, base, n, idx, sig96, set_grp, table, table_ok,
+               table_n, comb, comb_ok, seed, nonce, S_out, Sh, Ph, status, Pset, Sset);
   }
 }
 void launch_sm_redo_g2(LaunchCfg c, uint32_t base, uint32_t n, const uint32_t* set_grp, const uint8_t* status, const G2A* S, const Seed& seed,
-                       uint32_t nonce, const uint8_t* seg_ok, const uint32_t* n_fallback, G2J* Sh) {
-  GBV_LAUNCH("k_sm_redo_g2", k_sm_redo_g2, dim3((n + 63) / 64), dim3(64), c.stream, n, base, n, set_grp, status, S, seed, nonce, seg_ok, n_fallback, Sh);
+                       uint32_t nonce, const uint8_t* seg_ok, const uint32_t* n_fallback, G2J* Sh, G2J* Sset) {
+  GBV_LAUNCH("k_sm_redo_g2", k_sm_redo_g2, dim3((n + 63) / 64), dim3(64), c.stream, n, base, n, set_grp, status, S, seed, nonce, seg_ok, n_fallback, Sh,
+             Sset);
 }
 void launch_sm_chunk_finish_s(LaunchCfg c, uint32_t g0, uint32_t G, uint32_t s0, const uint32_t* grp_off, const uint8_t* grp_state,
                               const G2J* Sh, const uint8_t* seg_ok, G2J* SgJ) {
@@ -522,7 +482,8 @@ void launch_sm_miller(LaunchCfg c, uint32_t g0, uint32_t G, const uint32_t* grp_
 }
 void launch_sm_fallback(LaunchCfg c, uint32_t n, const uint32_t* set_grp, const uint32_t* grp_msg, const uint8_t* grp_state,
                         const uint8_t* status, const uint32_t* idx, const G1A* table, const G2A* S, const G2A* H, uint8_t* valid,
-                        int do_fallback) {
-  GBV_LAUNCH("k_sm_fallback", k_sm_fallback, dim3(c.blocks), dim3(c.threads), c.stream, n, n, set_grp, grp_msg, grp_state, status, idx, table, S, H, valid, do_fallback);
+                        const uint32_t* grp_loc, int do_fallback) {
+  GBV_LAUNCH("k_sm_fallback", k_sm_fallback, dim3(c.blocks), dim3(c.threads), c.stream, n, n, set_grp, grp_msg, grp_state, status, idx, table, S, H,
+             valid, grp_loc, do_fallback);
 }
 }  // namespace gbv

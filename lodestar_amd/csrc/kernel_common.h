@@ -53,7 +53,9 @@ namespace gbv {
 struct Seed { uint32_t w[8]; };
 
 enum : uint8_t { SET_OK = 0, SET_BAD_SIG = 1, SET_BAD_PK = 2 };
-enum : uint8_t { GRP_PENDING = 0, GRP_FALLBACK = 1, GRP_OK = 2 };
+// GRP_LOCATED: the chunk failed, and its one invalid set (grp_loc[g]) was located with every other
+// set proven valid (k_sm_group_check, below); GRP_FALLBACK: run / per-set checks decide.
+enum : uint8_t { GRP_PENDING = 0, GRP_FALLBACK = 1, GRP_OK = 2, GRP_LOCATED = 3 };
 // Failure-path item counts up to which one wave per item (k_sm_fb_*_coop, latency) beats one
 // thread per item (k_sm_fb_blocks / k_sm_fb_sets, throughput).
 constexpr uint32_t FB_COOP_MAX = 256;

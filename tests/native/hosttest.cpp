@@ -6,6 +6,7 @@
 #include "../../lodestar_amd/csrc/hash_to_curve.h"
 #include "../../lodestar_amd/csrc/coop.h"
 #include "../../lodestar_amd/csrc/ssz.h"
+#include "../../lodestar_amd/csrc/locate.h"
 #include <vector>
 
 using namespace gbv;
@@ -285,6 +286,29 @@ void ht_att_signing_root(uint8_t* out32, const uint8_t* data128, const uint8_t* 
   for (int i = 0; i < 32; ++i) d[i] = (uint32_t)data128[4*i] | ((uint32_t)data128[4*i+1] << 8) | ((uint32_t)data128[4*i+2] << 16) | ((uint32_t)data128[4*i+3] << 24);
   ht_store_be(out32, ssz_signing_root(ssz_attestation_data_root(d), ht_chunk_be(domain32)));
 }
+}
+
+// ---- the failure path's locate (locate.h), as k_sm_group_check / k_sm_fb_blocks run it ------------
+// n sets over one message H: pk_i affine (96 B each), sig_i affine (192 B each, x.c0 x.c1 y.c0 y.c1), batch
+// scalars r64[i]; the per-set terms r_i pk_i / r_i sig_i by randomize_pair, the chunk check value D of
+// their sums, then locate_one.  Returns the located index, LOC_NONE, or 0xfffffffe when D == 1.
+extern "C" unsigned ht_locate(const uint8_t* pks96, const uint8_t* sigs192, const uint64_t* r64, unsigned n, const uint8_t* h192) {
+  std::vector<G1J> Pset(n);
+  std::vector<G2J> Sset(n);
+  G1J P = jac_infinity<Fp>();
+  G2J S = jac_infinity<Fp2>();
+  const G2A H{load_fp2(h192), load_fp2(h192 + 96)};
+  for (unsigned i = 0; i < n; ++i) {
+    const G1A pk{load_mont(pks96 + 96 * i), load_mont(pks96 + 96 * i + 48)};
+    const G2A sg{load_fp2(sigs192 + 192 * i), load_fp2(sigs192 + 192 * i + 96)};
+    if (!randomize_pair(pk, sg, r64[i], &Pset[i], &Sset[i])) return 0xfffffffdu;
+    P = jac_add(P, Pset[i]);
+    S = jac_add(S, Sset[i]);
+  }
+  Fp12 D;
+  if (!pair_value_to(&D, P, H, S)) return 0xfffffffcu;
+  if (fp12_is_one(D)) return 0xfffffffeu;
+  return locate_one(0, n, &D, H, Pset.data(), Sset.data());
 }
 
 // ---- Fp-product counts of the per-unit work of each kernel path (bench.py roofline numerators) ----

@@ -371,3 +371,39 @@ def test_coop_clear_cofactor(lib):
         got = [int.from_bytes(out.raw[48 * i:48 * i + 48], "big") for i in range(4)]
         want = o.clear_cofactor_g2(q)
         assert ((got[0], got[1]), (got[2], got[3])) == (want[0], want[1])
+
+
+@pytest.mark.parametrize("case", ["valid", "one_bad_first", "one_bad_mid", "one_bad_last", "two_bad", "cancelling"])
+def test_locate_one_invalid_set(lib, case):
+    """The same-message failure path's locate (locate.h: k_sm_group_check, k_sm_fb_blocks): for a chunk
+    whose randomised check fails, the position-weighted check + discrete log <= n + the candidate's own
+    check name the ONE invalid set; two invalid sets (also a crafted pair whose errors cancel in an
+    unrandomised sum) are never "located" -- they go to the run / per-set checks.  Sets and signatures
+    from the oracle, the arithmetic from the host build of the device code."""
+    rnd = random.Random(hash(case) & 0xffff)
+    n = 9
+    msg = bytes(rnd.randrange(256) for _ in range(32))
+    other = bytes(rnd.randrange(256) for _ in range(32))
+    h = o.hash_to_g2(msg)
+    sks = [rnd.randrange(1, o.R) for _ in range(n)]
+    pks = [o.sk_to_pk(k) for k in sks]
+    sigs = [o.sign(k, msg) for k in sks]
+    bad = {"valid": [], "one_bad_first": [0], "one_bad_mid": [4], "one_bad_last": [n - 1], "two_bad": [2, 6], "cancelling": [1, 3]}[case]
+    for w in bad:
+        sigs[w] = o.sign(sks[w], other)
+    if case == "cancelling":  # sig_1 + D, sig_3 - D: the plain sum of the signatures still verifies
+        d = o.g2_mul(o.hash_to_g2(other), 12345)
+        sigs[1] = o.g2_add(o.sign(sks[1], msg), d)
+        sigs[3] = o.g2_add(o.sign(sks[3], msg), o.g2_neg(d))
+    pk96 = b"".join(be(p[0]) + be(p[1]) for p in pks)
+    sig192 = b"".join(fp2b(s[0]) + fp2b(s[1]) for s in sigs)
+    r = (ctypes.c_uint64 * n)(*[rnd.getrandbits(64) | 1 for _ in range(n)])
+    lib.ht_locate.restype = ctypes.c_uint
+    lib.ht_locate.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint, ctypes.c_char_p]
+    got = lib.ht_locate(pk96, sig192, r, n, fp2b(h[0]) + fp2b(h[1]))
+    if case == "valid":
+        assert got == 0xFFFFFFFE
+    elif len(bad) == 1:
+        assert got == bad[0]
+    else:
+        assert got == 0xFFFFFFFF

@@ -24,6 +24,8 @@ def main():
     r = bench.c5_bench(v, call_off, idx, sigs, msgs, steps=a.steps, depth=a.depth)
     print("C5 %.3f M sets/s, %.1f ms per step, fallback chunks %s, failed segments %s; last batch kernel ms %s" % (
         r["value"] / 1e6, r["ms_per_step"], r["last_fallback_chunks"], r["last_failed_segments"], v.last_kernel_ms()))
+    for k in r["last_step_kernels"]:
+        print("  %-28s grid %8d units %8d %9.3f ms" % (k["kernel"], k["grid"], k["units"], k["ms"]))
     v.close_sync()
 
 
