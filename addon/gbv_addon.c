@@ -138,8 +138,9 @@ static int get_bytes(napi_env env, napi_value v, const uint8_t** data, size_t* l
 /* Property keys created once per marshalled argument, not once per object: napi_get_named_property
  * builds the key string on every call (~0.5-1 us each on this Node), a per-set cost in the object
  * forms and a per-call cost in the packed form. */
-enum { K_SIGNING_ROOT, K_SIGNATURE, K_PUBKEY, K_INDICES, K_INDEX, K_MESSAGE, K_SETS, K_SIGNATURES, K_N };
-static const char* const KEY_NAMES[K_N] = {"signingRoot", "signature", "pubkey", "indices", "index", "message", "sets", "signatures"};
+enum { K_SIGNING_ROOT, K_SIGNATURE, K_PUBKEY, K_INDICES, K_INDEX, K_MESSAGE, K_SETS, K_SIGNATURES, K_COUNTS, K_MESSAGES, K_N };
+static const char* const KEY_NAMES[K_N] = {"signingRoot", "signature", "pubkey", "indices", "index", "message", "sets", "signatures",
+                                           "counts", "messages"};
 typedef struct { napi_value k[K_N]; } keyset;
 static void keys_init(napi_env env, keyset* ks) {
   for (int i = 0; i < K_N; ++i) napi_create_string_utf8(env, KEY_NAMES[i], NAPI_AUTO_LENGTH, &ks->k[i]);
@@ -804,6 +805,7 @@ typedef struct pass_s {
   size_t n_df;             /* default calls */
   uint8_t *sm_valid, *df_valid;
   bvec sm_packed;          /* per same-message call: 1 = packed sets (result as a Uint8Array) */
+  int sm_flat;             /* the pass-wide flat form: one Uint8Array of every set's result */
   napi_deferred deferred;
   napi_async_work work;
   napi_ref ctx_ref;        /* the context external, alive while the pass is */
@@ -811,6 +813,45 @@ typedef struct pass_s {
   int done;                /* waitPass settled */
   int external_gone;       /* the JS pass object was finalized */
 } pass;
+
+/* The flat form of a pass's same-message calls, built by the JS queue (addon/gpu_bls_verifier.js
+ * _runPass): {counts: Uint32Array(calls), messages: Uint8Array(32 calls), indices: Uint32Array(n),
+ * signatures: Uint8Array(96 n)} -- four buffers per PASS, where the per-call forms cost ~10 Node-API
+ * calls per call (~4 us each call on this Node) and the object form ~4 per set.  Returns 1, 0 (and
+ * throws) on a malformed argument, -1 when obj is not the flat form. */
+static int marshal_same_message_flat(napi_env env, napi_value obj, uvec* off, uvec* idx, bvec* sigs, bvec* msgs) {
+  keyset ks;
+  keys_init(env, &ks);
+  napi_value cv, mv, iv, sv;
+  if (!get_key(env, obj, ks.k[K_COUNTS], &cv)) return -1;
+  const uint32_t *cnt, *ix;
+  const uint8_t *m, *sg;
+  size_t nc = 0, n = 0, ml = 0, sl = 0;
+  if (!get_u32_array(env, cv, &cnt, &nc) || !get_key(env, obj, ks.k[K_MESSAGES], &mv) || !get_bytes(env, mv, &m, &ml) || ml != 32 * nc ||
+      !get_key(env, obj, ks.k[K_INDICES], &iv) || !get_u32_array(env, iv, &ix, &n) || !get_key(env, obj, ks.k[K_SIGNATURES], &sv) ||
+      !get_bytes(env, sv, &sg, &sl) || sl != 96 * n) {
+    napi_throw_type_error(env, "GBV_E_ARG", "flat calls: {counts: Uint32Array(c), messages: Uint8Array(32 c), indices: Uint32Array(n), signatures: Uint8Array(96 n)}");
+    return 0;
+  }
+  uint64_t total = 0;
+  uv_push(off, 0);
+  for (size_t c = 0; c < nc; ++c) {
+    total += cnt[c];
+    if (total > n) {
+      napi_throw_range_error(env, "GBV_E_ARG", "flat calls: counts exceed the indices");
+      return 0;
+    }
+    uv_push(off, (uint32_t)total);
+  }
+  if (total != n) {
+    napi_throw_range_error(env, "GBV_E_ARG", "flat calls: counts do not sum to the indices");
+    return 0;
+  }
+  uv_push_n(idx, ix, n);
+  bv_push(sigs, sg, 96 * n);
+  bv_push(msgs, m, 32 * nc);
+  return 1;
+}
 
 /* Marshal a same-message call list ({sets, message}[]) into idx / sigs / msgs.  A call's sets are either
  * {index, signature}[] or the packed form {indices: Uint32Array(n), signatures: Uint8Array(96 n)}
@@ -1016,7 +1057,13 @@ static napi_value js_submit_pass(napi_env env, napi_callback_info info) {
   int ok = 1;
   if (t0 != napi_null && t0 != napi_undefined) {
     p->has_sm = 1;
-    ok = marshal_same_message(env, argv[1], &p->sm_off, &sm_idx, &sm_sigs, &sm_msgs, &p->sm_packed);
+    bool sm_arr = false;
+    napi_is_array(env, argv[1], &sm_arr);
+    const int flat = sm_arr ? -1 : marshal_same_message_flat(env, argv[1], &p->sm_off, &sm_idx, &sm_sigs, &sm_msgs);
+    if (flat < 0)
+      ok = marshal_same_message(env, argv[1], &p->sm_off, &sm_idx, &sm_sigs, &sm_msgs, &p->sm_packed);
+    else
+      ok = flat, p->sm_flat = 1;
   }
   if (ok && t1 != napi_null && t1 != napi_undefined) {
     bool ja = false;
@@ -1109,6 +1156,13 @@ static void pass_complete(napi_env env, napi_status status, void* data) {
       napi_get_null(env, &x);
     } else if (p->rc_sm) {
       x = make_error(env, p->rc_sm, p->err_sm);
+    } else if (p->sm_flat) {  /* one Uint8Array of 0 / 1 over every set of the pass, in call order */
+      const size_t n = p->sm_off.n ? p->sm_off.p[p->sm_off.n - 1] : 0;
+      void* dst = NULL;
+      napi_value ab;
+      napi_create_arraybuffer(env, n ? n : 1, &dst, &ab);
+      if (n) memcpy(dst, p->sm_valid, n);
+      napi_create_typedarray(env, napi_uint8_array, n, ab, 0, &x);
     } else {
       size_t nc = p->sm_off.n ? p->sm_off.n - 1 : 0;
       napi_create_array_with_length(env, nc, &x);

@@ -337,27 +337,11 @@ class GpuBlsVerifier {
   }
 
   /** The IBlsVerifier call shape (chain/bls/gpu/index.ts, validation/attestation.ts:131-137): one
-   * {index, signature} (+ publicKey, unused) per set -> boolean[], marshalled as the packed form: one
-   * Uint32Array of indices and the list of the caller's signature arrays, which the addon copies with
-   * one memcpy each (a property walk per set costs ~4x more in Node-API, a JS-side copy ~2x).  A
-   * signature of another length than 96 bytes becomes zero bytes: a bad encoding, false for that set
-   * alone -- as Signature.fromBytes throwing inside the pool's aggregate sends the chunk to the per-set
-   * retry, where that set fails (jobItem.ts:93-125). */
+   * {index, signature} (+ publicKey, unused) per set -> boolean[].  The objects ride in the job as they
+   * are; _runPass copies every job of a pass into four pass-wide buffers (_packSameMessage) -- a
+   * per-call typed array, or Node-API property reads per set, cost more. */
   verifySameMessageSets(sets, message, opts = {}) {
-    const n = sets.length;
-    const indices = new Uint32Array(n);
-    const signatures = new Array(n);
-    for (let i = 0; i < n; ++i) {
-      const s = sets[i];
-      if (!(s.index >= 0)) return Promise.reject(Object.assign(new TypeError("same-message set without a validator index"), {code: "GBV_E_ARG"}));
-      indices[i] = s.index;
-      signatures[i] = s.signature;
-    }
-    return this.verifySignatureSetsSameMessage({indices, signatures}, message, opts).then((r) => {
-      const out = new Array(n);
-      for (let i = 0; i < n; ++i) out[i] = r[i] === 1;
-      return out;
-    });
+    return this.verifySignatureSetsSameMessage(sets, message, opts);
   }
 
   async close() {
@@ -429,6 +413,43 @@ class GpuBlsVerifier {
     }
   }
 
+  /** The pass's same-message jobs as the addon's flat form: counts / messages per call, indices and
+   * 96-byte signatures per set, in job order (job.off: the job's first set).  A signature of another
+   * length stays zero bytes: a bad encoding, false for that set alone -- as Signature.fromBytes throwing
+   * inside the pool's aggregate sends the chunk to the per-set retry, where that set fails
+   * (jobItem.ts:93-125). */
+  _packSameMessage(sm) {
+    let total = 0;
+    for (const j of sm) total += j.sets.length;
+    const counts = new Uint32Array(sm.length);
+    const messages = new Uint8Array(32 * sm.length);
+    const indices = new Uint32Array(total);
+    const signatures = new Uint8Array(96 * total);
+    let o = 0;
+    for (let c = 0; c < sm.length; ++c) {
+      const j = sm[c], s = j.sets, n = s.length;
+      counts[c] = n;
+      messages.set(j.message, 32 * c);
+      j.off = o;
+      if (Array.isArray(s)) {
+        for (let i = 0; i < n; ++i) {
+          const e = s[i], g = e.signature;
+          indices[o + i] = e.index;
+          if (g.length === 96) signatures.set(g, 96 * (o + i));
+        }
+      } else {
+        indices.set(s.indices, o);
+        if (Array.isArray(s.signatures)) {
+          for (let i = 0; i < n; ++i) if (s.signatures[i].length === 96) signatures.set(s.signatures[i], 96 * (o + i));
+        } else {
+          signatures.set(s.signatures, 96 * o);
+        }
+      }
+      o += n;
+    }
+    return {counts, messages, indices, signatures};
+  }
+
   _runPass(jobs) {
     const m = this.metrics;
     const now = Date.now();
@@ -443,8 +464,7 @@ class GpuBlsVerifier {
     let pass;
     const t0 = process.hrtime();
     try {
-      pass = this.addon.submitPass(this.ctx, sm.length ? sm.map((j) => ({sets: j.sets, message: j.message})) : null,
-        df.length ? df.map((j) => j.sets) : null);
+      pass = this.addon.submitPass(this.ctx, sm.length ? this._packSameMessage(sm) : null, df.length ? df.map((j) => j.sets) : null);
     } catch (e) {
       for (const j of jobs) j.reject(e);
       return;
@@ -484,15 +504,24 @@ class GpuBlsVerifier {
       for (const j of sm) j.reject(res);
       return;
     }
-    sm.forEach((j, k) => {
-      const r = res[k];
+    // res: one 0 / 1 byte per set of the pass (the flat form); a job's sets start at job.off
+    sm.forEach((j) => {
+      const n = j.sets.length;
+      let r, all = true;
+      if (Array.isArray(j.sets)) {
+        r = new Array(n);
+        for (let i = 0; i < n; ++i) all = (r[i] = res[j.off + i] === 1) && all;
+      } else {
+        r = res.subarray(j.off, j.off + n);
+        all = r.indexOf(0) < 0;
+      }
       m.successJobsSignatureSetsCount.inc(1);
-      if (ArrayBuffer.isView(r) ? r.indexOf(0) < 0 : r.every(Boolean)) {
-        m.batchSigsSuccess.inc(r.length);
+      if (all) {
+        m.batchSigsSuccess.inc(n);
       } else {
         // the chunk's aggregate check failed: its sets were verified one by one on the device
         m.sameMessageRetryJobs.inc(1);
-        m.sameMessageRetrySets.inc(r.length);
+        m.sameMessageRetrySets.inc(n);
       }
       j.resolve(r);
     });

@@ -39,14 +39,12 @@ class FakeAddon {
   }
   submitPass(ctx, sm, df) {
     if (this.closed) throw Object.assign(new Error("QUEUE_ABORTED"), {code: "QUEUE_ABORTED"});
-    const rec = {sm: sm ? sm.map((c) => c.sets.length) : null, df: df ? df.map((c) => c.length) : null};
+    const rec = {sm: null, df: df ? df.map((c) => c.length) : null};
     this.passes.push(rec);
-    // a packed chunk {indices, signatures, length} answers with a Uint8Array, like the addon
-    const smRes = (c) => (Array.isArray(c.sets) ? c.sets.map((s) => this.valid(s))
-      : Uint8Array.from({length: c.sets.length}, (_, i) => (Array.isArray(c.sets.signatures)
-        ? (c.sets.signatures[i].length === 96 && c.sets.signatures[i][0] === 1 ? 1 : 0) : (c.sets.signatures[96 * i] === 1 ? 1 : 0))));
+    // the flat pass form {counts, messages, indices, signatures}: one 0 / 1 byte per set, like the addon
+    if (sm) rec.sm = Array.from(sm.counts);
     const res = {
-      sameMessage: sm ? sm.map(smRes) : null,
+      sameMessage: sm ? Uint8Array.from({length: sm.indices.length}, (_, i) => (sm.signatures[96 * i] === 1 ? 1 : 0)) : null,
       default: df
         ? df.map((c) =>
           c.some((s) => s.indices !== undefined && s.indices.length === 0)
