@@ -57,6 +57,15 @@ FME_RANDOMIZE_PAIR = 2086   # r_i pk_i and r_i sig_i with one shared inversion
 FME_RANDOMIZE_PAIR_JAC = 2096  # the same with P Jacobian (aggregate pubkeys straight from k_vs_agg)
 FME_HASH_TO_G2 = 4808       # RFC 9380 hash_to_G2 (SSWU with one norm exponentiation per map + 3-isogeny + h_eff + to affine)
 FME_MILLER_1J = 7244        # Miller value of one pair, Jacobian P
+# k_vs_miller_group: k pairs on one accumulator (one f^2 per bit): the first pair 7256 (P with Z != 1,
+# as r_i pk_i is on the device), each further pair 5012 (its lines without another squaring)
+FME_MILLER_GROUP_FIRST = 7256
+FME_MILLER_GROUP_MORE = 5012
+
+
+def fme_miller_group(k):
+    return FME_MILLER_GROUP_FIRST + (k - 1) * FME_MILLER_GROUP_MORE
+
 FME_G1_SCAN = 48            # 3-level 8-lane chunk scan of r_i pk_i (3 Jacobian G1 additions)
 FME_G2_DECODE = 941         # G2 decompression alone (k_sig_decode, k_vs_sig_decode)
 FME_G2_SUBGROUP = FME_SIG_VALIDATE - FME_G2_DECODE  # the psi-based G2 subgroup check (1170)
@@ -1056,9 +1065,10 @@ def vs_shard_main(args, v, sk_ints, world, rank, local_rank, dist, log):
 def vs_shard_measure(args, v, sk_ints, world, rank, log):
     """--mode vs-shard (and the `vs_shard` object of a multi-GPU gossip line): ONE verifySignatureSets
     call (args.shard_calls x 128 sets of 128-member aggregates, a C3-sized range-sync / replay call) sharded over the ranks by cost-balanced
-    contiguous ranges (lodestar_amd/sharded.py).  Each rank stages its shard in HBM; a step is
+    contiguous ranges (lodestar_amd/sharded.py).  Each rank stages its shard in HBM (twice); a step is
     gbv_vs_batch_partial (the shard's Fp12 Miller product) -> 577-byte RCCL all-gather -> one final
-    exponentiation over all partials (gbv_fp12_check) on every rank.  Before timing: the sharded
+    exponentiation over all partials (gbv_fp12_check) on every rank, streamed with two shard passes
+    in flight per rank (verify_staged_shards).  Before timing: the sharded
     answer equals the single-GPU gbv_verify_sets answer, and a call with one wrong signature in
     another shard is false."""
     import torch
@@ -1070,7 +1080,10 @@ def vs_shard_measure(args, v, sk_ints, world, rank, log):
     rng = np.random.Generator(np.random.PCG64(0x5A))
     sets = _agg_sets(v, sk_ints, 128 * args.shard_calls, b"gbv-shard", rng)
     lo, hi = sv.shard_of(sets)
-    staged = v.stage_signature_sets([sets[lo:hi]])
+    # two staged copies of this rank's shard: the step loop keeps two shard passes in flight
+    # (ShardedVerifier.verify_staged_shards), the exchange of pass k beside pass k + 1's kernels
+    stages = [v.stage_signature_sets([sets[lo:hi]]) for _ in range(2)]
+    staged = stages[0]
     log("vs-shard: %d sets, rank 0 shard [%d, %d), backend %s" % (len(sets), lo, hi, backend))
     assert sv.verify_staged_shard(staged) is True
     single = v.verify_signature_sets_sync(sets) if rank == 0 else None  # the same call on one GPU
@@ -1080,20 +1093,25 @@ def vs_shard_measure(args, v, sk_ints, world, rank, log):
     bad_small = bad[-256:]  # one-shot marshalling kept small: the wrong set sits in the last rank's share
     wrong = sv.verify_signature_sets(bad_small)
     ok_small = sv.verify_signature_sets(sets[-256:])
-    for _ in range(args.warmup):
-        assert sv.verify_staged_shard(staged) is True
+    seq = [stages[k % 2] for k in range(args.steps)]
+    if args.warmup:
+        assert sv.verify_staged_shards(seq[:max(2, args.warmup)]) == [True] * max(2, args.warmup)
     tdist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        assert sv.verify_staged_shard(staged) is True
+    assert sv.verify_staged_shards(seq) == [True] * args.steps
     torch.cuda.synchronize()
     tdist.barrier()
     elapsed = time.perf_counter() - t0
     t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
     tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
     elapsed = float(t.item())
-    staged.close()
+    # one pass alone (no overlap), for the per-pass latency the multi-GPU projection uses
+    t1 = time.perf_counter()
+    assert sv.verify_staged_shard(staged) is True
+    lone_ms = (time.perf_counter() - t1) * 1e3
+    for st in stages:
+        st.close()
     line = None
     if rank == 0:
         line = {"metric": "signature sets verified/sec (one verifySignatureSets call sharded over GPUs: Fp12 partials + RCCL all-gather)",
@@ -1104,7 +1122,8 @@ def vs_shard_measure(args, v, sk_ints, world, rank, log):
                 "config": {"workload": "C3-shaped call of %d aggregate sets as ONE verifySignatureSets call" % len(sets),
                            "parallelism": "cost-balanced shards%d + RCCL all-gather of 577-byte Fp12 partials" % world},
                 "world_size": world, "backend": backend, "gathered_from_ranks": list(range(world)),
-                "partial_bytes_per_gpu": 577, "rank0_shard": [lo, hi],
+                "partial_bytes_per_gpu": 577, "rank0_shard": [lo, hi], "passes_in_flight": 2,
+                "lone_pass_ms": round(lone_ms, 3),
                 "parity": {"sharded_equals_single_gpu": single is True, "wrong_signature_call_false": wrong is False,
                            "clean_small_call_true": ok_small is True}}
     return line

@@ -207,6 +207,12 @@ int gbv_vs_partial(gbv_ctx* ctx, const gbv_set* sets, size_t n, const uint32_t* 
 /* The same partial over every set of a staged batch (gbv_vs_batch_create / fill: all its calls as
  * one shard), device-resident inputs: the multi-GPU range-sync / replay form. */
 int gbv_vs_batch_partial(gbv_ctx* ctx, gbv_vs_batch* b, uint8_t out576[GBV_FP12_PARTIAL_BYTES], uint8_t* shard_ok);
+/* gbv_vs_batch_partial in two halves, so that a rank keeps several shard passes in flight (the
+ * exchange and final exponentiation of pass k overlap the kernels of pass k + 1, lodestar_amd/sharded.py
+ * verify_staged_shards): submit enqueues without a host wait (EMPTY_AGGREGATE rejects here); wait
+ * blocks on the pass, without the context lock, and writes the partial and shard_ok. */
+int gbv_vs_batch_partial_submit(gbv_ctx* ctx, gbv_vs_batch* b);
+int gbv_vs_batch_partial_wait(gbv_ctx* ctx, gbv_vs_batch* b, uint8_t out576[GBV_FP12_PARTIAL_BYTES], uint8_t* shard_ok);
 int gbv_fp12_check(gbv_ctx* ctx, const uint8_t* partials576, size_t k, uint8_t* is_one);
 
 /* Device time (ms, summed over launches) and launch count of each kernel of the last

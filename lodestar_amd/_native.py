@@ -29,7 +29,7 @@ EXPORTED_SYMBOLS = (
     "gbv_attestation_signing_roots", "gbv_ssz_last_kernel_ms", "gbv_verify_sets_multi", "gbv_vs_batch_create",
     "gbv_vs_batch_submit", "gbv_vs_batch_wait", "gbv_vs_batch_destroy", "gbv_vs_last_kernel_ms",
     "gbv_aggregate_serialized_pubkeys", "gbv_signatures_validate", "gbv_aggregate_signatures",
-    "gbv_sm_batch_fill", "gbv_vs_batch_fill", "gbv_vs_batch_partial", "gbv_tune", "gbv_last_ops",
+    "gbv_sm_batch_fill", "gbv_vs_batch_fill", "gbv_vs_batch_partial", "gbv_vs_batch_partial_submit", "gbv_vs_batch_partial_wait", "gbv_tune", "gbv_last_ops",
 )
 
 
@@ -119,6 +119,8 @@ def load_library(path=LIB_PATH):
         "gbv_sm_batch_fill": (i32, [vp, vp, sz, vp, vp, vp, vp]),
         "gbv_vs_batch_fill": (i32, [vp, vp, sz, vp, P(GbvSet), vp]),
         "gbv_vs_batch_partial": (i32, [vp, vp, vp, vp]),
+        "gbv_vs_batch_partial_submit": (i32, [vp, vp]),
+        "gbv_vs_batch_partial_wait": (i32, [vp, vp, vp, vp]),
         "gbv_tune": (i32, [vp, cp, u32]),
         "gbv_last_ops": (i32, [vp, i32, vp, sz]),
     }

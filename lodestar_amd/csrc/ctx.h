@@ -125,6 +125,7 @@ struct gbv_ctx {
   // at once, one per hardware queue (GPU_MAX_HW_QUEUES=4).
   hipStream_t stream = nullptr, stream2 = nullptr, stream4 = nullptr;
   hipStream_t stream5 = nullptr;
+  hipStream_t stream6 = nullptr;  // gbv_fp12_check: the multi-GPU exchange's final check, beside streamed shard passes
   gbv::G1A* table = nullptr;
   uint8_t* table_ok = nullptr;
   size_t table_cap = 0;

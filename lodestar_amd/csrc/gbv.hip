@@ -32,7 +32,7 @@ int gbv_fail(gbv_ctx* c, int code, const std::string& msg) {
 }
 
 void ctx_drain(gbv_ctx* c) {
-  for (hipStream_t s : {c->stream, c->stream2, c->stream4, c->stream5})
+  for (hipStream_t s : {c->stream, c->stream2, c->stream4, c->stream5, c->stream6})
     if (s) (void)hipStreamSynchronize(s);
   (void)hipGetLastError();
 }
@@ -233,9 +233,10 @@ int gbv_init(int device, gbv_ctx** out) {
             hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, prio_lo) == hipSuccess &&
             hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, prio_hi) == hipSuccess &&
             hipStreamCreateWithPriority(&c->stream4, hipStreamNonBlocking, prio_hi) == hipSuccess &&
-            hipStreamCreateWithPriority(&c->stream5, hipStreamNonBlocking, prio_hi) == hipSuccess;
+            hipStreamCreateWithPriority(&c->stream5, hipStreamNonBlocking, prio_hi) == hipSuccess &&
+            hipStreamCreateWithPriority(&c->stream6, hipStreamNonBlocking, prio_hi) == hipSuccess;
   if (!ok) {
-    for (hipStream_t s : {c->stream, c->stream2, c->stream4, c->stream5})
+    for (hipStream_t s : {c->stream, c->stream2, c->stream4, c->stream5, c->stream6})
       if (s) hipStreamDestroy(s);
     delete c;
     return GBV_E_DEVICE;
@@ -255,7 +256,7 @@ void gbv_destroy(gbv_ctx* c) {
   hipSetDevice(c->device);
   c->closed = true;
   // every stream drains before anything it may still read or write is freed
-  for (hipStream_t s : {c->stream, c->stream2, c->stream4, c->stream5})
+  for (hipStream_t s : {c->stream, c->stream2, c->stream4, c->stream5, c->stream6})
     if (s) hipStreamSynchronize(s);
   sm_destroy(c->sm_scratch);
   vs_batch_free(c->vs_scratch);
@@ -268,7 +269,7 @@ void gbv_destroy(gbv_ctx* c) {
   for (auto* p : c->ssz_buf) hipFree(p);
   for (auto e : c->ssz_ev)
     if (e) hipEventDestroy(e);
-  for (hipStream_t s : {c->stream, c->stream2, c->stream4, c->stream5})
+  for (hipStream_t s : {c->stream, c->stream2, c->stream4, c->stream5, c->stream6})
     if (s) hipStreamDestroy(s);
   delete c;
 }
@@ -1191,7 +1192,8 @@ bool tuning_set(const char* name, uint32_t v) {
       {"hash_pair_max", &g_tuning.hash_pair_max}, {"hash_quad_max", &g_tuning.hash_quad_max}, {"hash_coop_max", &g_tuning.hash_coop_max},
       {"prepare_split_max", &g_tuning.prepare_split_max}, {"chunk_finish_wave_max", &g_tuning.chunk_finish_wave_max},
       {"vs_pre_max", &g_tuning.vs_pre_max}, {"vs_fs_maxc", &g_tuning.vs_fs_maxc}, {"vs_quad_max", &g_tuning.vs_quad_max},
-      {"vs_pair_max", &g_tuning.vs_pair_max}};
+      {"vs_pair_max", &g_tuning.vs_pair_max}, {"vs_miller_k", &g_tuning.vs_miller_k}};
+  if (!strcmp(name, "vs_miller_k") && v != 1 && v != 2 && v != 4) return false;
   for (auto& t : tab)
     if (!strcmp(name, t.n)) {
       *t.p = v;

@@ -40,6 +40,9 @@ struct gbv_vs_batch {
   uint32_t *set_off = nullptr, *arena = nullptr, *agg_list = nullptr, *chunk_off = nullptr, *siglen = nullptr;
   uint4 *big = nullptr, *slices = nullptr;  // large aggregates: (set, first slice, count), slice (begin, end)
   uint8_t *raw_flag = nullptr, *raw_pk = nullptr, *msgs = nullptr, *sig = nullptr;
+  uint2* grp = nullptr;  // Miller groups (begin, end) of vs_miller_k sets within a chunk, or null
+  size_t ng = 0;
+  uint32_t mk = 1;
   // work
   G1J* pk = nullptr;  // aggregate pubkeys (Jacobian, k_vs_agg / k_vs_agg_big)
   uint8_t* pk_st = nullptr;
@@ -72,6 +75,7 @@ struct gbv_vs_batch {
   hipEvent_t copied = nullptr;  // the last fill's input copy (stream A); see gbv_sm_batch::copied
   hipEvent_t pre = nullptr;     // "pre" mode: k_vs_sig_pre_quad done (stream 5)
   bool in_flight = false;
+  bool part_in_flight = false;  // gbv_vs_batch_partial_submit'ed, not yet waited
   int tail = 0;
   KProf prof;  // per-kernel events of the last submit / partial (ctx kprof_on)
 };
@@ -87,7 +91,7 @@ static void vs_free_work(gbv_vs_batch* b) {
 
 void vs_batch_free(gbv_vs_batch* b) {
   if (!b) return;
-  if (b->in_flight && b->done) (void)hipEventSynchronize(b->done);
+  if ((b->in_flight || b->part_in_flight) && b->done) (void)hipEventSynchronize(b->done);
   if (b->copied) {
     (void)hipEventSynchronize(b->copied);
     (void)hipEventDestroy(b->copied);
@@ -137,7 +141,7 @@ static int vs_reserve(gbv_ctx* c, gbv_vs_batch* b, size_t n, size_t C) {
 // Stage n_calls calls (CSR call_off over sets) in b.  Argument errors fail the whole fill;
 // empty aggregates only mark their call rejected.
 static int vs_fill(gbv_ctx* c, gbv_vs_batch* b, size_t n_calls, const uint32_t* call_off, const gbv_set* sets, const uint32_t* arena) {
-  if (b->in_flight) return gbv_fail(c, GBV_E_ARG, "batch in flight");
+  if (b->in_flight || b->part_in_flight) return gbv_fail(c, GBV_E_ARG, "batch in flight");
   if (n_calls && !call_off) return gbv_fail(c, GBV_E_ARG, "null call offsets");
   if (b->copied) HIP_CHECK(c, hipEventSynchronize(b->copied));  // the pinned blob is free again
   size_t n = n_calls ? call_off[n_calls] : 0;
@@ -206,7 +210,13 @@ static int vs_fill(gbv_ctx* c, gbv_vs_batch* b, size_t n_calls, const uint32_t* 
   size_t o_so = 0, o_ar = align256(4 * (n + 1)), o_al = o_ar + align256(4 * A), o_co = o_al + align256(4 * n_agg);
   size_t o_sl = o_co + align256(8 * C), o_rf = o_sl + align256(4 * n), o_rp = o_rf + align256(n), o_m = o_rp + align256(48 * n);
   size_t o_sig = o_m + align256(32 * n), o_big = o_sig + align256((size_t)stride * n), o_slc = o_big + align256(16 * n_big);
-  size_t total = o_slc + align256(16 * n_slices);
+  // Miller groups (k_vs_miller_group): up to vs_miller_k consecutive sets of one chunk per thread
+  const uint32_t mk = tuning().vs_miller_k;
+  size_t ng = 0;
+  if (mk > 1 && n > tuning().vs_pair_max)
+    for (size_t k = 0; k < C; ++k) ng += (chunk_end[k] - chunk_off[k] + mk - 1) / mk;
+  size_t o_gr = o_slc + align256(16 * n_slices);
+  size_t total = o_gr + align256(8 * ng);
   if (b->in_cap < total) {
     hipFree(b->in_dev);
     hipHostFree(b->in_host);
@@ -260,6 +270,12 @@ static int vs_fill(gbv_ctx* c, gbv_vs_batch* b, size_t n_calls, const uint32_t* 
     co[2 * k] = chunk_off[k];
     co[2 * k + 1] = chunk_end[k];
   }
+  uint32_t* gr = (uint32_t*)(h + o_gr);
+  for (size_t k = 0, q = 0; ng && k < C; ++k)
+    for (uint32_t i = chunk_off[k]; i < chunk_end[k]; i += mk, ++q) {
+      gr[2 * q] = i;
+      gr[2 * q + 1] = std::min(i + mk, chunk_end[k]);
+    }
   b->set_off = (uint32_t*)(b->in_dev + o_so);
   b->arena = (uint32_t*)(b->in_dev + o_ar);
   b->agg_list = (uint32_t*)(b->in_dev + o_al);
@@ -271,6 +287,9 @@ static int vs_fill(gbv_ctx* c, gbv_vs_batch* b, size_t n_calls, const uint32_t* 
   b->sig = b->in_dev + o_sig;
   b->big = (uint4*)(b->in_dev + o_big);
   b->slices = (uint4*)(b->in_dev + o_slc);
+  b->grp = ng ? (uint2*)(b->in_dev + o_gr) : nullptr;
+  b->ng = ng;
+  b->mk = mk;
   // no host wait: stream A runs the copy ahead of the batch's kernels, other streams wait for the event
   if (!b->copied) HIP_CHECK(c, hipEventCreateWithFlags(&b->copied, hipEventDisableTiming));
   HIP_CHECK(c, hipMemcpyAsync(b->in_dev, h, total, hipMemcpyHostToDevice, c->stream));
@@ -347,7 +366,7 @@ static int vs_enqueue_sets(gbv_ctx* c, gbv_vs_batch* b, hipStream_t m, bool with
   if (b->n <= VS_COOP_MILLER_MAX)  // latency: one wave per set (cooperative Miller loop)
     launch_vs_miller_coop(m, (uint32_t)b->n, b->status, b->rP, b->H, b->F);
   else
-    launch_vs_miller(LaunchCfg{blocks_for(b->n), TPB, m}, (uint32_t)b->n, b->status, b->rP, b->H, b->F);
+    launch_vs_miller(LaunchCfg{blocks_for(b->n), TPB, m}, (uint32_t)b->n, b->status, b->rP, b->H, b->F, (uint32_t)b->ng, b->grp, b->mk);
   HIP_CHECK(c, hipEventRecord(b->ev[4], m));
   if (pre && small) {
     HIP_CHECK(c, hipStreamWaitEvent(m, b->ev[6], 0));
@@ -419,7 +438,7 @@ int gbv_vs_batch_submit(gbv_ctx* c, gbv_vs_batch* b) {
   if (!c || !b) return GBV_E_ARG;
   GBV_LOCK(c);
   if (c->closed) return GBV_E_CLOSED;
-  if (b->in_flight) return gbv_fail(c, GBV_E_ARG, "batch already in flight");
+  if (b->in_flight || b->part_in_flight) return gbv_fail(c, GBV_E_ARG, "batch already in flight");
   HIP_CHECK(c, hipSetDevice(c->device));
   if (b->n == 0 || b->C == 0) return GBV_OK;
   int rc = vs_submit_enqueue(c, b);
@@ -546,19 +565,36 @@ int gbv_vs_partial(gbv_ctx* c, const gbv_set* sets, size_t n, const uint32_t* ar
   return vs_partial_collect(c, b, out576, shard_ok);
 }
 
-int gbv_vs_batch_partial(gbv_ctx* c, gbv_vs_batch* b, uint8_t out576[GBV_FP12_PARTIAL_BYTES], uint8_t* shard_ok) {
+int gbv_vs_batch_partial_submit(gbv_ctx* c, gbv_vs_batch* b) {
+  if (!c || !b) return GBV_E_ARG;
+  GBV_LOCK(c);
+  if (c->closed) return GBV_E_CLOSED;
+  if (b->in_flight || b->part_in_flight) return gbv_fail(c, GBV_E_ARG, "batch in flight");
+  for (uint8_t r : b->call_reject)
+    if (r) return gbv_fail(c, GBV_E_EMPTY_AGGREGATE, "EMPTY_AGGREGATE_ARRAY");
+  int rc = vs_partial_enqueue(c, b);
+  if (rc) return rc;
+  b->part_in_flight = true;
+  return GBV_OK;
+}
+
+int gbv_vs_batch_partial_wait(gbv_ctx* c, gbv_vs_batch* b, uint8_t out576[GBV_FP12_PARTIAL_BYTES], uint8_t* shard_ok) {
   if (!c || !b || !out576 || !shard_ok) return GBV_E_ARG;
   {
     GBV_LOCK(c);
-    if (c->closed) return GBV_E_CLOSED;
-    if (b->in_flight) return gbv_fail(c, GBV_E_ARG, "batch in flight");
-    *shard_ok = 1;
-    for (uint8_t r : b->call_reject)
-      if (r) return gbv_fail(c, GBV_E_EMPTY_AGGREGATE, "EMPTY_AGGREGATE_ARRAY");
-    int rc = vs_partial_enqueue(c, b);
-    if (rc) return rc;
+    if (!b->part_in_flight) return gbv_fail(c, GBV_E_ARG, "partial not submitted");
+    b->part_in_flight = false;  // the batch belongs to this caller: collected below without the lock
   }
+  *shard_ok = 1;
   return vs_partial_collect(c, b, out576, shard_ok);
+}
+
+int gbv_vs_batch_partial(gbv_ctx* c, gbv_vs_batch* b, uint8_t out576[GBV_FP12_PARTIAL_BYTES], uint8_t* shard_ok) {
+  if (!c || !b || !out576 || !shard_ok) return GBV_E_ARG;
+  *shard_ok = 1;
+  int rc = gbv_vs_batch_partial_submit(c, b);
+  if (rc) return rc;
+  return gbv_vs_batch_partial_wait(c, b, out576, shard_ok);
 }
 
 static int vs_partial_enqueue(gbv_ctx* c, gbv_vs_batch* b) {
@@ -587,9 +623,11 @@ static int vs_partial_enqueue(gbv_ctx* c, gbv_vs_batch* b) {
   }
   HIP_CHECK(c, hipSetDevice(c->device));
   KProfScope kp(c->kprof_on ? &b->prof : nullptr);
-  // a shard of up to GBV_VS_PRE_MAX sets (a per-GPU share of one large call at N = 8): the hash on the
-  // tail stream beside the split signature / pubkey halves, the rest on the tail stream after them
-  hipStream_t s = vs_pre_on(b) ? c->stream2 : c->stream;
+  // a shard of up to vs_pre_max sets (a per-GPU share of one large call at N = 8): the hash on the
+  // tail stream beside the split signature / pubkey halves, the rest on the tail stream after them;
+  // larger shards: the per-set kernels on stream A, the Miller values and the reduction on the tail.
+  // The tail alternates per submit (stream 2 / stream 4) so that streamed shard passes overlap.
+  hipStream_t s = (c->sm_submits++ & 1) ? c->stream4 : c->stream2;
   if ((rc = vs_enqueue_sets(c, b, s, false, true))) {
     ctx_drain(c);
     return rc;
@@ -634,7 +672,9 @@ int gbv_fp12_check(gbv_ctx* c, const uint8_t* partials, size_t k, uint8_t* is_on
   GBV_LOCK(c);
   if (c->closed) return GBV_E_CLOSED;
   HIP_CHECK(c, hipSetDevice(c->device));
-  hipStream_t s = c->stream;
+  // a stream of its own (high priority): the check of shard pass k does not queue behind pass
+  // k + 1's kernels (sharded.py verify_staged_shards keeps two in flight)
+  hipStream_t s = c->stream6;
   uint8_t *d = nullptr, *h = nullptr;
   size_t o_o = align256(sizeof(Fp12) * std::max<size_t>(k, 1));
   int rc;

@@ -122,7 +122,8 @@ void launch_vs_pk_rand(hipStream_t s, uint32_t n, const uint32_t* set_off, const
 void launch_vs_miller_coop(hipStream_t s, uint32_t n, const uint8_t* status, const G1J* rP, const G2A* H, Fp12* F);
 void launch_vs_chunk_s_miller(hipStream_t s, uint32_t C, const uint8_t* status, const uint32_t* chunk_be, const G2J* rS, Fp12* Fs,
                               uint8_t* fs_flag);
-void launch_vs_miller(LaunchCfg c, uint32_t n, const uint8_t* status, const G1J* rP, const G2A* H, Fp12* F);
+void launch_vs_miller(LaunchCfg c, uint32_t n, const uint8_t* status, const G1J* rP, const G2A* H, Fp12* F, uint32_t ng = 0,
+                      const uint2* grp = nullptr, uint32_t k = 1);
 void launch_sig_validate(LaunchCfg c, uint32_t n, const uint8_t* sig, uint32_t sig_len, uint8_t* status, uint8_t* out96);
 void launch_sig_aggregate(hipStream_t s, uint32_t n, const uint8_t* sig, uint32_t sig_len, int validate, G2J* part, uint32_t* bad,
                           uint8_t* out96);

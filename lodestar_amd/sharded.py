@@ -11,7 +11,8 @@ Two shapes, both keeping the reference's booleans:
   the reference's <=128-set jobs (multithread/index.ts:157-207), up to the 2^-64 error of
   randomised batch verification that each job check has as well.
 * ``verify_same_message_multi`` -- many independent verifySignatureSetsSameMessage calls (the gossip
-  stream): calls are split across ranks with no collective on the data path; each rank verifies its
+  stream): calls are split across ranks in contiguous ranges of near-equal SET count, with no
+  collective on the data path; each rank verifies its
   own calls (per-set retries of failing chunks included, jobItem.ts:93-125) and the per-set booleans
   are all-gathered so every rank returns the full result.
 
@@ -108,33 +109,95 @@ class ShardedVerifier:
         """The same exchange for a call whose shard this rank has staged in HBM beforehand
         (StagedSignatureSets over shard_of(call)): gbv_vs_batch_partial -> 577-byte all-gather ->
         one final exponentiation (gbv_fp12_check) on every rank.  Every rank must call it together."""
-        from ._native import GbvError
         status, part = 2, bytes(PARTIAL_BYTES)
         try:
             part, ok = staged.partial()
             status = 1 if ok else 0
-        finally:
+        finally:  # a device error still takes part in the collective, then raises here
             blobs = self._all_gather_bytes(bytes(part) + bytes([status]), PARTIAL_BYTES + 1)
+        return self._decide(blobs)
+
+    def _exchange(self, part: bytes, status: int) -> bool:
+        return self._decide(self._all_gather_bytes(bytes(part) + bytes([status]), PARTIAL_BYTES + 1))
+
+    def _decide(self, blobs: List[bytes]) -> bool:
+        from ._native import GbvError
         if any(b[PARTIAL_BYTES] == 2 for b in blobs):
             raise GbvError(-2, "device error on a peer rank")
         if not all(b[PARTIAL_BYTES] == 1 for b in blobs):
             return False
         return self.device.fp12_check([b[:PARTIAL_BYTES] for b in blobs])
 
+    def verify_staged_shards(self, staged: Sequence, depth: int = 2) -> List[bool]:
+        """verify_staged_shard over a sequence of staged shards (one per call, or the same shards
+        re-verified: a range-sync stream of segments), streamed: up to `depth` shard passes in flight
+        on this rank (gbv_vs_batch_partial_submit), so the all-gather and final exponentiation of
+        pass k run while pass k + 1's kernels are on the device.  Pass k + depth is submitted before
+        pass k's exchange.  A handle must not appear twice within `depth` consecutive entries.  Every
+        rank calls it together with sequences of the same length; one answer per entry."""
+        n = len(staged)
+        depth = max(1, depth)
+        out: List[bool] = []
+        submitted = [False] * n
+        failed = None  # a local device error: this rank still joins every exchange, then raises
+
+        def submit(j):
+            nonlocal failed
+            if j < n and failed is None:
+                try:
+                    staged[j].partial_submit()
+                    submitted[j] = True
+                except Exception as e:  # noqa: BLE001 - reported after the collective
+                    failed = e
+
+        for j in range(min(depth, n)):
+            submit(j)
+        for k in range(n):
+            status, part = 2, bytes(PARTIAL_BYTES)
+            if submitted[k]:
+                try:
+                    part, ok = staged[k].partial_wait()
+                    status = 1 if ok else 0
+                except Exception as e:  # noqa: BLE001
+                    failed = failed or e
+                submitted[k] = False
+            submit(k + depth)  # before the exchange: the next pass overlaps it
+            try:
+                out.append(self._exchange(part, status))
+            except Exception:
+                for j in range(k + 1, n):  # drain what this rank still has in flight
+                    if submitted[j]:
+                        try:
+                            staged[j].partial_wait()
+                        except Exception:  # noqa: BLE001
+                            pass
+                raise
+        if failed is not None:
+            raise failed
+        return out
+
     # ---- many same-message calls (gossip stream / epoch replay) ----------------------------------
-    def calls_of(self, n_calls: int) -> Tuple[int, int]:
+    def call_ranges(self, sizes: Sequence[int]) -> List[Tuple[int, int]]:
+        """Contiguous call ranges, one per rank, balanced by SET count (the per-set work is what the
+        device does; call counts would give a rank of 128-set calls 4x the work of a rank of 32-set
+        ones)."""
+        return balanced_ranges([max(1, int(x)) for x in sizes], self.world)
+
+    def calls_of(self, n_calls: int, sizes: Optional[Sequence[int]] = None) -> Tuple[int, int]:
+        if sizes is not None:
+            return self.call_ranges(sizes)[self.rank]
         per = (n_calls + self.world - 1) // self.world
         return min(self.rank * per, n_calls), min((self.rank + 1) * per, n_calls)
 
     def verify_same_message_multi(self, calls: Sequence[Tuple[Sequence[Tuple[int, bytes]], bytes]]) -> List[List[bool]]:
         from ._native import GbvError
-        lo, hi = self.calls_of(len(calls))
-        # gather per-set booleans: fixed-size payload = all sets of the widest rank's slice, plus a
+        sizes = [len(c[0]) for c in calls]
+        ranges = self.call_ranges(sizes)
+        lo, hi = ranges[self.rank]
+        # gather per-set booleans: fixed-size payload = all sets of the widest rank's range, plus a
         # status byte (1 ok, 2 this rank raised) so a rank whose device call raises still joins the
         # collective and every rank raises together instead of the others blocking in all_gather
-        sizes = [len(c[0]) for c in calls]
-        per = (len(calls) + self.world - 1) // self.world
-        width = max((sum(sizes[r * per:(r + 1) * per]) for r in range(self.world)), default=0)
+        width = max((sum(sizes[a:b]) for a, b in ranges), default=0)
         flat, status = b"", 2
         try:
             mine = self.device.verify_same_message_multi_sync(list(calls[lo:hi])) if hi > lo else []
@@ -146,8 +209,7 @@ class ShardedVerifier:
             raise GbvError(-2, "device error on a peer rank")
         blobs = [b[1:] for b in blobs]
         out: List[List[bool]] = []
-        for r in range(self.world):
-            clo, chi = min(r * per, len(calls)), min((r + 1) * per, len(calls))
+        for r, (clo, chi) in enumerate(ranges):
             pos = 0
             for g in range(clo, chi):
                 out.append([x == 1 for x in blobs[r][pos:pos + sizes[g]]])

@@ -1046,6 +1046,21 @@ class StagedSignatureSets:
         v.device_passes += 1
         return out.raw, bool(ok.value)
 
+    def partial_submit(self):
+        """The first half of partial() (gbv_vs_batch_partial_submit): enqueue without a host wait, so
+        that several shard passes are in flight (sharded.py verify_staged_shards)."""
+        v = self._v
+        _native.check(v._lib, v._ctx, v._lib.gbv_vs_batch_partial_submit(v._ctx, self._h))
+
+    def partial_wait(self) -> Tuple[bytes, bool]:
+        """The second half: block on the submitted pass; (576-byte blob, shard_ok) as partial()."""
+        v = self._v
+        out = ctypes.create_string_buffer(576)
+        ok = ctypes.c_uint8(0)
+        _native.check(v._lib, v._ctx, v._lib.gbv_vs_batch_partial_wait(v._ctx, self._h, out, ctypes.byref(ok)))
+        v.device_passes += 1
+        return out.raw, bool(ok.value)
+
     def close(self):
         # the verifier destroys live handles before its context; after that there is nothing to free
         if self._h and self._v._ctx is not None:

@@ -32,6 +32,7 @@ struct gbv_sm_batch {
   uint8_t* valid;
   double ready;
   int in_flight;
+  int part_flying;
 };
 
 struct gbv_vs_batch {
@@ -423,6 +424,22 @@ int gbv_vs_batch_partial(gbv_ctx* c, gbv_vs_batch* b, uint8_t out576[GBV_FP12_PA
   out576[0] = all;
   *shard_ok = 1;
   return GBV_OK;
+}
+
+int gbv_vs_batch_partial_submit(gbv_ctx* c, gbv_vs_batch* b) {
+  if (!c || !b) return GBV_E_ARG;
+  if (b->part_flying) return fail(GBV_E_ARG, "batch in flight");
+  for (size_t g = 0; g < b->n_calls; ++g)
+    if (b->call_valid[g] == GBV_CALL_REJECTED) return fail(GBV_E_EMPTY_AGGREGATE, "EMPTY_AGGREGATE_ARRAY");
+  b->part_flying = 1;
+  return GBV_OK;
+}
+
+int gbv_vs_batch_partial_wait(gbv_ctx* c, gbv_vs_batch* b, uint8_t out576[GBV_FP12_PARTIAL_BYTES], uint8_t* shard_ok) {
+  if (!c || !b || !out576 || !shard_ok) return GBV_E_ARG;
+  if (!b->part_flying) return fail(GBV_E_ARG, "partial not submitted");
+  b->part_flying = 0;
+  return gbv_vs_batch_partial(c, b, out576, shard_ok);
 }
 
 int gbv_fp12_check(gbv_ctx* c, const uint8_t* partials, size_t k, uint8_t* is_one) {

@@ -375,6 +375,33 @@ unsigned long long ht_count_miller_1j(const uint8_t* p96, const uint8_t* q192) {
   (void)miller_loop_1j(P, Q);
   return g_fme_count;
 }
+// k_vs_miller_group's shared-accumulator loop against the product of per-pair Miller values: P_j =
+// 2 (p_j) (Jacobian, Z != 1), Q_j affine; mode 0 = product of miller_loop_1j, 1 = miller_loop_kj_to<4>,
+// 2 = miller_loop_kj_to<2> (k <= 2).  out = the Fp12 (12 canonical Fp, tower order); returns the FME count.
+unsigned long long ht_miller_group(uint8_t* out, const uint8_t* p96, const uint8_t* q192, int k, int mode) {
+  G1J P[4];
+  G2A Q[4];
+  for (int j = 0; j < k; ++j) {
+    P[j] = jac_dbl(jac_from_aff(G1A{load_mont(p96 + 96 * j), load_mont(p96 + 96 * j + 48)}));
+    Q[j] = G2A{load_fp2(q192 + 192 * j), load_fp2(q192 + 192 * j + 96)};
+  }
+  g_fme_count = 0;
+  Fp12 f;
+  if (mode == 0) {
+    f = fp12_one();
+    for (int j = 0; j < k; ++j) {
+      Fp12 g = miller_loop_1j(P[j], Q[j]);
+      f = fp12_mul(f, g);
+    }
+  } else if (mode == 1) {
+    miller_loop_kj_to<4>(&f, P, Q, k);
+  } else {
+    miller_loop_kj_to<2>(&f, P, Q, k);
+  }
+  const Fp2* c[6] = {&f.c0.c0, &f.c0.c1, &f.c0.c2, &f.c1.c0, &f.c1.c1, &f.c1.c2};
+  for (int i = 0; i < 6; ++i) store_fp2(out + 96 * i, *c[i]);
+  return g_fme_count;
+}
 // one mixed G1 addition (the gather-aggregate step), one full G1 addition (tree step),
 // one Fp12 product, one Jacobian G2 addition, one final exponentiation
 unsigned long long ht_count_op(int which, const uint8_t* p96, const uint8_t* q192) {

@@ -43,6 +43,8 @@ class OracleDevice:
     def __init__(self, pks):
         self.pks = pks
         self.rng = random.Random(os.getpid())
+        self.in_flight = 0
+        self.max_in_flight = 0
 
     def _pk(self, s):
         if isinstance(s, AggregatedSignatureSet):
@@ -96,13 +98,28 @@ def _sets(sks, bad=None):
 
 
 class OracleStaged:
-    """Stand-in for a StagedSignatureSets holding this rank's shard (ShardedVerifier.verify_staged_shard)."""
+    """Stand-in for a StagedSignatureSets holding this rank's shard (ShardedVerifier.verify_staged_shard,
+    verify_staged_shards): partial(), or partial_submit() / partial_wait() with the passes in flight
+    counted on the device stand-in."""
 
     def __init__(self, device, sets):
         self.device, self.sets = device, sets
+        self.flying = None
 
     def partial(self):
         return self.device.vs_partial(self.sets)
+
+    def partial_submit(self):
+        assert self.flying is None, "submitted twice"
+        self.flying = self.device.vs_partial(self.sets)
+        self.device.in_flight += 1
+        self.device.max_in_flight = max(self.device.max_in_flight, self.device.in_flight)
+
+    def partial_wait(self):
+        assert self.flying is not None, "not submitted"
+        r, self.flying = self.flying, None
+        self.device.in_flight -= 1
+        return r
 
 
 def _worker(rank, world, port, q):
@@ -125,6 +142,17 @@ def _worker(rank, world, port, q):
             call = _sets(sks, bad)
             lo, hi = sv.shard_of(call)
             res[name] = sv.verify_staged_shard(OracleStaged(sv.device, call[lo:hi]))
+        # streamed: four staged calls (two valid, one wrong message, one malformed in the last shard)
+        # with two shard passes in flight on each rank; one answer per call
+        stream = []
+        for bad in (None, "wrong_msg", None, "malformed_last"):
+            call = _sets(sks, bad)
+            lo, hi = sv.shard_of(call)
+            stream.append(OracleStaged(sv.device, call[lo:hi]))
+        res["streamed"] = sv.verify_staged_shards(stream, depth=2)
+        res["streamed_max_in_flight"] = sv.device.max_in_flight
+        res["streamed_left"] = sv.device.in_flight
+        res["ranges"] = sv.call_ranges([128, 128] + [32] * 8)
         res["empty"] = sv.verify_signature_sets([])
         try:
             sv.verify_signature_sets(_sets(sks) + [AggregatedSignatureSet([], bytes(32), bytes(96))])
@@ -187,6 +215,9 @@ def test_sharded_world2_gloo():
         assert r["valid"] is True and r["wrong_msg"] is False and r["malformed"] is False
         assert r["malformed_last"] is False
         assert r["staged"] is True and r["staged_wrong"] is False and r["staged_malformed"] is False
+        assert r["streamed"] == [True, False, True, False]
+        assert r["streamed_max_in_flight"] == 2 and r["streamed_left"] == 0
+        assert r["ranges"] == [(0, 2), (2, 10)]  # 256 sets each (by call count: 352 and 160)
         assert r["empty"] is False and r["empty_agg"] == "rejected"
         assert r["sm"] == [[True, True], [True, False], [False]]
         assert r["sm_err"] == "raised"

@@ -1,11 +1,10 @@
-"""Probe of a small verifySignatureSets pass (range-sync segment, C4 shape): builds --blocks blocks with
-bench.make_blocks, then times lone passes (one at a time, no overlap) and prints the median.  Run it
-under `rocprofv3 --kernel-trace` to get the per-kernel timeline of those passes (tools/vs_timeline.py
-prints the last pass).  Usage: python tools/vs_probe.py [--blocks 64] [--reps 5] [--electra]"""
+"""verifySignatureSets probe: the C3 pass (512 calls of 128-member aggregates) and the C1 throughput
+pass (512 calls of 128 single sets) under each Miller form for passes above vs_pair_max
+(vs_miller_k = 1: a thread per set, 2 / 4: k_vs_miller_group), every boolean checked, with the
+per-kernel times of the last pass.  Usage: python tools/vs_probe.py [--ks 1,2,4] [--steps 6]"""
 import argparse
 import os
 import sys
-import time
 
 import numpy as np
 
@@ -14,47 +13,44 @@ sys.path.insert(0, ROOT)
 import bench  # noqa: E402
 
 
+def run(v, calls, steps, label, k):
+    v.tune("vs_miller_k", k)
+    stages = [v.stage_signature_sets(calls) for _ in range(2)]
+    try:
+        for st in stages:
+            assert st.verify() == [1] * len(calls)
+        dt, ops = bench._timed_ops(v, stages, steps, [1] * len(calls))
+    finally:
+        for st in stages:
+            st.close()
+        v.tune("vs_miller_k", 1)
+    n = sum(len(c) for c in calls)
+    print("%s k=%d: %.3f M sets/s, %.2f ms per pass" % (label, k, n / dt / 1e6, dt * 1e3), flush=True)
+    for name, g, u, ms in ops:
+        print("  %-28s grid %8d units %8d %9.3f ms" % (name, g, u, ms), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--blocks", type=int, default=64)
-    ap.add_argument("--reps", type=int, default=5)
-    ap.add_argument("--electra", action="store_true")
-    ap.add_argument("--inflight", type=str, default="", help="comma list of pass depths for a throughput sweep, e.g. 1,2,3")
+    ap.add_argument("--ks", default="1,2,4")
+    ap.add_argument("--steps", type=int, default=6)
+    ap.add_argument("--calls", type=int, default=512)
     a = ap.parse_args()
     from lodestar_amd import GpuBlsVerifier
     v = GpuBlsVerifier(0)
-    log = lambda m: print("[probe] " + m, file=sys.stderr, flush=True)
-    bench.build_table(v, log)
+    log = lambda m: print("[vs] " + m, file=sys.stderr, flush=True)
+    sks, _ = bench.build_table(v, log)
     sk_ints = [bench.interop_sk_int(i) for i in range(bench.N_KEYS)]
-    rng = np.random.Generator(np.random.PCG64(0xC4E if a.electra else 0xC4))
-    calls = bench.make_blocks(v, sk_ints, a.blocks, rng, electra=a.electra)
-    n = sum(len(c) for c in calls)
-    st = v.stage_signature_sets(calls)
-    assert st.verify() == [1] * a.blocks
-    lat = []
-    for _ in range(a.reps):
-        t = time.perf_counter()
-        assert st.verify() == [1] * a.blocks
-        lat.append((time.perf_counter() - t) * 1e3)
-    ms = v.vs_last_kernel_ms()
-    print("pass of %d blocks, %d sets: median %.3f ms (%s); last pass stage ms %s; %.0f sets/s one pass at a time" % (
-        a.blocks, n, float(np.median(lat)), " ".join("%.2f" % x for x in lat), [round(x, 3) for x in ms], n / (np.median(lat) * 1e-3)))
-    st.close()
-    if a.inflight:
-        lone = []
-        for _ in range(2 + a.reps):
-            t = time.perf_counter()
-            assert v.verify_signature_sets_sync(calls[0]) is True
-            lone.append((time.perf_counter() - t) * 1e3)
-        print("lone block (%d sets): median %.3f ms" % (len(calls[0]), float(np.median(lone[2:]))))
-        for d in [int(x) for x in a.inflight.split(",")]:
-            stages = [v.stage_signature_sets(calls) for _ in range(d)]
-            for b in stages:
-                assert b.verify() == [1] * a.blocks
-            dt = bench._timed_staged(stages, max(6, 3 * d), [1] * a.blocks)
-            for b in stages:
-                b.close()
-            print("%d passes in flight: %.3f ms per pass, %.0f sets/s" % (d, dt * 1e3, n / dt))
+    rng = np.random.Generator(np.random.PCG64(0xC3))
+    c3 = bench._agg_sets(v, sk_ints, a.calls * 128, b"gbv-c3", rng)
+    c3 = [c3[i:i + 128] for i in range(0, len(c3), 128)]
+    c1 = bench._single_sets(v, sks, a.calls * 128, b"gbv-c1-many", rng)
+    c1 = [c1[i:i + 128] for i in range(0, len(c1), 128)]
+    ks = [int(x) for x in a.ks.split(",")]
+    for k in ks:
+        run(v, c3, a.steps, "C3", k)
+    for k in ks:
+        run(v, c1, a.steps, "C1", k)
     v.close_sync()
 
 
