@@ -106,11 +106,6 @@ struct gbv_sm_batch {
   size_t part_stride = 0;
   G1J* rP = nullptr;
   G1J* PgJ = nullptr;
-  // per-set terms r_i pk_i / r_i sig_i (k_sm_prepare, k_sm_redo_g2) and, per failing chunk, its located
-  // invalid set (k_sm_group_check): the failure path's weighted checks read them
-  G1J* Pset = nullptr;
-  G2J* Sset = nullptr;
-  uint32_t* grp_loc = nullptr;
   // failure path lists: runs of failed chunks (head, end, chunk), then sets of failing runs
   uint4* fb_runs = nullptr;
   uint32_t* fb_list = nullptr;
@@ -128,8 +123,6 @@ struct gbv_sm_batch {
 static void sm_free_work(gbv_sm_batch* b) {
   hipFree(b->n_fallback); hipFree(b->status); hipFree(b->grp_state); hipFree(b->valid);
   hipFree(b->H); hipFree(b->S); hipFree(b->SgJ); hipFree(b->rS); hipFree(b->rP); hipFree(b->PgJ);
-  hipFree(b->Pset); hipFree(b->Sset); hipFree(b->grp_loc);
-  b->Pset = nullptr; b->Sset = nullptr; b->grp_loc = nullptr;
   hipHostFree(b->valid_host); hipHostFree(b->nfb_host);
   hipFree(b->F); hipFree(b->Fpair); hipFree(b->pair_ok); hipFree(b->Hpre); hipFree(b->Ffb); hipFree(b->seg_ok); hipHostFree(b->seg_ok_host);
   hipFree(b->Fpart); hipFree(b->Spart); hipFree(b->has);
@@ -174,7 +167,6 @@ static int sm_reserve(gbv_ctx* c, gbv_sm_batch* b, size_t n, size_t G, size_t ca
   chk(dalloc(&b->status, n)); chk(dalloc(&b->grp_state, G)); chk(dalloc(&b->valid, n));
   chk(dalloc(&b->H, calls)); chk(dalloc(&b->Hpre, calls)); chk(dalloc(&b->S, n)); chk(dalloc(&b->rS, n)); chk(dalloc(&b->rP, n));
   chk(dalloc(&b->PgJ, G)); chk(dalloc(&b->SgJ, G)); chk(dalloc(&b->F, G));
-  chk(dalloc(&b->Pset, n)); chk(dalloc(&b->Sset, n)); chk(dalloc(&b->grp_loc, G));
   chk(dalloc(&b->Fpair, 2 * G)); chk(dalloc(&b->pair_ok, 2 * G)); chk(dalloc(&b->Ffb, 2 * FB_COOP_MAX));
   // block partials: one region per segment parity (two segments' reductions can be in flight)
   b->part_stride = seg_reduce_scratch(G);
@@ -766,7 +758,7 @@ static int sm_submit_enqueue(gbv_ctx* c, gbv_sm_batch* b) {
     HIP_CHECK(c, hipEventRecord(e[0], sa));
     launch_sm_prepare(LaunchCfg{0, 64, sa}, s0, s1 - s0, b->idx, b->sig, b->set_grp, c->table, c->table_ok, (uint32_t)c->table_n,
                       c->comb_on ? c->comb : nullptr, c->comb_ok, seed,
-                      nonce, b->S, Sh, b->rP, b->status, b->valid, b->Pset, b->Sset);  // valid: free until the tail's fallback writes it
+                      nonce, b->S, Sh, b->rP, b->status, b->valid);  // valid: free until the tail's fallback writes it
     HIP_CHECK(c, hipEventRecord(e[1], sa));
     // A segment of a few chunks (a lone gossip call) skips the combined check (seg_direct): each
     // chunk goes straight to its own one-wave check, which is the shorter dependency chain.
@@ -811,13 +803,11 @@ static int sm_submit_enqueue(gbv_ctx* c, gbv_sm_batch* b) {
     HIP_CHECK(c, hipEventRecord(e[7], sb));
     HIP_CHECK(c, hipEventRecord(e[8], sb));
     if (msm) {  // per-set / per-chunk G2 sums for the failure path (exit at once when nothing failed)
-      launch_sm_redo_g2(LaunchCfg{0, 64, sb}, s0, s1 - s0, b->set_grp, b->status, b->S, seed, nonce, b->seg_ok + s, b->n_fallback, b->rS,
-                        b->Sset);
+      launch_sm_redo_g2(LaunchCfg{0, 64, sb}, s0, s1 - s0, b->set_grp, b->status, b->S, seed, nonce, b->seg_ok + s, b->n_fallback, b->rS);
       launch_sm_chunk_finish_s(LaunchCfg{0, 64, sb}, g0, G, s0, b->grp_off, b->grp_state, b->rS, b->seg_ok + s, b->SgJ);
     }
     if (G >= GROUP_CHECK_THREAD_MIN)
-      launch_sm_group_check(LaunchCfg{0, 64, sb}, g0, G, b->F, b->SgJ, b->seg_ok + s, b->grp_state, b->n_fallback, b->grp_off, b->grp_msg,
-                            b->H, b->Pset, b->Sset, b->grp_loc);
+      launch_sm_group_check(LaunchCfg{0, 64, sb}, g0, G, b->F, b->SgJ, b->seg_ok + s, b->grp_state, b->n_fallback);
     else
       launch_sm_group_pairing(LaunchCfg{G, 64, sb}, g0, G, b->grp_msg, b->PgJ, b->SgJ, b->H, b->seg_ok + s, b->grp_state, b->n_fallback,
                               b->Fpair, b->pair_ok);
@@ -834,7 +824,7 @@ static int sm_submit_enqueue(gbv_ctx* c, gbv_sm_batch* b) {
   // valid = 1 for the sets of passing chunks; the sets of failed chunks go through 8-set run
   // checks and, for failing runs only, per-set checks (compacted lists, persistent grids)
   launch_sm_fallback(LaunchCfg{blocks_for(b->n), TPB, sf}, (uint32_t)b->n, b->set_grp, b->grp_msg, b->grp_state, b->status, b->idx,
-                     c->table, b->S, b->H, b->valid, b->grp_loc, 0);
+                     c->table, b->S, b->H, b->valid, 0);
   for (size_t s = 0; s < S; ++s) {
     uint32_t s0 = b->grp_off_host[gcut[s]], s1 = b->grp_off_host[gcut[s + 1]];
     launch_sm_fb_runs(LaunchCfg{0, 64, sf}, s0, s1 - s0, b->set_grp, b->grp_state, b->fb_runs, b->fb_cnt, (uint32_t)b->fb_cap);
@@ -843,7 +833,7 @@ static int sm_submit_enqueue(gbv_ctx* c, gbv_sm_batch* b) {
   launch_sm_fb_blocks_coop(LaunchCfg{0, 64, sf}, b->fb_runs, b->fb_cnt, (uint32_t)b->fb_cap, b->status, b->grp_msg, b->rS, b->rP,
                            b->H, b->valid, b->fb_list, b->fb_cnt + 1);
   launch_sm_fb_blocks(LaunchCfg{FB_GRID, 64, sf}, b->fb_runs, b->fb_cnt, (uint32_t)b->fb_cap, b->status, b->grp_msg, b->rS, b->rP, b->H,
-                      b->valid, b->fb_list, b->fb_cnt + 1, b->Pset, b->Sset);
+                      b->valid, b->fb_list, b->fb_cnt + 1);
   launch_sm_fb_sets_coop(LaunchCfg{0, 64, sf}, b->fb_list, b->fb_cnt + 1, b->set_grp, b->grp_msg, b->idx, c->table, b->S, b->H,
                          b->valid, b->Ffb);
   launch_sm_fb_sets(LaunchCfg{FB_GRID, 64, sf}, b->fb_list, b->fb_cnt + 1, b->set_grp, b->grp_msg, b->idx, c->table, b->S, b->H,
@@ -1192,8 +1182,7 @@ bool tuning_set(const char* name, uint32_t v) {
       {"hash_pair_max", &g_tuning.hash_pair_max}, {"hash_quad_max", &g_tuning.hash_quad_max}, {"hash_coop_max", &g_tuning.hash_coop_max},
       {"prepare_split_max", &g_tuning.prepare_split_max}, {"chunk_finish_wave_max", &g_tuning.chunk_finish_wave_max},
       {"vs_pre_max", &g_tuning.vs_pre_max}, {"vs_fs_maxc", &g_tuning.vs_fs_maxc}, {"vs_quad_max", &g_tuning.vs_quad_max},
-      {"vs_pair_max", &g_tuning.vs_pair_max}, {"vs_miller_k", &g_tuning.vs_miller_k}};
-  if (!strcmp(name, "vs_miller_k") && v != 1 && v != 2 && v != 4) return false;
+      {"vs_pair_max", &g_tuning.vs_pair_max}};
   for (auto& t : tab)
     if (!strcmp(name, t.n)) {
       *t.p = v;

@@ -40,9 +40,6 @@ struct gbv_vs_batch {
   uint32_t *set_off = nullptr, *arena = nullptr, *agg_list = nullptr, *chunk_off = nullptr, *siglen = nullptr;
   uint4 *big = nullptr, *slices = nullptr;  // large aggregates: (set, first slice, count), slice (begin, end)
   uint8_t *raw_flag = nullptr, *raw_pk = nullptr, *msgs = nullptr, *sig = nullptr;
-  uint2* grp = nullptr;  // Miller groups (begin, end) of vs_miller_k sets within a chunk, or null
-  size_t ng = 0;
-  uint32_t mk = 1;
   // work
   G1J* pk = nullptr;  // aggregate pubkeys (Jacobian, k_vs_agg / k_vs_agg_big)
   uint8_t* pk_st = nullptr;
@@ -210,13 +207,7 @@ static int vs_fill(gbv_ctx* c, gbv_vs_batch* b, size_t n_calls, const uint32_t* 
   size_t o_so = 0, o_ar = align256(4 * (n + 1)), o_al = o_ar + align256(4 * A), o_co = o_al + align256(4 * n_agg);
   size_t o_sl = o_co + align256(8 * C), o_rf = o_sl + align256(4 * n), o_rp = o_rf + align256(n), o_m = o_rp + align256(48 * n);
   size_t o_sig = o_m + align256(32 * n), o_big = o_sig + align256((size_t)stride * n), o_slc = o_big + align256(16 * n_big);
-  // Miller groups (k_vs_miller_group): up to vs_miller_k consecutive sets of one chunk per thread
-  const uint32_t mk = tuning().vs_miller_k;
-  size_t ng = 0;
-  if (mk > 1 && n > tuning().vs_pair_max)
-    for (size_t k = 0; k < C; ++k) ng += (chunk_end[k] - chunk_off[k] + mk - 1) / mk;
-  size_t o_gr = o_slc + align256(16 * n_slices);
-  size_t total = o_gr + align256(8 * ng);
+  size_t total = o_slc + align256(16 * n_slices);
   if (b->in_cap < total) {
     hipFree(b->in_dev);
     hipHostFree(b->in_host);
@@ -270,12 +261,6 @@ static int vs_fill(gbv_ctx* c, gbv_vs_batch* b, size_t n_calls, const uint32_t* 
     co[2 * k] = chunk_off[k];
     co[2 * k + 1] = chunk_end[k];
   }
-  uint32_t* gr = (uint32_t*)(h + o_gr);
-  for (size_t k = 0, q = 0; ng && k < C; ++k)
-    for (uint32_t i = chunk_off[k]; i < chunk_end[k]; i += mk, ++q) {
-      gr[2 * q] = i;
-      gr[2 * q + 1] = std::min(i + mk, chunk_end[k]);
-    }
   b->set_off = (uint32_t*)(b->in_dev + o_so);
   b->arena = (uint32_t*)(b->in_dev + o_ar);
   b->agg_list = (uint32_t*)(b->in_dev + o_al);
@@ -287,9 +272,6 @@ static int vs_fill(gbv_ctx* c, gbv_vs_batch* b, size_t n_calls, const uint32_t* 
   b->sig = b->in_dev + o_sig;
   b->big = (uint4*)(b->in_dev + o_big);
   b->slices = (uint4*)(b->in_dev + o_slc);
-  b->grp = ng ? (uint2*)(b->in_dev + o_gr) : nullptr;
-  b->ng = ng;
-  b->mk = mk;
   // no host wait: stream A runs the copy ahead of the batch's kernels, other streams wait for the event
   if (!b->copied) HIP_CHECK(c, hipEventCreateWithFlags(&b->copied, hipEventDisableTiming));
   HIP_CHECK(c, hipMemcpyAsync(b->in_dev, h, total, hipMemcpyHostToDevice, c->stream));
@@ -366,7 +348,7 @@ static int vs_enqueue_sets(gbv_ctx* c, gbv_vs_batch* b, hipStream_t m, bool with
   if (b->n <= VS_COOP_MILLER_MAX)  // latency: one wave per set (cooperative Miller loop)
     launch_vs_miller_coop(m, (uint32_t)b->n, b->status, b->rP, b->H, b->F);
   else
-    launch_vs_miller(LaunchCfg{blocks_for(b->n), TPB, m}, (uint32_t)b->n, b->status, b->rP, b->H, b->F, (uint32_t)b->ng, b->grp, b->mk);
+    launch_vs_miller(LaunchCfg{blocks_for(b->n), TPB, m}, (uint32_t)b->n, b->status, b->rP, b->H, b->F);
   HIP_CHECK(c, hipEventRecord(b->ev[4], m));
   if (pre && small) {
     HIP_CHECK(c, hipStreamWaitEvent(m, b->ev[6], 0));

@@ -3,7 +3,6 @@
 
 #include "launch.h"
 #include "kernel_common.h"
-#include "locate.h"
 
 
 namespace gbv {
@@ -38,8 +37,7 @@ __global__ void GBV_KERNEL_ATTR k_sm_prepare(uint32_t base, uint32_t n, const ui
                                              const uint32_t* __restrict__ set_grp, const G1A* __restrict__ table,
                                              const uint8_t* __restrict__ table_ok, uint32_t table_n, const uint4* __restrict__ comb,
                                              const uint8_t* __restrict__ comb_ok, Seed seed, uint32_t nonce, G2A* __restrict__ S_out,
-                                             G2J* __restrict__ Sh_out, G1J* __restrict__ Ph_out, uint8_t* __restrict__ status,
-                                             G1J* __restrict__ Pset, G2J* __restrict__ Sset) {
+                                             G2J* __restrict__ Sh_out, G1J* __restrict__ Ph_out, uint8_t* __restrict__ status) {
   unsigned lane = threadIdx.x;
   uint32_t t = blockIdx.x * 64 + lane;
   bool act = t < n;
@@ -75,9 +73,6 @@ __global__ void GBV_KERNEL_ATTR k_sm_prepare(uint32_t base, uint32_t n, const ui
         if (!randomize_g1(pk, r, &rp)) rp = g1_mul_u64(pk, r);
       }
     }
-    // the per-set terms (infinity for a rejected set), for locating an invalid set of a failing chunk
-    Pset[i] = rp;
-    if (WITH_G2) Sset[i] = rs;
   }
   // segmented suffix scan inside each group of SCAN_W lanes (3 levels: the whole wave pays every
   // level, so fewer levels = less work here; k_sm_chunk_finish adds the group sums of a chunk)
@@ -106,7 +101,7 @@ __global__ void GBV_KERNEL_ATTR k_sm_prepare(uint32_t base, uint32_t n, const ui
 __global__ void GBV_KERNEL_ATTR k_sm_prep_scan(uint32_t base, uint32_t n, const uint32_t* __restrict__ idx,
                                                const uint32_t* __restrict__ set_grp, const uint8_t* __restrict__ table_ok,
                                                uint32_t table_n, const uint8_t* __restrict__ sub_ok, uint8_t* __restrict__ status,
-                                               G2J* __restrict__ Sh, G1J* __restrict__ Ph, G1J* __restrict__ Pset, G2J* __restrict__ Sset) {
+                                               G2J* __restrict__ Sh, G1J* __restrict__ Ph) {
   const unsigned lane = threadIdx.x;
   const uint32_t t = blockIdx.x * 64 + lane;
   const bool act = t < n;
@@ -123,8 +118,6 @@ __global__ void GBV_KERNEL_ATTR k_sm_prep_scan(uint32_t base, uint32_t n, const 
       rs = Sh[i];
       rp = Ph[i];
     }
-    Pset[i] = rp;
-    Sset[i] = rs;
   }
   for (unsigned d = 1; d < SCAN_W; d <<= 1) {
     G1J po = shfl_down_jac(rp, d);
@@ -148,7 +141,7 @@ __global__ void GBV_KERNEL_ATTR k_sm_prep_scan(uint32_t base, uint32_t n, const 
 __global__ void GBV_KERNEL_ATTR k_sm_redo_g2(uint32_t base, uint32_t n, const uint32_t* __restrict__ set_grp,
                                              const uint8_t* __restrict__ status, const G2A* __restrict__ S, Seed seed, uint32_t nonce,
                                              const uint8_t* __restrict__ seg_ok, const uint32_t* __restrict__ n_fallback,
-                                             G2J* __restrict__ Sh_out, G2J* __restrict__ Sset) {
+                                             G2J* __restrict__ Sh_out) {
   // a passing segment still needs the per-set terms when one of its chunks went to the per-set
   // path (malformed / non-subgroup signature): the run checks read Sh (k_sm_fb_blocks*)
   if (*seg_ok && *n_fallback == 0) return;
@@ -163,7 +156,6 @@ __global__ void GBV_KERNEL_ATTR k_sm_redo_g2(uint32_t base, uint32_t n, const ui
     uint64_t r = prf_scalar(seed, i, nonce);
     if (!randomize_g2(s, r, &rs)) rs = g2_mul_u64(s, r);
   }
-  if (act) Sset[i] = rs;
   for (unsigned d = 1; d < SCAN_W; d <<= 1) {
     G2J so = shfl_down_jac(rs, d);
     uint32_t ko = __shfl_down(key, d, 64);
@@ -293,13 +285,13 @@ __global__ void GBV_KERNEL_ATTR k_sm_fallback(uint32_t n, const uint32_t* __rest
                                                     const uint8_t* __restrict__ grp_state, const uint8_t* __restrict__ status,
                                                     const uint32_t* __restrict__ idx, const G1A* __restrict__ table,
                                                     const G2A* __restrict__ S, const G2A* __restrict__ H, uint8_t* __restrict__ valid,
-                                                    const uint32_t* __restrict__ grp_loc, int do_fallback) {
+                                                    int do_fallback) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint32_t g = set_grp[i];
   uint8_t st = grp_state[g];
-  if (st == GRP_OK || st == GRP_LOCATED) {  // the chunk's check held (without its located set)
-    valid[i] = (status[i] == SET_OK && !(st == GRP_LOCATED && grp_loc[g] == i)) ? 1 : 0;
+  if (st == GRP_OK) {  // the chunk's check held for its decodable, in-group sets (k_sm_chunk_finish)
+    valid[i] = status[i] == SET_OK ? 1 : 0;
     return;
   }
   if (!do_fallback) return;
@@ -313,15 +305,12 @@ __global__ void GBV_KERNEL_ATTR k_sm_fallback(uint32_t n, const uint32_t* __rest
 
 // Failure path of a segment with many chunks: one thread per pending chunk.  It reuses the chunk's
 // Miller value F[g] = f(P_g, H(m_g)) from k_sm_miller, adds the (-g1, S_g) pair and runs the final
-// exponentiation: verify(msg, aggPk, aggSig) of the chunk (maybeBatch.ts:34-38); a failing chunk then
-// tries to locate its one invalid set (above: GRP_LOCATED, grp_loc[g]) before the run / per-set
-// checks (GRP_FALLBACK).  Thread-serial checks keep the lanes busy when thousands of chunks are
-// pending; a handful of chunks takes the wave-cooperative k_sm_group_pairing instead.
+// exponentiation: verify(msg, aggPk, aggSig) of the chunk (maybeBatch.ts:34-38).  Thread-serial
+// checks keep the lanes busy when thousands of chunks are pending; a handful of chunks takes the
+// wave-cooperative k_sm_group_pairing instead (lower latency per chunk).
 __global__ void GBV_KERNEL_ATTR k_sm_group_check(uint32_t g0, uint32_t G, const Fp12* __restrict__ F, const G2J* __restrict__ SgJ,
                                                  const uint8_t* __restrict__ seg_ok, uint8_t* __restrict__ grp_state,
-                                                 uint32_t* __restrict__ n_fallback, const uint32_t* __restrict__ grp_off,
-                                                 const uint32_t* __restrict__ grp_msg, const G2A* __restrict__ H,
-                                                 const G1J* __restrict__ Pset, const G2J* __restrict__ Sset, uint32_t* __restrict__ grp_loc) {
+                                                 uint32_t* __restrict__ n_fallback) {
   uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (*seg_ok || g >= G) return;  // launched unconditionally: no host round trip
   g += g0;
@@ -329,23 +318,14 @@ __global__ void GBV_KERNEL_ATTR k_sm_group_check(uint32_t g0, uint32_t G, const 
   G2A sa;
   Fp12 f = F[g];
   if (jac_to_aff(sa, SgJ[g])) f = fp12_mul(f, miller_loop_1(g1_neg_generator(), sa));
-  Fp12 D;
-  final_exponentiation_to(&D, &f);
-  if (fp12_is_one(D)) {
-    grp_state[g] = GRP_OK;
-    return;
-  }
-  atomicAdd(n_fallback, 1u);
-  const uint32_t w = locate_one(grp_off[g], grp_off[g + 1], &D, H[grp_msg[g]], Pset, Sset);
-  if (w != LOC_NONE) grp_loc[g] = w;
-  grp_state[g] = w != LOC_NONE ? GRP_LOCATED : GRP_FALLBACK;
+  bool ok = fp12_is_one(final_exponentiation(f));
+  grp_state[g] = ok ? GRP_OK : GRP_FALLBACK;
+  if (!ok) atomicAdd(n_fallback, 1u);
 }
 
 void launch_sm_group_check(LaunchCfg c, uint32_t g0, uint32_t G, const Fp12* F, const G2J* SgJ, const uint8_t* seg_ok, uint8_t* grp_state,
-                           uint32_t* n_fallback, const uint32_t* grp_off, const uint32_t* grp_msg, const G2A* H, const G1J* Pset,
-                           const G2J* Sset, uint32_t* grp_loc) {
-  GBV_LAUNCH("k_sm_group_check", k_sm_group_check, dim3((G + 63) / 64), dim3(64), c.stream, G, g0, G, F, SgJ, seg_ok, grp_state, n_fallback,
-             grp_off, grp_msg, H, Pset, Sset, grp_loc);
+                           uint32_t* n_fallback) {
+  GBV_LAUNCH("k_sm_group_check", k_sm_group_check, dim3((G + 63) / 64), dim3(64), c.stream, G, g0, G, F, SgJ, seg_ok, grp_state, n_fallback);
 }
 
 // ---- failure path of a chunk: 8-set block checks, then per-set checks ---------------------------
@@ -375,13 +355,11 @@ __global__ void GBV_KERNEL_ATTR k_sm_fb_runs(uint32_t s0, uint32_t n, const uint
   }
 }
 
-// Persistent over the run list: one randomised check per run; a failing run tries to locate its one
-// invalid set (locate_one over the run's sets), and otherwise appends its sets to the per-set list.
+// Persistent over the run list: one randomised check per run; failing runs append their sets.
 __global__ void GBV_KERNEL_ATTR k_sm_fb_blocks(const uint4* __restrict__ runs, const uint32_t* __restrict__ n_runs, uint32_t cap,
                                                const uint8_t* __restrict__ status, const uint32_t* __restrict__ grp_msg,
                                                const G2J* __restrict__ Sh, const G1J* __restrict__ Ph, const G2A* __restrict__ H,
-                                               uint8_t* __restrict__ valid, uint32_t* __restrict__ set_list, uint32_t* __restrict__ n_list,
-                                               const G1J* __restrict__ Pset, const G2J* __restrict__ Sset) {
+                                               uint8_t* __restrict__ valid, uint32_t* __restrict__ set_list, uint32_t* __restrict__ n_list) {
   uint32_t cnt = min(*n_runs, cap);
   if (cnt <= FB_COOP_MAX) return;  // k_sm_fb_blocks_coop has them
   for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < cnt; k += gridDim.x * blockDim.x) {
@@ -389,18 +367,18 @@ __global__ void GBV_KERNEL_ATTR k_sm_fb_blocks(const uint4* __restrict__ runs, c
     bool any = false;
     for (uint32_t i = r.x; i < r.y; ++i) any |= status[i] == SET_OK;
     bool ok = true;
-    uint32_t bad = LOC_NONE;
     if (any) {
-      const G2A Hm = H[grp_msg[r.z]];
-      Fp12 D;
-      ok = pair_value_to(&D, Ph[r.x], Hm, Sh[r.x]) && fp12_is_one(D);
-      if (!ok && !jac_is_inf(Ph[r.x])) bad = locate_one(r.x, r.y, &D, Hm, Pset, Sset);
+      G1A pa;
+      G2A sa;
+      bool p_fin = jac_to_aff(pa, Ph[r.x]);
+      bool s_fin = jac_to_aff(sa, Sh[r.x]);
+      ok = p_fin && pairing_check_2(pa, false, H[grp_msg[r.z]], g1_neg_generator(), !s_fin, sa);
     }
     for (uint32_t i = r.x; i < r.y; ++i) {
       if (status[i] != SET_OK) {
         valid[i] = 0;
-      } else if (ok || bad != LOC_NONE) {
-        valid[i] = i != bad ? 1 : 0;
+      } else if (ok) {
+        valid[i] = 1;
       } else {
         set_list[atomicAdd(n_list, 1u)] = i;
       }
@@ -427,10 +405,9 @@ void launch_sm_fb_runs(LaunchCfg c, uint32_t s0, uint32_t n, const uint32_t* set
   GBV_LAUNCH("k_sm_fb_runs", k_sm_fb_runs, dim3((windows + 63) / 64), dim3(64), c.stream, n, s0, n, set_grp, grp_state, runs, n_runs, cap);
 }
 void launch_sm_fb_blocks(LaunchCfg c, const uint4* runs, const uint32_t* n_runs, uint32_t cap, const uint8_t* status, const uint32_t* grp_msg,
-                         const G2J* Sh, const G1J* Ph, const G2A* H, uint8_t* valid, uint32_t* set_list, uint32_t* n_list, const G1J* Pset,
-                         const G2J* Sset) {
+                         const G2J* Sh, const G1J* Ph, const G2A* H, uint8_t* valid, uint32_t* set_list, uint32_t* n_list) {
   GBV_LAUNCH("k_sm_fb_blocks", k_sm_fb_blocks, dim3(c.blocks), dim3(64), c.stream, 0, runs, n_runs, cap, status, grp_msg, Sh, Ph, H, valid, set_list,
-             n_list, Pset, Sset);
+             n_list);
 }
 void launch_sm_fb_sets(LaunchCfg c, const uint32_t* set_list, const uint32_t* n_list, const uint32_t* set_grp, const uint32_t* grp_msg,
                        const uint32_t* idx, const G1A* table, const G2A* S, const G2A* H, uint8_t* valid) {
@@ -439,8 +416,7 @@ void launch_sm_fb_sets(LaunchCfg c, const uint32_t* set_list, const uint32_t* n_
 
 void launch_sm_prepare(LaunchCfg c, uint32_t base, uint32_t n, const uint32_t* idx, const uint8_t* sig96, const uint32_t* set_grp,
                        const G1A* table, const uint8_t* table_ok, uint32_t table_n, const uint4* comb, const uint8_t* comb_ok,
-                       const Seed& seed, uint32_t nonce, G2A* S_out, G2J* Sh, G1J* Ph, uint8_t* status, uint8_t* scratch8, G1J* Pset,
-                       G2J* Sset) {
+                       const Seed& seed, uint32_t nonce, G2A* S_out, G2J* Sh, G1J* Ph, uint8_t* status, uint8_t* scratch8) {
   // Sh == nullptr: G1 terms only (the segment's G2 sum comes from the bucket MSM); comb == nullptr:
   // no comb tables (gbv_tune "comb" 0, or not built), the ladder forms r pk
   const dim3 grid((n + 63) / 64);
@@ -449,20 +425,18 @@ void launch_sm_prepare(LaunchCfg c, uint32_t base, uint32_t n, const uint32_t* i
     // latency, few sets: the subgroup checks and the randomisation on lane quads side by side, then
     // the verdicts and the scan
     launch_sm_prep_roles_quad(c.stream, base, n, idx, table, table_ok, table_n, comb, comb_ok, seed, nonce, S_out, status, scratch8, Sh, Ph);
-    GBV_LAUNCH("k_sm_prep_scan", k_sm_prep_scan, grid, dim3(64), c.stream, n, base, n, idx, set_grp, table_ok, table_n, scratch8, status, Sh, Ph,
-               Pset, Sset);
+    GBV_LAUNCH("k_sm_prep_scan", k_sm_prep_scan, grid, dim3(64), c.stream, n, base, n, idx, set_grp, table_ok, table_n, scratch8, status, Sh, Ph);
   } else if (Sh) {
     GBV_LAUNCH("k_sm_prepare<true>", k_sm_prepare<true>, grid, dim3(64), c.stream, n, base, n, idx, sig96, set_grp, table, table_ok, table_n,
-               comb, comb_ok, seed, nonce, S_out, Sh, Ph, status, Pset, Sset);
+               comb, comb_ok, seed, nonce, S_out, Sh, Ph, status);
   } else {
     GBV_LAUNCH("k_sm_prepare<false>", k_sm_prepare<false>, grid, dim3(64), c.stream, n, base, n, idx, sig96, set_grp, table, table_ok,
-               table_n, comb, comb_ok, seed, nonce, S_out, Sh, Ph, status, Pset, Sset);
+               table_n, comb, comb_ok, seed, nonce, S_out, Sh, Ph, status);
   }
 }
 void launch_sm_redo_g2(LaunchCfg c, uint32_t base, uint32_t n, const uint32_t* set_grp, const uint8_t* status, const G2A* S, const Seed& seed,
-                       uint32_t nonce, const uint8_t* seg_ok, const uint32_t* n_fallback, G2J* Sh, G2J* Sset) {
-  GBV_LAUNCH("k_sm_redo_g2", k_sm_redo_g2, dim3((n + 63) / 64), dim3(64), c.stream, n, base, n, set_grp, status, S, seed, nonce, seg_ok, n_fallback, Sh,
-             Sset);
+                       uint32_t nonce, const uint8_t* seg_ok, const uint32_t* n_fallback, G2J* Sh) {
+  GBV_LAUNCH("k_sm_redo_g2", k_sm_redo_g2, dim3((n + 63) / 64), dim3(64), c.stream, n, base, n, set_grp, status, S, seed, nonce, seg_ok, n_fallback, Sh);
 }
 void launch_sm_chunk_finish_s(LaunchCfg c, uint32_t g0, uint32_t G, uint32_t s0, const uint32_t* grp_off, const uint8_t* grp_state,
                               const G2J* Sh, const uint8_t* seg_ok, G2J* SgJ) {
@@ -482,8 +456,8 @@ void launch_sm_miller(LaunchCfg c, uint32_t g0, uint32_t G, const uint32_t* grp_
 }
 void launch_sm_fallback(LaunchCfg c, uint32_t n, const uint32_t* set_grp, const uint32_t* grp_msg, const uint8_t* grp_state,
                         const uint8_t* status, const uint32_t* idx, const G1A* table, const G2A* S, const G2A* H, uint8_t* valid,
-                        const uint32_t* grp_loc, int do_fallback) {
+                        int do_fallback) {
   GBV_LAUNCH("k_sm_fallback", k_sm_fallback, dim3(c.blocks), dim3(c.threads), c.stream, n, n, set_grp, grp_msg, grp_state, status, idx, table, S, H,
-             valid, grp_loc, do_fallback);
+             valid, do_fallback);
 }
 }  // namespace gbv

@@ -20,40 +20,6 @@ __global__ void GBV_MILLER_ATTR k_vs_miller(uint32_t n, const uint8_t* __restric
   F[i] = miller_loop_1j(rP[i], H[i]);
 }
 
-// Group form for the largest passes: thread t takes group t of grp (up to K consecutive sets of one
-// chunk, vs_fill) and forms the product of the group's Miller values with one shared accumulator
-// (pairing.h miller_loop_kj_to: one f^2 per bit for the K pairs).  The product goes to F at the
-// group's first decoded set and Fp12 one to its other decoded sets, so every consumer multiplying F
-// over a chunk's (or a shard's) decoded sets reads the same product as with per-set values.
-template <int K>
-__global__ void GBV_MILLER_ATTR k_vs_miller_group(uint32_t ng, const uint2* __restrict__ grp, const uint8_t* __restrict__ status,
-                                                  const G1J* __restrict__ rP, const G2A* __restrict__ H, Fp12* __restrict__ F) {
-  const uint32_t t = blockIdx.x * 64 + threadIdx.x;
-  if (t >= ng) return;
-  const uint2 g = grp[t];
-  uint32_t idx[K];
-  int k = 0;
-  for (uint32_t i = g.x; i < g.y && k < K; ++i)
-    if (status[i] == SET_OK) idx[k++] = i;
-  if (k == 0) return;
-  G1J P[K];
-  G2A Q[K];
-#pragma unroll
-  for (int j = 0; j < K; ++j) {
-    if (j < k) {
-      P[j] = rP[idx[j]];
-      Q[j] = H[idx[j]];
-    }
-  }
-  Fp12 f;
-  miller_loop_kj_to<K>(&f, P, Q, k);
-  F[idx[0]] = f;
-  const Fp12 one = fp12_one();
-#pragma unroll
-  for (int j = 1; j < K; ++j)
-    if (j < k) F[idx[j]] = one;
-}
-
 // The same Miller values on lane pairs (pair.h): set i on lanes 2(i mod 32), 2(i mod 32) + 1 of block
 // i / 32; lane 0 of the pair writes c0 of the conjugated value, lane 1 c1.  Every lane runs the loop
 // (the pair exchanges need both lanes); pairs past n or whose set did not decode write nothing.
@@ -130,20 +96,14 @@ __global__ void GBV_MILLER_QUAD_ATTR k_vs_miller_quad(uint32_t n, const uint8_t*
   out[2] = fp_sel(L.s, M.c2.c1, M.c1.c0);
 }
 
-void launch_vs_miller(LaunchCfg c, uint32_t n, const uint8_t* status, const G1J* rP, const G2A* H, Fp12* F, uint32_t ng, const uint2* grp,
-                      uint32_t k) {
+void launch_vs_miller(LaunchCfg c, uint32_t n, const uint8_t* status, const G1J* rP, const G2A* H, Fp12* F) {
   if (n == 0) return;
   // Lane quads for passes of up to vs_quad_max sets (range-sync segments, shards: the pass has fewer
   // waves than SIMDs, and four lanes per set quarter each set's latency's product count), lane pairs
   // up to vs_pair_max, one thread per set above (C3-sized passes, measured equal or better:
-  // profiles/r03e), or one thread per group of k sets when vs_fill built a group table.
+  // profiles/r03e; groups of 2 / 4 sets on one accumulator per thread measured slower: profiles/r05d).
   const Tuning& t = tuning();
-  if (n > t.vs_pair_max && grp && ng) {
-    if (k == 4)
-      GBV_LAUNCH("k_vs_miller_group<4>", k_vs_miller_group<4>, dim3((ng + 63) / 64), dim3(64), c.stream, n, ng, grp, status, rP, H, F);
-    else
-      GBV_LAUNCH("k_vs_miller_group<2>", k_vs_miller_group<2>, dim3((ng + 63) / 64), dim3(64), c.stream, n, ng, grp, status, rP, H, F);
-  } else if (n > t.vs_pair_max) {
+  if (n > t.vs_pair_max) {
     GBV_LAUNCH("k_vs_miller", k_vs_miller, dim3((n + 63) / 64), dim3(64), c.stream, n, n, status, rP, H, F);
   } else if (n > t.vs_quad_max) {
     GBV_LAUNCH("k_vs_miller_pair", k_vs_miller_pair, dim3((n + 31) / 32), dim3(64), c.stream, n, n, status, rP, H, F);

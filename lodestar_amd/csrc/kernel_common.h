@@ -53,9 +53,7 @@ namespace gbv {
 struct Seed { uint32_t w[8]; };
 
 enum : uint8_t { SET_OK = 0, SET_BAD_SIG = 1, SET_BAD_PK = 2 };
-// GRP_LOCATED: the chunk failed, and its one invalid set (grp_loc[g]) was located with every other
-// set proven valid (k_sm_group_check, below); GRP_FALLBACK: run / per-set checks decide.
-enum : uint8_t { GRP_PENDING = 0, GRP_FALLBACK = 1, GRP_OK = 2, GRP_LOCATED = 3 };
+enum : uint8_t { GRP_PENDING = 0, GRP_FALLBACK = 1, GRP_OK = 2 };
 // Failure-path item counts up to which one wave per item (k_sm_fb_*_coop, latency) beats one
 // thread per item (k_sm_fb_blocks / k_sm_fb_sets, throughput).
 constexpr uint32_t FB_COOP_MAX = 256;
@@ -80,7 +78,6 @@ struct Tuning {
   uint32_t vs_fs_maxc = 256;               // per-chunk (-g1, sum) Miller value beside the per-set ones
   uint32_t vs_quad_max = 16384;            // per-set Miller values on lane quads up to this many sets
   uint32_t vs_pair_max = 32768;            // ... on lane pairs up to this many (one lane per set above)
-  uint32_t vs_miller_k = 1;                // above vs_pair_max: sets per thread sharing one accumulator (1, 2, 4)
   uint32_t sync_debug = 0;                 // GBV_SYNC_DEBUG: synchronise + report after every launch (debugging)
 };
 const Tuning& tuning();

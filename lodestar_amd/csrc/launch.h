@@ -23,8 +23,7 @@ void launch_vs_sig_decode(hipStream_t s, uint32_t n, const uint8_t* sig, uint32_
                           uint8_t* dec_st);
 void launch_sm_prepare(LaunchCfg c, uint32_t base, uint32_t n, const uint32_t* idx, const uint8_t* sig96, const uint32_t* set_grp,
                        const G1A* table, const uint8_t* table_ok, uint32_t table_n, const uint4* comb, const uint8_t* comb_ok,
-                       const Seed& seed, uint32_t nonce, G2A* S_out, G2J* Sh, G1J* Ph, uint8_t* status, uint8_t* scratch8, G1J* Pset,
-                       G2J* Sset);
+                       const Seed& seed, uint32_t nonce, G2A* S_out, G2J* Sh, G1J* Ph, uint8_t* status, uint8_t* scratch8);
 // few sets (k_sm_coop.hip): cooperative subgroup checks (one wave per set, verdict in sub_ok) beside
 // the per-set randomisation (r sig / r pk into Sh / Ph at the set's index), after k_sig_decode
 void launch_sm_prep_roles_quad(hipStream_t s, uint32_t base, uint32_t n, const uint32_t* idx, const G1A* table, const uint8_t* table_ok,
@@ -40,7 +39,7 @@ void launch_sm_seg_check(LaunchCfg c, uint32_t g0, uint32_t G, uint8_t* grp_stat
                          uint8_t* has, uint8_t* seg_ok, Fp12* miller_out = nullptr, const G2J* S_extra = nullptr);
 // runs when the segment check failed or any chunk went to the per-set path (n_fallback > 0)
 void launch_sm_redo_g2(LaunchCfg c, uint32_t base, uint32_t n, const uint32_t* set_grp, const uint8_t* status, const G2A* S, const Seed& seed,
-                       uint32_t nonce, const uint8_t* seg_ok, const uint32_t* n_fallback, G2J* Sh, G2J* Sset);
+                       uint32_t nonce, const uint8_t* seg_ok, const uint32_t* n_fallback, G2J* Sh);
 void launch_sm_chunk_finish_s(LaunchCfg c, uint32_t g0, uint32_t G, uint32_t s0, const uint32_t* grp_off, const uint8_t* grp_state,
                               const G2J* Sh, const uint8_t* seg_ok, G2J* SgJ);
 // Bucket MSM of a same-message segment: total = sum over its sets with status OK in pending chunks
@@ -65,18 +64,15 @@ void launch_sm_group_pairing(LaunchCfg c, uint32_t g0, uint32_t G, const uint32_
                              const uint8_t* seg_ok, uint8_t* grp_state, uint32_t* n_fallback, Fp12* Fpair, uint8_t* pair_ok);
 void launch_sm_fallback(LaunchCfg c, uint32_t n, const uint32_t* set_grp, const uint32_t* grp_msg, const uint8_t* grp_state,
                         const uint8_t* status, const uint32_t* idx, const G1A* table, const G2A* S, const G2A* H, uint8_t* valid,
-                        const uint32_t* grp_loc, int do_fallback);
+                        int do_fallback);
 
-// thread per pending chunk of a failed segment: the chunk's check, and for a failing chunk the
-// location of its one invalid set (GRP_LOCATED, grp_loc) from the per-set terms Pset / Sset
+// thread per pending chunk of a failed segment: the chunk's own check
 void launch_sm_group_check(LaunchCfg c, uint32_t g0, uint32_t G, const Fp12* F, const G2J* SgJ, const uint8_t* seg_ok, uint8_t* grp_state,
-                           uint32_t* n_fallback, const uint32_t* grp_off, const uint32_t* grp_msg, const G2A* H, const G1J* Pset,
-                           const G2J* Sset, uint32_t* grp_loc);
+                           uint32_t* n_fallback);
 void launch_sm_fb_runs(LaunchCfg c, uint32_t s0, uint32_t n, const uint32_t* set_grp, const uint8_t* grp_state, uint4* runs, uint32_t* n_runs,
                        uint32_t cap);
 void launch_sm_fb_blocks(LaunchCfg c, const uint4* runs, const uint32_t* n_runs, uint32_t cap, const uint8_t* status, const uint32_t* grp_msg,
-                         const G2J* Sh, const G1J* Ph, const G2A* H, uint8_t* valid, uint32_t* set_list, uint32_t* n_list, const G1J* Pset,
-                         const G2J* Sset);
+                         const G2J* Sh, const G1J* Ph, const G2A* H, uint8_t* valid, uint32_t* set_list, uint32_t* n_list);
 void launch_sm_fb_sets(LaunchCfg c, const uint32_t* set_list, const uint32_t* n_list, const uint32_t* set_grp, const uint32_t* grp_msg,
                        const uint32_t* idx, const G1A* table, const G2A* S, const G2A* H, uint8_t* valid);
 
@@ -122,8 +118,7 @@ void launch_vs_pk_rand(hipStream_t s, uint32_t n, const uint32_t* set_off, const
 void launch_vs_miller_coop(hipStream_t s, uint32_t n, const uint8_t* status, const G1J* rP, const G2A* H, Fp12* F);
 void launch_vs_chunk_s_miller(hipStream_t s, uint32_t C, const uint8_t* status, const uint32_t* chunk_be, const G2J* rS, Fp12* Fs,
                               uint8_t* fs_flag);
-void launch_vs_miller(LaunchCfg c, uint32_t n, const uint8_t* status, const G1J* rP, const G2A* H, Fp12* F, uint32_t ng = 0,
-                      const uint2* grp = nullptr, uint32_t k = 1);
+void launch_vs_miller(LaunchCfg c, uint32_t n, const uint8_t* status, const G1J* rP, const G2A* H, Fp12* F);
 void launch_sig_validate(LaunchCfg c, uint32_t n, const uint8_t* sig, uint32_t sig_len, uint8_t* status, uint8_t* out96);
 void launch_sig_aggregate(hipStream_t s, uint32_t n, const uint8_t* sig, uint32_t sig_len, int validate, G2J* part, uint32_t* bad,
                           uint8_t* out96);

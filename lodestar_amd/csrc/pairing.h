@@ -125,49 +125,6 @@ GBV_NI void miller_loop_1j_to(Fp12* out, G1J P, G2A Q0) {
   fp12_conj_to(out, &f);
 }
 
-// prod_{j<k} f_{|x|, Q_j}(P_j) over k <= K pairs (P_j Jacobian) with one shared accumulator: one
-// Fp12 squaring per bit for all k pairs (a third of one pair's per-bit products is that squaring:
-// 36 of ~109 FME), then each pair's doubling / addition line.  The product equals the product of the
-// k single-pair values (same lines, same Z^3 factors), so a chunk check multiplying Miller values
-// sees the same Fp12.
-template <int K>
-GBV_NI void miller_loop_kj_to(Fp12* out, const G1J* P, const G2A* Q, int k) {
-  Fp z3[K], nxz[K];
-  G2Proj T[K];
-#pragma unroll
-  for (int j = 0; j < K; ++j) {
-    if (j < k) {
-      z3[j] = fp_mul(fp_sqr(P[j].z), P[j].z);
-      nxz[j] = fp_neg(fp_mul(P[j].x, P[j].z));
-      T[j] = G2Proj{Q[j].x, Q[j].y, fp2_one()};
-    }
-  }
-  Fp12 f = fp12_one();
-  Line l;
-  for (int i = 62; i >= 0; --i) {
-    if (i != 62) fp12_sqr_to(&f, &f);
-#pragma unroll
-    for (int j = 0; j < K; ++j) {
-      if (j < k) {
-        l = dbl_step(T[j], nxz[j], P[j].y);
-        l.c0 = fp2_mul_fp(l.c0, z3[j]);
-        fp12_mul_line_to(&f, &l);
-      }
-    }
-    if ((X_ABS >> i) & 1ull) {
-#pragma unroll
-      for (int j = 0; j < K; ++j) {
-        if (j < k) {
-          l = add_step(T[j], Q[j], nxz[j], P[j].y);
-          l.c0 = fp2_mul_fp(l.c0, z3[j]);
-          fp12_mul_line_to(&f, &l);
-        }
-      }
-    }
-  }
-  fp12_conj_to(out, &f);
-}
-
 GBV_HD Fp12 miller_loop_2(const G1A& P0, bool inf0, const G2A& Q0, const G1A& P1, bool inf1, const G2A& Q1) {
   Fp12 r;
   miller_loop_2_to(&r, P0, inf0, Q0, P1, inf1, Q1);

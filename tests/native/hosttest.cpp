@@ -6,7 +6,7 @@
 #include "../../lodestar_amd/csrc/hash_to_curve.h"
 #include "../../lodestar_amd/csrc/coop.h"
 #include "../../lodestar_amd/csrc/ssz.h"
-#include "../../lodestar_amd/csrc/locate.h"
+#include "locate_proto.h"
 #include <vector>
 
 using namespace gbv;
@@ -375,9 +375,56 @@ unsigned long long ht_count_miller_1j(const uint8_t* p96, const uint8_t* q192) {
   (void)miller_loop_1j(P, Q);
   return g_fme_count;
 }
-// k_vs_miller_group's shared-accumulator loop against the product of per-pair Miller values: P_j =
-// 2 (p_j) (Jacobian, Z != 1), Q_j affine; mode 0 = product of miller_loop_1j, 1 = miller_loop_kj_to<4>,
-// 2 = miller_loop_kj_to<2> (k <= 2).  out = the Fp12 (12 canonical Fp, tower order); returns the FME count.
+// Measured and not adopted: a shared-accumulator Miller loop for k pairs,
+// as a thread-per-group kernel (k_vs_miller_group) it cut the per-set Fp products (7256 -> 6134 /
+// 5573 for k = 2 / 4) but ran slower on the device (fewer threads, a frame-resident state).  Kept
+// here as the counted prototype.
+// prod_{j<k} f_{|x|, Q_j}(P_j) over k <= K pairs (P_j Jacobian) with one shared accumulator: one
+// Fp12 squaring per bit for all k pairs (a third of one pair's per-bit products is that squaring:
+// 36 of ~109 FME), then each pair's doubling / addition line.  The product equals the product of the
+// k single-pair values (same lines, same Z^3 factors), so a chunk check multiplying Miller values
+// sees the same Fp12.
+static void miller_loop_kj_to(Fp12* out, const G1J* P, const G2A* Q, int k) {
+  constexpr int K = 4;
+  Fp z3[K], nxz[K];
+  G2Proj T[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    if (j < k) {
+      z3[j] = fp_mul(fp_sqr(P[j].z), P[j].z);
+      nxz[j] = fp_neg(fp_mul(P[j].x, P[j].z));
+      T[j] = G2Proj{Q[j].x, Q[j].y, fp2_one()};
+    }
+  }
+  Fp12 f = fp12_one();
+  Line l;
+  for (int i = 62; i >= 0; --i) {
+    if (i != 62) fp12_sqr_to(&f, &f);
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      if (j < k) {
+        l = dbl_step(T[j], nxz[j], P[j].y);
+        l.c0 = fp2_mul_fp(l.c0, z3[j]);
+        fp12_mul_line_to(&f, &l);
+      }
+    }
+    if ((X_ABS >> i) & 1ull) {
+#pragma unroll
+      for (int j = 0; j < K; ++j) {
+        if (j < k) {
+          l = add_step(T[j], Q[j], nxz[j], P[j].y);
+          l.c0 = fp2_mul_fp(l.c0, z3[j]);
+          fp12_mul_line_to(&f, &l);
+        }
+      }
+    }
+  }
+  fp12_conj_to(out, &f);
+}
+
+// The shared-accumulator loop against the product of per-pair Miller values: P_j =
+// 2 (p_j) (Jacobian, Z != 1), Q_j affine; mode 0 = product of miller_loop_1j, 1 and 2 = miller_loop_kj_to
+// (k <= 4).  out = the Fp12 (12 canonical Fp, tower order); returns the FME count.
 unsigned long long ht_miller_group(uint8_t* out, const uint8_t* p96, const uint8_t* q192, int k, int mode) {
   G1J P[4];
   G2A Q[4];
@@ -394,9 +441,9 @@ unsigned long long ht_miller_group(uint8_t* out, const uint8_t* p96, const uint8
       f = fp12_mul(f, g);
     }
   } else if (mode == 1) {
-    miller_loop_kj_to<4>(&f, P, Q, k);
+    miller_loop_kj_to(&f, P, Q, k);
   } else {
-    miller_loop_kj_to<2>(&f, P, Q, k);
+    miller_loop_kj_to(&f, P, Q, k);
   }
   const Fp2* c[6] = {&f.c0.c0, &f.c0.c1, &f.c0.c2, &f.c1.c0, &f.c1.c1, &f.c1.c2};
   for (int i = 0; i < 6; ++i) store_fp2(out + 96 * i, *c[i]);

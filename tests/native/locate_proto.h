@@ -1,8 +1,11 @@
-// Locating the one invalid set of a failing chunk / run of the same-message path from the per-set
-// randomised terms (k_sm.hip k_sm_group_check, k_sm_fb_blocks); host-tested against the oracle
-// (tests/native/hosttest.cpp ht_locate, tests/test_host_arith.py::test_locate_one_invalid_set).
+// Prototype (test-only): locating the one invalid set of a failing chunk / run of the same-message
+// path from the per-set randomised terms.  Round 5 ran it inside the thread-serial failure-path
+// kernels (k_sm_group_check, k_sm_fb_blocks) and measured C5 at 3.3 M sets/s against 6.15 M without
+// it (profiles/r05e/c5.txt: one long chain per failing chunk on ~100 waves), so the product path
+// does not use it; kept with its host test (tests/native/hosttest.cpp ht_locate,
+// tests/test_host_arith.py::test_locate_one_invalid_set) as the algorithm a cooperative form would run.
 #pragma once
-#include "pairing.h"
+#include "../../lodestar_amd/csrc/pairing.h"
 
 namespace gbv {
 

@@ -108,27 +108,3 @@ def test_c3_large_pass_thread_forms(c3):
     bad[319][127] = AggregatedSignatureSet(s.indices, s.signing_root, bytes([10]) * 96)
     assert v.verify_signature_sets_multi_sync(bad) == [c not in (250, 319) for c in range(320)]
 
-
-@pytest.mark.parametrize("k", [2, 4])
-def test_c3_large_pass_miller_groups(c3, k):
-    """The same 40 960-set pass with the per-set Miller values formed k to a thread on one shared
-    accumulator (k_vs_miller_group: one f^2 per bit for k sets of one chunk), with ragged calls (a
-    call of 127 sets, one of 3, one of 1: groups shorter than k at chunk ends) and a bad set inside a
-    group: the booleans equal the thread-per-set form's."""
-    from lodestar_amd import AggregatedSignatureSet
-    v, sets, _ = c3
-    calls = [list(sets[i:i + PER_CALL]) for i in range(0, N_SETS, PER_CALL)] * 4
-    calls[5] = calls[5][:127]
-    calls[6] = calls[6][:3]
-    calls[7] = calls[7][:1]
-    s = calls[100][2]  # committee one member short, the third set of a group
-    calls[100][2] = AggregatedSignatureSet(list(s.indices)[:-1], s.signing_root, s.signature)
-    s = calls[200][5]  # malformed signature: a set that does not decode inside a group
-    calls[200][5] = AggregatedSignatureSet(s.indices, s.signing_root, bytes([10]) * 96)
-    want = [c not in (100, 200) for c in range(320)]
-    v.tune("vs_miller_k", k)
-    try:
-        assert sum(len(c) for c in calls) > 32768
-        assert v.verify_signature_sets_multi_sync(calls) == want
-    finally:
-        v.tune("vs_miller_k", 1)

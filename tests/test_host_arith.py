@@ -375,9 +375,10 @@ def test_coop_clear_cofactor(lib):
 
 @pytest.mark.parametrize("k,mode", [(4, 1), (3, 1), (1, 1), (2, 2), (1, 2)])
 def test_miller_group_shared_accumulator(lib, k, mode):
-    """k_vs_miller_group's loop (pairing.h miller_loop_kj_to): one accumulator for k pairs with one
-    f^2 per bit gives exactly the product of the per-pair Miller values (P Jacobian with Z != 1),
-    for fewer Fp products than the k separate loops plus their product."""
+    """The shared-accumulator Miller loop (tests/native/hosttest.cpp miller_loop_kj_to, the prototype of
+    round 5's k_vs_miller_group, measured slower on the device and removed: DESIGN.md 7): one
+    accumulator for k pairs with one f^2 per bit gives exactly the product of the per-pair Miller
+    values (P Jacobian with Z != 1), for fewer Fp products than the k separate loops."""
     import sys
     sys.path.insert(0, os.path.join(HERE, ".."))
     import bench
@@ -401,7 +402,8 @@ def test_miller_group_shared_accumulator(lib, k, mode):
 
 @pytest.mark.parametrize("case", ["valid", "one_bad_first", "one_bad_mid", "one_bad_last", "two_bad", "cancelling"])
 def test_locate_one_invalid_set(lib, case):
-    """The same-message failure path's locate (locate.h: k_sm_group_check, k_sm_fb_blocks): for a chunk
+    """The locate prototype (tests/native/locate_proto.h; measured slower in the thread-serial failure
+    path and not in the product): for a chunk
     whose randomised check fails, the position-weighted check + discrete log <= n + the candidate's own
     check name the ONE invalid set; two invalid sets (also a crafted pair whose errors cancel in an
     unrandomised sum) are never "located" -- they go to the run / per-set checks.  Sets and signatures
