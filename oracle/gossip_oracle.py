@@ -22,6 +22,15 @@ ContributionAndProof {uint64, SyncCommitteeContribution, Bytes96}, SyncAggregato
 {uint64, uint64} (types/src/{phase0,altair,electra}/sszTypes.ts).  BitList roots: the packed bits
 merkleized to ceil(limit / 256) chunks, then the length mixed in; BitVector roots: the packed bits.
 Domains through oracle/block_oracle.py's getDomain / getDomainAtFork restatement.
+
+PARITY UNPINNED for the container roots: the phase0 / electra AggregateAndProof roots and the
+SyncCommitteeContribution / ContributionAndProof roots are restated here the same way as in
+lodestar_amd/gossip_sets.py and addon/gossip_sets.js, and no vector held by the reference fixes them
+(its validation tests build these containers at run time and sign them with its own BLS; nothing in
+/root/reference records a root).  tests/golden/gossip_sets.json is therefore self-consistent under
+this restatement, not pinned; K1 pins the merkleization primitives (uint64, Bytes48, container
+padding) and the domains / fork selection match selectionProof.ts, aggregateAndProof.ts and
+attestation.ts:657-665.
 """
 from oracle import block_oracle as BO
 from oracle import ssz_oracle as S

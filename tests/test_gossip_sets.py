@@ -8,9 +8,11 @@ CPU: the fixture is self-consistent under the oracle; the product builders repro
 validator indices, signing root) with a hashlib stand-in for the device hasher.  GPU: the same with
 the device computing every container root and signing root, and each call -- and each one-set
 corruption of it -- verified through GpuBlsVerifier with exactly the oracle's answer.
-Parity note: K1 pins the merkleization rules (uint64 / Bytes48 / container padding); the BitList
-length mix-in and BitVector packing are restated from the SSZ spec @chainsafe/ssz 0.11.1 implements
-(unpinned by a reference-held vector: none exists offline)."""
+Parity note -- PARITY UNPINNED for the container roots (phase0 / electra AggregateAndProof,
+SyncCommitteeContribution, ContributionAndProof): no reference-held vector records one, so the fixture
+is self-consistent under oracle/gossip_oracle.py's restatement, not pinned.  K1 pins the merkleization
+rules (uint64 / Bytes48 / container padding); the BitList length mix-in and BitVector packing are
+restated from the SSZ spec @chainsafe/ssz 0.11.1 implements."""
 import asyncio
 
 import pytest
