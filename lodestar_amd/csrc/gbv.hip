@@ -806,9 +806,7 @@ static int sm_submit_enqueue(gbv_ctx* c, gbv_sm_batch* b) {
       launch_sm_redo_g2(LaunchCfg{0, 64, sb}, s0, s1 - s0, b->set_grp, b->status, b->S, seed, nonce, b->seg_ok + s, b->n_fallback, b->rS);
       launch_sm_chunk_finish_s(LaunchCfg{0, 64, sb}, g0, G, s0, b->grp_off, b->grp_state, b->rS, b->seg_ok + s, b->SgJ);
     }
-    if (G >= GROUP_CHECK_THREAD_MIN && tuning().group_coop)
-      launch_sm_group_check_coop(LaunchCfg{0, 64, sb}, g0, G, b->F, b->SgJ, b->seg_ok + s, b->grp_state, b->n_fallback);
-    else if (G >= GROUP_CHECK_THREAD_MIN)
+    if (G >= GROUP_CHECK_THREAD_MIN)
       launch_sm_group_check(LaunchCfg{0, 64, sb}, g0, G, b->F, b->SgJ, b->seg_ok + s, b->grp_state, b->n_fallback);
     else
       launch_sm_group_pairing(LaunchCfg{G, 64, sb}, g0, G, b->grp_msg, b->PgJ, b->SgJ, b->H, b->seg_ok + s, b->grp_state, b->n_fallback,
@@ -1184,7 +1182,7 @@ bool tuning_set(const char* name, uint32_t v) {
       {"hash_pair_max", &g_tuning.hash_pair_max}, {"hash_quad_max", &g_tuning.hash_quad_max}, {"hash_coop_max", &g_tuning.hash_coop_max},
       {"prepare_split_max", &g_tuning.prepare_split_max}, {"chunk_finish_wave_max", &g_tuning.chunk_finish_wave_max},
       {"vs_pre_max", &g_tuning.vs_pre_max}, {"vs_fs_maxc", &g_tuning.vs_fs_maxc}, {"vs_quad_max", &g_tuning.vs_quad_max},
-      {"vs_pair_max", &g_tuning.vs_pair_max}, {"group_coop", &g_tuning.group_coop}};
+      {"vs_pair_max", &g_tuning.vs_pair_max}};
   for (auto& t : tab)
     if (!strcmp(name, t.n)) {
       *t.p = v;

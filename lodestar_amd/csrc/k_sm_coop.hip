@@ -132,44 +132,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
   }
 }
 
-// The same check for a segment with many pending chunks, one wave each, reusing the chunk's Miller
-// value F[g] from k_sm_miller (k_sm_group_check's check on the cooperative steps): the (-g1, S_g)
-// Miller value, times F[g], one final exponentiation.
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
-k_sm_group_check_coop(uint32_t g0, const Fp12* __restrict__ F, const G2J* __restrict__ SgJ, const uint8_t* __restrict__ seg_ok,
-                      uint8_t* __restrict__ grp_state, uint32_t* __restrict__ n_fallback) {
-  __shared__ coop::Slot ws[SEG_WS];
-  __shared__ Fp st[4];
-  __shared__ int sa_ok;
-  const uint32_t g = g0 + blockIdx.x;
-  if (*seg_ok || grp_state[g] != GRP_PENDING) return;  // launched unconditionally: no host round trip
-  const unsigned lane = threadIdx.x;
-  coop::load_consts();
-  if (lane == 0) {
-    G2A sa;
-    sa_ok = jac_to_aff(sa, SgJ[g]) ? 1 : 0;
-    st[0] = sa.x.c0;
-    st[1] = sa.x.c1;
-    st[2] = sa.y.c0;
-    st[3] = sa.y.c1;
-  }
-  coop::barrier();
-  if (sa_ok) {
-    coop::miller_load_pair(ws, 0, g1_neg_generator(), G2A{Fp2{st[0], st[1]}, Fp2{st[2], st[3]}});
-    coop::miller_loop(ws, 1);
-  } else {
-    coop::set_one12(ws + coop::E_F);
-  }
-  if (lane < 12) coop::put(ws + coop::E_TMP + lane, ((const Fp*)&F[g])[lane]);
-  coop::barrier();
-  coop::mul12(ws, coop::E_Z, coop::E_F, coop::E_TMP, coop::E_F);
-  const bool ok = coop::final_exp_is_one(ws);
-  if (lane == 0) {
-    grp_state[g] = ok ? GRP_OK : GRP_FALLBACK;
-    if (!ok) atomicAdd(n_fallback, 1u);
-  }
-}
-
 // The same check with its two Miller loops on two waves (latency: a lone gossip call ends here).
 // Block (g, j) forms the Miller value of pair j of chunk g -- j = 0: (P_g, H(m_g)), j = 1:
 // (-g1, S_g) -- so the chain is one Miller loop (Fp12 square + one line per bit) instead of the
@@ -470,10 +432,6 @@ void launch_sm_seg_check(LaunchCfg c, uint32_t g0, uint32_t G, uint8_t* grp_stat
   uint32_t nb = 0;
   const uint32_t off = launch_seg_reduce_quad(c.stream, g0, G, grp_state, F, SgJ, Fpart, Spart, has, &nb);
   GBV_LAUNCH("k_sm_seg_check", k_sm_seg_check, dim3(1), dim3(64), c.stream, G, g0, G, nb, Fpart + off, Spart + off, has + off, grp_state, seg_ok, miller_out, S_extra);
-}
-void launch_sm_group_check_coop(LaunchCfg c, uint32_t g0, uint32_t G, const Fp12* F, const G2J* SgJ, const uint8_t* seg_ok, uint8_t* grp_state,
-                                uint32_t* n_fallback) {
-  GBV_LAUNCH("k_sm_group_check_coop", k_sm_group_check_coop, dim3(G), dim3(64), c.stream, G, g0, F, SgJ, seg_ok, grp_state, n_fallback);
 }
 void launch_sm_group_pairing(LaunchCfg c, uint32_t g0, uint32_t G, const uint32_t* grp_msg, const G1J* PgJ, const G2J* SgJ, const G2A* H,
                              const uint8_t* seg_ok, uint8_t* grp_state, uint32_t* n_fallback, Fp12* Fpair, uint8_t* pair_ok) {

@@ -78,7 +78,6 @@ struct Tuning {
   uint32_t vs_fs_maxc = 256;               // per-chunk (-g1, sum) Miller value beside the per-set ones
   uint32_t vs_quad_max = 16384;            // per-set Miller values on lane quads up to this many sets
   uint32_t vs_pair_max = 32768;            // ... on lane pairs up to this many (one lane per set above)
-  uint32_t group_coop = 0;                 // failing segments of many chunks: chunk checks one wave each (1) or one thread each (0)
   uint32_t sync_debug = 0;                 // GBV_SYNC_DEBUG: synchronise + report after every launch (debugging)
 };
 const Tuning& tuning();

@@ -69,9 +69,6 @@ void launch_sm_fallback(LaunchCfg c, uint32_t n, const uint32_t* set_grp, const 
 // thread per pending chunk of a failed segment: the chunk's own check
 void launch_sm_group_check(LaunchCfg c, uint32_t g0, uint32_t G, const Fp12* F, const G2J* SgJ, const uint8_t* seg_ok, uint8_t* grp_state,
                            uint32_t* n_fallback);
-// the same check one wave per pending chunk (k_sm_coop.hip), F[g] reused
-void launch_sm_group_check_coop(LaunchCfg c, uint32_t g0, uint32_t G, const Fp12* F, const G2J* SgJ, const uint8_t* seg_ok, uint8_t* grp_state,
-                                uint32_t* n_fallback);
 void launch_sm_fb_runs(LaunchCfg c, uint32_t s0, uint32_t n, const uint32_t* set_grp, const uint8_t* grp_state, uint4* runs, uint32_t* n_runs,
                        uint32_t cap);
 void launch_sm_fb_blocks(LaunchCfg c, const uint4* runs, const uint32_t* n_runs, uint32_t cap, const uint8_t* status, const uint32_t* grp_msg,

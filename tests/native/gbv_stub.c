@@ -32,7 +32,6 @@ struct gbv_sm_batch {
   uint8_t* valid;
   double ready;
   int in_flight;
-  int part_flying;
 };
 
 struct gbv_vs_batch {
@@ -40,6 +39,7 @@ struct gbv_vs_batch {
   uint8_t* call_valid;
   double ready;
   int in_flight;
+  int part_flying;
 };
 
 static __thread char t_err[128];

@@ -1,9 +1,11 @@
-// Prototype (test-only): locating the one invalid set of a failing chunk / run of the same-message
-// path from the per-set randomised terms.  Round 5 ran it inside the thread-serial failure-path
-// kernels (k_sm_group_check, k_sm_fb_blocks) and measured C5 at 3.3 M sets/s against 6.15 M without
-// it (profiles/r05e/c5.txt: one long chain per failing chunk on ~100 waves), so the product path
-// does not use it; kept with its host test (tests/native/hosttest.cpp ht_locate,
-// tests/test_host_arith.py::test_locate_one_invalid_set) as the algorithm a cooperative form would run.
+// Prototype (test-only): locating the one invalid set of a failing same-message chunk from the
+// per-set randomised terms, host-tested against the oracle (tests/native/hosttest.cpp ht_locate,
+// tests/test_host_arith.py::test_locate_one_invalid_set).  Round 5 ran it on the GPU in three forms,
+// all slower than the run / per-set checks it shortcuts (C5 6.3 M sets/s without it): inside the
+// thread-per-chunk group check (3.3 M: half of each wave's lanes idle behind one ~50 k-product chain),
+// as one wave per chunk on the cooperative steps (5.2 M: the engine's per-product overhead on a
+// saturated device), and as compacted thread-per-chunk phases (5.4 M: ~6.5 k chains of ~30 k products
+// cannot fill 1 024 SIMDs, where the ~65 k run checks do).  DESIGN.md 7.
 #pragma once
 #include "../../lodestar_amd/csrc/pairing.h"
 

@@ -168,20 +168,15 @@ def test_same_message_injected_invalid(world, segments):
     assert res == expected
 
 
-@pytest.mark.parametrize("mode", ["ladder", "msm", "coop_groups"])
+@pytest.mark.parametrize("mode", ["ladder", "msm"])
 def test_same_message_one_percent_invalid(world, mode):
     """C5-style density: 1 % of 60 000 sets invalid, so hundreds of chunks fail.  The
     failure path then runs its thread-per-item kernels (group checks, 8-set run checks, per-set
     checks: more than FB_COOP_MAX items each) and must still return exactly the per-set booleans.
-    In MSM mode the failing segment first recomputes its per-set G2 terms (k_sm_redo_g2);
-    coop_groups: the chunk checks one wave each (k_sm_group_check_coop, gbv_tune group_coop)."""
+    In MSM mode the failing segment first recomputes its per-set G2 terms (k_sm_redo_g2)."""
     v, sks, _ = world
     _tune(v, 1, 1000 if mode == "msm" else 0, 0)
-    v.tune("group_coop", 1 if mode == "coop_groups" else 0)
-    try:
-        _one_percent(v, sks)
-    finally:
-        v.tune("group_coop", 0)
+    _one_percent(v, sks)
 
 
 def _one_percent(v, sks):
