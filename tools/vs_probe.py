@@ -1,5 +1,5 @@
 """verifySignatureSets probe: the C3 pass (512 calls of 128-member aggregates) and the C1 throughput
-pass (512 calls of 128 single sets), 2 passes in flight, every boolean checked, with the per-kernel
+pass (512 calls of 128 single sets), 2 (or --depths) passes in flight, every boolean checked, with the per-kernel
 times of the last pass; optional launch-shape settings (gbv_tune) per run.
 Usage: python tools/vs_probe.py [--tune name=value ...] [--steps 6]"""
 import argparse
@@ -13,8 +13,8 @@ sys.path.insert(0, ROOT)
 import bench  # noqa: E402
 
 
-def run(v, calls, steps, label):
-    stages = [v.stage_signature_sets(calls) for _ in range(2)]
+def run(v, calls, steps, label, depth):
+    stages = [v.stage_signature_sets(calls) for _ in range(depth)]
     try:
         for st in stages:
             assert st.verify() == [1] * len(calls)
@@ -23,7 +23,7 @@ def run(v, calls, steps, label):
         for st in stages:
             st.close()
     n = sum(len(c) for c in calls)
-    print("%s: %.3f M sets/s, %.2f ms per pass" % (label, n / dt / 1e6, dt * 1e3), flush=True)
+    print("%s (%d in flight): %.3f M sets/s, %.2f ms per pass" % (label, depth, n / dt / 1e6, dt * 1e3), flush=True)
     for name, g, u, ms in ops:
         print("  %-28s grid %8d units %8d %9.3f ms" % (name, g, u, ms), flush=True)
 
@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--tune", action="append", default=[], metavar="NAME=VALUE")
     ap.add_argument("--steps", type=int, default=6)
     ap.add_argument("--calls", type=int, default=512)
+    ap.add_argument("--depths", default="2", help="passes in flight, comma-separated")
     a = ap.parse_args()
     from lodestar_amd import GpuBlsVerifier
     v = GpuBlsVerifier(0)
@@ -47,8 +48,9 @@ def main():
     for t in a.tune:
         name, value = t.split("=")
         v.tune(name, int(value))
-    run(v, c3, a.steps, "C3")
-    run(v, c1, a.steps, "C1")
+    for d in [int(x) for x in a.depths.split(",")]:
+        run(v, c3, a.steps, "C3", d)
+        run(v, c1, a.steps, "C1", d)
     v.close_sync()
 
 
