@@ -1182,7 +1182,7 @@ bool tuning_set(const char* name, uint32_t v) {
       {"hash_pair_max", &g_tuning.hash_pair_max}, {"hash_quad_max", &g_tuning.hash_quad_max}, {"hash_coop_max", &g_tuning.hash_coop_max},
       {"prepare_split_max", &g_tuning.prepare_split_max}, {"chunk_finish_wave_max", &g_tuning.chunk_finish_wave_max},
       {"vs_pre_max", &g_tuning.vs_pre_max}, {"vs_fs_maxc", &g_tuning.vs_fs_maxc}, {"vs_quad_max", &g_tuning.vs_quad_max},
-      {"vs_pair_max", &g_tuning.vs_pair_max}};
+      {"vs_pair_max", &g_tuning.vs_pair_max}, {"agg_slice", &g_tuning.agg_slice}};
   for (auto& t : tab)
     if (!strcmp(name, t.n)) {
       *t.p = v;

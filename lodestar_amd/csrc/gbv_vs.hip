@@ -143,6 +143,7 @@ static int vs_fill(gbv_ctx* c, gbv_vs_batch* b, size_t n_calls, const uint32_t* 
   if (b->copied) HIP_CHECK(c, hipEventSynchronize(b->copied));  // the pinned blob is free again
   size_t n = n_calls ? call_off[n_calls] : 0;
   if (call_off && call_off[0] != 0) return gbv_fail(c, GBV_E_ARG, "call offsets must start at 0");
+  const uint32_t slice = std::max<uint32_t>(tuning().agg_slice, 256);  // members per k_vs_agg_big workgroup
   for (size_t g = 0; g < n_calls; ++g)
     if (call_off[g + 1] < call_off[g]) return gbv_fail(c, GBV_E_ARG, "call offsets not monotone");
   if (n && !sets) return gbv_fail(c, GBV_E_ARG, "null sets");
@@ -166,7 +167,7 @@ static int vs_fill(gbv_ctx* c, gbv_vs_batch* b, size_t n_calls, const uint32_t* 
       A += s.idx_len;
       if (s.idx_len >= AGG_BIG_MIN) {
         ++n_big;
-        n_slices += (s.idx_len + AGG_SLICE_MEMBERS - 1) / AGG_SLICE_MEMBERS;
+        n_slices += (s.idx_len + slice - 1) / slice;
       } else if (s.idx_len >= 2) {
         ++n_agg;
       }
@@ -237,10 +238,10 @@ static int vs_fill(gbv_ctx* c, gbv_vs_batch* b, size_t n_calls, const uint32_t* 
     } else if (s.idx_len) {
       memcpy(ar + a, arena + s.idx_off, 4 * (size_t)s.idx_len);
       if (s.idx_len >= AGG_BIG_MIN) {
-        const uint32_t k = (s.idx_len + AGG_SLICE_MEMBERS - 1) / AGG_SLICE_MEMBERS;
+        const uint32_t k = (s.idx_len + slice - 1) / slice;
         bg[nb++] = make_uint4((uint32_t)i, (uint32_t)ns, k, 0);
         for (uint32_t q = 0; q < k; ++q)
-          slc[ns++] = make_uint4((uint32_t)a + q * AGG_SLICE_MEMBERS, (uint32_t)a + std::min(s.idx_len, (q + 1) * AGG_SLICE_MEMBERS), 0, 0);
+          slc[ns++] = make_uint4((uint32_t)a + q * slice, (uint32_t)a + std::min(s.idx_len, (q + 1) * slice), 0, 0);
       } else if (s.idx_len >= 2) {
         al[na++] = (uint32_t)i;
       }

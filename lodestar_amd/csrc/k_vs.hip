@@ -65,7 +65,7 @@ k_vs_agg(uint32_t n_agg, const uint32_t* __restrict__ agg_list, const uint32_t* 
 
 // aggregatePublicKeys of LARGE sets (electra attestations: committee_bits name up to 64 committees,
 // so one aggregate holds thousands to tens of thousands of validators; epochCache.ts:953-973) by
-// slices of AGG_SLICE_MEMBERS members (launch.h): one 256-thread workgroup per slice.  Thread t reads index words
+// slices of tuning().agg_slice members (vs_fill): one 256-thread workgroup per slice.  Thread t reads index words
 // begin + t, begin + t + 256, ... (consecutive threads, consecutive words: coalesced) and gathers the
 // 128-byte table records; each thread sums its few records with mixed additions, a 6-level shuffle
 // tree sums each wave and the 4 wave sums meet in LDS.  part[w] is the slice's Jacobian sum,

@@ -78,6 +78,7 @@ struct Tuning {
   uint32_t vs_fs_maxc = 256;               // per-chunk (-g1, sum) Miller value beside the per-set ones
   uint32_t vs_quad_max = 16384;            // per-set Miller values on lane quads up to this many sets
   uint32_t vs_pair_max = 32768;            // ... on lane pairs up to this many (one lane per set above)
+  uint32_t agg_slice = 8192;               // large aggregates: members per k_vs_agg_big workgroup (256 threads; profiles/r05l)
   uint32_t sync_debug = 0;                 // GBV_SYNC_DEBUG: synchronise + report after every launch (debugging)
 };
 const Tuning& tuning();

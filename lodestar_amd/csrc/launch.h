@@ -101,7 +101,7 @@ void launch_vs_agg(LaunchCfg c, const uint32_t* agg_list, const uint32_t* set_of
                    const uint8_t* table_ok, G1J* pk_out, uint8_t* pk_st);
 // large aggregate sets (>= AGG_BIG_MIN members): slices (begin, end) of AGG_SLICE members, one
 // 256-thread workgroup each, then one wave per set over its slices; big = (set, first slice, count)
-constexpr uint32_t AGG_BIG_MIN = 1024, AGG_SLICE_MEMBERS = 2048;
+constexpr uint32_t AGG_BIG_MIN = 1024;  // slice size: tuning().agg_slice
 void launch_vs_agg_big(hipStream_t s, uint32_t n_slices, const uint4* slices, uint32_t n_big, const uint4* big, const uint32_t* arena,
                        const G1A* table, const uint8_t* table_ok, G1J* part, uint8_t* part_bad, G1J* pk_out, uint8_t* pk_st);
 void launch_vs_hash_sig(hipStream_t s, uint32_t n, const uint8_t* msgs32, const uint32_t* set_off, const uint32_t* arena,

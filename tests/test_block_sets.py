@@ -235,12 +235,13 @@ def test_gpu_electra_block_and_corruptions_one_pass(gpu):
 
 @pytest.mark.gpu
 def test_gpu_mixed_aggregate_sizes(gpu):
-    """Sets of 1, 2, 127, 512, 1023 (small kernel) and 1024, 2048, 2049, 5000 (sliced kernel)
-    members in one pass, each signed by the sum of its members' keys; then one member swapped."""
+    """Sets of 1, 2, 127, 512, 1023 (small kernel) and 1024, 2048, 2049, 5000, 8192, 8193, 20000
+    (sliced kernel: one slice up to agg_slice = 8192 members, then several) members in one pass,
+    each signed by the sum of its members' keys; then one member swapped."""
     from lodestar_amd import AggregatedSignatureSet, SingleSignatureSet
     import numpy as np
     rng = np.random.Generator(np.random.PCG64(0xA66))
-    sizes = [1, 2, 127, 512, 1023, 1024, 2048, 2049, 5000]
+    sizes = [1, 2, 127, 512, 1023, 1024, 2048, 2049, 5000, 8192, 8193, 20000]
     sks = [int.from_bytes(_sk(i), "big") for i in range(C.N_KEYS)]
     msgs = [hashlib.sha256(b"agg-size" + bytes([k])).digest() for k in range(len(sizes))]
     members = [rng.choice(C.N_VALIDATORS, size=n, replace=False).tolist() for n in sizes]
