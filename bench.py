@@ -55,7 +55,6 @@ FME_RANDOMIZE_G1 = 593      # r_i pk_i (endomorphism-split 32-step ladder + affi
 FME_COMB_G1 = 126           # r_i pk_i from the validator's comb table (7 doublings + 7 mixed additions)
 FME_RANDOMIZE_PAIR = 2086   # r_i pk_i and r_i sig_i with one shared inversion
 FME_RANDOMIZE_PAIR_JAC = 2096  # the same with P Jacobian (aggregate pubkeys straight from k_vs_agg)
-FME_RANDOMIZE_G1_JAC = 603  # r_i pk_i alone with P Jacobian (k_vs_hash_sig in an MSM pass: r_i sig_i from the bucket MSM)
 FME_HASH_TO_G2 = 4808       # RFC 9380 hash_to_G2 (SSWU with one norm exponentiation per map + 3-isogeny + h_eff + to affine)
 FME_MILLER_1J = 7244        # Miller value of one pair, Jacobian P
 # k_vs_miller_group: k pairs on one accumulator (one f^2 per bit): the first pair 7256 (P with Z != 1,
@@ -79,7 +78,6 @@ W_PREPARE_FME_MSM_COMB = FME_SIG_VALIDATE + FME_COMB_G1 + FME_G1_SCAN
 W_PREPARE_FME = FME_SIG_VALIDATE + FME_RANDOMIZE_PAIR + 177
 # k_vs_hash_sig: both block roles per set
 W_VS_HASH_SIG = FME_HASH_TO_G2 + FME_SIG_VALIDATE + FME_RANDOMIZE_PAIR_JAC
-W_VS_HASH_SIG_MSM = FME_HASH_TO_G2 + FME_SIG_VALIDATE + FME_RANDOMIZE_G1_JAC
 # Integer VALU peak: v_mad_u64_u32 measured at 37.0 T lane-ops/s on MI355X
 # (tools/ubench_int.hip, profiles/r01_ubench_int.txt); theoretical 256 CU x 4 SIMD x 16 lanes x 2.4 GHz = 39.3 T.
 PEAK_MAC_PER_S = 37.0e12
@@ -348,7 +346,7 @@ def vs_op_work(name, units, ps):
     table = {
         "k_vs_agg": (ps["members_small"] * FME_G1_MADD, ps["members_small"] * AGG_BYTES_PER_MEMBER),
         "k_vs_agg_big": (ps["members_big"] * FME_G1_MADD, ps["members_big"] * AGG_BYTES_PER_MEMBER),
-        "k_vs_hash_sig": (units * (W_VS_HASH_SIG_MSM if ps.get("msm") else W_VS_HASH_SIG), units * VS_ALG_BYTES["hash_sig"]),
+        "k_vs_hash_sig": (units * W_VS_HASH_SIG, units * VS_ALG_BYTES["hash_sig"]),
         "k_hash_msgs": (units * FME_HASH_TO_G2, units * (32 + 256)),
         "k_hash_msgs_pair": (units * FME_HASH_TO_G2, units * (32 + 256)),
         "k_hash_msgs_quad": (units * FME_HASH_TO_G2, units * (32 + 256)),
@@ -375,8 +373,7 @@ def _vs_roofline(v, n_sets, ops, members_small=0, members_big=0, n_chunks=0):
     describes the kernel that took longest among those whose algorithmic work is known (summed over
     its launches in the pass); `kernels` lists every launch with its fraction of the VALU peak.  PMC
     counters are attached only from a profiled launch of that kernel at the same grid."""
-    ps = {"n_sets": n_sets, "n_chunks": n_chunks or max(1, -(-n_sets // 128)), "members_small": members_small, "members_big": members_big,
-          "msm": any(o[0] == "k_msm_runs" for o in ops)}  # an MSM pass: hash_sig forms r_i pk_i only
+    ps = {"n_sets": n_sets, "n_chunks": n_chunks or max(1, -(-n_sets // 128)), "members_small": members_small, "members_big": members_big}
     agg = {}
     for name, threads, units, ms in ops:
         e = agg.setdefault(name, {"ms": 0.0, "launches": 0, "grid": threads, "units": units, "grids": []})

@@ -142,14 +142,11 @@ struct gbv_ctx {
   // A failing MSM segment pays the per-set G2 terms after all (k_sm_redo_g2) on top of the MSM, so
   // after one the next MSM_COOLDOWN submits use the per-set ladders (invalid-dense streams, C5)
   uint32_t msm_cooldown = 0;
-  // Settings (gbv_tune): segments of at least msm_min sets form their G2 sum with the bucket MSM
-  // (k_msm.hip; 0 = never); a failing MSM segment starts a cooldown of msm_cooldown_len submits; a
-  // batch is cut into at most `segments` pipeline segments (tests use several on small batches)
+  // Settings read once at gbv_init (GBV_MSM_MIN, GBV_MSM_COOLDOWN, GBV_SEGMENTS), changed only by
+  // gbv_tune: segments of at least msm_min sets form their G2 sum with the bucket MSM (k_msm.hip;
+  // 0 = never); a failing MSM segment starts a cooldown of msm_cooldown_len submits; a batch is cut
+  // into at most `segments` pipeline segments (tests use several on small batches)
   uint32_t msm_min = 131072, msm_cooldown_len = 16, segments = 1;
-  // verifySignatureSets passes of at least vs_msm_min sets (0 = never) check all their chunks at once
-  // against ONE bucket MSM of sum r_i sig_i (the per-set G2 ladders skipped); a failing pass pays the
-  // ladders and the per-chunk checks after all and starts a cooldown of msm_cooldown_len submits
-  uint32_t vs_msm_min = 0, vs_msm_cooldown = 0;
   static constexpr int NK = 8;  // hash, prepare, chunk_reduce, miller, seg_check, group_pairing, fallback, msm
   float last_ms[NK] = {};
   int last_launches[NK] = {};

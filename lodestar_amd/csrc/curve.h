@@ -490,22 +490,6 @@ template <class F> GBV_HD bool randomize_one(const Aff<F>& P, const Aff<F>& E, u
   return true;
 }
 GBV_NI bool randomize_g1(G1A P, uint64_t r64, G1J* rP) { return randomize_one<Fp>(P, g1_phi(P), r64, rP); }
-// randomize_g1 with P Jacobian (an aggregate pubkey): P +- phi(P) as two full additions, the two
-// tables normalised by one inversion of their z1 z2 -- randomize_pair_jac's G1 half alone, for passes
-// whose G2 sum comes from the bucket MSM (k_msm.hip) instead of per-set r_i sig_i.
-GBV_NI bool randomize_g1_jac(G1J P, uint64_t r64, G1J* rP) {
-  const G1J ph{fp_mul(P.x, FP_BETA), P.y, P.z};
-  const G1J a1 = jac_add(P, ph);
-  const G1J a2 = jac_add(P, jac_neg(ph));
-  const Fp z = fp_mul(a1.z, a2.z);
-  if (fp_is_zero(z)) return false;
-  const Fp inv = fp_inv(z);
-  RegTab2<G1A> t;
-  t.store(0, aff_from_jac_inv(a1, fp_mul(a2.z, inv)));
-  t.store(1, aff_from_jac_inv(a2, fp_mul(a1.z, inv)));
-  *rP = jac_mul_2d_signed_tab<Fp>(t, (uint32_t)r64, (uint32_t)(r64 >> 32));
-  return true;
-}
 GBV_NI bool randomize_g2(G2A Q, uint64_t r64, G2J* rQ) { return randomize_one<Fp2>(Q, g2_neg_psi2(Q), r64, rQ); }
 
 // ---- per-validator comb tables for r pk (the same-message path's G1 term) ---------------------

@@ -271,7 +271,6 @@ int gbv_tune(gbv_ctx* c, const char* name, uint32_t value) {
   GBV_LOCK(c);
   if (!strcmp(name, "msm_min")) c->msm_min = value;
   else if (!strcmp(name, "msm_cooldown")) c->msm_cooldown_len = value;
-  else if (!strcmp(name, "vs_msm_min")) c->vs_msm_min = value;
   else if (!strcmp(name, "segments")) c->segments = std::max<uint32_t>(value, 1);
   else if (!strcmp(name, "kprof")) c->kprof_on = value != 0;
   else if (!strcmp(name, "comb")) c->comb_on = value != 0 && (c->comb_on || c->table_n == 0);  // off at any time; on before ingest only

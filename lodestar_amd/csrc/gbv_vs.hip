@@ -71,16 +71,6 @@ struct gbv_vs_batch {
   hipEvent_t done = nullptr;
   hipEvent_t copied = nullptr;  // the last fill's input copy (stream A); see gbv_sm_batch::copied
   hipEvent_t pre = nullptr;     // "pre" mode: k_vs_sig_pre_quad done (stream 5)
-  // MSM pass (ctx vs_msm_min): the bucket MSM's buffers (k_msm.hip), a zero set->group map and group
-  // state (every set in one pending "group"), the combined check's reduction scratch and verdict
-  uint32_t *msm_cnt = nullptr, *msm_off = nullptr, *msm_cur = nullptr, *msm_ent = nullptr, *msm_zero = nullptr;
-  G2J *msm_buckets = nullptr, *msm_part = nullptr, *msm_head = nullptr, *msm_tail = nullptr, *msm_total = nullptr;
-  Fp12* pass_Fpart = nullptr;
-  G2J* pass_Spart = nullptr;
-  uint8_t *pass_has = nullptr, *msm_grp = nullptr, *pass_ok = nullptr, *pass_ok_host = nullptr;
-  size_t msm_cap = 0;
-  hipEvent_t msm_ev = nullptr;
-  bool used_msm = false;  // the last submit ran as an MSM pass
   bool in_flight = false;
   bool part_in_flight = false;  // gbv_vs_batch_partial_submit'ed, not yet waited
   int tail = 0;
@@ -96,44 +86,6 @@ static void vs_free_work(gbv_vs_batch* b) {
   b->allocated = false;
 }
 
-static void vs_msm_free(gbv_vs_batch* b) {
-  (void)hipFree(b->msm_cnt); (void)hipFree(b->msm_off); (void)hipFree(b->msm_cur); (void)hipFree(b->msm_ent); (void)hipFree(b->msm_zero);
-  (void)hipFree(b->msm_buckets); (void)hipFree(b->msm_part); (void)hipFree(b->msm_head); (void)hipFree(b->msm_tail); (void)hipFree(b->msm_total);
-  (void)hipFree(b->pass_Fpart); (void)hipFree(b->pass_Spart); (void)hipFree(b->pass_has); (void)hipFree(b->msm_grp); (void)hipFree(b->pass_ok);
-  (void)hipHostFree(b->pass_ok_host);
-  b->msm_cnt = b->msm_off = b->msm_cur = b->msm_ent = b->msm_zero = nullptr;
-  b->msm_buckets = b->msm_part = b->msm_head = b->msm_tail = b->msm_total = nullptr;
-  b->pass_Fpart = nullptr; b->pass_Spart = nullptr; b->pass_has = b->msm_grp = b->pass_ok = b->pass_ok_host = nullptr;
-  b->msm_cap = 0;
-}
-
-// MSM buffers for passes of up to n sets (filled once: the all-zero set->group map and group state)
-static int vs_msm_reserve(gbv_ctx* c, gbv_vs_batch* b, size_t n) {
-  if (b->msm_cap >= n) return GBV_OK;
-  vs_msm_free(b);
-  hipError_t e = hipSuccess;
-  auto chk = [&](hipError_t x) { if (x != hipSuccess && e == hipSuccess) e = x; };
-  chk(dalloc(&b->msm_cnt, MSM_KEYS)); chk(dalloc(&b->msm_off, MSM_KEYS)); chk(dalloc(&b->msm_cur, MSM_KEYS));
-  chk(dalloc(&b->msm_ent, 4 * n)); chk(dalloc(&b->msm_zero, n)); chk(dalloc(&b->msm_buckets, MSM_KEYS));
-  chk(dalloc(&b->msm_part, MSM_PARTS + 130)); chk(dalloc(&b->msm_head, 4 * n / MSM_RUN + 64)); chk(dalloc(&b->msm_tail, 4 * n / MSM_RUN + 64));
-  chk(dalloc(&b->msm_total, 1));
-  const size_t np = seg_reduce_scratch(n);
-  chk(dalloc(&b->pass_Fpart, np)); chk(dalloc(&b->pass_Spart, np)); chk(dalloc(&b->pass_has, np));
-  chk(dalloc(&b->msm_grp, 1)); chk(dalloc(&b->pass_ok, 1));
-  chk(hipHostMalloc((void**)&b->pass_ok_host, 1, hipHostMallocDefault));
-  if (e == hipSuccess) {
-    chk(hipMemset(b->msm_zero, 0, 4 * n));
-    chk(hipMemset(b->msm_grp, 0, 1));  // GRP_PENDING
-  }
-  if (!b->msm_ev) chk(hipEventCreateWithFlags(&b->msm_ev, hipEventDisableTiming));
-  if (e != hipSuccess) {
-    vs_msm_free(b);
-    return gbv_fail(c, GBV_E_OOM, std::string("hipMalloc (MSM pass): ") + hipGetErrorString(e));
-  }
-  b->msm_cap = n;
-  return GBV_OK;
-}
-
 void vs_batch_free(gbv_vs_batch* b) {
   if (!b) return;
   if ((b->in_flight || b->part_in_flight) && b->done) (void)hipEventSynchronize(b->done);
@@ -142,8 +94,6 @@ void vs_batch_free(gbv_vs_batch* b) {
     (void)hipEventDestroy(b->copied);
   }
   vs_free_work(b);
-  vs_msm_free(b);
-  if (b->msm_ev) hipEventDestroy(b->msm_ev);
   b->prof.destroy();
   hipFree(b->in_dev);
   hipHostFree(b->in_host);
@@ -240,7 +190,6 @@ static int vs_fill(gbv_ctx* c, gbv_vs_batch* b, size_t n_calls, const uint32_t* 
   HIP_CHECK(c, hipSetDevice(c->device));
   int rc = vs_reserve(c, b, n, C);
   if (rc) return rc;
-  if (c->vs_msm_min && n >= c->vs_msm_min && (rc = vs_msm_reserve(c, b, n))) return rc;
   if (b->agg_part_cap < n_slices) {
     // grow geometrically (each larger Electra aggregate would otherwise free + allocate, and a
     // hipFree synchronises the device under the passes in flight)
@@ -357,7 +306,7 @@ static bool vs_fs_small(const gbv_vs_batch* b) { return b->n <= VS_COOP_MILLER_M
 // with_fs: the chunk checks follow (gbv_vs_batch_submit), so a small pass also forms each chunk's
 // (-g1, sum r_i sig_i) Miller value beside the per-set ones.  partial: a shard's Fp12 partial follows
 // (gbv_vs_partial); it takes the same split of the signature half (pre mode) and the hash on stream m.
-static int vs_enqueue_sets(gbv_ctx* c, gbv_vs_batch* b, hipStream_t m, bool with_fs, bool partial = false, bool msm = false) {
+static int vs_enqueue_sets(gbv_ctx* c, gbv_vs_batch* b, hipStream_t m, bool with_fs, bool partial = false) {
   hipStream_t s = c->stream;
   Seed seed = fresh_seed();
   uint32_t nonce = c->nonce++;
@@ -392,14 +341,9 @@ static int vs_enqueue_sets(gbv_ctx* c, gbv_vs_batch* b, hipStream_t m, bool with
                       b->rP, b->status);
   } else {
     launch_vs_hash_sig(s, (uint32_t)b->n, b->msgs, b->set_off, b->arena, b->raw_flag, b->raw_pk, b->sig, b->sig_stride, b->siglen, c->table,
-                       c->table_ok, b->pk, b->pk_st, seed, nonce, b->H, b->rP, b->rS, b->status, split, msm ? b->Sd : nullptr);
+                       c->table_ok, b->pk, b->pk_st, seed, nonce, b->H, b->rP, b->rS, b->status, split);
   }
   HIP_CHECK(c, hipEventRecord(b->ev[2], s));
-  if (msm) {  // the pass's sum r_i sig_i: the bucket pass on stream A behind hash_sig (k_msm.hip)
-    launch_msm_g2_buckets(s, 0, (uint32_t)b->n, b->msm_zero, b->status, b->msm_grp, b->Sd, seed, nonce, b->msm_cnt, b->msm_off, b->msm_cur,
-                          b->msm_ent, b->msm_buckets, b->msm_head, b->msm_tail);
-    HIP_CHECK(c, hipEventRecord(b->msm_ev, s));
-  }
   if (m != s) HIP_CHECK(c, hipStreamWaitEvent(m, b->ev[2], 0));
   HIP_CHECK(c, hipEventRecord(b->ev[3], m));
   if (b->n <= VS_COOP_MILLER_MAX)  // latency: one wave per set (cooperative Miller loop)
@@ -407,14 +351,6 @@ static int vs_enqueue_sets(gbv_ctx* c, gbv_vs_batch* b, hipStream_t m, bool with
   else
     launch_vs_miller(LaunchCfg{blocks_for(b->n), TPB, m}, (uint32_t)b->n, b->status, b->rP, b->H, b->F);
   HIP_CHECK(c, hipEventRecord(b->ev[4], m));
-  if (msm) {
-    // one combined check over every decoded set: prod F_i * f(-g1, MSM sum), one final exponentiation;
-    // when it fails, the per-set r_i sig_i after all (k_vs_redo_g2) for the per-chunk checks
-    if (m != s) HIP_CHECK(c, hipStreamWaitEvent(m, b->msm_ev, 0));
-    launch_msm_g2_reduce(m, b->msm_buckets, b->msm_part, b->msm_total);
-    launch_vs_pass_check(m, (uint32_t)b->n, b->status, b->F, b->pass_Fpart, b->pass_Spart, b->pass_has, b->pass_ok, b->msm_total);
-    launch_vs_redo_g2(m, (uint32_t)b->n, b->status, b->Sd, seed, nonce, b->pass_ok, b->rS);
-  }
   if (pre && small) {
     HIP_CHECK(c, hipStreamWaitEvent(m, b->ev[6], 0));
   } else if (small) {  // beside the per-set Miller values, on stream A (free after hash_sig)
@@ -464,19 +400,13 @@ static int vs_submit_enqueue(gbv_ctx* c, gbv_vs_batch* b) {
   KProfScope kp(c->kprof_on ? &b->prof : nullptr);
   b->tail = (int)(c->sm_submits++ & 1);
   hipStream_t t = b->tail ? c->stream4 : c->stream2;
-  const bool fs = vs_fs_small(b);
-  // MSM pass: a large pass (thread forms, no precomputed chunk pairs), buffers reserved at fill, and
-  // no failing MSM pass within the last msm_cooldown_len submits (invalid-dense streams)
-  const bool msm = c->vs_msm_min && b->n >= c->vs_msm_min && b->msm_cap >= b->n && !fs && !vs_pre_on(b) && c->vs_msm_cooldown == 0;
-  if (c->vs_msm_cooldown) --c->vs_msm_cooldown;
-  b->used_msm = msm;
-  int rc = vs_enqueue_sets(c, b, t, true, false, msm);
+  int rc = vs_enqueue_sets(c, b, t, true);
   if (rc) return rc;
+  const bool fs = vs_fs_small(b);
   launch_vs_chunk_coop(LaunchCfg{(unsigned)b->C, 64, t}, (uint32_t)b->C, b->chunk_off, b->status, b->F, b->rS, b->chunk_valid,
-                       fs ? b->Fs : nullptr, b->fs_flag, msm ? b->pass_ok : nullptr);
+                       fs ? b->Fs : nullptr, b->fs_flag);
   HIP_CHECK(c, hipEventRecord(b->ev[5], t));
   HIP_CHECK(c, hipMemcpyAsync(b->chunk_valid_host, b->chunk_valid, b->C, hipMemcpyDeviceToHost, t));
-  if (msm) HIP_CHECK(c, hipMemcpyAsync(b->pass_ok_host, b->pass_ok, 1, hipMemcpyDeviceToHost, t));
   HIP_CHECK(c, hipEventRecord(b->done, t));
   HIP_CHECK(c, hipGetLastError());
   return GBV_OK;
@@ -519,7 +449,6 @@ int gbv_vs_batch_wait(gbv_ctx* c, gbv_vs_batch* b, uint8_t* call_valid) {
     for (int k = 0; k < 4; ++k)
       if (hipEventElapsedTime(&ms[k], b->ev[from[k]], b->ev[from[k] + 1]) != hipSuccess) ms[k] = 0.f;
     memcpy(c->last_vs_ms, ms, sizeof ms);
-    if (b->used_msm && !b->pass_ok_host[0]) c->vs_msm_cooldown = c->msm_cooldown_len;  // a failing MSM pass: ladders for a while
     if (!b->prof.recs.empty()) {
       c->last_ops[1] = kprof_format(b->prof);
       b->prof.reset();

@@ -359,7 +359,7 @@ void launch_sm_fb_sets_coop(LaunchCfg c, const uint32_t* set_list, const uint32_
 // product latencies against ~180).  has_out[b] = 0 when the block holds no active item.
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
 k_seg_reduce_quad(uint32_t n, const uint8_t* __restrict__ act, uint8_t act_val, const Fp12* __restrict__ Fin, const G2J* __restrict__ Sin,
-                  Fp12* __restrict__ Fout, G2J* __restrict__ Sout, uint8_t* __restrict__ has_out, uint32_t with_s) {
+                  Fp12* __restrict__ Fout, G2J* __restrict__ Sout, uint8_t* __restrict__ has_out) {
   GBV_TAIL_WAVE_PRIO();
   const unsigned lane = threadIdx.x;
   quad::Lane L;
@@ -374,12 +374,13 @@ k_seg_reduce_quad(uint32_t n, const uint8_t* __restrict__ act, uint8_t act_val, 
     const uint32_t k = blockIdx.x * 64 + j + 16 * m;
     if (k >= n || act[k] != act_val) continue;
     const Fp6 G = ((const Fp6*)&Fin[k])[hf];
+    const G2J P = Sin[k];
     if (has) {
       quad::mul12(M, G, L);
-      if (with_s) S = quad_g2_add(S, Sin[k], L.q);  // with_s = 0: Fp12 products only (S stays infinity)
+      S = quad_g2_add(S, P, L.q);
     } else {
       M = G;
-      if (with_s) S = Sin[k];
+      S = P;
       has = 1;
     }
   }
@@ -396,7 +397,7 @@ k_seg_reduce_quad(uint32_t n, const uint8_t* __restrict__ act, uint8_t act_val, 
     if (j < d && ho) {
       if (has) {
         quad::mul12(M, O, L);
-        if (with_s) S = quad_g2_add(S, T, L.q);
+        S = quad_g2_add(S, T, L.q);
       } else {
         M = O;
         S = T;
@@ -413,14 +414,12 @@ k_seg_reduce_quad(uint32_t n, const uint8_t* __restrict__ act, uint8_t act_val, 
 uint32_t launch_seg_reduce_quad(hipStream_t s, uint32_t g0, uint32_t G, const uint8_t* grp_state, const Fp12* F, const G2J* SgJ, Fp12* Fpart,
                                 G2J* Spart, uint8_t* has, uint32_t* n_out) {
   uint32_t n = (G + 63) / 64;
-  const uint32_t with_s = SgJ ? 1u : 0u;  // SgJ == nullptr: the Fp12 product alone (the MSM pass's check)
-  GBV_LAUNCH("k_seg_reduce_quad", k_seg_reduce_quad, dim3(n), dim3(64), s, G, G, grp_state + g0, (uint8_t)GRP_PENDING, F + g0,
-             SgJ ? SgJ + g0 : nullptr, Fpart, Spart, has, with_s);
+  GBV_LAUNCH("k_seg_reduce_quad", k_seg_reduce_quad, dim3(n), dim3(64), s, G, G, grp_state + g0, (uint8_t)GRP_PENDING, F + g0, SgJ + g0, Fpart, Spart, has);
   uint32_t off = 0;
   while (n > 4) {
     const uint32_t m = (n + 63) / 64;
     GBV_LAUNCH("k_seg_reduce_quad", k_seg_reduce_quad, dim3(m), dim3(64), s, n, n, has + off, (uint8_t)1, Fpart + off, Spart + off, Fpart + off + n,
-               Spart + off + n, has + off + n, with_s);
+               Spart + off + n, has + off + n);
     off += n;
     n = m;
   }
@@ -550,7 +549,7 @@ template <bool FS>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
 k_vs_chunk_coop(const uint32_t* __restrict__ chunk_be, const uint8_t* __restrict__ status, const Fp12* __restrict__ f,
                 const G2J* __restrict__ rS, uint8_t* __restrict__ chunk_valid, const Fp12* __restrict__ Fs,
-                const uint8_t* __restrict__ fs_flag, const uint8_t* __restrict__ pass_ok) {
+                const uint8_t* __restrict__ fs_flag) {
   __shared__ coop::Slot ws[SEG_WS];
   __shared__ int flags[2];
   __shared__ Fp stage[6];
@@ -561,10 +560,6 @@ k_vs_chunk_coop(const uint32_t* __restrict__ chunk_be, const uint8_t* __restrict
   for (uint32_t i = b + lane; i < e; i += 64) bad |= status[i] != SET_OK;
   if (__any(bad)) {
     if (lane == 0) chunk_valid[c] = 0;
-    return;
-  }
-  if (pass_ok && *pass_ok) {  // MSM pass: the pass's combined check held for every decoded set
-    if (lane == 0) chunk_valid[c] = 1;
     return;
   }
   coop::load_consts();
@@ -691,22 +686,11 @@ void launch_fp12_check(LaunchCfg c, uint32_t k, const Fp12* parts, uint8_t* out)
   GBV_LAUNCH("k_fp12_check", k_fp12_check, dim3(1), dim3(64), c.stream, k, k, parts, out);
 }
 void launch_vs_chunk_coop(LaunchCfg c, uint32_t C, const uint32_t* chunk_be, const uint8_t* status, const Fp12* f, const G2J* rS,
-                          uint8_t* chunk_valid, const Fp12* Fs, const uint8_t* fs_flag, const uint8_t* pass_ok) {
+                          uint8_t* chunk_valid, const Fp12* Fs, const uint8_t* fs_flag) {
   if (Fs)
-    GBV_LAUNCH("k_vs_chunk_coop<true>", k_vs_chunk_coop<true>, dim3(C), dim3(64), c.stream, C, chunk_be, status, f, rS, chunk_valid, Fs, fs_flag,
-               pass_ok);
+    GBV_LAUNCH("k_vs_chunk_coop<true>", k_vs_chunk_coop<true>, dim3(C), dim3(64), c.stream, C, chunk_be, status, f, rS, chunk_valid, Fs, fs_flag);
   else
-    GBV_LAUNCH("k_vs_chunk_coop<false>", k_vs_chunk_coop<false>, dim3(C), dim3(64), c.stream, C, chunk_be, status, f, rS, chunk_valid, Fs, fs_flag,
-               pass_ok);
-}
-void launch_vs_pass_check(hipStream_t s, uint32_t n, const uint8_t* status, const Fp12* F, Fp12* Fpart, G2J* Spart, uint8_t* has,
-                          uint8_t* pass_ok, const G2J* S_total) {
-  // the per-set Miller values of the decoded sets (status doubles as the "pending" flag: SET_OK ==
-  // GRP_PENDING), no per-set G2 terms (the MSM's S_total instead), no chunk marking (G = 0)
-  uint32_t nb = 0;
-  const uint32_t off = launch_seg_reduce_quad(s, 0, n, status, F, nullptr, Fpart, Spart, has, &nb);
-  GBV_LAUNCH("k_sm_seg_check", k_sm_seg_check, dim3(1), dim3(64), s, n, 0u, 0u, nb, Fpart + off, Spart + off, has + off, (uint8_t*)nullptr,
-             pass_ok, (Fp12*)nullptr, S_total);
+    GBV_LAUNCH("k_vs_chunk_coop<false>", k_vs_chunk_coop<false>, dim3(C), dim3(64), c.stream, C, chunk_be, status, f, rS, chunk_valid, Fs, fs_flag);
 }
 // hash_to_G2's cofactor clearing for few messages (launch_hash_msgs' latency form, n <= GBV_HASH_COOP_MAX):
 // h_eff P = [x^2 - x - 1] P + [x - 1] psi(P) + psi^2(2P) as quad_g2.h g2_clear_cofactor, with both

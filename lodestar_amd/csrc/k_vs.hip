@@ -153,7 +153,7 @@ __global__ void GBV_KERNEL_ATTR k_vs_hash_sig(uint32_t n, uint32_t nb, uint32_t 
                                               const G1A* __restrict__ table, const uint8_t* __restrict__ table_ok,
                                               const G1J* __restrict__ pk_agg, const uint8_t* __restrict__ pk_st, Seed seed, uint32_t nonce,
                                               G2A* __restrict__ H, G1J* __restrict__ rP_out, G2J* __restrict__ rS_out,
-                                              uint8_t* __restrict__ status, G2A* __restrict__ S_out) {
+                                              uint8_t* __restrict__ status) {
   if (blockIdx.x < nb) {
     if (pair) {  // few sets: lane pairs (hash_to_g2_lane_pair), nb = ceil(2n / 64)
       uint32_t i = (blockIdx.x * 64 + threadIdx.x) >> 1;
@@ -204,16 +204,6 @@ __global__ void GBV_KERNEL_ATTR k_vs_hash_sig(uint32_t n, uint32_t nb, uint32_t 
   if (check_only || st != SET_OK) return;
   uint64_t r = prf_scalar(seed, i, nonce);
   G1J rp;
-  if (S_out) {  // MSM pass: the set keeps its decoded point, the pass's sum r_i sig_i is a bucket MSM (k_msm.hip)
-    S_out[i] = s;
-    if (!randomize_g1_jac(pk, r, &rp)) {  // unreachable for subgroup keys (as randomize_pair_jac's fallback)
-      G1A pa;
-      jac_to_aff(pa, pk);
-      rp = g1_mul_u64(pa, r);
-    }
-    rP_out[i] = rp;
-    return;
-  }
   G2J rs;
   if (!randomize_pair_jac(pk, s, r, &rp, &rs)) {  // unreachable for subgroup points; plain 64-bit r then
     G1A pa;
@@ -441,28 +431,11 @@ void launch_vs_agg_big(hipStream_t s, uint32_t n_slices, const uint4* slices, ui
 void launch_vs_hash_sig(hipStream_t s, uint32_t n, const uint8_t* msgs32, const uint32_t* set_off, const uint32_t* arena,
                         const uint8_t* raw_flag, const uint8_t* raw_pk48, const uint8_t* sig, uint32_t sig_stride, const uint32_t* sig_len,
                         const G1A* table, const uint8_t* table_ok, const G1J* pk_agg, const uint8_t* pk_st, const Seed& seed,
-                        uint32_t nonce, G2A* H, G1J* rP, G2J* rS, uint8_t* status, bool split, G2A* S_out) {
+                        uint32_t nonce, G2A* H, G1J* rP, G2J* rS, uint8_t* status, bool split) {
   const uint32_t pair = n <= tuning().hash_pair_max ? 1u : 0u;
   const uint32_t nsig = (n + 63) / 64;
   const uint32_t nb = split ? 0u : pair ? (2 * n + 63) / 64 : (n + 63) / 64;  // split: the caller hashes
-  GBV_LAUNCH("k_vs_hash_sig", k_vs_hash_sig, dim3(nb + (split ? 2 : 1) * nsig), dim3(64), s, n, n, nb, pair, split ? 1u : 0u, msgs32, set_off, arena, raw_flag, raw_pk48, sig, sig_stride, sig_len, table, table_ok, pk_agg, pk_st, seed, nonce, H, rP, rS, status, S_out);
-}
-
-// MSM pass whose combined check failed: every decoded set's r_i sig_i after all (the same r_i =
-// a - b x^2 as its r_i pk_i), for the per-chunk checks; exits at once when the pass passed.
-__global__ void GBV_KERNEL_ATTR k_vs_redo_g2(uint32_t n, const uint8_t* __restrict__ status, const G2A* __restrict__ S, Seed seed,
-                                             uint32_t nonce, const uint8_t* __restrict__ pass_ok, G2J* __restrict__ rS) {
-  if (*pass_ok) return;
-  const uint32_t i = blockIdx.x * 64 + threadIdx.x;
-  if (i >= n || status[i] != SET_OK) return;
-  const uint64_t r = prf_scalar(seed, i, nonce);
-  G2J rs;
-  if (!randomize_g2(S[i], r, &rs)) rs = g2_mul_u64(S[i], r);
-  rS[i] = rs;
-}
-void launch_vs_redo_g2(hipStream_t s, uint32_t n, const uint8_t* status, const G2A* S, const Seed& seed, uint32_t nonce,
-                       const uint8_t* pass_ok, G2J* rS) {
-  GBV_LAUNCH("k_vs_redo_g2", k_vs_redo_g2, dim3((n + 63) / 64), dim3(64), s, n, n, status, S, seed, nonce, pass_ok, rS);
+  GBV_LAUNCH("k_vs_hash_sig", k_vs_hash_sig, dim3(nb + (split ? 2 : 1) * nsig), dim3(64), s, n, n, nb, pair, split ? 1u : 0u, msgs32, set_off, arena, raw_flag, raw_pk48, sig, sig_stride, sig_len, table, table_ok, pk_agg, pk_st, seed, nonce, H, rP, rS, status);
 }
 
 void launch_vs_sig_pre(hipStream_t s, uint32_t n, const uint8_t* sig, uint32_t sig_stride, const uint32_t* sig_len, const Seed& seed,

@@ -57,16 +57,9 @@ void launch_msm_g2_buckets(hipStream_t s, uint32_t s0, uint32_t n, const uint32_
 // latency part (tail stream): slice running sums and the tree sum into *total
 void launch_msm_g2_reduce(hipStream_t s, const G2J* buckets, G2J* part, G2J* total);
 void launch_fp12_check(LaunchCfg c, uint32_t k, const Fp12* parts, uint8_t* out);
-// verifySignatureSets MSM pass (gbv_vs.hip): per-set r_i sig_i for the chunk checks when the pass's
-// combined check failed (exits at once otherwise), and that combined check: prod over the decoded sets
-// of F_i times f(-g1, S_total), one final exponentiation -> pass_ok
-void launch_vs_redo_g2(hipStream_t s, uint32_t n, const uint8_t* status, const G2A* S, const Seed& seed, uint32_t nonce,
-                       const uint8_t* pass_ok, G2J* rS);
-void launch_vs_pass_check(hipStream_t s, uint32_t n, const uint8_t* status, const Fp12* F, Fp12* Fpart, G2J* Spart, uint8_t* has,
-                          uint8_t* pass_ok, const G2J* S_total);
 // chunk_be: (begin, end) set range of each of the C chunks
 void launch_vs_chunk_coop(LaunchCfg c, uint32_t C, const uint32_t* chunk_be, const uint8_t* status, const Fp12* f, const G2J* rS,
-                          uint8_t* chunk_valid, const Fp12* Fs = nullptr, const uint8_t* fs_flag = nullptr, const uint8_t* pass_ok = nullptr);
+                          uint8_t* chunk_valid, const Fp12* Fs = nullptr, const uint8_t* fs_flag = nullptr);
 void launch_sm_group_pairing(LaunchCfg c, uint32_t g0, uint32_t G, const uint32_t* grp_msg, const G1J* PgJ, const G2J* SgJ, const G2A* H,
                              const uint8_t* seg_ok, uint8_t* grp_state, uint32_t* n_fallback, Fp12* Fpair, uint8_t* pair_ok);
 void launch_sm_fallback(LaunchCfg c, uint32_t n, const uint32_t* set_grp, const uint32_t* grp_msg, const uint8_t* grp_state,
@@ -114,7 +107,7 @@ void launch_vs_agg_big(hipStream_t s, uint32_t n_slices, const uint4* slices, ui
 void launch_vs_hash_sig(hipStream_t s, uint32_t n, const uint8_t* msgs32, const uint32_t* set_off, const uint32_t* arena,
                         const uint8_t* raw_flag, const uint8_t* raw_pk48, const uint8_t* sig, uint32_t sig_stride, const uint32_t* sig_len,
                         const G1A* table, const uint8_t* table_ok, const G1J* pk_agg, const uint8_t* pk_st, const Seed& seed,
-                        uint32_t nonce, G2A* H, G1J* rP, G2J* rS, uint8_t* status, bool split = false, G2A* S_out = nullptr);
+                        uint32_t nonce, G2A* H, G1J* rP, G2J* rS, uint8_t* status, bool split = false);
 // the same per-set work in two halves for small passes: signatures (no pubkey needed) beside the
 // aggregation, then the pubkeys (k_vs.hip)
 void launch_vs_sig_pre(hipStream_t s, uint32_t n, const uint8_t* sig, uint32_t sig_stride, const uint32_t* sig_len, const Seed& seed,

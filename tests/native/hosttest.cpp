@@ -364,22 +364,8 @@ unsigned long long ht_count_randomize(const uint8_t* p96, const uint8_t* q192, u
   if (g1_only == 1) randomize_g1(P, r64, &rp);
   else if (g1_only == 2) randomize_pair_jac(PJ, Q, r64, &rp, &rq);
   else if (g1_only == 3) randomize_g2(Q, r64, &rq);
-  else if (g1_only == 4) randomize_g1_jac(PJ, r64, &rp);
   else randomize_pair(P, Q, r64, &rp, &rq);
   return g_fme_count;
-}
-// randomize_g1_jac (P Jacobian, the MSM pass's G1 term) against randomize_pair_jac's r_i pk_i: the
-// same point for the same r64 (both affine out); returns 1 when equal
-int ht_rand_g1_jac_matches(const uint8_t* p96, const uint8_t* q192, uint64_t r64) {
-  G1J P = jac_dbl(jac_from_aff(G1A{load_mont(p96), load_mont(p96 + 48)}));
-  G2A Q{load_fp2(q192), load_fp2(q192 + 96)};
-  G1J a, b;
-  G2J rq;
-  if (!randomize_pair_jac(P, Q, r64, &a, &rq) || !randomize_g1_jac(P, r64, &b)) return 0;
-  G1A x, y;
-  jac_to_aff(x, a);
-  jac_to_aff(y, b);
-  return fp_eq(x.x, y.x) && fp_eq(x.y, y.y);
 }
 // Miller value with Jacobian P (k_vs_miller / k_sm_miller)
 unsigned long long ht_count_miller_1j(const uint8_t* p96, const uint8_t* q192) {

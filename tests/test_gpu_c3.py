@@ -90,8 +90,7 @@ def test_c3_oracle_spot_check(c3):
         assert v.aggregate_pubkeys(list(s.indices)) == O.g1_compress(agg)
 
 
-@pytest.mark.parametrize("msm", [0, 32768])
-def test_c3_large_pass_thread_forms(c3, msm):
+def test_c3_large_pass_thread_forms(c3):
     """A pass of 40 960 sets (the fixture's 80 calls four times over): above the 16 384-set bound of
     the split signature/pubkey form and the 32 768-set bound of the lane-pair Miller values, so the
     throughput kernels run -- k_vs_hash_sig with both roles, k_vs_miller one thread per set, the chunk
@@ -99,20 +98,7 @@ def test_c3_large_pass_thread_forms(c3, msm):
     the last copy."""
     from lodestar_amd import AggregatedSignatureSet
     v, sets, _ = c3
-    # msm = 32768: the pass checks all its chunks at once against one bucket MSM of sum r_i sig_i
-    # (k_msm.hip) -- the all-valid pass passes outright, the pass with bad sets fails that check and
-    # falls back to the per-set r_i sig_i (k_vs_redo_g2) and the per-chunk checks
-    v.tune("vs_msm_min", msm)
-    try:
-        _large_pass(v, sets)
-    finally:
-        v.tune("vs_msm_min", 0)
-
-
-def _large_pass(v, sets):
-    from lodestar_amd import AggregatedSignatureSet
     calls = [list(sets[i:i + PER_CALL]) for i in range(0, N_SETS, PER_CALL)] * 4
-    calls = [list(c) for c in calls]
     assert sum(len(c) for c in calls) == 4 * N_SETS
     assert v.verify_signature_sets_multi_sync(calls) == [True] * 320
     bad = [list(c) for c in calls]

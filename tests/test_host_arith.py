@@ -349,7 +349,6 @@ def test_roofline_work_constants_are_counted(lib):
         assert 3 * (lib.ht_count_op(1, p96, q192) - 7) == bench.FME_G1_SCAN  # full G1 addition (minus the doubling)
         assert lib.ht_count_g2_decode(o.g2_compress(sig_pt)) == bench.FME_G2_DECODE
         assert lib.ht_count_randomize(p96, q192, r64, 3) == bench.FME_RANDOMIZE_G2
-        assert lib.ht_count_randomize(p96, q192, r64, 4) == bench.FME_RANDOMIZE_G1_JAC
         assert lib.ht_count_hash_part(msg, 0) == bench.FME_HASH_MAPS
         assert lib.ht_count_hash_part(msg, 1) == bench.FME_HASH_CLEAR
         assert lib.ht_count_op(0, p96, q192) == bench.FME_G1_MADD
@@ -372,16 +371,6 @@ def test_coop_clear_cofactor(lib):
         got = [int.from_bytes(out.raw[48 * i:48 * i + 48], "big") for i in range(4)]
         want = o.clear_cofactor_g2(q)
         assert ((got[0], got[1]), (got[2], got[3])) == (want[0], want[1])
-
-
-@pytest.mark.parametrize("r64", [1, 0xFFFFFFFFFFFFFFFF, 0x0123456789ABCDEF, 0x8000000000000001])
-def test_randomize_g1_jac_matches_pair(lib, r64):
-    """The MSM pass's G1 term (curve.h randomize_g1_jac, P Jacobian) equals randomize_pair_jac's
-    r_i pk_i for the same r (k_vs_hash_sig's two forms must pair with the same scalars)."""
-    P = o.g1_mul(o.G1_GEN, 0x51515)
-    Q = o.hash_to_g2(b"rand-g1-jac")
-    lib.ht_rand_g1_jac_matches.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint64]
-    assert lib.ht_rand_g1_jac_matches(be(P[0]) + be(P[1]), fp2b(Q[0]) + fp2b(Q[1]), r64) == 1
 
 
 @pytest.mark.parametrize("k,mode", [(4, 1), (3, 1), (1, 1), (2, 2), (1, 2)])
