@@ -50,27 +50,27 @@ MAC_PER_FME = 300  # u32 x u32 -> u64 MACs per Fp product (12-limb Montgomery: 1
 # Algorithmic work per unit in Fp-multiplication equivalents (FME), COUNTED on the device code path by
 # the host build of the same arithmetic (tests/native/hosttest.cpp ht_count_*; pinned by
 # tests/test_host_arith.py::test_roofline_work_constants_are_counted):
-FME_SIG_VALIDATE = 2111     # Signature.fromBytes(sig, true): G2 decompress + subgroup check
+FME_SIG_VALIDATE = 2108     # Signature.fromBytes(sig, true): G2 decompress + subgroup check
 FME_RANDOMIZE_G1 = 593      # r_i pk_i (endomorphism-split 32-step ladder + affine tables)
 FME_COMB_G1 = 126           # r_i pk_i from the validator's comb table (7 doublings + 7 mixed additions)
 FME_RANDOMIZE_PAIR = 2086   # r_i pk_i and r_i sig_i with one shared inversion
 FME_RANDOMIZE_PAIR_JAC = 2096  # the same with P Jacobian (aggregate pubkeys straight from k_vs_agg)
-FME_HASH_TO_G2 = 4808       # RFC 9380 hash_to_G2 (SSWU with one norm exponentiation per map + 3-isogeny + h_eff + to affine)
-FME_MILLER_1J = 7244        # Miller value of one pair, Jacobian P
-# k_vs_miller_group: k pairs on one accumulator (one f^2 per bit): the first pair 7256 (P with Z != 1,
-# as r_i pk_i is on the device), each further pair 5012 (its lines without another squaring)
-FME_MILLER_GROUP_FIRST = 7256
-FME_MILLER_GROUP_MORE = 5012
+FME_HASH_TO_G2 = 4802       # RFC 9380 hash_to_G2 (SSWU with one norm exponentiation per map + 3-isogeny + h_eff + to affine)
+FME_MILLER_1J = 6803        # Miller value of one pair, Jacobian P
+# k_vs_miller_group: k pairs on one accumulator (one f^2 per bit): the first pair 6815 (P with Z != 1,
+# as r_i pk_i is on the device), each further pair 4571 (its lines without another squaring)
+FME_MILLER_GROUP_FIRST = 6815
+FME_MILLER_GROUP_MORE = 4571
 
 
 def fme_miller_group(k):
     return FME_MILLER_GROUP_FIRST + (k - 1) * FME_MILLER_GROUP_MORE
 
 FME_G1_SCAN = 48            # 3-level 8-lane chunk scan of r_i pk_i (3 Jacobian G1 additions)
-FME_G2_DECODE = 941         # G2 decompression alone (k_sig_decode, k_vs_sig_decode)
+FME_G2_DECODE = 938         # G2 decompression alone (k_sig_decode, k_vs_sig_decode)
 FME_G2_SUBGROUP = FME_SIG_VALIDATE - FME_G2_DECODE  # the psi-based G2 subgroup check (1170)
 FME_RANDOMIZE_G2 = 1491     # r_i sig_i alone (randomize_g2: endomorphism-split ladder + affine tables)
-FME_HASH_MAPS = 2097        # hash_to_G2's two SSWU maps + isogenies + Q0 + Q1 (k_hash_msgs_pre)
+FME_HASH_MAPS = 2091        # hash_to_G2's two SSWU maps + isogenies + Q0 + Q1 (k_hash_msgs_pre)
 FME_HASH_CLEAR = 2711       # hash_to_G2's cofactor clearing + affine form (k_hash_clear_quad / _coop)
 # k_sm_prepare<false> (bench: G2 sum by bucket MSM) and <true> (per-set G2 ladders)
 W_PREPARE_FME_MSM = FME_SIG_VALIDATE + FME_RANDOMIZE_G1 + FME_G1_SCAN

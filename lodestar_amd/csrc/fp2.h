@@ -71,6 +71,14 @@ GBV_HD Fp2 fp2_sqr(const Fp2& a) {
 #endif
 
 GBV_HD Fp2 fp2_add_lazy(const Fp2& a, const Fp2& b) { return Fp2{fp_add_lazy(a.c0, b.c0), fp_add_lazy(a.c1, b.c1)}; }
+// a / 2 (canonical a): two halvings, no product
+GBV_HD Fp2 fp2_half(const Fp2& a) { return Fp2{fp_half(a.c0), fp_half(a.c1)}; }
+// 12 (1 + i) c = 3 b' c (b' = 4 (1 + i), the twist's constant) by additions, no product
+GBV_HD Fp2 fp2_mul_3b(const Fp2& c) {
+  Fp2 x = fp2_mul_xi(c);
+  Fp2 x4 = fp2_dbl(fp2_dbl(x));
+  return fp2_add(fp2_dbl(x4), x4);
+}
 
 
 GBV_HD Fp2 fp2_mul_fp(const Fp2& a, const Fp& s) { return Fp2{fp_mul(a.c0, s), fp_mul(a.c1, s)}; }
@@ -106,13 +114,13 @@ GBV_HD bool fp2_is_lexi_large(const Fp2& a) {
 // fp2_sqrt_with_norm_root is the second half, for callers that already hold a square root alpha
 // (either sign) of the norm a0^2 + a1^2.
 GBV_HD bool fp2_sqrt_with_norm_root(Fp2& root, const Fp2& a, const Fp& alpha) {
-  Fp delta = fp_mul(fp_add(a.c0, alpha), FP_INV2);
-  Fp delta2 = fp_mul(fp_sub(a.c0, alpha), FP_INV2);
+  Fp delta = fp_half(fp_add(a.c0, alpha));
+  Fp delta2 = fp_half(fp_sub(a.c0, alpha));
   delta = fp_sel(fp_is_zero(delta), delta2, delta);
   Fp t = fp_pow_sched(delta, SCHED_SQRT_M3_NSQ, SCHED_SQRT_M3_IDX, SCHED_SQRT_M3_STEPS);
   Fp x0 = fp_mul(t, delta);
   bool qr = fp_eq(fp_mul(x0, t), FP_ONE);
-  Fp h = fp_mul(fp_mul(a.c1, t), FP_INV2);
+  Fp h = fp_half(fp_mul(a.c1, t));
   root.c0 = fp_sel(qr, x0, fp_neg(h));
   root.c1 = fp_sel(qr, h, x0);
   return fp2_eq(fp2_sqr(root), a);

@@ -49,13 +49,6 @@ __device__ __forceinline__ Fp6 fp6_sel(bool c, const Fp6& a, const Fp6& b) {
 }
 // Karatsuba recombination of (a0 b0, a1 b1, (a0 + a1)(b0 + b1))
 __device__ __forceinline__ Fp2 kara(const Fp& t0, const Fp& t1, const Fp& t2) { return Fp2{fp_sub(t0, t1), fp_sub(fp_sub(t2, t0), t1)}; }
-// 12 (1 + i) c = 3 b' c (b' = 4 (1 + i), the twist's constant) by additions
-__device__ __forceinline__ Fp2 mul_3b(const Fp2& c) {
-  Fp2 x = fp2_mul_xi(c);
-  Fp2 x4 = fp2_dbl(fp2_dbl(x));
-  return fp2_add(fp2_dbl(x4), x4);
-}
-__device__ __forceinline__ Fp2 fp2_half(const Fp2& a) { return Fp2{fp_half(a.c0), fp_half(a.c1)}; }
 #define LZA fp_add_lazy
 #define LZS fp_sub_lazy4
 
@@ -101,7 +94,7 @@ __device__ __forceinline__ Line pair_dbl(PairT& T, const PairP& P, bool h) {
   const Fp2 w1 = pswap(sq01);
   const Fp2 w2 = pswap(C1);
   const Fp2 B = fp2_sel(h, sq01, w1), C = fp2_sel(h, C1, w2), X2 = fp2_sel(h, w1, sq01);
-  const Fp2 E = mul_3b(C), F = fp2_add(fp2_dbl(E), E);
+  const Fp2 E = fp2_mul_3b(C), F = fp2_add(fp2_dbl(E), E);
   const Fp2 A = fp2_half(xy);                         // lane 0 only
   const Fp2 BmF = fp2_sub(B, F), G = fp2_half(fp2_add(B, F));
   const Fp2 H = fp2_sub(S, fp2_add(B, C));            // lane 1 only

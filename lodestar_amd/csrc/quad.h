@@ -100,7 +100,7 @@ __device__ __forceinline__ Line dbl(PairT& T, const PairP& P, uint32_t q) {
   round4(r, q, x.c0, x.c1, QLZA(s.c0, s.c1), QLZS(s.c0, s.c1), s.c0, s.c1, zero, zero);
   const Fp2 X2{x2_re, fp_dbl(r[0])};
   const Fp2 S = sq(r[1], r[2]);
-  const Fp2 E = mul_3b(C), F = fp2_add(fp2_dbl(E), E);
+  const Fp2 E = fp2_mul_3b(C), F = fp2_add(fp2_dbl(E), E);
   const Fp2 A = fp2_half(xy);
   const Fp2 BmF = fp2_sub(B, F), G = fp2_half(fp2_add(B, F));
   const Fp2 H = fp2_sub(S, fp2_add(B, C));

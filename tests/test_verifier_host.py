@@ -262,8 +262,9 @@ def test_passes_overlap_and_the_next_takes_every_queued_job():
         return v, res
     v, res = run(go())
     assert res == [True] * MAX_PASSES_IN_FLIGHT + [True, False, True, True]
-    assert sorted(v.passes[:MAX_PASSES_IN_FLIGHT]) == [("multi", [k + 1]) for k in range(MAX_PASSES_IN_FLIGHT)]
-    assert v.passes[MAX_PASSES_IN_FLIGHT:] == [("multi", [1, 1, 1, 1])]
+    # passes are recorded as their device waits finish, so the queued jobs' pass may land among the
+    # first ones: compare as a multiset
+    assert sorted(v.passes) == sorted([("multi", [k + 1]) for k in range(MAX_PASSES_IN_FLIGHT)] + [("multi", [1, 1, 1, 1])])
     assert v.device_passes == MAX_PASSES_IN_FLIGHT + 1
 
 
