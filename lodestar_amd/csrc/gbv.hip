@@ -7,7 +7,6 @@ using namespace gbv;
 
 namespace {
 
-constexpr unsigned FB_GRID = 2048;  // persistent failure-path grids: 2 waves per SIMD
 // a failing segment with at least this many chunks checks them one thread each (throughput), below
 // it one wave each (latency); see k_sm_group_check / k_sm_group_pairing
 constexpr uint32_t GROUP_CHECK_THREAD_MIN = 512;

@@ -35,6 +35,14 @@
 #ifndef GBV_QUAD_WPE
 #define GBV_QUAD_WPE 1  // 512 registers, fewer frame spills: 64-block pass 12.2 -> 11.75 ms, 2 in flight 9.3 -> 8.3-8.6 ms
 #endif
+// thread-serial pairing checks of the same-message failure path (k_sm_fb.hip)
+#ifndef GBV_FB_WPE
+#define GBV_FB_WPE 2  // 1 wave: k_sm_fb_blocks / _sets 57.8 -> 63 ms (profiles/r05s)
+#endif
+#ifndef GBV_GRPCHK_WPE
+#define GBV_GRPCHK_WPE 1  // k_sm_group_check (~200 waves): 1 wave 31.8 -> 24-26 ms (profiles/r05s)
+#endif
+constexpr unsigned FB_GRID = 1024 * GBV_FB_WPE;  // persistent failure-path grids: GBV_FB_WPE waves per SIMD
 #define GBV_QUAD_ATTR __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GBV_QUAD_WPE, GBV_QUAD_WPE)))
 
 // Tail kernels (chunk Miller values, MSM reduction, segment reduction and check) share SIMDs with
