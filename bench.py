@@ -620,7 +620,7 @@ def _pmc_gather(ops, kernel, members):
             "launch_ms_at_pmc": round(d["duration_ms"], 3), "hbm_peak_GBps": 8000.0}
 
 
-def c4_bench(v, sk_ints, pk_rows, cpu, n_blocks=64, electra=False):
+def c4_bench(v, sk_ints, pk_rows, cpu, n_blocks=64, electra=False, depth=2):
     rng = np.random.Generator(np.random.PCG64(0xC4E if electra else 0xC4))
     t0 = time.time()
     calls = make_blocks(v, sk_ints, n_blocks, rng, electra=electra)
@@ -635,7 +635,7 @@ def c4_bench(v, sk_ints, pk_rows, cpu, n_blocks=64, electra=False):
         t = time.perf_counter()
         assert v.verify_signature_sets_sync(calls[0]) is True
         lat.append((time.perf_counter() - t) * 1e3)
-    stages = [v.stage_signature_sets(calls) for _ in range(2)]
+    stages = [v.stage_signature_sets(calls) for _ in range(depth)]
     for st in stages:
         assert st.verify() == [1] * n_blocks
     dt, ops = _timed_ops(v, stages, 6, [1] * n_blocks)
@@ -647,8 +647,8 @@ def c4_bench(v, sk_ints, pk_rows, cpu, n_blocks=64, electra=False):
                "electra " if electra else ""),
            "unit": "sets/s", "value": round(n_sets / dt, 1), "blocks_per_s": round(n_blocks / dt, 2),
            "lone_block_latency_ms_p50": round(float(np.median(lat)), 3), "sets_per_block": len(calls[0]),
-           "config": "range-sync segment of %d blocks (%d sets, %d pubkeys gathered), 2 passes in flight (built in %.1fs)" % (
-               n_blocks, n_sets, members, build_s),
+           "config": "range-sync segment of %d blocks (%d sets, %d pubkeys gathered), %d passes in flight (built in %.1fs)" % (
+               n_blocks, n_sets, members, depth, build_s),
            "roofline": _vs_roofline(v, n_sets, ops, members_small=small, members_big=big, n_chunks=n_chunks)}
     g = _pmc_gather(ops, "k_vs_agg_big" if electra else "k_vs_agg", big if electra else small)
     if g:
@@ -965,7 +965,10 @@ def main():
             from oracle import cpu_baseline
             pk_rows = cpu_baseline.affine_rows(cpu_baseline.load(), key_pks)
         for name, fn, a, kw in (("c1", c1_bench, sks, {}), ("c3", c3_bench, sk_ints, {"n_calls": args.c3_calls}),
-                                ("c4", c4_bench, sk_ints, {"n_blocks": args.c4_blocks}),
+                                # C4 at the verifier queue's MAX_PASSES_IN_FLIGHT (3): 64-block segments are
+                                # latency-bound, a third pass fills the device (1.27 -> 1.33 M, profiles/r05x);
+                                # C4e and the 65 536-set C1 / C3 passes gain nothing from it (r05x, r05y)
+                                ("c4", c4_bench, sk_ints, {"n_blocks": args.c4_blocks, "depth": 3}),
                                 ("c4e", c4_bench, sk_ints, {"n_blocks": args.c4e_blocks, "electra": True})):
             t = time.time()
             extras[name] = fn(v, a, pk_rows, cpu_ok, **kw)
