@@ -767,6 +767,7 @@ def main():
     ap.add_argument("--inflight", type=int, default=3, help="staged batches queued on the device at once")
     ap.add_argument("--c3-calls", type=int, default=512, help="128-set calls per C3 device pass")
     ap.add_argument("--c4-blocks", type=int, default=64, help="blocks per C4 device pass (range-sync segment)")
+    ap.add_argument("--c4-depth", type=int, default=3, help="C4 passes in flight (the verifier queue allows 3)")
     ap.add_argument("--c4e-blocks", type=int, default=16, help="electra blocks per C4e device pass")
     ap.add_argument("--tune", action="append", default=[], metavar="NAME=VALUE",
                     help="gbv_tune setting applied before anything runs (experiments; include/gbv.h lists the names)")
@@ -968,7 +969,7 @@ def main():
                                 # C4 at the verifier queue's MAX_PASSES_IN_FLIGHT (3): 64-block segments are
                                 # latency-bound, a third pass fills the device (1.27 -> 1.33 M, profiles/r05x);
                                 # C4e and the 65 536-set C1 / C3 passes gain nothing from it (r05x, r05y)
-                                ("c4", c4_bench, sk_ints, {"n_blocks": args.c4_blocks, "depth": 3}),
+                                ("c4", c4_bench, sk_ints, {"n_blocks": args.c4_blocks, "depth": args.c4_depth}),
                                 ("c4e", c4_bench, sk_ints, {"n_blocks": args.c4e_blocks, "electra": True})):
             t = time.time()
             extras[name] = fn(v, a, pk_rows, cpu_ok, **kw)
