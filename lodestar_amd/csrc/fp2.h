@@ -1,6 +1,5 @@
-// Fp2 = Fp[i]/(i^2 + 1).  Karatsuba multiplication; the three base products are inlined into one
-// out-of-line function so their independent v_mad_u64_u32 chains interleave (ILP inside one wave).
-// Fp2 arguments cross the call through scratch (4 x 64 B), negligible against ~2k VALU ops.
+// Fp2 = Fp[i]/(i^2 + 1).  Karatsuba multiplication and complex squaring, inlined into the caller
+// over the out-of-line Fp product (fp.h fp_mul); halvings and the twist constant by additions.
 #pragma once
 #include "fp.h"
 
@@ -20,40 +19,9 @@ GBV_HD Fp2 fp2_conj(const Fp2& a) { return Fp2{a.c0, fp_neg(a.c1)}; }
 // (a0 + a1 i)(1 + i) = (a0 - a1) + (a0 + a1) i
 GBV_HD Fp2 fp2_mul_xi(const Fp2& a) { return Fp2{fp_sub(a.c0, a.c1), fp_add(a.c0, a.c1)}; }
 
-#ifndef GBV_FP2_IMPL
-#define GBV_FP2_IMPL 1
-#endif
-
-#if GBV_FP2_IMPL == 0
-GBV_NI Fp2 fp2_mul(Fp2 a, Fp2 b) {
-  Fp t0 = fp_mul_inl(a.c0, b.c0);
-  Fp t1 = fp_mul_inl(a.c1, b.c1);
-  Fp t2 = fp_mul_inl(fp_add(a.c0, a.c1), fp_add(b.c0, b.c1));
-  return Fp2{fp_sub(t0, t1), fp_sub(fp_sub(t2, t0), t1)};
-}
-
-GBV_NI Fp2 fp2_sqr(Fp2 a) {
-  Fp t0 = fp_mul_inl(fp_add(a.c0, a.c1), fp_sub(a.c0, a.c1));
-  Fp t1 = fp_mul_inl(a.c0, a.c1);
-  return Fp2{t0, fp_dbl(t1)};
-}
-#elif GBV_FP2_IMPL == 2
-// Fully inlined Karatsuba (sequential Fp products): no calls anywhere in the point layer.
-GBV_HD Fp2 fp2_mul(const Fp2& a, const Fp2& b) {
-  Fp t0 = fp_mul_inl(a.c0, b.c0);
-  Fp t1 = fp_mul_inl(a.c1, b.c1);
-  Fp t2 = fp_mul_inl(fp_add(a.c0, a.c1), fp_add(b.c0, b.c1));
-  return Fp2{fp_sub(t0, t1), fp_sub(fp_sub(t2, t0), t1)};
-}
-
-GBV_HD Fp2 fp2_sqr(const Fp2& a) {
-  Fp t0 = fp_mul_inl(fp_add(a.c0, a.c1), fp_sub(a.c0, a.c1));
-  Fp t1 = fp_mul_inl(a.c0, a.c1);
-  return Fp2{t0, fp_dbl(t1)};
-}
-#else
 // Karatsuba over out-of-line Fp products: the Fp2 layer is inlined into its caller and only the
-// 70-VGPR Fp product is a call, so occupancy (not in-thread ILP) hides the mad latency.
+// 70-VGPR Fp product is a call, so occupancy (not in-thread ILP) hides the mad latency.  (One call
+// per Fp2 product with the three Fp products inline measured far slower: C2 21.3 -> 16.1 M, round 5.)
 // Inputs may be lazy (components below 4 p, fp_add_lazy): the Karatsuba sums and the (a0 - a1)
 // of the square are formed without reduction; outputs are canonical.
 GBV_HD Fp2 fp2_mul(const Fp2& a, const Fp2& b) {
@@ -68,7 +36,6 @@ GBV_HD Fp2 fp2_sqr(const Fp2& a) {
   Fp t1 = fp_mul(a.c0, a.c1);
   return Fp2{t0, fp_dbl(t1)};
 }
-#endif
 
 GBV_HD Fp2 fp2_add_lazy(const Fp2& a, const Fp2& b) { return Fp2{fp_add_lazy(a.c0, b.c0), fp_add_lazy(a.c1, b.c1)}; }
 // a / 2 (canonical a): two halvings, no product
