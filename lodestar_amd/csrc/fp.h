@@ -15,14 +15,6 @@
 
 namespace gbv {
 
-GBV_HD Fp fp_one_raw() {
-  Fp r;
-#pragma unroll
-  for (int i = 0; i < 12; ++i) r.v[i] = i == 0 ? 1u : 0u;
-  return r;
-}
-#define FP_ONE_RAW_ fp_one_raw()
-
 GBV_HD Fp fp_zero() {
   Fp r;
 #pragma unroll
@@ -411,51 +403,9 @@ GBV_HD Fp fp_half(const Fp& x) {
   return r;
 }
 
-// Inverse by a branch-free binary extended GCD on the canonical value A = a R (Montgomery form
-// in, Montgomery form out, 0 -> 0).  Invariants u = A x1, v = A x2 (mod p), v odd:
-//   if u odd: (u < v ? swap(u,v), swap(x1,x2)); u -= v; x1 -= x2;   then u /= 2, x1 /= 2 (mod p)
-// until u == 0, when v = 1 and x2 = A^-1; the result is A^-1 R^3 R^-1 = a^-1 R.  Every lane runs
-// the same straight-line step (~190 VALU ops), checked for completion every 32 steps: about
-// 2.5x cheaper than the 381-bit exponentiation (608 Fp products) it replaces.
-#ifndef GBV_INV_SAFEGCD
-#define GBV_INV_SAFEGCD 1  // 0: the binary extended GCD below (A/B)
-#endif
-GBV_NI Fp fp_inv_bgcd(Fp a) {
-  Fp u = a, v = P_RAW, x1 = FP_ONE_RAW_, x2 = fp_zero();
-  for (int outer = 0; outer < 48; ++outer) {  // <= 2 * 381 steps are needed; 48 * 32 = 1536
-    for (int k = 0; k < 32; ++k) {
-      Fp d;
-      uint32_t lt = raw_sub(d, u, v);     // borrow: u < v
-      bool odd = u.v[0] & 1u;
-      bool sw = odd && lt;
-      Fp nu = fp_sel(sw, v, u), nv = fp_sel(sw, u, v);
-      Fp nx1 = fp_sel(sw, x2, x1), nx2 = fp_sel(sw, x1, x2);
-      raw_sub(d, nu, nv);
-      u = fp_sel(odd, d, nu);
-      v = nv;
-      x1 = fp_sel(odd, fp_sub(nx1, nx2), nx1);
-      x2 = nx2;
-#pragma unroll
-      for (int i = 0; i < 11; ++i) u.v[i] = (u.v[i] >> 1) | (u.v[i + 1] << 31);
-      u.v[11] >>= 1;
-      x1 = fp_half(x1);
-    }
-#if defined(__HIP_DEVICE_COMPILE__)
-    if (!__any(!fp_is_zero(u))) break;
-#else
-    if (fp_is_zero(u)) break;
-#endif
-  }
-  return fp_mul(x2, R3_RAW);
-}
-
 // Inverse by safegcd divsteps (inv_sg.h): (a R)^-1 R^3 R^-1 = a^-1 R.  0 -> 0.
 GBV_NI Fp fp_inv(Fp a) {
-#if GBV_INV_SAFEGCD
   return fp_mul(sg::inv_raw(a), R3_RAW);
-#else
-  return fp_inv_bgcd(a);
-#endif
 }
 
 // Canonical (non-Montgomery) value comparisons used by sign rules ----------------------------
