@@ -5,8 +5,9 @@
 //   meta.json {n_sets, n_calls, n_keys, table}, call_off.u32, idx.u32, sigs.bin (96 n), msgs.bin (32 calls),
 //   keys.bin (48 n_keys: the table is keys[i mod n_keys], built with addPubkeys + replicatePubkeys)
 //   node addon/bench_api.js <dir> [reps]
-// Prints one JSON line: packed-form, IBlsVerifier-shaped ("ibls": objects packed per call inside the
-// clock, as the Lodestar binding does) and object-form sets/s (best of reps), passes, validity.
+// Prints one JSON line: packed-form, IBlsVerifier-shaped ("ibls": {publicKey, signature} objects, keys
+// found by identity and packed per pass inside the clock, as the Lodestar binding does) and index-form
+// object sets/s (best of reps), passes, validity.
 "use strict";
 const path = require("path");
 const fs = require("fs");
@@ -37,24 +38,36 @@ async function main() {
   addon.replicatePubkeys(v.ctx, 0, meta.n_keys, meta.n_keys, meta.table - meta.n_keys);
   const nCalls = meta.n_calls;
   const message = (g) => msgs.subarray(32 * g, 32 * g + 32);
-  // the caller's deserialized gossip data, built before the clock: packed views, and one object per set
+  // index2pubkey's PublicKey objects (stand-ins: identity is all the verifier reads of them), registered
+  // the way the binding's loadIndex2pubkey does
+  const keyObjs = new Array(meta.table);
+  for (let i = 0; i < meta.table; ++i) keyObjs[i] = {validator: i};
+  v.registerPubkeyObjects(0, keyObjs);
+  // the caller's deserialized gossip data, built before the clock: packed views; one {publicKey,
+  // signature} object per set, the reference's call shape (interface.ts:55-59, attestation.ts:134-137);
+  // and one {index, signature} object per set (the index form)
   const packed = [];
+  const ibls = [];
   const objects = [];
   for (let g = 0; g < nCalls; ++g) {
     const a = callOff[g], b = callOff[g + 1];
     packed.push({indices: idx.subarray(a, b), signatures: sigs.subarray(96 * a, 96 * b)});
-    const sets = new Array(b - a);
-    for (let i = a; i < b; ++i) sets[i - a] = {publicKey: null, index: idx[i], signature: sigs.subarray(96 * i, 96 * i + 96)};
+    const sets = new Array(b - a), isets = new Array(b - a);
+    for (let i = a; i < b; ++i) {
+      sets[i - a] = {index: idx[i], signature: sigs.subarray(96 * i, 96 * i + 96)};
+      isets[i - a] = {publicKey: keyObjs[idx[i]], signature: sigs.subarray(96 * i, 96 * i + 96)};
+    }
     objects.push(sets);
+    ibls.push(isets);
   }
   const nSets = callOff[nCalls];
   async function stream(form) {
-    const calls = form === "packed" ? packed : objects;
+    const calls = form === "packed" ? packed : form === "ibls" ? ibls : objects;
     const p0 = v.devicePasses;
     const t0 = process.hrtime.bigint();
     // "ibls": the IBlsVerifier call shape the Lodestar binding uses (chain/bls/gpu/index.ts over
-    // verifySameMessageSets): one {publicKey, signature, index} object per set in, boolean[] out; the
-    // packing into the device form happens here, inside the clock
+    // verifySameMessageSets): one {publicKey, signature} object per set in (index by key identity),
+    // boolean[] out; the packing into the device form happens here, inside the clock
     const res = form === "ibls"
       ? await Promise.all(calls.map((s, g) => v.verifySameMessageSets(s, message(g))))
       : await Promise.all(calls.map((s, g) => v.verifySignatureSetsSameMessage(s, message(g))));

@@ -226,10 +226,40 @@ class GpuBlsVerifier {
       });
     }
     this.devicePasses = 0;
+    // index2pubkey by object identity: the PublicKey objects of the node's table (registered by
+    // loadIndex2pubkey and the index2pubkey listener) -> their validator index.  The reference's
+    // same-message call hands {publicKey, signature} (interface.ts:55-59, attestation.ts:134-137); the
+    // key object it passes is index2pubkey[validatorIndex], so its index selects the HBM copy.
+    this.keyIndex = new WeakMap();
   }
 
   addPubkeys(firstIndex, pk48s, validate) {
     return this.addon.addPubkeys(this.ctx, firstIndex, pk48s, !!validate);
+  }
+
+  /** Record keys[k] (the node's PublicKey object for validator firstIndex + k) in the identity map.
+   * The device copy of those keys is added separately (addPubkeys). */
+  registerPubkeyObjects(firstIndex, keys) {
+    for (let k = 0; k < keys.length; ++k) {
+      const o = keys[k];
+      if (o !== null && typeof o === "object") this.keyIndex.set(o, firstIndex + k);
+    }
+  }
+
+  /** validator index of a key object of index2pubkey, or undefined for a key outside the table */
+  indexOf(publicKey) {
+    return publicKey !== null && typeof publicKey === "object" ? this.keyIndex.get(publicKey) : undefined;
+  }
+
+  /** the indices of a list of key objects, or undefined when any is outside the table */
+  indicesOf(publicKeys) {
+    const out = new Array(publicKeys.length);
+    for (let k = 0; k < publicKeys.length; ++k) {
+      const i = this.indexOf(publicKeys[k]);
+      if (i === undefined) return undefined;
+      out[k] = i;
+    }
+    return out;
   }
 
   /** Device hashing for the signature-set builders (addon/gossip_sets.js): Merkle roots of objects of
@@ -288,7 +318,11 @@ class GpuBlsVerifier {
     return results.every((r) => r === true);
   }
 
-  /** sets: {index, signature}[] (index form of {publicKey, signature}) -> boolean[]; or the packed form
+  /** sets: the reference's {publicKey, signature}[] (interface.ts:55-59) -> boolean[].  A set's key is
+   * found by `index` when the caller gives one, else by the identity of its publicKey object in
+   * index2pubkey (registerPubkeyObjects); a key outside the table is verified from its bytes
+   * (publicKey.toBytes()) as a one-set verifySignatureSets job, whose boolean is that set's answer
+   * (the reference's per-set retry verifies each set alone, jobItem.ts:93-125).  Or the packed form
    * {indices: Uint32Array(n), signatures: Uint8Array(96 n)} -> Uint8Array(n) of 0 / 1 (the same answer
    * without a JS object per set: two memcpys in the addon instead of 2n property reads) */
   async verifySignatureSetsSameMessage(sets, message, opts = {}) {
@@ -301,28 +335,41 @@ class GpuBlsVerifier {
       throw Object.assign(new TypeError("packed sets: {indices: Uint32Array(n), signatures: Uint8Array(96 n) | Uint8Array[n]}"), {code: "GBV_E_ARG"});
     const n = packed ? sets.indices.length : sets.length;
     const nKeys = n ? this.addon.pubkeyCount(this.ctx) : 0;
+    const badIndex = () => Object.assign(new RangeError("validator index out of range"), {code: "GBV_E_ARG"});
+    let ix = null; // object form: every set's validator index
+    let outside = null; // object form: the positions of sets whose key is not in index2pubkey
     if (packed) {
-      const ix = sets.indices;
-      for (let i = 0; i < n; ++i)
-        if (ix[i] >= nKeys) throw Object.assign(new RangeError("validator index out of range"), {code: "GBV_E_ARG"});
+      const pi = sets.indices;
+      for (let i = 0; i < n; ++i) if (pi[i] >= nKeys) throw badIndex();
     } else {
-      for (const s of sets) {
-        if (!(s.index >= 0 && s.index < nKeys)) throw Object.assign(new RangeError("validator index out of range"), {code: "GBV_E_ARG"});
+      ix = new Uint32Array(n);
+      for (let i = 0; i < n; ++i) {
+        const s = sets[i];
+        let k = s.index;
+        if (k === undefined) {
+          k = this.keyIndex.get(s.publicKey);
+          if (k === undefined) {
+            (outside || (outside = [])).push(i);
+            continue;
+          }
+        }
+        if (!(k >= 0 && k < nKeys)) throw badIndex();
+        ix[i] = k;
       }
+      if (outside) return this._sameMessageOutsideKeys(sets, ix, outside, message, opts);
     }
+    const job = (chunk, cix) =>
+      new Promise((resolve, reject) => this._queue({type: "sameMessage", resolve, reject, addedTimeMs: Date.now(), opts, sets: chunk, ix: cix, message}));
     if (n < 2 * MAX_SIGNATURE_SETS_PER_JOB) {
       // one chunk (every gossip call): its job's promise is the call's (no Promise.all, no concat)
-      const chunk = packed ? {indices: sets.indices, signatures: sets.signatures, length: n} : sets;
-      return new Promise((resolve, reject) => this._queue({type: "sameMessage", resolve, reject, addedTimeMs: Date.now(), opts, sets: chunk, message}));
+      return job(packed ? {indices: sets.indices, signatures: sets.signatures, length: n} : sets, ix);
     }
-    const chunks = packed
-      ? chunkRanges(n, MAX_SIGNATURE_SETS_PER_JOB).map(([a, b]) => ({indices: sets.indices.subarray(a, b),
-        signatures: sigList ? sets.signatures.slice(a, b) : sets.signatures.subarray(96 * a, 96 * b), length: b - a}))
-      : chunkifyMaximizeChunkSize(sets, MAX_SIGNATURE_SETS_PER_JOB);
     const results = await Promise.all(
-      chunks.map(
-        (chunk) =>
-          new Promise((resolve, reject) => this._queue({type: "sameMessage", resolve, reject, addedTimeMs: Date.now(), opts, sets: chunk, message}))
+      chunkRanges(n, MAX_SIGNATURE_SETS_PER_JOB).map(([a, b]) =>
+        packed
+          ? job({indices: sets.indices.subarray(a, b),
+            signatures: sigList ? sets.signatures.slice(a, b) : sets.signatures.subarray(96 * a, 96 * b), length: b - a}, null)
+          : job(sets.slice(a, b), ix.subarray(a, b))
       )
     );
     if (!packed) return [].concat(...results);
@@ -336,10 +383,38 @@ class GpuBlsVerifier {
     return out;
   }
 
-  /** The IBlsVerifier call shape (chain/bls/gpu/index.ts, validation/attestation.ts:131-137): one
-   * {index, signature} (+ publicKey, unused) per set -> boolean[].  The objects ride in the job as they
-   * are; _runPass copies every job of a pass into four pass-wide buffers (_packSameMessage) -- a
-   * per-call typed array, or Node-API property reads per set, cost more. */
+  /** A same-message call holding keys outside index2pubkey: the sets with table keys go to the device as
+   * one same-message job, every other set as a one-set verifySignatureSets job over its key bytes; the
+   * booleans come back in call order. */
+  async _sameMessageOutsideKeys(sets, ix, outside, message, opts) {
+    const n = sets.length;
+    const isOut = new Uint8Array(n);
+    for (const i of outside) isOut[i] = 1;
+    const inside = [];
+    for (let i = 0; i < n; ++i) if (!isOut[i]) inside.push(i);
+    const loose = outside.map((i) => {
+      const pk = sets[i].publicKey;
+      const bytes = pk instanceof Uint8Array ? pk : pk && typeof pk.toBytes === "function" ? pk.toBytes() : null;
+      if (!bytes || bytes.length !== 48)
+        throw Object.assign(new TypeError("set without index: publicKey must be an index2pubkey key, a PublicKey or 48 bytes"), {code: "GBV_E_ARG"});
+      return {pubkey: bytes, signingRoot: message, signature: sets[i].signature};
+    });
+    const pIn = inside.length
+      ? this.verifySignatureSetsSameMessage(inside.map((i) => ({index: ix[i], signature: sets[i].signature})), message, opts)
+      : Promise.resolve([]);
+    const pOut = loose.map((s) => new Promise((resolve, reject) => this._queue({type: "default", resolve, reject, addedTimeMs: Date.now(), opts, sets: [s]})));
+    const [rIn, rOut] = await Promise.all([pIn, Promise.all(pOut)]);
+    const out = new Array(n);
+    inside.forEach((i, k) => (out[i] = rIn[k]));
+    outside.forEach((i, k) => (out[i] = rOut[k] === true));
+    return out;
+  }
+
+  /** The IBlsVerifier call shape (chain/bls/gpu/index.ts, validation/attestation.ts:134-137): one
+   * {publicKey, signature} per set -> boolean[], keys resolved by identity.  The objects ride in the job
+   * as they are with their resolved indices beside them; _runPass copies every job of a pass into four
+   * pass-wide buffers (_packSameMessage) -- a per-call typed array of signatures, or Node-API property
+   * reads per set, cost more. */
   verifySameMessageSets(sets, message, opts = {}) {
     return this.verifySignatureSetsSameMessage(sets, message, opts);
   }
@@ -432,9 +507,9 @@ class GpuBlsVerifier {
       messages.set(j.message, 32 * c);
       j.off = o;
       if (Array.isArray(s)) {
+        indices.set(j.ix, o); // resolved when the call was validated
         for (let i = 0; i < n; ++i) {
-          const e = s[i], g = e.signature;
-          indices[o + i] = e.index;
+          const g = s[i].signature;
           if (g.length === 96) signatures.set(g, 96 * (o + i));
         }
       } else {

@@ -43,6 +43,8 @@ class FakeAddon {
     this.passes.push(rec);
     // the flat pass form {counts, messages, indices, signatures}: one 0 / 1 byte per set, like the addon
     if (sm) rec.sm = Array.from(sm.counts);
+    if (sm) rec.smIdx = Array.from(sm.indices);
+    if (df) rec.dfPk = df.map((c) => c.map((s) => (s.pubkey ? s.pubkey[0] : null)));
     const res = {
       sameMessage: sm ? Uint8Array.from({length: sm.indices.length}, (_, i) => (sm.signatures[96 * i] === 1 ? 1 : 0)) : null,
       default: df
@@ -177,9 +179,33 @@ async function cpu() {
   report.badIndex = (await expectReject(v.verifySignatureSets([set(1, 1 << 20)]), "GBV_E_ARG")) === "ok" &&
     (await expectReject(v.verifySignatureSetsSameMessage([smSet(1, 1 << 21)], msg), "GBV_E_ARG")) === "ok";
 
+  // the reference's same-message call shape (interface.ts:55-59, attestation.ts:134-137):
+  // {publicKey, signature} with no index, the key objects those of index2pubkey (registered by
+  // identity); a key outside the table is verified from its bytes as a one-set job
   // verifyOnMainThread: synchronous device call, no queue
   report.mainThread = (await v.verifySignatureSets([set(1)], {verifyOnMainThread: true})) === true &&
     JSON.stringify(a.passes[a.passes.length - 1]) === '["sync",1]';
+
+  const ka = new FakeAddon();
+  const kv = new V.GpuBlsVerifier({addon: ka});
+  const keyObjs = [0, 1, 2, 3].map((i) => ({toBytes: () => new Uint8Array(48).fill(i + 1)}));
+  kv.registerPubkeyObjects(10, keyObjs);
+  const pkSet = (ok, pk) => ({publicKey: pk, signature: smSet(ok).signature});
+  const stranger = {toBytes: () => new Uint8Array(48).fill(9)};
+  const rId = await kv.verifySignatureSetsSameMessage([pkSet(1, keyObjs[0]), pkSet(0, keyObjs[3]), pkSet(1, keyObjs[2])], msg);
+  const idPass = ka.passes[ka.passes.length - 1];
+  report.sameMessageByKeyIdentity = JSON.stringify(rId) === "[true,false,true]" && JSON.stringify(idPass.smIdx) === "[10,13,12]" &&
+    kv.indexOf(keyObjs[1]) === 11 && kv.indexOf(stranger) === undefined &&
+    JSON.stringify(kv.indicesOf([keyObjs[3], keyObjs[0]])) === "[13,10]" && kv.indicesOf([keyObjs[0], stranger]) === undefined;
+  const nPass = ka.passes.length;
+  const rOut = await kv.verifySignatureSetsSameMessage([pkSet(1, keyObjs[1]), pkSet(1, stranger), pkSet(0, stranger),
+    pkSet(0, new Uint8Array(48).fill(7))], msg);
+  const outPasses = ka.passes.slice(nPass);
+  const smIdx = [].concat(...outPasses.filter((p) => p.smIdx).map((p) => p.smIdx));
+  const dfPk = [].concat(...outPasses.filter((p) => p.dfPk).map((p) => [].concat(...p.dfPk)));
+  report.sameMessageOutsideKeys = JSON.stringify(rOut) === "[true,true,false,false]" && JSON.stringify(smIdx) === "[11]" &&
+    JSON.stringify(dfPk.sort()) === "[7,9,9]";
+  report.sameMessageKeyless = (await expectReject(kv.verifySignatureSetsSameMessage([{signature: smSet(1).signature}], msg), "GBV_E_ARG")) === "ok";
 
   // metrics: the reference's families
   const text = v.metricsText();
@@ -296,6 +322,18 @@ async function gpu(fixPath) {
     v.verifySignatureSetsSameMessage(c.indices.map((idx, k) => ({index: idx, signature: hex(c.sigs[k])})), hex(c.msg))
       .then((r) => JSON.stringify(r) === JSON.stringify(c.expected))));
   report.sameMessage = sm;
+  // the reference's call shape on the device: {publicKey, signature} with no index, stand-in PublicKey
+  // objects registered as index2pubkey's (loadIndex2pubkey); then every second set's key replaced by an
+  // unregistered object with the same bytes (a key outside the table): the same booleans
+  const keyObjs = fix.keys.pks.map((p) => ({toBytes: () => hex(p)}));
+  v.registerPubkeyObjects(0, keyObjs);
+  report.sameMessageByKey = await Promise.all(fix.same_message.map((c) =>
+    v.verifySignatureSetsSameMessage(c.indices.map((idx, k) => ({publicKey: keyObjs[idx], signature: hex(c.sigs[k])})), hex(c.msg))
+      .then((r) => JSON.stringify(r) === JSON.stringify(c.expected))));
+  report.sameMessageOutsideKeys = await Promise.all(fix.same_message.map((c) =>
+    v.verifySignatureSetsSameMessage(c.indices.map((idx, k) => ({publicKey: k % 2 ? {toBytes: () => hex(fix.keys.pks[idx])} : keyObjs[idx],
+      signature: hex(c.sigs[k])})), hex(c.msg))
+      .then((r) => JSON.stringify(r) === JSON.stringify(c.expected))));
   // multithread.test.ts:85-106: 8 x (verifySignatureSets + verifySignatureSetsSameMessage), synchronously
   // and with a tick between submissions, batched or not, with and without priority
   const valid = toSets(fix.verify_sets.find((c) => c.name === "distinct_valid"));

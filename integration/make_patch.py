@@ -16,11 +16,12 @@ What it changes:
     (SingleSignatureSet.index, AggregatedSignatureSet.indices); every builder that reads index2pubkey
     fills them (randao, proposer, proposer / attester slashings, attestations, exits, sync aggregate);
     index2pubkey growth is announced to listeners (syncPubkeys, addFinalizedPubkey);
-  * beacon-node: the gossip builders (selection proof, aggregate-and-proof, sync committee, contribution,
-    sync selection proof) and their callers pass the indices; the same-message gossip call passes each
-    set's index; a new chain option selects GpuBlsVerifier (chain/bls/gpu/index.ts, over
-    addon/gpu_bls_verifier.js + gbv_addon.node, copied beside it), which mirrors index2pubkey in HBM.
-  * callers of IBlsVerifier are not edited.
+  * beacon-node: the sync-committee gossip builders that read index2pubkey (sync committee message,
+    contribution, sync selection proof) fill the index; a new chain option selects GpuBlsVerifier
+    (chain/bls/gpu/index.ts, over addon/gpu_bls_verifier.js + gbv_addon.node, copied beside it), which
+    mirrors index2pubkey in HBM and finds any other key object's index by its identity.
+  * callers of IBlsVerifier are not edited (no file of chain/validation/ outside signatureSets/, and
+    not chain/bls/interface.ts): the same-message call keeps the interface's {publicKey, signature}.
 """
 import os
 import shutil
@@ -190,10 +191,11 @@ export function createAggregateSignatureSetFromIndices(
         ("""export type Index2PubkeyCache = PublicKey[];""", """export type Index2PubkeyCache = PublicKey[];
 
 /**
- * Called with (first index, compressed keys) whenever index2pubkey gains entries (syncPubkeys,
- * EpochCache.addFinalizedPubkey): GpuBlsVerifier keeps a copy of the table in GPU memory.
+ * Called with (first index, compressed keys, the new PublicKey objects) whenever index2pubkey gains
+ * entries (syncPubkeys, EpochCache.addFinalizedPubkey): GpuBlsVerifier keeps a copy of the table in GPU
+ * memory and finds a key object's index by its identity.
  */
-export type Index2PubkeyListener = (firstIndex: ValidatorIndex, pubkeys: Uint8Array[]) => void;
+export type Index2PubkeyListener = (firstIndex: ValidatorIndex, pubkeys: Uint8Array[], keys: PublicKey[]) => void;
 export const index2pubkeyListeners = new Set<Index2PubkeyListener>();"""),
         ("""  const newCount = validators.length;
   index2pubkey.length = newCount;
@@ -210,7 +212,8 @@ export const index2pubkeyListeners = new Set<Index2PubkeyListener>();"""),
 }""", """    index2pubkey[i] = PublicKey.fromBytes(pubkey); // Optimize for aggregation
   }
   if (added && added.length > 0) {
-    for (const listener of index2pubkeyListeners) listener(firstNew, added);
+    const keys = index2pubkey.slice(firstNew, newCount);
+    for (const listener of index2pubkeyListeners) listener(firstNew, added, keys);
   }
 }"""),
     ],
@@ -227,7 +230,7 @@ export const index2pubkeyListeners = new Set<Index2PubkeyListener>();"""),
 } from "./pubkeyCache.js";"""),
         ("""    this.index2pubkey[index] = PublicKey.fromBytes(pubkeyBytes); // Optimize for aggregation
   }""", """    this.index2pubkey[index] = PublicKey.fromBytes(pubkeyBytes); // Optimize for aggregation
-    for (const listener of index2pubkeyListeners) listener(index, [pubkeyBytes]);
+    for (const listener of index2pubkeyListeners) listener(index, [pubkeyBytes], [this.index2pubkey[index]]);
   }"""),
     ],
     ST + "index.ts": [
@@ -242,10 +245,6 @@ export const index2pubkeyListeners = new Set<Index2PubkeyListener>();"""),
   index2pubkeyListeners,
   newUnfinalizedPubkeyIndexMap,
 } from "./cache/pubkeyCache.js";"""),
-    ],
-    BN + "chain/bls/interface.ts": [
-        ("""    sets: {publicKey: PublicKey; signature: Uint8Array}[],""", """    /** index: the validator index of publicKey in index2pubkey (GpuBlsVerifier requires it) */
-    sets: {publicKey: PublicKey; signature: Uint8Array; index?: number}[],"""),
     ],
     BN + "chain/bls/index.ts": [
         ("""export {BlsSingleThreadVerifier} from "./singleThread.js";""", """export {BlsSingleThreadVerifier} from "./singleThread.js";
@@ -282,90 +281,6 @@ export {GpuBlsVerifier} from "./gpu/index.js";"""),
     if (bls instanceof GpuBlsVerifier) bls.loadIndex2pubkey(this.index2pubkey);
 """),
     ],
-    BN + "chain/validation/attestation.ts": [
-        ("""      signatureSets.map((set) => ({publicKey: set.pubkey, signature: set.signature})),""",
-         """      signatureSets.map((set) => ({publicKey: set.pubkey, signature: set.signature, index: set.index})),"""),
-        ("""    signatureSet = createSingleSignatureSetFromComponents(
-      chain.index2pubkey[validatorIndex],
-      attestationOrCache.cache.signingRoot,
-      signature
-    );""", """    signatureSet = createSingleSignatureSetFromComponents(
-      chain.index2pubkey[validatorIndex],
-      attestationOrCache.cache.signingRoot,
-      signature,
-      validatorIndex
-    );"""),
-        ("""    signatureSet = createSingleSignatureSetFromComponents(
-      chain.index2pubkey[validatorIndex],
-      getSigningRoot(),
-      signature
-    );""", """    signatureSet = createSingleSignatureSetFromComponents(
-      chain.index2pubkey[validatorIndex],
-      getSigningRoot(),
-      signature,
-      validatorIndex
-    );"""),
-    ],
-    BN + "chain/validation/aggregateAndProof.ts": [
-        ("""  const indexedAttestationSignatureSet = createAggregateSignatureSetFromComponents(
-    indexedAttestation.attestingIndices.map((i) => chain.index2pubkey[i]),
-    signingRoot,
-    indexedAttestation.signature
-  );
-  const signatureSets = [
-    getSelectionProofSignatureSet(chain.config, attSlot, aggregator, signedAggregateAndProof),
-    getAggregateAndProofSignatureSet(chain.config, attEpoch, aggregator, signedAggregateAndProof),""",
-         """  const indexedAttestationSignatureSet = createAggregateSignatureSetFromIndices(
-    chain.index2pubkey,
-    indexedAttestation.attestingIndices,
-    signingRoot,
-    indexedAttestation.signature
-  );
-  const aggregatorIndex = aggregateAndProof.aggregatorIndex;
-  const signatureSets = [
-    getSelectionProofSignatureSet(chain.config, attSlot, aggregator, signedAggregateAndProof, aggregatorIndex),
-    getAggregateAndProofSignatureSet(chain.config, attEpoch, aggregator, signedAggregateAndProof, aggregatorIndex),"""),
-    ],
-    BN + "chain/validation/signatureSets/selectionProof.ts": [
-        ('import {Slot, phase0, ssz} from "@lodestar/types";', 'import {Slot, ValidatorIndex, phase0, ssz} from "@lodestar/types";'),
-        ("""  aggregator: PublicKey,
-  aggregateAndProof: phase0.SignedAggregateAndProof
-): ISignatureSet {
-  return createSingleSignatureSetFromComponents(
-    aggregator,
-    getSelectionProofSigningRoot(config, slot),
-    aggregateAndProof.message.selectionProof
-  );""", """  aggregator: PublicKey,
-  aggregateAndProof: phase0.SignedAggregateAndProof,
-  aggregatorIndex?: ValidatorIndex
-): ISignatureSet {
-  return createSingleSignatureSetFromComponents(
-    aggregator,
-    getSelectionProofSigningRoot(config, slot),
-    aggregateAndProof.message.selectionProof,
-    aggregatorIndex
-  );"""),
-    ],
-    BN + "chain/validation/signatureSets/aggregateAndProof.ts": [
-        ('import {Epoch} from "@lodestar/types";', 'import {Epoch, ValidatorIndex} from "@lodestar/types";'),
-        ("""  aggregator: PublicKey,
-  aggregateAndProof: SignedAggregateAndProof
-): ISignatureSet {
-  return createSingleSignatureSetFromComponents(
-    aggregator,
-    getAggregateAndProofSigningRoot(config, epoch, aggregateAndProof),
-    aggregateAndProof.signature
-  );""", """  aggregator: PublicKey,
-  aggregateAndProof: SignedAggregateAndProof,
-  aggregatorIndex?: ValidatorIndex
-): ISignatureSet {
-  return createSingleSignatureSetFromComponents(
-    aggregator,
-    getAggregateAndProofSigningRoot(config, epoch, aggregateAndProof),
-    aggregateAndProof.signature,
-    aggregatorIndex
-  );"""),
-    ],
     BN + "chain/validation/signatureSets/syncCommittee.ts": [
         ("""    pubkey: state.epochCtx.index2pubkey[syncCommittee.validatorIndex],
 """, """    pubkey: state.epochCtx.index2pubkey[syncCommittee.validatorIndex],
@@ -384,34 +299,7 @@ export {GpuBlsVerifier} from "./gpu/index.js";"""),
     index: contributionAndProof.aggregatorIndex,
 """),
     ],
-    BN + "chain/validation/signatureSets/syncCommitteeContribution.ts": [
-        ('import {altair, ssz} from "@lodestar/types";', 'import {ValidatorIndex, altair, ssz} from "@lodestar/types";'),
-        ("""  pubkeys: PublicKey[]
-): ISignatureSet {""", """  pubkeys: PublicKey[],
-  /** the participants' validator indices, same order as pubkeys */
-  indices?: ValidatorIndex[]
-): ISignatureSet {"""),
-        ("""    type: SignatureSetType.aggregate,
-    pubkeys,
-""", """    type: SignatureSetType.aggregate,
-    pubkeys,
-    indices,
-"""),
-    ],
-    BN + "chain/validation/syncCommitteeContributionAndProof.ts": [
-        ("""    getSyncCommitteeContributionSignatureSet(headState as CachedBeaconStateAltair, contribution, participantPubkeys),""",
-         """    getSyncCommitteeContributionSignatureSet(
-      headState as CachedBeaconStateAltair,
-      contribution,
-      participantPubkeys,
-      syncCommitteeParticipantIndices
-    ),"""),
-    ],
 }
-
-# the aggregateAndProof.ts import of createAggregateSignatureSetFromComponents becomes ...FromIndices
-EXTRA_IMPORT = (BN + "chain/validation/aggregateAndProof.ts", "createAggregateSignatureSetFromComponents,",
-                "createAggregateSignatureSetFromIndices,")
 
 GPU_INDEX_TS = '''/**
  * GpuBlsVerifier: IBlsVerifier on an MI355X GPU (HIP kernels for gfx950 behind the C ABI include/gbv.h of
@@ -421,8 +309,11 @@ GPU_INDEX_TS = '''/**
  *                         batchable buffering, priority, canAcceptWork and close() semantics as
  *                         BlsMultiThreadWorkerPool (multithread/index.ts), with up to 3 passes on the device.
  * Signature sets are handed over in index form: the validator indices the builders put in
- * ISignatureSet.index / .indices select keys from the GPU's copy of index2pubkey; a set without
- * indices (a key from the message itself, e.g. a BLS-to-execution change) passes its compressed key.
+ * ISignatureSet.index / .indices, or else the index of the set's PublicKey object in index2pubkey (the
+ * queue keeps index2pubkey's objects in an identity map, filled here and by index2pubkeyListeners),
+ * select keys from the GPU's copy of index2pubkey; a key outside the table (e.g. a BLS-to-execution
+ * change's) passes its compressed bytes.  Callers are not edited: verifySignatureSetsSameMessage takes
+ * the interface's {publicKey, signature} sets as validation/attestation.ts hands them.
  */
 import {createRequire} from "node:module";
 import {PublicKey, aggregatePublicKeys} from "@chainsafe/blst";
@@ -442,10 +333,13 @@ const LOAD_BATCH = 1 << 16;
 /** the job queue of gpu_bls_verifier.js (its GpuBlsVerifier class) as this binding uses it */
 interface GpuQueue {
   addPubkeys(firstIndex: number, pk48s: Uint8Array, validate: boolean): Uint8Array;
+  registerPubkeyObjects(firstIndex: number, keys: PublicKey[]): void;
+  indexOf(publicKey: PublicKey): number | undefined;
+  indicesOf(publicKeys: PublicKey[]): number[] | undefined;
   canAcceptWork(): boolean;
   verifySignatureSets(sets: IndexFormSet[], opts: VerifySignatureOpts): Promise<boolean>;
   verifySameMessageSets(
-    sets: {signature: Uint8Array; index?: number}[],
+    sets: {publicKey: PublicKey; signature: Uint8Array}[],
     message: Uint8Array,
     opts: Omit<VerifySignatureOpts, "verifyOnMainThread">
   ): Promise<boolean[]>;
@@ -455,8 +349,9 @@ interface GpuQueue {
 export class GpuBlsVerifier implements IBlsVerifier {
   private readonly queue: GpuQueue;
   private readonly logger: Logger;
-  private readonly onNewPubkeys = (firstIndex: number, pubkeys: Uint8Array[]): void => {
+  private readonly onNewPubkeys = (firstIndex: number, pubkeys: Uint8Array[], keys: PublicKey[]): void => {
     this.queue.addPubkeys(firstIndex, Buffer.concat(pubkeys), false);
+    this.queue.registerPubkeyObjects(firstIndex, keys);
   };
 
   constructor(opts: {blsGpuDevice?: number}, modules: {logger: Logger; metrics: Metrics | null}) {
@@ -476,8 +371,9 @@ export class GpuBlsVerifier implements IBlsVerifier {
    * index2pubkeyListeners).  The keys were validated on deposit (processDeposit.ts:163-166). */
   loadIndex2pubkey(index2pubkey: Index2PubkeyCache): void {
     for (let first = 0; first < index2pubkey.length; first += LOAD_BATCH) {
-      const keys = index2pubkey.slice(first, first + LOAD_BATCH).map((pk) => pk.toBytes());
-      this.queue.addPubkeys(first, Buffer.concat(keys), false);
+      const objs = index2pubkey.slice(first, first + LOAD_BATCH);
+      this.queue.addPubkeys(first, Buffer.concat(objs.map((pk) => pk.toBytes())), false);
+      this.queue.registerPubkeyObjects(first, objs);
     }
     this.logger.info("GPU BLS verifier: index2pubkey loaded", {validators: index2pubkey.length});
   }
@@ -487,13 +383,18 @@ export class GpuBlsVerifier implements IBlsVerifier {
   }
 
   async verifySignatureSets(sets: ISignatureSet[], opts: VerifySignatureOpts = {}): Promise<boolean> {
-    return this.queue.verifySignatureSets(sets.map(toIndexForm), opts);
+    return this.queue.verifySignatureSets(
+      sets.map((set) => toIndexForm(set, this.queue)),
+      opts
+    );
   }
 
-  /** validation/attestation.ts:131-137 hands one {publicKey, signature, index} per set: the queue packs
-   * them into one Uint32Array of indices and one signature buffer per call (the addon's packed form) */
+  /** validation/attestation.ts:134-137 hands one {publicKey, signature} per set, publicKey being
+   * index2pubkey[validatorIndex]: the queue finds each index by the object's identity and packs the call
+   * into the pass-wide index / signature buffers of the addon; a key outside the table is verified from
+   * its bytes */
   async verifySignatureSetsSameMessage(
-    sets: {publicKey: PublicKey; signature: Uint8Array; index?: number}[],
+    sets: {publicKey: PublicKey; signature: Uint8Array}[],
     message: Uint8Array,
     opts: Omit<VerifySignatureOpts, "verifyOnMainThread"> = {}
   ): Promise<boolean[]> {
@@ -506,12 +407,14 @@ export class GpuBlsVerifier implements IBlsVerifier {
   }
 }
 
-function toIndexForm(set: ISignatureSet): IndexFormSet {
+function toIndexForm(set: ISignatureSet, queue: GpuQueue): IndexFormSet {
   const {signingRoot, signature} = set;
   if (set.type === SignatureSetType.single) {
-    return set.index !== undefined ? {index: set.index, signingRoot, signature} : {pubkey: set.pubkey.toBytes(), signingRoot, signature};
+    const index = set.index ?? queue.indexOf(set.pubkey);
+    return index !== undefined ? {index, signingRoot, signature} : {pubkey: set.pubkey.toBytes(), signingRoot, signature};
   }
-  if (set.indices !== undefined) return {indices: set.indices, signingRoot, signature};
+  const indices = set.indices ?? queue.indicesOf(set.pubkeys);
+  if (indices !== undefined) return {indices, signingRoot, signature};
   // an aggregate built from keys outside index2pubkey: hand the aggregate key over (validated on the device)
   return {pubkey: aggregatePublicKeys(set.pubkeys).toBytes(), signingRoot, signature};
 }
@@ -530,7 +433,7 @@ def main(ref):
                 os.makedirs(os.path.dirname(os.path.join(root, rel)), exist_ok=True)
                 shutil.copyfile(src, os.path.join(root, rel))
             text = open(src).read()
-            for old, new in edits + ([EXTRA_IMPORT[1:]] if rel == EXTRA_IMPORT[0] else []):
+            for old, new in edits:
                 if text.count(old) != 1:
                     raise SystemExit("%s: edit anchor found %d times:\n%s" % (rel, text.count(old), old))
                 text = text.replace(old, new)

@@ -54,6 +54,7 @@ def test_js_verifier_queue_semantics_without_gpu():
     # the binding's wiring: the node's own metric families (metrics.blsThreadPool + the gpu ones on
     # metrics.register) are fed by every call and scraped through queueLength.addCollect; the
     # IBlsVerifier-shaped same-message call packs its objects into the device form
+    assert r["sameMessageByKeyIdentity"] is True and r["sameMessageOutsideKeys"] is True and r["sameMessageKeyless"] is True
     assert r["nodeMetricsFed"] is True and r["nodeMetricsScrape"] is True and r["sameMessageObjectsPacked"] is True
 
 
@@ -66,6 +67,8 @@ def test_js_verifier_golden_cases_on_gpu():
     assert "fatal" not in r, r
     assert all(r["verifySets"]) and len(r["verifySets"]) == 16
     assert all(r["sameMessage"]) and len(r["sameMessage"]) == 8
+    # {publicKey, signature} with no index: keys found by identity, or verified from their bytes
+    assert r["sameMessageByKey"] == [True] * 8 and r["sameMessageOutsideKeys"] == [True] * 8
     assert r["manyCalls"] == [True] * 8
     assert r["batchedInvalid"] is True and r["mainThread"] is True and r["metrics"] is True
     assert r["devicePasses"] >= 4
