@@ -10,8 +10,9 @@
  *   verifySets(ctx, sets)                         -> Promise<boolean> (gbv_verify_sets; verifySignatureSets)
  *   verifySetsMulti(ctx, calls)                   -> Promise<Array<boolean | Error>> (gbv_verify_sets_multi:
  *                                                                      several calls in one device pass)
- *   verifySameMessageMulti(ctx, calls)            -> Promise<boolean[][]> (gbv_verify_same_message_multi;
- *                                                                      verifySignatureSetsSameMessage)
+ *   verifySameMessageMulti(ctx, calls)            -> Promise<(Uint8Array | boolean[])[]>
+ *                                                     (gbv_verify_same_message_multi; verifySignatureSetsSameMessage:
+ *                                                      a packed call answers with 0 / 1 bytes, an object call with booleans)
  *   aggregatePubkeys(ctx, indices)                -> Uint8Array(48)  (gbv_aggregate_pubkeys)
  *   aggregateSerializedPubkeys(ctx, pk48s, validate) -> Uint8Array(48) (syncCommittee.ts:37)
  *   close(ctx)                                    -> Promise<void>   (waits for in-flight work, gbv_destroy)
@@ -20,7 +21,9 @@
  * each on its own refillable batches -- gbv_sm_batch_fill / gbv_vs_batch_fill + submit):
  *   submitPass(ctx, sameMessageCalls | null, defaultCalls | null) -> pass  (synchronous: inputs copied
  *                                                  to pinned memory, kernels enqueued; no device wait)
- *   waitPass(pass)                                -> Promise<{sameMessage: boolean[][] | Error,
+ *   waitPass(pass)                                -> Promise<{sameMessage: Uint8Array (flat form: one
+ *                                                             0 / 1 byte per set of the pass) |
+ *                                                             (boolean[] | Uint8Array)[] (per call) | Error,
  *                                                             default: (boolean | Error)[] | Error}>
  *   freePasses(ctx)                               -> number of pass slots not in flight
  * and the rest of IBlsVerifier's needs: verifySetsSync(ctx, sets) -> boolean (verifyOnMainThread,

@@ -771,6 +771,7 @@ def main():
     ap.add_argument("--c4e-blocks", type=int, default=16, help="electra blocks per C4e device pass")
     ap.add_argument("--tune", action="append", default=[], metavar="NAME=VALUE",
                     help="gbv_tune setting applied before anything runs (experiments; include/gbv.h lists the names)")
+    ap.add_argument("--no-vs-shard", action="store_true", help="skip the sharded verifySignatureSets object of the gossip line")
     ap.add_argument("--shard-calls", type=int, default=512,
                     help="vs-shard: 128-member aggregate sets / 128 in the ONE sharded verifySignatureSets call")
     args = ap.parse_args()
@@ -790,9 +791,12 @@ def main():
     invalid_frac = args.invalid_frac if args.invalid_frac is not None else (0.01 if args.mode == "replay" else 0.0)
     dist = None
     torch = None
-    if world > 1 or args.mode == "vs-shard":
-        # torch (and RCCL) initialise the GPU before libgbv does; --mode vs-shard joins a real RCCL
-        # process group even at one rank, so the same collective runs at every N
+    # the sharded verifySignatureSets line (`vs_shard`) rides on the default gossip line at every N
+    want_vs_shard = args.mode == "gossip" and not args.no_extras and not args.no_vs_shard
+    if world > 1 or args.mode == "vs-shard" or want_vs_shard:
+        # torch (and RCCL) initialise the GPU before libgbv does; --mode vs-shard (and the vs_shard object
+        # of the default line) joins a real RCCL process group even at one rank, so the same collective
+        # runs at every N
         import torch
         import torch.distributed as dist
         torch.cuda.set_device(local_rank)
@@ -840,8 +844,14 @@ def main():
         if invalid_frac > 0:
             sigs_all, expect_all = inject_invalid(sigs_all, call_off_all, args.sets, invalid_frac)
         n_calls = len(call_off_all) - 1
-        per = (n_calls + world - 1) // world
-        c0, c1 = min(rank * per, n_calls), min((rank + 1) * per, n_calls)
+        # the product's split (ShardedVerifier.call_ranges): contiguous call ranges of near-equal SET count
+        sizes = np.diff(call_off_all.astype(np.int64)).tolist()
+        if dist is not None:
+            from lodestar_amd.sharded import ShardedVerifier
+            ranges = ShardedVerifier(v).call_ranges(sizes)
+        else:
+            ranges = [(0, n_calls)]
+        c0, c1 = ranges[rank]
         s0, s1 = int(call_off_all[c0]), int(call_off_all[c1])
         call_off = (call_off_all[c0:c1 + 1] - s0).astype(np.uint32)
         idx = idx_all[s0:s1]
@@ -849,7 +859,7 @@ def main():
         msgs = msgs_all[32 * c0:32 * c1]
         expect = expect_all[s0:s1]
         n_mine = s1 - s0
-        widths = [int(call_off_all[min((r + 1) * per, n_calls)] - call_off_all[min(r * per, n_calls)]) for r in range(world)]
+        widths = [int(call_off_all[b] - call_off_all[a]) for a, b in ranges]
         gather = (max(widths), widths, int(expect_all.sum())) if world > 1 else None
     if invalid_frac > 0:
         log("injected %d invalid sets on rank 0 (C5 recipe)" % int((expect == 0).sum()))
@@ -979,9 +989,10 @@ def main():
         log("c5: %s sets/s (%.1fs)" % (extras["c5"]["value"], time.time() - t))
 
     vs_shard = None
-    if world > 1 and args.mode == "gossip" and not args.no_extras:
+    if want_vs_shard:
         # the north_star multi-GPU path beside the gossip replicas: ONE verifySignatureSets call sharded
-        # over every rank, Fp12 Miller partials all-gathered over RCCL, one final exponentiation each
+        # over every rank, Fp12 Miller partials all-gathered over RCCL, one final exponentiation each;
+        # at N = 1 the same exchange over an RCCL group of one, the anchor of the strong-scaling curve
         vs_shard = vs_shard_measure(args, v, sk_ints, world, rank, log)
         if rank == 0:
             log("vs-shard: %s sets/s over %d ranks" % (vs_shard["value"], world))

@@ -121,17 +121,21 @@ struct gbv_ctx {
   // stream A (per-set throughput kernels) at the lowest priority; the tail stream 2 (chunk-level
   // latency-bound work), the hash stream 4 and stream 5 at the highest.  Stream 5 carries the
   // signature half of small verifySignatureSets passes and, in the invalid-dense same-message regime,
-  // every other batch's failure path (the hash then runs on stream A): at most four streams are live
-  // at once, one per hardware queue (GPU_MAX_HW_QUEUES=4).
+  // every other batch's failure path (the hash then runs on stream A).  Five streams exist per context
+  // (with stream 6 below) over GPU_MAX_HW_QUEUES=4 hardware queues, so the runtime maps two of them to
+  // one queue; the same-message and verifySignatureSets paths keep at most four busy at once.
   hipStream_t stream = nullptr, stream2 = nullptr, stream4 = nullptr;
   hipStream_t stream5 = nullptr;
-  hipStream_t stream6 = nullptr;  // gbv_fp12_check: the multi-GPU exchange's final check, beside streamed shard passes
+  // gbv_fp12_check: the multi-GPU exchange's final check, beside streamed shard passes.  Shard passes
+  // use streams A, 2 / 4 and 5, so stream 6 shares a hardware queue with one of them: the check can
+  // still queue behind that stream's kernels of the next pass.
+  hipStream_t stream6 = nullptr;
   gbv::G1A* table = nullptr;
   uint8_t* table_ok = nullptr;
   size_t table_cap = 0;
   std::atomic<size_t> table_n{0};  // read without the lock (gbv_pubkeys_count), written under it
   // per-slot comb tables for r pk (curve.h comb_mul; 128 affine entries = 12 KB per slot), built on
-  // append / replicate; comb_on = false (GBV_COMB=0, or an allocation that failed) -> the ladder
+  // append / replicate; comb_on = false (gbv_tune "comb" 0, or an allocation that failed) -> the ladder
   uint4* comb = nullptr;
   uint8_t* comb_ok = nullptr;
   size_t comb_cap = 0;
@@ -142,8 +146,8 @@ struct gbv_ctx {
   // A failing MSM segment pays the per-set G2 terms after all (k_sm_redo_g2) on top of the MSM, so
   // after one the next MSM_COOLDOWN submits use the per-set ladders (invalid-dense streams, C5)
   uint32_t msm_cooldown = 0;
-  // Settings read once at gbv_init (GBV_MSM_MIN, GBV_MSM_COOLDOWN, GBV_SEGMENTS), changed only by
-  // gbv_tune: segments of at least msm_min sets form their G2 sum with the bucket MSM (k_msm.hip;
+  // Per-context settings (defaults at gbv_init), changed only by gbv_tune ("msm_min", "msm_cooldown",
+  // "segments"): segments of at least msm_min sets form their G2 sum with the bucket MSM (k_msm.hip;
   // 0 = never); a failing MSM segment starts a cooldown of msm_cooldown_len submits; a batch is cut
   // into at most `segments` pipeline segments (tests use several on small batches)
   uint32_t msm_min = 131072, msm_cooldown_len = 16, segments = 1;

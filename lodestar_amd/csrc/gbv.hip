@@ -1173,18 +1173,18 @@ const Tuning& tuning() { return g_tuning; }
 void tuning_load() {
   // the only setting taken from the environment: a debugging aid that changes timing, never results
   std::call_once(g_tuning_once, [] {
-    if (const char* e = getenv("GBV_SYNC_DEBUG")) g_tuning.sync_debug = (uint32_t)strtoul(e, nullptr, 10);
+    if (const char* e = getenv("GBV_SYNC_DEBUG")) g_tuning.sync_debug.store((uint32_t)strtoul(e, nullptr, 10));
   });
 }
 bool tuning_set(const char* name, uint32_t v) {
-  struct { const char* n; uint32_t* p; } tab[] = {
+  struct { const char* n; std::atomic<uint32_t>* p; } tab[] = {
       {"hash_pair_max", &g_tuning.hash_pair_max}, {"hash_quad_max", &g_tuning.hash_quad_max}, {"hash_coop_max", &g_tuning.hash_coop_max},
       {"prepare_split_max", &g_tuning.prepare_split_max}, {"chunk_finish_wave_max", &g_tuning.chunk_finish_wave_max},
       {"vs_pre_max", &g_tuning.vs_pre_max}, {"vs_fs_maxc", &g_tuning.vs_fs_maxc}, {"vs_quad_max", &g_tuning.vs_quad_max},
       {"vs_pair_max", &g_tuning.vs_pair_max}, {"agg_slice", &g_tuning.agg_slice}};
   for (auto& t : tab)
     if (!strcmp(name, t.n)) {
-      *t.p = v;
+      t.p->store(v, std::memory_order_relaxed);
       return true;
     }
   return false;

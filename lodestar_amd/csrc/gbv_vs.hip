@@ -73,6 +73,11 @@ struct gbv_vs_batch {
   hipEvent_t pre = nullptr;     // "pre" mode: k_vs_sig_pre_quad done (stream 5)
   bool in_flight = false;
   bool part_in_flight = false;  // gbv_vs_batch_partial_submit'ed, not yet waited
+  // a wait is reading this batch without the context lock: a second wait is refused, a fill / submit
+  // is refused (in flight), and a destroy is deferred to the end of the wait (free_pending)
+  bool waiting = false;
+  bool free_pending = false;
+  bool fs_small = false;  // this submit forms each chunk's (-g1, sum) Miller value beside the per-set ones
   int tail = 0;
   KProf prof;  // per-kernel events of the last submit / partial (ctx kprof_on)
 };
@@ -298,7 +303,7 @@ static bool vs_pre_on(const gbv_vs_batch* b) { return b->n <= tuning().vs_pre_ma
 // Small passes, and passes of few chunks (a range-sync segment of blocks: 2 chunks per block), whose
 // chunk checks are latency-bound: each chunk's (-g1, sum r_i sig_i) Miller value is formed beside the
 // per-set ones instead of inside the chunk check.
-static bool vs_fs_small(const gbv_vs_batch* b) { return b->n <= VS_COOP_MILLER_MAX || b->C <= tuning().vs_fs_maxc; }
+static bool vs_fs_small(const gbv_vs_batch* b) { return b->n <= VS_COOP_MILLER_MAX || b->C <= tuning().vs_fs_maxc.load(std::memory_order_relaxed); }
 
 // Per-set kernels: aggregate and hash + signature + randomisation on stream A, the Miller values on
 // stream m (a tail stream, so that they overlap the next batch's stream-A kernels; or stream A).
@@ -311,7 +316,7 @@ static int vs_enqueue_sets(gbv_ctx* c, gbv_vs_batch* b, hipStream_t m, bool with
   Seed seed = fresh_seed();
   uint32_t nonce = c->nonce++;
   // passes up to GBV_VS_PRE_MAX sets: the signature half first, on stream 5, beside the aggregation below
-  const bool small = with_fs && vs_fs_small(b);
+  const bool small = with_fs && b->fs_small;  // decided once per submit (vs_submit_enqueue): the chunk checks read the same
   const bool pre = (with_fs || partial) && m != s && vs_pre_on(b);
   if (pre) {
     HIP_CHECK(c, hipStreamWaitEvent(c->stream5, b->copied, 0));
@@ -383,6 +388,10 @@ int gbv_vs_batch_create(gbv_ctx* c, size_t n_calls, const uint32_t* call_off, co
 void gbv_vs_batch_destroy(gbv_ctx* c, gbv_vs_batch* b) {
   if (c) {
     GBV_LOCK(c);
+    if (b && b->waiting) {  // a wait is reading it: that wait frees it when it is done
+      b->free_pending = true;
+      return;
+    }
     vs_batch_free(b);
   } else {
     vs_batch_free(b);
@@ -398,11 +407,12 @@ int gbv_vs_batch_fill(gbv_ctx* c, gbv_vs_batch* b, size_t n_calls, const uint32_
 
 static int vs_submit_enqueue(gbv_ctx* c, gbv_vs_batch* b) {
   KProfScope kp(c->kprof_on ? &b->prof : nullptr);
+  b->fs_small = vs_fs_small(b);  // one read of the setting for both the Miller stage and the chunk checks
   b->tail = (int)(c->sm_submits++ & 1);
   hipStream_t t = b->tail ? c->stream4 : c->stream2;
   int rc = vs_enqueue_sets(c, b, t, true);
   if (rc) return rc;
-  const bool fs = vs_fs_small(b);
+  const bool fs = b->fs_small;
   launch_vs_chunk_coop(LaunchCfg{(unsigned)b->C, 64, t}, (uint32_t)b->C, b->chunk_off, b->status, b->F, b->rS, b->chunk_valid,
                        fs ? b->Fs : nullptr, b->fs_flag);
   HIP_CHECK(c, hipEventRecord(b->ev[5], t));
@@ -415,8 +425,8 @@ static int vs_submit_enqueue(gbv_ctx* c, gbv_vs_batch* b) {
 // Enqueue the whole verification without a host round trip: the per-set kernels on stream A, the
 // Miller values and chunk checks on a tail stream, alternating per submit between stream 2 and the
 // hash stream (idle in this path), so that consecutive batches' tails overlap each other and the
-// next batch's per-set kernels; small passes add stream 5 for the signature half (four live streams,
-// one per hardware queue: GPU_MAX_HW_QUEUES=4).
+// next batch's per-set kernels; small passes add stream 5 for the signature half (four busy streams
+// at most over the GPU_MAX_HW_QUEUES=4 hardware queues; ctx.h).
 int gbv_vs_batch_submit(gbv_ctx* c, gbv_vs_batch* b) {
   if (!c || !b) return GBV_E_ARG;
   GBV_LOCK(c);
@@ -436,11 +446,21 @@ int gbv_vs_batch_wait(gbv_ctx* c, gbv_vs_batch* b, uint8_t* call_valid) {
   bool flying;
   {
     GBV_LOCK(c);
+    if (b->waiting) return gbv_fail(c, GBV_E_ARG, "batch already being waited on");
     flying = b->in_flight;
+    b->waiting = flying;
   }
-  // the device wait runs without the context lock; the batch belongs to this caller
+  // the device wait runs without the context lock; in_flight stays set (fill / submit refuse the batch)
+  // and a destroy meanwhile is deferred to the end of this call
   hipError_t we = flying ? hipEventSynchronize(b->done) : hipSuccess;
   GBV_LOCK(c);
+  struct FreeIfPending {  // runs last, after the results below are read
+    gbv_vs_batch* b;
+    ~FreeIfPending() {
+      b->waiting = false;
+      if (b->free_pending) vs_batch_free(b);
+    }
+  } fin{b};
   if (flying) {
     b->in_flight = false;
     if (we != hipSuccess) return gbv_fail(c, GBV_E_DEVICE, std::string("hipEventSynchronize: ") + hipGetErrorString(we));
@@ -566,10 +586,18 @@ int gbv_vs_batch_partial_wait(gbv_ctx* c, gbv_vs_batch* b, uint8_t out576[GBV_FP
   {
     GBV_LOCK(c);
     if (!b->part_in_flight) return gbv_fail(c, GBV_E_ARG, "partial not submitted");
-    b->part_in_flight = false;  // the batch belongs to this caller: collected below without the lock
+    if (b->waiting) return gbv_fail(c, GBV_E_ARG, "partial already being waited on");
+    // collected below without the lock: part_in_flight stays set until then (fill / submit refuse the
+    // batch, so part_host is neither regrown nor refilled) and a destroy is deferred to the end
+    b->waiting = true;
   }
   *shard_ok = 1;
-  return vs_partial_collect(c, b, out576, shard_ok);
+  const int rc = vs_partial_collect(c, b, out576, shard_ok);
+  GBV_LOCK(c);
+  b->part_in_flight = false;
+  b->waiting = false;
+  if (b->free_pending) vs_batch_free(b);
+  return rc;
 }
 
 int gbv_vs_batch_partial(gbv_ctx* c, gbv_vs_batch* b, uint8_t out576[GBV_FP12_PARTIAL_BYTES], uint8_t* shard_ok) {

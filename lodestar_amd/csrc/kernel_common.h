@@ -21,6 +21,7 @@
 //                       (maybeBatch.ts:17-26)
 //   k_fp12_check        product of per-GPU Miller partials + one final exponentiation (multi-GPU)
 #pragma once
+#include <atomic>
 #include "hash_to_curve.h"
 #include "pairing.h"
 
@@ -76,18 +77,18 @@ constexpr uint32_t HASH_PAIR_MAX = 4096;
 // DESIGN.md section 7; experiments change them through gbv_tune (tuning_set, by the names below), never
 // through a beacon node's environment.  Only GBV_SYNC_DEBUG is read from the environment (tuning_load,
 // first gbv_init): it synchronises after every launch, which changes timing, not results.
-struct Tuning {
-  uint32_t hash_pair_max = HASH_PAIR_MAX;  // hash on lane pairs up to this many messages
-  uint32_t hash_quad_max = 16384;          // hash on lane quads up to this many messages
-  uint32_t hash_coop_max = 128;            // latency form, cofactor clearing one workgroup per message (two waves each: past ~128 messages they crowd the signature work beside them)
-  uint32_t prepare_split_max = 2048;       // same-message latency prepare up to this many sets
-  uint32_t chunk_finish_wave_max = 32;     // chunk sums one wave per chunk up to this many
-  uint32_t vs_pre_max = 16384;             // verifySignatureSets signature half (lane quads) beside the aggregation
-  uint32_t vs_fs_maxc = 256;               // per-chunk (-g1, sum) Miller value beside the per-set ones
-  uint32_t vs_quad_max = 16384;            // per-set Miller values on lane quads up to this many sets
-  uint32_t vs_pair_max = 32768;            // ... on lane pairs up to this many (one lane per set above)
-  uint32_t agg_slice = 8192;               // large aggregates: members per k_vs_agg_big workgroup (256 threads; profiles/r05l)
-  uint32_t sync_debug = 0;                 // GBV_SYNC_DEBUG: synchronise + report after every launch (debugging)
+struct Tuning {  // relaxed atomics: gbv_tune may run beside another context's enqueue
+  std::atomic<uint32_t> hash_pair_max{HASH_PAIR_MAX};  // hash on lane pairs up to this many messages
+  std::atomic<uint32_t> hash_quad_max{16384};          // hash on lane quads up to this many messages
+  std::atomic<uint32_t> hash_coop_max{128};            // latency form, cofactor clearing one workgroup per message (two waves each: past ~128 messages they crowd the signature work beside them)
+  std::atomic<uint32_t> prepare_split_max{2048};       // same-message latency prepare up to this many sets
+  std::atomic<uint32_t> chunk_finish_wave_max{32};     // chunk sums one wave per chunk up to this many
+  std::atomic<uint32_t> vs_pre_max{16384};             // verifySignatureSets signature half (lane quads) beside the aggregation
+  std::atomic<uint32_t> vs_fs_maxc{256};               // per-chunk (-g1, sum) Miller value beside the per-set ones
+  std::atomic<uint32_t> vs_quad_max{16384};            // per-set Miller values on lane quads up to this many sets
+  std::atomic<uint32_t> vs_pair_max{32768};            // ... on lane pairs up to this many (one lane per set above)
+  std::atomic<uint32_t> agg_slice{8192};               // large aggregates: members per k_vs_agg_big workgroup (256 threads; profiles/r05l)
+  std::atomic<uint32_t> sync_debug{0};                 // GBV_SYNC_DEBUG: synchronise + report after every launch (debugging)
 };
 const Tuning& tuning();
 void tuning_load();

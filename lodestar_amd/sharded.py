@@ -37,7 +37,11 @@ def set_weight(s) -> int:
 
 
 def balanced_ranges(weights: Sequence[int], parts: int) -> List[Tuple[int, int]]:
-    """Contiguous [lo, hi) ranges, one per part, with near-equal total weight (every set once)."""
+    """Contiguous [lo, hi) ranges, one per part, with near-equal total weight (every set once).
+    Part p ends where the running sum is closest to p+1 parts' share of the total: the next item is
+    taken when that overshoots the share by no more than leaving it undershoots -- so an item larger
+    than a share still starts on the first rank that reaches it instead of piling every later item on
+    the last rank.  Ranges are empty only when there are fewer items than parts."""
     n = len(weights)
     total = sum(weights)
     out, lo, acc = [], 0, 0
@@ -47,7 +51,7 @@ def balanced_ranges(weights: Sequence[int], parts: int) -> List[Tuple[int, int]]
             break
         target = total * (p + 1) / parts
         hi = lo
-        while hi < n and acc + weights[hi] <= target:
+        while hi < n and acc + weights[hi] - target <= target - acc:
             acc += weights[hi]
             hi += 1
         out.append((lo, hi))
@@ -164,13 +168,15 @@ class ShardedVerifier:
             submit(k + depth)  # before the exchange: the next pass overlaps it
             try:
                 out.append(self._exchange(part, status))
-            except Exception:
+            except Exception as ex:
                 for j in range(k + 1, n):  # drain what this rank still has in flight
                     if submitted[j]:
                         try:
                             staged[j].partial_wait()
                         except Exception:  # noqa: BLE001
                             pass
+                if failed is not None:  # this rank's own error is the cause of the collective's
+                    raise failed from ex
                 raise
         if failed is not None:
             raise failed

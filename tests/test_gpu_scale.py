@@ -44,7 +44,7 @@ def test_comb_tables_match_ladder(world):
     checked against the oracle."""
     v, sks, pks = world
     if not v.comb_enabled():
-        pytest.skip("comb tables disabled (GBV_COMB=0)")
+        pytest.skip("comb tables disabled (gbv_tune comb 0)")
     rng = np.random.Generator(np.random.PCG64(77))
     slots = [0, 1, N_KEYS - 1, N_KEYS, N_KEYS + 1, N_TABLE - 1] + [int(x) for x in rng.integers(0, N_TABLE, size=250)]
     r64 = [0, 2**64 - 1, 0x0123456789ABCDEF, 1 << 63, 0xFFFFFFFF, 1 << 32] + [int(x) for x in rng.integers(0, 2**63, size=250)]

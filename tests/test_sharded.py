@@ -194,6 +194,10 @@ def test_balanced_ranges_cover_and_balance():
         r = balanced_ranges(w, parts)
         assert len(r) == parts and r[0][0] == 0 and r[-1][1] == len(w)
         assert all(r[i][1] == r[i + 1][0] for i in range(parts - 1))
+    # one call larger than a rank's share starts on the first rank, not piled onto the last one
+    assert balanced_ranges([200, 50, 50], 2) == [(0, 1), (1, 3)]
+    assert balanced_ranges([50, 50, 200], 2) == [(0, 2), (2, 3)]
+    assert sum(b - a for a, b in balanced_ranges([128] * 3, 8)) == 3  # fewer calls than ranks: some ranges empty
 
 
 def test_sharded_world2_gloo():
@@ -228,3 +232,109 @@ def test_sharded_world2_gloo():
         sets = _sets(sks, bad)
         d = [dict(t, msg=bytes(s.signing_root), sig=bytes(s.signature)) for t, s in zip(table_sets(sets), sets)]
         assert O.pool_verify_signature_sets(d) is want
+
+
+# ---- world sizes 4 and 8 (the driver's 8-GPU node has one rank per GPU) ---------------------------
+def _presigned():
+    """Signatures made once in the parent (oracle signing is slow): the _sets() call, its wrong-message
+    variant, and four same-message signatures."""
+    sks, pks = _keys()
+    msgs = [bytes([i + 1]) * 32 for i in range(5)]
+    sig = {i: O.g2_compress(O.sign(sks[i], msgs[i])) for i in range(3)}
+    sig["agg"] = O.g2_compress(O.sign((sks[3] + sks[4]) % O.R, msgs[3]))
+    sig[5] = O.g2_compress(O.sign(sks[5], msgs[4]))
+    sig["wrong"] = O.g2_compress(O.sign(sks[5], msgs[0]))
+    msg = bytes([7]) * 32
+    sm = [O.g2_compress(O.sign(sks[i], msg)) for i in range(4)]
+    return {"pks": pks, "msgs": msgs, "sig": sig, "sm_msg": msg, "sm": sm}
+
+
+def _call(d, bad=None):
+    m, sig = d["msgs"], d["sig"]
+    sets = [SingleSignatureSet(i, m[i], sig[i]) for i in range(3)]
+    sets.append(AggregatedSignatureSet([3, 4], m[3], sig["agg"]))
+    sets.append(SingleSignatureSet(5, m[4], sig["wrong"] if bad == "wrong_last" else sig[5]))
+    if bad == "malformed_last":
+        sets[4] = SingleSignatureSet(5, m[4], bytes([10]) * 96)
+    return sets
+
+
+def _world_n_worker(rank, world, port, q, d):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from lodestar_amd import GbvError
+        from lodestar_amd.sharded import ShardedVerifier
+        sv = ShardedVerifier(OracleDevice(d["pks"]))
+        res = {"shard": sv.shard_of(_call(d))}
+        # streamed staged shards, two in flight: 5 sets over `world` ranks leave some shards empty; the
+        # bad set of the second and third calls sits in the last non-empty shard
+        stream = []
+        for bad in (None, "wrong_last", "malformed_last"):
+            call = _call(d, bad)
+            lo, hi = sv.shard_of(call)
+            stream.append(OracleStaged(sv.device, call[lo:hi]))
+        res["streamed"] = sv.verify_staged_shards(stream, depth=2)
+        res["left"] = sv.device.in_flight
+        # fewer same-message calls than ranks: ranks without calls still join the gather
+        msg, sm = d["sm_msg"], d["sm"]
+        calls = [([(0, sm[0]), (1, sm[1])], msg), ([(2, sm[2]), (3, bytes([10]) * 96)], msg), ([(0, sm[1])], msg)]
+        res["sm_ranges"] = sv.call_ranges([len(c[0]) for c in calls])
+        res["sm"] = sv.verify_same_message_multi(calls)
+
+        # a device error on the LAST rank during a streamed pass: every rank raises (none blocks in the
+        # all-gather), the failing rank with its own error
+        class FailingStaged(OracleStaged):
+            def partial_wait(self):
+                super().partial_wait()
+                raise GbvError(-5, "device fault on rank %d" % rank)
+        err_stream = []
+        for k in range(3):
+            call = _call(d)
+            lo, hi = sv.shard_of(call)
+            cls = FailingStaged if (rank == world - 1 and k == 1) else OracleStaged
+            err_stream.append(cls(sv.device, call[lo:hi]))
+        try:
+            sv.verify_staged_shards(err_stream, depth=2)
+            res["err"] = "no error"
+        except GbvError as e:
+            res["err"] = str(e)
+        res["err_left"] = sv.device.in_flight
+        q.put((rank, res))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [4, 8])
+def test_sharded_world_n_gloo(world):
+    """verify_staged_shards and verify_same_message_multi at 4 and 8 ranks (gloo): uneven and empty
+    shards, fewer calls than ranks, a bad set in the last shard, a device error on one rank."""
+    d = _presigned()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_world_n_worker, args=(r, world, port, q, d)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=900) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    shards = [out[r]["shard"] for r in range(world)]
+    assert shards[0][0] == 0 and shards[-1][1] == 5 and all(shards[r][1] == shards[r + 1][0] for r in range(world - 1))
+    if world == 8:
+        assert any(lo == hi for lo, hi in shards)  # empty shards take part with the Fp12 one
+    sm_ranges = out[0]["sm_ranges"]
+    assert sum(1 for a, b in sm_ranges if b > a) <= 3 and sm_ranges[-1][1] == 3
+    for r in range(world):
+        x = out[r]
+        assert x["streamed"] == [True, False, False] and x["left"] == 0
+        assert x["sm"] == [[True, True], [True, False], [False]]
+        assert x["sm_ranges"] == sm_ranges
+        assert x["err_left"] == 0
+        if r == world - 1:
+            assert x["err"].endswith("device fault on rank %d" % r), x["err"]
+        else:
+            assert x["err"].endswith("device error on a peer rank"), x["err"]
