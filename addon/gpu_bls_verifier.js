@@ -30,6 +30,9 @@ const MAX_JOBS_CAN_ACCEPT_WORK = 512; // multithread/index.ts:79
 // of gossip calls then becomes several passes, so the addon's marshalling of pass k + 1 and the
 // resolution of pass k - 1 run while pass k is on the device.
 const MAX_PASS_SETS = 1 << 18;
+// index2pubkey position of a registered key object, kept on the object itself (a symbol-keyed property,
+// invisible to other code): one monomorphic property load per set instead of a WeakMap lookup
+const KEY_INDEX = Symbol("gbv.validatorIndex");
 
 /** chunkifyMaximizeChunkSize (multithread/utils.ts:4-18) */
 function chunkifyMaximizeChunkSize(arr, minPerChunk) {
@@ -242,13 +245,26 @@ class GpuBlsVerifier {
   registerPubkeyObjects(firstIndex, keys) {
     for (let k = 0; k < keys.length; ++k) {
       const o = keys[k];
-      if (o !== null && typeof o === "object") this.keyIndex.set(o, firstIndex + k);
+      if (o === null || typeof o !== "object") continue;
+      if (Object.isExtensible(o)) o[KEY_INDEX] = firstIndex + k;
+      else this.keyIndex.set(o, firstIndex + k); // a frozen / sealed key object: by identity in the map
     }
   }
 
   /** validator index of a key object of index2pubkey, or undefined for a key outside the table */
   indexOf(publicKey) {
-    return publicKey !== null && typeof publicKey === "object" ? this.keyIndex.get(publicKey) : undefined;
+    if (publicKey === null || typeof publicKey !== "object") return undefined;
+    const k = publicKey[KEY_INDEX];
+    return k !== undefined ? k : this.keyIndex.get(publicKey);
+  }
+
+  /** a same-message set's validator index: its `index`, else its key object's */
+  _setIndex(s) {
+    if (s.index !== undefined) return s.index;
+    const pk = s.publicKey;
+    if (pk === null || typeof pk !== "object") return undefined;
+    const k = pk[KEY_INDEX];
+    return k !== undefined ? k : this.keyIndex.get(pk);
   }
 
   /** the indices of a list of key objects, or undefined when any is outside the table */
@@ -336,40 +352,31 @@ class GpuBlsVerifier {
     const n = packed ? sets.indices.length : sets.length;
     const nKeys = n ? this.addon.pubkeyCount(this.ctx) : 0;
     const badIndex = () => Object.assign(new RangeError("validator index out of range"), {code: "GBV_E_ARG"});
-    let ix = null; // object form: every set's validator index
     let outside = null; // object form: the positions of sets whose key is not in index2pubkey
     if (packed) {
       const pi = sets.indices;
       for (let i = 0; i < n; ++i) if (pi[i] >= nKeys) throw badIndex();
     } else {
-      ix = new Uint32Array(n);
       for (let i = 0; i < n; ++i) {
-        const s = sets[i];
-        let k = s.index;
-        if (k === undefined) {
-          k = this.keyIndex.get(s.publicKey);
-          if (k === undefined) {
-            (outside || (outside = [])).push(i);
-            continue;
-          }
-        }
-        if (!(k >= 0 && k < nKeys)) throw badIndex();
-        ix[i] = k;
+        const k = this._setIndex(sets[i]); // resolved again when the pass is packed (_packSameMessage)
+        if (k === undefined) (outside || (outside = [])).push(i);
+        else if (!(k >= 0 && k < nKeys)) throw badIndex();
       }
-      if (outside) return this._sameMessageOutsideKeys(sets, ix, outside, message, opts);
+      if (outside) return this._sameMessageOutsideKeys(sets, outside, message, opts);
     }
-    const job = (chunk, cix) =>
-      new Promise((resolve, reject) => this._queue({type: "sameMessage", resolve, reject, addedTimeMs: Date.now(), opts, sets: chunk, ix: cix, message}));
     if (n < 2 * MAX_SIGNATURE_SETS_PER_JOB) {
       // one chunk (every gossip call): its job's promise is the call's (no Promise.all, no concat)
-      return job(packed ? {indices: sets.indices, signatures: sets.signatures, length: n} : sets, ix);
+      const chunk = packed ? {indices: sets.indices, signatures: sets.signatures, length: n} : sets;
+      return new Promise((resolve, reject) => this._queue({type: "sameMessage", resolve, reject, addedTimeMs: Date.now(), opts, sets: chunk, message}));
     }
+    const chunks = packed
+      ? chunkRanges(n, MAX_SIGNATURE_SETS_PER_JOB).map(([a, b]) => ({indices: sets.indices.subarray(a, b),
+        signatures: sigList ? sets.signatures.slice(a, b) : sets.signatures.subarray(96 * a, 96 * b), length: b - a}))
+      : chunkifyMaximizeChunkSize(sets, MAX_SIGNATURE_SETS_PER_JOB);
     const results = await Promise.all(
-      chunkRanges(n, MAX_SIGNATURE_SETS_PER_JOB).map(([a, b]) =>
-        packed
-          ? job({indices: sets.indices.subarray(a, b),
-            signatures: sigList ? sets.signatures.slice(a, b) : sets.signatures.subarray(96 * a, 96 * b), length: b - a}, null)
-          : job(sets.slice(a, b), ix.subarray(a, b))
+      chunks.map(
+        (chunk) =>
+          new Promise((resolve, reject) => this._queue({type: "sameMessage", resolve, reject, addedTimeMs: Date.now(), opts, sets: chunk, message}))
       )
     );
     if (!packed) return [].concat(...results);
@@ -386,7 +393,7 @@ class GpuBlsVerifier {
   /** A same-message call holding keys outside index2pubkey: the sets with table keys go to the device as
    * one same-message job, every other set as a one-set verifySignatureSets job over its key bytes; the
    * booleans come back in call order. */
-  async _sameMessageOutsideKeys(sets, ix, outside, message, opts) {
+  async _sameMessageOutsideKeys(sets, outside, message, opts) {
     const n = sets.length;
     const isOut = new Uint8Array(n);
     for (const i of outside) isOut[i] = 1;
@@ -400,7 +407,7 @@ class GpuBlsVerifier {
       return {pubkey: bytes, signingRoot: message, signature: sets[i].signature};
     });
     const pIn = inside.length
-      ? this.verifySignatureSetsSameMessage(inside.map((i) => ({index: ix[i], signature: sets[i].signature})), message, opts)
+      ? this.verifySignatureSetsSameMessage(inside.map((i) => ({index: this._setIndex(sets[i]), signature: sets[i].signature})), message, opts)
       : Promise.resolve([]);
     const pOut = loose.map((s) => new Promise((resolve, reject) => this._queue({type: "default", resolve, reject, addedTimeMs: Date.now(), opts, sets: [s]})));
     const [rIn, rOut] = await Promise.all([pIn, Promise.all(pOut)]);
@@ -507,9 +514,9 @@ class GpuBlsVerifier {
       messages.set(j.message, 32 * c);
       j.off = o;
       if (Array.isArray(s)) {
-        indices.set(j.ix, o); // resolved when the call was validated
         for (let i = 0; i < n; ++i) {
-          const g = s[i].signature;
+          const e = s[i], g = e.signature;
+          indices[o + i] = this._setIndex(e); // in the table: checked when the call was validated
           if (g.length === 96) signatures.set(g, 96 * (o + i));
         }
       } else {
