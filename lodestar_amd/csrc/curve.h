@@ -333,9 +333,17 @@ GBV_HD G2J g2_psi_jac(const G2J& a) {
   return G2J{fp2_mul(fp2_conj(a.x), PSI_X), fp2_mul(fp2_conj(a.y), PSI_Y), fp2_conj(a.z)};
 }
 
-// G2 membership (Scott 2021): psi(Q) == [x] Q = -[|x|] Q.  Q affine, not infinity.
+}  // namespace gbv
+#include "g2_lazy.h"
+namespace gbv {
+
+// G2 membership (Scott 2021): psi(Q) == [x] Q = -[|x|] Q.  Q affine, not infinity.  [|x|] Q on the
+// signed lazy 28-bit form (g2_lazy.h; the canonical chain g2_mul_xabs gives the same point).
+#ifndef GBV_G2_LAZY
+#define GBV_G2_LAZY 1  // 0: the canonical chain (A/B builds only, tools/build_variant.sh)
+#endif
 GBV_NI bool g2_in_subgroup(G2A q) {
-  G2J xq = jac_neg(g2_mul_xabs(q));
+  G2J xq = jac_neg(GBV_G2_LAZY ? g2_mul_xabs_lazy(q) : g2_mul_xabs(q));
   return jac_eq_aff(xq, g2_psi(q));
 }
 

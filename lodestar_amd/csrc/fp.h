@@ -243,6 +243,28 @@ GBV_HD Fp fp_from28(const F28& z) {  // z < 2^384, limbs < 2^28
   return r;
 }
 
+// Column carry of the product scans: s >> 28 (arithmetic; unsigned columns stay below 2^63).  The 64-bit
+// shift issues at half the rate of v_mad_u64_u32 in isolation (tools/ubench_int2.hip: 19.3 vs 36.6 T
+// lane-ops/s), but inside the product it is on the carry chain beside the column's mads, and the
+// two-instruction form (v_alignbit_b32 + v_ashrrev_i32, GBV_SAR28=1) measured slower there.
+// (The halves go through an ext_vector bit cast: rebuilt with shifts and ors, the backend adds a zero
+// move and two 64-bit adds per column.)
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+#ifndef GBV_SAR28
+#define GBV_SAR28 0  // 1: the two 32-bit ops below -- measured SLOWER than the 64-bit shift in the product
+#endif              // (tools/ubench_prod.hip, profiles/r06f: mul28s 68.8 -> 66.0 G/s at 2 waves per SIMD)
+GBV_HD int64_t sar28(int64_t s) {
+#if defined(__HIP_DEVICE_COMPILE__) && GBV_SAR28
+  const u32x2 w = __builtin_bit_cast(u32x2, s);
+  u32x2 r;
+  r.x = __builtin_amdgcn_alignbit(w.y, w.x, 28);
+  r.y = (uint32_t)((int32_t)w.y >> 28);
+  return __builtin_bit_cast(int64_t, r);
+#else
+  return s >> 28;
+#endif
+}
+
 #if defined(GBV_HOST_TEST)
 // Host build only (tests/native/hosttest.cpp): every Fp product is counted, so the algorithmic work
 // per signature set that bench.py's roofline uses is measured on the code, not estimated.
@@ -278,7 +300,7 @@ GBV_HD F28 mul28_inl(const F28& a, const F28& b) {
     } else {
       r[k - 14] = (uint32_t)s & M28;
     }
-    acc = s >> 28;
+    acc = (uint64_t)sar28((int64_t)s);
   }
   r[13] = (uint32_t)acc;
   F28 o;
@@ -318,7 +340,7 @@ GBV_HD F28 sqr28_inl(const F28& a) {
     } else {
       r[k - 14] = (uint32_t)s & M28;
     }
-    acc = s >> 28;
+    acc = (uint64_t)sar28((int64_t)s);
   }
   r[13] = (uint32_t)acc;
   F28 o;

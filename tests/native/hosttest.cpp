@@ -57,6 +57,77 @@ int ht_g2_in_subgroup(const uint8_t* xy) {
   G2A a{load_fp2(xy), load_fp2(xy + 96)};
   return g2_in_subgroup(a);
 }
+// The lazy G2 chain (g2_lazy.h) against the canonical one: [|x|] Q both ways, coordinates compared
+// exactly (the same formulas mod p).  Returns 1 when equal; *max_col_bits: widest product column seen.
+int ht_g2_mul_xabs_lazy_cmp(const uint8_t* xy, long long* max_col_bits) {
+  G2A a{load_fp2(xy), load_fp2(xy + 96)};
+  g_s28_max_col_bits = 0;
+  const G2J lazy = g2_mul_xabs_lazy(a);
+  const G2J ref = jac_mul_xabs(a);
+  *max_col_bits = g_s28_max_col_bits;
+  return fp2_eq(lazy.x, ref.x) && fp2_eq(lazy.y, ref.y) && fp2_eq(lazy.z, ref.z);
+}
+// One lazy doubling from adversarial limbs: x, y, z with low limbs drawn from {-8, 2^28 + 7, random in
+// range} (mode bits select the extremes) and top limbs up to +-31 p's top limb (values below 32 p),
+// checked against jac_dbl of their canonical values.  The host build aborts on any bound violation.
+int ht_s2j_dbl_extreme(uint64_t seed, int mode, long long* max_col_bits) {
+  uint64_t st = seed * 0x9E3779B97F4A7C15ull + 1;
+  auto rnd = [&]() { st ^= st << 13; st ^= st >> 7; st ^= st << 17; return st; };
+  auto limb_of = [&](int i) -> int32_t {
+    const int m = (mode >> (i % 3)) & 3;
+    if (m == 1) return 268435456 + 7;
+    if (m == 2) return -8;
+    return (int32_t)(rnd() % (268435456ull + 16)) - 8;
+  };
+  S2J p;
+  S28* f[6] = {&p.x.c0, &p.x.c1, &p.y.c0, &p.y.c1, &p.z.c0, &p.z.c1};
+  for (int k = 0; k < 6; ++k) {
+    for (int i = 0; i < 13; ++i) f[k]->v[i] = limb_of(i + k);
+    const int32_t top = (int32_t)(rnd() % (2u * 60u * P28[13])) - (int32_t)(60u * P28[13]);
+    f[k]->v[13] = top;
+  }
+  g_s28_max_col_bits = 0;
+  S2J r = p;
+  G2J want;
+  if (mode & 64) {  // the mixed addition of q = 2^k G (canonical, affine) instead of the doubling
+    uint32_t w[8] = {(uint32_t)seed, (uint32_t)mode, 1, 2, 3, 4, 5, 6};
+    const G2A q = hash_to_g2(w);
+    const S2 qs[2] = {s2_from(q.x), s2_from(q.y)};
+    s2j_madd(&r, qs);
+    want = jac_add_aff(s2j_to(p), q);
+  } else {
+    r = s2j_dbl(p);
+    want = jac_dbl(s2j_to(p));
+  }
+  *max_col_bits = g_s28_max_col_bits;
+  const G2J got = s2j_to(r);
+  // the outputs stay normalized (limbs 0..12 in [-8, 2^28 + 8)) for the next doubling
+  const S28* g[6] = {&r.x.c0, &r.x.c1, &r.y.c0, &r.y.c1, &r.z.c0, &r.z.c1};
+  bool norm = true;
+  for (int k = 0; k < 6; ++k)
+    for (int i = 0; i < 13; ++i) norm = norm && g[k]->v[i] >= -8 && g[k]->v[i] < 268435456 + 8;
+  return norm && fp2_eq(got.x, want.x) && fp2_eq(got.y, want.y) && fp2_eq(got.z, want.z);
+}
+// The lazy mixed addition at its exceptional inputs *r = q and *r = -q (Jacobian, scaled by a random
+// lambda): the formula leaves Z = 0 mod p (which g2_mul_xabs_lazy turns into a canonical recomputation),
+// and a doubling of such a point keeps Z = 0 mod p.  Returns 1 when both hold for both inputs.
+int ht_s2j_madd_exceptional(uint64_t seed) {
+  uint32_t w[8] = {(uint32_t)seed, 7, 7, 7, 7, 7, 7, 7};
+  const G2A q = hash_to_g2(w);
+  const S2 qs[2] = {s2_from(q.x), s2_from(q.y)};
+  Fp2 lam{fp_to_mont(Fp{{(uint32_t)seed | 1u, 3, 5, 7, 11, 13, 17, 19, 23, 29, 31, 1}}), FP_ONE};
+  int ok = 1;
+  for (int neg = 0; neg < 2; ++neg) {
+    const Fp2 l2 = fp2_sqr(lam);
+    G2J p{fp2_mul(q.x, l2), fp2_mul(neg ? fp2_neg(q.y) : q.y, fp2_mul(l2, lam)), lam};
+    S2J s = s2j_from(p);
+    s2j_madd(&s, qs);
+    ok &= fp2_is_zero(s2j_to(s).z);
+    s2j_dbl_n(&s, 3);
+    ok &= fp2_is_zero(s2j_to(s).z);
+  }
+  return ok;
+}
 int ht_g1_decompress(uint8_t* out, const uint8_t* in) {
   G1A a;
   uint8_t st = g1_decompress(a, in);

@@ -435,3 +435,48 @@ def test_locate_one_invalid_set(lib, case):
         assert got == bad[0]
     else:
         assert got == 0xFFFFFFFF
+
+
+def test_g2_lazy_chain_matches_canonical(lib):
+    """g2_lazy.h: [|x|] Q on signed lazy 28-bit limbs (the subgroup check's 63 doublings) equals the
+    canonical chain coordinate for coordinate, for subgroup points, the generator, and points outside
+    the subgroup (random curve points); every product column and limb op is range-checked by the host
+    build (an out-of-range intermediate aborts)."""
+    rng = random.Random(61)
+    pts = [o.G2_GEN] + [o.g2_mul(o.G2_GEN, rng.getrandbits(255)) for _ in range(3)]
+    pts += [o.hash_to_g2(bytes([i]) * 32) for i in range(2)]
+    # points on the curve outside G2 (no cofactor clearing)
+    while len(pts) < 9:
+        x = (rng.getrandbits(380), rng.getrandbits(380))
+        y2 = o.f2_add(o.f2_mul(o.f2_sqr(x), x), o.B2)
+        if not o.f2_is_square(y2):
+            continue
+        pts.append((x, o.f2_sqrt(y2)))
+    widest = 0
+    for pt in pts:
+        col = ctypes.c_longlong(0)
+        assert lib.ht_g2_mul_xabs_lazy_cmp(fp2b(pt[0]) + fp2b(pt[1]), ctypes.byref(col)) == 1
+        widest = max(widest, col.value)
+    assert 55 <= widest <= 63
+
+
+def test_g2_lazy_doubling_at_limb_extremes(lib):
+    """One lazy doubling (or mixed addition) from adversarial normalized inputs: low limbs at -8 /
+    2^28 + 7 / random, top limbs up to +-60 p's (values below 64 p): no intermediate leaves int32 limbs
+    or int64 product columns (the host build aborts otherwise), the outputs are normalized again, and
+    the point equals the canonical jac_dbl / jac_add_aff of the inputs."""
+    worst = 0
+    for mode in range(128):  # bit 6: the lazy mixed addition instead of the doubling
+        for seed in range(4):
+            col = ctypes.c_longlong(0)
+            assert lib.ht_s2j_dbl_extreme(ctypes.c_uint64(1000 * mode + seed), mode, ctypes.byref(col)) == 1, (mode, seed)
+            worst = max(worst, col.value)
+    assert worst <= 63
+
+
+def test_g2_lazy_addition_exceptional_inputs_leave_z_zero(lib):
+    """s2j_madd at *r = q and *r = -q: Z = 0 mod p afterwards and after further doublings, which is how
+    g2_mul_xabs_lazy detects the case and recomputes [|x|] Q on the canonical form (jac_add_aff's
+    doubling / infinity branches)."""
+    for seed in range(4):
+        assert lib.ht_s2j_madd_exceptional(ctypes.c_uint64(seed)) == 1
