@@ -455,8 +455,9 @@ unsigned long long ht_count_miller_1j(const uint8_t* p96, const uint8_t* q192) {
 // 36 of ~109 FME), then each pair's doubling / addition line.  The product equals the product of the
 // k single-pair values (same lines, same Z^3 factors), so a chunk check multiplying Miller values
 // sees the same Fp12.
+}  // extern "C"
+template <int K = 4>
 static void miller_loop_kj_to(Fp12* out, const G1J* P, const G2A* Q, int k) {
-  constexpr int K = 4;
   Fp z3[K], nxz[K];
   G2Proj T[K];
 #pragma unroll
@@ -492,6 +493,7 @@ static void miller_loop_kj_to(Fp12* out, const G1J* P, const G2A* Q, int k) {
   }
   fp12_conj_to(out, &f);
 }
+extern "C" {
 
 // The shared-accumulator loop against the product of per-pair Miller values: P_j =
 // 2 (p_j) (Jacobian, Z != 1), Q_j affine; mode 0 = product of miller_loop_1j, 1 and 2 = miller_loop_kj_to
@@ -512,13 +514,41 @@ unsigned long long ht_miller_group(uint8_t* out, const uint8_t* p96, const uint8
       f = fp12_mul(f, g);
     }
   } else if (mode == 1) {
-    miller_loop_kj_to(&f, P, Q, k);
+    miller_loop_kj_to<4>(&f, P, Q, k);
   } else {
-    miller_loop_kj_to(&f, P, Q, k);
+    miller_loop_kj_to<4>(&f, P, Q, k);
   }
   const Fp2* c[6] = {&f.c0.c0, &f.c0.c1, &f.c0.c2, &f.c1.c0, &f.c1.c1, &f.c1.c2};
   for (int i = 0; i < 6; ++i) store_fp2(out + 96 * i, *c[i]);
   return g_fme_count;
+}
+// A call of n sets as round 5's k_vs_miller_group<K> cut it: groups of K consecutive sets, the last one
+// ragged (n mod K sets), each group's product on one shared accumulator; against the product of the n
+// per-set values (miller_loop_1j).  P_j = 2 p_j (Jacobian, Z != 1).  Writes both Fp12 (576 bytes each).
+void ht_miller_call_groups(uint8_t* want, uint8_t* got, const uint8_t* p96, const uint8_t* q192, int n, int K) {
+  std::vector<G1J> P(n);
+  std::vector<G2A> Q(n);
+  for (int j = 0; j < n; ++j) {
+    P[j] = jac_dbl(jac_from_aff(G1A{load_mont(p96 + 96 * j), load_mont(p96 + 96 * j + 48)}));
+    Q[j] = G2A{load_fp2(q192 + 192 * j), load_fp2(q192 + 192 * j + 96)};
+  }
+  Fp12 a = fp12_one(), b = fp12_one();
+  for (int j = 0; j < n; ++j) a = fp12_mul(a, miller_loop_1j(P[j], Q[j]));
+  for (int j = 0; j < n; j += K) {
+    const int k = n - j < K ? n - j : K;
+    Fp12 g;
+    if (K == 2)
+      miller_loop_kj_to<2>(&g, &P[j], &Q[j], k);
+    else
+      miller_loop_kj_to<4>(&g, &P[j], &Q[j], k);
+    b = fp12_mul(b, g);
+  }
+  const Fp12* f[2] = {&a, &b};
+  uint8_t* o[2] = {want, got};
+  for (int t = 0; t < 2; ++t) {
+    const Fp2* c[6] = {&f[t]->c0.c0, &f[t]->c0.c1, &f[t]->c0.c2, &f[t]->c1.c0, &f[t]->c1.c1, &f[t]->c1.c2};
+    for (int i = 0; i < 6; ++i) store_fp2(o[t] + 96 * i, *c[i]);
+  }
 }
 // one mixed G1 addition (the gather-aggregate step), one full G1 addition (tree step),
 // one Fp12 product, one Jacobian G2 addition, one final exponentiation

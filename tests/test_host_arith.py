@@ -400,6 +400,42 @@ def test_miller_group_shared_accumulator(lib, k, mode):
         assert n_grp == bench.fme_miller_group(k)
 
 
+@pytest.mark.parametrize("K", [2, 4])
+def test_miller_groups_over_ragged_calls(lib, K):
+    """The call shapes of round 5's failing GPU run (gpurun_out/r05c, tests/test_gpu_c3.py:132 at the
+    time: calls of 127, 3 and 1 sets, so the last group of a call holds n mod K sets) through the host
+    build of the shared-accumulator loop, K = 2 and 4: the product of the groups' values equals the
+    product of the per-set Miller values, which equals the oracle's product of f_{|x|,Q}(P) (the
+    conjugate, x < 0).  The device kernel (k_vs_miller_group) was removed before its wrong boolean was
+    explained; this pins that the group arithmetic itself is exact for every ragged shape."""
+    rng = random.Random(77 + K)
+    lib.ht_miller_call_groups.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_int]
+    for n in (127, 3, 1, 2 * K + 1):
+        pts = []
+        ps, qs = b"", b""
+        for _ in range(n):
+            P = o.g1_mul(o.G1_GEN, rng.randrange(1, o.R))
+            Q = o.g2_mul(o.G2_GEN, rng.randrange(1, o.R))
+            pts.append((P, Q))
+            ps += be(P[0]) + be(P[1])
+            qs += fp2b(Q[0]) + fp2b(Q[1])
+        want, got = buf(576), buf(576)
+        lib.ht_miller_call_groups(want, got, ps, qs, n, K)
+        assert got.raw == want.raw, n
+        if n <= 3:  # the oracle's own product (P Jacobian 2p in the device loop: same value up to the FE)
+            f = o.F12_ONE
+            for P, Q in pts:
+                f = o.f12_mul(f, o.miller_loop(o.g1_mul(P, 2), Q))
+            fe = lambda b: o.final_exponentiation(_f12_from_be(b))
+            assert fe(got.raw) == o.final_exponentiation(f)
+
+
+def _f12_from_be(b):
+    v = [int.from_bytes(b[48 * i:48 * i + 48], "big") for i in range(12)]
+    f2 = [(v[2 * k], v[2 * k + 1]) for k in range(6)]
+    return ((f2[0], f2[1], f2[2]), (f2[3], f2[4], f2[5]))
+
+
 @pytest.mark.parametrize("case", ["valid", "one_bad_first", "one_bad_mid", "one_bad_last", "two_bad", "cancelling"])
 def test_locate_one_invalid_set(lib, case):
     """The locate prototype (tests/native/locate_proto.h; measured slower in the thread-serial failure
