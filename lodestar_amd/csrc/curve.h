@@ -333,20 +333,6 @@ GBV_HD G2J g2_psi_jac(const G2J& a) {
   return G2J{fp2_mul(fp2_conj(a.x), PSI_X), fp2_mul(fp2_conj(a.y), PSI_Y), fp2_conj(a.z)};
 }
 
-}  // namespace gbv
-#include "g2_lazy.h"
-namespace gbv {
-
-// G2 membership (Scott 2021): psi(Q) == [x] Q = -[|x|] Q.  Q affine, not infinity.  [|x|] Q on the
-// signed lazy 28-bit form (g2_lazy.h; the canonical chain g2_mul_xabs gives the same point).
-#ifndef GBV_G2_LAZY
-#define GBV_G2_LAZY 1  // 0: the canonical chain (A/B builds only, tools/build_variant.sh)
-#endif
-GBV_NI bool g2_in_subgroup(G2A q) {
-  G2J xq = jac_neg(GBV_G2_LAZY ? g2_mul_xabs_lazy(q) : g2_mul_xabs(q));
-  return jac_eq_aff(xq, g2_psi(q));
-}
-
 // G1 membership (Scott 2021): (beta x, y) == [-x^2] P.  P affine, not infinity.
 GBV_NI bool g1_in_subgroup(G1A p) {
   G1J t = jac_mul_xabs(p);           // [|x|] P
@@ -380,6 +366,20 @@ template <class F> GBV_HD Jac<F> jac_mul_2d_signed(const Aff<F>& S1, const Aff<F
     R = jac_add_aff(R, pick(i));
   }
   return R;
+}
+
+}  // namespace gbv
+#include "g2_lazy.h"
+namespace gbv {
+
+// G2 membership (Scott 2021): psi(Q) == [x] Q = -[|x|] Q.  Q affine, not infinity.  [|x|] Q on the
+// signed lazy 28-bit form (g2_lazy.h; the canonical chain g2_mul_xabs gives the same point).
+#ifndef GBV_G2_LAZY
+#define GBV_G2_LAZY 1  // 0: the canonical chain (A/B builds only, tools/build_variant.sh)
+#endif
+GBV_NI bool g2_in_subgroup(G2A q) {
+  G2J xq = jac_neg(GBV_G2_LAZY ? g2_mul_xabs_lazy(q) : g2_mul_xabs(q));
+  return jac_eq_aff(xq, g2_psi(q));
 }
 
 GBV_HD G1A g1_phi(const G1A& p) { return G1A{fp_mul(p.x, FP_BETA), p.y}; }
@@ -441,7 +441,7 @@ template <class Tab1, class Tab2> GBV_HD bool randomize_pair_tab(const G1A& P, c
   t2.store(1, aff_from_jac_inv(b2, fp2_mul(b1.z, Winv)));
   uint32_t sa = (uint32_t)r64, sb = (uint32_t)(r64 >> 32);
   *rP = jac_mul_2d_signed_tab<Fp>(t1, sa, sb);
-  *rQ = jac_mul_2d_signed_tab<Fp2>(t2, sa, sb);
+  *rQ = GBV_G2_LAZY ? g2_mul_2d_signed_lazy(t2.load(0), t2.load(1), sa, sb) : jac_mul_2d_signed_tab<Fp2>(t2, sa, sb);
   return true;
 }
 
@@ -478,13 +478,19 @@ GBV_NI bool randomize_pair_jac(G1J P, G2A Q, uint64_t r64, G1J* rP, G2J* rQ) {
   t2.store(1, aff_from_jac_inv(b2, fp2_mul(b1.z, Winv)));
   uint32_t sa = (uint32_t)r64, sb = (uint32_t)(r64 >> 32);
   *rP = jac_mul_2d_signed_tab<Fp>(t1, sa, sb);
-  *rQ = jac_mul_2d_signed_tab<Fp2>(t2, sa, sb);
+  *rQ = GBV_G2_LAZY ? g2_mul_2d_signed_lazy(t2.load(0), t2.load(1), sa, sb) : jac_mul_2d_signed_tab<Fp2>(t2, sa, sb);
   return true;
 }
 
 // [r] P in one group only (same r = a - b x^2 as randomize_pair): the same-message path's G1 term
 // when the G2 sum of a large segment comes from the bucket MSM (k_msm.hip), and the G2 term when
 // a failing segment needs its per-set r_i sig_i after all.  E(P) = phi(P) or -psi^2(P).
+// the signed 2-D ladder over a two-entry table: G1 on the canonical form, G2 on the lazy form (g2_lazy.h)
+template <class Tab> GBV_HD G1J mul_2d_tab(const Tab& t, const G1A*, uint32_t sa, uint32_t sb) { return jac_mul_2d_signed_tab<Fp>(t, sa, sb); }
+template <class Tab> GBV_HD G2J mul_2d_tab(const Tab& t, const G2A*, uint32_t sa, uint32_t sb) {
+  return GBV_G2_LAZY ? g2_mul_2d_signed_lazy(t.load(0), t.load(1), sa, sb) : jac_mul_2d_signed_tab<Fp2>(t, sa, sb);
+}
+
 template <class F> GBV_HD bool randomize_one(const Aff<F>& P, const Aff<F>& E, uint64_t r64, Jac<F>* rP) {
   Jac<F> a1 = jac_add_aff(jac_from_aff(P), E);
   Jac<F> a2 = jac_add_aff(jac_from_aff(P), Aff<F>{E.x, f_neg(E.y)});
@@ -494,7 +500,7 @@ template <class F> GBV_HD bool randomize_one(const Aff<F>& P, const Aff<F>& E, u
   RegTab2<Aff<F>> t;
   t.store(0, aff_from_jac_inv(a1, f_mul(a2.z, inv)));
   t.store(1, aff_from_jac_inv(a2, f_mul(a1.z, inv)));
-  *rP = jac_mul_2d_signed_tab<F>(t, (uint32_t)r64, (uint32_t)(r64 >> 32));
+  *rP = mul_2d_tab(t, (const Aff<F>*)nullptr, (uint32_t)r64, (uint32_t)(r64 >> 32));
   return true;
 }
 GBV_NI bool randomize_g1(G1A P, uint64_t r64, G1J* rP) { return randomize_one<Fp>(P, g1_phi(P), r64, rP); }

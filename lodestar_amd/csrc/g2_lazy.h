@@ -294,6 +294,42 @@ GBV_NI void s2j_madd(S2J* rp, const S2* q) {
   rp->y = s2_norm(s2_sub_k<2>(s2_mul(R, s2_sub(V, X3)), YJ));     // (-2L, L) - 2 (-2L, L): (-4L, 5L)
 }
 
+GBV_HD S2 s2_neg(const S2& a) { return S2{s28_sub(S28{}, a.c0), s28_sub(S28{}, a.c1)}; }
+GBV_HD S28 s28_sel(bool c, const S28& a, const S28& b) {
+  S28 r;
+#pragma unroll
+  for (int i = 0; i < 14; ++i) r.v[i] = c ? a.v[i] : b.v[i];
+  return r;
+}
+GBV_HD S2 s2_sel(bool c, const S2& a, const S2& b) { return S2{s28_sel(c, a.c0, b.c0), s28_sel(c, a.c1, b.c1)}; }
+
+// sum_i 2^i (d_i S) for the signed digit pairs of (sa, sb) -- curve.h jac_mul_2d_signed_tab, the batch
+// scalar r = a - b x^2 applied through the endomorphism -- on the lazy form: 31 doublings and 31 mixed
+// additions of +-S1 or +-S2 (affine, canonical, not infinity; held in the S2 form, a digit's sign
+// applied to y limbwise).  Same point as the canonical ladder; when Z = 0 mod p at the end (an addition
+// met R = +-S, impossible for points of the prime-order subgroup) the canonical ladder recomputes it.
+GBV_NI G2J g2_mul_2d_signed_lazy(G2A S1, G2A S2v, uint32_t sa, uint32_t sb) {
+  const S2 t1x = s2_from(S1.x), t1y = s2_from(S1.y), t2x = s2_from(S2v.x), t2y = s2_from(S2v.y);
+  S2 q[2];
+  auto pick = [&](int i) {
+    const bool s = (sa >> i) & 1u, t = (sb >> i) & 1u;
+    q[0] = s2_sel(s == t, t1x, t2x);
+    const S2 y = s2_sel(s == t, t1y, t2y);
+    q[1] = s2_sel(s, y, s2_neg(y));
+  };
+  pick(31);
+  S2J R{q[0], q[1], S2{s28_from_fp(FP_ONE), S28{}}};
+#pragma nounroll
+  for (int i = 30; i >= 0; --i) {
+    R = s2j_dbl(R);
+    pick(i);
+    s2j_madd(&R, q);
+  }
+  G2J r = s2j_to(R);
+  if (fp2_is_zero(r.z)) r = jac_mul_2d_signed(S1, S2v, sa, sb);
+  return ret_copy(r);
+}
+
 // [|x|] q, |x| = 0xd201000000010000: the runs of doublings between its set bits (62, 60, 57, 48, 16) and
 // the five mixed additions, all on the lazy form.  Same point as jac_mul_xabs(q): when Z = 0 mod p at the
 // end (an addition met *r = +-q, possible only for points of small order outside G2) the canonical chain

@@ -13,6 +13,7 @@ using namespace gbv;
 #define UB_W 2
 #endif
 
+GBV_NI G2J g2_ladder_canon(G2A a, G2A b, uint32_t sa, uint32_t sb) { return ret_copy(jac_mul_2d_signed(a, b, sa, sb)); }
 #define KATTR(W) __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(W, W)))
 template <int W> __global__ void KATTR(W) k_fp_mul(Fp* out) {
   Fp a = FP_ONE, b = FP_ONE;
@@ -67,6 +68,20 @@ template <int W, int V> __global__ void KATTR(W) k_dbl(Fp* out) {
   out[blockIdx.x * blockDim.x + threadIdx.x] = s28_to_fp(s28_add(s.x.c0, s.y.c1));
 }
 
+// the G2 batch randomisation r Q (curve.h randomize_g2: tables with one inversion, then the 2-D ladder)
+template <int W, bool LAZY> __global__ void KATTR(W) k_rand_g2(Fp* out) {
+  G2A q{Fp2{FP_ONE, FP_ONE}, Fp2{FP_B1, FP_ONE}};
+  q.x.c0.v[0] += threadIdx.x;
+  q.y.c1.v[1] += blockIdx.x;
+  const G2A e = g2_neg_psi2(q);
+  const G2J a1 = jac_add_aff(jac_from_aff(q), e), a2 = jac_add_aff(jac_from_aff(q), G2A{e.x, fp2_neg(e.y)});
+  const G2A t1{a1.x, a1.y}, t2{a2.x, a2.y};  // (not normalised: timing only)
+  const uint64_t r = 0x9E3779B97F4A7C15ull * (blockIdx.x * blockDim.x + threadIdx.x + 1);
+  const G2J R = LAZY ? g2_mul_2d_signed_lazy(t1, t2, (uint32_t)r, (uint32_t)(r >> 32))
+                     : g2_ladder_canon(t1, t2, (uint32_t)r, (uint32_t)(r >> 32));
+  out[blockIdx.x * blockDim.x + threadIdx.x] = fp_add(R.x.c0, R.z.c1);
+}
+
 typedef void (*kfn)(Fp*);
 static void run(const char* name, kfn f, Fp* out, int waves, double prods_per_thread) {
   hipEvent_t a, b;
@@ -103,6 +118,8 @@ int main() {
   const double xabs_prods = 63 * 16 + 5 * 29;
   run("xabs lazy", k_xabs<UB_W, true>, out, w, xabs_prods);
   run("xabs canon", k_xabs<UB_W, false>, out, w, xabs_prods);
+  run("rand_g2 lazy", k_rand_g2<UB_W, true>, out, w, 31 * 16 + 31 * 29);
+  run("rand_g2 canon", k_rand_g2<UB_W, false>, out, w, 31 * 16 + 31 * 29);
   run("dbl63 via s2j_dbl_n", k_dbl<UB_W, 0>, out, w, 63 * 16);
   run("dbl63 inline", k_dbl<UB_W, 100>, out, w, 63 * 16);
   run("dbl63 inline no norm", k_dbl<UB_W, 163>, out, w, 63 * 16);
