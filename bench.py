@@ -772,6 +772,7 @@ def main():
     ap.add_argument("--tune", action="append", default=[], metavar="NAME=VALUE",
                     help="gbv_tune setting applied before anything runs (experiments; include/gbv.h lists the names)")
     ap.add_argument("--no-vs-shard", action="store_true", help="skip the sharded verifySignatureSets object of the gossip line")
+    ap.add_argument("--shard-depth", type=int, default=2, help="vs-shard: shard passes in flight per rank (staged copies)")
     ap.add_argument("--shard-calls", type=int, default=512,
                     help="vs-shard: 128-member aggregate sets / 128 in the ONE sharded verifySignatureSets call")
     args = ap.parse_args()
@@ -1095,9 +1096,10 @@ def vs_shard_measure(args, v, sk_ints, world, rank, log):
     rng = np.random.Generator(np.random.PCG64(0x5A))
     sets = _agg_sets(v, sk_ints, 128 * args.shard_calls, b"gbv-shard", rng)
     lo, hi = sv.shard_of(sets)
-    # two staged copies of this rank's shard: the step loop keeps two shard passes in flight
+    # `depth` staged copies of this rank's shard: the step loop keeps that many shard passes in flight
     # (ShardedVerifier.verify_staged_shards), the exchange of pass k beside pass k + 1's kernels
-    stages = [v.stage_signature_sets([sets[lo:hi]]) for _ in range(2)]
+    depth = max(1, args.shard_depth)
+    stages = [v.stage_signature_sets([sets[lo:hi]]) for _ in range(depth)]
     staged = stages[0]
     log("vs-shard: %d sets, rank 0 shard [%d, %d), backend %s" % (len(sets), lo, hi, backend))
     assert sv.verify_staged_shard(staged) is True
@@ -1108,13 +1110,13 @@ def vs_shard_measure(args, v, sk_ints, world, rank, log):
     bad_small = bad[-256:]  # one-shot marshalling kept small: the wrong set sits in the last rank's share
     wrong = sv.verify_signature_sets(bad_small)
     ok_small = sv.verify_signature_sets(sets[-256:])
-    seq = [stages[k % 2] for k in range(args.steps)]
+    seq = [stages[k % depth] for k in range(args.steps)]
     if args.warmup:
-        assert sv.verify_staged_shards(seq[:max(2, args.warmup)]) == [True] * max(2, args.warmup)
+        assert sv.verify_staged_shards(seq[:max(depth, args.warmup)], depth=depth) == [True] * max(depth, args.warmup)
     tdist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    assert sv.verify_staged_shards(seq) == [True] * args.steps
+    assert sv.verify_staged_shards(seq, depth=depth) == [True] * args.steps
     torch.cuda.synchronize()
     tdist.barrier()
     elapsed = time.perf_counter() - t0
@@ -1137,7 +1139,7 @@ def vs_shard_measure(args, v, sk_ints, world, rank, log):
                 "config": {"workload": "C3-shaped call of %d aggregate sets as ONE verifySignatureSets call" % len(sets),
                            "parallelism": "cost-balanced shards%d + RCCL all-gather of 577-byte Fp12 partials" % world},
                 "world_size": world, "backend": backend, "gathered_from_ranks": list(range(world)),
-                "partial_bytes_per_gpu": 577, "rank0_shard": [lo, hi], "passes_in_flight": 2,
+                "partial_bytes_per_gpu": 577, "rank0_shard": [lo, hi], "passes_in_flight": depth,
                 "lone_pass_ms": round(lone_ms, 3),
                 "parity": {"sharded_equals_single_gpu": single is True, "wrong_signature_call_false": wrong is False,
                            "clean_small_call_true": ok_small is True}}

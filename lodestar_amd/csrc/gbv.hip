@@ -9,7 +9,6 @@ namespace {
 
 // a failing segment with at least this many chunks checks them one thread each (throughput), below
 // it one wave each (latency); see k_sm_group_check / k_sm_group_pairing
-constexpr uint32_t GROUP_CHECK_THREAD_MIN = 512;
 // segments of at most this many chunks skip the combined segment check (latency of small calls)
 constexpr uint32_t DIRECT_CHUNK_MAX = 32;
 // events per segment: [0,1] prepare, [2,3] chunk finish, [4,5] miller, [6,7] seg check,
@@ -166,7 +165,7 @@ static int sm_reserve(gbv_ctx* c, gbv_sm_batch* b, size_t n, size_t G, size_t ca
   chk(dalloc(&b->status, n)); chk(dalloc(&b->grp_state, G)); chk(dalloc(&b->valid, n));
   chk(dalloc(&b->H, calls)); chk(dalloc(&b->Hpre, calls)); chk(dalloc(&b->S, n)); chk(dalloc(&b->rS, n)); chk(dalloc(&b->rP, n));
   chk(dalloc(&b->PgJ, G)); chk(dalloc(&b->SgJ, G)); chk(dalloc(&b->F, G));
-  chk(dalloc(&b->Fpair, 2 * G)); chk(dalloc(&b->pair_ok, 2 * G)); chk(dalloc(&b->Ffb, 2 * FB_COOP_MAX));
+  chk(dalloc(&b->Fpair, 2 * G)); chk(dalloc(&b->pair_ok, 2 * G)); chk(dalloc(&b->Ffb, 2 * FB_COOP_CAP));
   // block partials: one region per segment parity (two segments' reductions can be in flight)
   b->part_stride = seg_reduce_scratch(G);
   chk(dalloc(&b->Fpart, 2 * b->part_stride)); chk(dalloc(&b->Spart, 2 * b->part_stride)); chk(dalloc(&b->has, 2 * b->part_stride));
@@ -805,7 +804,7 @@ static int sm_submit_enqueue(gbv_ctx* c, gbv_sm_batch* b) {
       launch_sm_redo_g2(LaunchCfg{0, 64, sb}, s0, s1 - s0, b->set_grp, b->status, b->S, seed, nonce, b->seg_ok + s, b->n_fallback, b->rS);
       launch_sm_chunk_finish_s(LaunchCfg{0, 64, sb}, g0, G, s0, b->grp_off, b->grp_state, b->rS, b->seg_ok + s, b->SgJ);
     }
-    if (G >= GROUP_CHECK_THREAD_MIN)
+    if (G >= tuning().group_thread_min)
       launch_sm_group_check(LaunchCfg{0, 64, sb}, g0, G, b->F, b->SgJ, b->seg_ok + s, b->grp_state, b->n_fallback);
     else
       launch_sm_group_pairing(LaunchCfg{G, 64, sb}, g0, G, b->grp_msg, b->PgJ, b->SgJ, b->H, b->seg_ok + s, b->grp_state, b->n_fallback,
@@ -828,15 +827,17 @@ static int sm_submit_enqueue(gbv_ctx* c, gbv_sm_batch* b) {
     uint32_t s0 = b->grp_off_host[gcut[s]], s1 = b->grp_off_host[gcut[s + 1]];
     launch_sm_fb_runs(LaunchCfg{0, 64, sf}, s0, s1 - s0, b->set_grp, b->grp_state, b->fb_runs, b->fb_cnt, (uint32_t)b->fb_cap);
   }
-  // few items: one wave each (latency); many: one thread each (throughput) -- one of each pair exits
+  // few items: one wave each (latency); many: one thread each (throughput) -- one of each pair exits.
+  // The split (gbv_tune "fb_coop_max") is read once, so both kernels of a pair agree on it.
+  const uint32_t cm = std::min(tuning().fb_coop_max.load(std::memory_order_relaxed), FB_COOP_CAP);
   launch_sm_fb_blocks_coop(LaunchCfg{0, 64, sf}, b->fb_runs, b->fb_cnt, (uint32_t)b->fb_cap, b->status, b->grp_msg, b->rS, b->rP,
-                           b->H, b->valid, b->fb_list, b->fb_cnt + 1);
+                           b->H, b->valid, b->fb_list, b->fb_cnt + 1, cm);
   launch_sm_fb_blocks(LaunchCfg{FB_GRID, 64, sf}, b->fb_runs, b->fb_cnt, (uint32_t)b->fb_cap, b->status, b->grp_msg, b->rS, b->rP, b->H,
-                      b->valid, b->fb_list, b->fb_cnt + 1);
+                      b->valid, b->fb_list, b->fb_cnt + 1, cm);
   launch_sm_fb_sets_coop(LaunchCfg{0, 64, sf}, b->fb_list, b->fb_cnt + 1, b->set_grp, b->grp_msg, b->idx, c->table, b->S, b->H,
-                         b->valid, b->Ffb);
+                         b->valid, b->Ffb, cm);
   launch_sm_fb_sets(LaunchCfg{FB_GRID, 64, sf}, b->fb_list, b->fb_cnt + 1, b->set_grp, b->grp_msg, b->idx, c->table, b->S, b->H,
-                    b->valid);
+                    b->valid, cm);
   HIP_CHECK(c, hipEventRecord(ep[1], sf));
   HIP_CHECK(c, hipMemcpyAsync(b->valid_host, b->valid, b->n, hipMemcpyDeviceToHost, sf));
   HIP_CHECK(c, hipMemcpyAsync(b->nfb_host, b->n_fallback, sizeof(uint32_t), hipMemcpyDeviceToHost, sf));
@@ -1181,7 +1182,9 @@ bool tuning_set(const char* name, uint32_t v) {
       {"hash_pair_max", &g_tuning.hash_pair_max}, {"hash_quad_max", &g_tuning.hash_quad_max}, {"hash_coop_max", &g_tuning.hash_coop_max},
       {"prepare_split_max", &g_tuning.prepare_split_max}, {"chunk_finish_wave_max", &g_tuning.chunk_finish_wave_max},
       {"vs_pre_max", &g_tuning.vs_pre_max}, {"vs_fs_maxc", &g_tuning.vs_fs_maxc}, {"vs_quad_max", &g_tuning.vs_quad_max},
-      {"vs_pair_max", &g_tuning.vs_pair_max}, {"agg_slice", &g_tuning.agg_slice}};
+      {"vs_pair_max", &g_tuning.vs_pair_max}, {"agg_slice", &g_tuning.agg_slice}, {"fb_coop_max", &g_tuning.fb_coop_max},
+      {"group_thread_min", &g_tuning.group_thread_min}};
+  if (!strcmp(name, "fb_coop_max")) v = std::min(v, FB_COOP_CAP);  // the scratch is sized for the cap
   for (auto& t : tab)
     if (!strcmp(name, t.n)) {
       t.p->store(v, std::memory_order_relaxed);

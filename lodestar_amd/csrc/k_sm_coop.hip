@@ -220,14 +220,15 @@ __device__ inline bool coop_pair_check(coop::Slot* ws, const G1A& P, const G2A& 
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
 k_sm_fb_blocks_coop(const uint4* __restrict__ runs, const uint32_t* __restrict__ n_runs, uint32_t cap, const uint8_t* __restrict__ status,
                     const uint32_t* __restrict__ grp_msg, const G2J* __restrict__ Sh, const G1J* __restrict__ Ph, const G2A* __restrict__ H,
-                    uint8_t* __restrict__ valid, uint32_t* __restrict__ set_list, uint32_t* __restrict__ n_list, int direct_ok) {
+                    uint8_t* __restrict__ valid, uint32_t* __restrict__ set_list, uint32_t* __restrict__ n_list, int direct_ok,
+                    uint32_t coop_max) {
   __shared__ coop::Slot ws[SEG_WS];
   __shared__ Fp st[6];
   __shared__ int flags[3];
   uint32_t cnt = min(*n_runs, cap);
-  if (cnt > FB_COOP_MAX) return;
+  if (cnt > coop_max) return;
   unsigned lane = threadIdx.x;
-  if (direct_ok && cnt * FB_RUN_MAX <= FB_COOP_MAX) {  // few sets in all: straight to the per-set checks
+  if (direct_ok && cnt * FB_RUN_MAX <= coop_max) {  // few sets in all: straight to the per-set checks
     for (uint32_t k = blockIdx.x; k < cnt; k += gridDim.x) {
       const uint4 r = runs[k];
       if (lane == 0)
@@ -281,10 +282,10 @@ k_sm_fb_blocks_coop(const uint4* __restrict__ runs, const uint32_t* __restrict__
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
 k_sm_fb_sets_coop(const uint32_t* __restrict__ set_list, const uint32_t* __restrict__ n_list, const uint32_t* __restrict__ set_grp,
                   const uint32_t* __restrict__ grp_msg, const uint32_t* __restrict__ idx, const G1A* __restrict__ table,
-                  const G2A* __restrict__ S, const G2A* __restrict__ H, uint8_t* __restrict__ valid) {
+                  const G2A* __restrict__ S, const G2A* __restrict__ H, uint8_t* __restrict__ valid, uint32_t coop_max) {
   __shared__ coop::Slot ws[SEG_WS];
   uint32_t cnt = *n_list;
-  if (cnt > FB_COOP_MAX) return;
+  if (cnt > coop_max) return;
   if (blockIdx.x < cnt) coop::load_consts();
   for (uint32_t k = blockIdx.x; k < cnt; k += gridDim.x) {
     uint32_t i = set_list[k];
@@ -299,10 +300,10 @@ k_sm_fb_sets_coop(const uint32_t* __restrict__ set_list, const uint32_t* __restr
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
 k_sm_fb_sets_miller2(const uint32_t* __restrict__ set_list, const uint32_t* __restrict__ n_list, const uint32_t* __restrict__ set_grp,
                      const uint32_t* __restrict__ grp_msg, const uint32_t* __restrict__ idx, const G1A* __restrict__ table,
-                     const G2A* __restrict__ S, const G2A* __restrict__ H, Fp12* __restrict__ Fpair) {
+                     const G2A* __restrict__ S, const G2A* __restrict__ H, Fp12* __restrict__ Fpair, uint32_t coop_max) {
   __shared__ coop::Slot ws[coop::MILLER_WS];
   const uint32_t cnt = *n_list;
-  if (cnt > FB_COOP_MAX) return;
+  if (cnt > coop_max) return;
   if (blockIdx.x < cnt) coop::load_consts();
   const uint32_t j = blockIdx.y;
   for (uint32_t k = blockIdx.x; k < cnt; k += gridDim.x) {
@@ -318,10 +319,10 @@ k_sm_fb_sets_miller2(const uint32_t* __restrict__ set_list, const uint32_t* __re
 }
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
 k_sm_fb_sets_fe(const uint32_t* __restrict__ set_list, const uint32_t* __restrict__ n_list, const Fp12* __restrict__ Fpair,
-                uint8_t* __restrict__ valid) {
+                uint8_t* __restrict__ valid, uint32_t coop_max) {
   __shared__ coop::Slot ws[coop::FINAL_EXP_WS];
   const uint32_t cnt = *n_list;
-  if (cnt > FB_COOP_MAX) return;
+  if (cnt > coop_max) return;
   if (blockIdx.x < cnt) coop::load_consts();
   const unsigned lane = threadIdx.x;
   for (uint32_t k = blockIdx.x; k < cnt; k += gridDim.x) {
@@ -339,17 +340,19 @@ k_sm_fb_sets_fe(const uint32_t* __restrict__ set_list, const uint32_t* __restric
 
 void launch_sm_fb_blocks_coop(LaunchCfg c, const uint4* runs, const uint32_t* n_runs, uint32_t cap, const uint8_t* status,
                               const uint32_t* grp_msg, const G2J* Sh, const G1J* Ph, const G2A* H, uint8_t* valid, uint32_t* set_list,
-                              uint32_t* n_list) {
-  GBV_LAUNCH("k_sm_fb_blocks_coop", k_sm_fb_blocks_coop, dim3(FB_COOP_MAX), dim3(64), c.stream, 0, runs, n_runs, cap, status, grp_msg, Sh, Ph, H, valid, set_list, n_list, 1);
+                              uint32_t* n_list, uint32_t cm) {
+  GBV_LAUNCH("k_sm_fb_blocks_coop", k_sm_fb_blocks_coop, dim3(std::max(cm, 1u)), dim3(64), c.stream, 0, runs, n_runs, cap, status, grp_msg, Sh, Ph, H,
+             valid, set_list, n_list, 1, cm);
 }
 void launch_sm_fb_sets_coop(LaunchCfg c, const uint32_t* set_list, const uint32_t* n_list, const uint32_t* set_grp, const uint32_t* grp_msg,
-                            const uint32_t* idx, const G1A* table, const G2A* S, const G2A* H, uint8_t* valid, Fp12* Fpair) {
-  if (Fpair) {  // 2 * FB_COOP_MAX Fp12 of scratch
-    GBV_LAUNCH("k_sm_fb_sets_miller2", k_sm_fb_sets_miller2, dim3(FB_COOP_MAX, 2), dim3(64), c.stream, 0, set_list, n_list, set_grp, grp_msg, idx, table, S, H, Fpair);
-    GBV_LAUNCH("k_sm_fb_sets_fe", k_sm_fb_sets_fe, dim3(FB_COOP_MAX), dim3(64), c.stream, 0, set_list, n_list, Fpair, valid);
+                            const uint32_t* idx, const G1A* table, const G2A* S, const G2A* H, uint8_t* valid, Fp12* Fpair, uint32_t cm) {
+  const uint32_t gx = std::max(cm, 1u);
+  if (Fpair) {  // 2 * FB_COOP_CAP Fp12 of scratch
+    GBV_LAUNCH("k_sm_fb_sets_miller2", k_sm_fb_sets_miller2, dim3(gx, 2), dim3(64), c.stream, 0, set_list, n_list, set_grp, grp_msg, idx, table, S, H, Fpair, cm);
+    GBV_LAUNCH("k_sm_fb_sets_fe", k_sm_fb_sets_fe, dim3(gx), dim3(64), c.stream, 0, set_list, n_list, Fpair, valid, cm);
     return;
   }
-  GBV_LAUNCH("k_sm_fb_sets_coop", k_sm_fb_sets_coop, dim3(FB_COOP_MAX), dim3(64), c.stream, 0, set_list, n_list, set_grp, grp_msg, idx, table, S, H, valid);
+  GBV_LAUNCH("k_sm_fb_sets_coop", k_sm_fb_sets_coop, dim3(gx), dim3(64), c.stream, 0, set_list, n_list, set_grp, grp_msg, idx, table, S, H, valid, cm);
 }
 
 // One level of a segment's reduction on lane quads: block b combines items k = 64 b + j + 16 m

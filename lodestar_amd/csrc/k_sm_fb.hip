@@ -42,9 +42,10 @@ void launch_sm_group_check(LaunchCfg c, uint32_t g0, uint32_t G, const Fp12* F, 
 __global__ void GBV_FB_ATTR k_sm_fb_blocks(const uint4* __restrict__ runs, const uint32_t* __restrict__ n_runs, uint32_t cap,
                                                const uint8_t* __restrict__ status, const uint32_t* __restrict__ grp_msg,
                                                const G2J* __restrict__ Sh, const G1J* __restrict__ Ph, const G2A* __restrict__ H,
-                                               uint8_t* __restrict__ valid, uint32_t* __restrict__ set_list, uint32_t* __restrict__ n_list) {
+                                               uint8_t* __restrict__ valid, uint32_t* __restrict__ set_list, uint32_t* __restrict__ n_list,
+                                               uint32_t coop_max) {
   uint32_t cnt = min(*n_runs, cap);
-  if (cnt <= FB_COOP_MAX) return;  // k_sm_fb_blocks_coop has them
+  if (cnt <= coop_max) return;  // k_sm_fb_blocks_coop has them
   for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < cnt; k += gridDim.x * blockDim.x) {
     uint4 r = runs[k];
     bool any = false;
@@ -73,9 +74,9 @@ __global__ void GBV_FB_ATTR k_sm_fb_blocks(const uint4* __restrict__ runs, const
 __global__ void GBV_FB_ATTR k_sm_fb_sets(const uint32_t* __restrict__ set_list, const uint32_t* __restrict__ n_list,
                                              const uint32_t* __restrict__ set_grp, const uint32_t* __restrict__ grp_msg,
                                              const uint32_t* __restrict__ idx, const G1A* __restrict__ table, const G2A* __restrict__ S,
-                                             const G2A* __restrict__ H, uint8_t* __restrict__ valid) {
+                                             const G2A* __restrict__ H, uint8_t* __restrict__ valid, uint32_t coop_max) {
   uint32_t cnt = *n_list;
-  if (cnt <= FB_COOP_MAX) return;  // k_sm_fb_sets_coop has them
+  if (cnt <= coop_max) return;  // k_sm_fb_sets_coop has them
   for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < cnt; k += gridDim.x * blockDim.x) {
     uint32_t i = set_list[k];
     valid[i] = pairing_check_2(table[idx[i]], false, H[grp_msg[set_grp[i]]], g1_neg_generator(), false, S[i]) ? 1 : 0;
@@ -83,13 +84,13 @@ __global__ void GBV_FB_ATTR k_sm_fb_sets(const uint32_t* __restrict__ set_list, 
 }
 
 void launch_sm_fb_blocks(LaunchCfg c, const uint4* runs, const uint32_t* n_runs, uint32_t cap, const uint8_t* status, const uint32_t* grp_msg,
-                         const G2J* Sh, const G1J* Ph, const G2A* H, uint8_t* valid, uint32_t* set_list, uint32_t* n_list) {
+                         const G2J* Sh, const G1J* Ph, const G2A* H, uint8_t* valid, uint32_t* set_list, uint32_t* n_list, uint32_t coop_max) {
   GBV_LAUNCH("k_sm_fb_blocks", k_sm_fb_blocks, dim3(c.blocks), dim3(64), c.stream, 0, runs, n_runs, cap, status, grp_msg, Sh, Ph, H, valid, set_list,
-             n_list);
+             n_list, coop_max);
 }
 void launch_sm_fb_sets(LaunchCfg c, const uint32_t* set_list, const uint32_t* n_list, const uint32_t* set_grp, const uint32_t* grp_msg,
-                       const uint32_t* idx, const G1A* table, const G2A* S, const G2A* H, uint8_t* valid) {
-  GBV_LAUNCH("k_sm_fb_sets", k_sm_fb_sets, dim3(c.blocks), dim3(64), c.stream, 0, set_list, n_list, set_grp, grp_msg, idx, table, S, H, valid);
+                       const uint32_t* idx, const G1A* table, const G2A* S, const G2A* H, uint8_t* valid, uint32_t coop_max) {
+  GBV_LAUNCH("k_sm_fb_sets", k_sm_fb_sets, dim3(c.blocks), dim3(64), c.stream, 0, set_list, n_list, set_grp, grp_msg, idx, table, S, H, valid, coop_max);
 }
 
 }  // namespace gbv

@@ -8,7 +8,10 @@
 namespace gbv {
 
 GBV_NI G1J vs_g1_add(G1J a, G1J b) { return jac_add(a, b); }
-GBV_NI G1J vs_g1_add_aff(G1J a, G1A b) { return jac_add_aff(a, b); }
+// The gather loops' mixed addition is inline: out of line, the G1J result returned through the caller's
+// frame was a 192-byte scratch write (and read) per member -- k_vs_agg_big's 3.9 MB of writes per 8 192
+// members in PMC.
+GBV_HD G1J vs_g1_add_aff(const G1J& a, const G1A& b) { return jac_add_aff(a, b); }
 
 __device__ inline Fp vs_shfl_down(const Fp& a, unsigned d) {
   Fp r;

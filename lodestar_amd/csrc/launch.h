@@ -72,15 +72,15 @@ void launch_sm_group_check(LaunchCfg c, uint32_t g0, uint32_t G, const Fp12* F, 
 void launch_sm_fb_runs(LaunchCfg c, uint32_t s0, uint32_t n, const uint32_t* set_grp, const uint8_t* grp_state, uint4* runs, uint32_t* n_runs,
                        uint32_t cap);
 void launch_sm_fb_blocks(LaunchCfg c, const uint4* runs, const uint32_t* n_runs, uint32_t cap, const uint8_t* status, const uint32_t* grp_msg,
-                         const G2J* Sh, const G1J* Ph, const G2A* H, uint8_t* valid, uint32_t* set_list, uint32_t* n_list);
+                         const G2J* Sh, const G1J* Ph, const G2A* H, uint8_t* valid, uint32_t* set_list, uint32_t* n_list, uint32_t coop_max);
 void launch_sm_fb_sets(LaunchCfg c, const uint32_t* set_list, const uint32_t* n_list, const uint32_t* set_grp, const uint32_t* grp_msg,
-                       const uint32_t* idx, const G1A* table, const G2A* S, const G2A* H, uint8_t* valid);
+                       const uint32_t* idx, const G1A* table, const G2A* S, const G2A* H, uint8_t* valid, uint32_t coop_max);
 
 void launch_sm_fb_blocks_coop(LaunchCfg c, const uint4* runs, const uint32_t* n_runs, uint32_t cap, const uint8_t* status,
                               const uint32_t* grp_msg, const G2J* Sh, const G1J* Ph, const G2A* H, uint8_t* valid, uint32_t* set_list,
-                              uint32_t* n_list);
+                              uint32_t* n_list, uint32_t coop_max);
 void launch_sm_fb_sets_coop(LaunchCfg c, const uint32_t* set_list, const uint32_t* n_list, const uint32_t* set_grp, const uint32_t* grp_msg,
-                            const uint32_t* idx, const G1A* table, const G2A* S, const G2A* H, uint8_t* valid, Fp12* Fpair = nullptr);
+                            const uint32_t* idx, const G1A* table, const G2A* S, const G2A* H, uint8_t* valid, Fp12* Fpair, uint32_t coop_max);
 
 void launch_pk_decompress(LaunchCfg c, uint32_t n, const uint8_t* pk48, int validate, G1A* table, uint8_t* table_ok, uint8_t* status);
 void launch_comb_build(hipStream_t s, uint32_t first, uint32_t n, const G1A* table, const uint8_t* table_ok, G1A* bases9, uint4* comb,
