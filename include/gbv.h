@@ -99,7 +99,8 @@ int gbv_comb_enabled(gbv_ctx* ctx);
  * "hash_quad_max", "hash_coop_max", "prepare_split_max", "chunk_finish_wave_max", "vs_pre_max",
  * "vs_fs_maxc", "vs_quad_max", "vs_pair_max", "agg_slice", and the same-message failure path's split between
  * one wave per check (latency) and one thread per check (throughput): "fb_coop_max" (run / per-set checks,
- * at most 16384) and "group_thread_min" (chunk checks).  GBV_E_ARG for an unknown name. */
+ * at most 16384) and "group_thread_min" (chunk checks); "sm_quad_max" (chunk Miller values on lane quads
+ * up to this many chunks of a segment).  GBV_E_ARG for an unknown name. */
 int gbv_tune(gbv_ctx* ctx, const char* name, uint32_t value);
 
 /* IBlsVerifier.verifySignatureSets (interface.ts:47; multithread/index.ts:157-207).

@@ -1183,7 +1183,7 @@ bool tuning_set(const char* name, uint32_t v) {
       {"prepare_split_max", &g_tuning.prepare_split_max}, {"chunk_finish_wave_max", &g_tuning.chunk_finish_wave_max},
       {"vs_pre_max", &g_tuning.vs_pre_max}, {"vs_fs_maxc", &g_tuning.vs_fs_maxc}, {"vs_quad_max", &g_tuning.vs_quad_max},
       {"vs_pair_max", &g_tuning.vs_pair_max}, {"agg_slice", &g_tuning.agg_slice}, {"fb_coop_max", &g_tuning.fb_coop_max},
-      {"group_thread_min", &g_tuning.group_thread_min}};
+      {"group_thread_min", &g_tuning.group_thread_min}, {"sm_quad_max", &g_tuning.sm_quad_max}};
   if (!strcmp(name, "fb_coop_max")) v = std::min(v, FB_COOP_CAP);  // the scratch is sized for the cap
   for (auto& t : tab)
     if (!strcmp(name, t.n)) {

@@ -373,6 +373,10 @@ void launch_sm_chunk_finish(LaunchCfg c, uint32_t g0, uint32_t G, uint32_t s0, c
 }
 void launch_sm_miller(LaunchCfg c, uint32_t g0, uint32_t G, const uint32_t* grp_msg, const uint8_t* grp_state, const G1J* PgJ, const G2A* H,
                       Fp12* F) {
+  if (G <= tuning().sm_quad_max.load(std::memory_order_relaxed)) {
+    launch_sm_miller_quad(c, g0, G, grp_msg, grp_state, PgJ, H, F);
+    return;
+  }
   GBV_LAUNCH("k_sm_miller", k_sm_miller, dim3((G + 63) / 64), dim3(64), c.stream, G, g0, G, grp_msg, grp_state, PgJ, H, F);
 }
 void launch_sm_fallback(LaunchCfg c, uint32_t n, const uint32_t* set_grp, const uint32_t* grp_msg, const uint8_t* grp_state,

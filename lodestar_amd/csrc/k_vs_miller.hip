@@ -61,21 +61,16 @@ __global__ void GBV_MILLER_ATTR k_vs_miller_pair(uint32_t n, const uint8_t* __re
 // block i / 16; lane 2h + s writes Fp components 3s .. 3s + 2 of half h of the conjugated value.
 // Every lane runs the loop (the quad exchanges need all four); quads past n or whose set did not
 // decode write nothing.
-__global__ void GBV_MILLER_QUAD_ATTR k_vs_miller_quad(uint32_t n, const uint8_t* __restrict__ status, const G1J* __restrict__ rP,
-                                                 const G2A* __restrict__ H, Fp12* __restrict__ F) {
+// One quad's Miller value of (p, Q); lanes of inactive quads run the loop and write nothing.
+__device__ __forceinline__ void quad_miller_store(const G1J& p, const G2A& Q, bool act, Fp12* __restrict__ Fi) {
   quad::Lane L;
   L.q = threadIdx.x & 3u;
   L.h = (L.q & 2u) != 0;
   L.s = (L.q & 1u) != 0;
-  const uint32_t i = blockIdx.x * 16 + (threadIdx.x >> 2);
-  const bool act = i < n && status[i] == SET_OK;
-  const uint32_t j = i < n ? i : n - 1;
-  const G1J p = rP[j];
   PairP P;
   P.z3 = fp_mul(fp_sqr(p.z), p.z);
   P.nxz = fp_neg(fp_mul(p.x, p.z));
   P.y = p.y;
-  const G2A Q = H[j];
   PairT T{Q.x, Q.y, fp2_one()};
   Fp6 M = fp6_sel(L.h, fp6_zero(), fp6_one());
   for (int b = 62; b >= 0; --b) {
@@ -90,10 +85,34 @@ __global__ void GBV_MILLER_QUAD_ATTR k_vs_miller_quad(uint32_t n, const uint8_t*
   if (!act) return;
   if (L.h) M = fp6_neg(M);
   // this lane's three Fp of the half: s = 0 -> c0.c0, c0.c1, c1.c0; s = 1 -> c1.c1, c2.c0, c2.c1
-  Fp* out = (Fp*)&F[i] + 6 * (L.h ? 1 : 0) + 3 * (L.s ? 1 : 0);
+  Fp* out = (Fp*)Fi + 6 * (L.h ? 1 : 0) + 3 * (L.s ? 1 : 0);
   out[0] = fp_sel(L.s, M.c1.c1, M.c0.c0);
   out[1] = fp_sel(L.s, M.c2.c0, M.c0.c1);
   out[2] = fp_sel(L.s, M.c2.c1, M.c1.c0);
+}
+
+__global__ void GBV_MILLER_QUAD_ATTR k_vs_miller_quad(uint32_t n, const uint8_t* __restrict__ status, const G1J* __restrict__ rP,
+                                                 const G2A* __restrict__ H, Fp12* __restrict__ F) {
+  const uint32_t i = blockIdx.x * 16 + (threadIdx.x >> 2);
+  const bool act = i < n && status[i] == SET_OK;
+  const uint32_t j = i < n ? i : n - 1;
+  quad_miller_store(rP[j], H[j], act, &F[j]);
+}
+
+// Same-message chunk Miller values f_g = f_{|x|, H(m_g)}(P_g) on lane quads (k_sm_miller's latency
+// form for segments of few chunks: a thread per chunk leaves such a launch a few waves long).
+__global__ void GBV_MILLER_QUAD_ATTR k_sm_miller_quad(uint32_t g0, uint32_t G, const uint32_t* __restrict__ grp_msg,
+                                                 const uint8_t* __restrict__ grp_state, const G1J* __restrict__ PgJ,
+                                                 const G2A* __restrict__ H, Fp12* __restrict__ F) {
+  const uint32_t k = blockIdx.x * 16 + (threadIdx.x >> 2);
+  const uint32_t g = g0 + (k < G ? k : G - 1);
+  const bool act = k < G && grp_state[g] == GRP_PENDING;
+  quad_miller_store(PgJ[g], H[grp_msg[g]], act, &F[g]);
+}
+void launch_sm_miller_quad(LaunchCfg c, uint32_t g0, uint32_t G, const uint32_t* grp_msg, const uint8_t* grp_state, const G1J* PgJ,
+                           const G2A* H, Fp12* F) {
+  if (G == 0) return;
+  GBV_LAUNCH("k_sm_miller_quad", k_sm_miller_quad, dim3((G + 15) / 16), dim3(64), c.stream, G, g0, G, grp_msg, grp_state, PgJ, H, F);
 }
 
 void launch_vs_miller(LaunchCfg c, uint32_t n, const uint8_t* status, const G1J* rP, const G2A* H, Fp12* F) {

@@ -65,7 +65,7 @@ enum : uint8_t { SET_OK = 0, SET_BAD_SIG = 1, SET_BAD_PK = 2 };
 enum : uint8_t { GRP_PENDING = 0, GRP_FALLBACK = 1, GRP_OK = 2 };
 // Failure-path item counts up to which one wave per item (k_sm_fb_*_coop, latency) beats one
 // thread per item (k_sm_fb_blocks / k_sm_fb_sets, throughput).
-constexpr uint32_t FB_COOP_MAX = 256;    // default of gbv_tune "fb_coop_max"
+constexpr uint32_t FB_COOP_MAX = 16384;  // default of gbv_tune "fb_coop_max" (131 072-set C5 batches +16 %, 1M unchanged: profiles/r06l)
 constexpr uint32_t FB_COOP_CAP = 16384;  // its largest value (the per-batch scratch of the two-wave per-set checks)
 // Sets per failure-path run (the 8-set scan windows of k_sm_prepare).  When the failing runs hold at
 // most FB_COOP_MAX sets in all, k_sm_fb_blocks_coop skips the run checks and hands every set to the
@@ -88,9 +88,10 @@ struct Tuning {  // relaxed atomics: gbv_tune may run beside another context's e
   std::atomic<uint32_t> vs_fs_maxc{256};               // per-chunk (-g1, sum) Miller value beside the per-set ones
   std::atomic<uint32_t> vs_quad_max{16384};            // per-set Miller values on lane quads up to this many sets
   std::atomic<uint32_t> vs_pair_max{32768};            // ... on lane pairs up to this many (one lane per set above)
-  std::atomic<uint32_t> agg_slice{8192};
-  std::atomic<uint32_t> fb_coop_max{FB_COOP_MAX};   // same-message failure path: run / per-set checks one wave each up to this many
-  std::atomic<uint32_t> group_thread_min{512};      // ... chunk checks one thread each from this many chunks of a segment (one wave each below)               // large aggregates: members per k_vs_agg_big workgroup (256 threads; profiles/r05l)
+  std::atomic<uint32_t> agg_slice{8192};               // large aggregates: members per k_vs_agg_big workgroup (256 threads; profiles/r05l)
+  std::atomic<uint32_t> fb_coop_max{FB_COOP_MAX};      // same-message failure path: run / per-set checks one wave each up to this many
+  std::atomic<uint32_t> group_thread_min{512};         // ... chunk checks one thread each from this many chunks of a segment (one wave each below)
+  std::atomic<uint32_t> sm_quad_max{8192};               // same-message chunk Miller values on lane quads up to this many chunks of a segment
   std::atomic<uint32_t> sync_debug{0};                 // GBV_SYNC_DEBUG: synchronise + report after every launch (debugging)
 };
 const Tuning& tuning();

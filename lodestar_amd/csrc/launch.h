@@ -31,6 +31,8 @@ void launch_sm_prep_roles_quad(hipStream_t s, uint32_t base, uint32_t n, const u
                                const uint8_t* status, uint8_t* sub_ok, G2J* Sh, G1J* Ph);
 void launch_sm_chunk_finish(LaunchCfg c, uint32_t g0, uint32_t G, uint32_t s0, const uint32_t* grp_off, const uint8_t* status, const G2J* Sh,
                             const G1J* Ph, G1J* PgJ, G2J* SgJ, uint8_t* grp_state, uint32_t* n_fallback);
+void launch_sm_miller_quad(LaunchCfg c, uint32_t g0, uint32_t G, const uint32_t* grp_msg, const uint8_t* grp_state, const G1J* PgJ,
+                           const G2A* H, Fp12* F);
 void launch_sm_miller(LaunchCfg c, uint32_t g0, uint32_t G, const uint32_t* grp_msg, const uint8_t* grp_state, const G1J* PgJ, const G2A* H,
                       Fp12* F);
 uint32_t launch_seg_reduce_quad(hipStream_t s, uint32_t g0, uint32_t G, const uint8_t* grp_state, const Fp12* F, const G2J* SgJ, Fp12* Fpart,

@@ -117,7 +117,18 @@ def _default_settings(request):
     """Every test starts from, and leaves, the context's default pipeline settings."""
     yield
     if "world" in request.fixturenames:
-        _tune(request.getfixturevalue("world")[0], 1, 131072, 16)
+        v = request.getfixturevalue("world")[0]
+        _tune(v, 1, 131072, 16)
+        for name, value in FORM_DEFAULTS.items():
+            v.tune(name, value)
+
+
+# process-wide launch-form defaults (kernel_common.h Tuning) that tests below move
+FORM_DEFAULTS = {"fb_coop_max": 16384, "group_thread_min": 512, "sm_quad_max": 8192}
+# "thread": one thread per chunk / run / set check and per chunk Miller value (throughput forms);
+# "wave": one wave per check and lane quads per chunk Miller value (latency forms)
+FORMS = {"thread": {"fb_coop_max": 0, "group_thread_min": 0, "sm_quad_max": 0},
+         "wave": {"fb_coop_max": 16384, "group_thread_min": 1 << 30, "sm_quad_max": 1 << 30}}
 
 
 @pytest.fixture(params=["ladder", "msm"])
@@ -168,14 +179,19 @@ def test_same_message_injected_invalid(world, segments):
     assert res == expected
 
 
+@pytest.mark.parametrize("form", ["thread", "wave"])
 @pytest.mark.parametrize("mode", ["ladder", "msm"])
-def test_same_message_one_percent_invalid(world, mode):
+def test_same_message_one_percent_invalid(world, mode, form):
     """C5-style density: 1 % of 60 000 sets invalid, so hundreds of chunks fail.  The
-    failure path then runs its thread-per-item kernels (group checks, 8-set run checks, per-set
-    checks: more than FB_COOP_MAX items each) and must still return exactly the per-set booleans.
-    In MSM mode the failing segment first recomputes its per-set G2 terms (k_sm_redo_g2)."""
+    failure path (group checks, 8-set run checks, per-set checks) must return exactly the per-set
+    booleans in both launch forms: one thread per check (k_sm_group_check, k_sm_fb_blocks,
+    k_sm_fb_sets, k_sm_miller) and one wave per check (k_sm_group_pairing, k_sm_fb_blocks_coop,
+    k_sm_fb_sets_*, k_sm_miller_quad).  In MSM mode the failing segment first recomputes its per-set
+    G2 terms (k_sm_redo_g2)."""
     v, sks, _ = world
     _tune(v, 1, 1000 if mode == "msm" else 0, 0)
+    for name, value in FORMS[form].items():
+        v.tune(name, value)
     _one_percent(v, sks)
 
 
