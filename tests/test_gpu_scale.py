@@ -358,6 +358,28 @@ def test_same_message_msm_single_segment(world):
     assert fb == 1 and seg == 1
 
 
+def test_msm_duplicate_signatures(world):
+    """One key signing one message 20 000 times in one MSM segment: every (half, window) of the bucket
+    MSM then holds thousands of repeated digits of the same point, so the bucket sums (k_msm_runs) meet
+    acc = +-q -- the doubling and infinity cases of the complete mixed addition. The segment check must
+    pass on the MSM's sum, and a wrong-message signature among the copies must be the one set
+    rejected."""
+    v, sks, _ = world
+    _tune(v, 1, 1000, 0)
+    n = 20000
+    off = np.array([0, n], dtype=np.uint32)
+    idx = np.full(n, 7, dtype=np.uint32)
+    msg = hashlib.sha256(b"gbv-dup").digest()
+    sig = v.util_sign([sks[7]], [0], [msg])[0]
+    sigs = [sig] * n
+    assert all(_run_staged(v, off, idx, sigs, [msg]))
+    assert v.last_stats() == (0, 0)
+    ms, cnt = v.last_kernel_ms()
+    assert cnt[7] == 1
+    sigs[12345] = v.util_sign([sks[7]], [0], [hashlib.sha256(b"gbv-dup-other").digest()])[0]
+    assert _run_staged(v, off, idx, sigs, [msg]) == [i != 12345 for i in range(n)]
+
+
 def test_msm_cooldown_after_failing_segment(world):
     """After an MSM segment fails, the next submits use the per-set ladders (an invalid-dense stream
     would otherwise pay the MSM and the G2 recomputation); booleans are the same either way."""
