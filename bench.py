@@ -772,7 +772,7 @@ def main():
     ap.add_argument("--tune", action="append", default=[], metavar="NAME=VALUE",
                     help="gbv_tune setting applied before anything runs (experiments; include/gbv.h lists the names)")
     ap.add_argument("--no-vs-shard", action="store_true", help="skip the sharded verifySignatureSets object of the gossip line")
-    ap.add_argument("--shard-depth", type=int, default=2, help="vs-shard: shard passes in flight per rank (staged copies)")
+    ap.add_argument("--shard-depth", type=int, default=3, help="vs-shard: shard passes in flight per rank (staged copies; 3 measured best for 8 192 - 16 384-set shards, profiles/r06/shards)")
     ap.add_argument("--shard-calls", type=int, default=512,
                     help="vs-shard: 128-member aggregate sets / 128 in the ONE sharded verifySignatureSets call")
     args = ap.parse_args()
@@ -1112,7 +1112,8 @@ def vs_shard_measure(args, v, sk_ints, world, rank, log):
     ok_small = sv.verify_signature_sets(sets[-256:])
     seq = [stages[k % depth] for k in range(args.steps)]
     if args.warmup:
-        assert sv.verify_staged_shards(seq[:max(depth, args.warmup)], depth=depth) == [True] * max(depth, args.warmup)
+        warm = [stages[k % depth] for k in range(max(depth, args.warmup))]
+        assert sv.verify_staged_shards(warm, depth=depth) == [True] * len(warm)
     tdist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
