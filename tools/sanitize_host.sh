@@ -29,8 +29,10 @@ LD_PRELOAD="$GCC_ASAN $GCC_UBSAN" node "$ROOT/addon/test_verifier.js" cpu | tee 
 echo "[sanitize] host build of the device arithmetic (hipcc --offload-host-only $SAN)"
 CLANG_ASAN=$(find /opt/rocm/lib/llvm/lib/clang -name 'libclang_rt.asan-x86_64.so' | head -1)
 hipcc --offload-host-only $SAN -fno-gpu-sanitize -fPIC -shared -o "$OUT/libhosttest.so" "$ROOT/tests/native/hosttest.cpp"
+# (the ~130-pairing shared-accumulator and locate prototypes are left out here: minutes under ASan, and
+# their Miller / exponentiation code is the same the other host tests run)
 GBV_HOSTTEST_LIB="$OUT/libhosttest.so" LD_PRELOAD="$CLANG_ASAN" \
-    python3 -m pytest -q -p no:cacheprovider "$ROOT/tests/test_host_arith.py" 2>&1 | tail -3
+    python3 -m pytest -q -p no:cacheprovider "$ROOT/tests/test_host_arith.py" -k "not ragged_calls and not locate_one_invalid" 2>&1 | tail -3
 
 echo "[sanitize] oracle C port (gcc $SAN)"
 gcc $SAN -fPIC -shared -pthread -O1 -o "$OUT/libblsport.so" "$ROOT/oracle/c/blsport.c"
