@@ -44,6 +44,11 @@
  * malformed arguments with "GBV_E_ARG" (or a TypeError for a wrong JS type).
  */
 #define NAPI_VERSION 6
+#define _GNU_SOURCE
+#include <execinfo.h>
+#include <signal.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 #include <node_api.h>
 #include <pthread.h>
 #include <stdint.h>
@@ -1492,7 +1497,31 @@ static napi_value js_close(napi_env env, napi_callback_info info) {
   return queue(env, j, "gbvClose", argv[0]);
 }
 
+/* GBV_SEGV_TRACE=1 (diagnosis only): on SIGSEGV / SIGBUS, print the faulting address, the thread and
+ * a backtrace of that thread to stderr, then die by the same signal.  It replaces the process's own
+ * handler for these signals (V8's WebAssembly trap handler among them), so it stays off by default. */
+static void segv_trace(int sig, siginfo_t* si, void* uc) {
+  (void)uc;
+  void* frames[64];
+  char msg[160];
+  int n = backtrace(frames, 64);
+  int l = snprintf(msg, sizeof msg, "[gbv addon] signal %d at address %p in thread %ld\n", sig, si ? si->si_addr : NULL,
+                   (long)syscall(SYS_gettid));
+  if (l > 0 && write(2, msg, (size_t)l) < 0) {}
+  backtrace_symbols_fd(frames, n, 2);
+  signal(sig, SIG_DFL);
+  raise(sig);
+}
+
 static napi_value init(napi_env env, napi_value exports) {
+  if (getenv("GBV_SEGV_TRACE")) {
+    struct sigaction sa;
+    memset(&sa, 0, sizeof sa);
+    sa.sa_sigaction = segv_trace;
+    sa.sa_flags = SA_SIGINFO;
+    sigaction(SIGSEGV, &sa, NULL);
+    sigaction(SIGBUS, &sa, NULL);
+  }
   napi_property_descriptor props[] = {
       {"open", NULL, js_open, NULL, NULL, NULL, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), NULL},
       {"addPubkeys", NULL, js_add_pubkeys, NULL, NULL, NULL, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), NULL},

@@ -157,6 +157,7 @@ async function gpu(fixPath) {
   if (mode === "cpu") await cpu();
   else await gpu(process.argv[3]);
   process.stdout.write(JSON.stringify(report) + "\n");
+  process.exit(0);  // Node 12's teardown finalizer crash: see bench_api.js
 })().catch((e) => {
   process.stdout.write(JSON.stringify({fatal: String(e && e.stack || e), code: e && e.code}) + "\n");
   process.exit(1);

@@ -130,4 +130,7 @@ main()
   .catch((e) => {
     report.fatal = String(e && e.stack ? e.stack : e);
   })
-  .then(() => console.log(JSON.stringify(report)));
+  .then(() => {
+    console.log(JSON.stringify(report));
+    process.exit(0);  // Node 12's teardown finalizer crash: see bench_api.js
+  });

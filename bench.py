@@ -305,7 +305,9 @@ def api_path_js(call_off, idx, sigs, msgs, key_pks, log, reps=3):
     addon = os.path.join(ROOT, "addon", "gbv_addon.node")
     if node is None or not os.path.exists(addon):
         return None
-    d = tempfile.mkdtemp(prefix="gbv-api-js-")
+    keep = os.environ.get("GBV_JS_INPUTS")  # diagnosis: keep the child's inputs in this directory
+    d = keep or tempfile.mkdtemp(prefix="gbv-api-js-")
+    os.makedirs(d, exist_ok=True)
     try:
         n_calls = len(call_off) - 1
         with open(os.path.join(d, "meta.json"), "w") as f:
@@ -317,19 +319,25 @@ def api_path_js(call_off, idx, sigs, msgs, key_pks, log, reps=3):
                 f.write(blob)
         p = subprocess.run([node, os.path.join(ROOT, "addon", "bench_api.js"), d, str(reps)], capture_output=True, text=True, timeout=400)
         lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
-        if p.returncode != 0 or not lines:
-            log("api path (js) failed: rc %d %s %s" % (p.returncode, p.stdout[-500:], p.stderr[-500:]))
+        r = json.loads(lines[-1]) if lines else {}
+        if p.returncode != 0:
+            log("api path (js): child exit %d %s %s" % (p.returncode, p.stdout[-500:], p.stderr[-1500:]))
+        # a child that printed its checked results and then died at process teardown (after close():
+        # no device work left) still measured them; its exit status goes into the record
+        if not (r.get("all_valid") and (p.returncode == 0 or (p.returncode < 0 and r.get("closed")))):
             return None
-        r = json.loads(lines[-1])
+        if p.returncode != 0:
+            r["child_exit"] = p.returncode
         r["how"] = ("node addon/bench_api.js: every gossip call of the C2 workload through GpuBlsVerifier.verifySignatureSetsSameMessage "
                     "(addon/gpu_bls_verifier.js) over the Node-API addon, all promises awaited, every boolean checked; "
                     "'packed' = {indices: Uint32Array, signatures: Uint8Array} per call, 'objects' = one {index, signature} per set "
                     "(built before the clock); 'ibls' = the IBlsVerifier shape the Lodestar binding uses (chain/bls/gpu/index.ts): one "
-                    "{publicKey, index, signature} object per set, packed per call into the device form INSIDE the clock, boolean[] out "
+                    "{publicKey, signature} object per set (the key found by the identity of its index2pubkey object), packed per call into the device form INSIDE the clock, boolean[] out "
                     "(verifySameMessageSets); best of %d; its own device context beside the bench's" % reps)
         return r
     finally:
-        shutil.rmtree(d, ignore_errors=True)
+        if not keep:
+            shutil.rmtree(d, ignore_errors=True)
 
 
 # ---- verifySignatureSets configs (C1, C3, C4) ------------------------------------------------------
@@ -936,10 +944,6 @@ def main():
     api_stream, api_stream_n, api_stream_passes = api_stream_rate(v, call_off, idx, sigs, msgs) if do_api else (None, 0, 0)
     if api_stream:
         log("api stream: %s sets/s over %d sets in %d device passes" % (api_stream, api_stream_n, api_stream_passes))
-    api_js = api_path_js(call_off, idx, sigs, msgs, key_pks, log) if do_api and world == 1 else None
-    if api_js:
-        log("api stream (js): packed %s, IBlsVerifier-shaped %s, objects %s sets/s, lone call %s ms" % (
-            api_js["packed"]["sets_per_s"], api_js["ibls"]["sets_per_s"], api_js["objects"]["sets_per_s"], api_js["lone_call_p50_ms"]))
 
     # per launch: algorithmic MACs of the sets one k_sm_prepare launch processes / its average duration
     units_per_launch = n_mine / max(prep_launches_per_step, 1)
@@ -1002,6 +1006,12 @@ def main():
     if rank == 0 and world == 1 and not args.no_signing_roots:
         ssz = signing_roots_bench(v, cpu_sample=0 if args.no_cpu_baseline else 20000)
         log("signing roots: %s roots/s" % ssz["value"])
+
+    # the Node child last: every other device measurement of this process is done before it runs
+    api_js = api_path_js(call_off, idx, sigs, msgs, key_pks, log) if do_api and world == 1 else None
+    if api_js:
+        log("api stream (js): packed %s, IBlsVerifier-shaped %s, objects %s sets/s, lone call %s ms" % (
+            api_js["packed"]["sets_per_s"], api_js["ibls"]["sets_per_s"], api_js["objects"]["sets_per_s"], api_js["lone_call_p50_ms"]))
 
     cpu = None
     cpu_lat = None
