@@ -353,21 +353,25 @@ class GpuBlsVerifier {
     const nKeys = n ? this.addon.pubkeyCount(this.ctx) : 0;
     const badIndex = () => Object.assign(new RangeError("validator index out of range"), {code: "GBV_E_ARG"});
     let outside = null; // object form: the positions of sets whose key is not in index2pubkey
+    let resolved = null; // object form: the sets' indices, resolved once here (a key object is read once)
     if (packed) {
       const pi = sets.indices;
       for (let i = 0; i < n; ++i) if (pi[i] >= nKeys) throw badIndex();
     } else {
+      resolved = new Uint32Array(n);
       for (let i = 0; i < n; ++i) {
-        const k = this._setIndex(sets[i]); // resolved again when the pass is packed (_packSameMessage)
+        const k = this._setIndex(sets[i]);
         if (k === undefined) (outside || (outside = [])).push(i);
         else if (!(k >= 0 && k < nKeys)) throw badIndex();
+        else resolved[i] = k;
       }
       if (outside) return this._sameMessageOutsideKeys(sets, outside, message, opts);
     }
     if (n < 2 * MAX_SIGNATURE_SETS_PER_JOB) {
       // one chunk (every gossip call): its job's promise is the call's (no Promise.all, no concat)
       const chunk = packed ? {indices: sets.indices, signatures: sets.signatures, length: n} : sets;
-      return new Promise((resolve, reject) => this._queue({type: "sameMessage", resolve, reject, addedTimeMs: Date.now(), opts, sets: chunk, message}));
+      return new Promise((resolve, reject) =>
+        this._queue({type: "sameMessage", resolve, reject, addedTimeMs: Date.now(), opts, sets: chunk, message, indices: resolved}));
     }
     const chunks = packed
       ? chunkRanges(n, MAX_SIGNATURE_SETS_PER_JOB).map(([a, b]) => ({indices: sets.indices.subarray(a, b),
@@ -514,9 +518,10 @@ class GpuBlsVerifier {
       messages.set(j.message, 32 * c);
       j.off = o;
       if (Array.isArray(s)) {
+        if (j.indices) indices.set(j.indices, o); // resolved and checked when the call was validated
         for (let i = 0; i < n; ++i) {
           const e = s[i], g = e.signature;
-          indices[o + i] = this._setIndex(e); // in the table: checked when the call was validated
+          if (!j.indices) indices[o + i] = this._setIndex(e); // a chunk of a long call: in the table, checked
           if (g.length === 96) signatures.set(g, 96 * (o + i));
         }
       } else {
