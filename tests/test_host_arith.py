@@ -410,12 +410,15 @@ def test_miller_groups_over_ragged_calls(lib, K):
     explained; this pins that the group arithmetic itself is exact for every ragged shape."""
     rng = random.Random(77 + K)
     lib.ht_miller_call_groups.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_int]
+    # points: random multiples of the generators stepped by random strides (one addition per set
+    # instead of a scalar multiplication: the oracle's G2 multiplications dominated this test's time)
+    P, Q = o.g1_mul(o.G1_GEN, rng.randrange(1, o.R)), o.g2_mul(o.G2_GEN, rng.randrange(1, o.R))
+    dP, dQ = o.g1_mul(o.G1_GEN, rng.randrange(1, o.R)), o.g2_mul(o.G2_GEN, rng.randrange(1, o.R))
     for n in (127, 3, 1, 2 * K + 1):
         pts = []
         ps, qs = b"", b""
         for _ in range(n):
-            P = o.g1_mul(o.G1_GEN, rng.randrange(1, o.R))
-            Q = o.g2_mul(o.G2_GEN, rng.randrange(1, o.R))
+            P, Q = o.g1_add(P, dP), o.g2_add(Q, dQ)
             pts.append((P, Q))
             ps += be(P[0]) + be(P[1])
             qs += fp2b(Q[0]) + fp2b(Q[1])
