@@ -1050,6 +1050,10 @@ def main():
         "config": {"workload": workload, "sets_per_gpu": n_mine, "calls_per_gpu": len(call_off) - 1, "table": N_VALIDATORS,
                    "parallelism": parallelism,
                    "submission": "streamed: %d batches in flight" % depth if depth > 1 else "one batch at a time",
+                   "timed_region": "device passes over staged batches: the inputs were copied to HBM once before the "
+                                   "clock (host-to-device copies outside the timed region); per-set booleans copied back "
+                                   "inside it. The host-inclusive rates are api_path_sets_per_s, api_path.oneshot_sets_per_s "
+                                   "(PCIe included) and the api_path_js lines",
                    "invalid_frac": invalid_frac},
         "api_path_sets_per_s": api_stream,
         "api_path": {"how": "asyncio: every gossip call of the workload issued through GpuBlsVerifier.verify_signature_sets_same_message "
