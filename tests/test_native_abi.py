@@ -46,3 +46,20 @@ def test_no_oracle_import_in_product():
                         assert (node.module or "").split(".")[0] != "oracle", path
             elif f.endswith((".h", ".hip", ".cpp")):
                 assert "oracle/" not in open(path).read(), path
+
+
+def test_tuning_names_documented():
+    """Every gbv_tune name the library accepts (gbv.hip tuning_set's table and the per-context names in
+    gbv_tune) is listed in include/gbv.h's gbv_tune comment, and every listed name is accepted."""
+    import re
+    src = open(os.path.join(ROOT, "lodestar_amd", "csrc", "gbv.hip")).read()
+    table = src[src.index("bool tuning_set("):]
+    table = table[:table.index("};")]
+    process_wide = set(re.findall(r'\{"([a-z_0-9]+)", &g_tuning\.', table))
+    per_ctx = set(re.findall(r'!strcmp\(name, "([a-z_0-9]+)"\)', src[src.index("int gbv_tune("):]))
+    hdr = open(os.path.join(ROOT, "include", "gbv.h")).read()
+    doc = hdr[:hdr.index("int gbv_tune(")]
+    doc = doc[doc.rindex("/*"):]
+    listed = set(re.findall(r'"([a-z_0-9]+)"', doc))
+    assert process_wide and per_ctx
+    assert process_wide | per_ctx == listed, (sorted((process_wide | per_ctx) - listed), sorted(listed - (process_wide | per_ctx)))
